@@ -1,0 +1,190 @@
+"""ctypes mirror of include/sfmcore.h (plumbing for tests and bench.py).
+
+The product is libsfmcore.so (HIP kernels + C-ABI); this module only
+describes its structs and loads it.  Loading order matters on ROCm: torch
+ships its own libamdhip64.so.7 / librccl.so.1 and both libraries must share
+one HIP runtime, so torch is imported (if available) before the library.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsfmcore.so")
+
+SFM_OK = 0
+SFM_ERR_INVALID_ARG = -1
+SFM_ERR_DEVICE = -2
+SFM_ERR_NOT_FINITE = -3
+SFM_ERR_UNSUPPORTED = -4
+SFM_ERR_COMM = -5
+SFM_ERR_OOM = -6
+SFM_ERR_SOLVER = -7
+
+SFM_TERM_CONVERGENCE = 0
+SFM_TERM_NO_CONVERGENCE = 1
+SFM_TERM_FAILURE = 2
+
+SFM_MATCH_RATIO = 0
+SFM_MATCH_MUTUAL = 1
+
+i32p = C.POINTER(C.c_int32)
+i64p = C.POINTER(C.c_int64)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+u8p = C.POINTER(C.c_uint8)
+f64p = C.POINTER(C.c_double)
+
+
+class CtxOpts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
+                ("reserved", C.c_int32), ("comm_id", u8p)]
+
+
+class BAProblem(C.Structure):
+    _fields_ = [("n_img", C.c_int32), ("n_intr", C.c_int32), ("n_pt", C.c_int64),
+                ("n_obs", C.c_int64), ("pt_offsets", i64p), ("obs_img", i32p),
+                ("obs_uv", f64p), ("img_intr", i32p), ("const_img", C.c_int32),
+                ("reserved", C.c_int32), ("huber_a", C.c_double)]
+
+
+class BAOptions(C.Structure):
+    _fields_ = [("max_num_iterations", C.c_int32),
+                ("max_num_consecutive_invalid_steps", C.c_int32),
+                ("jacobi_scaling", C.c_int32), ("reserved", C.c_int32),
+                ("function_tolerance", C.c_double), ("gradient_tolerance", C.c_double),
+                ("parameter_tolerance", C.c_double),
+                ("initial_trust_region_radius", C.c_double),
+                ("max_trust_region_radius", C.c_double),
+                ("min_trust_region_radius", C.c_double),
+                ("min_relative_decrease", C.c_double), ("min_lm_diagonal", C.c_double),
+                ("max_lm_diagonal", C.c_double)]
+
+
+class BASummary(C.Structure):
+    _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("num_residuals", C.c_int64), ("iterations", C.c_int32),
+                ("successful_steps", C.c_int32), ("unsuccessful_steps", C.c_int32),
+                ("termination", C.c_int32), ("usable", C.c_int32), ("reserved", C.c_int32),
+                ("rmse_initial", C.c_double), ("rmse_final", C.c_double),
+                ("seconds", C.c_double)]
+
+
+class BAIter(C.Structure):
+    _fields_ = [("iteration", C.c_int32), ("step_is_valid", C.c_int32),
+                ("step_is_successful", C.c_int32), ("reserved", C.c_int32),
+                ("cost", C.c_double), ("cost_change", C.c_double),
+                ("model_cost_change", C.c_double), ("relative_decrease", C.c_double),
+                ("trust_region_radius", C.c_double), ("step_norm", C.c_double),
+                ("gradient_max_norm", C.c_double)]
+
+
+class BAPlanInfo(C.Structure):
+    _fields_ = [("shard_pt_begin", C.c_int64), ("shard_pt_end", C.c_int64),
+                ("shard_obs", C.c_int64), ("n_chunks", C.c_int32),
+                ("band_blocks", C.c_int32), ("n_cam_active", C.c_int32),
+                ("n_intr_active", C.c_int32), ("rcs_dim", C.c_int64),
+                ("last_kernel_ms", C.c_double * 8), ("schur_flops_per_iter", C.c_int64),
+                ("schur_launches", C.c_int64), ("schur_ms_total", C.c_double)]
+
+
+class SynthBAConfig(C.Structure):
+    _fields_ = [("n_cam", C.c_int32), ("k", C.c_int32), ("vis_mode", C.c_int32),
+                ("n_intr", C.c_int32), ("n_pt", C.c_int64), ("seed", C.c_uint64),
+                ("noise_px", C.c_double), ("outlier_frac", C.c_double),
+                ("perturb_rot", C.c_double), ("perturb_t", C.c_double),
+                ("perturb_X", C.c_double), ("perturb_f", C.c_double),
+                ("const_img", C.c_int32), ("reserved", C.c_int32)]
+
+
+class MatchOptions(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("ratio", C.c_float)]
+
+
+def default_options():
+    o = BAOptions()
+    o.max_num_iterations = 50
+    o.max_num_consecutive_invalid_steps = 5
+    o.jacobi_scaling = 1
+    o.function_tolerance = 1e-6
+    o.gradient_tolerance = 1e-10
+    o.parameter_tolerance = 1e-8
+    o.initial_trust_region_radius = 1e4
+    o.max_trust_region_radius = 1e16
+    o.min_trust_region_radius = 1e-32
+    o.min_relative_decrease = 1e-3
+    o.min_lm_diagonal = 1e-6
+    o.max_lm_diagonal = 1e32
+    return o
+
+
+# (name, restype, argtypes) for every symbol declared in include/sfmcore.h
+SIGNATURES = [
+    ("sfm_version", C.c_char_p, []),
+    ("sfm_last_error", C.c_char_p, []),
+    ("sfm_comm_unique_id", C.c_int, [u8p]),
+    ("sfm_ctx_create", C.c_int, [C.POINTER(CtxOpts), C.POINTER(C.c_void_p)]),
+    ("sfm_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("sfm_ctx_synchronize", C.c_int, [C.c_void_p]),
+    ("sfm_ba_default_options", None, [C.POINTER(BAOptions)]),
+    ("sfm_ba_solve", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,
+                               C.POINTER(BAOptions), C.POINTER(BASummary)]),
+    ("sfm_ba_plan_create", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,
+                                     C.POINTER(C.c_void_p)]),
+    ("sfm_ba_plan_run", C.c_int, [C.c_void_p, C.POINTER(BAOptions), C.POINTER(BASummary)]),
+    ("sfm_ba_plan_download", C.c_int, [C.c_void_p, f64p, f64p, f64p]),
+    ("sfm_ba_plan_destroy", C.c_int, [C.c_void_p]),
+    ("sfm_ba_plan_get_info", C.c_int, [C.c_void_p, C.POINTER(BAPlanInfo)]),
+    ("sfm_ba_plan_get_trace", C.c_int, [C.c_void_p, C.POINTER(BAIter), C.c_int32, i32p]),
+    ("sfm_ba_partition", C.c_int, [C.POINTER(BAProblem), C.c_int32, i64p, i64p]),
+    ("sfm_synth_ba", C.c_int, [C.POINTER(SynthBAConfig), i64p, i32p, f64p, i32p, f64p,
+                               f64p, f64p, f64p, f64p, f64p, i64p]),
+    ("sfm_match_dense", C.c_int, [C.c_void_p, u8p, C.c_int32, u8p, C.c_int32,
+                                  C.POINTER(MatchOptions), i32p, i32p]),
+    ("sfm_match_plan_create", C.c_int, [C.c_void_p, u8p, i64p, C.c_int32,
+                                        C.POINTER(C.c_void_p)]),
+    ("sfm_match_plan_run", C.c_int, [C.c_void_p, i32p, C.c_int64, C.POINTER(MatchOptions),
+                                     i64p]),
+    ("sfm_match_plan_fetch", C.c_int, [C.c_void_p, i64p, u32p, u32p, i32p]),
+    ("sfm_match_plan_digest", C.c_int, [C.c_void_p, u64p]),
+    ("sfm_match_plan_get_last_ms", C.c_int, [C.c_void_p, f64p, i64p]),
+    ("sfm_match_plan_destroy", C.c_int, [C.c_void_p]),
+    ("sfm_exhaustive_pairs", C.c_int, [C.c_int32, i32p]),
+    ("sfm_synth_descriptors", C.c_int, [C.c_int32, C.c_int32, C.c_uint64, u8p]),
+]
+
+_lib = None
+
+
+def load(path=None):
+    """Load libsfmcore.so (after torch, so both share one HIP runtime)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (shares libamdhip64.so.7 / librccl.so.1)
+    except Exception:
+        pass
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"libsfmcore.so not built: {p} (run __graft_entry__.build())")
+    lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    missing = []
+    for name, res, args in SIGNATURES:
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            missing.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    lib.missing_symbols = missing
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def ptr(a, t):
+    """numpy array -> ctypes pointer (None for None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(t)

@@ -1,0 +1,176 @@
+"""Thin numpy wrappers over libsfmcore.so (ctypes) for tests and bench.py.
+
+Every call goes through the C-ABI in include/sfmcore.h; there is no Python
+compute path and no fallback: if the library or a gfx950 device is missing,
+these raise.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi as abi
+
+
+class SfmError(RuntimeError):
+    def __init__(self, code, where):
+        lib = abi.load()
+        msg = lib.sfm_last_error().decode(errors="replace")
+        super().__init__(f"{where} failed with {code}: {msg}")
+        self.code = code
+
+
+def _check(rc, where):
+    if rc != abi.SFM_OK:
+        raise SfmError(rc, where)
+
+
+class Context:
+    """sfm_ctx: one HIP device (+ RCCL communicator when world_size > 1)."""
+
+    def __init__(self, device=0, rank=0, world_size=1, comm_id=None):
+        self.lib = abi.load()
+        o = abi.CtxOpts()
+        o.device, o.rank, o.world_size = device, rank, world_size
+        self._id = None
+        if comm_id is not None:
+            self._id = (C.c_uint8 * 128).from_buffer_copy(bytes(comm_id))
+            o.comm_id = C.cast(self._id, abi.u8p)
+        h = C.c_void_p()
+        _check(self.lib.sfm_ctx_create(C.byref(o), C.byref(h)), "sfm_ctx_create")
+        self.h = h
+
+    def synchronize(self):
+        _check(self.lib.sfm_ctx_synchronize(self.h), "sfm_ctx_synchronize")
+
+    def close(self):
+        if self.h:
+            self.lib.sfm_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    lib = abi.load()
+    buf = (C.c_uint8 * 128)()
+    _check(lib.sfm_comm_unique_id(buf), "sfm_comm_unique_id")
+    return bytes(buf)
+
+
+def match_dense(ctx, a, b, mode=abi.SFM_MATCH_RATIO, ratio=0.8):
+    a = np.ascontiguousarray(a, np.uint8).reshape(-1, 128)
+    b = np.ascontiguousarray(b, np.uint8).reshape(-1, 128)
+    n_out = len(b) if mode == abi.SFM_MATCH_RATIO else len(a)
+    idx = np.zeros(max(n_out, 1), np.int32)
+    d2 = np.zeros(max(n_out, 1), np.int32)
+    o = abi.MatchOptions(mode, ratio)
+    _check(ctx.lib.sfm_match_dense(ctx.h, abi.ptr(a, abi.u8p), len(a), abi.ptr(b, abi.u8p), len(b),
+                                   C.byref(o), abi.ptr(idx, abi.i32p), abi.ptr(d2, abi.i32p)),
+           "sfm_match_dense")
+    return idx[:n_out], d2[:n_out]
+
+
+class MatchPlan:
+    """Resident descriptor collection for all-pairs matching."""
+
+    def __init__(self, ctx, desc, offsets):
+        self.ctx = ctx
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 128)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        self.n_img = len(offsets) - 1
+        h = C.c_void_p()
+        _check(ctx.lib.sfm_match_plan_create(ctx.h, abi.ptr(desc, abi.u8p),
+                                             abi.ptr(offsets, abi.i64p), self.n_img, C.byref(h)),
+               "sfm_match_plan_create")
+        self.h = h
+        self.n_pairs = 0
+
+    def run(self, pairs, mode=abi.SFM_MATCH_RATIO, ratio=0.8, count=True):
+        pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        self.n_pairs = len(pairs)
+        o = abi.MatchOptions(mode, ratio)
+        tot = C.c_int64()
+        _check(self.ctx.lib.sfm_match_plan_run(self.h, abi.ptr(pairs, abi.i32p), len(pairs),
+                                               C.byref(o), C.byref(tot) if count else None),
+               "sfm_match_plan_run")
+        return tot.value if count else None
+
+    def fetch(self):
+        counts = np.zeros(max(self.n_pairs, 1), np.int64)
+        _check(self.ctx.lib.sfm_match_plan_fetch(self.h, abi.ptr(counts, abi.i64p), None, None,
+                                                 None), "sfm_match_plan_fetch")
+        counts = counts[:self.n_pairs]
+        tot = int(counts.sum())
+        i = np.zeros(max(tot, 1), np.uint32)
+        j = np.zeros(max(tot, 1), np.uint32)
+        d = np.zeros(max(tot, 1), np.int32)
+        _check(self.ctx.lib.sfm_match_plan_fetch(self.h, abi.ptr(counts, abi.i64p),
+                                                 abi.ptr(i, abi.u32p), abi.ptr(j, abi.u32p),
+                                                 abi.ptr(d, abi.i32p)), "sfm_match_plan_fetch")
+        return counts, i[:tot], j[:tot], d[:tot]
+
+    def digest(self):
+        v = C.c_uint64()
+        _check(self.ctx.lib.sfm_match_plan_digest(self.h, C.byref(v)), "sfm_match_plan_digest")
+        return v.value
+
+    def last_ms(self):
+        ms = C.c_double()
+        n = C.c_int64()
+        _check(self.ctx.lib.sfm_match_plan_get_last_ms(self.h, C.byref(ms), C.byref(n)),
+               "sfm_match_plan_get_last_ms")
+        return ms.value, n.value
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.sfm_match_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _mix64(z):
+    z = np.uint64(z)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def match_digest(counts, i, j, d):
+    """Host restatement of the device digest (order-independent)."""
+    tot = np.uint64(0)
+    off = 0
+    with np.errstate(over="ignore"):
+        for p, c in enumerate(counts):
+            h = np.uint64(0)
+            for k in range(off, off + int(c)):
+                key = (np.uint64(i[k]) << np.uint64(32)) | np.uint64(j[k])
+                h = h + _mix64(key ^ (np.uint64(np.uint32(d[k])) << np.uint64(21)))
+            off += int(c)
+            tot = tot + _mix64(h + np.uint64(0x9E3779B97F4A7C15) * np.uint64(p + 1))
+    return int(tot)
+
+
+def exhaustive_pairs(n):
+    lib = abi.load()
+    m = n * (n - 1) // 2
+    out = np.zeros(max(2 * m, 2), np.int32)
+    _check(lib.sfm_exhaustive_pairs(n, abi.ptr(out, abi.i32p)), "sfm_exhaustive_pairs")
+    return out[:2 * m].reshape(-1, 2)
+
+
+def synth_descriptors(n_img, n_kp, seed=0xC3):
+    lib = abi.load()
+    d = np.zeros(max(n_img * n_kp * 128, 1), np.uint8)
+    _check(lib.sfm_synth_descriptors(n_img, n_kp, seed, abi.ptr(d, abi.u8p)),
+           "sfm_synth_descriptors")
+    return d[:n_img * n_kp * 128].reshape(-1, 128)

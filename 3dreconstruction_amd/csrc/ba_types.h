@@ -1,0 +1,72 @@
+// Types shared by the BA host planner (ba_plan.cpp), the LM driver
+// (ba_solver.cpp) and the gfx950 kernels (ba_kernels.hip).
+//
+// HBM layout (DESIGN.md §BA data layout), per rank:
+//   points   : X[3*n_spt] in shard order (landmark-major, sorted by first
+//              active camera), scaleE[3*n_spt] (Jacobi scale, fixed at iter 0)
+//   obs      : obs_uv[2*n_sobs], obs_img[n_sobs], obs_pt[n_sobs], pt_off[n_spt+1]
+//              (observations of a point contiguous)
+//   cameras  : extr[6*n_img], intr[4*n_intr] (full tables, replicated),
+//              CamPre[n_img] (per-camera rotation terms), scaleF[nF]
+//   RCS      : Sband[ncam][D+1][6][6] (block (i,i-d)), Sarrow[nintr][ncam][4][6],
+//              Scorner[nintr][nintr][4][4], rhs[nF], bF[nF], cnF[nF]
+//   chunk slab: tiles[n_chunk][80][80] (-Z Z^T, row 79 = -Z w)
+//   image slab: Uimg[n_img][10][10], Ub[n_img][10], Ucn[n_img][10]
+#pragma once
+#include <cstdint>
+
+namespace sfm {
+
+constexpr int kTileN = 5;                 // 16-row MFMA tiles per chunk side
+constexpr int kTileR = 16 * kTileN;       // 80 rows
+constexpr int kTileRowsUsed = 76;         // rows 0..75 for F blocks
+constexpr int kTileWRow = 79;             // row carrying w = L^-1 g_E
+constexpr int kSubPts = 16;               // points per LDS panel sub-batch
+constexpr int kSubObs = 256;              // observations per sub-batch (<= threads)
+constexpr int kChunkPts = 256;            // points per chunk (upper bound)
+constexpr int kMaxSlots = 16;
+
+// Per-camera precomputed rotation terms (for current or candidate params).
+//   Rodrigues branch: P = X c + (u x X) s + u (u.X)(1-c) + t,
+//                     dP/dX = R, dP/dw = -R [X]x Ar  (Ar = (w w' + (R'-I)[w]x)/|w|^2)
+//   small-angle branch (|w|^2 <= eps): P = X + w x X + t, dP/dX = I + [w]x,
+//                     dP/dw = -[X]x (R := I + [w]x for dP/dX, Al = I, Ar = I)
+struct CamPre {
+    double c, s, omc, small;   // cos, sin, 1-cos, small-angle flag (0/1)
+    double u[3];               // unit axis (Rodrigues) or w (small angle)
+    double t[3];
+    double R[9];               // dP/dX
+    double Al[9];              // left factor of dP/dw
+    double Ar[9];              // right factor of dP/dw
+};
+
+struct ChunkDesc {
+    int32_t pt_begin, pt_end;      // shard point range
+    int32_t obs_begin, obs_end;    // shard obs range
+    int32_t sub_begin, sub_end;    // range into the sub-batch start list
+    int32_t n_slots, pad;
+    int32_t slot_img[kMaxSlots];   // image of a camera slot (or -1)
+    int32_t slot_intr[kMaxSlots];  // intrinsic block of an intr slot (or -1)
+    int32_t slot_row[kMaxSlots];   // first tile row of the slot
+    int32_t slot_col[kMaxSlots];   // global F column of the slot
+};
+
+// Reduce-plan term sources (kind).
+enum : int32_t { kSrcTile = 0, kSrcU = 1, kSrcUb = 2, kSrcUcn = 3 };
+
+struct ReduceTarget {
+    int64_t dst;        // element offset of the block in its destination array
+    int32_t dst_kind;   // 0 Sband, 1 Sarrow, 2 Scorner, 3 rhs, 4 bF, 5 cnF
+    int32_t rows, cols; // block shape (vectors: cols = 1)
+    int32_t ld;         // destination row stride
+    int32_t c_begin, c_end;  // contribution range
+};
+
+struct ReduceTerm {
+    int32_t kind;       // kSrc*
+    int32_t index;      // chunk or image
+    int16_t roff, coff; // source block origin
+    float sign;         // +1 / -1
+};
+
+}  // namespace sfm

@@ -1,0 +1,154 @@
+// Context management, error reporting and the run-time RCCL binding.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+
+#include "common.h"
+
+namespace sfm {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl* rccl() {
+    static Rccl r;
+    static bool ok = false;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.error_string;
+    });
+    SFM_REQUIRE(ok, SFM_ERR_COMM, "RCCL (librccl.so.1) not available");
+    return &r;
+}
+
+int rccl_comm_init(void** comm, int world, const uint8_t* id128, int rank) {
+    const Rccl* r = rccl();
+    ncclUniqueId id;
+    static_assert(sizeof(id) == 128, "ncclUniqueId size");
+    std::memcpy(&id, id128, 128);
+    ncclComm_t c = nullptr;
+    ncclResult_t e = r->comm_init_rank(&c, world, id, rank);
+    SFM_REQUIRE(e == ncclSuccess, SFM_ERR_COMM, "ncclCommInitRank: %s", r->error_string(e));
+    *comm = c;
+    return SFM_OK;
+}
+
+void rccl_comm_destroy(void* comm) {
+    if (comm) rccl()->comm_destroy((ncclComm_t)comm);
+}
+
+int rccl_allreduce_f64(void* comm, double* buf, size_t n, int op_max, hipStream_t s) {
+    const Rccl* r = rccl();
+    ncclResult_t e = r->all_reduce(buf, buf, n, ncclFloat64, op_max ? ncclMax : ncclSum,
+                                   (ncclComm_t)comm, s);
+    SFM_REQUIRE(e == ncclSuccess, SFM_ERR_COMM, "ncclAllReduce: %s", r->error_string(e));
+    return SFM_OK;
+}
+
+}  // namespace sfm
+
+using namespace sfm;
+
+extern "C" const char* sfm_version(void) { return "sfmcore 0.1.0 (gfx950)"; }
+
+extern "C" const char* sfm_last_error(void) { return g_err.c_str(); }
+
+extern "C" int sfm_comm_unique_id(uint8_t* out128) {
+    return guarded([&] {
+        SFM_REQUIRE(out128, SFM_ERR_INVALID_ARG, "null output");
+        ncclUniqueId id;
+        ncclResult_t e = rccl()->get_unique_id(&id);
+        SFM_REQUIRE(e == ncclSuccess, SFM_ERR_COMM, "ncclGetUniqueId: %s",
+                    rccl()->error_string(e));
+        std::memcpy(out128, &id, 128);
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
+    return guarded([&] {
+        SFM_REQUIRE(opts && out, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_REQUIRE(opts->world_size >= 1 && opts->rank >= 0 && opts->rank < opts->world_size,
+                    SFM_ERR_INVALID_ARG, "bad rank %d / world_size %d", opts->rank,
+                    opts->world_size);
+        int ndev = 0;
+        hipError_t e = hipGetDeviceCount(&ndev);
+        SFM_REQUIRE(e == hipSuccess && ndev > 0, SFM_ERR_DEVICE, "no HIP device available (%s)",
+                    hipGetErrorString(e));
+        SFM_REQUIRE(opts->device >= 0 && opts->device < ndev, SFM_ERR_INVALID_ARG,
+                    "device %d out of range (%d devices)", opts->device, ndev);
+        hipDeviceProp_t prop;
+        SFM_HIP(hipGetDeviceProperties(&prop, opts->device));
+        SFM_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, SFM_ERR_DEVICE,
+                    "device %d is %s; this build targets gfx950 (MI355X) only", opts->device,
+                    prop.gcnArchName);
+        auto* c = new sfm_ctx;
+        c->device = opts->device;
+        c->rank = opts->rank;
+        c->world = opts->world_size;
+        c->cu_count = prop.multiProcessorCount;
+        SFM_HIP(hipSetDevice(c->device));
+        SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        if (c->world > 1) {
+            SFM_REQUIRE(opts->comm_id, SFM_ERR_INVALID_ARG, "world_size>1 needs comm_id");
+            try {
+                rccl_comm_init(&c->comm, c->world, opts->comm_id, c->rank);
+            } catch (...) {
+                (void)hipStreamDestroy(c->stream);
+                delete c;
+                throw;
+            }
+        }
+        *out = c;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
+    return guarded([&] {
+        if (!ctx) return SFM_OK;
+        (void)hipSetDevice(ctx->device);
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        rccl_comm_destroy(ctx->comm);
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ctx_synchronize(sfm_ctx* ctx) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx, SFM_ERR_INVALID_ARG, "null ctx");
+        SFM_HIP(hipSetDevice(ctx->device));
+        SFM_HIP(hipStreamSynchronize(ctx->stream));
+        return SFM_OK;
+    });
+}

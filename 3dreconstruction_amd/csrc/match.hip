@@ -1,0 +1,576 @@
+// All-pairs 128-D SIFT descriptor matching on CDNA4 (gfx950).
+//
+// Reference path: src/sparseBuilder/sparseBuilder.cpp:809-1023 (match(),
+// Matcher_Regions(0.8, BRUTE_FORCE_L2) :919-921, fDistRatio :812) over the
+// exhaustive pair list of matchPair() :758-807; and the legacy exact matcher
+// src/frame/LocalFrame.h:31-47 / GlobalFrame.h:22-43 (BFMatcher crossCheck).
+//
+// Design:
+//   * descriptors are uint8 128-D; they are stored once in HBM as int8
+//     a' = a - 128 (translation keeps |a-b|^2) with |a'|^2 per row, so the
+//     distance matrix is an exact integer contraction on the i8 MFMA
+//     (v_mfma_i32_32x32x32_i8, int32 accumulate): |a'|^2+|b'|^2-2a'.b'.
+//   * one workgroup = 4 waves = 256 queries of image J against all of image I;
+//     each wave keeps its 64 queries' B fragments in VGPRs and streams the
+//     database in 32-row MFMA tiles; the C tile has the database row on the
+//     registers and the query on the lane, so the top-2 update is lane-local:
+//     key = ((|d'|^2 << 8) | row&255) - 512 * dot, b2 = med3(b1,b2,key),
+//     b1 = min(b1,key) (3 VALU ops per distance), merged with the running
+//     (value, index) state every 256 rows; lowest index wins ties.
+//   * the ratio test d1 < fl32(ratio^2) * d2 and the result write are fused
+//     into the epilogue; nothing but (idx, d1) per query leaves the chip.
+//   * blockIdx -> (pair, query block) is XCD-aware: the query blocks of one
+//     pair, and consecutive pairs (which share image I), land on one XCD so
+//     the database image is served from that XCD's L2.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace sfm {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int kQB = 256;   // queries per workgroup (4 waves x 64)
+constexpr int kRowPad = 256;  // rows of every image padded to this multiple
+
+// u8 -> int8 (a ^ 0x80 == a - 128), per-row |a'|^2 and the packed key base.
+__global__ void prep_kernel(uint8_t* __restrict__ d, int32_t* __restrict__ nrm,
+                            int32_t* __restrict__ ntr, const int64_t* __restrict__ row_img_start,
+                            const int32_t* __restrict__ row_valid, int64_t n_rows) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n_rows) return;
+    uint16_t* row = reinterpret_cast<uint16_t*>(d + r * 128);
+    uint16_t v = row[lane];
+    v ^= 0x8080;
+    row[lane] = v;
+    const int lo = (int)(int8_t)(v & 0xff), hi = (int)(int8_t)(v >> 8);
+    int s = lo * lo + hi * hi;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) {
+        const bool valid = row_valid[r] != 0;
+        nrm[r] = s;
+        const int64_t local = r - row_img_start[r];
+        ntr[r] = valid ? ((s << 8) | (int)(local & 255)) : INT_MAX;
+    }
+}
+
+struct Top2 {
+    int g1v, g1i, g2v;
+};
+
+__device__ __forceinline__ void merge_tile(Top2& g, int b1, int b2, int base) {
+    // tile keys: value = key >> 8, index = base + (key & 255); tiles arrive in
+    // increasing index order so strict '<' keeps the lower index on ties.
+    const int t1v = b1 >> 8, t2v = b2 >> 8;
+    const int t1i = base + (b1 & 255);
+    if (t1v < g.g1v) {
+        g.g2v = min(g.g1v, t2v);
+        g.g1v = t1v;
+        g.g1i = t1i;
+    } else {
+        g.g2v = min(g.g2v, t1v);
+    }
+}
+
+__device__ __forceinline__ void merge_lanes(Top2& g) {
+    const int o1v = __shfl_xor(g.g1v, 32), o1i = __shfl_xor(g.g1i, 32),
+              o2v = __shfl_xor(g.g2v, 32);
+    const bool other_first = o1v < g.g1v || (o1v == g.g1v && o1i < g.g1i);
+    if (other_first) {
+        g.g2v = min(g.g1v, o2v);
+        g.g1v = o1v;
+        g.g1i = o1i;
+    } else {
+        g.g2v = min(g.g2v, o1v);
+    }
+}
+
+struct MatchArgs {
+    const int8_t* desc;        // padded rows x 128 (int8, a - 128)
+    const int32_t* nrm;        // |a'|^2 per padded row
+    const int32_t* ntr;        // (|a'|^2 << 8) | (row & 255); INT_MAX for pad rows
+    const int64_t* img_row0;   // first padded row of each image
+    const int32_t* img_n;      // valid rows per image
+    const int32_t* pairs;      // (I, J) per pair of this batch
+    int32_t n_pairs;
+    int32_t qblocks;           // query blocks per pair (max over the batch)
+    int32_t swap;              // 0: queries = J, database = I; 1: queries = I, db = J
+    int32_t ratio_test;        // apply d1 < r2*d2 (RATIO mode)
+    int32_t kmul;              // -512 (runtime, keeps v_mad_i32_i24)
+    float r2;
+    int64_t out_stride;        // entries per pair in the outputs
+    int32_t* out_idx;          // [n_pairs][out_stride]
+    int32_t* out_d;            // [n_pairs][out_stride]
+};
+
+__global__ __launch_bounds__(256, 2) void match_top2_kernel(MatchArgs a) {
+    // XCD-aware bijective remap of the flat workgroup id (guide §5 T1):
+    // blocks b and b+8 share an XCD, so give each XCD a contiguous range of
+    // work items (pair-major, query block minor).
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int pair = work / a.qblocks;
+    const int qblk = work - pair * a.qblocks;
+    if (pair >= a.n_pairs) return;
+    const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
+    const int db_img = a.swap ? J : I, q_img = a.swap ? I : J;
+    const int n_db = a.img_n[db_img], n_q = a.img_n[q_img];
+    if (qblk * kQB >= n_q) return;
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int h = lane >> 5, c = lane & 31;
+    const int64_t q_row0 = a.img_row0[q_img] + qblk * kQB + wave * 64;
+    const int64_t db_row0 = a.img_row0[db_img];
+
+    // B fragments: 2 column tiles x 4 k-steps, lane holds bytes [64h+16s, +16)
+    // of query row c (k assignment shared with A; MFMA pairs equal slots).
+    v4i bq[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const v4i* src = reinterpret_cast<const v4i*>(a.desc + (q_row0 + 32 * t + c) * 128 + 64 * h);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bq[t][s] = src[s];
+    }
+
+    Top2 g[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) { g[t].g1v = INT_MAX; g[t].g1i = -1; g[t].g2v = INT_MAX; }
+
+    const int n_db_pad = (n_db + kRowPad - 1) / kRowPad * kRowPad;
+    for (int sup = 0; sup < n_db_pad; sup += 256) {
+        int b1[2] = {INT_MAX, INT_MAX}, b2[2] = {INT_MAX, INT_MAX};
+#pragma unroll 2
+        for (int tile = 0; tile < 256; tile += 32) {
+            const int64_t row = db_row0 + sup + tile;
+            const v4i* src = reinterpret_cast<const v4i*>(a.desc + (row + c) * 128 + 64 * h);
+            v4i af[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) af[s] = src[s];
+            // packed key bases of this lane's 16 rows: rows (j&3) + 8(j>>2) + 4h
+            const v4i* nsrc = reinterpret_cast<const v4i*>(a.ntr + row + 4 * h);
+            v4i nt4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nt4[q] = nsrc[2 * q];
+            v16i acc0 = {}, acc1 = {};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[0][s], acc0, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[1][s], acc1, 0, 0, 0);
+            // epilogue for both column tiles, interleaved for ILP:
+            // key = nt - 512*dot (v_mad_i32_i24; |dot| < 2^21 fits 24 bits; the
+            // multiplier is a kernel argument so it is not strength-reduced),
+            // b2 = med3(b1, b2, key), b1 = min(b1, key): 3 VALU per distance.
+            // The accumulators are consumed by compiler-generated code only: an
+            // inline asm reading MFMA results gets no hazard padding.
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int k0 = __mul24(acc0[j], a.kmul) + nt4[j >> 2][j & 3];
+                const int k1 = __mul24(acc1[j], a.kmul) + nt4[j >> 2][j & 3];
+                asm("v_med3_i32 %1, %0, %1, %4\n\t"
+                    "v_med3_i32 %3, %2, %3, %5\n\t"
+                    "v_min_i32 %0, %0, %4\n\t"
+                    "v_min_i32 %2, %2, %5"
+                    : "+v"(b1[0]), "+v"(b2[0]), "+v"(b1[1]), "+v"(b2[1])
+                    : "v"(k0), "v"(k1));
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) merge_tile(g[t], b1[t], b2[t], sup);
+    }
+
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        merge_lanes(g[t]);
+        const int q = qblk * kQB + wave * 64 + 32 * t + c;
+        if (h == 0 && q < n_q) {
+            const int nq = a.nrm[a.img_row0[q_img] + q];
+            int idx = g[t].g1i, d1 = nq + g[t].g1v;
+            if (a.ratio_test) {
+                const bool keep = n_db >= 2 && (float)d1 < a.r2 * (float)(nq + g[t].g2v);
+                if (!keep) idx = -1;
+            }
+            if (n_db == 0) { idx = -1; d1 = -1; }
+            a.out_idx[(int64_t)pair * a.out_stride + q] = idx;
+            a.out_d[(int64_t)pair * a.out_stride + q] = idx >= 0 ? d1 : -1;
+        }
+    }
+}
+
+// MUTUAL: keep (q, t) iff nnJ[q] = t and nnI[t] = q.
+__global__ void mutual_kernel(int32_t* __restrict__ idx_q, int32_t* __restrict__ d_q,
+                              const int32_t* __restrict__ idx_t, const int32_t* __restrict__ pairs,
+                              const int32_t* __restrict__ img_n, int n_pairs, int64_t stride) {
+    const int pair = blockIdx.y;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pair >= n_pairs) return;
+    const int nI = img_n[pairs[2 * pair]];
+    if (q >= nI) return;
+    const int64_t o = (int64_t)pair * stride;
+    const int t = idx_q[o + q];
+    if (t < 0 || idx_t[o + t] != q) { idx_q[o + q] = -1; d_q[o + q] = -1; }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// Order-independent digest: sum over pairs of mix(pair_id, sum over matches
+// of mix(i, j, d)), plus the total match count.
+__global__ void digest_kernel(const int32_t* __restrict__ idx, const int32_t* __restrict__ d,
+                              const int32_t* __restrict__ pairs, const int32_t* __restrict__ img_n,
+                              int mode, int64_t pair_base, int n_pairs, int64_t stride,
+                              unsigned long long* out) {
+    const int pair = blockIdx.x;
+    if (pair >= n_pairs) return;
+    const int I = pairs[2 * pair], J = pairs[2 * pair + 1];
+    const int n_out = mode == SFM_MATCH_RATIO ? img_n[J] : img_n[I];
+    uint64_t h = 0, cnt = 0;
+    for (int q = threadIdx.x; q < n_out; q += blockDim.x) {
+        const int m = idx[(int64_t)pair * stride + q];
+        if (m < 0) continue;
+        const uint32_t ii = mode == SFM_MATCH_RATIO ? (uint32_t)m : (uint32_t)q;
+        const uint32_t jj = mode == SFM_MATCH_RATIO ? (uint32_t)q : (uint32_t)m;
+        h += mix64(((uint64_t)ii << 32 | jj) ^ ((uint64_t)(uint32_t)d[(int64_t)pair * stride + q] << 21));
+        ++cnt;
+    }
+    __shared__ unsigned long long sh[2][256];
+    sh[0][threadIdx.x] = h;
+    sh[1][threadIdx.x] = cnt;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) { sh[0][threadIdx.x] += sh[0][threadIdx.x + o]; sh[1][threadIdx.x] += sh[1][threadIdx.x + o]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(&out[0], (unsigned long long)mix64(sh[0][0] + 0x9E3779B97F4A7C15ULL * (uint64_t)(pair_base + pair + 1)));
+        atomicAdd(&out[1], sh[1][0]);
+    }
+}
+
+}  // namespace
+}  // namespace sfm
+
+using namespace sfm;
+
+struct sfm_match_plan {
+    sfm_ctx* ctx = nullptr;
+    int32_t n_img = 0;
+    std::vector<int64_t> row0;   // padded row start per image
+    std::vector<int32_t> nrows;
+    int32_t max_n = 0;
+    DBuf<uint8_t> desc;
+    DBuf<int32_t> nrm, ntr, img_n;
+    DBuf<int64_t> img_row0;
+    // last run
+    int32_t mode = 0;
+    int64_t n_pairs = 0, stride = 0;
+    std::vector<int32_t> pairs_h;
+    DBuf<int32_t> pairs_d, out_idx, out_d, tmp_idx, tmp_d;
+    DBuf<unsigned long long> digest;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0;
+    int64_t launches = 0;
+};
+
+namespace {
+
+void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* off, int32_t n_img) {
+    hipStream_t s = p->ctx->stream;
+    p->n_img = n_img;
+    p->row0.resize(n_img);
+    p->nrows.resize(n_img);
+    int64_t rows = 0;
+    for (int i = 0; i < n_img; ++i) {
+        const int64_t n = off[i + 1] - off[i];
+        SFM_REQUIRE(n >= 0 && n < (1 << 24), SFM_ERR_INVALID_ARG, "image %d has %lld rows", i,
+                    (long long)n);
+        p->row0[i] = rows;
+        p->nrows[i] = (int32_t)n;
+        p->max_n = std::max<int32_t>(p->max_n, (int32_t)n);
+        rows += (n + kRowPad - 1) / kRowPad * kRowPad;
+    }
+    rows += kRowPad;  // guard rows for tile over-reads
+    std::vector<uint8_t> staging((size_t)rows * 128, 128);  // pad rows -> a' = 0
+    std::vector<int64_t> rstart(rows, 0);
+    std::vector<int32_t> rvalid(rows, 0);
+    for (int i = 0; i < n_img; ++i) {
+        std::memcpy(&staging[(size_t)p->row0[i] * 128], desc + off[i] * 128, (size_t)p->nrows[i] * 128);
+        const int64_t padded = (p->nrows[i] + kRowPad - 1) / kRowPad * kRowPad;
+        for (int64_t r = 0; r < padded; ++r) {
+            rstart[p->row0[i] + r] = p->row0[i];
+            rvalid[p->row0[i] + r] = r < p->nrows[i];
+        }
+    }
+    p->desc.alloc(staging.size());
+    p->desc.upload(staging.data(), staging.size(), s);
+    DBuf<int64_t> rs;
+    DBuf<int32_t> rv;
+    rs.alloc(rows);
+    rv.alloc(rows);
+    rs.upload(rstart.data(), rows, s);
+    rv.upload(rvalid.data(), rows, s);
+    p->nrm.alloc(rows);
+    p->ntr.alloc(rows);
+    hipLaunchKernelGGL(prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, p->desc.p,
+                       p->nrm.p, p->ntr.p, rs.p, rv.p, rows);
+    SFM_HIP(hipGetLastError());
+    p->img_n.alloc(n_img);
+    p->img_n.upload(p->nrows.data(), n_img, s);
+    p->img_row0.alloc(n_img);
+    p->img_row0.upload(p->row0.data(), n_img, s);
+    SFM_HIP(hipStreamSynchronize(s));  // staging buffers die here
+}
+
+// Run the top-2 kernel over pairs [0, n_pairs) in launch batches.
+void run_top2(sfm_match_plan* p, const int32_t* pairs_d, int64_t n_pairs, int swap, int ratio_test,
+              float r2, int32_t* out_idx, int32_t* out_d, int64_t stride) {
+    hipStream_t s = p->ctx->stream;
+    const int qblocks = std::max(1, (p->max_n + kQB - 1) / kQB);
+    const int64_t max_wg = 1 << 22;
+    const int64_t batch = std::max<int64_t>(1, max_wg / qblocks);
+    for (int64_t b0 = 0; b0 < n_pairs; b0 += batch) {
+        const int64_t nb = std::min(batch, n_pairs - b0);
+        MatchArgs a;
+        a.desc = reinterpret_cast<const int8_t*>(p->desc.p);
+        a.nrm = p->nrm.p;
+        a.ntr = p->ntr.p;
+        a.img_row0 = p->img_row0.p;
+        a.img_n = p->img_n.p;
+        a.pairs = pairs_d + 2 * b0;
+        a.n_pairs = (int32_t)nb;
+        a.qblocks = qblocks;
+        a.swap = swap;
+        a.ratio_test = ratio_test;
+        a.kmul = -512;
+        a.r2 = r2;
+        a.out_stride = stride;
+        a.out_idx = out_idx + b0 * stride;
+        a.out_d = out_d + b0 * stride;
+        hipLaunchKernelGGL(match_top2_kernel, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+        SFM_HIP(hipGetLastError());
+        ++p->launches;
+    }
+}
+
+void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const sfm_match_options* o) {
+    hipStream_t s = p->ctx->stream;
+    SFM_REQUIRE(o && (o->mode == SFM_MATCH_RATIO || o->mode == SFM_MATCH_MUTUAL),
+                SFM_ERR_INVALID_ARG, "bad match options");
+    for (int64_t q = 0; q < n_pairs; ++q)
+        SFM_REQUIRE(pairs[2 * q] >= 0 && pairs[2 * q] < p->n_img && pairs[2 * q + 1] >= 0 &&
+                        pairs[2 * q + 1] < p->n_img,
+                    SFM_ERR_INVALID_ARG, "pair %lld out of range", (long long)q);
+    p->mode = o->mode;
+    p->n_pairs = n_pairs;
+    p->stride = std::max<int64_t>(1, p->max_n);
+    p->pairs_h.assign(pairs, pairs + 2 * n_pairs);
+    if ((int64_t)p->pairs_d.n < 2 * n_pairs) p->pairs_d.alloc(std::max<int64_t>(2, 2 * n_pairs));
+    p->pairs_d.upload(pairs, 2 * n_pairs, s);
+    const size_t need = (size_t)std::max<int64_t>(1, n_pairs * p->stride);
+    if (p->out_idx.n < need) { p->out_idx.alloc(need); p->out_d.alloc(need); }
+    p->launches = 0;
+    if (!p->ev0) { SFM_HIP(hipEventCreate(&p->ev0)); SFM_HIP(hipEventCreate(&p->ev1)); }
+    SFM_HIP(hipEventRecord(p->ev0, s));
+    if (n_pairs > 0) {
+        if (o->mode == SFM_MATCH_RATIO) {
+            run_top2(p, p->pairs_d.p, n_pairs, 0, 1, o->ratio * o->ratio, p->out_idx.p, p->out_d.p,
+                     p->stride);
+        } else {
+            if (p->tmp_idx.n < need) { p->tmp_idx.alloc(need); p->tmp_d.alloc(need); }
+            // nn over J for every row of I, and nn over I for every row of J
+            run_top2(p, p->pairs_d.p, n_pairs, 1, 0, 0.f, p->out_idx.p, p->out_d.p, p->stride);
+            run_top2(p, p->pairs_d.p, n_pairs, 0, 0, 0.f, p->tmp_idx.p, p->tmp_d.p, p->stride);
+            dim3 grid((unsigned)((p->max_n + 255) / 256), 1, 1);
+            for (int64_t b0 = 0; b0 < n_pairs; b0 += 65535) {
+                const int64_t nb = std::min<int64_t>(65535, n_pairs - b0);
+                grid.y = (unsigned)nb;
+                hipLaunchKernelGGL(mutual_kernel, grid, dim3(256), 0, s, p->out_idx.p + b0 * p->stride,
+                                   p->out_d.p + b0 * p->stride, p->tmp_idx.p + b0 * p->stride,
+                                   p->pairs_d.p + 2 * b0, p->img_n.p, (int)nb, p->stride);
+                SFM_HIP(hipGetLastError());
+                ++p->launches;
+            }
+        }
+    }
+    SFM_HIP(hipEventRecord(p->ev1, s));
+}
+
+}  // namespace
+
+extern "C" int sfm_match_plan_create(sfm_ctx* ctx, const uint8_t* desc, const int64_t* offsets,
+                                     int32_t n_img, sfm_match_plan** out) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && out && offsets && n_img >= 0, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_REQUIRE(desc || offsets[n_img] == 0, SFM_ERR_INVALID_ARG, "null descriptors");
+        SFM_HIP(hipSetDevice(ctx->device));
+        auto* p = new sfm_match_plan;
+        p->ctx = ctx;
+        try {
+            upload_collection(p, desc, offsets, n_img);
+        } catch (...) {
+            delete p;
+            throw;
+        }
+        *out = p;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_run(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs,
+                                  const sfm_match_options* o, int64_t* total) {
+    return guarded([&] {
+        SFM_REQUIRE(p && (pairs || n_pairs == 0) && n_pairs >= 0, SFM_ERR_INVALID_ARG,
+                    "bad arguments");
+        SFM_HIP(hipSetDevice(p->ctx->device));
+        run_pairs(p, pairs, n_pairs, o);
+        if (total) {
+            uint64_t dg;
+            (void)dg;
+            if (!p->digest.p) p->digest.alloc(2);
+            p->digest.zero(p->ctx->stream);
+            for (int64_t b0 = 0; b0 < n_pairs; b0 += 65535) {
+                const int64_t nb = std::min<int64_t>(65535, n_pairs - b0);
+                hipLaunchKernelGGL(digest_kernel, dim3((unsigned)nb), dim3(256), 0, p->ctx->stream,
+                                   p->out_idx.p + b0 * p->stride, p->out_d.p + b0 * p->stride,
+                                   p->pairs_d.p + 2 * b0, p->img_n.p, p->mode, b0, (int)nb,
+                                   p->stride, p->digest.p);
+                SFM_HIP(hipGetLastError());
+            }
+            unsigned long long h[2];
+            SFM_HIP(hipMemcpyAsync(h, p->digest.p, sizeof h, hipMemcpyDeviceToHost, p->ctx->stream));
+            SFM_HIP(hipStreamSynchronize(p->ctx->stream));
+            *total = (int64_t)h[1];
+        }
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_digest(sfm_match_plan* p, uint64_t* digest) {
+    return guarded([&] {
+        SFM_REQUIRE(p && digest, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_HIP(hipSetDevice(p->ctx->device));
+        if (!p->digest.p) p->digest.alloc(2);
+        p->digest.zero(p->ctx->stream);
+        for (int64_t b0 = 0; b0 < p->n_pairs; b0 += 65535) {
+            const int64_t nb = std::min<int64_t>(65535, p->n_pairs - b0);
+            hipLaunchKernelGGL(digest_kernel, dim3((unsigned)nb), dim3(256), 0, p->ctx->stream,
+                               p->out_idx.p + b0 * p->stride, p->out_d.p + b0 * p->stride,
+                               p->pairs_d.p + 2 * b0, p->img_n.p, p->mode, b0, (int)nb, p->stride,
+                               p->digest.p);
+            SFM_HIP(hipGetLastError());
+        }
+        unsigned long long h[2];
+        SFM_HIP(hipMemcpyAsync(h, p->digest.p, sizeof h, hipMemcpyDeviceToHost, p->ctx->stream));
+        SFM_HIP(hipStreamSynchronize(p->ctx->stream));
+        *digest = h[0];
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_fetch(sfm_match_plan* p, int64_t* counts, uint32_t* i, uint32_t* j,
+                                    int32_t* d2) {
+    return guarded([&] {
+        SFM_REQUIRE(p && counts, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_HIP(hipSetDevice(p->ctx->device));
+        const size_t n = (size_t)(p->n_pairs * p->stride);
+        std::vector<int32_t> hi(n), hd(n);
+        if (n) {
+            SFM_HIP(hipMemcpyAsync(hi.data(), p->out_idx.p, n * 4, hipMemcpyDeviceToHost, p->ctx->stream));
+            SFM_HIP(hipMemcpyAsync(hd.data(), p->out_d.p, n * 4, hipMemcpyDeviceToHost, p->ctx->stream));
+        }
+        SFM_HIP(hipStreamSynchronize(p->ctx->stream));
+        int64_t off = 0;
+        std::vector<std::pair<uint64_t, int32_t>> v;
+        for (int64_t q = 0; q < p->n_pairs; ++q) {
+            const int I = p->pairs_h[2 * q], J = p->pairs_h[2 * q + 1];
+            const int n_out = p->mode == SFM_MATCH_RATIO ? p->nrows[J] : p->nrows[I];
+            v.clear();
+            for (int t = 0; t < n_out; ++t) {
+                const int m = hi[(size_t)q * p->stride + t];
+                if (m < 0) continue;
+                const uint32_t ii = p->mode == SFM_MATCH_RATIO ? (uint32_t)m : (uint32_t)t;
+                const uint32_t jj = p->mode == SFM_MATCH_RATIO ? (uint32_t)t : (uint32_t)m;
+                v.emplace_back(((uint64_t)ii << 32) | jj, hd[(size_t)q * p->stride + t]);
+            }
+            std::sort(v.begin(), v.end());  // IndMatch::getDeduplicated order
+            counts[q] = (int64_t)v.size();
+            if (i) {
+                for (const auto& m : v) {
+                    i[off] = (uint32_t)(m.first >> 32);
+                    j[off] = (uint32_t)(m.first & 0xffffffffu);
+                    d2[off] = m.second;
+                    ++off;
+                }
+            }
+        }
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_get_last_ms(sfm_match_plan* p, double* ms, int64_t* launches) {
+    return guarded([&] {
+        SFM_REQUIRE(p && ms, SFM_ERR_INVALID_ARG, "null argument");
+        float f = 0.f;
+        if (p->ev0) {
+            SFM_HIP(hipEventSynchronize(p->ev1));
+            SFM_HIP(hipEventElapsedTime(&f, p->ev0, p->ev1));
+        }
+        *ms = f;
+        if (launches) *launches = p->launches;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_destroy(sfm_match_plan* p) {
+    return guarded([&] {
+        if (!p) return SFM_OK;
+        (void)hipSetDevice(p->ctx->device);
+        (void)hipStreamSynchronize(p->ctx->stream);
+        if (p->ev0) { (void)hipEventDestroy(p->ev0); (void)hipEventDestroy(p->ev1); }
+        delete p;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a, const uint8_t* b,
+                               int32_t n_b, const sfm_match_options* o, int32_t* match_idx,
+                               int32_t* match_d2) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && o && match_idx && match_d2 && n_a >= 0 && n_b >= 0 &&
+                        (a || n_a == 0) && (b || n_b == 0),
+                    SFM_ERR_INVALID_ARG, "bad arguments");
+        SFM_HIP(hipSetDevice(ctx->device));
+        std::vector<uint8_t> desc((size_t)(n_a + n_b) * 128);
+        if (n_a) std::memcpy(desc.data(), a, (size_t)n_a * 128);
+        if (n_b) std::memcpy(desc.data() + (size_t)n_a * 128, b, (size_t)n_b * 128);
+        const int64_t off[3] = {0, n_a, (int64_t)n_a + n_b};
+        sfm_match_plan plan;
+        plan.ctx = ctx;
+        upload_collection(&plan, desc.data(), off, 2);
+        const int32_t pair[2] = {0, 1};
+        run_pairs(&plan, pair, 1, o);
+        const int32_t n_out = o->mode == SFM_MATCH_RATIO ? n_b : n_a;
+        if (n_out) {
+            SFM_HIP(hipMemcpyAsync(match_idx, plan.out_idx.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
+            SFM_HIP(hipMemcpyAsync(match_d2, plan.out_d.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
+        }
+        SFM_HIP(hipStreamSynchronize(ctx->stream));
+        if (plan.ev0) { (void)hipEventDestroy(plan.ev0); (void)hipEventDestroy(plan.ev1); plan.ev0 = nullptr; }
+        return SFM_OK;
+    });
+}

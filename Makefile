@@ -1,0 +1,36 @@
+# libsfmcore.so: hand-written HIP for gfx950 + host C++ (C-ABI in include/sfmcore.h)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := 3dreconstruction_amd
+CSRC := $(PKG)/csrc
+LIB := $(PKG)/lib/libsfmcore.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -mcode-object-version=5 \
+            -Wall -Wno-unused-result -I/opt/rocm/include
+SRCS := $(wildcard $(CSRC)/*.cpp $(CSRC)/*.hip)
+OBJS := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
+HDRS := $(wildcard $(CSRC)/*.h) include/sfmcore.h
+
+all: $(LIB) oracle/liboracle.so
+
+build/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(PKG)/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -ldl
+
+oracle/liboracle.so: FORCE
+	$(MAKE) -C oracle
+
+FORCE:
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean FORCE

@@ -1,0 +1,275 @@
+/*
+ * sfmcore.h — C-ABI of the MI355X-native bundle-adjustment and descriptor
+ * matching core (libsfmcore.so).
+ *
+ * This is the drop-in boundary for the two hot paths of
+ * RainbowXXX/3DReconstruction (reference tree, read-only):
+ *
+ *   BA   : src/adjuster/BundleAdjuster.h:100-141  (ceres::Solve over the
+ *          whole WorldStructure; ReprojectCost :33-69, HuberLoss(4) :109,
+ *          gauge :105, options :167-174, write-back :143-156)
+ *   Match: src/sparseBuilder/sparseBuilder.cpp:758-807 (matchPair,
+ *          exhaustive pairs) and :809-1023 (match, Matcher_Regions(0.8,
+ *          BRUTE_FORCE_L2) :919-921), plus the legacy exact matcher
+ *          src/frame/LocalFrame.h:31-47 / GlobalFrame.h:22-43
+ *          (cv::BFMatcher(NORM_L2, crossCheck) knnMatch k=1).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; every buffer is caller owned.  No
+ *     allocation crosses the ABI.  Nothing here throws.
+ *   - Every function returns 0 (SFM_OK) on success or a negative SFM_ERR_*
+ *     code; sfm_last_error() returns a thread-local message for the last
+ *     failure on the calling thread.
+ *   - One sfm_ctx per thread (contexts are independent; a context is not
+ *     re-entrant).  A context owns its HIP device, stream(s) and, when
+ *     world_size > 1, an RCCL communicator over xGMI.
+ *   - Functions marked [cpu] never touch the GPU and work without one.
+ */
+#ifndef SFMCORE_H
+#define SFMCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFM_OK                 0
+#define SFM_ERR_INVALID_ARG   -1
+#define SFM_ERR_DEVICE        -2   /* HIP runtime error / no gfx950 device      */
+#define SFM_ERR_NOT_FINITE    -3   /* non-finite residual at the initial point   */
+#define SFM_ERR_UNSUPPORTED   -4   /* problem shape outside this build's kernels */
+#define SFM_ERR_COMM          -5   /* RCCL failure                               */
+#define SFM_ERR_OOM           -6
+#define SFM_ERR_SOLVER        -7   /* LM terminated with FAILURE (not usable)    */
+
+/* [cpu] library identification and last error message (thread local). */
+const char* sfm_version(void);
+const char* sfm_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* Context                                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct sfm_ctx sfm_ctx;
+
+typedef struct sfm_ctx_opts {
+    int32_t device;          /* HIP device ordinal (local to the process)      */
+    int32_t rank;            /* 0 .. world_size-1                              */
+    int32_t world_size;      /* 1 = single GPU; >1 = landmark-sharded BA       */
+    int32_t reserved;
+    const uint8_t* comm_id;  /* 128-byte RCCL unique id from rank 0's
+                                sfm_comm_unique_id(); NULL when world_size==1 */
+} sfm_ctx_opts;
+
+/* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
+int sfm_comm_unique_id(uint8_t* out128);
+int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out);
+int sfm_ctx_destroy(sfm_ctx* ctx);
+int sfm_ctx_synchronize(sfm_ctx* ctx);
+
+/* ------------------------------------------------------------------------ */
+/* Bundle adjustment                                                         */
+/*                                                                          */
+/* Residual (BundleAdjuster.h:40-65): P = R(w) X + t (ceres::AngleAxisRotate- */
+/* Point), u = fx P0/P2 + cx, v = fy P1/P2 + cy, r = (u - obs.x, v - obs.y).   */
+/* Parameter blocks: extr[6*n_img] = {w0,w1,w2,t0,t1,t2} per image,          */
+/* intr[4*n_intr] = {fx,fy,cx,cy}, X[3*n_pt].  Loss HuberLoss(huber_a).       */
+/* ------------------------------------------------------------------------ */
+typedef struct sfm_ba_problem {
+    int32_t n_img;           /* posed images (extrinsic blocks)                */
+    int32_t n_intr;          /* intrinsic blocks (Camera objects)              */
+    int64_t n_pt;            /* world points                                   */
+    int64_t n_obs;           /* observations = residual blocks                 */
+    const int64_t* pt_offsets;/* [n_pt+1] landmark-major: obs of point p are
+                                 pt_offsets[p] .. pt_offsets[p+1]-1          */
+    const int32_t* obs_img;  /* [n_obs] image of each observation              */
+    const double*  obs_uv;   /* [2*n_obs] observed pixel (x, y)                */
+    const int32_t* img_intr; /* [n_img] intrinsic block of each image          */
+    int32_t const_img;       /* gauge: image whose pose is held constant
+                                (BundleAdjuster.h:105); -1 for none          */
+    int32_t reserved;
+    double huber_a;          /* HuberLoss scale a (reference: 4.0); <=0: none  */
+} sfm_ba_problem;
+
+typedef struct sfm_ba_options {  /* ceres::Solver::Options semantics      */
+    int32_t max_num_iterations;            /* 50   */
+    int32_t max_num_consecutive_invalid_steps; /* 5 */
+    int32_t jacobi_scaling;                /* 1    */
+    int32_t reserved;
+    double function_tolerance;             /* 1e-6 */
+    double gradient_tolerance;             /* 1e-10 */
+    double parameter_tolerance;            /* 1e-8 */
+    double initial_trust_region_radius;    /* 1e4  */
+    double max_trust_region_radius;        /* 1e16 */
+    double min_trust_region_radius;        /* 1e-32 */
+    double min_relative_decrease;          /* 1e-3 */
+    double min_lm_diagonal;                /* 1e-6 */
+    double max_lm_diagonal;                /* 1e32 */
+} sfm_ba_options;
+
+/* ceres::TerminationType subset */
+#define SFM_TERM_CONVERGENCE     0
+#define SFM_TERM_NO_CONVERGENCE  1
+#define SFM_TERM_FAILURE         2
+
+typedef struct sfm_ba_summary {
+    double initial_cost;     /* 1/2 sum rho(|r|^2) at the input parameters     */
+    double final_cost;
+    int64_t num_residuals;   /* 2 * n_obs                                      */
+    int32_t iterations;      /* ceres summary.iterations.size()-1 (iteration 0
+                                is the initial evaluation)                    */
+    int32_t successful_steps;/* counts iteration 0, as Ceres does             */
+    int32_t unsuccessful_steps;
+    int32_t termination;     /* SFM_TERM_*                                     */
+    int32_t usable;          /* summary.IsSolutionUsable()                     */
+    int32_t reserved;
+    double rmse_initial;     /* sqrt(initial_cost/num_residuals), the metric
+                                BundleAdjuster.h:137 prints                  */
+    double rmse_final;       /* sqrt(final_cost/num_residuals)  (:138)         */
+    double seconds;          /* wall time of the LM loop                        */
+} sfm_ba_summary;
+
+/* One entry per minimizer iteration (ceres::IterationSummary subset); used to
+ * compare accept/reject sequences between implementations. */
+typedef struct sfm_ba_iter {
+    int32_t iteration;
+    int32_t step_is_valid;
+    int32_t step_is_successful;
+    int32_t reserved;
+    double cost;
+    double cost_change;
+    double model_cost_change;
+    double relative_decrease;
+    double trust_region_radius;  /* radius after the iteration's update */
+    double step_norm;
+    double gradient_max_norm;
+} sfm_ba_iter;
+
+/* [cpu] Ceres defaults as used by BundleAdjuster() (BundleAdjuster.h:167-174). */
+void sfm_ba_default_options(sfm_ba_options* opts);
+
+/* One-shot: upload, solve, and (only if usable) write extr/intr/X back —
+ * mirrors BundleAdjuster::operator() (BundleAdjuster.h:176-186).  With
+ * world_size>1 every rank passes the full problem; each rank solves the
+ * landmark shard sfm_ba_partition assigns it and writes back the cameras and
+ * its own points only. */
+int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob,
+                 double* extr, double* intr, double* X,
+                 const sfm_ba_options* opts, sfm_ba_summary* summary);
+
+/* Resident variant (used by the benchmark): the plan uploads the problem and
+ * the initial parameters once; every sfm_ba_plan_run restarts from those
+ * initial parameters with all data already in HBM. */
+typedef struct sfm_ba_plan sfm_ba_plan;
+int sfm_ba_plan_create(sfm_ctx* ctx, const sfm_ba_problem* prob,
+                       const double* extr, const double* intr, const double* X,
+                       sfm_ba_plan** out);
+int sfm_ba_plan_run(sfm_ba_plan* plan, const sfm_ba_options* opts,
+                    sfm_ba_summary* summary);
+int sfm_ba_plan_download(sfm_ba_plan* plan, double* extr, double* intr, double* X);
+int sfm_ba_plan_destroy(sfm_ba_plan* plan);
+
+typedef struct sfm_ba_plan_info {
+    int64_t shard_pt_begin, shard_pt_end;   /* rank's range in sorted order   */
+    int64_t shard_obs;                      /* observations on this rank      */
+    int32_t n_chunks;                       /* Schur work chunks              */
+    int32_t band_blocks;                    /* block half-bandwidth D of S    */
+    int32_t n_cam_active, n_intr_active;    /* RCS blocks                     */
+    int64_t rcs_dim;                        /* 6*n_cam_active+4*n_intr_active */
+    double  last_kernel_ms[8];              /* per-phase device time of the
+                                               last iteration (HIP events)   */
+    int64_t schur_flops_per_iter;           /* algorithmic flops, Schur kernel*/
+    int64_t schur_launches;                 /* Schur launches in last run     */
+    double  schur_ms_total;                 /* summed Schur kernel time        */
+} sfm_ba_plan_info;
+int sfm_ba_plan_get_info(sfm_ba_plan* plan, sfm_ba_plan_info* info);
+/* Iteration log of the last sfm_ba_plan_run (n <= cap entries written). */
+int sfm_ba_plan_get_trace(sfm_ba_plan* plan, sfm_ba_iter* out, int32_t cap, int32_t* n);
+
+/* [cpu] Landmark-block partition: contiguous point ranges of the
+ * (min-camera)-sorted point order with ~equal observation counts.
+ * order[n_pt] receives the sorted point order, bounds[world_size+1] the
+ * ranges into it. */
+int sfm_ba_partition(const sfm_ba_problem* prob, int32_t world_size,
+                     int64_t* order, int64_t* bounds);
+
+/* [cpu] Deterministic synthetic scenes.  Two calls: first with
+ * NULL arrays to get sizes, then with caller-allocated arrays.  vis_mode 0 =
+ * banded orbit visibility (k consecutive cameras), 1 = random k cameras.
+ * gt_* receive ground truth, extr/intr/X the perturbed initial point. */
+typedef struct sfm_synth_ba_config {
+    int32_t n_cam, k, vis_mode, n_intr;   /* n_intr 1 = shared intrinsics      */
+    int64_t n_pt;
+    uint64_t seed;
+    double noise_px, outlier_frac;        /* 0.5, 0.01                         */
+    double perturb_rot, perturb_t, perturb_X, perturb_f; /* .01,.05,.05,5      */
+    int32_t const_img;                    /* gauge (1)                          */
+    int32_t reserved;
+} sfm_synth_ba_config;
+int sfm_synth_ba(const sfm_synth_ba_config* cfg,
+                 int64_t* pt_offsets, int32_t* obs_img, double* obs_uv,
+                 int32_t* img_intr, double* extr, double* intr, double* X,
+                 double* gt_extr, double* gt_intr, double* gt_X,
+                 int64_t* n_obs_out);
+
+/* ------------------------------------------------------------------------ */
+/* Descriptor matching (128-D uint8 SIFT/RootSIFT, exact integer L2^2)       */
+/* ------------------------------------------------------------------------ */
+#define SFM_MATCH_RATIO   0   /* Matcher_Regions(0.8, BRUTE_FORCE_L2): for each
+                                 query j of image J, top-2 over image I; keep
+                                 if d1 < fl32(ratio*ratio)*d2; emit (i, j)   */
+#define SFM_MATCH_MUTUAL  1   /* BFMatcher(NORM_L2, crossCheck) knnMatch k=1:
+                                 keep (i, j) iff j = NN_J(i) and i = NN_I(j) */
+
+typedef struct sfm_match_options {
+    int32_t mode;            /* SFM_MATCH_*                                    */
+    float ratio;             /* fDistRatio (sparseBuilder.cpp:812): 0.8f       */
+} sfm_match_options;
+
+/* Single image pair, dense output (behind LocalFrame/GlobalFrame::matchFeature).
+ * Descriptors are row-major [n][128] uint8.  For RATIO the database is `a`
+ * and the queries are `b` (OpenMVG: regions I vs queries J); for MUTUAL `a`
+ * is the OpenCV query set and `b` the train set.  Outputs, per row of `b`
+ * (RATIO) or per row of `a` (MUTUAL): the matched index in the other set or
+ * -1, and the exact squared L2 distance of that match. */
+int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a,
+                    const uint8_t* b, int32_t n_b,
+                    const sfm_match_options* opts,
+                    int32_t* match_idx, int32_t* match_d2);
+
+/* All-pairs matching over a resident descriptor collection. */
+typedef struct sfm_match_plan sfm_match_plan;
+/* desc: concatenated [sum n_img][128] uint8; desc_offsets[n_img+1]. */
+int sfm_match_plan_create(sfm_ctx* ctx, const uint8_t* desc,
+                          const int64_t* desc_offsets, int32_t n_img,
+                          sfm_match_plan** out);
+/* pairs[2*n_pairs] = (I, J).  Results stay on the device. */
+int sfm_match_plan_run(sfm_match_plan* plan, const int32_t* pairs,
+                       int64_t n_pairs, const sfm_match_options* opts,
+                       int64_t* total_matches);
+/* Fetch: counts[n_pairs]; i/j/d2[total] pair-ordered, each pair's matches
+ * sorted by (i, j) as openMVG IndMatch::getDeduplicated leaves them. */
+int sfm_match_plan_fetch(sfm_match_plan* plan, int64_t* counts,
+                         uint32_t* i, uint32_t* j, int32_t* d2);
+/* Order-independent digest of the last run's results (checksum of per-pair
+ * checksums) computed on the device. */
+int sfm_match_plan_digest(sfm_match_plan* plan, uint64_t* digest);
+int sfm_match_plan_get_last_ms(sfm_match_plan* plan, double* kernel_ms,
+                               int64_t* launches);
+int sfm_match_plan_destroy(sfm_match_plan* plan);
+
+/* [cpu] exhaustive pair list of openMVG exhaustivePairs(N)
+ * (sparseBuilder.cpp:786): all (i, j), 0 <= i < j < N, in i-major order.
+ * pairs[2 * N*(N-1)/2]. */
+int sfm_exhaustive_pairs(int32_t n_img, int32_t* pairs);
+
+/* [cpu] Deterministic synthetic RootSIFT-like descriptors for config C3:
+ * n_img frames x n_kp descriptors; frames share landmark descriptors with
+ * their neighbours (true correspondences) plus integer noise. */
+int sfm_synth_descriptors(int32_t n_img, int32_t n_kp, uint64_t seed,
+                          uint8_t* desc /* [n_img*n_kp*128] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SFMCORE_H */

@@ -1,0 +1,126 @@
+// CPU restatement of the reference's descriptor matchers — TEST
+// INFRASTRUCTURE ONLY (see oracle.h; parity unpinned).
+//
+// RATIO  (src/sparseBuilder/sparseBuilder.cpp:919-921, fDistRatio :812):
+//   OpenMVG Matcher_Regions(BRUTE_FORCE_L2) builds the matcher on regions I
+//   and queries it with regions J; for every query j the two nearest database
+//   entries (squared L2, exact for uchar) d1 <= d2 are found and the match
+//   IndMatch(i = nn index, j) is kept iff d1 < fl32(ratio^2) * d2 (OpenMVG
+//   NNdistanceRatio with Square(f_dist_ratio)).  Ties: lowest database index
+//   wins (documented choice; OpenMVG's partial_sort leaves it unspecified).
+//   Pairs with fewer than 2 database entries give no matches.  Output order:
+//   sorted by (i, j) (IndMatch::getDeduplicated).
+// MUTUAL (src/frame/LocalFrame.h:31-47, GlobalFrame.h:22-43 with
+//   cv::BFMatcher(NORM_L2, crossCheck=true), SequentialActuator.h:77):
+//   keep (q, t) iff t = argmin_t d(q, .) and q = argmin_q d(., t); first
+//   minimum (lowest index) wins.  Integer d ordering equals OpenCV's
+//   fl32(sqrt(d)) ordering for d < 2^22, which covers 512-normalised SIFT.
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "oracle.h"
+
+namespace {
+
+inline int32_t l2sq(const uint8_t* a, const uint8_t* b) {
+    int32_t s = 0;
+    for (int k = 0; k < 128; ++k) {
+        const int32_t d = (int32_t)a[k] - (int32_t)b[k];
+        s += d * d;
+    }
+    return s;
+}
+
+// For every row of q: best and second-best (value) over rows of db.
+void top2(const uint8_t* db, int32_t n_db, const uint8_t* q, int32_t n_q,
+          int32_t* best_idx, int32_t* best_d, int32_t* second_d) {
+    for (int32_t t = 0; t < n_q; ++t) {
+        int32_t b1 = INT32_MAX, b2 = INT32_MAX, i1 = -1;
+        const uint8_t* qt = q + (int64_t)t * 128;
+        for (int32_t s = 0; s < n_db; ++s) {
+            const int32_t d = l2sq(db + (int64_t)s * 128, qt);
+            if (d < b1) { b2 = b1; b1 = d; i1 = s; }
+            else if (d < b2) { b2 = d; }
+        }
+        best_idx[t] = i1; best_d[t] = b1;
+        if (second_d) second_d[t] = b2;
+    }
+}
+
+}  // namespace
+
+extern "C" int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,
+                               int32_t mode, float ratio, int32_t* match_idx,
+                               int32_t* match_d2) {
+    if (n_a < 0 || n_b < 0) return SFM_ERR_INVALID_ARG;
+    if (mode == SFM_MATCH_RATIO) {
+        std::vector<int32_t> bi(n_b), bd(n_b), sd(n_b);
+        top2(a, n_a, b, n_b, bi.data(), bd.data(), sd.data());
+        const float r2 = ratio * ratio;  // Square(f_dist_ratio) in float
+        for (int32_t t = 0; t < n_b; ++t) {
+            bool keep = n_a >= 2 && (float)bd[t] < r2 * (float)sd[t];
+            match_idx[t] = keep ? bi[t] : -1;
+            match_d2[t] = keep ? bd[t] : -1;
+        }
+        return SFM_OK;
+    }
+    if (mode == SFM_MATCH_MUTUAL) {
+        std::vector<int32_t> nq(n_a), dq(n_a), nt(n_b), dt(n_b);
+        top2(b, n_b, a, n_a, nq.data(), dq.data(), nullptr);  // per query row of a
+        top2(a, n_a, b, n_b, nt.data(), dt.data(), nullptr);  // per train row of b
+        for (int32_t q = 0; q < n_a; ++q) {
+            const int32_t t = nq[q];
+            const bool keep = t >= 0 && nt[t] == q;
+            match_idx[q] = keep ? t : -1;
+            match_d2[q] = keep ? dq[q] : -1;
+        }
+        return SFM_OK;
+    }
+    return SFM_ERR_INVALID_ARG;
+}
+
+extern "C" int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,
+                               const int32_t* pairs, int64_t n_pairs, int32_t mode,
+                               float ratio, int32_t n_threads, int64_t* counts, uint32_t* i,
+                               uint32_t* j, int32_t* d2) {
+    if (n_pairs < 0 || !counts) return SFM_ERR_INVALID_ARG;
+    std::vector<std::vector<std::pair<uint64_t, int32_t>>> res(n_pairs);
+    int err = SFM_OK;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : 1)
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        const int32_t I = pairs[2 * p], J = pairs[2 * p + 1];
+        if (I < 0 || J < 0 || I >= n_img || J >= n_img) { err = SFM_ERR_INVALID_ARG; continue; }
+        const int32_t nI = (int32_t)(offsets[I + 1] - offsets[I]);
+        const int32_t nJ = (int32_t)(offsets[J + 1] - offsets[J]);
+        const uint8_t* dI = desc + offsets[I] * 128;
+        const uint8_t* dJ = desc + offsets[J] * 128;
+        const int32_t n_out = mode == SFM_MATCH_RATIO ? nJ : nI;
+        std::vector<int32_t> idx(n_out), dd(n_out);
+        orc_match_dense(dI, nI, dJ, nJ, mode, ratio, idx.data(), dd.data());
+        auto& v = res[p];
+        for (int32_t t = 0; t < n_out; ++t) {
+            if (idx[t] < 0) continue;
+            const uint32_t ii = mode == SFM_MATCH_RATIO ? (uint32_t)idx[t] : (uint32_t)t;
+            const uint32_t jj = mode == SFM_MATCH_RATIO ? (uint32_t)t : (uint32_t)idx[t];
+            v.emplace_back(((uint64_t)ii << 32) | jj, dd[t]);
+        }
+        std::sort(v.begin(), v.end());
+    }
+    if (err) return err;
+    int64_t off = 0;
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        counts[p] = (int64_t)res[p].size();
+        if (i) {
+            for (const auto& m : res[p]) {
+                i[off] = (uint32_t)(m.first >> 32);
+                j[off] = (uint32_t)(m.first & 0xffffffffu);
+                d2[off] = m.second;
+                ++off;
+            }
+        }
+    }
+    return SFM_OK;
+}

@@ -1,0 +1,70 @@
+/*
+ * oracle.h — CPU restatement of the reference semantics.  TEST
+ * INFRASTRUCTURE ONLY: used by tests/, __graft_entry__.smoke() and the
+ * bench.py cpu_baseline leg as the checker / CPU baseline.  The product
+ * (libsfmcore.so) never links, loads or calls anything here.
+ *
+ * PARITY STATUS: parity unpinned.  The reference's BA arithmetic lives in
+ * Ceres 2.2 (CMakeLists.txt:32) and its matchers in OpenMVG (unpinned,
+ * un-vendored) and OpenCV 4 — none is present in /root/reference or in this
+ * image, and the reference ships no tests or golden outputs for either path
+ * (SURVEY.md §4, §8c).  This file restates:
+ *   - src/adjuster/BundleAdjuster.h:33-69 (ReprojectCost), :109 (Huber 4),
+ *     :105 (gauge), :125-139 (Solve + RMSE definition) with the published
+ *     Ceres 2.2 TrustRegionMinimizer / LevenbergMarquardtStrategy /
+ *     SchurEliminator control flow (documented in oracle/ba_oracle.cpp);
+ *   - OpenMVG Matcher_Regions(BRUTE_FORCE_L2) ratio matching as selected by
+ *     src/sparseBuilder/sparseBuilder.cpp:919-921 with fDistRatio 0.8 (:812);
+ *   - OpenCV BFMatcher(NORM_L2, crossCheck) knnMatch(k=1) as used by
+ *     src/frame/LocalFrame.h:31-47 and src/frame/GlobalFrame.h:22-43.
+ * The only reference-produced artefacts available are VLFeat descriptors
+ * compiled from src/nonFree/sift/vl (oracle/build_ref.sh), used as golden
+ * matcher inputs.
+ */
+#ifndef SFM_ORACLE_H
+#define SFM_ORACLE_H
+#include <stdint.h>
+#include "../include/sfmcore.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* op: 0 = sum, 1 = max.  In-place over buf[n]. */
+typedef void (*orc_allreduce_fn)(void* user, double* buf, int64_t n, int32_t op);
+
+/* Full LM solve.  shard_pts (optional) = the global point ids this rank owns
+ * (in processing order); NULL = all points.  allreduce may be NULL for a
+ * single rank.  n_threads: OpenMP threads for the per-point work. */
+int orc_ba_solve(const sfm_ba_problem* prob, double* extr, double* intr, double* X,
+                 const sfm_ba_options* opts, sfm_ba_summary* summary,
+                 sfm_ba_iter* trace, int32_t trace_cap, int32_t* trace_n,
+                 const int64_t* shard_pts, int64_t n_shard_pts,
+                 orc_allreduce_fn allreduce, void* user, int32_t n_threads);
+
+/* Cost 1/2 sum rho(|r|^2) and raw residuals r (2*n_obs, may be NULL). */
+int orc_ba_cost(const sfm_ba_problem* prob, const double* extr, const double* intr,
+                const double* X, double* cost, double* residuals);
+
+/* Residual and Jacobian of one observation, J row-major 2x13 over
+ * (fx,fy,cx,cy | w0,w1,w2,t0,t1,t2 | X0,X1,X2).  mode 0: analytic (the
+ * formulas the oracle and the GPU use), mode 1: forward-mode dual numbers
+ * through a restatement of BundleAdjuster.h:40-65 and
+ * ceres::AngleAxisRotatePoint (the Ceres AutoDiff path). */
+int orc_ba_jacobian(int32_t mode, const double* intr, const double* extr, const double* X,
+                    const double* uv, double* r, double* J);
+
+/* Dense single-pair matching: same contract as sfm_match_dense. */
+int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,
+                    int32_t mode, float ratio, int32_t* match_idx, int32_t* match_d2);
+
+/* All-pairs, compacted (counts per pair; matches sorted by (i,j)).
+ * Two calls: counts only when i/j/d2 are NULL. */
+int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,
+                    const int32_t* pairs, int64_t n_pairs, int32_t mode, float ratio,
+                    int32_t n_threads, int64_t* counts, uint32_t* i, uint32_t* j, int32_t* d2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
