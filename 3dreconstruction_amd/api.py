@@ -38,12 +38,21 @@ class Context:
         h = C.c_void_p()
         _check(self.lib.sfm_ctx_create(C.byref(o), C.byref(h)), "sfm_ctx_create")
         self.h = h
+        self._children = []
+
+    def _adopt(self, child):
+        import weakref
+        self._children.append(weakref.ref(child))
 
     def synchronize(self):
         _check(self.lib.sfm_ctx_synchronize(self.h), "sfm_ctx_synchronize")
 
     def close(self):
         if self.h:
+            for r in self._children:  # plans must die before their context
+                c = r()
+                if c is not None:
+                    c.close()
             self.lib.sfm_ctx_destroy(self.h)
             self.h = None
 
@@ -88,6 +97,7 @@ class MatchPlan:
                "sfm_match_plan_create")
         self.h = h
         self.n_pairs = 0
+        ctx._adopt(self)
 
     def run(self, pairs, mode=abi.SFM_MATCH_RATIO, ratio=0.8, count=True):
         pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
@@ -174,3 +184,74 @@ def synth_descriptors(n_img, n_kp, seed=0xC3):
     _check(lib.sfm_synth_descriptors(n_img, n_kp, seed, abi.ptr(d, abi.u8p)),
            "sfm_synth_descriptors")
     return d[:n_img * n_kp * 128].reshape(-1, 128)
+
+
+class BAPlan:
+    """Resident BA problem (sfm_ba_plan): upload once, run many times."""
+
+    def __init__(self, ctx, problem, extr, intr, X):
+        self.ctx = ctx
+        self._keep = (problem, extr, intr, X)
+        h = C.c_void_p()
+        _check(ctx.lib.sfm_ba_plan_create(ctx.h, C.byref(problem), abi.ptr(extr, abi.f64p),
+                                          abi.ptr(intr, abi.f64p), abi.ptr(X, abi.f64p),
+                                          C.byref(h)), "sfm_ba_plan_create")
+        self.h = h
+        self.shape = (len(extr), len(intr), len(X))
+        ctx._adopt(self)
+
+    def run(self, opts=None, check=True):
+        o = opts or abi.default_options()
+        s = abi.BASummary()
+        rc = self.ctx.lib.sfm_ba_plan_run(self.h, C.byref(o), C.byref(s))
+        if check and rc not in (abi.SFM_OK, abi.SFM_ERR_SOLVER):
+            _check(rc, "sfm_ba_plan_run")
+        return rc, s
+
+    def download(self):
+        e, i, x = (np.zeros(n) for n in self.shape)
+        _check(self.ctx.lib.sfm_ba_plan_download(self.h, abi.ptr(e, abi.f64p), abi.ptr(i, abi.f64p),
+                                                 abi.ptr(x, abi.f64p)), "sfm_ba_plan_download")
+        return e, i, x
+
+    def info(self):
+        inf = abi.BAPlanInfo()
+        _check(self.ctx.lib.sfm_ba_plan_get_info(self.h, C.byref(inf)), "sfm_ba_plan_get_info")
+        return inf
+
+    def trace(self, cap=256):
+        tr = (abi.BAIter * cap)()
+        n = C.c_int32()
+        _check(self.ctx.lib.sfm_ba_plan_get_trace(self.h, tr, cap, C.byref(n)),
+               "sfm_ba_plan_get_trace")
+        return [tr[k] for k in range(n.value)]
+
+    def close(self):
+        if self.h:
+            self.ctx.lib.sfm_ba_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ba_solve(ctx, problem, extr, intr, X, opts=None):
+    """sfm_ba_solve: in-place update of extr/intr/X when the solution is usable."""
+    o = opts or abi.default_options()
+    s = abi.BASummary()
+    rc = ctx.lib.sfm_ba_solve(ctx.h, C.byref(problem), abi.ptr(extr, abi.f64p),
+                              abi.ptr(intr, abi.f64p), abi.ptr(X, abi.f64p), C.byref(o),
+                              C.byref(s))
+    return rc, s
+
+
+def ba_partition(problem, world_size):
+    lib = abi.load()
+    order = np.zeros(max(problem.n_pt, 1), np.int64)
+    bounds = np.zeros(world_size + 1, np.int64)
+    _check(lib.sfm_ba_partition(C.byref(problem), world_size, abi.ptr(order, abi.i64p),
+                                abi.ptr(bounds, abi.i64p)), "sfm_ba_partition")
+    return order[:problem.n_pt], bounds

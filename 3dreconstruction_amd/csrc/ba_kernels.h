@@ -1,0 +1,90 @@
+// Launch wrappers for the BA kernels (ba_kernels.hip), called by the LM
+// driver (ba_solver.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ba_types.h"
+
+namespace sfm {
+
+// Scalar slots produced by ba_finalize (one double each).
+enum : int {
+    kScCost = 0, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E,  // summed over ranks
+    kScBadX, kScGmaxE, kScCandBad, kScStepBad,                           // max over ranks
+    kScXnorm2F, kScStepnorm2F, kScGmaxF, kScSolveFail,                   // replicated
+    kScCount
+};
+constexpr int kScSumBegin = 0, kScSumEnd = 5, kScMaxBegin = 5, kScMaxEnd = 9;
+constexpr int kPartT = 5;  // per step block: model acc, cand cost, step norm^2, step bad, cand bad
+
+struct DevProblem {
+    int32_t n_img, n_intr, n_spt, n_sobs, n_chunk, ncam, nintr, D;
+    int64_t nb, nF;
+    double huber_a, min_diag, max_diag;
+    // shard data
+    const int32_t* pt_off;
+    const int32_t* obs_img;
+    const int32_t* obs_pt;
+    const int32_t* obs_slot;
+    const double* obs_uv;
+    const ChunkDesc* chunks;
+    const int32_t* sub_starts;
+    const int32_t* img_obs_ptr;
+    const int32_t* img_obs;
+    const int32_t* img_colc;
+    const int32_t* img_coli;
+    const int32_t* img_intr;
+    const ReduceTarget* targets;
+    const ReduceTerm* terms;
+    int32_t n_targets;
+    // state
+    double* scaleE;     // [3*n_spt]
+    double* scaleF;     // [nF]
+    double* tiles;      // [n_chunk][80][80]
+    double* U;          // [n_img][100]
+    double* Ub;         // [n_img][10]
+    double* Ucn;        // [n_img][10]
+    double* Sband;      // [ncam][D+1][36]
+    double* Sarrow;     // [nintr][ncam][24]
+    double* Scorner;    // [nintr][nintr][16]
+    double* rhs;        // [nF]
+    double* bF;         // [nF]
+    double* cnF;        // [nF]
+    double* Lcol;       // [ncam][D+1][36]
+    double* Larrow;     // [ncam][nintr][24]
+    double* zF;         // [nF]
+    double* yF;         // [nF]
+    double* Wglobal;    // solve window when it does not fit LDS
+    double* part_u;     // [n_img][2]
+    double* part_s;     // [n_chunk][2]
+    double* part_t;     // [n_step_blocks][kPartT]
+    double* scal;       // [kScCount]
+};
+
+void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s);
+// U blocks, cost and non-finite flag at (cp, intr, X); scaled with scaleF.
+void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
+                   hipStream_t s);
+// Jacobi scaling at iteration 0: scaleE from per-point column norms,
+// scaleF from the reduced cnF (must run after ba_reduce of an unscaled pass).
+void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
+                    hipStream_t s);
+void ba_fscale(const DevProblem& P, hipStream_t s);
+void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
+              double radius, hipStream_t s);
+void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s);
+void ba_solve(const DevProblem& P, double radius, hipStream_t s);
+// candidate cameras/intrinsics, F-part norms and gradient
+void ba_fvec(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
+             double* cand_intr, const int32_t* blk_img, const int32_t* blk_intr, hipStream_t s);
+void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
+             const double* intr_cand, const double* X, double* X_cand, double radius,
+             hipStream_t s);
+void ba_finalize(const DevProblem& P, hipStream_t s);
+size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
+size_t solve_window_doubles(const DevProblem& P);
+int ba_step_blocks(const DevProblem& P);
+
+}  // namespace sfm

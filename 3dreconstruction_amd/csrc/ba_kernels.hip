@@ -1,0 +1,1010 @@
+// Bundle-adjustment kernels for CDNA4 (gfx950), fp64 throughout.
+//
+// Reference: src/adjuster/BundleAdjuster.h — ReprojectCost :33-69 (pinhole,
+// ceres::AngleAxisRotatePoint), HuberLoss(4) :109, ceres::Solve with
+// SPARSE_SCHUR (point blocks eliminated) :125-126, 167-174.
+//
+// One LM iteration on device:
+//   campre      per-camera rotation terms (sin/cos once per camera, not per obs)
+//   image_gram  per image (WG): U = J_F' J_F over its observations (10x10:
+//               pose 6 | intrinsics 4), b = J_F' f, cost 1/2 sum rho   [after
+//               an accepted step only]
+//   schur       per chunk (WG): observations -> corrected, Jacobi-scaled
+//               Jacobians (VALU) -> per point V + D^2, Cholesky L, w = L^-1 g
+//               -> Z = W L^-T written into an LDS panel [48 x 80] -> the 80x80
+//               chunk tile -Z Z' (and -Z w in row 79) on the fp64 MFMA
+//               (v_mfma_f64_16x16x4_f64), lower tiles only
+//   reduce      static gather plan: tiles + image blocks -> banded RCS
+//   solve       one workgroup: block-banded Cholesky with the intrinsics arrow
+//               over an LDS sliding window, forward/back substitution
+//   fvec/step   candidate cameras; per point back-substitution y_E =
+//               L^-T (w - Z' y_F), model cost change, candidate cost
+//   finalize    fixed-order reduction of per-block partials (deterministic)
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "ba_kernels.h"
+#include "common.h"
+
+namespace sfm {
+namespace {
+
+constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::epsilon()
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double clampd(double v, double lo, double hi) {
+    return fmin(fmax(v, lo), hi);
+}
+
+// ---------------------------------------------------------------------------
+// per-camera precompute
+// ---------------------------------------------------------------------------
+__global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* e = extr + 6 * (size_t)i;
+    CamPre cp;
+    const double w[3] = {e[0], e[1], e[2]};
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    cp.t[0] = e[3]; cp.t[1] = e[4]; cp.t[2] = e[5];
+    if (th2 > kEps) {
+        const double th = sqrt(th2), c = cos(th), s = sin(th), it = 1.0 / th, oc = 1.0 - c;
+        const double u[3] = {w[0] * it, w[1] * it, w[2] * it};
+        cp.c = c; cp.s = s; cp.omc = oc; cp.small = 0.0;
+        for (int a = 0; a < 3; ++a) cp.u[a] = u[a];
+        double* R = cp.R;
+        R[0] = c + oc * u[0] * u[0];        R[1] = oc * u[0] * u[1] - s * u[2]; R[2] = oc * u[0] * u[2] + s * u[1];
+        R[3] = oc * u[1] * u[0] + s * u[2]; R[4] = c + oc * u[1] * u[1];        R[5] = oc * u[1] * u[2] - s * u[0];
+        R[6] = oc * u[2] * u[0] - s * u[1]; R[7] = oc * u[2] * u[1] + s * u[0]; R[8] = c + oc * u[2] * u[2];
+        const double Wx[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                double acc = w[a] * w[b];
+                for (int k = 0; k < 3; ++k) acc += (R[k * 3 + a] - (a == k ? 1.0 : 0.0)) * Wx[k * 3 + b];
+                cp.Ar[a * 3 + b] = acc / th2;
+                cp.Al[a * 3 + b] = R[a * 3 + b];
+            }
+    } else {
+        cp.c = 1.0; cp.s = 0.0; cp.omc = 0.0; cp.small = 1.0;
+        for (int a = 0; a < 3; ++a) cp.u[a] = w[a];
+        const double Rs[9] = {1, -w[2], w[1], w[2], 1, -w[0], -w[1], w[0], 1};
+        for (int a = 0; a < 9; ++a) {
+            cp.R[a] = Rs[a];
+            cp.Al[a] = (a % 4 == 0) ? 1.0 : 0.0;
+            cp.Ar[a] = (a % 4 == 0) ? 1.0 : 0.0;
+        }
+    }
+    out[i] = cp;
+}
+
+// ---------------------------------------------------------------------------
+// residual + loss-corrected Jacobian of one observation
+// (BundleAdjuster.h:40-65 model; ceres Corrector with rho'' <= 0: r and J
+// scaled by sqrt(rho'))
+// ---------------------------------------------------------------------------
+struct Lin {
+    double f[2];
+    double Jc[2][6];
+    double Ji[2][4];
+    double Jx[2][3];
+    double half_rho;
+    bool ok;
+};
+
+template <bool JC, bool JI, bool JX>
+__device__ __forceinline__ void linearize(const CamPre& cp, const double* in, const double* X, double u0,
+                                          double u1, double huber_a, Lin& L) {
+    double P[3];
+    const double* u = cp.u;
+    const double cr0 = u[1] * X[2] - u[2] * X[1], cr1 = u[2] * X[0] - u[0] * X[2],
+                 cr2 = u[0] * X[1] - u[1] * X[0];
+    if (cp.small != 0.0) {
+        P[0] = X[0] + cr0; P[1] = X[1] + cr1; P[2] = X[2] + cr2;
+    } else {
+        const double tmp = (u[0] * X[0] + u[1] * X[1] + u[2] * X[2]) * cp.omc;
+        P[0] = X[0] * cp.c + cr0 * cp.s + u[0] * tmp;
+        P[1] = X[1] * cp.c + cr1 * cp.s + u[1] * tmp;
+        P[2] = X[2] * cp.c + cr2 * cp.s + u[2] * tmp;
+    }
+    P[0] += cp.t[0]; P[1] += cp.t[1]; P[2] += cp.t[2];
+    const double x = P[0] / P[2], y = P[1] / P[2];
+    const double r0 = in[0] * x + in[2] - u0, r1 = in[1] * y + in[3] - u1;
+    L.ok = isfinite(r0) && isfinite(r1);
+    const double sq = r0 * r0 + r1 * r1;
+    double rho0, rho1;
+    if (huber_a > 0.0 && sq > huber_a * huber_a) {
+        const double rr = sqrt(sq);
+        rho0 = 2.0 * huber_a * rr - huber_a * huber_a;
+        rho1 = fmax(DBL_MIN, huber_a / rr);
+    } else {
+        rho0 = sq; rho1 = 1.0;
+    }
+    L.half_rho = 0.5 * rho0;
+    const double sr = sqrt(rho1);
+    L.f[0] = r0 * sr; L.f[1] = r1 * sr;
+    if (JC || JI || JX) {
+        const double iz = 1.0 / P[2];
+        const double A[2][3] = {{in[0] * iz * sr, 0.0, -in[0] * x * iz * sr},
+                                {0.0, in[1] * iz * sr, -in[1] * y * iz * sr}};
+        if (JI) {
+            L.Ji[0][0] = x * sr; L.Ji[0][1] = 0.0; L.Ji[0][2] = sr; L.Ji[0][3] = 0.0;
+            L.Ji[1][0] = 0.0; L.Ji[1][1] = y * sr; L.Ji[1][2] = 0.0; L.Ji[1][3] = sr;
+        }
+        if (JX) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int j = 0; j < 3; ++j)
+                    L.Jx[r][j] = A[r][0] * cp.R[j] + A[r][1] * cp.R[3 + j] + A[r][2] * cp.R[6 + j];
+        }
+        if (JC) {
+            // dP/dw = -Al [X]x Ar
+            double N[9];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                N[0 + j] = -X[2] * cp.Ar[3 + j] + X[1] * cp.Ar[6 + j];
+                N[3 + j] = X[2] * cp.Ar[0 + j] - X[0] * cp.Ar[6 + j];
+                N[6 + j] = -X[1] * cp.Ar[0 + j] + X[0] * cp.Ar[3 + j];
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double B[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    B[k] = A[r][0] * cp.Al[k] + A[r][1] * cp.Al[3 + k] + A[r][2] * cp.Al[6 + k];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    L.Jc[r][j] = -(B[0] * N[j] + B[1] * N[3 + j] + B[2] * N[6 + j]);
+                    L.Jc[r][3 + j] = A[r][j];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// block reduction helpers (256 threads, fixed order => deterministic)
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wave_sum(double (&v)[N]) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] += __shfl_xor(v[k], o);
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// per-image Gram blocks: U = J_F' J_F (10x10), b = J_F' f, cost
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                         const double* __restrict__ intr,
+                                                         const double* __restrict__ X) {
+    const int img = blockIdx.x;
+    const int o0 = P.img_obs_ptr[img], o1 = P.img_obs_ptr[img + 1];
+    const int colc = P.img_colc[img], coli = P.img_coli[img];
+    const CamPre cp = cps[img];
+    const double* in = intr + 4 * P.img_intr[img];
+    double sc[10];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) sc[a] = colc >= 0 ? P.scaleF[colc + a] : 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) sc[6 + a] = P.scaleF[coli + a];
+    double acc[55 + 10 + 2];
+#pragma unroll
+    for (int k = 0; k < 67; ++k) acc[k] = 0.0;
+    for (int q = o0 + threadIdx.x; q < o1; q += blockDim.x) {
+        const int o = P.img_obs[q];
+        const int p = P.obs_pt[o];
+        Lin L;
+        linearize<true, true, false>(cp, in, X + 3 * p, P.obs_uv[2 * o], P.obs_uv[2 * o + 1], P.huber_a, L);
+        acc[65] += L.half_rho;
+        acc[66] = fmax(acc[66], L.ok ? 0.0 : 1.0);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            double v[10];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) v[a] = L.Jc[r][a] * sc[a];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) v[6 + a] = L.Ji[r][a] * sc[6 + a];
+            int k = 0;
+#pragma unroll
+            for (int i = 0; i < 10; ++i) {
+#pragma unroll
+                for (int j = 0; j <= i; ++j) acc[k++] += v[i] * v[j];
+                acc[55 + i] += v[i] * L.f[r];
+            }
+        }
+    }
+    // reduce: wave then across the 4 waves
+    double bad = acc[66];
+    bad = wave_max(bad);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < 66; ++k) acc[k] += __shfl_xor(acc[k], o);
+    __shared__ double red[4][67];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 66; ++k) red[wave][k] = acc[k];
+        red[wave][66] = bad;
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int i = threadIdx.x / 10, j = threadIdx.x % 10;
+        const int k = i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
+        const double v = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+        P.U[(size_t)img * 100 + threadIdx.x] = v;
+        if (i == j) P.Ucn[(size_t)img * 10 + i] = v;
+    }
+    if (threadIdx.x >= 128 && threadIdx.x < 138) {
+        const int i = threadIdx.x - 128;
+        P.Ub[(size_t)img * 10 + i] = red[0][55 + i] + red[1][55 + i] + red[2][55 + i] + red[3][55 + i];
+    }
+    if (threadIdx.x == 192) {
+        P.part_u[2 * (size_t)img] = red[0][65] + red[1][65] + red[2][65] + red[3][65];
+        P.part_u[2 * (size_t)img + 1] = fmax(fmax(red[0][66], red[1][66]), fmax(red[2][66], red[3][66]));
+    }
+}
+
+// Jacobi scale of the point columns (iteration 0): 1 / (1 + |J col|).
+__global__ void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                   const double* __restrict__ intr, const double* __restrict__ X) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P.n_spt) return;
+    double cn[3] = {0, 0, 0};
+    for (int o = P.pt_off[p]; o < P.pt_off[p + 1]; ++o) {
+        const int img = P.obs_img[o];
+        Lin L;
+        linearize<false, false, true>(cps[img], intr + 4 * P.img_intr[img], X + 3 * p, P.obs_uv[2 * o],
+                                      P.obs_uv[2 * o + 1], P.huber_a, L);
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) cn[a] += L.Jx[r][a] * L.Jx[r][a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) P.scaleE[3 * (size_t)p + a] = 1.0 / (1.0 + sqrt(cn[a]));
+}
+
+__global__ void fscale_kernel(DevProblem P) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < P.nF) P.scaleF[c] = 1.0 / (1.0 + sqrt(P.cnF[c]));
+}
+
+// ---------------------------------------------------------------------------
+// Schur chunk kernel
+// ---------------------------------------------------------------------------
+constexpr int kPanelK = 3 * kSubPts;  // 48 panel columns (3 per point)
+
+__global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                        const double* __restrict__ intr,
+                                                        const double* __restrict__ X,
+                                                        double radius) {
+    __shared__ double panel[kPanelK][kTileR];   // [k][row]
+    __shared__ double obsbuf[kSubObs][8];       // Jx (6) | f (2)
+    __shared__ double ptbuf[kSubPts][12];       // Linv (6) | w (3)
+    __shared__ double zibuf[kSubObs][12];       // per-observation J_i' M (4x3)
+    const int c = blockIdx.x;
+    const ChunkDesc& cd = P.chunks[c];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+    // wave -> lower 16x16 tiles of the 5x5 tile grid
+    constexpr int kTi[16] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 0};
+    constexpr int kTj[16] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0};
+    v4d acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+
+    double xn2 = 0.0, gmx = 0.0;
+    for (int sb = cd.sub_begin; sb < cd.sub_end; ++sb) {
+        const int p0 = P.sub_starts[sb];
+        const int p1 = (sb + 1 < cd.sub_end) ? P.sub_starts[sb + 1] : cd.pt_end;
+        const int o0 = P.pt_off[p0], nobs = P.pt_off[p1] - o0, npts = p1 - p0;
+        for (int e = tid; e < kPanelK * kTileR; e += 256) (&panel[0][0])[e] = 0.0;
+        // ---- phase A: observations -> scaled, corrected Jacobians ----------
+        Lin L;
+        int cs = -1, is = -1, pl = 0;
+        if (tid < nobs) {
+            const int o = o0 + tid;
+            const int img = P.obs_img[o];
+            const int slot = P.obs_slot[o];
+            cs = (slot & 255) - 1;
+            is = ((slot >> 8) & 255) - 1;
+            const int p = P.obs_pt[o];
+            pl = p - p0;
+            linearize<true, true, true>(cps[img], intr + 4 * P.img_intr[img], X + 3 * p, P.obs_uv[2 * o],
+                                        P.obs_uv[2 * o + 1], P.huber_a, L);
+            const int colc = P.img_colc[img], coli = P.img_coli[img];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+#pragma unroll
+                for (int a = 0; a < 6; ++a) L.Jc[r][a] *= colc >= 0 ? P.scaleF[colc + a] : 0.0;
+#pragma unroll
+                for (int a = 0; a < 4; ++a) L.Ji[r][a] *= P.scaleF[coli + a];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) L.Jx[r][a] *= P.scaleE[3 * (size_t)p + a];
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int a = 0; a < 3; ++a) obsbuf[tid][3 * r + a] = L.Jx[r][a];
+            obsbuf[tid][6] = L.f[0];
+            obsbuf[tid][7] = L.f[1];
+        }
+        __syncthreads();
+        // ---- phase B: per point V + D^2, Cholesky, w = L^-1 g_E -------------
+        if (tid < npts) {
+            const int p = p0 + tid;
+            double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};  // V00 V10 V11 V20 V21 V22
+            for (int q = P.pt_off[p] - o0; q < P.pt_off[p + 1] - o0; ++q) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const double j0 = obsbuf[q][3 * r], j1 = obsbuf[q][3 * r + 1], j2 = obsbuf[q][3 * r + 2];
+                    const double fr = obsbuf[q][6 + r];
+                    V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
+                    V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
+                    b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
+                }
+            }
+            // gradient / norm bookkeeping at x (used after a relinearisation)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double xv = X[3 * (size_t)p + a];
+                const double g = b[a] / P.scaleE[3 * (size_t)p + a];
+                xn2 += xv * xv;
+                gmx = fmax(gmx, fabs(xv - (xv - g)));
+            }
+            const int di[3] = {0, 2, 5};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) / radius);
+                V[di[a]] += lm * lm;
+            }
+            const double l00 = sqrt(V[0]), l10 = V[1] / l00, l20 = V[3] / l00;
+            const double l11 = sqrt(V[2] - l10 * l10), l21 = (V[4] - l20 * l10) / l11;
+            const double l22 = sqrt(V[5] - l20 * l20 - l21 * l21);
+            const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+            const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
+            const double i20 = -(l20 * i00 + l21 * i10) * i22;
+            const double w0 = i00 * b[0], w1 = i10 * b[0] + i11 * b[1], w2 = i20 * b[0] + i21 * b[1] + i22 * b[2];
+            ptbuf[tid][0] = i00; ptbuf[tid][1] = i10; ptbuf[tid][2] = i11;
+            ptbuf[tid][3] = i20; ptbuf[tid][4] = i21; ptbuf[tid][5] = i22;
+            panel[3 * tid + 0][kTileWRow] = w0;
+            panel[3 * tid + 1][kTileWRow] = w1;
+            panel[3 * tid + 2][kTileWRow] = w2;
+        }
+        __syncthreads();
+        // ---- phase C: Z = W L^-T into the panel -------------------------------
+        if (tid < nobs) {
+            const double i00 = ptbuf[pl][0], i10 = ptbuf[pl][1], i11 = ptbuf[pl][2];
+            const double i20 = ptbuf[pl][3], i21 = ptbuf[pl][4], i22 = ptbuf[pl][5];
+            double M[2][3];  // Jx L^-T
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                M[r][0] = L.Jx[r][0] * i00;
+                M[r][1] = L.Jx[r][0] * i10 + L.Jx[r][1] * i11;
+                M[r][2] = L.Jx[r][0] * i20 + L.Jx[r][1] * i21 + L.Jx[r][2] * i22;
+            }
+            if (cs >= 0) {
+                const int row = cd.slot_row[cs];
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int k = 0; k < 6; ++k)
+                        panel[3 * pl + a][row + k] = L.Jc[0][k] * M[0][a] + L.Jc[1][k] * M[1][a];
+            }
+#pragma unroll
+            for (int a = 0; a < 3; ++a)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) zibuf[tid][4 * a + k] = L.Ji[0][k] * M[0][a] + L.Ji[1][k] * M[1][a];
+        }
+        __syncthreads();
+        // intrinsics rows of Z: ordered sum over each point's observations
+        // (one thread per panel column => deterministic, no atomics)
+        if (tid < 3 * npts) {
+            const int pt = tid / 3, a = tid % 3, p = p0 + pt;
+            for (int q = P.pt_off[p] - o0; q < P.pt_off[p + 1] - o0; ++q) {
+                const int is2 = ((P.obs_slot[o0 + q] >> 8) & 255) - 1;
+                const int row = cd.slot_row[is2];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) panel[3 * pt + a][row + k] += zibuf[q][4 * a + k];
+            }
+        }
+        __syncthreads();
+        // ---- phase D: tile += panel panel' on the fp64 MFMA ------------------
+        const int kk = lane >> 4, ii = lane & 15;
+#pragma unroll
+        for (int ks = 0; ks < kPanelK / 4; ++ks) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int t = wave + 4 * q;
+                if (t < 15) {
+                    const double av = panel[4 * ks + kk][16 * kTi[t] + ii];
+                    const double bv = panel[4 * ks + kk][16 * kTj[t] + ii];
+                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- write the negated tile (full symmetric 80x80) -----------------------
+    double* out = P.tiles + (size_t)c * kTileR * kTileR;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int t = wave + 4 * q;
+        if (t < 15) {
+            const int ti = kTi[t], tj = kTj[t];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * ti + (lane >> 4) + 4 * r, col = 16 * tj + (lane & 15);
+                const double v = -acc[q][r];
+                out[row * kTileR + col] = v;
+                if (ti != tj) out[col * kTileR + row] = v;
+            }
+        }
+    }
+    // ---- point partials ------------------------------------------------------
+    __shared__ double red[4][2];
+    double s1[1] = {xn2};
+    wave_sum(s1);
+    const double m1 = wave_max(gmx);
+    if (lane == 0) { red[wave][0] = s1[0]; red[wave][1] = m1; }
+    __syncthreads();
+    if (tid == 0) {
+        P.part_s[2 * (size_t)c] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        P.part_s[2 * (size_t)c + 1] = fmax(fmax(red[0][1], red[1][1]), fmax(red[2][1], red[3][1]));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// static gather-reduce: one wave per target block
+// ---------------------------------------------------------------------------
+__global__ void reduce_kernel(DevProblem P, int min_kind) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int e = threadIdx.x & 63;
+    if (t >= P.n_targets) return;
+    const ReduceTarget T = P.targets[t];
+    if (T.dst_kind < min_kind) return;
+    if (e >= T.rows * T.cols) return;
+    const int r = e / T.cols, cc = e % T.cols;
+    const bool vec = T.cols == 1;
+    double s = 0.0;
+    for (int k = T.c_begin; k < T.c_end; ++k) {
+        const ReduceTerm q = P.terms[k];
+        double v;
+        if (q.kind == kSrcTile) {
+            const double* tile = P.tiles + (size_t)q.index * kTileR * kTileR;
+            v = vec ? tile[q.roff * kTileR + q.coff + r] : tile[(q.roff + r) * kTileR + q.coff + cc];
+        } else if (q.kind == kSrcU) {
+            v = P.U[(size_t)q.index * 100 + (q.roff + r) * 10 + q.coff + cc];
+        } else if (q.kind == kSrcUb) {
+            v = P.Ub[(size_t)q.index * 10 + q.roff + r];
+        } else {
+            v = P.Ucn[(size_t)q.index * 10 + q.roff + r];
+        }
+        s += (double)q.sign * v;
+    }
+    double* dst;
+    switch (T.dst_kind) {
+        case 0: dst = P.Sband; break;
+        case 1: dst = P.Sarrow; break;
+        case 2: dst = P.Scorner; break;
+        case 3: dst = P.rhs; break;
+        case 4: dst = P.bF; break;
+        default: dst = P.cnF; break;
+    }
+    dst[T.dst + (vec ? r : r * T.ld + cc)] = s;
+}
+
+// ---------------------------------------------------------------------------
+// RCS solve: block-banded (6x6 blocks, half-bandwidth D) Cholesky with a dense
+// intrinsics arrow, over a circular window of D+1 block rows.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double lm2(const DevProblem& P, int64_t col, double radius) {
+    const double lm = sqrt(clampd(P.cnF[col], P.min_diag, P.max_diag) / radius);
+    return lm * lm;
+}
+
+__device__ bool chol_inplace(double* A, int n, int ld) {  // lower, serial
+    bool ok = true;
+    for (int j = 0; j < n; ++j) {
+        double s = A[j * ld + j];
+        for (int k = 0; k < j; ++k) s -= A[j * ld + k] * A[j * ld + k];
+        if (!(s > 0.0)) ok = false;
+        const double d = sqrt(s);
+        A[j * ld + j] = d;
+        const double id = 1.0 / d;
+        for (int i = j + 1; i < n; ++i) {
+            double t = A[i * ld + j];
+            for (int k = 0; k < j; ++k) t -= A[i * ld + k] * A[j * ld + k];
+            A[i * ld + j] = t * id;
+        }
+    }
+    return ok;
+}
+
+__global__ __launch_bounds__(256) void solve_kernel(DevProblem P, double radius, int use_lds) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int ncam = P.ncam, nintr = P.nintr, D = P.D, Dp = D + 1;
+    const int tid = threadIdx.x;
+    // LDS: [fail (2 doubles) | YW (Dp x 6) | window if it fits]; else window in HBM
+    double* failp = lds;
+    double* YW = lds + 2;                                   // [Dp][6], always LDS
+    double* W = use_lds ? lds + 2 + (size_t)Dp * 6 : P.Wglobal;
+    double* WA = W + (size_t)Dp * Dp * 36;                // [nintr][Dp][24]
+    double* WC = WA + (size_t)nintr * Dp * 24;             // [4nintr][4nintr]
+    double* WR = WC + (size_t)16 * nintr * nintr;          // [Dp][6]
+    double* WRA = WR + (size_t)Dp * 6;                     // [4nintr]
+    int fail_local = 0;
+    const int na4 = 4 * nintr;
+
+    auto Wb = [&](int i, int d) { return W + ((size_t)(i % Dp) * Dp + d) * 36; };
+    auto WAb = [&](int k, int j) { return WA + ((size_t)k * Dp + (j % Dp)) * 24; };
+
+    auto load_row = [&](int i) {
+        const int dm = min(D, i);
+        for (int e = tid; e < (dm + 1) * 36; e += 256) {
+            const int d = e / 36, q = e % 36;
+            double v = P.Sband[((size_t)i * Dp + d) * 36 + q];
+            if (d == 0 && q % 7 == 0) v += lm2(P, 6LL * i + q / 7, radius);
+            Wb(i, d)[q] = v;
+        }
+        for (int e = tid; e < nintr * 24; e += 256) {
+            const int k = e / 24, q = e % 24;
+            WAb(k, i)[q] = P.Sarrow[((size_t)k * ncam + i) * 24 + q];
+        }
+        if (tid < 6) WR[(i % Dp) * 6 + tid] = P.rhs[6LL * i + tid];
+    };
+    // corner (dense 4nintr x 4nintr from 4x4 blocks) and arrow rhs
+    for (int e = tid; e < na4 * na4; e += 256) {
+        const int rr = e / na4, cc = e % na4;
+        double v = P.Scorner[(((size_t)(rr / 4) * nintr + cc / 4) * 16) + (rr % 4) * 4 + cc % 4];
+        if (rr == cc) v += lm2(P, P.nb + rr, radius);
+        WC[e] = v;
+    }
+    if (tid < na4) WRA[tid] = P.rhs[P.nb + tid];
+    for (int i = 0; i < min(Dp, ncam); ++i) load_row(i);
+    __syncthreads();
+
+    for (int j = 0; j < ncam; ++j) {
+        const int dm = min(D, ncam - 1 - j);
+        // (a) factor the diagonal block; forward-substitute its rhs
+        if (tid == 0) {
+            double* Ljj = Wb(j, 0);
+            if (!chol_inplace(Ljj, 6, 6)) fail_local = 1;
+            double* z = WR + (j % Dp) * 6;
+            for (int r = 0; r < 6; ++r) {
+                double s = z[r];
+                for (int k = 0; k < r; ++k) s -= Ljj[r * 6 + k] * z[k];
+                z[r] = s / Ljj[r * 6 + r];
+            }
+        }
+        __syncthreads();
+        // (b) TRSM: rows of blocks (j+d, j) and arrow rows: X L_jj' = S
+        {
+            const double* Ljj = Wb(j, 0);
+            const int nrows = 6 * dm + na4;
+            for (int t = tid; t < nrows; t += 256) {
+                double* row;
+                if (t < 6 * dm) row = Wb(j + t / 6 + 1, t / 6 + 1) + (t % 6) * 6;
+                else row = WAb((t - 6 * dm) / 4, j) + ((t - 6 * dm) % 4) * 6;
+                for (int cc = 0; cc < 6; ++cc) {
+                    double s = row[cc];
+                    for (int m = 0; m < cc; ++m) s -= row[m] * Ljj[cc * 6 + m];
+                    row[cc] = s / Ljj[cc * 6 + cc];
+                }
+            }
+        }
+        __syncthreads();
+        // (c) trailing updates + rhs updates + write column j out
+        {
+            const double* z = WR + (j % Dp) * 6;
+            const int npair = dm * (dm + 1) / 2;
+            const int nb_el = npair * 36, na_el = nintr * dm * 24, nc_el = na4 * na4;
+            const int nr_el = 6 * dm + na4;
+            const int total = nb_el + na_el + nc_el + nr_el;
+            for (int t = tid; t < total; t += 256) {
+                if (t < nb_el) {
+                    const int q = t / 36, e = t % 36, r = e / 6, cc = e % 6;
+                    int di = (int)((1.0 + sqrt(1.0 + 8.0 * q)) * 0.5);
+                    while (di * (di - 1) / 2 > q) --di;
+                    while ((di + 1) * di / 2 <= q) ++di;
+                    const int dk = q - di * (di - 1) / 2 + 1;
+                    const double* Li = Wb(j + di, di) + r * 6;
+                    const double* Lk = Wb(j + dk, dk) + cc * 6;
+                    double s = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) s += Li[m] * Lk[m];
+                    Wb(j + di, di - dk)[e] -= s;
+                } else if (t < nb_el + na_el) {
+                    const int u = t - nb_el, k = u / (dm * 24), rem = u % (dm * 24);
+                    const int dk = rem / 24 + 1, e = rem % 24, r = e / 6, cc = e % 6;
+                    const double* La = WAb(k, j) + r * 6;
+                    const double* Lk = Wb(j + dk, dk) + cc * 6;
+                    double s = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) s += La[m] * Lk[m];
+                    WAb(k, j + dk)[e] -= s;
+                } else if (t < nb_el + na_el + nc_el) {
+                    const int u = t - nb_el - na_el, rr = u / na4, cc = u % na4;
+                    const double* La = WAb(rr / 4, j) + (rr % 4) * 6;
+                    const double* Lb = WAb(cc / 4, j) + (cc % 4) * 6;
+                    double s = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) s += La[m] * Lb[m];
+                    WC[u] -= s;
+                } else {
+                    const int u = t - nb_el - na_el - nc_el;
+                    if (u < 6 * dm) {
+                        const int di = u / 6 + 1, r = u % 6;
+                        const double* Li = Wb(j + di, di) + r * 6;
+                        double s = 0.0;
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) s += Li[m] * z[m];
+                        WR[((j + di) % Dp) * 6 + r] -= s;
+                    } else {
+                        const int a = u - 6 * dm;
+                        const double* La = WAb(a / 4, j) + (a % 4) * 6;
+                        double s = 0.0;
+#pragma unroll
+                        for (int m = 0; m < 6; ++m) s += La[m] * z[m];
+                        WRA[a] -= s;
+                    }
+                }
+            }
+            for (int e = tid; e < (dm + 1) * 36; e += 256)
+                P.Lcol[((size_t)j * Dp + e / 36) * 36 + e % 36] = Wb(j + e / 36, e / 36)[e % 36];
+            for (int e = tid; e < nintr * 24; e += 256)
+                P.Larrow[((size_t)j * nintr + e / 24) * 24 + e % 24] = WAb(e / 24, j)[e % 24];
+            if (tid < 6) P.zF[6LL * j + tid] = z[tid];
+        }
+        __syncthreads();
+        // (d) slide the window: block row j+Dp takes row j's slot
+        if (j + Dp < ncam) load_row(j + Dp);
+        __syncthreads();
+    }
+    // corner: factor, forward, backward
+    if (tid == 0) {
+        if (na4 > 0 && !chol_inplace(WC, na4, na4)) fail_local = 1;
+        for (int r = 0; r < na4; ++r) {
+            double s = WRA[r];
+            for (int k = 0; k < r; ++k) s -= WC[r * na4 + k] * WRA[k];
+            WRA[r] = s / WC[r * na4 + r];
+        }
+        for (int r = na4 - 1; r >= 0; --r) {
+            double s = WRA[r];
+            for (int k = r + 1; k < na4; ++k) s -= WC[k * na4 + r] * WRA[k];
+            WRA[r] = s / WC[r * na4 + r];
+            P.yF[P.nb + r] = WRA[r];
+        }
+    }
+    __syncthreads();
+    // back substitution over the band (wave 0)
+    if (tid < 64) {
+        const int lane = tid;
+        for (int j = ncam - 1; j >= 0; --j) {
+            const int dm = min(D, ncam - 1 - j);
+            double s[6] = {0, 0, 0, 0, 0, 0};
+            const int nterm = 6 * dm + na4;
+            for (int t = lane; t < nterm; t += 64) {
+                const double* Lrow;  // row (c) of the block: L[c][0..5]
+                double yv;
+                if (t < 6 * dm) {
+                    const int d = t / 6 + 1, cc = t % 6;
+                    Lrow = P.Lcol + ((size_t)j * Dp + d) * 36 + cc * 6;
+                    yv = YW[((j + d) % Dp) * 6 + cc];
+                } else {
+                    const int a = t - 6 * dm;
+                    Lrow = P.Larrow + ((size_t)j * nintr + a / 4) * 24 + (a % 4) * 6;
+                    yv = WRA[a];
+                }
+#pragma unroll
+                for (int r = 0; r < 6; ++r) s[r] += Lrow[r] * yv;
+            }
+            wave_sum(s);
+            if (lane == 0) {
+                const double* Ljj = P.Lcol + ((size_t)j * Dp) * 36;
+                double y[6];
+                for (int r = 5; r >= 0; --r) {
+                    double v = P.zF[6LL * j + r] - s[r];
+                    for (int k = r + 1; k < 6; ++k) v -= Ljj[k * 6 + r] * y[k];
+                    y[r] = v / Ljj[r * 6 + r];
+                }
+                for (int r = 0; r < 6; ++r) {
+                    YW[(j % Dp) * 6 + r] = y[r];
+                    P.yF[6LL * j + r] = y[r];
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __syncthreads();
+    (void)failp;
+    if (tid == 0) P.scal[kScSolveFail] = fail_local ? 1.0 : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// F-vector epilogue: candidate cameras/intrinsics, norms, gradient
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fvec_kernel(DevProblem P, const double* __restrict__ extr,
+                                                   const double* __restrict__ intr,
+                                                   double* __restrict__ cand_extr,
+                                                   double* __restrict__ cand_intr,
+                                                   const int32_t* __restrict__ blk_img,
+                                                   const int32_t* __restrict__ blk_intr) {
+    double v[2] = {0.0, 0.0};
+    double gm = 0.0;
+    for (int64_t c = threadIdx.x; c < P.nF; c += 256) {
+        double x;
+        double* dst;
+        if (c < P.nb) {
+            const size_t o = 6 * (size_t)blk_img[c / 6] + c % 6;
+            x = extr[o]; dst = cand_extr + o;
+        } else {
+            const size_t o = 4 * (size_t)blk_intr[(c - P.nb) / 4] + (c - P.nb) % 4;
+            x = intr[o]; dst = cand_intr + o;
+        }
+        const double cand = x + (-P.yF[c]) * P.scaleF[c];
+        *dst = cand;
+        const double d = x - cand;
+        v[0] += x * x;
+        v[1] += d * d;
+        const double g = P.bF[c] / P.scaleF[c];
+        gm = fmax(gm, fabs(x - (x - g)));
+    }
+    wave_sum(v);
+    gm = wave_max(gm);
+    __shared__ double red[4][3];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) { red[wave][0] = v[0]; red[wave][1] = v[1]; red[wave][2] = gm; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        P.scal[kScXnorm2F] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        P.scal[kScStepnorm2F] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        P.scal[kScGmaxF] = fmax(fmax(red[0][2], red[1][2]), fmax(red[2][2], red[3][2]));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-point back substitution, model cost change, candidate cost
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                   const double* __restrict__ intr,
+                                                   const CamPre* __restrict__ cps_c,
+                                                   const double* __restrict__ intr_c,
+                                                   const double* __restrict__ X,
+                                                   double* __restrict__ Xc, double radius) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    double acc[3] = {0.0, 0.0, 0.0};  // model acc, candidate cost, step norm^2
+    double bad = 0.0, cbad = 0.0;     // non-finite step / non-finite candidate residual
+    if (p < P.n_spt) {
+        const double* Xp = X + 3 * (size_t)p;
+        const double* sE = P.scaleE + 3 * (size_t)p;
+        double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+        const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+        for (int o = o0; o < o1; ++o) {
+            const int img = P.obs_img[o];
+            Lin L;
+            linearize<true, true, true>(cps[img], intr + 4 * P.img_intr[img], Xp, P.obs_uv[2 * o],
+                                        P.obs_uv[2 * o + 1], P.huber_a, L);
+            const int colc = P.img_colc[img], coli = P.img_coli[img];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double q = 0.0;  // (J_F y_F) for this row
+                if (colc >= 0)
+#pragma unroll
+                    for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * P.scaleF[colc + a] * P.yF[colc + a];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) q += L.Ji[r][a] * P.scaleF[coli + a] * P.yF[coli + a];
+                const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
+                const double fr = L.f[r] - q;
+                V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
+                V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
+                b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
+            }
+        }
+        const int di[3] = {0, 2, 5};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) / radius);
+            V[di[a]] += lm * lm;
+        }
+        // y_E = (V + D^2)^-1 (g_E - W' y_F) via Cholesky
+        const double l00 = sqrt(V[0]), l10 = V[1] / l00, l20 = V[3] / l00;
+        const double l11 = sqrt(V[2] - l10 * l10), l21 = (V[4] - l20 * l10) / l11;
+        const double l22 = sqrt(V[5] - l20 * l20 - l21 * l21);
+        const double z0 = b[0] / l00, z1 = (b[1] - l10 * z0) / l11, z2 = (b[2] - l20 * z0 - l21 * z1) / l22;
+        const double y2 = z2 / l22, y1 = (z1 - l21 * y2) / l11, y0 = (z0 - l10 * y1 - l20 * y2) / l00;
+        const double yE[3] = {y0, y1, y2};
+        double xc[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            xc[a] = Xp[a] + (-yE[a]) * sE[a];
+            const double d = Xp[a] - xc[a];
+            acc[2] += d * d;
+            Xc[3 * (size_t)p + a] = xc[a];
+            if (!isfinite(xc[a])) bad = 1.0;
+        }
+        for (int o = o0; o < o1; ++o) {
+            const int img = P.obs_img[o];
+            Lin L;
+            linearize<true, true, true>(cps[img], intr + 4 * P.img_intr[img], Xp, P.obs_uv[2 * o],
+                                        P.obs_uv[2 * o + 1], P.huber_a, L);
+            const int colc = P.img_colc[img], coli = P.img_coli[img];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double m = 0.0;  // J_s step, step = -y
+                if (colc >= 0)
+#pragma unroll
+                    for (int a = 0; a < 6; ++a) m -= L.Jc[r][a] * P.scaleF[colc + a] * P.yF[colc + a];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) m -= L.Ji[r][a] * P.scaleF[coli + a] * P.yF[coli + a];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) m -= L.Jx[r][a] * sE[a] * yE[a];
+                acc[0] += m * (L.f[r] + m / 2.0);
+            }
+            Lin C;
+            linearize<false, false, false>(cps_c[img], intr_c + 4 * P.img_intr[img], xc, P.obs_uv[2 * o],
+                                           P.obs_uv[2 * o + 1], P.huber_a, C);
+            acc[1] += C.half_rho;
+            if (!C.ok) cbad = 1.0;
+        }
+        if (!isfinite(acc[0])) bad = 1.0;
+    }
+    wave_sum(acc);
+    bad = wave_max(bad);
+    cbad = wave_max(cbad);
+    __shared__ double red[4][kPartT];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        red[wave][0] = acc[0]; red[wave][1] = acc[1]; red[wave][2] = acc[2];
+        red[wave][3] = bad; red[wave][4] = cbad;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3)
+        P.part_t[kPartT * (size_t)blockIdx.x + threadIdx.x] =
+            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (threadIdx.x >= 3 && threadIdx.x < kPartT)
+        P.part_t[kPartT * (size_t)blockIdx.x + threadIdx.x] =
+            fmax(fmax(red[0][threadIdx.x], red[1][threadIdx.x]), fmax(red[2][threadIdx.x], red[3][threadIdx.x]));
+}
+
+// fixed-order reduction of the per-block partials
+__global__ __launch_bounds__(256) void finalize_kernel(DevProblem P, int n_step_blocks) {
+    double s[5] = {0, 0, 0, 0, 0};
+    double m[4] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < P.n_img; i += 256) { s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]); }
+    for (int i = threadIdx.x; i < P.n_chunk; i += 256) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
+    for (int i = threadIdx.x; i < n_step_blocks; i += 256) {
+        s[2] += P.part_t[kPartT * i]; s[3] += P.part_t[kPartT * i + 1]; s[4] += P.part_t[kPartT * i + 2];
+        m[2] = fmax(m[2], P.part_t[kPartT * i + 4]);
+        m[3] = fmax(m[3], P.part_t[kPartT * i + 3]);
+    }
+    wave_sum(s);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = wave_max(m[k]);
+    __shared__ double red[4][9];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        for (int k = 0; k < 5; ++k) red[wave][k] = s[k];
+        for (int k = 0; k < 4; ++k) red[wave][5 + k] = m[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t[9];
+        for (int k = 0; k < 5; ++k) t[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+        for (int k = 5; k < 9; ++k) t[k] = fmax(fmax(red[0][k], red[1][k]), fmax(red[2][k], red[3][k]));
+        P.scal[kScCost] = t[0];
+        P.scal[kScXnorm2E] = t[1];
+        P.scal[kScModelAcc] = t[2];
+        P.scal[kScCandCost] = t[3];
+        P.scal[kScStepnorm2E] = t[4];
+        P.scal[kScBadX] = t[5];
+        P.scal[kScGmaxE] = t[6];
+        P.scal[kScCandBad] = t[7];
+        P.scal[kScStepBad] = t[8];
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
+    if (n_img <= 0) return;
+    hipLaunchKernelGGL(campre_kernel, dim3((n_img + 127) / 128), dim3(128), 0, s, extr, n_img, out);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
+                   hipStream_t s) {
+    hipLaunchKernelGGL(image_gram_kernel, dim3(P.n_img), dim3(256), 0, s, P, cp, intr, X);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
+                    hipStream_t s) {
+    if (P.n_spt <= 0) return;
+    hipLaunchKernelGGL(point_scale_kernel, dim3((P.n_spt + 255) / 256), dim3(256), 0, s, P, cp, intr, X);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_fscale(const DevProblem& P, hipStream_t s) {
+    if (P.nF <= 0) return;
+    hipLaunchKernelGGL(fscale_kernel, dim3((unsigned)((P.nF + 255) / 256)), dim3(256), 0, s, P);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
+              hipStream_t s) {
+    if (P.n_chunk <= 0) return;
+    hipLaunchKernelGGL(schur_kernel, dim3(P.n_chunk), dim3(256), 0, s, P, cp, intr, X, radius);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
+    if (P.n_targets <= 0) return;
+    hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P, vectors_only ? 4 : 0);
+    SFM_HIP(hipGetLastError());
+}
+
+size_t solve_window_doubles(const DevProblem& P) {
+    const size_t Dp = P.D + 1;
+    return Dp * Dp * 36 + (size_t)P.nintr * Dp * 24 + 16 * (size_t)P.nintr * P.nintr + Dp * 6 +
+           4 * (size_t)P.nintr;
+}
+
+size_t solve_lds_bytes(const DevProblem& P, bool* use_lds) {
+    const size_t small = (2 + (size_t)(P.D + 1) * 6) * sizeof(double);
+    const size_t full = small + solve_window_doubles(P) * sizeof(double);
+    *use_lds = full <= 150 * 1024;
+    return *use_lds ? full : small;
+}
+
+void ba_solve(const DevProblem& P, double radius, hipStream_t s) {
+    bool lds = false;
+    const size_t bytes = solve_lds_bytes(P, &lds);
+    SFM_REQUIRE(bytes <= 160 * 1024, SFM_ERR_UNSUPPORTED, "RCS band too wide (D=%d)", P.D);
+    if (bytes > 64 * 1024)
+        SFM_HIP(hipFuncSetAttribute((const void*)solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)bytes));
+    hipLaunchKernelGGL(solve_kernel, dim3(1), dim3(256), bytes, s, P, radius, lds ? 1 : 0);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_fvec(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
+             double* cand_intr, const int32_t* blk_img, const int32_t* blk_intr, hipStream_t s) {
+    hipLaunchKernelGGL(fvec_kernel, dim3(1), dim3(256), 0, s, P, extr, intr, cand_extr, cand_intr,
+                       blk_img, blk_intr);
+    SFM_HIP(hipGetLastError());
+}
+
+int ba_step_blocks(const DevProblem& P) { return (P.n_spt + 255) / 256; }
+
+void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
+             const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
+    const int nb = ba_step_blocks(P);
+    if (nb <= 0) return;
+    hipLaunchKernelGGL(step_kernel, dim3(nb), dim3(256), 0, s, P, cp, intr, cp_cand, intr_cand, X, X_cand,
+                       radius);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_finalize(const DevProblem& P, hipStream_t s) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, P, ba_step_blocks(P));
+    SFM_HIP(hipGetLastError());
+}
+
+}  // namespace sfm

@@ -1,0 +1,351 @@
+// Host planning for the BA kernels: active parameter blocks (the reduced
+// program Ceres builds: constant and unobserved blocks removed), reduced
+// camera system (RCS) ordering, landmark partition across ranks, Schur work
+// chunks (camera windows that fit one 80-row MFMA tile), and the static
+// gather plan that sums chunk tiles and per-image blocks into the banded RCS.
+//
+// Reference: BundleAdjuster.h:100-123 builds the problem (pose blocks 6,
+// intrinsic blocks 4, point blocks 3, one residual block per observation,
+// gauge :105); ceres SPARSE_SCHUR eliminates the point blocks.
+#include "ba_plan.h"
+
+#include <algorithm>
+#include <climits>
+#include <map>
+#include <numeric>
+
+#include "common.h"
+
+namespace sfm {
+
+namespace {
+
+void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
+    pl.cam_blk.assign(P.n_img, -1);
+    pl.intr_blk.assign(P.n_intr, -1);
+    std::vector<char> cu(P.n_img, 0), iu(P.n_intr, 0);
+    for (int64_t o = 0; o < P.n_obs; ++o) {
+        cu[P.obs_img[o]] = 1;
+        iu[P.img_intr[P.obs_img[o]]] = 1;
+    }
+    for (int i = 0; i < P.n_img; ++i)
+        if (cu[i] && i != P.const_img) { pl.cam_blk[i] = pl.ncam++; pl.blk_img.push_back(i); }
+    for (int q = 0; q < P.n_intr; ++q)
+        if (iu[q]) { pl.intr_blk[q] = pl.nintr++; pl.blk_intr.push_back(q); }
+    pl.nb = 6LL * pl.ncam;
+    pl.na = 4LL * pl.nintr;
+    pl.nF = pl.nb + pl.na;
+    pl.img_colc.assign(P.n_img, -1);
+    pl.img_coli.assign(P.n_img, -1);
+    pl.img_intr.assign(P.img_intr, P.img_intr + P.n_img);
+    for (int i = 0; i < P.n_img; ++i) {
+        if (pl.cam_blk[i] >= 0) pl.img_colc[i] = 6 * pl.cam_blk[i];
+        const int q = pl.intr_blk[P.img_intr[i]];
+        if (q >= 0) pl.img_coli[i] = (int32_t)(pl.nb + 4 * q);
+    }
+}
+
+}  // namespace
+
+void partition_points(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int world,
+                      std::vector<int64_t>& order, std::vector<int64_t>& bounds) {
+    struct Key { int32_t lo, hi; int64_t id; };
+    std::vector<Key> keys(P.n_pt);
+    for (int64_t p = 0; p < P.n_pt; ++p) {
+        int lo = INT_MAX, hi = -1;
+        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+            const int b = cam_blk[P.obs_img[o]];
+            if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+        }
+        keys[p] = {lo, hi, p};
+    }
+    std::stable_sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
+        return a.lo != b.lo ? a.lo < b.lo : a.hi < b.hi;
+    });
+    order.resize(P.n_pt);
+    for (int64_t k = 0; k < P.n_pt; ++k) order[k] = keys[k].id;
+    bounds.assign(world + 1, P.n_pt);
+    bounds[0] = 0;
+    int64_t acc = 0, r = 1;
+    for (int64_t k = 0; k < P.n_pt && r < world; ++k) {
+        const int64_t p = order[k];
+        acc += P.pt_offsets[p + 1] - P.pt_offsets[p];
+        while (r < world && acc * world >= r * P.n_obs) bounds[r++] = k + 1;
+    }
+}
+
+void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
+    SFM_REQUIRE(P.n_img >= 1 && P.n_intr >= 1 && P.n_pt >= 0 && P.n_obs >= 0 &&
+                    P.pt_offsets && (P.n_obs == 0 || (P.obs_img && P.obs_uv)) && P.img_intr,
+                SFM_ERR_INVALID_ARG, "incomplete BA problem");
+    SFM_REQUIRE(P.pt_offsets[0] == 0 && P.pt_offsets[P.n_pt] == P.n_obs, SFM_ERR_INVALID_ARG,
+                "pt_offsets must run from 0 to n_obs");
+    SFM_REQUIRE(P.n_obs < INT32_MAX && P.n_pt < INT32_MAX, SFM_ERR_UNSUPPORTED,
+                "more than 2^31 observations per process");
+    for (int64_t p = 0; p < P.n_pt; ++p)
+        SFM_REQUIRE(P.pt_offsets[p + 1] >= P.pt_offsets[p], SFM_ERR_INVALID_ARG,
+                    "pt_offsets not monotone at point %lld", (long long)p);
+    for (int64_t o = 0; o < P.n_obs; ++o)
+        SFM_REQUIRE(P.obs_img[o] >= 0 && P.obs_img[o] < P.n_img, SFM_ERR_INVALID_ARG,
+                    "obs %lld references image %d", (long long)o, P.obs_img[o]);
+    for (int i = 0; i < P.n_img; ++i)
+        SFM_REQUIRE(P.img_intr[i] >= 0 && P.img_intr[i] < P.n_intr, SFM_ERR_INVALID_ARG,
+                    "image %d references intrinsics %d", i, P.img_intr[i]);
+    SFM_REQUIRE(P.const_img >= -1 && P.const_img < P.n_img, SFM_ERR_INVALID_ARG, "bad const_img");
+
+    pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
+    pl.rank = rank; pl.world = world;
+    active_sets(P, pl);
+    SFM_REQUIRE(pl.nintr <= 4, SFM_ERR_UNSUPPORTED,
+                "%d active intrinsic blocks; this build supports up to 4 (dense arrow)", pl.nintr);
+
+    // band half-width (blocks) over active cameras; duplicate views rejected
+    int32_t D = 0;
+    for (int64_t p = 0; p < P.n_pt; ++p) {
+        int lo = INT_MAX, hi = -1;
+        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+            for (int64_t o2 = P.pt_offsets[p]; o2 < o; ++o2)
+                SFM_REQUIRE(P.obs_img[o2] != P.obs_img[o], SFM_ERR_UNSUPPORTED,
+                            "point %lld observed twice by image %d", (long long)p, P.obs_img[o]);
+            const int b = pl.cam_blk[P.obs_img[o]];
+            if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+        }
+        if (hi >= 0) D = std::max(D, hi - lo);
+    }
+    pl.D = D;
+
+    partition_points(P, pl.cam_blk, world, pl.order, pl.bounds);
+
+    // ---- shard arrays ------------------------------------------------------
+    const int64_t b0 = pl.bounds[rank], b1 = pl.bounds[rank + 1];
+    pl.n_spt = b1 - b0;
+    pl.spt_global.assign(pl.order.begin() + b0, pl.order.begin() + b1);
+    pl.pt_off.assign(pl.n_spt + 1, 0);
+    for (int64_t k = 0; k < pl.n_spt; ++k) {
+        const int64_t p = pl.spt_global[k];
+        pl.pt_off[k + 1] = pl.pt_off[k] + (int32_t)(P.pt_offsets[p + 1] - P.pt_offsets[p]);
+    }
+    pl.n_sobs = pl.pt_off[pl.n_spt];
+    pl.obs_img.resize(pl.n_sobs);
+    pl.obs_pt.resize(pl.n_sobs);
+    pl.obs_uv.resize(2 * pl.n_sobs);
+    pl.obs_slot.assign(pl.n_sobs, 0);
+    for (int64_t k = 0; k < pl.n_spt; ++k) {
+        const int64_t p = pl.spt_global[k];
+        for (int64_t o = P.pt_offsets[p], s = pl.pt_off[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
+            pl.obs_img[s] = P.obs_img[o];
+            pl.obs_pt[s] = (int32_t)k;
+            pl.obs_uv[2 * s] = P.obs_uv[2 * o];
+            pl.obs_uv[2 * s + 1] = P.obs_uv[2 * o + 1];
+        }
+    }
+
+    // ---- Schur chunks --------------------------------------------------------
+    // Greedy over shard points: a chunk's F blocks (camera 6 rows, intrinsics 4
+    // rows) must fit kTileRowsUsed rows of one 80x80 tile.
+    int64_t flops = 0;
+    {
+        ChunkDesc cd{};
+        std::vector<int> cams, intrs;  // images / intrinsics in the current chunk
+        int rows = 0;
+        auto reset = [&](int32_t p) {
+            cd = ChunkDesc{};
+            cd.pt_begin = p;
+            cd.obs_begin = pl.pt_off[p];
+            for (int s = 0; s < kMaxSlots; ++s) { cd.slot_img[s] = -1; cd.slot_intr[s] = -1; cd.slot_row[s] = -1; cd.slot_col[s] = -1; }
+            cams.clear(); intrs.clear(); rows = 0;
+            cd.sub_begin = (int32_t)pl.sub_starts.size();
+        };
+        auto close = [&](int32_t p_end) {
+            cd.pt_end = p_end;
+            cd.obs_end = pl.pt_off[p_end];
+            // sub-batches: <= kSubPts points and <= kSubObs observations
+            int32_t p = cd.pt_begin;
+            while (p < p_end) {
+                pl.sub_starts.push_back(p);
+                int32_t q = p, n = 0;
+                while (q < p_end && q - p < kSubPts && n + (pl.pt_off[q + 1] - pl.pt_off[q]) <= kSubObs) {
+                    n += pl.pt_off[q + 1] - pl.pt_off[q];
+                    ++q;
+                }
+                p = q;
+            }
+            cd.sub_end = (int32_t)pl.sub_starts.size();
+            cd.n_slots = (int32_t)(cams.size() + intrs.size());
+            pl.chunks.push_back(cd);
+        };
+        if (pl.n_spt > 0) reset(0);
+        for (int32_t k = 0; k < (int32_t)pl.n_spt; ++k) {
+            const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
+            SFM_REQUIRE(nobs <= kSubObs, SFM_ERR_UNSUPPORTED, "point with %d observations (> %d)",
+                        nobs, kSubObs);
+            std::vector<int> pc, pi;
+            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                const int img = pl.obs_img[s];
+                if (pl.cam_blk[img] >= 0) pc.push_back(img);
+                const int q = P.img_intr[img];
+                if (std::find(pi.begin(), pi.end(), q) == pi.end()) pi.push_back(q);
+            }
+            const int own = 6 * (int)pc.size() + 4 * (int)pi.size();
+            SFM_REQUIRE(own <= kTileRowsUsed, SFM_ERR_UNSUPPORTED,
+                        "point %lld spans %d F rows (> %d): track too long for this build",
+                        (long long)pl.spt_global[k], own, kTileRowsUsed);
+            int add = 0, add_slots = 0;
+            for (int img : pc) if (std::find(cams.begin(), cams.end(), img) == cams.end()) { add += 6; ++add_slots; }
+            for (int q : pi) if (std::find(intrs.begin(), intrs.end(), q) == intrs.end()) { add += 4; ++add_slots; }
+            const bool full = k > cd.pt_begin &&
+                              (rows + add > kTileRowsUsed || k - cd.pt_begin >= kChunkPts ||
+                               (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots);
+            if (full) { close(k); reset(k); }
+            for (int img : pc)
+                if (std::find(cams.begin(), cams.end(), img) == cams.end()) {
+                    const int s = (int)(cams.size() + intrs.size());
+                    cams.push_back(img);
+                    cd.slot_img[s] = img; cd.slot_row[s] = rows; cd.slot_col[s] = pl.img_colc[img];
+                    rows += 6;
+                }
+            for (int q : pi)
+                if (std::find(intrs.begin(), intrs.end(), q) == intrs.end()) {
+                    const int s = (int)(cams.size() + intrs.size());
+                    intrs.push_back(q);
+                    cd.slot_intr[s] = q; cd.slot_row[s] = rows;
+                    cd.slot_col[s] = (int32_t)(pl.nb + 4 * pl.intr_blk[q]);
+                    rows += 4;
+                }
+            // observation -> slot indices (1-based; 0 = none)
+            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                const int img = pl.obs_img[s];
+                int cs = 0, is = 0;
+                for (int t = 0; t < kMaxSlots; ++t) {
+                    if (cd.slot_img[t] == img && pl.cam_blk[img] >= 0) cs = t + 1;
+                    if (cd.slot_intr[t] == P.img_intr[img]) is = t + 1;
+                }
+                pl.obs_slot[s] = cs | (is << 8);
+            }
+            const int64_t nfp = own;
+            flops += 2LL * 3 * nfp * nfp + 600LL * nobs;   // Z Z' over the point's F rows + linearisation
+        }
+        if (pl.n_spt > 0) close((int32_t)pl.n_spt);
+        pl.sub_starts.push_back((int32_t)pl.n_spt);  // sentinel
+    }
+    pl.schur_flops = flops;
+    pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +
+                     (int64_t)pl.chunks.size() * kTileR * kTileR * 8;
+
+    // ---- image CSR of shard observations ------------------------------------
+    pl.img_obs_ptr.assign(P.n_img + 1, 0);
+    for (int64_t s = 0; s < pl.n_sobs; ++s) pl.img_obs_ptr[pl.obs_img[s] + 1]++;
+    for (int i = 0; i < P.n_img; ++i) pl.img_obs_ptr[i + 1] += pl.img_obs_ptr[i];
+    pl.img_obs.resize(pl.n_sobs);
+    {
+        std::vector<int32_t> fill(pl.img_obs_ptr.begin(), pl.img_obs_ptr.end() - 1);
+        for (int64_t s = 0; s < pl.n_sobs; ++s) pl.img_obs[fill[pl.obs_img[s]]++] = (int32_t)s;
+    }
+
+    // ---- reduce plan -----------------------------------------------------------
+    const int Dp = pl.D + 1;
+    pl.n_sband = (int64_t)pl.ncam * Dp * 36;
+    pl.n_sarrow = (int64_t)pl.nintr * pl.ncam * 24;
+    pl.n_scorner = (int64_t)pl.nintr * pl.nintr * 16;
+    // chunk slot lookups: block -> (chunk, row)
+    std::map<int64_t, std::vector<ReduceTerm>> band, arrow, corner, rhs;  // keyed by target
+    for (int32_t c = 0; c < (int32_t)pl.chunks.size(); ++c) {
+        const ChunkDesc& cd = pl.chunks[c];
+        for (int a = 0; a < cd.n_slots; ++a) {
+            // rhs contribution (-Z w) from tile row 79
+            rhs[cd.slot_col[a]].push_back(ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f});
+            for (int b = 0; b < cd.n_slots; ++b) {
+                const bool ac = cd.slot_img[a] >= 0, bc = cd.slot_img[b] >= 0;
+                if (ac && bc) {
+                    const int ia = pl.cam_blk[cd.slot_img[a]], ib = pl.cam_blk[cd.slot_img[b]];
+                    if (ia < ib) continue;
+                    band[(int64_t)ia * Dp + (ia - ib)].push_back(
+                        ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
+                } else if (!ac && bc) {
+                    const int k = pl.intr_blk[cd.slot_intr[a]], ib = pl.cam_blk[cd.slot_img[b]];
+                    arrow[(int64_t)k * pl.ncam + ib].push_back(
+                        ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
+                } else if (!ac && !bc) {
+                    const int k = pl.intr_blk[cd.slot_intr[a]], l = pl.intr_blk[cd.slot_intr[b]];
+                    corner[(int64_t)k * pl.nintr + l].push_back(
+                        ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
+                }
+            }
+        }
+    }
+    auto emit = [&](int32_t kind, int64_t dst, int rows, int cols, int ld, std::vector<ReduceTerm>* tl,
+                    std::vector<ReduceTerm> extra) {
+        ReduceTarget t{};
+        t.dst = dst; t.dst_kind = kind; t.rows = rows; t.cols = cols; t.ld = ld;
+        t.c_begin = (int32_t)pl.terms.size();
+        for (const auto& e : extra) pl.terms.push_back(e);
+        if (tl) for (const auto& e : *tl) pl.terms.push_back(e);
+        t.c_end = (int32_t)pl.terms.size();
+        pl.targets.push_back(t);
+    };
+    for (int i = 0; i < pl.ncam; ++i) {
+        const int img = pl.blk_img[i];
+        for (int d = 0; d <= std::min(pl.D, i); ++d) {
+            auto it = band.find((int64_t)i * Dp + d);
+            std::vector<ReduceTerm> ex;
+            if (d == 0) ex.push_back(ReduceTerm{kSrcU, img, 0, 0, 1.f});
+            emit(0, ((int64_t)i * Dp + d) * 36, 6, 6, 6, it == band.end() ? nullptr : &it->second, ex);
+        }
+    }
+    for (int k = 0; k < pl.nintr; ++k)
+        for (int i = 0; i < pl.ncam; ++i) {
+            const int img = pl.blk_img[i];
+            auto it = arrow.find((int64_t)k * pl.ncam + i);
+            std::vector<ReduceTerm> ex;
+            if (pl.intr_blk[P.img_intr[img]] == k) ex.push_back(ReduceTerm{kSrcU, img, 6, 0, 1.f});
+            emit(1, ((int64_t)k * pl.ncam + i) * 24, 4, 6, 6, it == arrow.end() ? nullptr : &it->second, ex);
+        }
+    for (int k = 0; k < pl.nintr; ++k)
+        for (int l = 0; l < pl.nintr; ++l) {
+            auto it = corner.find((int64_t)k * pl.nintr + l);
+            std::vector<ReduceTerm> ex;
+            if (k == l)
+                for (int img = 0; img < P.n_img; ++img)
+                    if (pl.intr_blk[P.img_intr[img]] == k) ex.push_back(ReduceTerm{kSrcU, img, 6, 6, 1.f});
+            emit(2, ((int64_t)k * pl.nintr + l) * 16, 4, 4, 4, it == corner.end() ? nullptr : &it->second, ex);
+        }
+    // vectors: rhs = bF - Z w, bF, cnF
+    for (int vk = 3; vk <= 5; ++vk) {
+        for (int i = 0; i < pl.ncam; ++i) {
+            const int img = pl.blk_img[i];
+            std::vector<ReduceTerm> ex{ReduceTerm{vk == 5 ? kSrcUcn : kSrcUb, img, 0, 0, 1.f}};
+            auto it = rhs.find(6LL * i);
+            emit(vk, 6LL * i, 6, 1, 1, (vk == 3 && it != rhs.end()) ? &it->second : nullptr, ex);
+        }
+        for (int k = 0; k < pl.nintr; ++k) {
+            std::vector<ReduceTerm> ex;
+            for (int img = 0; img < P.n_img; ++img)
+                if (pl.intr_blk[P.img_intr[img]] == k)
+                    ex.push_back(ReduceTerm{vk == 5 ? kSrcUcn : kSrcUb, img, 6, 0, 1.f});
+            auto it = rhs.find(pl.nb + 4LL * k);
+            emit(vk, pl.nb + 4LL * k, 4, 1, 1, (vk == 3 && it != rhs.end()) ? &it->second : nullptr, ex);
+        }
+    }
+}
+
+}  // namespace sfm
+
+extern "C" int sfm_ba_partition(const sfm_ba_problem* prob, int32_t world_size, int64_t* order,
+                                int64_t* bounds) {
+    using namespace sfm;
+    return guarded([&] {
+        SFM_REQUIRE(prob && order && bounds && world_size >= 1, SFM_ERR_INVALID_ARG, "bad arguments");
+        BAHostPlan tmp;
+        std::vector<int32_t> cam_blk(prob->n_img, -1);
+        int nc = 0;
+        std::vector<char> used(prob->n_img, 0);
+        for (int64_t o = 0; o < prob->n_obs; ++o) used[prob->obs_img[o]] = 1;
+        for (int i = 0; i < prob->n_img; ++i)
+            if (used[i] && i != prob->const_img) cam_blk[i] = nc++;
+        std::vector<int64_t> ord, bnd;
+        partition_points(*prob, cam_blk, world_size, ord, bnd);
+        std::copy(ord.begin(), ord.end(), order);
+        std::copy(bnd.begin(), bnd.end(), bounds);
+        return SFM_OK;
+    });
+}

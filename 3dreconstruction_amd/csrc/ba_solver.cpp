@@ -1,0 +1,469 @@
+// Levenberg-Marquardt driver for the gfx950 BA kernels and the BA C-ABI.
+//
+// Mirrors BundleAdjuster::operator() (src/adjuster/BundleAdjuster.h:176-186):
+// parameters are copied in, solved, and written back only if the solution is
+// usable (:128-131, :143-156).  The trust-region control flow is the Ceres
+// 2.2 TrustRegionMinimizer + LevenbergMarquardtStrategy restated in
+// oracle/ba_oracle.cpp; every decision here is taken on the host from scalars
+// the kernels reduce on the device (one device->host sync per iteration), so
+// the accept/reject sequence follows the oracle's decision for decision.
+//
+// Multi-GPU (world_size > 1): each rank owns a landmark block (contiguous
+// range of the camera-sorted point order); per iteration the reduced camera
+// system and the E-part scalars are summed with RCCL all-reduce over xGMI and
+// every rank solves the (identical) RCS redundantly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "ba_kernels.h"
+#include "ba_plan.h"
+#include "common.h"
+
+using namespace sfm;
+
+struct sfm_ba_plan {
+    sfm_ctx* ctx = nullptr;
+    BAHostPlan hp;
+    DevProblem P{};
+    DBuf<int32_t> pt_off, obs_img, obs_pt, obs_slot, sub_starts, img_obs_ptr, img_obs, img_colc,
+        img_coli, img_intr, blk_img, blk_intr;
+    DBuf<double> obs_uv;
+    DBuf<ChunkDesc> chunks;
+    DBuf<ReduceTarget> targets;
+    DBuf<ReduceTerm> terms;
+    DBuf<double> X0, Xa, Xb, extr0, intr0, ea, eb, ia, ib;
+    DBuf<CamPre> cpa, cpb;
+    DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
+        part_t, scal;
+    int64_t rcs_n = 0;
+    double* scal_h = nullptr;  // pinned
+    std::vector<sfm_ba_iter> trace;
+    double last_ms[8] = {0};
+    double schur_ms_total = 0;
+    int64_t schur_launches = 0;
+    std::vector<hipEvent_t> ev;
+    bool cur_is_a = true;
+    ~sfm_ba_plan() {
+        if (scal_h) (void)hipHostFree(scal_h);
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+namespace {
+
+template <class T>
+void up(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
+    d.alloc(std::max<size_t>(h.size(), 1));
+    d.upload(h.data(), h.size(), s);
+}
+
+void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr, const double* intr,
+                 const double* X) {
+    sfm_ctx* ctx = pl->ctx;
+    hipStream_t s = ctx->stream;
+    BAHostPlan& h = pl->hp;
+    build_plan(prob, ctx->rank, ctx->world, h);
+    up(pl->pt_off, h.pt_off, s);
+    up(pl->obs_img, h.obs_img, s);
+    up(pl->obs_pt, h.obs_pt, s);
+    up(pl->obs_slot, h.obs_slot, s);
+    up(pl->obs_uv, h.obs_uv, s);
+    up(pl->chunks, h.chunks, s);
+    up(pl->sub_starts, h.sub_starts, s);
+    up(pl->img_obs_ptr, h.img_obs_ptr, s);
+    up(pl->img_obs, h.img_obs, s);
+    up(pl->img_colc, h.img_colc, s);
+    up(pl->img_coli, h.img_coli, s);
+    up(pl->img_intr, h.img_intr, s);
+    up(pl->blk_img, h.blk_img, s);
+    up(pl->blk_intr, h.blk_intr, s);
+    up(pl->targets, h.targets, s);
+    up(pl->terms, h.terms, s);
+    std::vector<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
+    for (int64_t k = 0; k < h.n_spt; ++k)
+        for (int a = 0; a < 3; ++a) xs[3 * k + a] = X[3 * h.spt_global[k] + a];
+    up(pl->X0, xs, s);
+    pl->Xa.alloc(xs.size());
+    pl->Xb.alloc(xs.size());
+    std::vector<double> e(extr, extr + 6 * (size_t)prob.n_img), in(intr, intr + 4 * (size_t)prob.n_intr);
+    up(pl->extr0, e, s);
+    up(pl->intr0, in, s);
+    pl->ea.alloc(e.size()); pl->eb.alloc(e.size());
+    pl->ia.alloc(in.size()); pl->ib.alloc(in.size());
+    pl->cpa.alloc(prob.n_img); pl->cpb.alloc(prob.n_img);
+    const int64_t nF = std::max<int64_t>(h.nF, 1);
+    pl->scaleE.alloc(xs.size());
+    pl->scaleF.alloc(nF);
+    pl->tiles.alloc(std::max<size_t>(h.chunks.size(), 1) * kTileR * kTileR);
+    pl->U.alloc(100 * (size_t)prob.n_img);
+    pl->Ub.alloc(10 * (size_t)prob.n_img);
+    pl->Ucn.alloc(10 * (size_t)prob.n_img);
+    pl->rcs_n = h.n_sband + h.n_sarrow + h.n_scorner + 3 * h.nF + 1;
+    pl->rcs.alloc(pl->rcs_n);
+    pl->rcs.zero(s);
+    const int Dp = h.D + 1;
+    pl->Lcol.alloc(std::max<size_t>((size_t)h.ncam * Dp * 36, 1));
+    pl->Larrow.alloc(std::max<size_t>((size_t)h.ncam * h.nintr * 24, 1));
+    pl->zF.alloc(nF);
+    pl->yF.alloc(nF);
+    pl->part_u.alloc(2 * (size_t)prob.n_img);
+    pl->part_s.alloc(2 * std::max<size_t>(h.chunks.size(), 1));
+    pl->scal.alloc(kScCount);
+    pl->scal.zero(s);
+    SFM_HIP(hipHostMalloc((void**)&pl->scal_h, kScCount * sizeof(double), hipHostMallocDefault));
+
+    DevProblem& P = pl->P;
+    P.n_img = prob.n_img; P.n_intr = prob.n_intr;
+    P.n_spt = (int32_t)h.n_spt; P.n_sobs = (int32_t)h.n_sobs;
+    P.n_chunk = (int32_t)h.chunks.size();
+    P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D;
+    P.nb = h.nb; P.nF = h.nF;
+    P.huber_a = prob.huber_a;
+    P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p; P.obs_pt = pl->obs_pt.p;
+    P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
+    P.sub_starts = pl->sub_starts.p; P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
+    P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
+    P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
+    P.scaleE = pl->scaleE.p; P.scaleF = pl->scaleF.p; P.tiles = pl->tiles.p;
+    P.U = pl->U.p; P.Ub = pl->Ub.p; P.Ucn = pl->Ucn.p;
+    P.Sband = pl->rcs.p;
+    P.Sarrow = P.Sband + h.n_sband;
+    P.Scorner = P.Sarrow + h.n_sarrow;
+    P.rhs = P.Scorner + h.n_scorner;
+    P.bF = P.rhs + h.nF;
+    P.cnF = P.bF + h.nF;
+    P.Lcol = pl->Lcol.p; P.Larrow = pl->Larrow.p; P.zF = pl->zF.p; P.yF = pl->yF.p;
+    bool lds = true;
+    solve_lds_bytes(P, &lds);
+    if (!lds) pl->Wg.alloc(solve_window_doubles(P));
+    P.Wglobal = pl->Wg.p;
+    P.part_u = pl->part_u.p; P.part_s = pl->part_s.p;
+    pl->part_t.alloc((size_t)kPartT * std::max(ba_step_blocks(P), 1));
+    P.part_t = pl->part_t.p;
+    P.scal = pl->scal.p;
+    pl->ev.resize(16);
+    for (auto& e2 : pl->ev) SFM_HIP(hipEventCreate(&e2));
+    SFM_HIP(hipStreamSynchronize(s));
+}
+
+struct IterState {
+    double* X; double* Xc; double* e; double* ec; double* in; double* inc; CamPre* cp; CamPre* cpc;
+};
+
+int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
+    sfm_ctx* ctx = pl->ctx;
+    hipStream_t s = ctx->stream;
+    BAHostPlan& h = pl->hp;
+    DevProblem& P = pl->P;
+    P.min_diag = O.min_lm_diagonal;
+    P.max_diag = O.max_lm_diagonal;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::memset(sum, 0, sizeof *sum);
+    sum->num_residuals = 2 * h.n_obs;
+    pl->trace.clear();
+    pl->schur_ms_total = 0;
+    pl->schur_launches = 0;
+
+    // working buffers: a = current point, b = candidate
+    IterState S{pl->Xa.p, pl->Xb.p, pl->ea.p, pl->eb.p, pl->ia.p, pl->ib.p, pl->cpa.p, pl->cpb.p};
+    const size_t ne = 6 * (size_t)h.n_img, ni = 4 * (size_t)h.n_intr, nx = 3 * (size_t)h.n_spt;
+    if (nx) SFM_HIP(hipMemcpyAsync(S.X, pl->X0.p, nx * 8, hipMemcpyDeviceToDevice, s));
+    SFM_HIP(hipMemcpyAsync(S.e, pl->extr0.p, ne * 8, hipMemcpyDeviceToDevice, s));
+    SFM_HIP(hipMemcpyAsync(S.in, pl->intr0.p, ni * 8, hipMemcpyDeviceToDevice, s));
+
+    auto allreduce_rcs = [&] {
+        if (ctx->world > 1) rccl_allreduce_f64(ctx->comm, pl->rcs.p, pl->rcs_n, 0, s);
+    };
+    auto relinearize = [&] {
+        ba_image_gram(P, S.cp, S.in, S.X, s);
+    };
+
+    // ---- iteration zero: Jacobi scaling from the corrected Jacobian at x0 ----
+    ba_campre(S.e, h.n_img, S.cp, s);
+    {
+        std::vector<double> ones(std::max<size_t>(std::max<int64_t>(h.nF, nx), 1), 1.0);
+        pl->scaleF.upload(ones.data(), std::max<int64_t>(h.nF, 1), s);
+        if (nx) pl->scaleE.upload(ones.data(), nx, s);
+        SFM_HIP(hipStreamSynchronize(s));
+    }
+    if (O.jacobi_scaling) {
+        relinearize();                 // unscaled column norms of the F blocks
+        ba_reduce(P, true, s);
+        allreduce_rcs();
+        ba_fscale(P, s);
+        ba_point_scale(P, S.cp, S.in, S.X, s);
+    }
+    relinearize();
+
+    double radius = O.initial_trust_region_radius, decrease_factor = 2.0;
+    int consecutive_invalid = 0;
+    double x_cost = 0.0, x_norm = 0.0;
+    bool relin_pending = true;   // Finalize of iteration 0 / of an accepted step pending
+    sfm_ba_iter pending{};
+    pending.iteration = 0; pending.step_is_valid = 1; pending.step_is_successful = 1;
+    int term = -1;
+    int ev_i = 0;
+    int last_iter = 0;
+
+    auto finalize = [&](const sfm_ba_iter& cur, double gmax) -> int {
+        pl->trace.push_back(cur);
+        last_iter = cur.iteration;
+        if (cur.step_is_successful) sum->successful_steps++; else sum->unsuccessful_steps++;
+        if (cur.iteration >= O.max_num_iterations) return SFM_TERM_NO_CONVERGENCE;
+        if (gmax <= O.gradient_tolerance) return SFM_TERM_CONVERGENCE;
+        if (radius < O.min_trust_region_radius) return SFM_TERM_CONVERGENCE;
+        return -1;
+    };
+
+    double prev_gmax = 0.0;
+    while (term < 0) {
+        // ---- one step on the device ------------------------------------------
+        const bool timed = ev_i + 1 < (int)pl->ev.size();
+        if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i], s));
+        ba_schur(P, S.cp, S.in, S.X, radius, s);
+        if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
+        ba_reduce(P, false, s);
+        allreduce_rcs();
+        ba_solve(P, radius, s);
+        SFM_HIP(hipMemcpyAsync(S.ec, S.e, ne * 8, hipMemcpyDeviceToDevice, s));
+        SFM_HIP(hipMemcpyAsync(S.inc, S.in, ni * 8, hipMemcpyDeviceToDevice, s));
+        ba_fvec(P, S.e, S.in, S.ec, S.inc, pl->blk_img.p, pl->blk_intr.p, s);
+        ba_campre(S.ec, h.n_img, S.cpc, s);
+        ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
+        ba_finalize(P, s);
+        if (ctx->world > 1) {
+            rccl_allreduce_f64(ctx->comm, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);
+            rccl_allreduce_f64(ctx->comm, P.scal + kScMaxBegin, kScMaxEnd - kScMaxBegin, 1, s);
+        }
+        SFM_HIP(hipMemcpyAsync(pl->scal_h, P.scal, kScCount * 8, hipMemcpyDeviceToHost, s));
+        SFM_HIP(hipStreamSynchronize(s));
+        if (timed) {
+            float ms = 0.f;
+            SFM_HIP(hipEventElapsedTime(&ms, pl->ev[ev_i], pl->ev[ev_i + 1]));
+            pl->schur_ms_total += ms;
+            pl->schur_launches++;
+            pl->last_ms[0] = ms;
+        }
+        const double* sc = pl->scal_h;
+
+        // ---- Finalize of the previous accepted iteration (needs g, x at x) ----
+        if (relin_pending) {
+            relin_pending = false;
+            x_cost = sc[kScCost];
+            if (pending.iteration == 0) {
+                sum->initial_cost = x_cost;
+                if (sc[kScBadX] != 0.0 || !std::isfinite(x_cost)) {
+                    term = SFM_TERM_FAILURE;
+                    sum->termination = term;
+                    set_error("residual evaluation at the initial point is not finite");
+                    sum->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                    return SFM_ERR_NOT_FINITE;
+                }
+            }
+            x_norm = std::sqrt(sc[kScXnorm2E] + sc[kScXnorm2F]);
+            pending.cost = x_cost;
+            pending.gradient_max_norm = std::max(sc[kScGmaxE], sc[kScGmaxF]);
+            pending.trust_region_radius = radius;
+            prev_gmax = pending.gradient_max_norm;
+            term = finalize(pending, pending.gradient_max_norm);
+            if (term >= 0) break;
+        }
+
+        // ---- this iteration -----------------------------------------------------
+        sfm_ba_iter cur{};
+        cur.iteration = last_iter + 1;
+        const double model_change = -sc[kScModelAcc];
+        cur.model_cost_change = model_change;
+        const bool finite = sc[kScSolveFail] == 0.0 && sc[kScStepBad] == 0.0 && std::isfinite(model_change);
+        cur.step_is_valid = finite && model_change > 0.0;
+        if (!cur.step_is_valid) {
+            if (++consecutive_invalid >= O.max_num_consecutive_invalid_steps) { term = SFM_TERM_FAILURE; break; }
+            radius = radius / decrease_factor;
+            decrease_factor *= 2.0;
+            cur.cost = x_cost;
+            cur.gradient_max_norm = prev_gmax;
+            cur.trust_region_radius = radius;
+            term = finalize(cur, prev_gmax);
+            continue;
+        }
+        consecutive_invalid = 0;
+        const double cand_cost = sc[kScCandBad] != 0.0 ? std::numeric_limits<double>::max() : sc[kScCandCost];
+        cur.step_norm = std::sqrt(sc[kScStepnorm2E] + sc[kScStepnorm2F]);
+        if (cur.step_norm <= O.parameter_tolerance * (x_norm + O.parameter_tolerance)) { term = SFM_TERM_CONVERGENCE; break; }
+        cur.cost_change = x_cost - cand_cost;
+        if (std::fabs(cur.cost_change) <= O.function_tolerance * x_cost) { term = SFM_TERM_CONVERGENCE; break; }
+        cur.relative_decrease = cand_cost >= std::numeric_limits<double>::max()
+                                    ? std::numeric_limits<double>::lowest()
+                                    : (x_cost - cand_cost) / model_change;
+        if (cur.relative_decrease > O.min_relative_decrease) {
+            std::swap(S.X, S.Xc); std::swap(S.e, S.ec); std::swap(S.in, S.inc); std::swap(S.cp, S.cpc);
+            cur.step_is_successful = 1;
+            const double q = cur.relative_decrease;
+            radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * q - 1.0, 3));
+            radius = std::min(O.max_trust_region_radius, radius);
+            decrease_factor = 2.0;
+            relinearize();
+            relin_pending = true;
+            pending = cur;
+            continue;   // Finalize after the gradient at the new x is known
+        }
+        cur.step_is_successful = 0;
+        cur.cost = cand_cost;
+        cur.gradient_max_norm = prev_gmax;
+        radius = radius / decrease_factor;
+        decrease_factor *= 2.0;
+        cur.trust_region_radius = radius;
+        term = finalize(cur, prev_gmax);
+    }
+    pl->cur_is_a = S.X == pl->Xa.p;
+    // keep the final state where download() finds it
+    if (!pl->cur_is_a) {
+        if (nx) SFM_HIP(hipMemcpyAsync(pl->Xa.p, S.X, nx * 8, hipMemcpyDeviceToDevice, s));
+        SFM_HIP(hipMemcpyAsync(pl->ea.p, S.e, ne * 8, hipMemcpyDeviceToDevice, s));
+        SFM_HIP(hipMemcpyAsync(pl->ia.p, S.in, ni * 8, hipMemcpyDeviceToDevice, s));
+        SFM_HIP(hipStreamSynchronize(s));
+    }
+    sum->termination = term;
+    sum->usable = term != SFM_TERM_FAILURE;
+    sum->iterations = pl->trace.empty() ? 0 : pl->trace.back().iteration;
+    sum->final_cost = sum->initial_cost;
+    for (const auto& it : pl->trace)
+        if (it.step_is_successful) sum->final_cost = std::min(sum->final_cost, it.cost);
+    sum->rmse_initial = sum->num_residuals ? std::sqrt(sum->initial_cost / sum->num_residuals) : 0.0;
+    sum->rmse_final = sum->num_residuals ? std::sqrt(sum->final_cost / sum->num_residuals) : 0.0;
+    sum->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (term == SFM_TERM_FAILURE) set_error("bundle adjustment failed (solution not usable)");
+    return term == SFM_TERM_FAILURE ? SFM_ERR_SOLVER : SFM_OK;
+}
+
+void download(sfm_ba_plan* pl, double* extr, double* intr, double* X) {
+    hipStream_t s = pl->ctx->stream;
+    const BAHostPlan& h = pl->hp;
+    if (extr) SFM_HIP(hipMemcpyAsync(extr, pl->ea.p, 6 * (size_t)h.n_img * 8, hipMemcpyDeviceToHost, s));
+    if (intr) SFM_HIP(hipMemcpyAsync(intr, pl->ia.p, 4 * (size_t)h.n_intr * 8, hipMemcpyDeviceToHost, s));
+    std::vector<double> xs(3 * (size_t)h.n_spt);
+    if (X && h.n_spt) SFM_HIP(hipMemcpyAsync(xs.data(), pl->Xa.p, xs.size() * 8, hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
+    if (X)
+        for (int64_t k = 0; k < h.n_spt; ++k)
+            for (int a = 0; a < 3; ++a) X[3 * h.spt_global[k] + a] = xs[3 * k + a];
+}
+
+}  // namespace
+
+extern "C" void sfm_ba_default_options(sfm_ba_options* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof *o);
+    o->max_num_iterations = 50;
+    o->max_num_consecutive_invalid_steps = 5;
+    o->jacobi_scaling = 1;
+    o->function_tolerance = 1e-6;
+    o->gradient_tolerance = 1e-10;
+    o->parameter_tolerance = 1e-8;
+    o->initial_trust_region_radius = 1e4;
+    o->max_trust_region_radius = 1e16;
+    o->min_trust_region_radius = 1e-32;
+    o->min_relative_decrease = 1e-3;
+    o->min_lm_diagonal = 1e-6;
+    o->max_lm_diagonal = 1e32;
+}
+
+extern "C" int sfm_ba_plan_create(sfm_ctx* ctx, const sfm_ba_problem* prob, const double* extr,
+                                  const double* intr, const double* X, sfm_ba_plan** out) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && prob && extr && intr && (X || prob->n_pt == 0) && out, SFM_ERR_INVALID_ARG,
+                    "null argument");
+        SFM_HIP(hipSetDevice(ctx->device));
+        auto* pl = new sfm_ba_plan;
+        pl->ctx = ctx;
+        try {
+            create_plan(pl, *prob, extr, intr, X);
+        } catch (...) {
+            delete pl;
+            throw;
+        }
+        *out = pl;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ba_plan_run(sfm_ba_plan* pl, const sfm_ba_options* opts, sfm_ba_summary* sum) {
+    return guarded([&] {
+        SFM_REQUIRE(pl && sum, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_HIP(hipSetDevice(pl->ctx->device));
+        sfm_ba_options O;
+        if (opts) O = *opts; else sfm_ba_default_options(&O);
+        return run_plan(pl, O, sum);
+    });
+}
+
+extern "C" int sfm_ba_plan_download(sfm_ba_plan* pl, double* extr, double* intr, double* X) {
+    return guarded([&] {
+        SFM_REQUIRE(pl, SFM_ERR_INVALID_ARG, "null plan");
+        SFM_HIP(hipSetDevice(pl->ctx->device));
+        download(pl, extr, intr, X);
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ba_plan_destroy(sfm_ba_plan* pl) {
+    return guarded([&] {
+        if (!pl) return SFM_OK;
+        (void)hipSetDevice(pl->ctx->device);
+        (void)hipStreamSynchronize(pl->ctx->stream);
+        delete pl;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ba_plan_get_info(sfm_ba_plan* pl, sfm_ba_plan_info* info) {
+    return guarded([&] {
+        SFM_REQUIRE(pl && info, SFM_ERR_INVALID_ARG, "null argument");
+        const BAHostPlan& h = pl->hp;
+        std::memset(info, 0, sizeof *info);
+        info->shard_pt_begin = h.bounds[h.rank];
+        info->shard_pt_end = h.bounds[h.rank + 1];
+        info->shard_obs = h.n_sobs;
+        info->n_chunks = (int32_t)h.chunks.size();
+        info->band_blocks = h.D;
+        info->n_cam_active = h.ncam;
+        info->n_intr_active = h.nintr;
+        info->rcs_dim = h.nF;
+        for (int k = 0; k < 8; ++k) info->last_kernel_ms[k] = pl->last_ms[k];
+        info->schur_flops_per_iter = h.schur_flops;
+        info->schur_launches = pl->schur_launches;
+        info->schur_ms_total = pl->schur_ms_total;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ba_plan_get_trace(sfm_ba_plan* pl, sfm_ba_iter* out, int32_t cap, int32_t* n) {
+    return guarded([&] {
+        SFM_REQUIRE(pl && n, SFM_ERR_INVALID_ARG, "null argument");
+        const int32_t m = (int32_t)std::min<size_t>(pl->trace.size(), cap > 0 ? cap : 0);
+        for (int32_t k = 0; k < m; ++k) out[k] = pl->trace[k];
+        *n = m;
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* extr, double* intr,
+                            double* X, const sfm_ba_options* opts, sfm_ba_summary* sum) {
+    sfm_ba_plan* pl = nullptr;
+    int rc = sfm_ba_plan_create(ctx, prob, extr, intr, X, &pl);
+    if (rc != SFM_OK) return rc;
+    rc = sfm_ba_plan_run(pl, opts, sum);
+    if (sum && sum->usable) {  // BundleAdjuster::updateWorld only on success (:179-184)
+        const int rc2 = sfm_ba_plan_download(pl, extr, intr, X);
+        if (rc == SFM_OK) rc = rc2;
+    }
+    sfm_ba_plan_destroy(pl);
+    return rc;
+}

@@ -135,3 +135,12 @@ def oracle_match_dense(a, b, mode, ratio=0.8):
                              ratio, abi.ptr(idx, abi.i32p), abi.ptr(d2, abi.i32p))
     assert rc == 0
     return idx, d2
+
+
+def oracle_cost(scene, e, i, x):
+    lib = oracle()
+    c = C.c_double()
+    rc = lib.orc_ba_cost(C.byref(scene.problem()), abi.ptr(e, abi.f64p), abi.ptr(i, abi.f64p),
+                         abi.ptr(x, abi.f64p), C.byref(c), None)
+    assert rc == 0
+    return c.value
