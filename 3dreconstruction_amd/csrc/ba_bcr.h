@@ -1,0 +1,26 @@
+// Block cyclic reduction solve of the reduced camera system (ba_bcr.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ba_kernels.h"
+
+namespace sfm {
+
+constexpr int kBcrM = 64;   // super-block size (scalars)
+constexpr int kBcrK = 10;   // camera blocks per super-block (6*K <= 64)
+
+struct BcrArgs {
+    int N = 0;      // super-blocks
+    int K = 0;      // camera blocks per super-block
+    int nrhs = 0;   // 1 + 4*nintr, padded to a multiple of 8
+    double *A = nullptr, *C = nullptr, *L = nullptr, *Wl = nullptr, *Wr = nullptr;
+    double *R = nullptr, *R0 = nullptr, *Z = nullptr, *Y = nullptr, *fail = nullptr;
+};
+
+bool bcr_supported(const DevProblem& P);
+void bcr_setup(BcrArgs& b, const DevProblem& P);
+size_t bcr_doubles(const BcrArgs& b);
+void bcr_bind(BcrArgs& b, double* base);
+void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s);
+
+}  // namespace sfm

@@ -39,6 +39,8 @@ struct DevProblem {
     const ReduceTarget* targets;
     const ReduceTerm* terms;
     int32_t n_targets;
+    int32_t n_long;                 // targets with > reduce_long_threshold() terms
+    const int32_t* long_targets;
     // state
     double* scaleE;     // [3*n_spt]
     double* scaleF;     // [nF]
@@ -86,5 +88,6 @@ void ba_finalize(const DevProblem& P, hipStream_t s);
 size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
 size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);
+int reduce_long_threshold();
 
 }  // namespace sfm

@@ -469,41 +469,75 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
 // ---------------------------------------------------------------------------
 // static gather-reduce: one wave per target block
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ double term_value(const DevProblem& P, const ReduceTerm& q, int r, int cc, bool vec) {
+    if (q.kind == kSrcTile) {
+        const double* tile = P.tiles + (size_t)q.index * kTileR * kTileR;
+        return vec ? tile[q.roff * kTileR + q.coff + r] : tile[(q.roff + r) * kTileR + q.coff + cc];
+    } else if (q.kind == kSrcU) {
+        return P.U[(size_t)q.index * 100 + (q.roff + r) * 10 + q.coff + cc];
+    } else if (q.kind == kSrcUb) {
+        return P.Ub[(size_t)q.index * 10 + q.roff + r];
+    }
+    return P.Ucn[(size_t)q.index * 10 + q.roff + r];
+}
+
+__device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {
+    switch (kind) {
+        case 0: return P.Sband;
+        case 1: return P.Sarrow;
+        case 2: return P.Scorner;
+        case 3: return P.rhs;
+        case 4: return P.bF;
+        default: return P.cnF;
+    }
+}
+
+constexpr int kLongTerms = 48;   // longer term lists are summed by a whole workgroup
+
 __global__ void reduce_kernel(DevProblem P, int min_kind) {
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int e = threadIdx.x & 63;
     if (t >= P.n_targets) return;
     const ReduceTarget T = P.targets[t];
-    if (T.dst_kind < min_kind) return;
+    if (T.dst_kind < min_kind || T.c_end - T.c_begin > kLongTerms) return;
     if (e >= T.rows * T.cols) return;
     const int r = e / T.cols, cc = e % T.cols;
     const bool vec = T.cols == 1;
     double s = 0.0;
     for (int k = T.c_begin; k < T.c_end; ++k) {
         const ReduceTerm q = P.terms[k];
-        double v;
-        if (q.kind == kSrcTile) {
-            const double* tile = P.tiles + (size_t)q.index * kTileR * kTileR;
-            v = vec ? tile[q.roff * kTileR + q.coff + r] : tile[(q.roff + r) * kTileR + q.coff + cc];
-        } else if (q.kind == kSrcU) {
-            v = P.U[(size_t)q.index * 100 + (q.roff + r) * 10 + q.coff + cc];
-        } else if (q.kind == kSrcUb) {
-            v = P.Ub[(size_t)q.index * 10 + q.roff + r];
-        } else {
-            v = P.Ucn[(size_t)q.index * 10 + q.roff + r];
-        }
-        s += (double)q.sign * v;
+        s += (double)q.sign * term_value(P, q, r, cc, vec);
     }
     double* dst;
-    switch (T.dst_kind) {
-        case 0: dst = P.Sband; break;
-        case 1: dst = P.Sarrow; break;
-        case 2: dst = P.Scorner; break;
-        case 3: dst = P.rhs; break;
-        case 4: dst = P.bF; break;
-        default: dst = P.cnF; break;
-    }
+    dst = target_base(P, T.dst_kind);
     dst[T.dst + (vec ? r : r * T.ld + cc)] = s;
+}
+
+// one workgroup per long target: thread (g, e) sums terms g, g+G, ... of
+// element e; the G partial sums are combined in fixed order (deterministic)
+__global__ __launch_bounds__(256) void reduce_long_kernel(DevProblem P, const int32_t* __restrict__ list,
+                                                          int n, int min_kind) {
+    if ((int)blockIdx.x >= n) return;
+    const ReduceTarget T = P.targets[list[blockIdx.x]];
+    if (T.dst_kind < min_kind) return;
+    const int E = T.rows * T.cols, G = 256 / E;
+    const int g = threadIdx.x / E, e = threadIdx.x % E;
+    const int r = e / T.cols, cc = e % T.cols;
+    const bool vec = T.cols == 1;
+    __shared__ double part[256];
+    double s = 0.0;
+    if (g < G)
+        for (int k = T.c_begin + g; k < T.c_end; k += G) {
+            const ReduceTerm q = P.terms[k];
+            s += (double)q.sign * term_value(P, q, r, cc, vec);
+        }
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < E) {
+        double t = 0.0;
+        for (int q = 0; q < G; ++q) t += part[q * E + threadIdx.x];
+        target_base(P, T.dst_kind)[T.dst + (vec ? r : r * T.ld + cc)] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -958,7 +992,14 @@ void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     if (P.n_targets <= 0) return;
     hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P, vectors_only ? 4 : 0);
     SFM_HIP(hipGetLastError());
+    if (P.n_long > 0) {
+        hipLaunchKernelGGL(reduce_long_kernel, dim3(P.n_long), dim3(256), 0, s, P, P.long_targets, P.n_long,
+                           vectors_only ? 4 : 0);
+        SFM_HIP(hipGetLastError());
+    }
 }
+
+int reduce_long_threshold() { return kLongTerms; }
 
 size_t solve_window_doubles(const DevProblem& P) {
     const size_t Dp = P.D + 1;

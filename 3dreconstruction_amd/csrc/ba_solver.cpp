@@ -18,10 +18,12 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
 
+#include "ba_bcr.h"
 #include "ba_kernels.h"
 #include "ba_plan.h"
 #include "common.h"
@@ -41,7 +43,10 @@ struct sfm_ba_plan {
     DBuf<double> X0, Xa, Xb, extr0, intr0, ea, eb, ia, ib;
     DBuf<CamPre> cpa, cpb;
     DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
-        part_t, scal;
+        part_t, scal, bcr_buf;
+    DBuf<int32_t> long_targets;
+    BcrArgs bcr;
+    bool use_bcr = false;
     int64_t rcs_n = 0;
     double* scal_h = nullptr;  // pinned
     std::vector<sfm_ba_iter> trace;
@@ -131,6 +136,14 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.sub_starts = pl->sub_starts.p; P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
+    {
+        std::vector<int32_t> lt;
+        for (size_t t = 0; t < h.targets.size(); ++t)
+            if (h.targets[t].c_end - h.targets[t].c_begin > reduce_long_threshold()) lt.push_back((int32_t)t);
+        up(pl->long_targets, lt, s);
+        P.n_long = (int32_t)lt.size();
+        P.long_targets = pl->long_targets.p;
+    }
     P.scaleE = pl->scaleE.p; P.scaleF = pl->scaleF.p; P.tiles = pl->tiles.p;
     P.U = pl->U.p; P.Ub = pl->Ub.p; P.Ucn = pl->Ucn.p;
     P.Sband = pl->rcs.p;
@@ -148,6 +161,12 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->part_t.alloc((size_t)kPartT * std::max(ba_step_blocks(P), 1));
     P.part_t = pl->part_t.p;
     P.scal = pl->scal.p;
+    pl->use_bcr = bcr_supported(P) && std::getenv("SFM_BA_BAND_SOLVER") == nullptr;
+    if (pl->use_bcr) {
+        bcr_setup(pl->bcr, P);
+        pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
+        bcr_bind(pl->bcr, pl->bcr_buf.p);
+    }
     pl->ev.resize(16);
     for (auto& e2 : pl->ev) SFM_HIP(hipEventCreate(&e2));
     SFM_HIP(hipStreamSynchronize(s));
@@ -231,7 +250,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
         ba_reduce(P, false, s);
         allreduce_rcs();
-        ba_solve(P, radius, s);
+        if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s);
+        else ba_solve(P, radius, s);
         SFM_HIP(hipMemcpyAsync(S.ec, S.e, ne * 8, hipMemcpyDeviceToDevice, s));
         SFM_HIP(hipMemcpyAsync(S.inc, S.in, ni * 8, hipMemcpyDeviceToDevice, s));
         ba_fvec(P, S.e, S.in, S.ec, S.inc, pl->blk_img.p, pl->blk_intr.p, s);

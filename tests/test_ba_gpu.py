@@ -149,3 +149,20 @@ def test_c2_banded_scale(ctx):
     sc = H.Scene(200, 50000, 10, seed=0x5F3D0002)
     gs, os_ = _compare(ctx, sc)
     assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
+
+
+def test_bcr_matches_sequential_band_solver(ctx, monkeypatch):
+    sc = H.Scene(95, 8000, 8, n_intr=2, seed=31)     # D = 7 -> BCR over 10 super-blocks
+    res = []
+    for band in (False, True):
+        if band:
+            monkeypatch.setenv("SFM_BA_BAND_SOLVER", "1")
+        plan = api.BAPlan(ctx, sc.problem(), *sc.params())
+        _, s = plan.run()
+        res.append((s, plan.trace()))
+        plan.close()
+    (s0, t0), (s1, t1) = res
+    assert s0.iterations == s1.iterations
+    assert abs(s0.final_cost / s1.final_cost - 1) < 1e-9
+    for a, b in zip(t0, t1):
+        assert a.step_is_successful == b.step_is_successful
