@@ -74,8 +74,9 @@ void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, co
 void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                     hipStream_t s);
 void ba_fscale(const DevProblem& P, hipStream_t s);
+// stamps (diagnostic builds only, else nullptr): per chunk 6 phase cycle sums
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
-              double radius, hipStream_t s);
+              double radius, hipStream_t s, unsigned long long* stamps = nullptr);
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s);
 void ba_solve(const DevProblem& P, double radius, hipStream_t s);
 // candidate cameras/intrinsics, F-part norms and gradient

@@ -286,10 +286,24 @@ __global__ void fscale_kernel(DevProblem P) {
 // ---------------------------------------------------------------------------
 constexpr int kPanelK = 3 * kSubPts;  // 48 panel columns (3 per point)
 
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
 __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                         const double* __restrict__ intr,
                                                         const double* __restrict__ X,
-                                                        double radius) {
+                                                        double radius, unsigned long long* __restrict__ stamps) {
+    unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
+    if (stamps) tprev = stamp();
+#define SFM_STAMP(k)                                      \
+    if (stamps) {                                         \
+        const unsigned long long tn_ = stamp();           \
+        tacc[k] += tn_ - tprev;                           \
+        tprev = tn_;                                      \
+    }
     __shared__ double panel[kPanelK][kTileR];   // [k][row]
     __shared__ double obsbuf[kSubObs][8];       // Jx (6) | f (2)
     __shared__ double ptbuf[kSubPts][12];       // Linv (6) | w (3)
@@ -311,6 +325,7 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
         const int p1 = (sb + 1 < cd.sub_end) ? P.sub_starts[sb + 1] : cd.pt_end;
         const int o0 = P.pt_off[p0], nobs = P.pt_off[p1] - o0, npts = p1 - p0;
         for (int e = tid; e < kPanelK * kTileR; e += 256) (&panel[0][0])[e] = 0.0;
+        SFM_STAMP(0)
         // ---- phase A: observations -> scaled, corrected Jacobians ----------
         Lin L;
         int cs = -1, is = -1, pl = 0;
@@ -342,6 +357,7 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
             obsbuf[tid][7] = L.f[1];
         }
         __syncthreads();
+        SFM_STAMP(1)
         // ---- phase B: per point V + D^2, Cholesky, w = L^-1 g_E -------------
         if (tid < npts) {
             const int p = p0 + tid;
@@ -384,6 +400,7 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
             panel[3 * tid + 2][kTileWRow] = w2;
         }
         __syncthreads();
+        SFM_STAMP(2)
         // ---- phase C: Z = W L^-T into the panel -------------------------------
         if (tid < nobs) {
             const double i00 = ptbuf[pl][0], i10 = ptbuf[pl][1], i11 = ptbuf[pl][2];
@@ -421,6 +438,7 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
             }
         }
         __syncthreads();
+        SFM_STAMP(3)
         // ---- phase D: tile += panel panel' on the fp64 MFMA ------------------
         const int kk = lane >> 4, ii = lane & 15;
 #pragma unroll
@@ -436,6 +454,7 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
             }
         }
         __syncthreads();
+        SFM_STAMP(4)
     }
     // ---- write the negated tile (full symmetric 80x80) -----------------------
     double* out = P.tiles + (size_t)c * kTileR * kTileR;
@@ -464,6 +483,10 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
         P.part_s[2 * (size_t)c] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
         P.part_s[2 * (size_t)c + 1] = fmax(fmax(red[0][1], red[1][1]), fmax(red[2][1], red[3][1]));
     }
+    SFM_STAMP(5)
+    if (stamps && tid == 0)
+        for (int k = 0; k < 6; ++k) stamps[6 * (size_t)c + k] = tacc[k];
+#undef SFM_STAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -982,9 +1005,9 @@ void ba_fscale(const DevProblem& P, hipStream_t s) {
 }
 
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
-              hipStream_t s) {
+              hipStream_t s, unsigned long long* stamps) {
     if (P.n_chunk <= 0) return;
-    hipLaunchKernelGGL(schur_kernel, dim3(P.n_chunk), dim3(256), 0, s, P, cp, intr, X, radius);
+    hipLaunchKernelGGL(schur_kernel, dim3(P.n_chunk), dim3(256), 0, s, P, cp, intr, X, radius, stamps);
     SFM_HIP(hipGetLastError());
 }
 

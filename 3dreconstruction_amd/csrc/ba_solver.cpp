@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -45,6 +46,7 @@ struct sfm_ba_plan {
     DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
         part_t, scal, bcr_buf;
     DBuf<int32_t> long_targets;
+    DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
     BcrArgs bcr;
     bool use_bcr = false;
     int64_t rcs_n = 0;
@@ -167,6 +169,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
         bcr_bind(pl->bcr, pl->bcr_buf.p);
     }
+    if (std::getenv("SFM_SCHUR_STAMPS")) pl->stamps.alloc(6 * std::max<size_t>(h.chunks.size(), 1));
     pl->ev.resize(16);
     for (auto& e2 : pl->ev) SFM_HIP(hipEventCreate(&e2));
     SFM_HIP(hipStreamSynchronize(s));
@@ -246,7 +249,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         // ---- one step on the device ------------------------------------------
         const bool timed = ev_i + 1 < (int)pl->ev.size();
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i], s));
-        ba_schur(P, S.cp, S.in, S.X, radius, s);
+        ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p);
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
         ba_reduce(P, false, s);
         allreduce_rcs();
@@ -341,6 +344,15 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         decrease_factor *= 2.0;
         cur.trust_region_radius = radius;
         term = finalize(cur, prev_gmax);
+    }
+    if (pl->stamps.p) {  // diagnostic: average phase cycles per chunk (last Schur launch)
+        std::vector<unsigned long long> st(pl->stamps.n);
+        SFM_HIP(hipMemcpy(st.data(), pl->stamps.p, st.size() * 8, hipMemcpyDeviceToHost));
+        double avg[6] = {0};
+        for (size_t c = 0; c < h.chunks.size(); ++c)
+            for (int k = 0; k < 6; ++k) avg[k] += (double)st[6 * c + k] / h.chunks.size();
+        std::fprintf(stderr, "[schur stamps] cycles/chunk zero %.0f A %.0f B %.0f C %.0f D %.0f tail %.0f\n",
+                     avg[0], avg[1], avg[2], avg[3], avg[4], avg[5]);
     }
     pl->cur_is_a = S.X == pl->Xa.p;
     // keep the final state where download() finds it

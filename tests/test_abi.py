@@ -81,3 +81,8 @@ def test_partition_balances_observations(world):
     counts = np.diff(sc.pt_offsets)[order]
     per = [counts[bounds[r]:bounds[r + 1]].sum() for r in range(world)]
     assert max(per) - min(per) <= counts.max() + 1
+
+
+def test_cpp_facade_builds():
+    exe = os.path.join(ROOT, "tests", "cpp", "facade_test")
+    assert os.path.exists(exe), "run make (builds the C++ façade test)"

@@ -166,3 +166,15 @@ def test_bcr_matches_sequential_band_solver(ctx, monkeypatch):
     assert abs(s0.final_cost / s1.final_cost - 1) < 1e-9
     for a, b in zip(t0, t1):
         assert a.step_is_successful == b.step_is_successful
+
+
+def test_cpp_facade_drop_in():
+    """The C++ façade (include/sfm/sfm.hpp) driven like SequentialActuator /
+    sparseBuilder, checked against the oracle inside the binary."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "cpp",
+                       "facade_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "facade ok" in r.stdout
