@@ -11,6 +11,11 @@
 //
 // Mathematically the same direct solution ceres' SPARSE_SCHUR + EIGEN_SPARSE
 // computes for the reduced camera system (BundleAdjuster.h:171-173).
+//
+// Dense 64x64 work is blocked in 16x16 tiles: each diagonal tile is factored
+// and inverted inside one wavefront (no block barriers), everything else is
+// fp64 MFMA (v_mfma_f64_16x16x4_f64) tile products.  A factored super-block
+// keeps X = L^-1 explicitly, so every triangular solve is a product.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -28,67 +33,144 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
 
-// ---- dense helpers on LDS tiles, 256 threads --------------------------------
-// in-place lower Cholesky of a 64x64 tile; returns false on a non-positive pivot
-// `bad` lives in the dynamic LDS region (a static __shared__ would misalign it)
-__device__ bool chol64(double* A, double* bad) {
-    if (threadIdx.x == 0) bad[0] = 0.0;
-    __syncthreads();
-    for (int k = 0; k < M; ++k) {
-        if (threadIdx.x == 0) {
-            const double d = A[k * LD + k];
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 1/sqrt(d): hardware estimate + two Newton steps (full fp64 accuracy)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double hy = 0.5 * d * y;
+        y = fma(y, fma(-hy, y, 0.5), y);
+    }
+    return y;
+}
+
+// One wave, one 16x16 output tile: acc += op(A)[ar.., k] op(B)[k, bc..] for
+// k in [k0, k1) (multiple of 4).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
+// op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.
+template <bool TA, bool TB, bool NEG>
+__device__ __forceinline__ v4d tile_mm(v4d acc, const double* A, int lda, int ar, const double* B, int ldb,
+                                       int bc, int k0, int k1) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    for (int k = k0; k < k1; k += 4) {
+        const double a = TA ? A[(k + kk) * lda + ar + i] : A[(ar + i) * lda + k + kk];
+        const double b = TB ? B[(bc + i) * ldb + k + kk] : B[(k + kk) * ldb + bc + i];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a : a, b, acc, 0, 0, 0);
+    }
+    return acc;
+}
+__device__ __forceinline__ v4d tile_ld(const double* C, int ldc, int r0, int c0) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    v4d v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = C[(r0 + kk + 4 * r) * ldc + c0 + i];
+    return v;
+}
+__device__ __forceinline__ void tile_st(double* C, int ldc, int r0, int c0, v4d v) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[(r0 + kk + 4 * r) * ldc + c0 + i] = v[r];
+}
+__device__ __forceinline__ v4d zero4() { return v4d{0.0, 0.0, 0.0, 0.0}; }
+
+// global [64][ld_src] -> LDS [64][ld_dst], first nc columns
+__device__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src, int nc) {
+    for (int e = threadIdx.x; e < M * nc; e += NT) dst[(e / nc) * ld_dst + e % nc] = src[(e / nc) * ld_src + e % nc];
+}
+
+// Wave-local factor + inverse of one 16x16 diagonal tile (lanes 0..15 own a
+// row, then a column).  L overwrites the lower tile (upper zeroed); X gets
+// L^-1 (upper zeroed).  sc: LDS scratch [33].
+__device__ void diag16(double* A, double* X, double* sc, double* bad) {
+    const int lane = threadIdx.x & 63, i = lane;
+    const bool act = lane < 16;
+    double a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? A[i * LD + j] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (i == k) sc[0] = a[k];
+        wave_sync();
+        const double d = sc[0];
+        const double rinv = rsqrt_nr(d);
+        if (lane == 0) {
             if (!(d > 0.0)) bad[0] = 1.0;
-            A[k * LD + k] = sqrt(d);
+            sc[17 + k] = rinv;
+        }
+        if (i == k) a[k] = d * rinv;
+        else if (i > k) a[k] *= rinv;
+        if (act) sc[1 + i] = a[k];
+        wave_sync();
+#pragma unroll
+        for (int j = k + 1; j < 16; ++j) a[j] = fma(-a[k], sc[1 + j], a[j]);
+        wave_sync();
+    }
+    if (act) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
+    }
+    wave_sync();
+    // X = L^-1 by columns: lane c solves L x = e_c (rows of L are LDS broadcasts)
+    const int c = lane;
+    double x[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        double t = (m == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int p = 0; p < m; ++p) t = fma(-A[m * LD + p], x[p], t);
+        x[m] = t * sc[17 + m];
+    }
+    if (act) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) X[m * LD + c] = x[m];
+    }
+    wave_sync();
+}
+
+// Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
+// the caller).  All 256 threads; ends synchronised.
+__device__ void chol_inv64(double* A, double* X, double* sc, double* bad) {
+    const int wave = threadIdx.x >> 6;
+    for (int k = 0; k < 4; ++k) {
+        if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), sc, bad);
+        __syncthreads();
+        if (wave < 3 - k) {   // panel: L_ik = A_ik X_kk'
+            const int i = k + 1 + wave;
+            const v4d t = tile_mm<false, true, false>(zero4(), A, LD, 16 * i, X, LD, 16 * k, 16 * k, 16 * k + 16);
+            tile_st(A, LD, 16 * i, 16 * k, t);
         }
         __syncthreads();
-        const double inv = 1.0 / A[k * LD + k];
-        for (int i = k + 1 + threadIdx.x; i < M; i += NT) A[i * LD + k] *= inv;
+        int t = 0;            // trailing: A_ij -= L_ik L_jk', k < j <= i
+        for (int i = k + 1; i < 4; ++i)
+            for (int j = k + 1; j <= i; ++j, ++t)
+                if ((t & 3) == wave) {
+                    v4d acc = tile_ld(A, LD, 16 * i, 16 * j);
+                    acc = tile_mm<false, true, true>(acc, A, LD, 16 * i, A, LD, 16 * j, 16 * k, 16 * k + 16);
+                    tile_st(A, LD, 16 * i, 16 * j, acc);
+                }
         __syncthreads();
-        // trailing lower update: A[i][j] -= A[i][k] A[j][k], k < j <= i
-        const int n = M - 1 - k;
-        for (int e = threadIdx.x; e < n * n; e += NT) {
-            const int i = k + 1 + e / n, j = k + 1 + e % n;
-            if (j <= i) A[i * LD + j] -= A[i * LD + k] * A[j * LD + k];
+    }
+    // X_ij = -X_ii sum_{m=j}^{i-1} L_im X_mj, by distance from the diagonal
+    for (int dd = 1; dd < 4; ++dd) {
+        if (wave < 4 - dd) {
+            const int i = dd + wave, j = i - dd;
+            v4d acc = zero4();
+            for (int m = j; m < i; ++m)
+                acc = tile_mm<false, false, false>(acc, A, LD, 16 * i, X, LD, 16 * j, 16 * m, 16 * m + 16);
+            tile_st(X, LD, 16 * i, 16 * j, acc);
+            wave_sync();
+            acc = tile_mm<false, false, true>(zero4(), X, LD, 16 * i, X, LD, 16 * j, 16 * i, 16 * i + 16);
+            tile_st(X, LD, 16 * i, 16 * j, acc);
         }
         __syncthreads();
     }
-    return bad[0] == 0.0;
-}
-
-// B <- L^-1 B for B [64][nc] with row stride ldb (lower L from chol64)
-__device__ void trsm64(const double* L, double* B, int nc, int ldb) {
-    for (int k = 0; k < M; ++k) {
-        const double inv = 1.0 / L[k * LD + k];
-        for (int c = threadIdx.x; c < nc; c += NT) B[k * ldb + c] *= inv;
-        __syncthreads();
-        const int n = M - 1 - k;
-        for (int e = threadIdx.x; e < n * nc; e += NT) {
-            const int i = k + 1 + e / nc, c = e % nc;
-            B[i * ldb + c] -= L[i * LD + k] * B[k * ldb + c];
-        }
-        __syncthreads();
-    }
-}
-
-// B <- L^-T B
-__device__ void trsm64_t(const double* L, double* B, int nc, int ldb) {
-    for (int k = M - 1; k >= 0; --k) {
-        const double inv = 1.0 / L[k * LD + k];
-        for (int c = threadIdx.x; c < nc; c += NT) B[k * ldb + c] *= inv;
-        __syncthreads();
-        for (int e = threadIdx.x; e < k * nc; e += NT) {
-            const int i = e / nc, c = e % nc;
-            B[i * ldb + c] -= L[k * LD + i] * B[k * ldb + c];
-        }
-        __syncthreads();
-    }
-}
-
-__device__ void load64(double* dst, const double* src) {  // global [64][64] -> LDS [64][LD]
-    for (int e = threadIdx.x; e < M * M; e += NT) dst[(e / M) * LD + e % M] = src[e];
-}
-__device__ void store64(double* dst, const double* src) {
-    for (int e = threadIdx.x; e < M * M; e += NT) dst[e] = src[(e / M) * LD + e % M];
 }
 
 // ---- pack: band (6x6 blocks) -> 64x64 super-blocks, D^2 added, identity pad --
@@ -146,41 +228,45 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
     }
 }
 
-// ---- level l: factor every odd super-block, W = L^-1 C, z = L^-1 R -----------
+// ---- level l: factor every odd super-block; X = L^-1, W = X C, z = X R -------
 __global__ __launch_bounds__(NT) void bcr_factor_kernel(BcrArgs b, int s) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* A = sm;                 // [64][LD]
-    double* B = A + M * LD;         // [64][LD]
-    double* R = B + M * LD;         // [64][nrhs+1]
+    double* X = A + M * LD;         // [64][LD]
+    double* Cl = X + M * LD;        // [64][LD]  C_i  = block (i, i-s)
+    double* Cr = Cl + M * LD;       // [64][LD]  C_r  = block (r, i)
+    double* R = Cr + M * LD;        // [64][nrhs+1]
     const int ldr = b.nrhs + 1;
-    double* flag = R + M * ldr;     // [2]
+    double* sc = R + M * ldr;       // [33]
+    double* bad = sc + 33;
     const int i = s + 2 * s * blockIdx.x;   // odd at this level
     if (i >= b.N) return;
-    const int r = i + s;
-    load64(A, b.A + (size_t)i * M * M);
+    const int r = i + s, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) bad[0] = 0.0;
+    load_rows(A, LD, b.A + (size_t)i * M * M, M, M);
+    load_rows(Cl, LD, b.C + (size_t)i * M * M, M, M);
+    if (r < b.N) load_rows(Cr, LD, b.C + (size_t)r * M * M, M, M);
+    load_rows(R, ldr, b.R + (size_t)i * M * b.nrhs, b.nrhs, b.nrhs);
+    for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
-    if (!chol64(A, flag) && threadIdx.x == 0) b.fail[0] = 1.0;
-    store64(b.L + (size_t)i * M * M, A);
-    // W_l = L^-1 C_i   (C_i = block (i, i-s))
-    load64(B, b.C + (size_t)i * M * M);
-    __syncthreads();
-    trsm64(A, B, M, LD);
-    store64(b.Wl + (size_t)i * M * M, B);
-    __syncthreads();
-    if (r < b.N) {  // W_r = L^-1 C_r'   (C_r = block (r, i))
-        const double* Cr = b.C + (size_t)r * M * M;
-        for (int e = threadIdx.x; e < M * M; e += NT) B[(e % M) * LD + e / M] = Cr[e];
-        __syncthreads();
-        trsm64(A, B, M, LD);
-        store64(b.Wr + (size_t)i * M * M, B);
-        __syncthreads();
+    chol_inv64(A, X, sc, bad);
+    if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
+    double* Xg = b.L + (size_t)i * M * M;
+    for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
+    const int kend = 16 * (wave + 1);   // X is lower triangular
+    double* Wl = b.Wl + (size_t)i * M * M;
+    double* Wr = b.Wr + (size_t)i * M * M;
+    for (int tj = 0; tj < 4; ++tj) {
+        tile_st(Wl, M, 16 * wave, 16 * tj,
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Cl, LD, 16 * tj, 0, kend));
+        if (r < b.N)
+            tile_st(Wr, M, 16 * wave, 16 * tj,
+                    tile_mm<false, true, false>(zero4(), X, LD, 16 * wave, Cr, LD, 16 * tj, 0, kend));
     }
-    const double* Rg = b.R + (size_t)i * M * b.nrhs;
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) R[(e / b.nrhs) * ldr + e % b.nrhs] = Rg[e];
-    __syncthreads();
-    trsm64(A, R, b.nrhs, ldr);
     double* Z = b.Z + (size_t)i * M * b.nrhs;
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) Z[e] = R[(e / b.nrhs) * ldr + e % b.nrhs];
+    for (int tj = 0; tj < b.nrhs / 16; ++tj)
+        tile_st(Z, b.nrhs, 16 * wave, 16 * tj,
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, kend));
 }
 
 // ---- level l: update every even super-block from its odd neighbours ---------
@@ -188,163 +274,153 @@ __global__ __launch_bounds__(NT) void bcr_factor_kernel(BcrArgs b, int s) {
 // new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}
 __global__ __launch_bounds__(NT) void bcr_update_kernel(BcrArgs b, int s) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* X = sm;            // [64][LD]
-    double* Y = X + M * LD;    // [64][LD]
+    const int ldr = b.nrhs + 1;
+    double* Wa = sm;               // Wr_{j-s}
+    double* Wb = Wa + M * LD;      // Wl_{j+s}
+    double* Wc = Wb + M * LD;      // Wl_{j-s}
+    double* Za = Wc + M * LD;      // z_{j-s}
+    double* Zb = Za + M * ldr;     // z_{j+s}
     const int j = 2 * s * blockIdx.x;
     if (j >= b.N) return;
-    const int il = j - s, ir = j + s;   // odd neighbours
+    const int il = j - s, ir = j + s, wave = threadIdx.x >> 6;
+    const bool hl = il >= 0, hr = ir < b.N, hc = hl && j - 2 * s >= 0;
+    if (hl) {
+        load_rows(Wa, LD, b.Wr + (size_t)il * M * M, M, M);
+        load_rows(Za, ldr, b.Z + (size_t)il * M * b.nrhs, b.nrhs, b.nrhs);
+    }
+    if (hr) {
+        load_rows(Wb, LD, b.Wl + (size_t)ir * M * M, M, M);
+        load_rows(Zb, ldr, b.Z + (size_t)ir * M * b.nrhs, b.nrhs, b.nrhs);
+    }
+    if (hc) load_rows(Wc, LD, b.Wl + (size_t)il * M * M, M, M);
+    __syncthreads();
     double* Aj = b.A + (size_t)j * M * M;
+    for (int tj = 0; tj < 4; ++tj) {
+        v4d acc = tile_ld(Aj, M, 16 * wave, 16 * tj);
+        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * wave, Wa, LD, 16 * tj, 0, M);
+        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * wave, Wb, LD, 16 * tj, 0, M);
+        tile_st(Aj, M, 16 * wave, 16 * tj, acc);
+    }
     double* Rj = b.R + (size_t)j * M * b.nrhs;
-    const int tr = threadIdx.x / 16, tc = threadIdx.x % 16;   // 4x4 output blocks
-    double acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[a][c] = 0.0;
-    auto gemm_tn = [&](const double* P1, const double* P2) {  // acc += P1' P2 (LDS)
-        for (int k = 0; k < M; ++k) {
-            double x[4], y[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) { x[a] = P1[k * LD + 4 * tr + a]; y[a] = P2[k * LD + 4 * tc + a]; }
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[a][c] += x[a] * y[c];
-        }
-    };
-    if (il >= 0) {
-        load64(X, b.Wr + (size_t)il * M * M);
-        __syncthreads();
-        gemm_tn(X, X);
-        __syncthreads();
+    for (int tj = 0; tj < b.nrhs / 16; ++tj) {
+        v4d acc = tile_ld(Rj, b.nrhs, 16 * wave, 16 * tj);
+        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * wave, Za, ldr, 16 * tj, 0, M);
+        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * wave, Zb, ldr, 16 * tj, 0, M);
+        tile_st(Rj, b.nrhs, 16 * wave, 16 * tj, acc);
     }
-    if (ir < b.N) {
-        load64(Y, b.Wl + (size_t)ir * M * M);
-        __syncthreads();
-        gemm_tn(Y, Y);
-        __syncthreads();
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) Aj[(4 * tr + a) * M + 4 * tc + c] -= acc[a][c];
-    // rhs
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) {
-        const int row = e / b.nrhs, c = e % b.nrhs;
-        double v = 0.0;
-        if (il >= 0) {
-            const double* W = b.Wr + (size_t)il * M * M;
-            const double* Z = b.Z + (size_t)il * M * b.nrhs;
-            for (int k = 0; k < M; ++k) v += W[k * M + row] * Z[k * b.nrhs + c];
-        }
-        if (ir < b.N) {
-            const double* W = b.Wl + (size_t)ir * M * M;
-            const double* Z = b.Z + (size_t)ir * M * b.nrhs;
-            for (int k = 0; k < M; ++k) v += W[k * M + row] * Z[k * b.nrhs + c];
-        }
-        Rj[e] -= v;
-    }
-    // new coupling to j - 2s
-    if (il >= 0 && j - 2 * s >= 0) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[a][c] = 0.0;
-        load64(X, b.Wr + (size_t)il * M * M);
-        load64(Y, b.Wl + (size_t)il * M * M);
-        __syncthreads();
-        gemm_tn(X, Y);
+    if (hc) {
         double* Cj = b.C + (size_t)j * M * M;
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) Cj[(4 * tr + a) * M + 4 * tc + c] = -acc[a][c];
+        for (int tj = 0; tj < 4; ++tj)
+            tile_st(Cj, M, 16 * wave, 16 * tj,
+                    tile_mm<true, false, true>(zero4(), Wa, LD, 16 * wave, Wc, LD, 16 * tj, 0, M));
     }
 }
 
-// ---- top: super-block 0 alone; y_0 = A_0^-1 R_0 -------------------------------
+// ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------
 __global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* A = sm;
-    double* R = A + M * LD;
     const int ldr = b.nrhs + 1;
-    double* flag = R + M * ldr;
-    load64(A, b.A);
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) R[(e / b.nrhs) * ldr + e % b.nrhs] = b.R[e];
+    double* A = sm;
+    double* X = A + M * LD;
+    double* R = X + M * LD;
+    double* T = R + M * ldr;
+    double* sc = T + M * ldr;
+    double* bad = sc + 33;
+    const int wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) bad[0] = 0.0;
+    load_rows(A, LD, b.A, M, M);
+    load_rows(R, ldr, b.R, b.nrhs, b.nrhs);
+    for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
-    if (!chol64(A, flag) && threadIdx.x == 0) b.fail[0] = 1.0;
-    trsm64(A, R, b.nrhs, ldr);
-    trsm64_t(A, R, b.nrhs, ldr);
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) b.Y[e] = R[(e / b.nrhs) * ldr + e % b.nrhs];
+    chol_inv64(A, X, sc, bad);
+    if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
+    for (int tj = 0; tj < b.nrhs / 16; ++tj)
+        tile_st(T, ldr, 16 * wave, 16 * tj,
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
+    __syncthreads();
+    for (int tj = 0; tj < b.nrhs / 16; ++tj)   // X' is upper triangular
+        tile_st(b.Y, b.nrhs, 16 * wave, 16 * tj,
+                tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
 }
 
-// ---- back substitution at level l: y_i = L_i^-T (z_i - Wl y_l - Wr y_r) -------
+// ---- back substitution at level l: y_i = X_i' (z_i - Wl y_l - Wr y_r) ----------
 __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, int s) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* A = sm;
-    double* R = A + M * LD;
     const int ldr = b.nrhs + 1;
+    double* X = sm;
+    double* Wl = X + M * LD;
+    double* Wr = Wl + M * LD;
+    double* Yl = Wr + M * LD;
+    double* Yr = Yl + M * ldr;
+    double* T = Yr + M * ldr;
     const int i = s + 2 * s * blockIdx.x;
     if (i >= b.N) return;
-    const int l = i - s, r = i + s;
-    load64(A, b.L + (size_t)i * M * M);
-    const double* Z = b.Z + (size_t)i * M * b.nrhs;
-    const double* Wl = b.Wl + (size_t)i * M * M;
-    const double* Wr = b.Wr + (size_t)i * M * M;
-    const double* Yl = b.Y + (size_t)l * M * b.nrhs;
-    const double* Yr = b.Y + (size_t)r * M * b.nrhs;
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) {
-        const int row = e / b.nrhs, c = e % b.nrhs;
-        double v = Z[e];
-        for (int k = 0; k < M; ++k) v -= Wl[row * M + k] * Yl[k * b.nrhs + c];
-        if (r < b.N)
-            for (int k = 0; k < M; ++k) v -= Wr[row * M + k] * Yr[k * b.nrhs + c];
-        R[row * ldr + c] = v;
+    const int l = i - s, r = i + s, wave = threadIdx.x >> 6;
+    const bool hr = r < b.N;
+    load_rows(X, LD, b.L + (size_t)i * M * M, M, M);
+    load_rows(Wl, LD, b.Wl + (size_t)i * M * M, M, M);
+    load_rows(Yl, ldr, b.Y + (size_t)l * M * b.nrhs, b.nrhs, b.nrhs);
+    if (hr) {
+        load_rows(Wr, LD, b.Wr + (size_t)i * M * M, M, M);
+        load_rows(Yr, ldr, b.Y + (size_t)r * M * b.nrhs, b.nrhs, b.nrhs);
     }
     __syncthreads();
-    trsm64_t(A, R, b.nrhs, ldr);
+    const double* Z = b.Z + (size_t)i * M * b.nrhs;
+    for (int tj = 0; tj < b.nrhs / 16; ++tj) {
+        v4d acc = tile_ld(Z, b.nrhs, 16 * wave, 16 * tj);
+        acc = tile_mm<false, false, true>(acc, Wl, LD, 16 * wave, Yl, ldr, 16 * tj, 0, M);
+        if (hr) acc = tile_mm<false, false, true>(acc, Wr, LD, 16 * wave, Yr, ldr, 16 * tj, 0, M);
+        tile_st(T, ldr, 16 * wave, 16 * tj, acc);
+    }
+    __syncthreads();
     double* Y = b.Y + (size_t)i * M * b.nrhs;
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) Y[e] = R[(e / b.nrhs) * ldr + e % b.nrhs];
+    for (int tj = 0; tj < b.nrhs / 16; ++tj)
+        tile_st(Y, b.nrhs, 16 * wave, 16 * tj,
+                tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
 }
 
 // ---- bordered arrow: corner system and final y_F --------------------------------
 // M_c = S_corner + D^2 - sum_I B_I' Yb_I ; v = rhs_c - sum_I B_I' y0_I
+// The two sums run over all N*64 band rows as 16x16 MFMA tiles, each wave a
+// contiguous quarter of the rows, partials added in wave order.
 __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
-    const int na4 = 4 * P.nintr;
+    const int na4 = 4 * P.nintr, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = lane & 15, kk = lane >> 4;
+    __shared__ double part[4][2][16][16];
     __shared__ double Mc[16 * 16 + 16];
-    __shared__ double red[NT];
-    const int nent = na4 * na4 + na4;
-    for (int q = 0; q < nent; ++q) {
-        // q < na4*na4: (a, c) -> sum_I sum_row B_I[row][a] Yb_I[row][c]; else v_a
-        const int a = q < na4 * na4 ? q / na4 : q - na4 * na4;
-        const int c = q < na4 * na4 ? q % na4 : -1;
-        double v = 0.0;
-        for (int e = threadIdx.x; e < b.N * M; e += NT) {
-            const int I = e / M, row = e % M;
-            const double* R0 = b.R0 + ((size_t)I * M + row) * b.nrhs;  // original R (B in cols 1..)
-            const double* Y = b.Y + ((size_t)I * M + row) * b.nrhs;
-            v += R0[1 + a] * (c >= 0 ? Y[1 + c] : Y[0]);
-        }
-        red[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = NT / 2; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) {
-            if (c >= 0) {
-                double m = P.Scorner[(((size_t)(a / 4) * P.nintr + c / 4) * 16) + (a % 4) * 4 + c % 4];
-                if (a == c) {
-                    const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
-                    m += lm * lm;
-                }
-                Mc[a * 16 + c] = m - red[0];
-            } else {
-                Mc[256 + a] = P.rhs[P.nb + a] - red[0];
-            }
-        }
-        __syncthreads();
+    const int rows = b.N * M, q = rows / 4, k0 = wave * q;
+    v4d m1 = zero4(), m2 = zero4();
+    for (int k = k0; k < k0 + q; k += 4) {
+        const double* R0 = b.R0 + (size_t)(k + kk) * b.nrhs;
+        const double* Y = b.Y + (size_t)(k + kk) * b.nrhs;
+        const double a = i < na4 ? R0[1 + i] : 0.0;
+        const double y1 = i < na4 ? Y[1 + i] : 0.0;
+        const double y0 = i == 0 ? Y[0] : 0.0;
+        m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y1, m1, 0, 0, 0);
+        m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y0, m2, 0, 0, 0);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        part[wave][0][kk + 4 * r][i] = m1[r];
+        part[wave][1][kk + 4 * r][i] = m2[r];
+    }
+    __syncthreads();
+    if (threadIdx.x < na4 * na4) {
+        const int a = threadIdx.x / na4, c = threadIdx.x % na4;
+        const double red = part[0][0][a][c] + part[1][0][a][c] + part[2][0][a][c] + part[3][0][a][c];
+        double m = P.Scorner[(((size_t)(a / 4) * P.nintr + c / 4) * 16) + (a % 4) * 4 + c % 4];
+        if (a == c) {
+            const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
+            m += lm * lm;
+        }
+        Mc[a * 16 + c] = m - red;
+    }
+    if (threadIdx.x < na4) {
+        const int a = threadIdx.x;
+        const double red = part[0][1][a][0] + part[1][1][a][0] + part[2][1][a][0] + part[3][1][a][0];
+        Mc[256 + a] = P.rhs[P.nb + a] - red;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         // dense Cholesky solve of the corner (<= 16 x 16)
         bool ok = true;
@@ -354,23 +430,23 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
             if (!(d > 0.0)) ok = false;
             d = sqrt(d);
             Mc[j * 16 + j] = d;
-            for (int i = j + 1; i < na4; ++i) {
-                double t = Mc[i * 16 + j];
-                for (int k = 0; k < j; ++k) t -= Mc[i * 16 + k] * Mc[j * 16 + k];
-                Mc[i * 16 + j] = t / d;
+            for (int i2 = j + 1; i2 < na4; ++i2) {
+                double t = Mc[i2 * 16 + j];
+                for (int k = 0; k < j; ++k) t -= Mc[i2 * 16 + k] * Mc[j * 16 + k];
+                Mc[i2 * 16 + j] = t / d;
             }
         }
         double* v = Mc + 256;
-        for (int i = 0; i < na4; ++i) {
-            double t = v[i];
-            for (int k = 0; k < i; ++k) t -= Mc[i * 16 + k] * v[k];
-            v[i] = t / Mc[i * 16 + i];
+        for (int i2 = 0; i2 < na4; ++i2) {
+            double t = v[i2];
+            for (int k = 0; k < i2; ++k) t -= Mc[i2 * 16 + k] * v[k];
+            v[i2] = t / Mc[i2 * 16 + i2];
         }
-        for (int i = na4 - 1; i >= 0; --i) {
-            double t = v[i];
-            for (int k = i + 1; k < na4; ++k) t -= Mc[k * 16 + i] * v[k];
-            v[i] = t / Mc[i * 16 + i];
-            P.yF[P.nb + i] = v[i];
+        for (int i2 = na4 - 1; i2 >= 0; --i2) {
+            double t = v[i2];
+            for (int k = i2 + 1; k < na4; ++k) t -= Mc[k * 16 + i2] * v[k];
+            v[i2] = t / Mc[i2 * 16 + i2];
+            P.yF[P.nb + i2] = v[i2];
         }
         if (!ok) b.fail[0] = 1.0;
     }
@@ -395,12 +471,12 @@ bool bcr_supported(const DevProblem& P) { return P.D <= kBcrK && P.ncam > 0 && 1
 void bcr_setup(BcrArgs& b, const DevProblem& P) {
     b.K = kBcrK;
     b.N = (P.ncam + b.K - 1) / b.K;
-    b.nrhs = ((1 + 4 * P.nintr) + 7) / 8 * 8;
+    b.nrhs = ((1 + 4 * P.nintr) + 15) / 16 * 16;   // MFMA column tiles
 }
 
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
-    return 5 * mm + 4 * mr + 8;  // A C L Wl Wr | R R0 Z Y | fail
+    return 5 * mm + 4 * mr + 8;  // A C L(=X) Wl Wr | R R0 Z Y | fail
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
@@ -414,15 +490,18 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     hipLaunchKernelGGL(bcr_pack_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipMemcpyAsync(b.R0, b.R, (size_t)b.N * M * b.nrhs * sizeof(double), hipMemcpyDeviceToDevice, s));
-    const size_t lds_f = (2 * M * LD + M * (b.nrhs + 1) + 2) * sizeof(double);
-    const size_t lds_u = 2 * M * LD * sizeof(double);
-    const size_t lds_t = (M * LD + M * (b.nrhs + 1) + 2) * sizeof(double);
+    const size_t ldr = b.nrhs + 1;
+    const size_t lds_f = (4 * M * LD + M * ldr + 34) * sizeof(double);
+    const size_t lds_u = (3 * M * LD + 2 * M * ldr) * sizeof(double);
+    const size_t lds_t = (2 * M * LD + 2 * M * ldr + 34) * sizeof(double);
+    const size_t lds_b = (3 * M * LD + 3 * M * ldr) * sizeof(double);
     static bool attr = false;
-    if (!attr) {
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_factor_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_u));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(M * LD + M * 33 + 2) * 8));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(M * LD + M * 33 + 2) * 8));
+    if (!attr) {   // sized for the largest nrhs (32)
+        const int cap = 160 * 1024;
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_factor_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         attr = true;
     }
     int s_top = 1;
@@ -440,7 +519,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     for (int stride = s_top / 2; stride >= 1; stride /= 2) {
         if (stride >= b.N) continue;
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-        hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_t, s, b, stride);
+        hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, stride);
         SFM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(bcr_corner_kernel, dim3(1), dim3(NT), 0, s, b, P, radius);

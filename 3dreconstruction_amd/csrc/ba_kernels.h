@@ -21,6 +21,7 @@ constexpr int kPartT = 5;  // per step block: model acc, cand cost, step norm^2,
 
 struct DevProblem {
     int32_t n_img, n_intr, n_spt, n_sobs, n_chunk, ncam, nintr, D;
+    int32_t tile_nt;    // 16-row MFMA tiles per chunk side: 4 (64 F rows) or 5 (76 + w row)
     int64_t nb, nF;
     double huber_a, min_diag, max_diag;
     // shard data
@@ -30,7 +31,6 @@ struct DevProblem {
     const int32_t* obs_slot;
     const double* obs_uv;
     const ChunkDesc* chunks;
-    const int32_t* sub_starts;
     const int32_t* img_obs_ptr;
     const int32_t* img_obs;
     const int32_t* img_colc;

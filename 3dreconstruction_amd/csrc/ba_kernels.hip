@@ -65,7 +65,6 @@ __global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __
                 double acc = w[a] * w[b];
                 for (int k = 0; k < 3; ++k) acc += (R[k * 3 + a] - (a == k ? 1.0 : 0.0)) * Wx[k * 3 + b];
                 cp.Ar[a * 3 + b] = acc / th2;
-                cp.Al[a * 3 + b] = R[a * 3 + b];
             }
     } else {
         cp.c = 1.0; cp.s = 0.0; cp.omc = 0.0; cp.small = 1.0;
@@ -73,7 +72,6 @@ __global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __
         const double Rs[9] = {1, -w[2], w[1], w[2], 1, -w[0], -w[1], w[0], 1};
         for (int a = 0; a < 9; ++a) {
             cp.R[a] = Rs[a];
-            cp.Al[a] = (a % 4 == 0) ? 1.0 : 0.0;
             cp.Ar[a] = (a % 4 == 0) ? 1.0 : 0.0;
         }
     }
@@ -133,15 +131,21 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
             L.Ji[0][0] = x * sr; L.Ji[0][1] = 0.0; L.Ji[0][2] = sr; L.Ji[0][3] = 0.0;
             L.Ji[1][0] = 0.0; L.Ji[1][1] = y * sr; L.Ji[1][2] = 0.0; L.Ji[1][3] = sr;
         }
+        // dP/dX = R; dP/dw = -Al [X]x Ar with Al = R (Rodrigues) or I (small
+        // angle), so the left factor A Al is J_X itself or A.
+        double Jx[2][3];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                Jx[r][j] = A[r][0] * cp.R[j] + A[r][1] * cp.R[3 + j] + A[r][2] * cp.R[6 + j];
         if (JX) {
 #pragma unroll
             for (int r = 0; r < 2; ++r)
 #pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    L.Jx[r][j] = A[r][0] * cp.R[j] + A[r][1] * cp.R[3 + j] + A[r][2] * cp.R[6 + j];
+                for (int j = 0; j < 3; ++j) L.Jx[r][j] = Jx[r][j];
         }
         if (JC) {
-            // dP/dw = -Al [X]x Ar
             double N[9];
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -149,12 +153,12 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
                 N[3 + j] = X[2] * cp.Ar[0 + j] - X[0] * cp.Ar[6 + j];
                 N[6 + j] = -X[1] * cp.Ar[0 + j] + X[0] * cp.Ar[3 + j];
             }
+            const bool small = cp.small != 0.0;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 double B[3];
 #pragma unroll
-                for (int k = 0; k < 3; ++k)
-                    B[k] = A[r][0] * cp.Al[k] + A[r][1] * cp.Al[3 + k] + A[r][2] * cp.Al[6 + k];
+                for (int k = 0; k < 3; ++k) B[k] = small ? A[r][k] : Jx[r][k];
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
                     L.Jc[r][j] = -(B[0] * N[j] + B[1] * N[3 + j] + B[2] * N[6 + j]);
@@ -282,9 +286,20 @@ __global__ void fscale_kernel(DevProblem P) {
 }
 
 // ---------------------------------------------------------------------------
-// Schur chunk kernel
+// Schur chunk kernel: one wavefront per chunk
+//
+// The wave owns the chunk's whole 80x80 tile as 15 lower 16x16 fp64 MFMA
+// accumulators and walks the chunk in batches of <= kSubPts points /
+// <= kSubObs (= 64) observations:
+//   A  lane = observation: linearise, Jacobi-scale, stage Jx | f | J_intr
+//   B  lane = point: V + D^2, Cholesky, L^-1, w = L^-1 g  (panel row 79)
+//   C  lane = observation: M = Jx L^-T, camera rows of Z = J_c' M
+//   C2 lane = (point, column): intrinsics rows of Z, ordered sum
+//   D  tile -= panel panel' : ceil(3 npts / 4) k-steps x 15 MFMAs
+// No block barriers: co-resident waves overlap each other's VALU and MFMA
+// phases.  Every sum has a fixed order, so results are bit-reproducible.
 // ---------------------------------------------------------------------------
-constexpr int kPanelK = 3 * kSubPts;  // 48 panel columns (3 per point)
+constexpr int kPanelK = 4 * ((3 * kSubPts + 3) / 4);  // 3 columns per point, padded to the MFMA k
 
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
@@ -292,10 +307,16 @@ __device__ __forceinline__ unsigned long long stamp() {
     return t;
 }
 
-__global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPre* __restrict__ cps,
-                                                        const double* __restrict__ intr,
-                                                        const double* __restrict__ X,
-                                                        double radius, unsigned long long* __restrict__ stamps) {
+// lower 16x16 tiles (ti >= tj) of the NT x NT tile grid, row-major
+__device__ constexpr int kTi[15] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4};
+__device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4};
+
+// NT = 5: rows 0..75 F blocks, row 79 = w, so -Z w comes out of the MFMA.
+// NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
+template <int NT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void schur_kernel(
+    DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
+    const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
     unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
     if (stamps) tprev = stamp();
 #define SFM_STAMP(k)                                      \
@@ -305,68 +326,113 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
         tprev = tn_;                                      \
     }
     __shared__ double panel[kPanelK][kTileR];   // [k][row]
-    __shared__ double obsbuf[kSubObs][8];       // Jx (6) | f (2)
-    __shared__ double ptbuf[kSubPts][12];       // Linv (6) | w (3)
-    __shared__ double zibuf[kSubObs][12];       // per-observation J_i' M (4x3)
-    const int c = blockIdx.x;
+    __shared__ double ob[kSubObs][12];          // Jx 6 | f 2 | J_intr 4 ; then M 6
+    __shared__ double li[kSubPts][6];           // L^-1 (lower, packed)
+    __shared__ double xb[kSubPts][6];           // X | scaleE of the batch's points
+    __shared__ int orow[kSubObs];               // tile row of the obs' intrinsics block
+    // chunk-level staging: every camera / intrinsics block the chunk touches
+    __shared__ CamPre scp[kCamSlots];
+    __shared__ double csc[kCamSlots][6];        // camera column scales (0: constant image)
+    __shared__ double isc[kIntrSlots][8];       // intrinsics | their column scales
+    __shared__ int crow[kCamSlots], irow[kIntrSlots];
+    __shared__ int cpoff[kChunkPts + 1];        // chunk point offsets, relative to obs_begin
+    const int c = blockIdx.x, lane = threadIdx.x;
     const ChunkDesc& cd = P.chunks[c];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int pb = cd.pt_begin, np = cd.pt_end - pb, ob0 = cd.obs_begin;
 
-    // wave -> lower 16x16 tiles of the 5x5 tile grid
-    constexpr int kTi[16] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4, 0};
-    constexpr int kTj[16] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0};
-    v4d acc[4];
+    for (int e = lane; e <= np; e += 64) cpoff[e] = P.pt_off[pb + e] - ob0;
+    {
+        constexpr int kCpW = sizeof(CamPre) / 8;
+        for (int e = lane; e < cd.n_cams * kCpW; e += 64) {
+            const int t = e / kCpW;
+            reinterpret_cast<double*>(&scp[t])[e - t * kCpW] =
+                reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
+        }
+        for (int e = lane; e < cd.n_cams * 6; e += 64) {
+            const int t = e / 6, col = cd.cam_col[t];
+            csc[t][e - 6 * t] = col >= 0 ? P.scaleF[col + e - 6 * t] : 0.0;
+        }
+        if (lane < cd.n_cams) crow[lane] = cd.cam_row[lane];
+        if (lane < 4 * cd.n_intr) {
+            const int t = lane >> 2, k = lane & 3;
+            isc[t][k] = intr[4 * cd.intr_id[t] + k];
+            isc[t][4 + k] = P.scaleF[cd.intr_col[t] + k];
+        }
+        if (lane < cd.n_intr) irow[lane] = cd.intr_row[lane];
+    }
+
+    constexpr int kNTiles = NT * (NT + 1) / 2;
+    v4d acc[kNTiles];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < kNTiles; ++q) acc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+    double wacc = 0.0;   // NT = 4: -(Z w)[lane]
 
     double xn2 = 0.0, gmx = 0.0;
-    for (int sb = cd.sub_begin; sb < cd.sub_end; ++sb) {
-        const int p0 = P.sub_starts[sb];
-        const int p1 = (sb + 1 < cd.sub_end) ? P.sub_starts[sb + 1] : cd.pt_end;
-        const int o0 = P.pt_off[p0], nobs = P.pt_off[p1] - o0, npts = p1 - p0;
-        for (int e = tid; e < kPanelK * kTileR; e += 256) (&panel[0][0])[e] = 0.0;
+    __syncthreads();
+    for (int p0 = 0; p0 < np;) {
+        // batch [p0, p1): <= kSubPts points and <= kSubObs observations
+        const int q1 = p0 + 1 + lane;
+        const bool fits = lane < kSubPts && q1 <= np && cpoff[q1] - cpoff[p0] <= kSubObs;
+        const unsigned long long m = __ballot(fits);
+        const int npts = __builtin_ctzll(~m);
+        const int p1 = p0 + npts;
+        const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
+#pragma unroll
+        for (int e = lane; e < kPanelK * kTileR / 2; e += 64)
+            reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
+        if (lane < 6 * npts) {
+            const int pt = lane / 6, k = lane - 6 * pt;
+            const size_t g = 3 * (size_t)(pb + p0 + pt) + (k % 3);
+            xb[pt][k] = k < 3 ? X[g] : P.scaleE[g];
+        }
+        int slot = 0, pl = 0;
+        double u0 = 0.0, u1 = 0.0;
+        if (lane < nobs) {
+            const int o = ob0 + o0 + lane;
+            slot = P.obs_slot[o];
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+            u0 = uv.x; u1 = uv.y;
+#pragma unroll
+            for (int j = 1; j < kSubPts; ++j) pl += (j < npts && cpoff[p0 + j] - o0 <= lane) ? 1 : 0;
+        }
+        __syncthreads();
         SFM_STAMP(0)
-        // ---- phase A: observations -> scaled, corrected Jacobians ----------
+        // ---- A: observations -> scaled, corrected Jacobians -----------------
         Lin L;
-        int cs = -1, is = -1, pl = 0;
-        if (tid < nobs) {
-            const int o = o0 + tid;
-            const int img = P.obs_img[o];
-            const int slot = P.obs_slot[o];
-            cs = (slot & 255) - 1;
-            is = ((slot >> 8) & 255) - 1;
-            const int p = P.obs_pt[o];
-            pl = p - p0;
-            linearize<true, true, true>(cps[img], intr + 4 * P.img_intr[img], X + 3 * p, P.obs_uv[2 * o],
-                                        P.obs_uv[2 * o + 1], P.huber_a, L);
-            const int colc = P.img_colc[img], coli = P.img_coli[img];
+        const int cs = slot & 255, is = (slot >> 8) & 255;
+        if (lane < nobs) {
+            const double Xp[3] = {xb[pl][0], xb[pl][1], xb[pl][2]};
+            linearize<true, true, true>(scp[cs], &isc[is][0], Xp, u0, u1, P.huber_a, L);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
 #pragma unroll
-                for (int a = 0; a < 6; ++a) L.Jc[r][a] *= colc >= 0 ? P.scaleF[colc + a] : 0.0;
+                for (int a = 0; a < 6; ++a) L.Jc[r][a] *= csc[cs][a];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) L.Ji[r][a] *= P.scaleF[coli + a];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) L.Jx[r][a] *= P.scaleE[3 * (size_t)p + a];
+                for (int a = 0; a < 3; ++a) L.Jx[r][a] *= xb[pl][3 + a];
             }
 #pragma unroll
             for (int r = 0; r < 2; ++r)
 #pragma unroll
-                for (int a = 0; a < 3; ++a) obsbuf[tid][3 * r + a] = L.Jx[r][a];
-            obsbuf[tid][6] = L.f[0];
-            obsbuf[tid][7] = L.f[1];
+                for (int a = 0; a < 3; ++a) ob[lane][3 * r + a] = L.Jx[r][a];
+            ob[lane][6] = L.f[0];
+            ob[lane][7] = L.f[1];
+            // J_intr rows are [x s, 0, s, 0] and [0, y s, 0, s]: keep the 4 nonzeros
+            ob[lane][8] = L.Ji[0][0] * isc[is][4];
+            ob[lane][9] = L.Ji[1][1] * isc[is][5];
+            ob[lane][10] = L.Ji[0][2] * isc[is][6];
+            ob[lane][11] = L.Ji[1][3] * isc[is][7];
+            orow[lane] = irow[is];
         }
         __syncthreads();
         SFM_STAMP(1)
-        // ---- phase B: per point V + D^2, Cholesky, w = L^-1 g_E -------------
-        if (tid < npts) {
-            const int p = p0 + tid;
+        // ---- B: per point V + D^2, Cholesky, w = L^-1 g_E ---------------------
+        if (lane < npts) {
             double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};  // V00 V10 V11 V20 V21 V22
-            for (int q = P.pt_off[p] - o0; q < P.pt_off[p + 1] - o0; ++q) {
+            for (int q = cpoff[p0 + lane] - o0; q < cpoff[p0 + lane + 1] - o0; ++q) {
 #pragma unroll
                 for (int r = 0; r < 2; ++r) {
-                    const double j0 = obsbuf[q][3 * r], j1 = obsbuf[q][3 * r + 1], j2 = obsbuf[q][3 * r + 2];
-                    const double fr = obsbuf[q][6 + r];
+                    const double j0 = ob[q][3 * r], j1 = ob[q][3 * r + 1], j2 = ob[q][3 * r + 2];
+                    const double fr = ob[q][6 + r];
                     V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
                     V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
                     b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
@@ -375,8 +441,8 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
             // gradient / norm bookkeeping at x (used after a relinearisation)
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const double xv = X[3 * (size_t)p + a];
-                const double g = b[a] / P.scaleE[3 * (size_t)p + a];
+                const double xv = xb[lane][a];
+                const double g = b[a] / xb[lane][3 + a];
                 xn2 += xv * xv;
                 gmx = fmax(gmx, fabs(xv - (xv - g)));
             }
@@ -386,34 +452,34 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
                 const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) / radius);
                 V[di[a]] += lm * lm;
             }
-            const double l00 = sqrt(V[0]), l10 = V[1] / l00, l20 = V[3] / l00;
-            const double l11 = sqrt(V[2] - l10 * l10), l21 = (V[4] - l20 * l10) / l11;
-            const double l22 = sqrt(V[5] - l20 * l20 - l21 * l21);
-            const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+            const double i00 = 1.0 / sqrt(V[0]);
+            const double l10 = V[1] * i00, l20 = V[3] * i00;
+            const double i11 = 1.0 / sqrt(V[2] - l10 * l10);
+            const double l21 = (V[4] - l20 * l10) * i11;
+            const double i22 = 1.0 / sqrt(V[5] - l20 * l20 - l21 * l21);
             const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
             const double i20 = -(l20 * i00 + l21 * i10) * i22;
-            const double w0 = i00 * b[0], w1 = i10 * b[0] + i11 * b[1], w2 = i20 * b[0] + i21 * b[1] + i22 * b[2];
-            ptbuf[tid][0] = i00; ptbuf[tid][1] = i10; ptbuf[tid][2] = i11;
-            ptbuf[tid][3] = i20; ptbuf[tid][4] = i21; ptbuf[tid][5] = i22;
-            panel[3 * tid + 0][kTileWRow] = w0;
-            panel[3 * tid + 1][kTileWRow] = w1;
-            panel[3 * tid + 2][kTileWRow] = w2;
+            li[lane][0] = i00; li[lane][1] = i10; li[lane][2] = i11;
+            li[lane][3] = i20; li[lane][4] = i21; li[lane][5] = i22;
+            panel[3 * lane + 0][kTileWRow] = i00 * b[0];
+            panel[3 * lane + 1][kTileWRow] = i10 * b[0] + i11 * b[1];
+            panel[3 * lane + 2][kTileWRow] = i20 * b[0] + i21 * b[1] + i22 * b[2];
         }
         __syncthreads();
         SFM_STAMP(2)
-        // ---- phase C: Z = W L^-T into the panel -------------------------------
-        if (tid < nobs) {
-            const double i00 = ptbuf[pl][0], i10 = ptbuf[pl][1], i11 = ptbuf[pl][2];
-            const double i20 = ptbuf[pl][3], i21 = ptbuf[pl][4], i22 = ptbuf[pl][5];
-            double M[2][3];  // Jx L^-T
+        // ---- C: M = Jx L^-T; camera rows of Z = J_c' M ------------------------
+        if (lane < nobs) {
+            const double i00 = li[pl][0], i10 = li[pl][1], i11 = li[pl][2];
+            const double i20 = li[pl][3], i21 = li[pl][4], i22 = li[pl][5];
+            double M[2][3];
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 M[r][0] = L.Jx[r][0] * i00;
                 M[r][1] = L.Jx[r][0] * i10 + L.Jx[r][1] * i11;
                 M[r][2] = L.Jx[r][0] * i20 + L.Jx[r][1] * i21 + L.Jx[r][2] * i22;
             }
-            if (cs >= 0) {
-                const int row = cd.slot_row[cs];
+            const int row = crow[cs];
+            if (row >= 0) {
 #pragma unroll
                 for (int a = 0; a < 3; ++a)
 #pragma unroll
@@ -421,70 +487,78 @@ __global__ __launch_bounds__(256, 2) void schur_kernel(DevProblem P, const CamPr
                         panel[3 * pl + a][row + k] = L.Jc[0][k] * M[0][a] + L.Jc[1][k] * M[1][a];
             }
 #pragma unroll
-            for (int a = 0; a < 3; ++a)
+            for (int r = 0; r < 2; ++r)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) zibuf[tid][4 * a + k] = L.Ji[0][k] * M[0][a] + L.Ji[1][k] * M[1][a];
+                for (int a = 0; a < 3; ++a) ob[lane][3 * r + a] = M[r][a];
         }
         __syncthreads();
-        // intrinsics rows of Z: ordered sum over each point's observations
-        // (one thread per panel column => deterministic, no atomics)
-        if (tid < 3 * npts) {
-            const int pt = tid / 3, a = tid % 3, p = p0 + pt;
-            for (int q = P.pt_off[p] - o0; q < P.pt_off[p + 1] - o0; ++q) {
-                const int is2 = ((P.obs_slot[o0 + q] >> 8) & 255) - 1;
-                const int row = cd.slot_row[is2];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) panel[3 * pt + a][row + k] += zibuf[q][4 * a + k];
+        // ---- C2: intrinsics rows, ordered per point ---------------------------
+        // (register sums per run of observations sharing an intrinsics block)
+        if (lane < 3 * npts) {
+            const int pt = lane / 3, a = lane - 3 * pt;
+            const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
+            int row = orow[q0];
+            double z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+            for (int q = q0; q < q1; ++q) {
+                const int rq = orow[q];
+                if (rq != row) {
+                    panel[3 * pt + a][row + 0] += z0; panel[3 * pt + a][row + 1] += z1;
+                    panel[3 * pt + a][row + 2] += z2; panel[3 * pt + a][row + 3] += z3;
+                    z0 = z1 = z2 = z3 = 0.0;
+                    row = rq;
+                }
+                const double m0 = ob[q][a], m1 = ob[q][3 + a];
+                z0 += ob[q][8] * m0;
+                z1 += ob[q][9] * m1;
+                z2 += ob[q][10] * m0;
+                z3 += ob[q][11] * m1;
             }
+            panel[3 * pt + a][row + 0] += z0; panel[3 * pt + a][row + 1] += z1;
+            panel[3 * pt + a][row + 2] += z2; panel[3 * pt + a][row + 3] += z3;
         }
         __syncthreads();
         SFM_STAMP(3)
-        // ---- phase D: tile += panel panel' on the fp64 MFMA ------------------
+        // ---- D: tile += panel panel' on the fp64 MFMA -------------------------
         const int kk = lane >> 4, ii = lane & 15;
+        const int nks = (3 * npts + 3) >> 2;
+        for (int ks = 0; ks < nks; ++ks) {
+            double op[NT];
 #pragma unroll
-        for (int ks = 0; ks < kPanelK / 4; ++ks) {
+            for (int t = 0; t < NT; ++t) op[t] = panel[4 * ks + kk][16 * t + ii];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int t = wave + 4 * q;
-                if (t < 15) {
-                    const double av = panel[4 * ks + kk][16 * kTi[t] + ii];
-                    const double bv = panel[4 * ks + kk][16 * kTj[t] + ii];
-                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
-                }
-            }
+            for (int q = 0; q < kNTiles; ++q)
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[kTi[q]], op[kTj[q]], acc[q], 0, 0, 0);
         }
+        if (NT == 4)
+            for (int k = 0; k < 3 * npts; ++k) wacc += panel[k][lane] * panel[k][kTileWRow];
         __syncthreads();
         SFM_STAMP(4)
+        p0 = p1;
     }
     // ---- write the negated tile (full symmetric 80x80) -----------------------
     double* out = P.tiles + (size_t)c * kTileR * kTileR;
+    if (NT == 4) out[kTileWRow * kTileR + lane] = -wacc;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int t = wave + 4 * q;
-        if (t < 15) {
-            const int ti = kTi[t], tj = kTj[t];
+    for (int q = 0; q < kNTiles; ++q) {
+        const int ti = kTi[q], tj = kTj[q];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 16 * ti + (lane >> 4) + 4 * r, col = 16 * tj + (lane & 15);
-                const double v = -acc[q][r];
-                out[row * kTileR + col] = v;
-                if (ti != tj) out[col * kTileR + row] = v;
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * ti + (lane >> 4) + 4 * r, col = 16 * tj + (lane & 15);
+            const double v = -acc[q][r];
+            out[row * kTileR + col] = v;
+            if (ti != tj) out[col * kTileR + row] = v;
         }
     }
-    // ---- point partials ------------------------------------------------------
-    __shared__ double red[4][2];
+    // ---- point partials (fixed-order wave reduction) --------------------------
     double s1[1] = {xn2};
     wave_sum(s1);
     const double m1 = wave_max(gmx);
-    if (lane == 0) { red[wave][0] = s1[0]; red[wave][1] = m1; }
-    __syncthreads();
-    if (tid == 0) {
-        P.part_s[2 * (size_t)c] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        P.part_s[2 * (size_t)c + 1] = fmax(fmax(red[0][1], red[1][1]), fmax(red[2][1], red[3][1]));
+    if (lane == 0) {
+        P.part_s[2 * (size_t)c] = s1[0];
+        P.part_s[2 * (size_t)c + 1] = m1;
     }
     SFM_STAMP(5)
-    if (stamps && tid == 0)
+    if (stamps && lane == 0)
         for (int k = 0; k < 6; ++k) stamps[6 * (size_t)c + k] = tacc[k];
 #undef SFM_STAMP
 }
@@ -1007,7 +1081,10 @@ void ba_fscale(const DevProblem& P, hipStream_t s) {
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
               hipStream_t s, unsigned long long* stamps) {
     if (P.n_chunk <= 0) return;
-    hipLaunchKernelGGL(schur_kernel, dim3(P.n_chunk), dim3(256), 0, s, P, cp, intr, X, radius, stamps);
+    if (P.tile_nt == 4)
+        hipLaunchKernelGGL(schur_kernel<4>, dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
+    else
+        hipLaunchKernelGGL(schur_kernel<5>, dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
     SFM_HIP(hipGetLastError());
 }
 

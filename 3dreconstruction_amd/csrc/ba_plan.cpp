@@ -10,6 +10,7 @@
 #include "ba_plan.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <map>
 #include <numeric>
@@ -142,91 +143,130 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
 
     // ---- Schur chunks --------------------------------------------------------
     // Greedy over shard points: a chunk's F blocks (camera 6 rows, intrinsics 4
-    // rows) must fit kTileRowsUsed rows of one 80x80 tile.
-    int64_t flops = 0;
-    {
+    // rows) must fit `cap` rows of its tile: 64 (4x4 MFMA tiles, -Zw on the
+    // VALU) or 76 (5x5 tiles, -Zw in row 79).  The 64-row form does 2/3 of the
+    // MFMA work per point; it is used unless it would need many more chunks.
+    // 128 points per chunk: ~2x the co-resident waves of the chip at C4 size,
+    // so the last round of chunks is short (256 measured 17% slower).
+    int chunk_pts = kChunkPts / 2;   // tuning override (diagnostics)
+    if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));
+    auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, std::vector<int32_t>& slot_out) -> int64_t {
+        int64_t flops = 0;
+        slot_out.assign(pl.n_sobs, 0);
         ChunkDesc cd{};
-        std::vector<int> cams, intrs;  // images / intrinsics in the current chunk
+        std::vector<int> cams, intrs, dcams;  // F-slot images / intrinsics, staged images
         int rows = 0;
         auto reset = [&](int32_t p) {
             cd = ChunkDesc{};
             cd.pt_begin = p;
             cd.obs_begin = pl.pt_off[p];
             for (int s = 0; s < kMaxSlots; ++s) { cd.slot_img[s] = -1; cd.slot_intr[s] = -1; cd.slot_row[s] = -1; cd.slot_col[s] = -1; }
-            cams.clear(); intrs.clear(); rows = 0;
-            cd.sub_begin = (int32_t)pl.sub_starts.size();
+            for (int s = 0; s < kCamSlots; ++s) { cd.cam_img[s] = -1; cd.cam_row[s] = -1; cd.cam_col[s] = -1; }
+            for (int s = 0; s < kIntrSlots; ++s) { cd.intr_id[s] = -1; cd.intr_row[s] = -1; cd.intr_col[s] = -1; }
+            cams.clear(); intrs.clear(); dcams.clear(); rows = 0;
         };
         auto close = [&](int32_t p_end) {
             cd.pt_end = p_end;
             cd.obs_end = pl.pt_off[p_end];
-            // sub-batches: <= kSubPts points and <= kSubObs observations
-            int32_t p = cd.pt_begin;
-            while (p < p_end) {
-                pl.sub_starts.push_back(p);
-                int32_t q = p, n = 0;
-                while (q < p_end && q - p < kSubPts && n + (pl.pt_off[q + 1] - pl.pt_off[q]) <= kSubObs) {
-                    n += pl.pt_off[q + 1] - pl.pt_off[q];
-                    ++q;
-                }
-                p = q;
-            }
-            cd.sub_end = (int32_t)pl.sub_starts.size();
             cd.n_slots = (int32_t)(cams.size() + intrs.size());
-            pl.chunks.push_back(cd);
+            cd.n_cams = (int32_t)dcams.size();
+            cd.n_intr = (int32_t)intrs.size();
+            chunks_out.push_back(cd);
         };
+        auto has = [](const std::vector<int>& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); };
         if (pl.n_spt > 0) reset(0);
         for (int32_t k = 0; k < (int32_t)pl.n_spt; ++k) {
             const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
             SFM_REQUIRE(nobs <= kSubObs, SFM_ERR_UNSUPPORTED, "point with %d observations (> %d)",
                         nobs, kSubObs);
-            std::vector<int> pc, pi;
+            std::vector<int> pc, pi, pd;
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
                 const int img = pl.obs_img[s];
                 if (pl.cam_blk[img] >= 0) pc.push_back(img);
+                pd.push_back(img);
                 const int q = P.img_intr[img];
-                if (std::find(pi.begin(), pi.end(), q) == pi.end()) pi.push_back(q);
+                if (!has(pi, q)) pi.push_back(q);
             }
             const int own = 6 * (int)pc.size() + 4 * (int)pi.size();
-            SFM_REQUIRE(own <= kTileRowsUsed, SFM_ERR_UNSUPPORTED,
-                        "point %lld spans %d F rows (> %d): track too long for this build",
-                        (long long)pl.spt_global[k], own, kTileRowsUsed);
-            int add = 0, add_slots = 0;
-            for (int img : pc) if (std::find(cams.begin(), cams.end(), img) == cams.end()) { add += 6; ++add_slots; }
-            for (int q : pi) if (std::find(intrs.begin(), intrs.end(), q) == intrs.end()) { add += 4; ++add_slots; }
+            SFM_REQUIRE(own <= cap && (int)pd.size() <= kCamSlots && (int)pi.size() <= kIntrSlots,
+                        SFM_ERR_UNSUPPORTED,
+                        "point %lld spans %d F rows / %d images (> %d / %d): track too long for this build",
+                        (long long)pl.spt_global[k], own, (int)pd.size(), cap, kCamSlots);
+            int add = 0, add_slots = 0, add_d = 0, add_i = 0;
+            for (int img : pc) if (!has(cams, img)) { add += 6; ++add_slots; }
+            for (int q : pi) if (!has(intrs, q)) { add += 4; ++add_slots; ++add_i; }
+            for (int img : pd) if (!has(dcams, img)) ++add_d;
             const bool full = k > cd.pt_begin &&
-                              (rows + add > kTileRowsUsed || k - cd.pt_begin >= kChunkPts ||
-                               (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots);
+                              (rows + add > cap || k - cd.pt_begin >= chunk_pts ||
+                               (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots ||
+                               (int)dcams.size() + add_d > kCamSlots ||
+                               (int)intrs.size() + add_i > kIntrSlots);
             if (full) { close(k); reset(k); }
             for (int img : pc)
-                if (std::find(cams.begin(), cams.end(), img) == cams.end()) {
+                if (!has(cams, img)) {
                     const int s = (int)(cams.size() + intrs.size());
                     cams.push_back(img);
                     cd.slot_img[s] = img; cd.slot_row[s] = rows; cd.slot_col[s] = pl.img_colc[img];
                     rows += 6;
                 }
             for (int q : pi)
-                if (std::find(intrs.begin(), intrs.end(), q) == intrs.end()) {
+                if (!has(intrs, q)) {
                     const int s = (int)(cams.size() + intrs.size());
+                    const int t = (int)intrs.size();
                     intrs.push_back(q);
                     cd.slot_intr[s] = q; cd.slot_row[s] = rows;
                     cd.slot_col[s] = (int32_t)(pl.nb + 4 * pl.intr_blk[q]);
+                    cd.intr_id[t] = q; cd.intr_row[t] = rows; cd.intr_col[t] = cd.slot_col[s];
                     rows += 4;
                 }
-            // observation -> slot indices (1-based; 0 = none)
+            for (int img : pd)
+                if (!has(dcams, img)) {
+                    const int t = (int)dcams.size();
+                    dcams.push_back(img);
+                    cd.cam_img[t] = img;
+                    for (int s = 0; s < kMaxSlots; ++s)
+                        if (cd.slot_img[s] == img) { cd.cam_row[t] = cd.slot_row[s]; cd.cam_col[t] = cd.slot_col[s]; }
+                }
+            // observation -> staged camera | staged intrinsics << 8
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
                 const int img = pl.obs_img[s];
-                int cs = 0, is = 0;
-                for (int t = 0; t < kMaxSlots; ++t) {
-                    if (cd.slot_img[t] == img && pl.cam_blk[img] >= 0) cs = t + 1;
-                    if (cd.slot_intr[t] == P.img_intr[img]) is = t + 1;
-                }
-                pl.obs_slot[s] = cs | (is << 8);
+                const int cs = (int)(std::find(dcams.begin(), dcams.end(), img) - dcams.begin());
+                const int is = (int)(std::find(intrs.begin(), intrs.end(), P.img_intr[img]) - intrs.begin());
+                slot_out[s] = cs | (is << 8);
             }
             const int64_t nfp = own;
             flops += 2LL * 3 * nfp * nfp + 600LL * nobs;   // Z Z' over the point's F rows + linearisation
         }
         if (pl.n_spt > 0) close((int32_t)pl.n_spt);
-        pl.sub_starts.push_back((int32_t)pl.n_spt);  // sentinel
+        return flops;
+    };
+    int max_own = 0;
+    for (int64_t k = 0; k < pl.n_spt; ++k) {
+        int nc = 0;
+        std::vector<int> pi;
+        for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+            if (pl.cam_blk[pl.obs_img[s]] >= 0) ++nc;
+            const int q = P.img_intr[pl.obs_img[s]];
+            if (std::find(pi.begin(), pi.end(), q) == pi.end()) pi.push_back(q);
+        }
+        max_own = std::max(max_own, 6 * nc + 4 * (int)pi.size());
+    }
+    int64_t flops = 0;
+    pl.tile_nt = 5;
+    if (max_own <= 64 && !std::getenv("SFM_BA_TILE80")) {
+        std::vector<ChunkDesc> c4;
+        std::vector<int32_t> s4;
+        const int64_t f4 = make_chunks(64, c4, s4);
+        std::vector<ChunkDesc> c5;
+        std::vector<int32_t> s5;
+        const int64_t f5 = make_chunks(kTileRowsUsed, c5, s5);
+        if (c4.size() * 4 <= c5.size() * 5) {
+            pl.tile_nt = 4; pl.chunks.swap(c4); pl.obs_slot.swap(s4); flops = f4;
+        } else {
+            pl.chunks.swap(c5); pl.obs_slot.swap(s5); flops = f5;
+        }
+    } else {
+        flops = make_chunks(kTileRowsUsed, pl.chunks, pl.obs_slot);
     }
     pl.schur_flops = flops;
     pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +

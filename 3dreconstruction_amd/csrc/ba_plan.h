@@ -31,7 +31,7 @@ struct BAHostPlan {
     std::vector<int32_t> obs_img, obs_pt, obs_slot;
     std::vector<double> obs_uv;
     std::vector<ChunkDesc> chunks;
-    std::vector<int32_t> sub_starts;  // sub-batch start points, sentinel-terminated per chunk
+    int32_t tile_nt = 5;              // 16-row MFMA tiles per chunk side (4 or 5)
     std::vector<int32_t> img_obs_ptr, img_obs;
 
     // ---- reduce plan ------------------------------------------------------

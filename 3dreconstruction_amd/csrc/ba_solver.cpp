@@ -35,7 +35,7 @@ struct sfm_ba_plan {
     sfm_ctx* ctx = nullptr;
     BAHostPlan hp;
     DevProblem P{};
-    DBuf<int32_t> pt_off, obs_img, obs_pt, obs_slot, sub_starts, img_obs_ptr, img_obs, img_colc,
+    DBuf<int32_t> pt_off, obs_img, obs_pt, obs_slot, img_obs_ptr, img_obs, img_colc,
         img_coli, img_intr, blk_img, blk_intr;
     DBuf<double> obs_uv;
     DBuf<ChunkDesc> chunks;
@@ -83,7 +83,6 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->obs_slot, h.obs_slot, s);
     up(pl->obs_uv, h.obs_uv, s);
     up(pl->chunks, h.chunks, s);
-    up(pl->sub_starts, h.sub_starts, s);
     up(pl->img_obs_ptr, h.img_obs_ptr, s);
     up(pl->img_obs, h.img_obs, s);
     up(pl->img_colc, h.img_colc, s);
@@ -130,12 +129,13 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.n_img = prob.n_img; P.n_intr = prob.n_intr;
     P.n_spt = (int32_t)h.n_spt; P.n_sobs = (int32_t)h.n_sobs;
     P.n_chunk = (int32_t)h.chunks.size();
+    P.tile_nt = h.tile_nt;
     P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D;
     P.nb = h.nb; P.nF = h.nF;
     P.huber_a = prob.huber_a;
     P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p; P.obs_pt = pl->obs_pt.p;
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
-    P.sub_starts = pl->sub_starts.p; P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
+    P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
     {

@@ -21,30 +21,38 @@ constexpr int kTileN = 5;                 // 16-row MFMA tiles per chunk side
 constexpr int kTileR = 16 * kTileN;       // 80 rows
 constexpr int kTileRowsUsed = 76;         // rows 0..75 for F blocks
 constexpr int kTileWRow = 79;             // row carrying w = L^-1 g_E
-constexpr int kSubPts = 16;               // points per LDS panel sub-batch
-constexpr int kSubObs = 256;              // observations per sub-batch (<= threads)
+constexpr int kSubPts = 6;                // points per wave batch (3 panel columns each)
+constexpr int kSubObs = 64;               // observations per wave batch (one per lane)
 constexpr int kChunkPts = 256;            // points per chunk (upper bound)
-constexpr int kMaxSlots = 16;
+constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
+constexpr int kCamSlots = 16;             // staged cameras per chunk (incl. constant images)
+constexpr int kIntrSlots = 4;             // staged intrinsics blocks per chunk
 
 // Per-camera precomputed rotation terms (for current or candidate params).
 //   Rodrigues branch: P = X c + (u x X) s + u (u.X)(1-c) + t,
 //                     dP/dX = R, dP/dw = -R [X]x Ar  (Ar = (w w' + (R'-I)[w]x)/|w|^2)
 //   small-angle branch (|w|^2 <= eps): P = X + w x X + t, dP/dX = I + [w]x,
-//                     dP/dw = -[X]x (R := I + [w]x for dP/dX, Al = I, Ar = I)
-struct CamPre {
+//                     dP/dw = -[X]x (R := I + [w]x for dP/dX, left factor I, Ar = I)
+struct alignas(16) CamPre {
     double c, s, omc, small;   // cos, sin, 1-cos, small-angle flag (0/1)
     double u[3];               // unit axis (Rodrigues) or w (small angle)
     double t[3];
-    double R[9];               // dP/dX
-    double Al[9];              // left factor of dP/dw
+    double R[9];               // dP/dX; left factor of dP/dw is R (Rodrigues) or I (small)
     double Ar[9];              // right factor of dP/dw
 };
 
+// obs_slot of an observation: staged camera index | (staged intrinsics index << 8)
 struct ChunkDesc {
     int32_t pt_begin, pt_end;      // shard point range
     int32_t obs_begin, obs_end;    // shard obs range
-    int32_t sub_begin, sub_end;    // range into the sub-batch start list
-    int32_t n_slots, pad;
+    int32_t n_slots;               // F slots (reduce plan)
+    int32_t n_cams, n_intr, pad;   // staged cameras / intrinsics
+    int32_t cam_img[kCamSlots];    // image of a staged camera
+    int32_t cam_row[kCamSlots];    // its first tile row, -1 for a constant image
+    int32_t cam_col[kCamSlots];    // its first scaleF column, -1 for a constant image
+    int32_t intr_id[kIntrSlots];   // staged intrinsics block
+    int32_t intr_row[kIntrSlots];  // its first tile row
+    int32_t intr_col[kIntrSlots];  // its first scaleF column
     int32_t slot_img[kMaxSlots];   // image of a camera slot (or -1)
     int32_t slot_intr[kMaxSlots];  // intrinsic block of an intr slot (or -1)
     int32_t slot_row[kMaxSlots];   // first tile row of the slot

@@ -72,6 +72,16 @@ def test_trace_matches(ctx):
     plan.close()
 
 
+@pytest.mark.parametrize("tile80", [False, True])
+def test_chunk_tile_heights(ctx, monkeypatch, tile80):
+    # 64-row chunk tiles (4x4 MFMA tiles, -Zw on the VALU) are the default when
+    # every track fits 64 F rows; SFM_BA_TILE80 forces the 80-row form.
+    if tile80:
+        monkeypatch.setenv("SFM_BA_TILE80", "1")
+    sc = H.Scene(24, 3000, 8, seed=17)
+    _compare(ctx, sc)
+
+
 def test_noise_free_recovers_ground_truth(ctx):
     sc = H.Scene(12, 800, 5, noise=0.0, outliers=0.0)
     pr = sc.problem()
@@ -117,7 +127,10 @@ def test_ragged_tracks_and_no_gauge(ctx):
     sc.obs_uv = np.ascontiguousarray(sc.obs_uv.reshape(-1, 2)[keep].reshape(-1))
     sc.pt_offsets = np.array(off, np.int64)
     sc.n_obs = len(keep)
-    _compare(ctx, sc, rtol=1e-5, check_trace=False)
+    # No gauge => the normal equations are rank-deficient (7-DoF similarity),
+    # so the LM path amplifies summation order: the oracle alone returns final
+    # costs spread by 1.5e-5 relative across 1/2/3/8 threads on this scene.
+    _compare(ctx, sc, rtol=4e-5, check_trace=False)
 
 
 def test_deterministic_and_plan_reuse(ctx):
