@@ -14,7 +14,7 @@ struct BcrArgs {
     int K = 0;      // camera blocks per super-block
     int nrhs = 0;   // 1 + 4*nintr, padded to a multiple of 8
     double *A = nullptr, *C = nullptr, *L = nullptr, *Wl = nullptr, *Wr = nullptr;
-    double *R = nullptr, *R0 = nullptr, *Z = nullptr, *Y = nullptr, *fail = nullptr;
+    double *R = nullptr, *R0 = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
 };
 
 bool bcr_supported(const DevProblem& P);

@@ -85,61 +85,58 @@ __device__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src
     for (int e = threadIdx.x; e < M * nc; e += NT) dst[(e / nc) * ld_dst + e % nc] = src[(e / nc) * ld_src + e % nc];
 }
 
-// Wave-local factor + inverse of one 16x16 diagonal tile (lanes 0..15 own a
-// row, then a column).  L overwrites the lower tile (upper zeroed); X gets
-// L^-1 (upper zeroed).  sc: LDS scratch [33].
-__device__ void diag16(double* A, double* X, double* sc, double* bad) {
+// value of v in lane l (l wave-uniform): two v_readlane_b32
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)bits, l);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Wave-local factor + inverse of one 16x16 diagonal tile: lane i < 16 owns
+// row i in registers, pivots and L columns are broadcast with v_readlane.
+// L overwrites the lower tile (upper zeroed); X gets L^-1 (upper zeroed).
+__device__ void diag16(double* A, double* X, double* bad) {
     const int lane = threadIdx.x & 63, i = lane;
     const bool act = lane < 16;
-    double a[16];
+    double a[16], rinv[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? A[i * LD + j] : 0.0;
+    bool ok = true;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        if (i == k) sc[0] = a[k];
-        wave_sync();
-        const double d = sc[0];
-        const double rinv = rsqrt_nr(d);
-        if (lane == 0) {
-            if (!(d > 0.0)) bad[0] = 1.0;
-            sc[17 + k] = rinv;
-        }
-        if (i == k) a[k] = d * rinv;
-        else if (i > k) a[k] *= rinv;
-        if (act) sc[1 + i] = a[k];
-        wave_sync();
+        const double d = rdlane(a[k], k);
+        ok = ok && d > 0.0;
+        rinv[k] = rsqrt_nr(d);
+        a[k] = i == k ? d * rinv[k] : (i > k ? a[k] * rinv[k] : a[k]);
 #pragma unroll
-        for (int j = k + 1; j < 16; ++j) a[j] = fma(-a[k], sc[1 + j], a[j]);
-        wave_sync();
+        for (int j = k + 1; j < 16; ++j) a[j] = fma(-a[k], rdlane(a[k], j), a[j]);
     }
-    if (act) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
-    }
-    wave_sync();
-    // X = L^-1 by columns: lane c solves L x = e_c (rows of L are LDS broadcasts)
+    if (lane == 0 && !ok) bad[0] = 1.0;
+    // X = L^-1 by columns: lane c solves L x = e_c
     const int c = lane;
     double x[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         double t = (m == c) ? 1.0 : 0.0;
 #pragma unroll
-        for (int p = 0; p < m; ++p) t = fma(-A[m * LD + p], x[p], t);
-        x[m] = t * sc[17 + m];
+        for (int p = 0; p < m; ++p) t = fma(-rdlane(a[p], m), x[p], t);
+        x[m] = t * rinv[m];
     }
     if (act) {
 #pragma unroll
+        for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
+#pragma unroll
         for (int m = 0; m < 16; ++m) X[m * LD + c] = x[m];
     }
-    wave_sync();
 }
 
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
 // the caller).  All 256 threads; ends synchronised.
-__device__ void chol_inv64(double* A, double* X, double* sc, double* bad) {
+__device__ void chol_inv64(double* A, double* X, double* bad) {
     const int wave = threadIdx.x >> 6;
     for (int k = 0; k < 4; ++k) {
-        if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), sc, bad);
+        if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), bad);
         __syncthreads();
         if (wave < 3 - k) {   // panel: L_ik = A_ik X_kk'
             const int i = k + 1 + wave;
@@ -249,24 +246,25 @@ __global__ __launch_bounds__(NT) void bcr_factor_kernel(BcrArgs b, int s) {
     load_rows(R, ldr, b.R + (size_t)i * M * b.nrhs, b.nrhs, b.nrhs);
     for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
-    chol_inv64(A, X, sc, bad);
+    chol_inv64(A, X, bad);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     double* Xg = b.L + (size_t)i * M * M;
     for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
-    const int kend = 16 * (wave + 1);   // X is lower triangular
+    // X is lower triangular: output tile row ti needs k < 16 (ti + 1); wave w
+    // takes tile column w of every output so the waves get equal work
     double* Wl = b.Wl + (size_t)i * M * M;
     double* Wr = b.Wr + (size_t)i * M * M;
-    for (int tj = 0; tj < 4; ++tj) {
-        tile_st(Wl, M, 16 * wave, 16 * tj,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Cl, LD, 16 * tj, 0, kend));
+    for (int ti = 0; ti < 4; ++ti) {
+        tile_st(Wl, M, 16 * ti, 16 * wave,
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * ti, Cl, LD, 16 * wave, 0, 16 * (ti + 1)));
         if (r < b.N)
-            tile_st(Wr, M, 16 * wave, 16 * tj,
-                    tile_mm<false, true, false>(zero4(), X, LD, 16 * wave, Cr, LD, 16 * tj, 0, kend));
+            tile_st(Wr, M, 16 * ti, 16 * wave,
+                    tile_mm<false, true, false>(zero4(), X, LD, 16 * ti, Cr, LD, 16 * wave, 0, 16 * (ti + 1)));
     }
     double* Z = b.Z + (size_t)i * M * b.nrhs;
     for (int tj = 0; tj < b.nrhs / 16; ++tj)
         tile_st(Z, b.nrhs, 16 * wave, 16 * tj,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, kend));
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
 }
 
 // ---- level l: update every even super-block from its odd neighbours ---------
@@ -332,7 +330,7 @@ __global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b) {
     load_rows(R, ldr, b.R, b.nrhs, b.nrhs);
     for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
-    chol_inv64(A, X, sc, bad);
+    chol_inv64(A, X, bad);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     for (int tj = 0; tj < b.nrhs / 16; ++tj)
         tile_st(T, ldr, 16 * wave, 16 * tj,
@@ -381,16 +379,11 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, int s) {
 
 // ---- bordered arrow: corner system and final y_F --------------------------------
 // M_c = S_corner + D^2 - sum_I B_I' Yb_I ; v = rhs_c - sum_I B_I' y0_I
-// The two sums run over all N*64 band rows as 16x16 MFMA tiles, each wave a
-// contiguous quarter of the rows, partials added in wave order.
-__global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
-    const int na4 = 4 * P.nintr, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = lane & 15, kk = lane >> 4;
-    __shared__ double part[4][2][16][16];
-    __shared__ double Mc[16 * 16 + 16];
-    const int rows = b.N * M, q = rows / 4, k0 = wave * q;
+// Pass 1: one wave per super-block, its 64 rows as 16 MFMA k-steps.
+__global__ __launch_bounds__(64) void bcr_corner_part_kernel(BcrArgs b, int na4) {
+    const int I = blockIdx.x, lane = threadIdx.x, i = lane & 15, kk = lane >> 4;
     v4d m1 = zero4(), m2 = zero4();
-    for (int k = k0; k < k0 + q; k += 4) {
+    for (int k = I * M; k < I * M + M; k += 4) {
         const double* R0 = b.R0 + (size_t)(k + kk) * b.nrhs;
         const double* Y = b.Y + (size_t)(k + kk) * b.nrhs;
         const double a = i < na4 ? R0[1 + i] : 0.0;
@@ -399,15 +392,27 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
         m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y1, m1, 0, 0, 0);
         m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y0, m2, 0, 0, 0);
     }
+    double* out = b.part + (size_t)I * 512;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        part[wave][0][kk + 4 * r][i] = m1[r];
-        part[wave][1][kk + 4 * r][i] = m2[r];
+        out[(kk + 4 * r) * 16 + i] = m1[r];
+        out[256 + (kk + 4 * r) * 16 + i] = m2[r];
     }
-    __syncthreads();
+}
+
+// Pass 2: partials added in super-block order, then the small dense solve.
+__global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
+    const int na4 = 4 * P.nintr;
+    __shared__ double Mc[16 * 16 + 16];
+    auto sum_parts = [&](int off) {   // fixed order; loads unrolled to overlap
+        double t = 0.0;
+#pragma unroll 16
+        for (int I = 0; I < b.N; ++I) t += b.part[(size_t)I * 512 + off];
+        return t;
+    };
     if (threadIdx.x < na4 * na4) {
         const int a = threadIdx.x / na4, c = threadIdx.x % na4;
-        const double red = part[0][0][a][c] + part[1][0][a][c] + part[2][0][a][c] + part[3][0][a][c];
+        const double red = sum_parts(a * 16 + c);
         double m = P.Scorner[(((size_t)(a / 4) * P.nintr + c / 4) * 16) + (a % 4) * 4 + c % 4];
         if (a == c) {
             const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
     }
     if (threadIdx.x < na4) {
         const int a = threadIdx.x;
-        const double red = part[0][1][a][0] + part[1][1][a][0] + part[2][1][a][0] + part[3][1][a][0];
+        const double red = sum_parts(256 + a * 16);
         Mc[256 + a] = P.rhs[P.nb + a] - red;
     }
     __syncthreads();
@@ -476,13 +481,14 @@ void bcr_setup(BcrArgs& b, const DevProblem& P) {
 
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
-    return 5 * mm + 4 * mr + 8;  // A C L(=X) Wl Wr | R R0 Z Y | fail
+    return 5 * mm + 4 * mr + 512 * (size_t)b.N + 8;  // A C L(=X) Wl Wr | R R0 Z Y | part | fail
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
     b.A = base; b.C = b.A + mm; b.L = b.C + mm; b.Wl = b.L + mm; b.Wr = b.Wl + mm;
-    b.R = b.Wr + mm; b.R0 = b.R + mr; b.Z = b.R0 + mr; b.Y = b.Z + mr; b.fail = b.Y + mr;
+    b.R = b.Wr + mm; b.R0 = b.R + mr; b.Z = b.R0 + mr; b.Y = b.Z + mr;
+    b.part = b.Y + mr; b.fail = b.part + 512 * (size_t)b.N;
 }
 
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s) {
@@ -522,6 +528,8 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, stride);
         SFM_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(bcr_corner_part_kernel, dim3(b.N), dim3(64), 0, s, b, 4 * P.nintr);
+    SFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bcr_corner_kernel, dim3(1), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bcr_final_kernel, dim3((unsigned)((P.nb + 255) / 256 + 1)), dim3(256), 0, s, b, P);

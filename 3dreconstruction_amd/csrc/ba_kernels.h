@@ -40,7 +40,11 @@ struct DevProblem {
     const ReduceTerm* terms;
     int32_t n_targets;
     int32_t n_long;                 // targets with > reduce_long_threshold() terms
-    const int32_t* long_targets;
+    const int32_t* long_targets;    // [n_long] target ids
+    int32_t n_lseg;                 // kReduceSeg-term segments of the long targets
+    const int32_t* lseg_off;        // [n_long+1] segment ranges per long target
+    const int32_t* lseg;            // [n_lseg][2] (long index, first term)
+    double* lpart;                  // [n_lseg][36] segment partial sums
     // state
     double* scaleE;     // [3*n_spt]
     double* scaleF;     // [nF]
@@ -90,5 +94,6 @@ size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
 size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);
 int reduce_long_threshold();
+constexpr int kReduceSeg = 256;   // terms per long-target segment (one workgroup)
 
 }  // namespace sfm

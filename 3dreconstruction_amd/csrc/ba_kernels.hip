@@ -589,7 +589,11 @@ __device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {
     }
 }
 
-constexpr int kLongTerms = 48;   // longer term lists are summed by a whole workgroup
+// Longer term lists are summed by a whole workgroup (256 parallel chains);
+// shorter ones by one lane per element.  A camera's band blocks collect
+// ~2 * points-per-camera / chunk-points terms (about 80 at C4), the
+// intrinsics corner one per chunk (thousands).
+constexpr int kLongTerms = 256;
 
 __global__ void reduce_kernel(DevProblem P, int min_kind) {
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -601,6 +605,7 @@ __global__ void reduce_kernel(DevProblem P, int min_kind) {
     const int r = e / T.cols, cc = e % T.cols;
     const bool vec = T.cols == 1;
     double s = 0.0;
+#pragma unroll 4
     for (int k = T.c_begin; k < T.c_end; ++k) {
         const ReduceTerm q = P.terms[k];
         s += (double)q.sign * term_value(P, q, r, cc, vec);
@@ -610,31 +615,53 @@ __global__ void reduce_kernel(DevProblem P, int min_kind) {
     dst[T.dst + (vec ? r : r * T.ld + cc)] = s;
 }
 
-// one workgroup per long target: thread (g, e) sums terms g, g+G, ... of
-// element e; the G partial sums are combined in fixed order (deterministic)
-__global__ __launch_bounds__(256) void reduce_long_kernel(DevProblem P, const int32_t* __restrict__ list,
-                                                          int n, int min_kind) {
-    if ((int)blockIdx.x >= n) return;
-    const ReduceTarget T = P.targets[list[blockIdx.x]];
+// Long targets, pass 1: one workgroup per kReduceSeg-term segment, one term
+// per thread (every element of the block, <= 36, in registers); the 256
+// partial blocks are combined by xor-butterflies and wave order (fixed).
+__global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int min_kind) {
+    const int sg = blockIdx.x;
+    const int j = P.lseg[2 * sg], k0 = P.lseg[2 * sg + 1];
+    const ReduceTarget T = P.targets[P.long_targets[j]];
     if (T.dst_kind < min_kind) return;
-    const int E = T.rows * T.cols, G = 256 / E;
-    const int g = threadIdx.x / E, e = threadIdx.x % E;
-    const int r = e / T.cols, cc = e % T.cols;
+    const int E = T.rows * T.cols;
     const bool vec = T.cols == 1;
-    __shared__ double part[256];
-    double s = 0.0;
-    if (g < G)
-        for (int k = T.c_begin + g; k < T.c_end; k += G) {
-            const ReduceTerm q = P.terms[k];
-            s += (double)q.sign * term_value(P, q, r, cc, vec);
-        }
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x < E) {
-        double t = 0.0;
-        for (int q = 0; q < G; ++q) t += part[q * E + threadIdx.x];
-        target_base(P, T.dst_kind)[T.dst + (vec ? r : r * T.ld + cc)] = t;
+    double s[36];
+#pragma unroll
+    for (int e = 0; e < 36; ++e) s[e] = 0.0;
+    const int k = k0 + (int)threadIdx.x;
+    if (k < T.c_end && k - k0 < kReduceSeg) {
+        const ReduceTerm q = P.terms[k];
+        const double sgn = (double)q.sign;
+#pragma unroll
+        for (int e = 0; e < 36; ++e)
+            if (e < E) s[e] = sgn * term_value(P, q, e / T.cols, e % T.cols, vec);
     }
+    wave_sum(s);
+    __shared__ double part[4][36];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < 36; ++e) part[wave][e] = s[e];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < E) {
+        const int e = threadIdx.x;
+        P.lpart[(size_t)sg * 36 + e] = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
+    }
+}
+
+// pass 2: segment partials added in segment order
+__global__ __launch_bounds__(64) void reduce_long_kernel(DevProblem P, int min_kind) {
+    const int j = blockIdx.x;
+    const ReduceTarget T = P.targets[P.long_targets[j]];
+    if (T.dst_kind < min_kind) return;
+    const int E = T.rows * T.cols, e = threadIdx.x;
+    if (e >= E) return;
+    double t = 0.0;
+#pragma unroll 8
+    for (int sg = P.lseg_off[j]; sg < P.lseg_off[j + 1]; ++sg) t += P.lpart[(size_t)sg * 36 + e];
+    const int r = e / T.cols, cc = e % T.cols;
+    target_base(P, T.dst_kind)[T.dst + (T.cols == 1 ? r : r * T.ld + cc)] = t;
 }
 
 // ---------------------------------------------------------------------------
@@ -1093,8 +1120,9 @@ void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P, vectors_only ? 4 : 0);
     SFM_HIP(hipGetLastError());
     if (P.n_long > 0) {
-        hipLaunchKernelGGL(reduce_long_kernel, dim3(P.n_long), dim3(256), 0, s, P, P.long_targets, P.n_long,
-                           vectors_only ? 4 : 0);
+        hipLaunchKernelGGL(reduce_seg_kernel, dim3(P.n_lseg), dim3(256), 0, s, P, vectors_only ? 4 : 0);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(reduce_long_kernel, dim3(P.n_long), dim3(64), 0, s, P, vectors_only ? 4 : 0);
         SFM_HIP(hipGetLastError());
     }
 }

@@ -46,6 +46,7 @@ struct sfm_ba_plan {
     DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
         part_t, scal, bcr_buf;
     DBuf<int32_t> long_targets;
+    DBuf<double> lpart;          // long-target segment partials [n_lseg][36]
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
     BcrArgs bcr;
     bool use_bcr = false;
@@ -139,12 +140,29 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
     {
-        std::vector<int32_t> lt;
-        for (size_t t = 0; t < h.targets.size(); ++t)
-            if (h.targets[t].c_end - h.targets[t].c_begin > reduce_long_threshold()) lt.push_back((int32_t)t);
-        up(pl->long_targets, lt, s);
+        // long targets: [n_long targets | n_long+1 segment offsets | n_seg (long idx, term begin)]
+        std::vector<int32_t> lt, off{0}, seg;
+        for (size_t t = 0; t < h.targets.size(); ++t) {
+            const int32_t b0 = h.targets[t].c_begin, n = h.targets[t].c_end - b0;
+            if (n <= reduce_long_threshold()) continue;
+            for (int32_t k = 0; k < n; k += kReduceSeg) {
+                seg.push_back((int32_t)lt.size());
+                seg.push_back(b0 + k);
+            }
+            lt.push_back((int32_t)t);
+            off.push_back((int32_t)(seg.size() / 2));
+        }
         P.n_long = (int32_t)lt.size();
+        P.n_lseg = (int32_t)(seg.size() / 2);
+        std::vector<int32_t> all(lt);
+        all.insert(all.end(), off.begin(), off.end());
+        all.insert(all.end(), seg.begin(), seg.end());
+        up(pl->long_targets, all, s);
         P.long_targets = pl->long_targets.p;
+        P.lseg_off = P.long_targets + P.n_long;
+        P.lseg = P.lseg_off + P.n_long + 1;
+        pl->lpart.alloc(36 * std::max<size_t>(P.n_lseg, 1));
+        P.lpart = pl->lpart.p;
     }
     P.scaleE = pl->scaleE.p; P.scaleF = pl->scaleF.p; P.tiles = pl->tiles.p;
     P.U = pl->U.p; P.Ub = pl->Ub.p; P.Ucn = pl->Ucn.p;
