@@ -80,9 +80,31 @@ __device__ __forceinline__ void tile_st(double* C, int ldc, int r0, int c0, v4d 
 }
 __device__ __forceinline__ v4d zero4() { return v4d{0.0, 0.0, 0.0, 0.0}; }
 
-// global [64][ld_src] -> LDS [64][ld_dst], first nc columns
-__device__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src, int nc) {
-    for (int e = threadIdx.x; e < M * nc; e += NT) dst[(e / nc) * ld_dst + e % nc] = src[(e / nc) * ld_src + e % nc];
+// global [R][ld_src] -> LDS [R][ld_dst], first NC columns: every thread
+// issues all its 16-byte loads before the first LDS store
+template <int NC, int R = M>
+__device__ __forceinline__ void load_tile(double* dst, int ld_dst, const double* __restrict__ src, int ld_src) {
+    constexpr int n2 = R * NC / 2, per = (n2 + NT - 1) / NT;
+    double2 v[per];
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        const int e = threadIdx.x + q * NT;
+        if (e < n2) v[q] = *reinterpret_cast<const double2*>(src + (e / (NC / 2)) * ld_src + 2 * (e % (NC / 2)));
+    }
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        const int e = threadIdx.x + q * NT;
+        if (e < n2) {
+            double* d = dst + (e / (NC / 2)) * ld_dst + 2 * (e % (NC / 2));
+            d[0] = v[q].x;
+            d[1] = v[q].y;
+        }
+    }
+}
+__device__ __forceinline__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src, int nc) {
+    if (nc == 64) load_tile<64>(dst, ld_dst, src, ld_src);
+    else if (nc == 32) load_tile<32>(dst, ld_dst, src, ld_src);
+    else load_tile<16>(dst, ld_dst, src, ld_src);
 }
 
 // value of v in lane l (l wave-uniform): two v_readlane_b32
@@ -225,51 +247,57 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
     }
 }
 
-// ---- level l: factor every odd super-block; X = L^-1, W = X C, z = X R -------
+// ---- level l, step 1: factor every odd super-block, X_i = L_i^-1 --------------
 __global__ __launch_bounds__(NT) void bcr_factor_kernel(BcrArgs b, int s) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* A = sm;                 // [64][LD]
     double* X = A + M * LD;         // [64][LD]
-    double* Cl = X + M * LD;        // [64][LD]  C_i  = block (i, i-s)
-    double* Cr = Cl + M * LD;       // [64][LD]  C_r  = block (r, i)
-    double* R = Cr + M * LD;        // [64][nrhs+1]
-    const int ldr = b.nrhs + 1;
-    double* sc = R + M * ldr;       // [33]
-    double* bad = sc + 33;
+    double* bad = X + M * LD;
     const int i = s + 2 * s * blockIdx.x;   // odd at this level
     if (i >= b.N) return;
-    const int r = i + s, wave = threadIdx.x >> 6;
     if (threadIdx.x == 0) bad[0] = 0.0;
     load_rows(A, LD, b.A + (size_t)i * M * M, M, M);
-    load_rows(Cl, LD, b.C + (size_t)i * M * M, M, M);
-    if (r < b.N) load_rows(Cr, LD, b.C + (size_t)r * M * M, M, M);
-    load_rows(R, ldr, b.R + (size_t)i * M * b.nrhs, b.nrhs, b.nrhs);
     for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
     chol_inv64(A, X, bad);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     double* Xg = b.L + (size_t)i * M * M;
     for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
-    // X is lower triangular: output tile row ti needs k < 16 (ti + 1); wave w
-    // takes tile column w of every output so the waves get equal work
-    double* Wl = b.Wl + (size_t)i * M * M;
-    double* Wr = b.Wr + (size_t)i * M * M;
-    for (int ti = 0; ti < 4; ++ti) {
-        tile_st(Wl, M, 16 * ti, 16 * wave,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * ti, Cl, LD, 16 * wave, 0, 16 * (ti + 1)));
-        if (r < b.N)
-            tile_st(Wr, M, 16 * ti, 16 * wave,
-                    tile_mm<false, true, false>(zero4(), X, LD, 16 * ti, Cr, LD, 16 * wave, 0, 16 * (ti + 1)));
-    }
-    double* Z = b.Z + (size_t)i * M * b.nrhs;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj)
-        tile_st(Z, b.nrhs, 16 * wave, 16 * tj,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
 }
 
-// ---- level l: update every even super-block from its odd neighbours ---------
+// ---- level l, step 2: Wl = X C_i, Wr = X C_r', z = X R_i, one workgroup per
+// (odd block, 16-column tile); wave v computes output tile row v ------------
+__global__ __launch_bounds__(NT) void bcr_wz_kernel(BcrArgs b, int s) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    constexpr int L16 = 17;
+    double* X = sm;                 // [64][LD]
+    double* Cl = X + M * LD;        // [64][17]  columns 16w.. of C_i = block (i, i-s)
+    double* Cr = Cl + M * L16;      // [16][LD]  rows 16w.. of C_r = block (r, i)
+    double* R = Cr + 16 * LD;       // [64][17]  columns 16w.. of R_i
+    const int i = s + 2 * s * (blockIdx.x >> 2), w = blockIdx.x & 3;
+    if (i >= b.N) return;
+    const int r = i + s, wave = threadIdx.x >> 6;
+    const bool hr = r < b.N, hz = 16 * w < b.nrhs;
+    load_rows(X, LD, b.L + (size_t)i * M * M, M, M);
+    load_rows(Cl, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
+    if (hr) load_tile<64, 16>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
+    if (hz) load_rows(R, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
+    __syncthreads();
+    const int kend = 16 * (wave + 1);   // X is lower triangular
+    tile_st(b.Wl + (size_t)i * M * M, M, 16 * wave, 16 * w,
+            tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Cl, L16, 0, 0, kend));
+    if (hr)   // op(B)[k][n] = C_r[16w + n][k]
+        tile_st(b.Wr + (size_t)i * M * M, M, 16 * wave, 16 * w,
+                tile_mm<false, true, false>(zero4(), X, LD, 16 * wave, Cr, LD, 0, 0, kend));
+    if (hz)
+        tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * wave, 16 * w,
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, L16, 0, 0, kend));
+}
+
+// ---- level l, step 3: update every even super-block from its odd neighbours --
 // A_j -= Wr_{j-s}' Wr_{j-s} + Wl_{j+s}' Wl_{j+s};  R_j -= Wr' z + Wl' z;
-// new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}
+// new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}.
+// One workgroup per (even block, 16-row tile w); wave v: output tile (w, v).
 __global__ __launch_bounds__(NT) void bcr_update_kernel(BcrArgs b, int s) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int ldr = b.nrhs + 1;
@@ -278,9 +306,9 @@ __global__ __launch_bounds__(NT) void bcr_update_kernel(BcrArgs b, int s) {
     double* Wc = Wb + M * LD;      // Wl_{j-s}
     double* Za = Wc + M * LD;      // z_{j-s}
     double* Zb = Za + M * ldr;     // z_{j+s}
-    const int j = 2 * s * blockIdx.x;
+    const int j = 2 * s * (blockIdx.x >> 2), w = blockIdx.x & 3;
     if (j >= b.N) return;
-    const int il = j - s, ir = j + s, wave = threadIdx.x >> 6;
+    const int il = j - s, ir = j + s, v = threadIdx.x >> 6;
     const bool hl = il >= 0, hr = ir < b.N, hc = hl && j - 2 * s >= 0;
     if (hl) {
         load_rows(Wa, LD, b.Wr + (size_t)il * M * M, M, M);
@@ -293,25 +321,22 @@ __global__ __launch_bounds__(NT) void bcr_update_kernel(BcrArgs b, int s) {
     if (hc) load_rows(Wc, LD, b.Wl + (size_t)il * M * M, M, M);
     __syncthreads();
     double* Aj = b.A + (size_t)j * M * M;
-    for (int tj = 0; tj < 4; ++tj) {
-        v4d acc = tile_ld(Aj, M, 16 * wave, 16 * tj);
-        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * wave, Wa, LD, 16 * tj, 0, M);
-        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * wave, Wb, LD, 16 * tj, 0, M);
-        tile_st(Aj, M, 16 * wave, 16 * tj, acc);
+    {
+        v4d acc = tile_ld(Aj, M, 16 * w, 16 * v);
+        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * w, Wa, LD, 16 * v, 0, M);
+        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * w, Wb, LD, 16 * v, 0, M);
+        tile_st(Aj, M, 16 * w, 16 * v, acc);
     }
-    double* Rj = b.R + (size_t)j * M * b.nrhs;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj) {
-        v4d acc = tile_ld(Rj, b.nrhs, 16 * wave, 16 * tj);
-        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * wave, Za, ldr, 16 * tj, 0, M);
-        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * wave, Zb, ldr, 16 * tj, 0, M);
-        tile_st(Rj, b.nrhs, 16 * wave, 16 * tj, acc);
+    if (16 * v < b.nrhs) {
+        double* Rj = b.R + (size_t)j * M * b.nrhs;
+        v4d acc = tile_ld(Rj, b.nrhs, 16 * w, 16 * v);
+        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * w, Za, ldr, 16 * v, 0, M);
+        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * w, Zb, ldr, 16 * v, 0, M);
+        tile_st(Rj, b.nrhs, 16 * w, 16 * v, acc);
     }
-    if (hc) {
-        double* Cj = b.C + (size_t)j * M * M;
-        for (int tj = 0; tj < 4; ++tj)
-            tile_st(Cj, M, 16 * wave, 16 * tj,
-                    tile_mm<true, false, true>(zero4(), Wa, LD, 16 * wave, Wc, LD, 16 * tj, 0, M));
-    }
+    if (hc)
+        tile_st(b.C + (size_t)j * M * M, M, 16 * w, 16 * v,
+                tile_mm<true, false, true>(zero4(), Wa, LD, 16 * w, Wc, LD, 16 * v, 0, M));
 }
 
 // ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------
@@ -497,7 +522,8 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipMemcpyAsync(b.R0, b.R, (size_t)b.N * M * b.nrhs * sizeof(double), hipMemcpyDeviceToDevice, s));
     const size_t ldr = b.nrhs + 1;
-    const size_t lds_f = (4 * M * LD + M * ldr + 34) * sizeof(double);
+    const size_t lds_f = (2 * M * LD + 2) * sizeof(double);
+    const size_t lds_w = (M * LD + 2 * M * 17 + 16 * LD) * sizeof(double);
     const size_t lds_u = (3 * M * LD + 2 * M * ldr) * sizeof(double);
     const size_t lds_t = (2 * M * LD + 2 * M * ldr + 34) * sizeof(double);
     const size_t lds_b = (3 * M * LD + 3 * M * ldr) * sizeof(double);
@@ -505,6 +531,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     if (!attr) {   // sized for the largest nrhs (32)
         const int cap = 160 * 1024;
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_factor_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_wz_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
@@ -516,7 +543,9 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         const int n_even = (b.N + 2 * stride - 1) / (2 * stride);
         hipLaunchKernelGGL(bcr_factor_kernel, dim3(n_odd), dim3(NT), lds_f, s, b, stride);
         SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(bcr_update_kernel, dim3(n_even), dim3(NT), lds_u, s, b, stride);
+        hipLaunchKernelGGL(bcr_wz_kernel, dim3(4 * n_odd), dim3(NT), lds_w, s, b, stride);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(bcr_update_kernel, dim3(4 * n_even), dim3(NT), lds_u, s, b, stride);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }

@@ -307,6 +307,27 @@ __device__ __forceinline__ unsigned long long stamp() {
     return t;
 }
 
+// copy the chunk's staged cameras' CamPre into LDS (one wave)
+__device__ __forceinline__ void stage_campre(const ChunkDesc& cd, const CamPre* __restrict__ cps, CamPre* dst) {
+    constexpr int kCpW = sizeof(CamPre) / 8;
+    for (int e = threadIdx.x; e < cd.n_cams * kCpW; e += 64) {
+        const int t = e / kCpW;
+        reinterpret_cast<double*>(&dst[t])[e - t * kCpW] =
+            reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
+    }
+}
+
+// next wave batch from p0: <= kSubPts points and <= kSubObs observations
+// (cpoff = chunk-relative point offsets in LDS); returns its point count
+__device__ __forceinline__ int batch_points(const int* cpoff, int p0, int np) {
+    const int lane = threadIdx.x & 63, q1 = p0 + 1 + lane;
+    const bool fits = lane < kSubPts && q1 <= np && cpoff[q1] - cpoff[p0] <= kSubObs;
+    return __builtin_ctzll(~__ballot(fits));
+}
+
+// staged camera t is optimised (has F columns); constant images are not
+__device__ __forceinline__ bool crow_valid(const ChunkDesc& cd, int t) { return cd.cam_col[t] >= 0; }
+
 // lower 16x16 tiles (ti >= tj) of the NT x NT tile grid, row-major
 __device__ constexpr int kTi[15] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4};
 __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4};
@@ -341,13 +362,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int pb = cd.pt_begin, np = cd.pt_end - pb, ob0 = cd.obs_begin;
 
     for (int e = lane; e <= np; e += 64) cpoff[e] = P.pt_off[pb + e] - ob0;
+    stage_campre(cd, cps, scp);
     {
-        constexpr int kCpW = sizeof(CamPre) / 8;
-        for (int e = lane; e < cd.n_cams * kCpW; e += 64) {
-            const int t = e / kCpW;
-            reinterpret_cast<double*>(&scp[t])[e - t * kCpW] =
-                reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
-        }
         for (int e = lane; e < cd.n_cams * 6; e += 64) {
             const int t = e / 6, col = cd.cam_col[t];
             csc[t][e - 6 * t] = col >= 0 ? P.scaleF[col + e - 6 * t] : 0.0;
@@ -370,11 +386,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     double xn2 = 0.0, gmx = 0.0;
     __syncthreads();
     for (int p0 = 0; p0 < np;) {
-        // batch [p0, p1): <= kSubPts points and <= kSubObs observations
-        const int q1 = p0 + 1 + lane;
-        const bool fits = lane < kSubPts && q1 <= np && cpoff[q1] - cpoff[p0] <= kSubObs;
-        const unsigned long long m = __ballot(fits);
-        const int npts = __builtin_ctzll(~m);
+        const int npts = batch_points(cpoff, p0, np);   // batch [p0, p1)
         const int p1 = p0 + npts;
         const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
 #pragma unroll
