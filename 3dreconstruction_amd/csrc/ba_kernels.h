@@ -33,6 +33,8 @@ struct DevProblem {
     const ChunkDesc* chunks;
     const int32_t* img_obs_ptr;
     const int32_t* img_obs;
+    const int32_t* img_pt;          // image order (img_obs_ptr): point, measurement
+    const double* img_uv;
     const int32_t* img_colc;
     const int32_t* img_coli;
     const int32_t* img_intr;

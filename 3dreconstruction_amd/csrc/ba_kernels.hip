@@ -35,6 +35,17 @@ constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+// 1/sqrt(d): hardware estimate + two Newton steps (full fp64 accuracy)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double hy = 0.5 * d * y;
+        y = fma(y, fma(-hy, y, 0.5), y);
+    }
+    return y;
+}
+
 __device__ __forceinline__ double clampd(double v, double lo, double hi) {
     return fmin(fmax(v, lo), hi);
 }
@@ -188,75 +199,119 @@ __device__ __forceinline__ double wave_max(double v) {
 
 // ---------------------------------------------------------------------------
 // per-image Gram blocks: U = J_F' J_F (10x10), b = J_F' f, cost
+// One workgroup per image.  Each lane linearises one observation and stores
+// its two scaled rows [J_c (6) | J_i (4) | f | 0 ...] in wave-private LDS;
+// [J | f]' [J | f] is then a 16x16 fp64 MFMA tile (k = Jacobian rows), the
+// same LDS element feeding both operands.  Waves add in fixed order.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const double* __restrict__ X) {
-    const int img = blockIdx.x;
-    const int o0 = P.img_obs_ptr[img], o1 = P.img_obs_ptr[img + 1];
+    const int img = blockIdx.x / kGramSeg, seg = blockIdx.x - kGramSeg * img;   // slice of the image
+    const int a0 = P.img_obs_ptr[img], n = P.img_obs_ptr[img + 1] - a0;
+    const int o0 = a0 + (int)((int64_t)n * seg / kGramSeg), o1 = a0 + (int)((int64_t)n * (seg + 1) / kGramSeg);
     const int colc = P.img_colc[img], coli = P.img_coli[img];
-    const CamPre cp = cps[img];
-    const double* in = intr + 4 * P.img_intr[img];
-    double sc[10];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) sc[a] = colc >= 0 ? P.scaleF[colc + a] : 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) sc[6 + a] = P.scaleF[coli + a];
-    double acc[55 + 10 + 2];
-#pragma unroll
-    for (int k = 0; k < 67; ++k) acc[k] = 0.0;
-    for (int q = o0 + threadIdx.x; q < o1; q += blockDim.x) {
-        const int o = P.img_obs[q];
-        const int p = P.obs_pt[o];
-        Lin L;
-        linearize<true, true, false>(cp, in, X + 3 * p, P.obs_uv[2 * o], P.obs_uv[2 * o + 1], P.huber_a, L);
-        acc[65] += L.half_rho;
-        acc[66] = fmax(acc[66], L.ok ? 0.0 : 1.0);
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            double v[10];
-#pragma unroll
-            for (int a = 0; a < 6; ++a) v[a] = L.Jc[r][a] * sc[a];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) v[6 + a] = L.Ji[r][a] * sc[6 + a];
-            int k = 0;
-#pragma unroll
-            for (int i = 0; i < 10; ++i) {
-#pragma unroll
-                for (int j = 0; j <= i; ++j) acc[k++] += v[i] * v[j];
-                acc[55 + i] += v[i] * L.f[r];
-            }
-        }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ CamPre scp;
+    __shared__ double sin_[4], ssc[10];
+    constexpr int kJ = 11;                     // [J_c | J_i | f]; MFMA columns 11..15 read as 0
+    __shared__ double jl[4][128 * kJ];         // per wave: 64 observations x 2 rows
+    // after the loop each wave's 16x16 tile reuses its own jl region
+    auto part = [&](int w, int i, int j) -> double& { return jl[w][i * 17 + j]; };
+    if (threadIdx.x < sizeof(CamPre) / 8)
+        reinterpret_cast<double*>(&scp)[threadIdx.x] = reinterpret_cast<const double*>(&cps[img])[threadIdx.x];
+    if (threadIdx.x >= 64 && threadIdx.x < 68) sin_[threadIdx.x - 64] = intr[4 * P.img_intr[img] + threadIdx.x - 64];
+    if (threadIdx.x >= 96 && threadIdx.x < 106) {
+        const int a = threadIdx.x - 96;
+        ssc[a] = a < 6 ? (colc >= 0 ? P.scaleF[colc + a] : 0.0) : P.scaleF[coli + a - 6];
     }
-    // reduce: wave then across the 4 waves
-    double bad = acc[66];
+    __syncthreads();
+    v4d acc = v4d{0.0, 0.0, 0.0, 0.0}, acc2 = acc;
+    double cost = 0.0, bad = 0.0;
+    const int kk = lane >> 4, ii = lane & 15;
+    // software pipeline: point ids / measurements two iterations ahead, the
+    // point itself one iteration ahead
+    auto fetch_ids = [&](int base, int& p, double2& uv) {
+        const int q = base + lane;
+        p = q < o1 ? P.img_pt[q] : -1;
+        uv = q < o1 ? reinterpret_cast<const double2*>(P.img_uv)[q] : double2{0.0, 0.0};
+    };
+    auto fetch_x = [&](int p, double (&x)[3]) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) x[a] = p >= 0 ? X[3 * (size_t)p + a] : 0.0;
+    };
+    int p_c, p_n;
+    double2 uv_c, uv_n;
+    double x_c[3];
+    fetch_ids(o0 + 64 * wave, p_c, uv_c);
+    fetch_ids(o0 + 64 * wave + 256, p_n, uv_n);
+    fetch_x(p_c, x_c);
+    for (int base = o0 + 64 * wave; base < o1; base += 256) {
+        const int p_cur = p_c;
+        const double2 uv = uv_c;
+        const double Xp[3] = {x_c[0], x_c[1], x_c[2]};
+        // issue the next loads before this observation's arithmetic
+        p_c = p_n; uv_c = uv_n;
+        fetch_x(p_c, x_c);
+        fetch_ids(base + 512, p_n, uv_n);
+        double v[2][11];
+        if (p_cur >= 0) {
+            Lin L;
+            linearize<true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
+            cost += L.half_rho;
+            bad = fmax(bad, L.ok ? 0.0 : 1.0);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+#pragma unroll
+                for (int a = 0; a < 6; ++a) v[r][a] = L.Jc[r][a] * ssc[a];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) v[r][6 + a] = L.Ji[r][a] * ssc[6 + a];
+                v[r][10] = L.f[r];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int a = 0; a < 11; ++a) v[r][a] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int a = 0; a < kJ; ++a) jl[wave][(2 * lane + r) * kJ + a] = v[r][a];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nrow = 2 * min(64, o1 - base);
+        for (int k = 0; k < nrow; k += 8) {   // two independent chains (rows 0 mod 8 / 4 mod 8)
+            const double op0 = ii < kJ ? jl[wave][(k + kk) * kJ + ii] : 0.0;
+            const double op1 = (ii < kJ && k + 4 < nrow) ? jl[wave][(k + 4 + kk) * kJ + ii] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(op0, op0, acc, 0, 0, 0);
+            acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(op1, op1, acc2, 0, 0, 0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    double cs[1] = {cost};
+    wave_sum(cs);
     bad = wave_max(bad);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-        for (int k = 0; k < 66; ++k) acc[k] += __shfl_xor(acc[k], o);
-    __shared__ double red[4][67];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < 66; ++k) red[wave][k] = acc[k];
-        red[wave][66] = bad;
-    }
+    for (int r = 0; r < 4; ++r) part(wave, kk + 4 * r, ii) = acc[r] + acc2[r];
+    if (lane == 0) { part(wave, 11, 16) = cs[0]; part(wave, 12, 16) = bad; }
     __syncthreads();
     if (threadIdx.x < 100) {
         const int i = threadIdx.x / 10, j = threadIdx.x % 10;
-        const int k = i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
-        const double v = red[0][k] + red[1][k] + red[2][k] + red[3][k];
-        P.U[(size_t)img * 100 + threadIdx.x] = v;
-        if (i == j) P.Ucn[(size_t)img * 10 + i] = v;
+        const double u = ((part(0, i, j) + part(1, i, j)) + part(2, i, j)) + part(3, i, j);
+        P.U[(size_t)blockIdx.x * 100 + threadIdx.x] = u;
+        if (i == j) P.Ucn[(size_t)blockIdx.x * 10 + i] = u;
     }
     if (threadIdx.x >= 128 && threadIdx.x < 138) {
         const int i = threadIdx.x - 128;
-        P.Ub[(size_t)img * 10 + i] = red[0][55 + i] + red[1][55 + i] + red[2][55 + i] + red[3][55 + i];
+        P.Ub[(size_t)blockIdx.x * 10 + i] = ((part(0, i, 10) + part(1, i, 10)) + part(2, i, 10)) + part(3, i, 10);
     }
     if (threadIdx.x == 192) {
-        P.part_u[2 * (size_t)img] = red[0][65] + red[1][65] + red[2][65] + red[3][65];
-        P.part_u[2 * (size_t)img + 1] = fmax(fmax(red[0][66], red[1][66]), fmax(red[2][66], red[3][66]));
+        P.part_u[2 * (size_t)blockIdx.x] = ((part(0, 11, 16) + part(1, 11, 16)) + part(2, 11, 16)) + part(3, 11, 16);
+        P.part_u[2 * (size_t)blockIdx.x + 1] = fmax(fmax(part(0, 12, 16), part(1, 12, 16)), fmax(part(2, 12, 16), part(3, 12, 16)));
     }
 }
 
@@ -349,6 +404,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __shared__ double panel[kPanelK][kTileR];   // [k][row]
     __shared__ double ob[kSubObs][12];          // Jx 6 | f 2 | J_intr 4 ; then M 6
     __shared__ double li[kSubPts][6];           // L^-1 (lower, packed)
+    __shared__ double vb[kSubPts][9];           // V (packed lower) | g_E per point
     __shared__ double xb[kSubPts][6];           // X | scaleE of the batch's points
     __shared__ int orow[kSubObs];               // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
@@ -437,19 +493,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
         __syncthreads();
         SFM_STAMP(1)
-        // ---- B: per point V + D^2, Cholesky, w = L^-1 g_E ---------------------
-        if (lane < npts) {
-            double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};  // V00 V10 V11 V20 V21 V22
-            for (int q = cpoff[p0 + lane] - o0; q < cpoff[p0 + lane + 1] - o0; ++q) {
+        // ---- B1: lane (point, component): V00 V10 V11 V20 V21 V22 | g0 g1 g2 ------
+        // (each sum in observation-then-row order)
+        if (lane < 9 * npts) {
+            const int pt = lane / 9, cmp = lane - 9 * pt;
+            const int ia = cmp < 6 ? (cmp >= 3 ? 2 : (cmp >= 1 ? 1 : 0)) : cmp - 6;
+            const int ib = cmp < 6 ? cmp - (ia * (ia + 1)) / 2 : 3;
+            double v = 0.0;
+            for (int q = cpoff[p0 + pt] - o0; q < cpoff[p0 + pt + 1] - o0; ++q) {
 #pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const double j0 = ob[q][3 * r], j1 = ob[q][3 * r + 1], j2 = ob[q][3 * r + 2];
-                    const double fr = ob[q][6 + r];
-                    V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
-                    V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
-                    b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
-                }
+                for (int r = 0; r < 2; ++r)
+                    v += ob[q][3 * r + ia] * (ib < 3 ? ob[q][3 * r + ib] : ob[q][6 + r]);
             }
+            vb[pt][cmp] = v;
+        }
+        __syncthreads();
+        // ---- B2: per point V + D^2, Cholesky, w = L^-1 g_E --------------------
+        if (lane < npts) {
+            double V[6], b[3];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) V[k] = vb[lane][k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) b[k] = vb[lane][6 + k];
             // gradient / norm bookkeeping at x (used after a relinearisation)
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -464,11 +529,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                 const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) / radius);
                 V[di[a]] += lm * lm;
             }
-            const double i00 = 1.0 / sqrt(V[0]);
+            const double i00 = rsqrt_nr(V[0]);
             const double l10 = V[1] * i00, l20 = V[3] * i00;
-            const double i11 = 1.0 / sqrt(V[2] - l10 * l10);
+            const double i11 = rsqrt_nr(V[2] - l10 * l10);
             const double l21 = (V[4] - l20 * l10) * i11;
-            const double i22 = 1.0 / sqrt(V[5] - l20 * l20 - l21 * l21);
+            const double i22 = rsqrt_nr(V[5] - l20 * l20 - l21 * l21);
             const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
             const double i20 = -(l20 * i00 + l21 * i10) * i22;
             li[lane][0] = i00; li[lane][1] = i10; li[lane][2] = i11;
@@ -531,16 +596,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         __syncthreads();
         SFM_STAMP(3)
         // ---- D: tile += panel panel' on the fp64 MFMA -------------------------
+        // all operands first (padding columns are zero), then the MFMAs
         const int kk = lane >> 4, ii = lane & 15;
-        const int nks = (3 * npts + 3) >> 2;
-        for (int ks = 0; ks < nks; ++ks) {
-            double op[NT];
+        constexpr int kKs = kPanelK / 4;
+        double op[kKs][NT];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) op[t] = panel[4 * ks + kk][16 * t + ii];
+        for (int ks = 0; ks < kKs; ++ks)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) op[ks][t] = panel[4 * ks + kk][16 * t + ii];
+#pragma unroll
+        for (int ks = 0; ks < kKs; ++ks)
 #pragma unroll
             for (int q = 0; q < kNTiles; ++q)
-                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[kTi[q]], op[kTj[q]], acc[q], 0, 0, 0);
-        }
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ks][kTi[q]], op[ks][kTj[q]], acc[q], 0, 0, 0);
         if (NT == 4)
             for (int k = 0; k < 3 * npts; ++k) wacc += panel[k][lane] * panel[k][kTileWRow];
         __syncthreads();
@@ -1054,7 +1122,7 @@ __global__ __launch_bounds__(256) void step_kernel(DevProblem P, const CamPre* _
 __global__ __launch_bounds__(256) void finalize_kernel(DevProblem P, int n_step_blocks) {
     double s[5] = {0, 0, 0, 0, 0};
     double m[4] = {0, 0, 0, 0};
-    for (int i = threadIdx.x; i < P.n_img; i += 256) { s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]); }
+    for (int i = threadIdx.x; i < P.n_img * kGramSeg; i += 256) { s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]); }
     for (int i = threadIdx.x; i < P.n_chunk; i += 256) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
     for (int i = threadIdx.x; i < n_step_blocks; i += 256) {
         s[2] += P.part_t[kPartT * i]; s[3] += P.part_t[kPartT * i + 1]; s[4] += P.part_t[kPartT * i + 2];
@@ -1100,7 +1168,7 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
 
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                    hipStream_t s) {
-    hipLaunchKernelGGL(image_gram_kernel, dim3(P.n_img), dim3(256), 0, s, P, cp, intr, X);
+    hipLaunchKernelGGL(image_gram_kernel, dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp, intr, X);
     SFM_HIP(hipGetLastError());
 }
 

@@ -277,9 +277,17 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     for (int64_t s = 0; s < pl.n_sobs; ++s) pl.img_obs_ptr[pl.obs_img[s] + 1]++;
     for (int i = 0; i < P.n_img; ++i) pl.img_obs_ptr[i + 1] += pl.img_obs_ptr[i];
     pl.img_obs.resize(pl.n_sobs);
+    pl.img_pt.resize(pl.n_sobs);
+    pl.img_uv.resize(2 * pl.n_sobs);
     {
         std::vector<int32_t> fill(pl.img_obs_ptr.begin(), pl.img_obs_ptr.end() - 1);
-        for (int64_t s = 0; s < pl.n_sobs; ++s) pl.img_obs[fill[pl.obs_img[s]]++] = (int32_t)s;
+        for (int64_t s = 0; s < pl.n_sobs; ++s) {
+            const int32_t q = fill[pl.obs_img[s]]++;
+            pl.img_obs[q] = (int32_t)s;
+            pl.img_pt[q] = pl.obs_pt[s];
+            pl.img_uv[2 * q] = pl.obs_uv[2 * s];
+            pl.img_uv[2 * q + 1] = pl.obs_uv[2 * s + 1];
+        }
     }
 
     // ---- reduce plan -----------------------------------------------------------
@@ -318,7 +326,12 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         ReduceTarget t{};
         t.dst = dst; t.dst_kind = kind; t.rows = rows; t.cols = cols; t.ld = ld;
         t.c_begin = (int32_t)pl.terms.size();
-        for (const auto& e : extra) pl.terms.push_back(e);
+        for (const auto& e : extra)   // image Gram blocks come in kGramSeg partial slices
+            for (int g = 0; g < (e.kind == kSrcTile ? 1 : kGramSeg); ++g) {
+                ReduceTerm q = e;
+                if (e.kind != kSrcTile) q.index = e.index * kGramSeg + g;
+                pl.terms.push_back(q);
+            }
         if (tl) for (const auto& e : *tl) pl.terms.push_back(e);
         t.c_end = (int32_t)pl.terms.size();
         pl.targets.push_back(t);

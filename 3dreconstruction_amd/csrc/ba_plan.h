@@ -33,6 +33,8 @@ struct BAHostPlan {
     std::vector<ChunkDesc> chunks;
     int32_t tile_nt = 5;              // 16-row MFMA tiles per chunk side (4 or 5)
     std::vector<int32_t> img_obs_ptr, img_obs;
+    std::vector<int32_t> img_pt;      // image order: point of each observation
+    std::vector<double> img_uv;       // image order: its measurement
 
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;

@@ -46,7 +46,9 @@ struct sfm_ba_plan {
     DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
         part_t, scal, bcr_buf;
     DBuf<int32_t> long_targets;
-    DBuf<double> lpart;          // long-target segment partials [n_lseg][36]
+    DBuf<double> lpart;
+    DBuf<int32_t> img_pt;
+    DBuf<double> img_uv;          // long-target segment partials [n_lseg][36]
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
     BcrArgs bcr;
     bool use_bcr = false;
@@ -86,6 +88,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->chunks, h.chunks, s);
     up(pl->img_obs_ptr, h.img_obs_ptr, s);
     up(pl->img_obs, h.img_obs, s);
+    up(pl->img_pt, h.img_pt, s);
+    up(pl->img_uv, h.img_uv, s);
     up(pl->img_colc, h.img_colc, s);
     up(pl->img_coli, h.img_coli, s);
     up(pl->img_intr, h.img_intr, s);
@@ -109,9 +113,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->scaleE.alloc(xs.size());
     pl->scaleF.alloc(nF);
     pl->tiles.alloc(std::max<size_t>(h.chunks.size(), 1) * kTileR * kTileR);
-    pl->U.alloc(100 * (size_t)prob.n_img);
-    pl->Ub.alloc(10 * (size_t)prob.n_img);
-    pl->Ucn.alloc(10 * (size_t)prob.n_img);
+    pl->U.alloc(100 * (size_t)prob.n_img * kGramSeg);
+    pl->Ub.alloc(10 * (size_t)prob.n_img * kGramSeg);
+    pl->Ucn.alloc(10 * (size_t)prob.n_img * kGramSeg);
     pl->rcs_n = h.n_sband + h.n_sarrow + h.n_scorner + 3 * h.nF + 1;
     pl->rcs.alloc(pl->rcs_n);
     pl->rcs.zero(s);
@@ -120,7 +124,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->Larrow.alloc(std::max<size_t>((size_t)h.ncam * h.nintr * 24, 1));
     pl->zF.alloc(nF);
     pl->yF.alloc(nF);
-    pl->part_u.alloc(2 * (size_t)prob.n_img);
+    pl->part_u.alloc(2 * (size_t)prob.n_img * kGramSeg);
     pl->part_s.alloc(2 * std::max<size_t>(h.chunks.size(), 1));
     pl->scal.alloc(kScCount);
     pl->scal.zero(s);
@@ -137,6 +141,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p; P.obs_pt = pl->obs_pt.p;
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
     P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
+    P.img_pt = pl->img_pt.p; P.img_uv = pl->img_uv.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
     {
