@@ -1016,35 +1016,64 @@ __global__ __launch_bounds__(256) void fvec_kernel(DevProblem P, const double* _
 
 // ---------------------------------------------------------------------------
 // per-point back substitution, model cost change, candidate cost
+// One workgroup per Schur chunk, one thread per point.  The chunk's current
+// and candidate cameras, intrinsics, column scales and y_F are staged in LDS
+// once, so the per-observation work gathers only the measurement.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
-                                                   const double* __restrict__ intr,
-                                                   const CamPre* __restrict__ cps_c,
-                                                   const double* __restrict__ intr_c,
-                                                   const double* __restrict__ X,
-                                                   double* __restrict__ Xc, double radius) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                         const double* __restrict__ intr,
+                                                         const CamPre* __restrict__ cps_c,
+                                                         const double* __restrict__ intr_c,
+                                                         const double* __restrict__ X,
+                                                         double* __restrict__ Xc, double radius) {
+    __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
+    __shared__ double csy[kCamSlots][12];       // camera scaleF | yF (0 for a constant image)
+    __shared__ double isy[kIntrSlots][16];      // intrinsics | candidate | scaleF | yF
+    const int c = blockIdx.x, tid = threadIdx.x;
+    const ChunkDesc& cd = P.chunks[c];
+    {
+        constexpr int kCpW = sizeof(CamPre) / 8;
+        for (int e = tid; e < cd.n_cams * kCpW; e += blockDim.x) {
+            const int t = e / kCpW, w = e - t * kCpW;
+            reinterpret_cast<double*>(&scp[t])[w] = reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[w];
+            reinterpret_cast<double*>(&scc[t])[w] = reinterpret_cast<const double*>(&cps_c[cd.cam_img[t]])[w];
+        }
+        for (int e = tid; e < cd.n_cams * 6; e += blockDim.x) {
+            const int t = e / 6, k = e - 6 * t, col = cd.cam_col[t];
+            csy[t][k] = col >= 0 ? P.scaleF[col + k] : 0.0;
+            csy[t][6 + k] = col >= 0 ? P.yF[col + k] : 0.0;
+        }
+        if (tid < 4 * cd.n_intr) {
+            const int t = tid >> 2, k = tid & 3, col = cd.intr_col[t];
+            isy[t][k] = intr[4 * cd.intr_id[t] + k];
+            isy[t][4 + k] = intr_c[4 * cd.intr_id[t] + k];
+            isy[t][8 + k] = P.scaleF[col + k];
+            isy[t][12 + k] = P.yF[col + k];
+        }
+    }
+    __syncthreads();
+    const int p = cd.pt_begin + tid;
     double acc[3] = {0.0, 0.0, 0.0};  // model acc, candidate cost, step norm^2
     double bad = 0.0, cbad = 0.0;     // non-finite step / non-finite candidate residual
-    if (p < P.n_spt) {
-        const double* Xp = X + 3 * (size_t)p;
-        const double* sE = P.scaleE + 3 * (size_t)p;
+    if (p < cd.pt_end) {
+        const double Xp[3] = {X[3 * (size_t)p], X[3 * (size_t)p + 1], X[3 * (size_t)p + 2]};
+        const double sE[3] = {P.scaleE[3 * (size_t)p], P.scaleE[3 * (size_t)p + 1], P.scaleE[3 * (size_t)p + 2]};
         double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
         const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
         for (int o = o0; o < o1; ++o) {
-            const int img = P.obs_img[o];
+            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
             Lin L;
-            linearize<true, true, true>(cps[img], intr + 4 * P.img_intr[img], Xp, P.obs_uv[2 * o],
-                                        P.obs_uv[2 * o + 1], P.huber_a, L);
-            const int colc = P.img_colc[img], coli = P.img_coli[img];
+            linearize<true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
+            const bool cam = crow_valid(cd, cs);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 double q = 0.0;  // (J_F y_F) for this row
-                if (colc >= 0)
+                if (cam)
 #pragma unroll
-                    for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * P.scaleF[colc + a] * P.yF[colc + a];
+                    for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * csy[cs][a] * csy[cs][6 + a];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) q += L.Ji[r][a] * P.scaleF[coli + a] * P.yF[coli + a];
+                for (int a = 0; a < 4; ++a) q += L.Ji[r][a] * isy[is][8 + a] * isy[is][12 + a];
                 const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
                 const double fr = L.f[r] - q;
                 V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
@@ -1075,26 +1104,25 @@ __global__ __launch_bounds__(256) void step_kernel(DevProblem P, const CamPre* _
             if (!isfinite(xc[a])) bad = 1.0;
         }
         for (int o = o0; o < o1; ++o) {
-            const int img = P.obs_img[o];
+            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
             Lin L;
-            linearize<true, true, true>(cps[img], intr + 4 * P.img_intr[img], Xp, P.obs_uv[2 * o],
-                                        P.obs_uv[2 * o + 1], P.huber_a, L);
-            const int colc = P.img_colc[img], coli = P.img_coli[img];
+            linearize<true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
+            const bool cam = crow_valid(cd, cs);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 double m = 0.0;  // J_s step, step = -y
-                if (colc >= 0)
+                if (cam)
 #pragma unroll
-                    for (int a = 0; a < 6; ++a) m -= L.Jc[r][a] * P.scaleF[colc + a] * P.yF[colc + a];
+                    for (int a = 0; a < 6; ++a) m -= L.Jc[r][a] * csy[cs][a] * csy[cs][6 + a];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) m -= L.Ji[r][a] * P.scaleF[coli + a] * P.yF[coli + a];
+                for (int a = 0; a < 4; ++a) m -= L.Ji[r][a] * isy[is][8 + a] * isy[is][12 + a];
 #pragma unroll
                 for (int a = 0; a < 3; ++a) m -= L.Jx[r][a] * sE[a] * yE[a];
                 acc[0] += m * (L.f[r] + m / 2.0);
             }
             Lin C;
-            linearize<false, false, false>(cps_c[img], intr_c + 4 * P.img_intr[img], xc, P.obs_uv[2 * o],
-                                           P.obs_uv[2 * o + 1], P.huber_a, C);
+            linearize<false, false, false>(scc[cs], &isy[is][4], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;
             if (!C.ok) cbad = 1.0;
         }
@@ -1103,19 +1131,18 @@ __global__ __launch_bounds__(256) void step_kernel(DevProblem P, const CamPre* _
     wave_sum(acc);
     bad = wave_max(bad);
     cbad = wave_max(cbad);
-    __shared__ double red[4][kPartT];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ double red[kChunkPts / 64][kPartT];
+    const int wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
     if (lane == 0) {
         red[wave][0] = acc[0]; red[wave][1] = acc[1]; red[wave][2] = acc[2];
         red[wave][3] = bad; red[wave][4] = cbad;
     }
     __syncthreads();
-    if (threadIdx.x < 3)
-        P.part_t[kPartT * (size_t)blockIdx.x + threadIdx.x] =
-            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (threadIdx.x >= 3 && threadIdx.x < kPartT)
-        P.part_t[kPartT * (size_t)blockIdx.x + threadIdx.x] =
-            fmax(fmax(red[0][threadIdx.x], red[1][threadIdx.x]), fmax(red[2][threadIdx.x], red[3][threadIdx.x]));
+    if (tid < kPartT) {
+        double v = red[0][tid];
+        for (int w = 1; w < nw; ++w) v = tid < 3 ? v + red[w][tid] : fmax(v, red[w][tid]);
+        P.part_t[kPartT * (size_t)c + tid] = v;
+    }
 }
 
 // fixed-order reduction of the per-block partials
@@ -1240,13 +1267,13 @@ void ba_fvec(const DevProblem& P, const double* extr, const double* intr, double
     SFM_HIP(hipGetLastError());
 }
 
-int ba_step_blocks(const DevProblem& P) { return (P.n_spt + 255) / 256; }
+int ba_step_blocks(const DevProblem& P) { return P.n_chunk; }
 
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
     const int nb = ba_step_blocks(P);
     if (nb <= 0) return;
-    hipLaunchKernelGGL(step_kernel, dim3(nb), dim3(256), 0, s, P, cp, intr, cp_cand, intr_cand, X, X_cand,
+    hipLaunchKernelGGL(step_kernel, dim3(nb), dim3(kChunkPts), 0, s, P, cp, intr, cp_cand, intr_cand, X, X_cand,
                        radius);
     SFM_HIP(hipGetLastError());
 }

@@ -148,7 +148,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // MFMA work per point; it is used unless it would need many more chunks.
     // 128 points per chunk: ~2x the co-resident waves of the chip at C4 size,
     // so the last round of chunks is short (256 measured 17% slower).
-    int chunk_pts = kChunkPts / 2;   // tuning override (diagnostics)
+    int chunk_pts = kChunkPts;   // tuning override (diagnostics)
     if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));
     auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, std::vector<int32_t>& slot_out) -> int64_t {
         int64_t flops = 0;

@@ -23,7 +23,7 @@ constexpr int kTileRowsUsed = 76;         // rows 0..75 for F blocks
 constexpr int kTileWRow = 79;             // row carrying w = L^-1 g_E
 constexpr int kSubPts = 6;                // points per wave batch (3 panel columns each)
 constexpr int kSubObs = 64;               // observations per wave batch (one per lane)
-constexpr int kChunkPts = 256;            // points per chunk (upper bound)
+constexpr int kChunkPts = 128;            // points per chunk (upper bound; step_kernel threads)
 constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
 constexpr int kCamSlots = 16;             // staged cameras per chunk (incl. constant images)

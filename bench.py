@@ -117,6 +117,26 @@ def cpu_baseline_match(desc, n_kp, pairs, n_pairs=24, threads=1):
             "sample": f"first {n_pairs} pairs of C3, exact integer brute force, {dt:.1f} s wall"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
+    summary of this configuration (profiles/r*/pmc_summary.json, written by
+    tools/pmc_summary.py: FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE).
+    None when no summary is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "profiles", "r*", "pmc_summary.json")))
+    if not files:
+        return None
+    try:
+        ks = json.load(open(files[-1]))["kernels"]
+    except Exception:
+        return None
+    for name, e in ks.items():
+        if name.startswith(kernel) and "traffic_bytes" in e:
+            return e["traffic_bytes"]
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,7 +239,8 @@ def main():
                                         f"{len(pairs)} exhaustive pairs"},
                  "dtype": "u8 (i8 MFMA, i32 accumulate: exact)",
                  "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
-                              "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS, "traffic": None,
+                              "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS,
+                              "traffic": pmc_traffic("match_top2_kernel"),
                               "kernel": "match_top2_kernel",
                               "per_launch_ms": kms / max(kl, 1)},
                  "digest": mplan.digest()}
@@ -253,7 +274,8 @@ def main():
             "lm_iterations_per_solve": summ.iterations,
             "rmse_initial": summ.rmse_initial, "rmse_final": summ.rmse_final,
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TF,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TF, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TF,
+                         "traffic": pmc_traffic("schur_kernel"),
                          "kernel": "schur_kernel", "per_launch_ms": schur_avg_ms,
                          "algorithmic_flops_per_launch": flops},
             "cpu_baseline": cpu,
