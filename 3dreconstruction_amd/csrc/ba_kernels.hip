@@ -24,6 +24,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "ba_kernels.h"
 #include "common.h"
@@ -354,7 +355,6 @@ __global__ void fscale_kernel(DevProblem P) {
 // No block barriers: co-resident waves overlap each other's VALU and MFMA
 // phases.  Every sum has a fixed order, so results are bit-reproducible.
 // ---------------------------------------------------------------------------
-constexpr int kPanelK = 4 * ((3 * kSubPts + 3) / 4);  // 3 columns per point, padded to the MFMA k
 
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
@@ -374,9 +374,10 @@ __device__ __forceinline__ void stage_campre(const ChunkDesc& cd, const CamPre* 
 
 // next wave batch from p0: <= kSubPts points and <= kSubObs observations
 // (cpoff = chunk-relative point offsets in LDS); returns its point count
+template <int SP = kSubPts, int SO = kSubObs>
 __device__ __forceinline__ int batch_points(const int* cpoff, int p0, int np) {
     const int lane = threadIdx.x & 63, q1 = p0 + 1 + lane;
-    const bool fits = lane < kSubPts && q1 <= np && cpoff[q1] - cpoff[p0] <= kSubObs;
+    const bool fits = lane < SP && q1 <= np && cpoff[q1] - cpoff[p0] <= SO;
     return __builtin_ctzll(~__ballot(fits));
 }
 
@@ -389,7 +390,9 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 
 // NT = 5: rows 0..75 F blocks, row 79 = w, so -Z w comes out of the MFMA.
 // NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
-template <int NT>
+// SP / SO: points / observations per wave batch.  The panel holds 3 columns
+// per point padded to the MFMA k of 4 and NT*16 rows (NT = 4 keeps w apart).
+template <int NT, int SP = kSubPts, int SO = kSubObs>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
@@ -401,12 +404,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         tacc[k] += tn_ - tprev;                           \
         tprev = tn_;                                      \
     }
-    __shared__ double panel[kPanelK][kTileR];   // [k][row]
-    __shared__ double ob[kSubObs][12];          // Jx 6 | f 2 | J_intr 4 ; then M 6
-    __shared__ double li[kSubPts][6];           // L^-1 (lower, packed)
-    __shared__ double vb[kSubPts][9];           // V (packed lower) | g_E per point
-    __shared__ double xb[kSubPts][6];           // X | scaleE of the batch's points
-    __shared__ int orow[kSubObs];               // tile row of the obs' intrinsics block
+    constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT;
+    __shared__ double panel[kPK][kPR];          // [k][row]
+    __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
+    __shared__ double ob[SO][12];               // Jx 6 | f 2 | J_intr 4 ; then M 6
+    __shared__ double li[SP][6];                // L^-1 (lower, packed)
+    __shared__ double vb[SP][9];                // V (packed lower) | g_E per point
+    __shared__ double xb[SP][6];                // X | scaleE of the batch's points
+    __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
     __shared__ CamPre scp[kCamSlots];
     __shared__ double csc[kCamSlots][6];        // camera column scales (0: constant image)
@@ -442,11 +447,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     double xn2 = 0.0, gmx = 0.0;
     __syncthreads();
     for (int p0 = 0; p0 < np;) {
-        const int npts = batch_points(cpoff, p0, np);   // batch [p0, p1)
+        const int npts = batch_points<SP, SO>(cpoff, p0, np);   // batch [p0, p1)
         const int p1 = p0 + npts;
         const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
 #pragma unroll
-        for (int e = lane; e < kPanelK * kTileR / 2; e += 64)
+        for (int e = lane; e < kPK * kPR / 2; e += 64)
             reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
         if (lane < 6 * npts) {
             const int pt = lane / 6, k = lane - 6 * pt;
@@ -461,7 +466,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
             u0 = uv.x; u1 = uv.y;
 #pragma unroll
-            for (int j = 1; j < kSubPts; ++j) pl += (j < npts && cpoff[p0 + j] - o0 <= lane) ? 1 : 0;
+            for (int j = 1; j < SP; ++j) pl += (j < npts && cpoff[p0 + j] - o0 <= lane) ? 1 : 0;
         }
         __syncthreads();
         SFM_STAMP(0)
@@ -538,9 +543,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             const double i20 = -(l20 * i00 + l21 * i10) * i22;
             li[lane][0] = i00; li[lane][1] = i10; li[lane][2] = i11;
             li[lane][3] = i20; li[lane][4] = i21; li[lane][5] = i22;
-            panel[3 * lane + 0][kTileWRow] = i00 * b[0];
-            panel[3 * lane + 1][kTileWRow] = i10 * b[0] + i11 * b[1];
-            panel[3 * lane + 2][kTileWRow] = i20 * b[0] + i21 * b[1] + i22 * b[2];
+            const double w3[3] = {i00 * b[0], i10 * b[0] + i11 * b[1], i20 * b[0] + i21 * b[1] + i22 * b[2]};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                if (NT == 5) panel[3 * lane + a][kTileWRow % kPR] = w3[a];
+                else wcol[3 * lane + a] = w3[a];
+            }
         }
         __syncthreads();
         SFM_STAMP(2)
@@ -598,7 +606,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         // ---- D: tile += panel panel' on the fp64 MFMA -------------------------
         // all operands first (padding columns are zero), then the MFMAs
         const int kk = lane >> 4, ii = lane & 15;
-        constexpr int kKs = kPanelK / 4;
+        constexpr int kKs = kPK / 4;
         double op[kKs][NT];
 #pragma unroll
         for (int ks = 0; ks < kKs; ++ks)
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             for (int q = 0; q < kNTiles; ++q)
                 acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ks][kTi[q]], op[ks][kTj[q]], acc[q], 0, 0, 0);
         if (NT == 4)
-            for (int k = 0; k < 3 * npts; ++k) wacc += panel[k][lane] * panel[k][kTileWRow];
+            for (int k = 0; k < 3 * npts; ++k) wacc += panel[k][lane] * wcol[k];
         __syncthreads();
         SFM_STAMP(4)
         p0 = p1;
@@ -1215,8 +1223,10 @@ void ba_fscale(const DevProblem& P, hipStream_t s) {
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
               hipStream_t s, unsigned long long* stamps) {
     if (P.n_chunk <= 0) return;
+    // 64-row tiles: 4-point batches (12 panel columns, no k padding) keep LDS
+    // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
     if (P.tile_nt == 4)
-        hipLaunchKernelGGL(schur_kernel<4>, dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
+        hipLaunchKernelGGL((schur_kernel<4, 4, 48>), dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
     else
         hipLaunchKernelGGL(schur_kernel<5>, dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
     SFM_HIP(hipGetLastError());

@@ -26,7 +26,7 @@ constexpr int kSubObs = 64;               // observations per wave batch (one pe
 constexpr int kChunkPts = 128;            // points per chunk (upper bound; step_kernel threads)
 constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
-constexpr int kCamSlots = 16;             // staged cameras per chunk (incl. constant images)
+constexpr int kCamSlots = 14;             // staged cameras per chunk (incl. constant images)
 constexpr int kIntrSlots = 4;             // staged intrinsics blocks per chunk
 
 // Per-camera precomputed rotation terms (for current or candidate params).
