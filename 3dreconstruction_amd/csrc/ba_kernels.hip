@@ -448,6 +448,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     __syncthreads();
     for (int p0 = 0; p0 < np;) {
         const int npts = batch_points<SP, SO>(cpoff, p0, np);   // batch [p0, p1)
+        if (npts == 0) break;   // a point above SO observations: excluded by the planner
         const int p1 = p0 + npts;
         const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
 #pragma unroll

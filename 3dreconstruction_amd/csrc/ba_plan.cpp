@@ -240,8 +240,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         if (pl.n_spt > 0) close((int32_t)pl.n_spt);
         return flops;
     };
-    int max_own = 0;
+    int max_own = 0, max_obs = 0;
     for (int64_t k = 0; k < pl.n_spt; ++k) {
+        max_obs = std::max(max_obs, pl.pt_off[k + 1] - pl.pt_off[k]);
         int nc = 0;
         std::vector<int> pi;
         for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
@@ -253,7 +254,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     }
     int64_t flops = 0;
     pl.tile_nt = 5;
-    if (max_own <= 64 && !std::getenv("SFM_BA_TILE80")) {
+    // the 64-row kernel walks 48-observation batches (ba_kernels.hip)
+    if (max_own <= 64 && max_obs <= 48 && !std::getenv("SFM_BA_TILE80")) {
         std::vector<ChunkDesc> c4;
         std::vector<int32_t> s4;
         const int64_t f4 = make_chunks(64, c4, s4);
