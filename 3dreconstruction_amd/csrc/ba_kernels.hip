@@ -407,10 +407,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT;
     __shared__ double panel[kPK][kPR];          // [k][row]
     __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
-    __shared__ double ob[SO][12];               // Jx 6 | f 2 | J_intr 4 ; then M 6
-    __shared__ double li[SP][6];                // L^-1 (lower, packed)
-    __shared__ double vb[SP][9];                // V (packed lower) | g_E per point
-    __shared__ double xb[SP][6];                // X | scaleE of the batch's points
+    __shared__ double ob[SO][12];               // Jx 6 | f 2 | J_intr 4
+    __shared__ double obm[SO][6];               // M = Jx L^-T
     __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
     __shared__ CamPre scp[kCamSlots];
@@ -454,13 +452,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int e = lane; e < kPK * kPR / 2; e += 64)
             reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
-        if (lane < 6 * npts) {
-            const int pt = lane / 6, k = lane - 6 * pt;
-            const size_t g = 3 * (size_t)(pb + p0 + pt) + (k % 3);
-            xb[pt][k] = k < 3 ? X[g] : P.scaleE[g];
-        }
         int slot = 0, pl = 0;
-        double u0 = 0.0, u1 = 0.0;
+        double u0 = 0.0, u1 = 0.0, Xp[3] = {0.0, 0.0, 0.0}, sE[3] = {1.0, 1.0, 1.0};
         if (lane < nobs) {
             const int o = ob0 + o0 + lane;
             slot = P.obs_slot[o];
@@ -468,21 +461,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             u0 = uv.x; u1 = uv.y;
 #pragma unroll
             for (int j = 1; j < SP; ++j) pl += (j < npts && cpoff[p0 + j] - o0 <= lane) ? 1 : 0;
+            const size_t g = 3 * (size_t)(pb + p0 + pl);   // same address for the point's lanes
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { Xp[k] = X[g + k]; sE[k] = P.scaleE[g + k]; }
         }
-        __syncthreads();
         SFM_STAMP(0)
         // ---- A: observations -> scaled, corrected Jacobians -----------------
         Lin L;
         const int cs = slot & 255, is = (slot >> 8) & 255;
         if (lane < nobs) {
-            const double Xp[3] = {xb[pl][0], xb[pl][1], xb[pl][2]};
             linearize<true, true, true>(scp[cs], &isc[is][0], Xp, u0, u1, P.huber_a, L);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
 #pragma unroll
                 for (int a = 0; a < 6; ++a) L.Jc[r][a] *= csc[cs][a];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) L.Jx[r][a] *= xb[pl][3 + a];
+                for (int a = 0; a < 3; ++a) L.Jx[r][a] *= sE[a];
             }
 #pragma unroll
             for (int r = 0; r < 2; ++r)
@@ -499,35 +493,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
         __syncthreads();
         SFM_STAMP(1)
-        // ---- B1: lane (point, component): V00 V10 V11 V20 V21 V22 | g0 g1 g2 ------
-        // (each sum in observation-then-row order)
-        if (lane < 9 * npts) {
-            const int pt = lane / 9, cmp = lane - 9 * pt;
-            const int ia = cmp < 6 ? (cmp >= 3 ? 2 : (cmp >= 1 ? 1 : 0)) : cmp - 6;
-            const int ib = cmp < 6 ? cmp - (ia * (ia + 1)) / 2 : 3;
-            double v = 0.0;
-            for (int q = cpoff[p0 + pt] - o0; q < cpoff[p0 + pt + 1] - o0; ++q) {
+        // ---- B: every observation lane forms its point's V + D^2 and g_E (sum
+        // in observation-then-row order: identical on all lanes of the point),
+        // factors it, and goes on to M = Jx L^-T and the camera rows of Z ----
+        if (lane < nobs) {
+            const int q0 = cpoff[p0 + pl] - o0, q1 = cpoff[p0 + pl + 1] - o0;
+            double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};  // V00 V10 V11 V20 V21 V22
+            for (int q = q0; q < q1; ++q) {
 #pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    v += ob[q][3 * r + ia] * (ib < 3 ? ob[q][3 * r + ib] : ob[q][6 + r]);
+                for (int r = 0; r < 2; ++r) {
+                    const double j0 = ob[q][3 * r], j1 = ob[q][3 * r + 1], j2 = ob[q][3 * r + 2];
+                    const double fr = ob[q][6 + r];
+                    V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
+                    V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
+                    b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
+                }
             }
-            vb[pt][cmp] = v;
-        }
-        __syncthreads();
-        // ---- B2: per point V + D^2, Cholesky, w = L^-1 g_E --------------------
-        if (lane < npts) {
-            double V[6], b[3];
+            const bool first = lane == q0;
+            if (first) {   // gradient / norm bookkeeping at x (used after a relinearisation)
 #pragma unroll
-            for (int k = 0; k < 6; ++k) V[k] = vb[lane][k];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) b[k] = vb[lane][6 + k];
-            // gradient / norm bookkeeping at x (used after a relinearisation)
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const double xv = xb[lane][a];
-                const double g = b[a] / xb[lane][3 + a];
-                xn2 += xv * xv;
-                gmx = fmax(gmx, fabs(xv - (xv - g)));
+                for (int a = 0; a < 3; ++a) {
+                    const double g = b[a] / sE[a];
+                    xn2 += Xp[a] * Xp[a];
+                    gmx = fmax(gmx, fabs(Xp[a] - (Xp[a] - g)));
+                }
             }
             const int di[3] = {0, 2, 5};
 #pragma unroll
@@ -542,21 +531,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             const double i22 = rsqrt_nr(V[5] - l20 * l20 - l21 * l21);
             const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
             const double i20 = -(l20 * i00 + l21 * i10) * i22;
-            li[lane][0] = i00; li[lane][1] = i10; li[lane][2] = i11;
-            li[lane][3] = i20; li[lane][4] = i21; li[lane][5] = i22;
-            const double w3[3] = {i00 * b[0], i10 * b[0] + i11 * b[1], i20 * b[0] + i21 * b[1] + i22 * b[2]};
+            if (first) {
+                const double w3[3] = {i00 * b[0], i10 * b[0] + i11 * b[1], i20 * b[0] + i21 * b[1] + i22 * b[2]};
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                if (NT == 5) panel[3 * lane + a][kTileWRow % kPR] = w3[a];
-                else wcol[3 * lane + a] = w3[a];
+                for (int a = 0; a < 3; ++a) {
+                    if (NT == 5) panel[3 * pl + a][kTileWRow % kPR] = w3[a];
+                    else wcol[3 * pl + a] = w3[a];
+                }
             }
-        }
-        __syncthreads();
-        SFM_STAMP(2)
-        // ---- C: M = Jx L^-T; camera rows of Z = J_c' M ------------------------
-        if (lane < nobs) {
-            const double i00 = li[pl][0], i10 = li[pl][1], i11 = li[pl][2];
-            const double i20 = li[pl][3], i21 = li[pl][4], i22 = li[pl][5];
             double M[2][3];
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
@@ -575,9 +557,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
             for (int r = 0; r < 2; ++r)
 #pragma unroll
-                for (int a = 0; a < 3; ++a) ob[lane][3 * r + a] = M[r][a];
+                for (int a = 0; a < 3; ++a) obm[lane][3 * r + a] = M[r][a];
         }
         __syncthreads();
+        SFM_STAMP(2)
         // ---- C2: intrinsics rows, ordered per point ---------------------------
         // (register sums per run of observations sharing an intrinsics block)
         if (lane < 3 * npts) {
@@ -593,7 +576,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                     z0 = z1 = z2 = z3 = 0.0;
                     row = rq;
                 }
-                const double m0 = ob[q][a], m1 = ob[q][3 + a];
+                const double m0 = obm[q][a], m1 = obm[q][3 + a];
                 z0 += ob[q][8] * m0;
                 z1 += ob[q][9] * m1;
                 z2 += ob[q][10] * m0;
