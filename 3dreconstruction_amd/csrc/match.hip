@@ -39,6 +39,7 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int kQB = 256;   // queries per workgroup (4 waves x 64)
 constexpr int kRowPad = 256;  // rows of every image padded to this multiple
+constexpr int kStage = 128;   // database rows per LDS stage (kRowPad multiple of it)
 
 // u8 -> int8 (a ^ 0x80 == a - 128), per-row |a'|^2 and the packed key base.
 __global__ void prep_kernel(uint8_t* __restrict__ d, int32_t* __restrict__ nrm,
@@ -112,7 +113,7 @@ struct MatchArgs {
     int32_t* out_d;            // [n_pairs][out_stride]
 };
 
-__global__ __launch_bounds__(256, 2) void match_top2_kernel(MatchArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void match_top2_kernel(MatchArgs a) {
     // XCD-aware bijective remap of the flat workgroup id (guide §5 T1):
     // blocks b and b+8 share an XCD, so give each XCD a contiguous range of
     // work items (pair-major, query block minor).
@@ -147,28 +148,55 @@ __global__ __launch_bounds__(256, 2) void match_top2_kernel(MatchArgs a) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) { g[t].g1v = INT_MAX; g[t].g1i = -1; g[t].g2v = INT_MAX; }
 
+    // Database rows are staged once per workgroup through LDS (double-buffered
+    // kStage-row stages filled by global_load_lds, 16 B per lane), instead of
+    // every wave loading its fragments from L2.  The LDS image is lane-linear;
+    // bank conflicts of the 32-rows-one-chunk fragment reads are removed by
+    // storing logical 16-byte chunk k of row r at slot k ^ (r & 7) (the XOR is
+    // applied to the global SOURCE address, and again on the read).
+    __shared__ __attribute__((aligned(16))) int8_t sA[2][kStage * 128];
+    __shared__ __attribute__((aligned(16))) int32_t sN[2][kStage];
+    auto issue = [&](int buf, int row_base) {
+#pragma unroll
+        for (int q = 0; q < kStage * 8 / 256; ++q) {
+            const int L = q * 256 + wave * 64 + lane;          // 16-byte slot in the stage
+            const int r = L >> 3, k = (L & 7) ^ (r & 7);
+            const int8_t* src = a.desc + (db_row0 + row_base + r) * 128 + k * 16;
+            __builtin_amdgcn_global_load_lds(src, &sA[buf][(q * 256 + wave * 64) * 16], 16, 0, 0);
+        }
+        if (wave == 0) {
+#pragma unroll
+            for (int q = 0; q < kStage / 64; ++q)
+                __builtin_amdgcn_global_load_lds(a.ntr + db_row0 + row_base + q * 64 + lane, &sN[buf][q * 64], 4, 0, 0);
+        }
+    };
+
     const int n_db_pad = (n_db + kRowPad - 1) / kRowPad * kRowPad;
-    for (int sup = 0; sup < n_db_pad; sup += 256) {
-        int b1[2] = {INT_MAX, INT_MAX}, b2[2] = {INT_MAX, INT_MAX};
-#pragma unroll 2
-        for (int tile = 0; tile < 256; tile += 32) {
-            const int64_t row = db_row0 + sup + tile;
-            const v4i* src = reinterpret_cast<const v4i*>(a.desc + (row + c) * 128 + 64 * h);
+    int b1[2] = {INT_MAX, INT_MAX}, b2[2] = {INT_MAX, INT_MAX};
+    if (n_db_pad > 0) issue(0, 0);
+    for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
+        __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
+        if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
+        const int8_t* A = sA[st & 1];
+        const int32_t* N = sN[st & 1];
+#pragma unroll 1
+        for (int tile = 0; tile < kStage; tile += 32) {
+            const int r = tile + c;
             v4i af[4];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) af[s] = src[s];
+            for (int s4 = 0; s4 < 4; ++s4)
+                af[s4] = *reinterpret_cast<const v4i*>(A + r * 128 + (((4 * h + s4) ^ (r & 7)) << 4));
             // packed key bases of this lane's 16 rows: rows (j&3) + 8(j>>2) + 4h
-            const v4i* nsrc = reinterpret_cast<const v4i*>(a.ntr + row + 4 * h);
             v4i nt4[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) nt4[q] = nsrc[2 * q];
+            for (int q = 0; q < 4; ++q) nt4[q] = *reinterpret_cast<const v4i*>(N + tile + 4 * h + 8 * q);
             v16i acc0 = {}, acc1 = {};
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[0][s], acc0, 0, 0, 0);
+            for (int s4 = 0; s4 < 4; ++s4)
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[0][s4], acc0, 0, 0, 0);
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s], bq[1][s], acc1, 0, 0, 0);
+            for (int s4 = 0; s4 < 4; ++s4)
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[1][s4], acc1, 0, 0, 0);
             // epilogue for both column tiles, interleaved for ILP:
             // key = nt - 512*dot (v_mad_i32_i24; |dot| < 2^21 fits 24 bits; the
             // multiplier is a kernel argument so it is not strength-reduced),
@@ -187,8 +215,13 @@ __global__ __launch_bounds__(256, 2) void match_top2_kernel(MatchArgs a) {
                     : "v"(k0), "v"(k1));
             }
         }
+        if (((sup + kStage) & 255) == 0) {   // keys carry row & 255: merge every 256 rows
 #pragma unroll
-        for (int t = 0; t < 2; ++t) merge_tile(g[t], b1[t], b2[t], sup);
+            for (int t = 0; t < 2; ++t) {
+                merge_tile(g[t], b1[t], b2[t], sup + kStage - 256);
+                b1[t] = INT_MAX; b2[t] = INT_MAX;
+            }
+        }
     }
 
 #pragma unroll
