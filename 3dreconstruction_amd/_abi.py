@@ -164,7 +164,7 @@ def load(path=None):
         import torch  # noqa: F401  (shares libamdhip64.so.7 / librccl.so.1)
     except Exception:
         pass
-    p = path or LIB_PATH
+    p = path or os.environ.get("SFMCORE_LIB") or LIB_PATH   # override: A/B of library builds
     if not os.path.exists(p):
         raise RuntimeError(f"libsfmcore.so not built: {p} (run __graft_entry__.build())")
     lib = C.CDLL(p, mode=C.RTLD_GLOBAL)

@@ -40,6 +40,12 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kQB = 256;   // queries per workgroup (4 waves x 64)
 constexpr int kRowPad = 256;  // rows of every image padded to this multiple
 constexpr int kStage = 128;   // database rows per LDS stage (kRowPad multiple of it)
+#ifndef MATCH_TILE_UNROLL
+#define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
+#endif
+#ifndef MATCH_WAVES_PER_EU
+#define MATCH_WAVES_PER_EU 4           // waves per SIMD the register budget targets
+#endif
 
 // u8 -> int8 (a ^ 0x80 == a - 128), per-row |a'|^2 and the packed key base.
 __global__ void prep_kernel(uint8_t* __restrict__ d, int32_t* __restrict__ nrm,
@@ -113,7 +119,7 @@ struct MatchArgs {
     int32_t* out_d;            // [n_pairs][out_stride]
 };
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void match_top2_kernel(MatchArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES_PER_EU, MATCH_WAVES_PER_EU))) void match_top2_kernel(MatchArgs a) {
     // XCD-aware bijective remap of the flat workgroup id (guide §5 T1):
     // blocks b and b+8 share an XCD, so give each XCD a contiguous range of
     // work items (pair-major, query block minor).
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
         const int8_t* A = sA[st & 1];
         const int32_t* N = sN[st & 1];
-#pragma unroll 1
+#pragma unroll MATCH_TILE_UNROLL
         for (int tile = 0; tile < kStage; tile += 32) {
             const int r = tile + c;
             v4i af[4];
