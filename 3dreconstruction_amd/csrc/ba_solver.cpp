@@ -46,9 +46,9 @@ struct sfm_ba_plan {
     DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
         part_t, scal, bcr_buf;
     DBuf<int32_t> long_targets;
-    DBuf<double> lpart;
-    DBuf<int32_t> img_pt;
-    DBuf<double> img_uv;          // long-target segment partials [n_lseg][36]
+    DBuf<double> lpart;           // long-target segment partials [n_lseg][36]
+    DBuf<int32_t> img_pt;         // image-ordered observations (image Gram pass)
+    DBuf<double> img_uv;
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
     BcrArgs bcr;
     bool use_bcr = false;
