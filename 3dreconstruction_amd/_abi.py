@@ -37,7 +37,12 @@ f64p = C.POINTER(C.c_double)
 
 class CtxOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
-                ("reserved", C.c_int32), ("comm_id", u8p)]
+                ("reserved", C.c_int32), ("comm_id", u8p),
+                ("allreduce", C.c_void_p), ("allreduce_user", C.c_void_p)]
+
+
+# int32_t (*)(void* user, double* buf, int64_t n, int32_t op)
+ALLREDUCE_HOOK = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32)
 
 
 class BAProblem(C.Structure):

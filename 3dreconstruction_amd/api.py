@@ -25,16 +25,33 @@ def _check(rc, where):
 
 
 class Context:
-    """sfm_ctx: one HIP device (+ RCCL communicator when world_size > 1)."""
+    """sfm_ctx: one HIP device (+ RCCL communicator when world_size > 1).
 
-    def __init__(self, device=0, rank=0, world_size=1, comm_id=None):
+    allreduce: optional callable (numpy float64 array, op) -> None reducing the
+    array in place across ranks (op 0 sum, 1 max); replaces RCCL, e.g. with a
+    torch.distributed gloo group."""
+
+    def __init__(self, device=0, rank=0, world_size=1, comm_id=None, allreduce=None):
         self.lib = abi.load()
         o = abi.CtxOpts()
         o.device, o.rank, o.world_size = device, rank, world_size
         self._id = None
+        self._hook = None
         if comm_id is not None:
             self._id = (C.c_uint8 * 128).from_buffer_copy(bytes(comm_id))
             o.comm_id = C.cast(self._id, abi.u8p)
+        if allreduce is not None:
+            import numpy as np
+
+            def hook(user, buf, n, op):
+                try:
+                    allreduce(np.ctypeslib.as_array(buf, shape=(n,)), int(op))
+                    return 0
+                except Exception:
+                    return -1
+
+            self._hook = abi.ALLREDUCE_HOOK(hook)
+            o.allreduce = C.cast(self._hook, C.c_void_p)
         h = C.c_void_p()
         _check(self.lib.sfm_ctx_create(C.byref(o), C.byref(h)), "sfm_ctx_create")
         self.h = h

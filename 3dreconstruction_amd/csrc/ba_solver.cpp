@@ -224,7 +224,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     SFM_HIP(hipMemcpyAsync(S.in, pl->intr0.p, ni * 8, hipMemcpyDeviceToDevice, s));
 
     auto allreduce_rcs = [&] {
-        if (ctx->world > 1) rccl_allreduce_f64(ctx->comm, pl->rcs.p, pl->rcs_n, 0, s);
+        ctx_allreduce(ctx, pl->rcs.p, pl->rcs_n, 0, s);
     };
     auto relinearize = [&] {
         ba_image_gram(P, S.cp, S.in, S.X, s);
@@ -285,8 +285,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         ba_finalize(P, s);
         if (ctx->world > 1) {
-            rccl_allreduce_f64(ctx->comm, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);
-            rccl_allreduce_f64(ctx->comm, P.scal + kScMaxBegin, kScMaxEnd - kScMaxBegin, 1, s);
+            ctx_allreduce(ctx, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);
+            ctx_allreduce(ctx, P.scal + kScMaxBegin, kScMaxEnd - kScMaxBegin, 1, s);
         }
         SFM_HIP(hipMemcpyAsync(pl->scal_h, P.scal, kScCount * 8, hipMemcpyDeviceToHost, s));
         SFM_HIP(hipStreamSynchronize(s));

@@ -57,6 +57,9 @@ int guarded(F&& body) {
 struct Rccl;
 const Rccl* rccl();  // throws SFM_ERR_COMM if unavailable
 int rccl_allreduce_f64(void* comm, double* buf, size_t n, int op_max, hipStream_t s);
+// All-reduce of a device buffer across the context's ranks (RCCL, or the
+// host hook through pinned memory); no-op at world 1.
+void ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStream_t s);
 int rccl_comm_init(void** comm, int world, const uint8_t* id128, int rank);
 void rccl_comm_destroy(void* comm);
 
@@ -100,6 +103,10 @@ struct sfm_ctx {
     int rank = 0;
     int world = 1;
     hipStream_t stream = nullptr;
-    void* comm = nullptr;  // ncclComm_t when world > 1
+    void* comm = nullptr;  // ncclComm_t when world > 1 (RCCL path)
+    sfm_allreduce_fn host_allreduce = nullptr;   // host-staged path instead of RCCL
+    void* host_allreduce_user = nullptr;
+    double* host_buf = nullptr;                  // pinned staging for host_allreduce
+    size_t host_cap = 0;
     int cu_count = 0;
 };

@@ -81,6 +81,27 @@ extern "C" const char* sfm_version(void) { return "sfmcore 0.1.0 (gfx950)"; }
 
 extern "C" const char* sfm_last_error(void) { return g_err.c_str(); }
 
+void sfm::ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStream_t s) {
+    if (ctx->world <= 1 || n == 0) return;
+    if (!ctx->host_allreduce) {
+        SFM_REQUIRE(rccl_allreduce_f64(ctx->comm, dev_buf, n, op_max, s) == 0, SFM_ERR_COMM,
+                    "RCCL all-reduce failed");
+        return;
+    }
+    if (ctx->host_cap < n) {
+        if (ctx->host_buf) SFM_HIP(hipHostFree(ctx->host_buf));
+        ctx->host_buf = nullptr;
+        SFM_HIP(hipHostMalloc(&ctx->host_buf, n * sizeof(double)));
+        ctx->host_cap = n;
+    }
+    SFM_HIP(hipMemcpyAsync(ctx->host_buf, dev_buf, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
+    SFM_REQUIRE(ctx->host_allreduce(ctx->host_allreduce_user, ctx->host_buf, (int64_t)n, op_max) == 0,
+                SFM_ERR_COMM, "host all-reduce hook failed");
+    SFM_HIP(hipMemcpyAsync(dev_buf, ctx->host_buf, n * sizeof(double), hipMemcpyHostToDevice, s));
+    SFM_HIP(hipStreamSynchronize(s));   // the staging buffer is reused by the next exchange
+}
+
 extern "C" int sfm_comm_unique_id(uint8_t* out128) {
     return guarded([&] {
         SFM_REQUIRE(out128, SFM_ERR_INVALID_ARG, "null output");
@@ -117,8 +138,11 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         c->cu_count = prop.multiProcessorCount;
         SFM_HIP(hipSetDevice(c->device));
         SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        if (c->world > 1) {
-            SFM_REQUIRE(opts->comm_id, SFM_ERR_INVALID_ARG, "world_size>1 needs comm_id");
+        if (c->world > 1 && opts->allreduce && !opts->comm_id) {
+            c->host_allreduce = opts->allreduce;
+            c->host_allreduce_user = opts->allreduce_user;
+        } else if (c->world > 1) {
+            SFM_REQUIRE(opts->comm_id, SFM_ERR_INVALID_ARG, "world_size>1 needs comm_id or an allreduce hook");
             try {
                 rccl_comm_init(&c->comm, c->world, opts->comm_id, c->rank);
             } catch (...) {
@@ -138,6 +162,7 @@ extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
         (void)hipSetDevice(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         rccl_comm_destroy(ctx->comm);
+        if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
         if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
         return SFM_OK;

@@ -52,13 +52,23 @@ const char* sfm_last_error(void);
 /* ------------------------------------------------------------------------ */
 typedef struct sfm_ctx sfm_ctx;
 
+/* Host-side all-reduce hook: reduce buf[n] across all ranks in place,
+ * op 0 = sum, 1 = max; return 0 on success. */
+typedef int32_t (*sfm_allreduce_fn)(void* user, double* buf, int64_t n, int32_t op);
+
 typedef struct sfm_ctx_opts {
     int32_t device;          /* HIP device ordinal (local to the process)      */
     int32_t rank;            /* 0 .. world_size-1                              */
     int32_t world_size;      /* 1 = single GPU; >1 = landmark-sharded BA       */
     int32_t reserved;
     const uint8_t* comm_id;  /* 128-byte RCCL unique id from rank 0's
-                                sfm_comm_unique_id(); NULL when world_size==1 */
+                                sfm_comm_unique_id(); NULL when world_size==1
+                                or when `allreduce` is given                  */
+    sfm_allreduce_fn allreduce; /* optional (world_size > 1, comm_id NULL):
+                                the per-iteration exchanges are staged through
+                                pinned host memory and handed to this hook
+                                (MPI, gloo, ...) instead of RCCL over xGMI   */
+    void* allreduce_user;
 } sfm_ctx_opts;
 
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */

@@ -2,6 +2,7 @@
 (Ceres-semantics restatement): same accept/reject sequence, final cost /
 "RMSE" (BundleAdjuster.h:137-138) within 1e-6 relative, parameters close."""
 import importlib
+import os
 
 import numpy as np
 import pytest
@@ -191,3 +192,56 @@ def test_cpp_facade_drop_in():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "facade ok" in r.stdout
+
+
+# ---- landmark-sharded path on one GPU: two ranks, host all-reduce (gloo) ----
+def _shard_worker(rank, world, port, out_path, scene_args):
+    import sys as _s
+    _s.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    _s.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import importlib as _il
+    import torch
+    import torch.distributed as dist
+    import _helpers as H2
+    api2 = _il.import_module("3dreconstruction_amd.api")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allreduce(a, op):
+        dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM)
+
+    ctx2 = api2.Context(device=0, rank=rank, world_size=world, allreduce=allreduce)
+    sc = H2.Scene(**scene_args)
+    e, i, x = sc.params()
+    rc, s = api2.ba_solve(ctx2, sc.problem(), e, i, x)
+    order, bounds = api2.ba_partition(sc.problem(), world)
+    own = np.zeros(sc.n_pt, bool)
+    own[order[bounds[rank]:bounds[rank + 1]]] = True
+    xs = torch.from_numpy(np.where(own[:, None], x.reshape(-1, 3), 0.0).reshape(-1).copy())
+    dist.all_reduce(xs)
+    if rank == 0:
+        np.savez(out_path, rc=rc, it=s.iterations, cost=s.final_cost, init=s.initial_cost,
+                 e=e, i=i, x=xs.numpy())
+    dist.barrier()
+    ctx2.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scene_args", [dict(n_cam=16, n_pt=1200, k=4, seed=101),
+                                        dict(n_cam=40, n_pt=4000, k=10, seed=7)])
+def test_sharded_two_ranks_one_gpu(ctx, tmp_path, scene_args):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "r.npz")
+    port = 31500 + (os.getpid() % 2000)
+    mp.spawn(_shard_worker, args=(2, port, out, scene_args), nprocs=2, join=True)
+    r = np.load(out)
+    sc = H.Scene(**scene_args)
+    e, i, x = sc.params()
+    rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
+    assert int(r["rc"]) == rc == 0
+    assert abs(float(r["init"]) / gs.initial_cost - 1) < 1e-12
+    assert abs(int(r["it"]) - gs.iterations) <= 1
+    assert abs(float(r["cost"]) / gs.final_cost - 1) < 2e-6
+    np.testing.assert_allclose(r["e"], e, atol=2e-3)
+    np.testing.assert_allclose(r["x"], x, atol=5e-3 * (np.abs(x).max() + 1))
