@@ -18,6 +18,7 @@
 // keeps X = L^-1 explicitly, so every triangular solve is a product.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -115,10 +116,18 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Wave-local factor + inverse of one 16x16 diagonal tile: lane i < 16 owns
-// row i in registers, pivots and L columns are broadcast with v_readlane.
+// row i in registers.  Step k: the pivot comes from lane k (v_readlane), each
+// lane scales its column-k entry and publishes it in `col` (LDS); the rank-1
+// update reads column k back as same-address (broadcast) LDS loads.
 // L overwrites the lower tile (upper zeroed); X gets L^-1 (upper zeroed).
-__device__ void diag16(double* A, double* X, double* bad) {
+__device__ void diag16(double* A, double* X, double* bad, double* col) {
     const int lane = threadIdx.x & 63, i = lane;
     const bool act = lane < 16;
     double a[16], rinv[16];
@@ -131,23 +140,34 @@ __device__ void diag16(double* A, double* X, double* bad) {
         ok = ok && d > 0.0;
         rinv[k] = rsqrt_nr(d);
         a[k] = i == k ? d * rinv[k] : (i > k ? a[k] * rinv[k] : a[k]);
+        if (k < 15) {
+            if (act) col[i] = a[k];
+            wave_sync_lds();
+            double cv[16];
 #pragma unroll
-        for (int j = k + 1; j < 16; ++j) a[j] = fma(-a[k], rdlane(a[k], j), a[j]);
+            for (int j = k + 1; j < 16; ++j) cv[j] = col[j];
+#pragma unroll
+            for (int j = k + 1; j < 16; ++j) a[j] = fma(-a[k], cv[j], a[j]);
+            wave_sync_lds();
+        }
     }
     if (lane == 0 && !ok) bad[0] = 1.0;
-    // X = L^-1 by columns: lane c solves L x = e_c
+    if (act) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
+    }
+    wave_sync_lds();
+    // X = L^-1 by columns: lane c solves L x = e_c, rows of L read as broadcasts
     const int c = lane;
     double x[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         double t = (m == c) ? 1.0 : 0.0;
 #pragma unroll
-        for (int p = 0; p < m; ++p) t = fma(-rdlane(a[p], m), x[p], t);
+        for (int p = 0; p < m; ++p) t = fma(-A[m * LD + p], x[p], t);
         x[m] = t * rinv[m];
     }
     if (act) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
 #pragma unroll
         for (int m = 0; m < 16; ++m) X[m * LD + c] = x[m];
     }
@@ -155,11 +175,12 @@ __device__ void diag16(double* A, double* X, double* bad) {
 
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
 // the caller).  All 256 threads; ends synchronised.
-__device__ void chol_inv64(double* A, double* X, double* bad) {
+__device__ void chol_inv64(double* A, double* X, double* bad, double* col) {
     const int wave = threadIdx.x >> 6;
     for (int k = 0; k < 4; ++k) {
-        if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), bad);
+        if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), bad, col);
         __syncthreads();
+
         if (wave < 3 - k) {   // panel: L_ik = A_ik X_kk'
             const int i = k + 1 + wave;
             const v4d t = tile_mm<false, true, false>(zero4(), A, LD, 16 * i, X, LD, 16 * k, 16 * k, 16 * k + 16);
@@ -247,67 +268,17 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
     }
 }
 
-// ---- level l, step 1: factor every odd super-block, X_i = L_i^-1 --------------
-__global__ __launch_bounds__(NT) void bcr_factor_kernel(BcrArgs b, int s) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* A = sm;                 // [64][LD]
-    double* X = A + M * LD;         // [64][LD]
-    double* bad = X + M * LD;
-    const int i = s + 2 * s * blockIdx.x;   // odd at this level
-    if (i >= b.N) return;
-    if (threadIdx.x == 0) bad[0] = 0.0;
-    load_rows(A, LD, b.A + (size_t)i * M * M, M, M);
-    for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
-    __syncthreads();
-    chol_inv64(A, X, bad);
-    if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
-    double* Xg = b.L + (size_t)i * M * M;
-    for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
-}
-
-// ---- level l, step 2: Wl = X C_i, Wr = X C_r', z = X R_i, one workgroup per
-// (odd block, 16-column tile); wave v computes output tile row v ------------
-__global__ __launch_bounds__(NT) void bcr_wz_kernel(BcrArgs b, int s) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    constexpr int L16 = 17;
-    double* X = sm;                 // [64][LD]
-    double* Cl = X + M * LD;        // [64][17]  columns 16w.. of C_i = block (i, i-s)
-    double* Cr = Cl + M * L16;      // [16][LD]  rows 16w.. of C_r = block (r, i)
-    double* R = Cr + 16 * LD;       // [64][17]  columns 16w.. of R_i
-    const int i = s + 2 * s * (blockIdx.x >> 2), w = blockIdx.x & 3;
-    if (i >= b.N) return;
-    const int r = i + s, wave = threadIdx.x >> 6;
-    const bool hr = r < b.N, hz = 16 * w < b.nrhs;
-    load_rows(X, LD, b.L + (size_t)i * M * M, M, M);
-    load_rows(Cl, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
-    if (hr) load_tile<64, 16>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
-    if (hz) load_rows(R, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
-    __syncthreads();
-    const int kend = 16 * (wave + 1);   // X is lower triangular
-    tile_st(b.Wl + (size_t)i * M * M, M, 16 * wave, 16 * w,
-            tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Cl, L16, 0, 0, kend));
-    if (hr)   // op(B)[k][n] = C_r[16w + n][k]
-        tile_st(b.Wr + (size_t)i * M * M, M, 16 * wave, 16 * w,
-                tile_mm<false, true, false>(zero4(), X, LD, 16 * wave, Cr, LD, 0, 0, kend));
-    if (hz)
-        tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * wave, 16 * w,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, L16, 0, 0, kend));
-}
-
-// ---- level l, step 3: update every even super-block from its odd neighbours --
+// ---- update of one 16-row tile w of an even block j after eliminating its odd
+// neighbours at stride s (they hold Wl = L^-1 C, Wr = L^-1 C_r', z = L^-1 R):
 // A_j -= Wr_{j-s}' Wr_{j-s} + Wl_{j+s}' Wl_{j+s};  R_j -= Wr' z + Wl' z;
-// new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}.
-// One workgroup per (even block, 16-row tile w); wave v: output tile (w, v).
-__global__ __launch_bounds__(NT) void bcr_update_kernel(BcrArgs b, int s) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+// new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}.  Wave v: tile (w, v).
+__device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* sm) {
     const int ldr = b.nrhs + 1;
     double* Wa = sm;               // Wr_{j-s}
     double* Wb = Wa + M * LD;      // Wl_{j+s}
     double* Wc = Wb + M * LD;      // Wl_{j-s}
     double* Za = Wc + M * LD;      // z_{j-s}
     double* Zb = Za + M * ldr;     // z_{j+s}
-    const int j = 2 * s * (blockIdx.x >> 2), w = blockIdx.x & 3;
-    if (j >= b.N) return;
     const int il = j - s, ir = j + s, v = threadIdx.x >> 6;
     const bool hl = il >= 0, hr = ir < b.N, hc = hl && j - 2 * s >= 0;
     if (hl) {
@@ -339,6 +310,99 @@ __global__ __launch_bounds__(NT) void bcr_update_kernel(BcrArgs b, int s) {
                 tile_mm<true, false, true>(zero4(), Wa, LD, 16 * w, Wc, LD, 16 * v, 0, M));
 }
 
+// ---- one cyclic-reduction level at stride s, one launch --------------------------
+// Workgroups (item, w), w = 16-column / 16-row tile:
+//   odd block i (items < n_odd): bring A_i, column tile w of C_i (block (i, i-s)),
+//     row tile w of C_r (block (r, i), r = i+s) and column tile w of R_i up to
+//     date with the previous level (stride s/2) in LDS -- each of the block's 4
+//     workgroups does this redundantly -- factor A_i = L L', X = L^-1 (stored by
+//     w = 0 for the back substitution), and store column tile w of
+//     Wl = X C_i, Wr = X C_r', z = X R_i.
+//   even block j (items >= n_odd, s > 1): update(s/2) of its row tile w, stored.
+// At s = 1 the inputs come straight from bcr_pack.
+__global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_odd) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int item = blockIdx.x >> 2, w = blockIdx.x & 3, sp = s >> 1;
+    if (item >= n_odd) {
+        const int j = 2 * s * (item - n_odd);
+        if (sp > 0 && j < b.N) update_tile_rows(b, sp, j, w, sm);
+        return;
+    }
+    const int i = s + 2 * s * item;
+    if (i >= b.N) return;
+    const int r = i + s, wave = threadIdx.x >> 6;
+    const bool hr = r < b.N, hz = 16 * w < b.nrhs;
+    constexpr int L16 = 17;
+    double* A = sm;                 // [64][LD]
+    double* X = A + M * LD;         // [64][LD]
+    double* Wa = X + M * LD;        // [64][64] Wr_{i-sp}
+    double* Wb = Wa + M * M;        // [64][64] Wl_{i+sp}
+    double* Cc = Wb + M * M;        // [64][17] column tile w of C_i
+    double* Cr = Cc + M * L16;      // [16][LD] row tile w of C_r
+    double* Rc = Cr + 16 * LD;      // [64][17] column tile w of R_i
+    double* bad = Rc + M * L16;
+    double* col = bad + 2;          // [16] diag16 column broadcast
+    if (threadIdx.x == 0) bad[0] = 0.0;
+    load_rows(A, LD, b.A + (size_t)i * M * M, M, M);
+    load_rows(Cc, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
+    if (hr) load_tile<64, 16>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
+    if (hz) load_rows(Rc, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
+    if (sp > 0) {
+        // neighbours eliminated at stride sp: i-sp (always there) and i+sp
+        const int il = i - sp, ir = i + sp;
+        const bool hir = ir < b.N;
+        // column tile w of z_{i-sp}, z_{i+sp}, Wl_{i-sp} and of Wr_{i+sp}, staged in
+        // X's space (free until the factorisation)
+        double* Z1 = X;
+        double* Z2 = Z1 + M * 16;
+        double* WL = Z2 + M * 16;
+        double* WR = WL + M * 16;
+        load_tile<64, 64>(Wa, M, b.Wr + (size_t)il * M * M, M);
+        load_tile<16>(WL, 16, b.Wl + (size_t)il * M * M + 16 * w, M);
+        if (hz) load_tile<16>(Z1, 16, b.Z + (size_t)il * M * b.nrhs + 16 * w, b.nrhs);
+        if (hir) {
+            load_tile<64, 64>(Wb, M, b.Wl + (size_t)ir * M * M, M);
+            if (hz) load_tile<16>(Z2, 16, b.Z + (size_t)ir * M * b.nrhs + 16 * w, b.nrhs);
+            if (hr) load_tile<16>(WR, 16, b.Wr + (size_t)ir * M * M + 16 * w, M);
+        }
+        __syncthreads();
+        // A_i -= Wa' Wa + Wb' Wb  (wave v: tile row v, all 4 tile columns)
+        for (int tj = 0; tj < 4; ++tj) {
+            v4d acc = tile_ld(A, LD, 16 * wave, 16 * tj);
+            acc = tile_mm<true, false, true>(acc, Wa, M, 16 * wave, Wa, M, 16 * tj, 0, M);
+            if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * wave, Wb, M, 16 * tj, 0, M);
+            tile_st(A, LD, 16 * wave, 16 * tj, acc);
+        }
+        // R_i[:, w] -= Wa' z_{i-sp}[:, w] + Wb' z_{i+sp}[:, w]
+        if (hz) {
+            v4d acc = tile_ld(Rc, L16, 16 * wave, 0);
+            acc = tile_mm<true, false, true>(acc, Wa, M, 16 * wave, Z1, 16, 0, 0, M);
+            if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * wave, Z2, 16, 0, 0, M);
+            tile_st(Rc, L16, 16 * wave, 0, acc);
+        }
+        // C_i[:, w] = -Wa' Wl_{i-sp}[:, w]   (block (i, i-2sp) = (i, i-s))
+        tile_st(Cc, L16, 16 * wave, 0, tile_mm<true, false, true>(zero4(), Wa, M, 16 * wave, WL, 16, 0, 0, M));
+        // C_r[w rows, :] = -(Wr_{i+sp}[:, w])' Wl_{i+sp}   (block (r, r-s) = (r, i))
+        if (hr && hir) tile_st(Cr, LD, 0, 16 * wave, tile_mm<true, false, true>(zero4(), WR, 16, 0, Wb, M, 16 * wave, 0, M));
+    }
+    __syncthreads();
+    chol_inv64(A, X, bad, col);
+    if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
+    if (w == 0) {
+        double* Xg = b.L + (size_t)i * M * M;
+        for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
+    }
+    const int kend = 16 * (wave + 1);   // X is lower triangular
+    tile_st(b.Wl + (size_t)i * M * M, M, 16 * wave, 16 * w,
+            tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Cc, L16, 0, 0, kend));
+    if (hr)   // op(B)[k][n] = C_r[16w + n][k]
+        tile_st(b.Wr + (size_t)i * M * M, M, 16 * wave, 16 * w,
+                tile_mm<false, true, false>(zero4(), X, LD, 16 * wave, Cr, LD, 0, 0, kend));
+    if (hz)
+        tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * wave, 16 * w,
+                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Rc, L16, 0, 0, kend));
+}
+
 // ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------
 __global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -355,7 +419,7 @@ __global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b) {
     load_rows(R, ldr, b.R, b.nrhs, b.nrhs);
     for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
-    chol_inv64(A, X, bad);
+    chol_inv64(A, X, bad, sc);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     for (int tj = 0; tj < b.nrhs / 16; ++tj)
         tile_st(T, ldr, 16 * wave, 16 * tj,
@@ -522,17 +586,15 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     SFM_HIP(hipGetLastError());
     SFM_HIP(hipMemcpyAsync(b.R0, b.R, (size_t)b.N * M * b.nrhs * sizeof(double), hipMemcpyDeviceToDevice, s));
     const size_t ldr = b.nrhs + 1;
-    const size_t lds_f = (2 * M * LD + 2) * sizeof(double);
-    const size_t lds_w = (M * LD + 2 * M * 17 + 16 * LD) * sizeof(double);
-    const size_t lds_u = (3 * M * LD + 2 * M * ldr) * sizeof(double);
+    const size_t lds_odd = (2 * M * LD + 2 * M * M + 2 * M * 17 + 16 * LD + 18) * sizeof(double);
+    const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);
+    const size_t lds_l = std::max(lds_odd, lds_even);
     const size_t lds_t = (2 * M * LD + 2 * M * ldr + 34) * sizeof(double);
     const size_t lds_b = (3 * M * LD + 3 * M * ldr) * sizeof(double);
     static bool attr = false;
     if (!attr) {   // sized for the largest nrhs (32)
         const int cap = 160 * 1024;
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_factor_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_wz_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_level_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         attr = true;
@@ -540,14 +602,14 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     int s_top = 1;
     for (int stride = 1; stride < b.N; stride *= 2) {
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-        const int n_even = (b.N + 2 * stride - 1) / (2 * stride);
-        hipLaunchKernelGGL(bcr_factor_kernel, dim3(n_odd), dim3(NT), lds_f, s, b, stride);
-        SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(bcr_wz_kernel, dim3(4 * n_odd), dim3(NT), lds_w, s, b, stride);
-        SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(bcr_update_kernel, dim3(4 * n_even), dim3(NT), lds_u, s, b, stride);
+        const int n_even = stride > 1 ? (b.N + 2 * stride - 1) / (2 * stride) : 0;
+        hipLaunchKernelGGL(bcr_level_kernel, dim3(4 * (n_odd + n_even)), dim3(NT), lds_l, s, b, stride, n_odd);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
+    }
+    if (s_top > 1) {   // block 0's update from the last level
+        hipLaunchKernelGGL(bcr_level_kernel, dim3(4), dim3(NT), lds_l, s, b, s_top, 0);
+        SFM_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NT), lds_t, s, b);
     SFM_HIP(hipGetLastError());
