@@ -120,23 +120,23 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
         P[2] = X[2] * cp.c + cr2 * cp.s + u[2] * tmp;
     }
     P[0] += cp.t[0]; P[1] += cp.t[1]; P[2] += cp.t[2];
-    const double x = P[0] / P[2], y = P[1] / P[2];
+    // one reciprocal for the projection and its Jacobian (x = P0/P2 to 1 ulp)
+    const double iz = 1.0 / P[2];
+    const double x = P[0] * iz, y = P[1] * iz;
     const double r0 = in[0] * x + in[2] - u0, r1 = in[1] * y + in[3] - u1;
     L.ok = isfinite(r0) && isfinite(r1);
     const double sq = r0 * r0 + r1 * r1;
-    double rho0, rho1;
+    double rho0, sr = 1.0;   // Huber: rho' = 1 (inlier) needs no square root
     if (huber_a > 0.0 && sq > huber_a * huber_a) {
         const double rr = sqrt(sq);
         rho0 = 2.0 * huber_a * rr - huber_a * huber_a;
-        rho1 = fmax(DBL_MIN, huber_a / rr);
+        sr = sqrt(fmax(DBL_MIN, huber_a / rr));
     } else {
-        rho0 = sq; rho1 = 1.0;
+        rho0 = sq;
     }
     L.half_rho = 0.5 * rho0;
-    const double sr = sqrt(rho1);
     L.f[0] = r0 * sr; L.f[1] = r1 * sr;
     if (JC || JI || JX) {
-        const double iz = 1.0 / P[2];
         const double A[2][3] = {{in[0] * iz * sr, 0.0, -in[0] * x * iz * sr},
                                 {0.0, in[1] * iz * sr, -in[1] * y * iz * sr}};
         if (JI) {
