@@ -219,6 +219,7 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
     double* A = b.A + (size_t)I * M * M;
     double* Cm = b.C + (size_t)I * M * M;
     double* R = b.R + (size_t)I * M * b.nrhs;
+    double* R0 = b.R0 + (size_t)I * M * b.nrhs;
     const int c0 = I * b.K, nreal = min(b.K, P.ncam - c0) * 6;
     const int Dp = P.D + 1;
     for (int e = threadIdx.x; e < M * M; e += NT) {
@@ -265,7 +266,9 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
             }
         }
         R[e] = v;
+        R0[e] = v;
     }
+    if (I == 0 && threadIdx.x == 0) *b.fail = 0.0;
 }
 
 // ---- update of one 16-row tile w of an even block j after eliminating its odd
@@ -581,10 +584,8 @@ void bcr_bind(BcrArgs& b, double* base) {
 }
 
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s) {
-    SFM_HIP(hipMemsetAsync(b.fail, 0, sizeof(double), s));
     hipLaunchKernelGGL(bcr_pack_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());
-    SFM_HIP(hipMemcpyAsync(b.R0, b.R, (size_t)b.N * M * b.nrhs * sizeof(double), hipMemcpyDeviceToDevice, s));
     const size_t ldr = b.nrhs + 1;
     const size_t lds_odd = (2 * M * LD + 2 * M * M + 2 * M * 17 + 16 * LD + 18) * sizeof(double);
     const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);

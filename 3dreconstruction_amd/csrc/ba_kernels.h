@@ -38,8 +38,10 @@ struct DevProblem {
     const int32_t* img_colc;
     const int32_t* img_coli;
     const int32_t* img_intr;
+    const int32_t* intr_col;        // [n_intr] first F column of the intrinsic block or -1
     const ReduceTarget* targets;
-    const ReduceTerm* terms;
+    const FlatTerm* terms;
+    const double* src;              // contiguous [tiles | U | Ub | Ucn] the terms index
     int32_t n_targets;
     int32_t n_long;                 // targets with > reduce_long_threshold() terms
     const int32_t* long_targets;    // [n_long] target ids
@@ -68,6 +70,8 @@ struct DevProblem {
     double* part_u;     // [n_img][2]
     double* part_s;     // [n_chunk][2]
     double* part_t;     // [n_step_blocks][kPartT]
+    double* part_f;     // [n_fblk][3] candidate-kernel partials
+    int32_t n_fblk;
     double* scal;       // [kScCount]
 };
 
@@ -85,9 +89,12 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
               double radius, hipStream_t s, unsigned long long* stamps = nullptr);
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s);
 void ba_solve(const DevProblem& P, double radius, hipStream_t s);
-// candidate cameras/intrinsics, F-part norms and gradient
-void ba_fvec(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
-             double* cand_intr, const int32_t* blk_img, const int32_t* blk_intr, hipStream_t s);
+// candidate cameras/intrinsics and their CamPre; F-part norm/gradient partials
+// into part_f (summed by ba_finalize)
+constexpr int kCandThreads = 256;
+int ba_cand_blocks(const DevProblem& P);
+void ba_cand(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
+             double* cand_intr, CamPre* cand_cp, hipStream_t s);
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius,
              hipStream_t s);

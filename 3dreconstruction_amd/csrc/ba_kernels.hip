@@ -22,6 +22,7 @@
 //   finalize    fixed-order reduction of per-block partials (deterministic)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -54,10 +55,7 @@ __device__ __forceinline__ double clampd(double v, double lo, double hi) {
 // ---------------------------------------------------------------------------
 // per-camera precompute
 // ---------------------------------------------------------------------------
-__global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double* e = extr + 6 * (size_t)i;
+__device__ inline CamPre make_campre(const double* e) {
     CamPre cp;
     const double w[3] = {e[0], e[1], e[2]};
     const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
@@ -87,7 +85,15 @@ __global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __
             cp.Ar[a] = (a % 4 == 0) ? 1.0 : 0.0;
         }
     }
-    out[i] = cp;
+    return cp;
+}
+
+__global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double e[6];
+    for (int a = 0; a < 6; ++a) e[a] = extr[6 * (size_t)i + a];
+    out[i] = make_campre(e);
 }
 
 // ---------------------------------------------------------------------------
@@ -638,16 +644,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 // ---------------------------------------------------------------------------
 // static gather-reduce: one wave per target block
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double term_value(const DevProblem& P, const ReduceTerm& q, int r, int cc, bool vec) {
-    if (q.kind == kSrcTile) {
-        const double* tile = P.tiles + (size_t)q.index * kTileR * kTileR;
-        return vec ? tile[q.roff * kTileR + q.coff + r] : tile[(q.roff + r) * kTileR + q.coff + cc];
-    } else if (q.kind == kSrcU) {
-        return P.U[(size_t)q.index * 100 + (q.roff + r) * 10 + q.coff + cc];
-    } else if (q.kind == kSrcUb) {
-        return P.Ub[(size_t)q.index * 10 + q.roff + r];
-    }
-    return P.Ucn[(size_t)q.index * 10 + q.roff + r];
+__device__ __forceinline__ double term_value(const DevProblem& P, const FlatTerm& q, int r, int cc) {
+    return (double)q.sign * P.src[q.off + (int64_t)r * q.rs + cc];
 }
 
 __device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {
@@ -676,12 +674,17 @@ __global__ void reduce_kernel(DevProblem P, int min_kind) {
     if (e >= T.rows * T.cols) return;
     const int r = e / T.cols, cc = e % T.cols;
     const bool vec = T.cols == 1;
+    // batches of 8 independent loads, summed in term order (deterministic)
     double s = 0.0;
-#pragma unroll 4
-    for (int k = T.c_begin; k < T.c_end; ++k) {
-        const ReduceTerm q = P.terms[k];
-        s += (double)q.sign * term_value(P, q, r, cc, vec);
+    int k = T.c_begin;
+    for (; k + 8 <= T.c_end; k += 8) {
+        double v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = term_value(P, P.terms[k + j], r, cc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[j];
     }
+    for (; k < T.c_end; ++k) s += term_value(P, P.terms[k], r, cc);
     double* dst;
     dst = target_base(P, T.dst_kind);
     dst[T.dst + (vec ? r : r * T.ld + cc)] = s;
@@ -696,17 +699,15 @@ __global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int min_k
     const ReduceTarget T = P.targets[P.long_targets[j]];
     if (T.dst_kind < min_kind) return;
     const int E = T.rows * T.cols;
-    const bool vec = T.cols == 1;
     double s[36];
 #pragma unroll
     for (int e = 0; e < 36; ++e) s[e] = 0.0;
     const int k = k0 + (int)threadIdx.x;
     if (k < T.c_end && k - k0 < kReduceSeg) {
-        const ReduceTerm q = P.terms[k];
-        const double sgn = (double)q.sign;
+        const FlatTerm q = P.terms[k];
 #pragma unroll
         for (int e = 0; e < 36; ++e)
-            if (e < E) s[e] = sgn * term_value(P, q, e / T.cols, e % T.cols, vec);
+            if (e < E) s[e] = term_value(P, q, e / T.cols, e % T.cols);
     }
     wave_sum(s);
     __shared__ double part[4][36];
@@ -965,44 +966,60 @@ __global__ __launch_bounds__(256) void solve_kernel(DevProblem P, double radius,
 }
 
 // ---------------------------------------------------------------------------
-// F-vector epilogue: candidate cameras/intrinsics, norms, gradient
+// Candidate parameters: one thread per image / intrinsic block.  Active
+// columns take x - yF*scaleF (Ceres' x + delta in the unscaled frame),
+// inactive (constant) blocks are copied; the candidate CamPre is built inline.
+// Per-workgroup partials of |x|^2, |delta|^2 and max|g| over the F columns go
+// to part_f and are summed in fixed order by finalize_kernel.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fvec_kernel(DevProblem P, const double* __restrict__ extr,
-                                                   const double* __restrict__ intr,
-                                                   double* __restrict__ cand_extr,
-                                                   double* __restrict__ cand_intr,
-                                                   const int32_t* __restrict__ blk_img,
-                                                   const int32_t* __restrict__ blk_intr) {
+__global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
+                                                            const double* __restrict__ extr,
+                                                            const double* __restrict__ intr,
+                                                            double* __restrict__ cand_extr,
+                                                            double* __restrict__ cand_intr,
+                                                            CamPre* __restrict__ cand_cp) {
+    const int t = blockIdx.x * kCandThreads + threadIdx.x;
     double v[2] = {0.0, 0.0};
     double gm = 0.0;
-    for (int64_t c = threadIdx.x; c < P.nF; c += 256) {
-        double x;
-        double* dst;
-        if (c < P.nb) {
-            const size_t o = 6 * (size_t)blk_img[c / 6] + c % 6;
-            x = extr[o]; dst = cand_extr + o;
-        } else {
-            const size_t o = 4 * (size_t)blk_intr[(c - P.nb) / 4] + (c - P.nb) % 4;
-            x = intr[o]; dst = cand_intr + o;
-        }
+    auto col = [&](double x, int64_t c) {
         const double cand = x + (-P.yF[c]) * P.scaleF[c];
-        *dst = cand;
         const double d = x - cand;
         v[0] += x * x;
         v[1] += d * d;
         const double g = P.bF[c] / P.scaleF[c];
         gm = fmax(gm, fabs(x - (x - g)));
+        return cand;
+    };
+    if (t < P.n_img) {
+        const int c0 = P.img_colc[t];
+        double e[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const double x = extr[6 * (size_t)t + a];
+            e[a] = c0 >= 0 ? col(x, (int64_t)c0 + a) : x;
+            cand_extr[6 * (size_t)t + a] = e[a];
+        }
+        cand_cp[t] = make_campre(e);
+    } else if (t < P.n_img + P.n_intr) {
+        const int q = t - P.n_img;
+        const int c0 = P.intr_col[q];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const double x = intr[4 * (size_t)q + a];
+            cand_intr[4 * (size_t)q + a] = c0 >= 0 ? col(x, (int64_t)c0 + a) : x;
+        }
     }
     wave_sum(v);
     gm = wave_max(gm);
-    __shared__ double red[4][3];
+    constexpr int kW = kCandThreads / 64;
+    __shared__ double red[kW][3];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) { red[wave][0] = v[0]; red[wave][1] = v[1]; red[wave][2] = gm; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        P.scal[kScXnorm2F] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        P.scal[kScStepnorm2F] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-        P.scal[kScGmaxF] = fmax(fmax(red[0][2], red[1][2]), fmax(red[2][2], red[3][2]));
+        double r[3] = {0.0, 0.0, 0.0};
+        for (int w = 0; w < kW; ++w) { r[0] += red[w][0]; r[1] += red[w][1]; r[2] = fmax(r[2], red[w][2]); }
+        for (int k = 0; k < 3; ++k) P.part_f[3 * (size_t)blockIdx.x + k] = r[k];
     }
 }
 
@@ -1139,10 +1156,17 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
 
 // fixed-order reduction of the per-block partials
 __global__ __launch_bounds__(256) void finalize_kernel(DevProblem P, int n_step_blocks) {
-    double s[5] = {0, 0, 0, 0, 0};
-    double m[4] = {0, 0, 0, 0};
+    double s[7] = {0, 0, 0, 0, 0, 0, 0};
+    double m[5] = {0, 0, 0, 0, 0};
+#pragma unroll 4
+    for (int i = threadIdx.x; i < P.n_fblk; i += 256) {
+        s[5] += P.part_f[3 * i]; s[6] += P.part_f[3 * i + 1]; m[4] = fmax(m[4], P.part_f[3 * i + 2]);
+    }
+#pragma unroll 4
     for (int i = threadIdx.x; i < P.n_img * kGramSeg; i += 256) { s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]); }
+#pragma unroll 4
     for (int i = threadIdx.x; i < P.n_chunk; i += 256) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
+#pragma unroll 4
     for (int i = threadIdx.x; i < n_step_blocks; i += 256) {
         s[2] += P.part_t[kPartT * i]; s[3] += P.part_t[kPartT * i + 1]; s[4] += P.part_t[kPartT * i + 2];
         m[2] = fmax(m[2], P.part_t[kPartT * i + 4]);
@@ -1150,27 +1174,30 @@ __global__ __launch_bounds__(256) void finalize_kernel(DevProblem P, int n_step_
     }
     wave_sum(s);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) m[k] = wave_max(m[k]);
-    __shared__ double red[4][9];
+    for (int k = 0; k < 5; ++k) m[k] = wave_max(m[k]);
+    __shared__ double red[4][12];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) {
-        for (int k = 0; k < 5; ++k) red[wave][k] = s[k];
-        for (int k = 0; k < 4; ++k) red[wave][5 + k] = m[k];
+        for (int k = 0; k < 7; ++k) red[wave][k] = s[k];
+        for (int k = 0; k < 5; ++k) red[wave][7 + k] = m[k];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        double t[9];
-        for (int k = 0; k < 5; ++k) t[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
-        for (int k = 5; k < 9; ++k) t[k] = fmax(fmax(red[0][k], red[1][k]), fmax(red[2][k], red[3][k]));
+        double t[12];
+        for (int k = 0; k < 7; ++k) t[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+        for (int k = 7; k < 12; ++k) t[k] = fmax(fmax(red[0][k], red[1][k]), fmax(red[2][k], red[3][k]));
         P.scal[kScCost] = t[0];
         P.scal[kScXnorm2E] = t[1];
         P.scal[kScModelAcc] = t[2];
         P.scal[kScCandCost] = t[3];
         P.scal[kScStepnorm2E] = t[4];
-        P.scal[kScBadX] = t[5];
-        P.scal[kScGmaxE] = t[6];
-        P.scal[kScCandBad] = t[7];
-        P.scal[kScStepBad] = t[8];
+        P.scal[kScXnorm2F] = t[5];
+        P.scal[kScStepnorm2F] = t[6];
+        P.scal[kScBadX] = t[7];
+        P.scal[kScGmaxE] = t[8];
+        P.scal[kScCandBad] = t[9];
+        P.scal[kScStepBad] = t[10];
+        P.scal[kScGmaxF] = t[11];
     }
 }
 
@@ -1254,10 +1281,13 @@ void ba_solve(const DevProblem& P, double radius, hipStream_t s) {
     SFM_HIP(hipGetLastError());
 }
 
-void ba_fvec(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
-             double* cand_intr, const int32_t* blk_img, const int32_t* blk_intr, hipStream_t s) {
-    hipLaunchKernelGGL(fvec_kernel, dim3(1), dim3(256), 0, s, P, extr, intr, cand_extr, cand_intr,
-                       blk_img, blk_intr);
+int ba_cand_blocks(const DevProblem& P) {
+    return std::max(1, (P.n_img + P.n_intr + kCandThreads - 1) / kCandThreads);
+}
+void ba_cand(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
+             double* cand_intr, CamPre* cand_cp, hipStream_t s) {
+    hipLaunchKernelGGL(cand_kernel, dim3(P.n_fblk), dim3(kCandThreads), 0, s, P, extr, intr,
+                       cand_extr, cand_intr, cand_cp);
     SFM_HIP(hipGetLastError());
 }
 

@@ -36,15 +36,15 @@ struct sfm_ba_plan {
     BAHostPlan hp;
     DevProblem P{};
     DBuf<int32_t> pt_off, obs_img, obs_pt, obs_slot, img_obs_ptr, img_obs, img_colc,
-        img_coli, img_intr, blk_img, blk_intr;
+        img_coli, img_intr, intr_col, blk_img, blk_intr;
     DBuf<double> obs_uv;
     DBuf<ChunkDesc> chunks;
     DBuf<ReduceTarget> targets;
-    DBuf<ReduceTerm> terms;
+    DBuf<FlatTerm> terms;
     DBuf<double> X0, Xa, Xb, extr0, intr0, ea, eb, ia, ib;
     DBuf<CamPre> cpa, cpb;
-    DBuf<double> scaleE, scaleF, tiles, U, Ub, Ucn, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
-        part_t, scal, bcr_buf;
+    DBuf<double> scaleE, scaleF, gram, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
+        part_t, part_f, scal, bcr_buf;
     DBuf<int32_t> long_targets;
     DBuf<double> lpart;           // long-target segment partials [n_lseg][36]
     DBuf<int32_t> img_pt;         // image-ordered observations (image Gram pass)
@@ -92,11 +92,16 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->img_uv, h.img_uv, s);
     up(pl->img_colc, h.img_colc, s);
     up(pl->img_coli, h.img_coli, s);
+    {
+        std::vector<int32_t> ic(std::max(prob.n_intr, 1), -1);
+        for (int q = 0; q < prob.n_intr; ++q)
+            if (h.intr_blk[q] >= 0) ic[q] = (int32_t)(h.nb + 4 * (int64_t)h.intr_blk[q]);
+        up(pl->intr_col, ic, s);
+    }
     up(pl->img_intr, h.img_intr, s);
     up(pl->blk_img, h.blk_img, s);
     up(pl->blk_intr, h.blk_intr, s);
     up(pl->targets, h.targets, s);
-    up(pl->terms, h.terms, s);
     std::vector<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
     for (int64_t k = 0; k < h.n_spt; ++k)
         for (int a = 0; a < 3; ++a) xs[3 * k + a] = X[3 * h.spt_global[k] + a];
@@ -112,10 +117,43 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     const int64_t nF = std::max<int64_t>(h.nF, 1);
     pl->scaleE.alloc(xs.size());
     pl->scaleF.alloc(nF);
-    pl->tiles.alloc(std::max<size_t>(h.chunks.size(), 1) * kTileR * kTileR);
-    pl->U.alloc(100 * (size_t)prob.n_img * kGramSeg);
-    pl->Ub.alloc(10 * (size_t)prob.n_img * kGramSeg);
-    pl->Ucn.alloc(10 * (size_t)prob.n_img * kGramSeg);
+    // per-chunk Schur tiles and per-image Gram slices share one buffer so the
+    // reduction terms address every source with a single offset
+    const size_t n_tiles = std::max<size_t>(h.chunks.size(), 1) * kTileR * kTileR;
+    const size_t o_u = n_tiles, o_ub = o_u + 100 * (size_t)prob.n_img * kGramSeg,
+                 o_ucn = o_ub + 10 * (size_t)prob.n_img * kGramSeg,
+                 n_gram = o_ucn + 10 * (size_t)prob.n_img * kGramSeg;
+    pl->gram.alloc(n_gram);
+    {
+        std::vector<FlatTerm> ft(std::max<size_t>(h.terms.size(), 1));
+        for (const ReduceTarget& T : h.targets) {
+            const bool vec = T.cols == 1;
+            for (int32_t k = T.c_begin; k < T.c_end; ++k) {
+                const ReduceTerm& q = h.terms[k];
+                FlatTerm& f = ft[k];
+                f.sign = q.sign;
+                switch (q.kind) {
+                    case kSrcTile:
+                        f.off = (int64_t)q.index * kTileR * kTileR + q.roff * kTileR + q.coff;
+                        f.rs = vec ? 1 : kTileR;
+                        break;
+                    case kSrcU:
+                        f.off = (int64_t)o_u + (int64_t)q.index * 100 + q.roff * 10 + q.coff;
+                        f.rs = 10;
+                        break;
+                    case kSrcUb:
+                        f.off = (int64_t)o_ub + (int64_t)q.index * 10 + q.roff;
+                        f.rs = 1;
+                        break;
+                    default:
+                        f.off = (int64_t)o_ucn + (int64_t)q.index * 10 + q.roff;
+                        f.rs = 1;
+                        break;
+                }
+            }
+        }
+        up(pl->terms, ft, s);
+    }
     pl->rcs_n = h.n_sband + h.n_sarrow + h.n_scorner + 3 * h.nF + 1;
     pl->rcs.alloc(pl->rcs_n);
     pl->rcs.zero(s);
@@ -143,6 +181,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
     P.img_pt = pl->img_pt.p; P.img_uv = pl->img_uv.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
+    P.intr_col = pl->intr_col.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
     {
         // long targets: [n_long targets | n_long+1 segment offsets | n_seg (long idx, term begin)]
@@ -169,8 +208,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->lpart.alloc(36 * std::max<size_t>(P.n_lseg, 1));
         P.lpart = pl->lpart.p;
     }
-    P.scaleE = pl->scaleE.p; P.scaleF = pl->scaleF.p; P.tiles = pl->tiles.p;
-    P.U = pl->U.p; P.Ub = pl->Ub.p; P.Ucn = pl->Ucn.p;
+    P.scaleE = pl->scaleE.p; P.scaleF = pl->scaleF.p; P.tiles = pl->gram.p;
+    P.U = P.tiles + o_u; P.Ub = P.tiles + o_ub; P.Ucn = P.tiles + o_ucn;
+    P.src = pl->gram.p;
     P.Sband = pl->rcs.p;
     P.Sarrow = P.Sband + h.n_sband;
     P.Scorner = P.Sarrow + h.n_sarrow;
@@ -185,6 +225,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.part_u = pl->part_u.p; P.part_s = pl->part_s.p;
     pl->part_t.alloc((size_t)kPartT * std::max(ba_step_blocks(P), 1));
     P.part_t = pl->part_t.p;
+    P.n_fblk = ba_cand_blocks(P);
+    pl->part_f.alloc(3 * (size_t)P.n_fblk);
+    P.part_f = pl->part_f.p;
     P.scal = pl->scal.p;
     pl->use_bcr = bcr_supported(P) && std::getenv("SFM_BA_BAND_SOLVER") == nullptr;
     if (pl->use_bcr) {
@@ -278,10 +321,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         allreduce_rcs();
         if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s);
         else ba_solve(P, radius, s);
-        SFM_HIP(hipMemcpyAsync(S.ec, S.e, ne * 8, hipMemcpyDeviceToDevice, s));
-        SFM_HIP(hipMemcpyAsync(S.inc, S.in, ni * 8, hipMemcpyDeviceToDevice, s));
-        ba_fvec(P, S.e, S.in, S.ec, S.inc, pl->blk_img.p, pl->blk_intr.p, s);
-        ba_campre(S.ec, h.n_img, S.cpc, s);
+        ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         ba_finalize(P, s);
         if (ctx->world > 1) {

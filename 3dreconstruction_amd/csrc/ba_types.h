@@ -71,6 +71,14 @@ struct ReduceTarget {
     int32_t c_begin, c_end;  // contribution range
 };
 
+// ReduceTerm resolved against the contiguous [tiles | U | Ub | Ucn] buffer:
+// element (r, c) of the source block is src[off + r * rs + c].
+struct FlatTerm {
+    int64_t off;
+    int32_t rs;
+    float sign;
+};
+
 struct ReduceTerm {
     int32_t kind;       // kSrc*
     int32_t index;      // chunk or image
