@@ -15,6 +15,7 @@ struct BcrArgs {
     int nrhs = 0;   // 1 + 4*nintr, padded to a multiple of 8
     double *A = nullptr, *C = nullptr, *L = nullptr, *Wl = nullptr, *Wr = nullptr;
     double *R = nullptr, *R0 = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
+    unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums
 };
 
 bool bcr_supported(const DevProblem& P);

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <utility>
 
 #include "ba_bcr.h"
 #include "common.h"
@@ -35,6 +36,12 @@ constexpr int NT = 256;
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -122,64 +129,116 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// 1/d: hardware estimate + two Newton steps (full fp64 accuracy)
+__device__ __forceinline__ double rcp_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) y = fma(y, fma(-d, y, 1.0), y);
+    return y;
+}
+
+// value of v in lane l of this lane's 16-lane row (DPP row_newbcast, 64-bit);
+// l must fold to a constant
+__device__ __forceinline__ double row_bcast(double v, int l) {
+#define SFM_BC(n) case n: return __builtin_amdgcn_mov_dpp(v, 0x150 + n, 0xf, 0xf, true);
+    switch (l) {
+        SFM_BC(0) SFM_BC(1) SFM_BC(2) SFM_BC(3) SFM_BC(4) SFM_BC(5) SFM_BC(6) SFM_BC(7)
+        SFM_BC(8) SFM_BC(9) SFM_BC(10) SFM_BC(11) SFM_BC(12) SFM_BC(13) SFM_BC(14)
+        default: return __builtin_amdgcn_mov_dpp(v, 0x15f, 0xf, 0xf, true);
+    }
+#undef SFM_BC
+}
+
+// acc += (src of lane l of this lane's 16-lane row) * mul, one v_fmac_f64 with
+// a DPP row_newbcast source.  The compiler does not see inside the asm, so the
+// DPP read-after-VALU-write hazard (2 wait states) is covered by NOP = true on
+// the first FMA of each group; tests/test_bcr_asm.py checks the schedule.
+#define SFM_FMAC_BC(n)                                                                                 \
+    case n:                                                                                            \
+        if (NOP)                                                                                       \
+            asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf" \
+                         : "+v"(acc) : "v"(src), "v"(mul));                                            \
+        else                                                                                           \
+            asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf"   \
+                         : "+v"(acc) : "v"(src), "v"(mul));                                            \
+        break;
+template <bool NOP>
+__device__ __forceinline__ void fmac_bc(double& acc, double src, double mul, int l) {
+    switch (l) {
+        SFM_FMAC_BC(0) SFM_FMAC_BC(1) SFM_FMAC_BC(2) SFM_FMAC_BC(3) SFM_FMAC_BC(4) SFM_FMAC_BC(5)
+        SFM_FMAC_BC(6) SFM_FMAC_BC(7) SFM_FMAC_BC(8) SFM_FMAC_BC(9) SFM_FMAC_BC(10) SFM_FMAC_BC(11)
+        SFM_FMAC_BC(12) SFM_FMAC_BC(13) SFM_FMAC_BC(14) SFM_FMAC_BC(15)
+        default: break;
+    }
+}
+#undef SFM_FMAC_BC
+
 // Wave-local factor + inverse of one 16x16 diagonal tile: lane i < 16 owns
-// row i in registers.  Step k: the pivot comes from lane k (v_readlane), each
-// lane scales its column-k entry and publishes it in `col` (LDS); the rank-1
-// update reads column k back as same-address (broadcast) LDS loads.
+// row i of A in registers and column i of X = L^-1.  Step k broadcasts the
+// unscaled column k of every row across the 16 lanes with DPP row_newbcast
+// folded into the FMAs (no LDS, no scalar round trip) and applies
+// a_ij -= (a_ik / d_k) a_jk.  Row k of X (x_k = (e_k - sum_p L_kp x_p) / L_kk)
+// is computed as soon as row k of L is final.  Single-wave issue bound:
+// about 30 fp64 instructions per pivot.
 // L overwrites the lower tile (upper zeroed); X gets L^-1 (upper zeroed).
+// step K of diag16, expanded at compile time (an inline-asm body defeats the
+// loop unroller, and every broadcast lane must be an immediate)
+template <int K, int... J>
+__device__ __forceinline__ void diag16_update(double (&a)[16], double nt, std::integer_sequence<int, J...>) {
+    (fmac_bc<J == 0>(a[K + 1 + J], a[K], nt, K + 1 + J), ...);
+}
+template <int K, int... P>
+__device__ __forceinline__ void diag16_xrow(const double (&a)[16], const double (&x)[16], double& u0, double& u1,
+                                            std::integer_sequence<int, P...>) {
+    ((P & 1 ? fmac_bc<false>(u1, a[P], x[P], K) : fmac_bc<P == 0>(u0, a[P], x[P], K)), ...);
+}
+template <int K>
+__device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], bool& ok, int i) {
+    const double d = row_bcast(a[K], K);
+    ok = ok && d > 0.0;
+    const double rinv = rsqrt_nr(d);
+    const double lk = a[K] * rinv;       // L_ik (i > K)
+    const double nt = -(lk * rinv);      // -a_iK / d_K
+    diag16_update<K>(a, nt, std::make_integer_sequence<int, 15 - K>{});
+    a[K] = i == K ? d * rinv : (i > K ? lk : a[K]);
+    // row K of L is final: lane c gets x_K = (delta_Kc - sum_p L_Kp x_p) / L_KK
+    double u0 = 0.0, u1 = 0.0;
+    diag16_xrow<K>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
+    x[K] = ((K == i ? 1.0 : 0.0) - (u0 + u1)) * rinv;
+    if constexpr (K < 15) diag16_step<K + 1>(a, x, ok, i);
+}
+
 __device__ void diag16(double* A, double* X, double* bad, double* col) {
+    (void)col;
     const int lane = threadIdx.x & 63, i = lane;
     const bool act = lane < 16;
-    double a[16], rinv[16];
+    double a[16], x[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? A[i * LD + j] : 0.0;
     bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const double d = rdlane(a[k], k);
-        ok = ok && d > 0.0;
-        rinv[k] = rsqrt_nr(d);
-        a[k] = i == k ? d * rinv[k] : (i > k ? a[k] * rinv[k] : a[k]);
-        if (k < 15) {
-            if (act) col[i] = a[k];
-            wave_sync_lds();
-            double cv[16];
-#pragma unroll
-            for (int j = k + 1; j < 16; ++j) cv[j] = col[j];
-#pragma unroll
-            for (int j = k + 1; j < 16; ++j) a[j] = fma(-a[k], cv[j], a[j]);
-            wave_sync_lds();
-        }
-    }
+    diag16_step<0>(a, x, ok, i);
     if (lane == 0 && !ok) bad[0] = 1.0;
     if (act) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
-    }
-    wave_sync_lds();
-    // X = L^-1 by columns: lane c solves L x = e_c, rows of L read as broadcasts
-    const int c = lane;
-    double x[16];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        double t = (m == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int p = 0; p < m; ++p) t = fma(-A[m * LD + p], x[p], t);
-        x[m] = t * rinv[m];
-    }
-    if (act) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m) X[m * LD + c] = x[m];
+        for (int m = 0; m < 16; ++m) X[m * LD + i] = x[m];
     }
 }
 
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
 // the caller).  All 256 threads; ends synchronised.
-__device__ void chol_inv64(double* A, double* X, double* bad, double* col) {
+__device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
+                           unsigned long long* st = nullptr) {
     const int wave = threadIdx.x >> 6;
+    unsigned long long t0 = 0, td = 0;
+    if (st) t0 = stamp();
     for (int k = 0; k < 4; ++k) {
+        unsigned long long ta = 0;
+        if (st) ta = stamp();
         if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), bad, col);
         __syncthreads();
+        if (st) td += stamp() - ta;
 
         if (wave < 3 - k) {   // panel: L_ik = A_ik X_kk'
             const int i = k + 1 + wave;
@@ -210,6 +269,10 @@ __device__ void chol_inv64(double* A, double* X, double* bad, double* col) {
             tile_st(X, LD, 16 * i, 16 * j, acc);
         }
         __syncthreads();
+    }
+    if (st && threadIdx.x == 0) {
+        atomicAdd(st + 0, td);
+        atomicAdd(st + 1, stamp() - t0);
     }
 }
 
@@ -345,6 +408,9 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
     double* Rc = Cr + 16 * LD;      // [64][17] column tile w of R_i
     double* bad = Rc + M * L16;
     double* col = bad + 2;          // [16] diag16 column broadcast
+    unsigned long long* st = (b.stamps && w == 0) ? b.stamps : nullptr;
+    unsigned long long t0 = 0, t1 = 0;
+    if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
     load_rows(A, LD, b.A + (size_t)i * M * M, M, M);
     load_rows(Cc, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
@@ -369,6 +435,7 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
             if (hr) load_tile<16>(WR, 16, b.Wr + (size_t)ir * M * M + 16 * w, M);
         }
         __syncthreads();
+        if (st && threadIdx.x == 0) atomicAdd(st + 5, stamp() - t0);   // loads
         // A_i -= Wa' Wa + Wb' Wb  (wave v: tile row v, all 4 tile columns)
         for (int tj = 0; tj < 4; ++tj) {
             v4d acc = tile_ld(A, LD, 16 * wave, 16 * tj);
@@ -389,11 +456,16 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
         if (hr && hir) tile_st(Cr, LD, 0, 16 * wave, tile_mm<true, false, true>(zero4(), WR, 16, 0, Wb, M, 16 * wave, 0, M));
     }
     __syncthreads();
-    chol_inv64(A, X, bad, col);
+    if (st) t1 = stamp();
+    chol_inv64(A, X, bad, col, st);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     if (w == 0) {
         double* Xg = b.L + (size_t)i * M * M;
         for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
+    }
+    if (st) {
+        __syncthreads();
+        if (threadIdx.x == 0) atomicAdd(st + 6, stamp() - t0);   // through the X copy
     }
     const int kend = 16 * (wave + 1);   // X is lower triangular
     tile_st(b.Wl + (size_t)i * M * M, M, 16 * wave, 16 * w,
@@ -404,6 +476,14 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
     if (hz)
         tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * wave, 16 * w,
                 tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Rc, L16, 0, 0, kend));
+    if (st) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            atomicAdd(st + 2, t1 - t0);              // loads + update
+            atomicAdd(st + 3, stamp() - t0);         // whole block
+            atomicAdd(st + 4, 1ull);
+        }
+    }
 }
 
 // ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------

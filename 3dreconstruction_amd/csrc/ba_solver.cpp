@@ -50,6 +50,7 @@ struct sfm_ba_plan {
     DBuf<int32_t> img_pt;         // image-ordered observations (image Gram pass)
     DBuf<double> img_uv;
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
+    DBuf<unsigned long long> bcr_stamps;   // SFM_BCR_STAMPS=1 diagnostic
     BcrArgs bcr;
     bool use_bcr = false;
     int64_t rcs_n = 0;
@@ -234,6 +235,11 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         bcr_setup(pl->bcr, P);
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
         bcr_bind(pl->bcr, pl->bcr_buf.p);
+        if (std::getenv("SFM_BCR_STAMPS")) {
+            pl->bcr_stamps.alloc(7);
+            pl->bcr_stamps.zero(s);
+            pl->bcr.stamps = pl->bcr_stamps.p;
+        }
     }
     if (std::getenv("SFM_SCHUR_STAMPS")) pl->stamps.alloc(6 * std::max<size_t>(h.chunks.size(), 1));
     pl->ev.resize(16);
@@ -407,6 +413,14 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         decrease_factor *= 2.0;
         cur.trust_region_radius = radius;
         term = finalize(cur, prev_gmax);
+    }
+    if (pl->bcr.stamps) {  // diagnostic: average cycles per odd block, all levels
+        unsigned long long st[7];
+        SFM_HIP(hipMemcpy(st, pl->bcr.stamps, sizeof st, hipMemcpyDeviceToHost));
+        const double n = st[4] ? (double)st[4] : 1.0;
+        std::fprintf(stderr, "[bcr stamps] cycles/odd block: loads %.0f load+update %.0f chol %.0f (diag16 %.0f) "
+                     "to X copy %.0f total %.0f over %llu\n",
+                     st[5] / n, st[2] / n, st[1] / n, st[0] / n, st[6] / n, st[3] / n, st[4]);
     }
     if (pl->stamps.p) {  // diagnostic: average phase cycles per chunk (last Schur launch)
         std::vector<unsigned long long> st(pl->stamps.n);
