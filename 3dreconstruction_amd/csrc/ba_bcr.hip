@@ -61,16 +61,34 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 }
 
 // One wave, one 16x16 output tile: acc += op(A)[ar.., k] op(B)[k, bc..] for
-// k in [k0, k1) (multiple of 4).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
-// op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.
+// k in [k0, k1) (k1 - k0 a multiple of 16).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
+// op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.  The LDS
+// operands of the next 16-wide k chunk are read while the current chunk's four
+// MFMAs run, so a runtime-length product is not LDS-latency bound.
 template <bool TA, bool TB, bool NEG>
 __device__ __forceinline__ v4d tile_mm(v4d acc, const double* A, int lda, int ar, const double* B, int ldb,
                                        int bc, int k0, int k1) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
-    for (int k = k0; k < k1; k += 4) {
-        const double a = TA ? A[(k + kk) * lda + ar + i] : A[(ar + i) * lda + k + kk];
-        const double b = TB ? B[(bc + i) * ldb + k + kk] : B[(k + kk) * ldb + bc + i];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a : a, b, acc, 0, 0, 0);
+    double a[4], b[4];
+    auto load = [&](int k, double (&av)[4], double (&bv)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int kj = k + 4 * j + kk;
+            av[j] = TA ? A[kj * lda + ar + i] : A[(ar + i) * lda + kj];
+            bv[j] = TB ? B[(bc + i) * ldb + kj] : B[kj * ldb + bc + i];
+        }
+    };
+    load(k0, a, b);
+    for (int k = k0; k < k1; k += 16) {
+        double an[4], bn[4];
+        const bool more = k + 16 < k1;
+        if (more) load(k + 16, an, bn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[j] = an[j]; b[j] = bn[j]; }
+        }
     }
     return acc;
 }
