@@ -454,12 +454,15 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
         }
         __syncthreads();
         if (st && threadIdx.x == 0) atomicAdd(st + 5, stamp() - t0);   // loads
-        // A_i -= Wa' Wa + Wb' Wb  (wave v: tile row v, all 4 tile columns)
-        for (int tj = 0; tj < 4; ++tj) {
-            v4d acc = tile_ld(A, LD, 16 * wave, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wa, M, 16 * wave, Wa, M, 16 * tj, 0, M);
-            if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * wave, Wb, M, 16 * tj, 0, M);
-            tile_st(A, LD, 16 * wave, 16 * tj, acc);
+        // A_i -= Wa' Wa + Wb' Wb on the 10 lower tiles (the factorisation reads
+        // nothing above the diagonal): wave v takes tiles v, v+4, v+8
+        for (int q = wave; q < 10; q += 4) {
+            const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
+            const int tj = q - ti * (ti + 1) / 2;
+            v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
+            acc = tile_mm<true, false, true>(acc, Wa, M, 16 * ti, Wa, M, 16 * tj, 0, M);
+            if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * ti, Wb, M, 16 * tj, 0, M);
+            tile_st(A, LD, 16 * ti, 16 * tj, acc);
         }
         // R_i[:, w] -= Wa' z_{i-sp}[:, w] + Wb' z_{i+sp}[:, w]
         if (hz) {
