@@ -394,6 +394,13 @@ __device__ __forceinline__ bool crow_valid(const ChunkDesc& cd, int t) { return 
 __device__ constexpr int kTi[15] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4};
 __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4};
 
+#ifndef SFM_SCHUR4_SP   // points / observations per batch of the 64-row variant
+#define SFM_SCHUR4_SP 4
+#endif
+#ifndef SFM_SCHUR4_SO
+#define SFM_SCHUR4_SO 48
+#endif
+
 // NT = 5: rows 0..75 F blocks, row 79 = w, so -Z w comes out of the MFMA.
 // NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
 // SP / SO: points / observations per wave batch.  The panel holds 3 columns
@@ -410,10 +417,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         tacc[k] += tn_ - tprev;                           \
         tprev = tn_;                                      \
     }
-    constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT;
-    __shared__ double panel[kPK][kPR];          // [k][row]
+    // LDS strides padded against bank conflicts (MI355X_MICROARCH.md §LDS):
+    // panel rows 4 doubles past the tile width put the 12 (point, axis) rows
+    // that the intrinsics pass updates at one column on distinct banks, and
+    // 14-double observation rows spread ds_write_b128 lane groups.
+    constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT, kPS = kPR + 4;
+    __shared__ double panel[kPK][kPS];          // [k][row]
     __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
-    __shared__ double ob[SO][12];               // Jx 6 | f 2 | J_intr 4
+    __shared__ double ob[SO][14];               // Jx 6 | f 2 | J_intr 4 | pad
     __shared__ double obm[SO][6];               // M = Jx L^-T
     __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
@@ -456,7 +467,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         const int p1 = p0 + npts;
         const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
 #pragma unroll
-        for (int e = lane; e < kPK * kPR / 2; e += 64)
+        for (int e = lane; e < kPK * kPS / 2; e += 64)
             reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
         int slot = 0, pl = 0;
         double u0 = 0.0, u1 = 0.0, Xp[3] = {0.0, 0.0, 0.0}, sE[3] = {1.0, 1.0, 1.0};
@@ -569,7 +580,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         SFM_STAMP(2)
         // ---- C2: intrinsics rows, ordered per point ---------------------------
         // (register sums per run of observations sharing an intrinsics block)
-        if (lane < 3 * npts) {
+        if constexpr (12 * SP <= 64) {
+            // one lane per (point, axis, intrinsics column): z_k = sum_q Ji[q][k] M[q][k & 1][a]
+            if (lane < 12 * npts) {
+                const int pt = lane / 12, rem = lane - 12 * pt, a = rem >> 2, k = rem & 3;
+                const int mo = 3 * (k & 1) + a;
+                const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
+                int row = orow[q0];
+                double z = 0.0;
+                for (int q = q0; q < q1; ++q) {
+                    const int rq = orow[q];
+                    if (rq != row) {
+                        panel[3 * pt + a][row + k] += z;
+                        z = 0.0;
+                        row = rq;
+                    }
+                    z = fma(ob[q][8 + k], obm[q][mo], z);
+                }
+                panel[3 * pt + a][row + k] += z;
+            }
+        } else if (lane < 3 * npts) {
             const int pt = lane / 3, a = lane - 3 * pt;
             const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
             int row = orow[q0];
@@ -1237,7 +1267,8 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
     // 64-row tiles: 4-point batches (12 panel columns, no k padding) keep LDS
     // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
     if (P.tile_nt == 4)
-        hipLaunchKernelGGL((schur_kernel<4, 4, 48>), dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
+        hipLaunchKernelGGL((schur_kernel<4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>), dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X,
+                           radius, stamps);
     else
         hipLaunchKernelGGL(schur_kernel<5>, dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
     SFM_HIP(hipGetLastError());
