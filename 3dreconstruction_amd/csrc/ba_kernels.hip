@@ -424,7 +424,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT, kPS = kPR + 4;
     __shared__ double panel[kPK][kPS];          // [k][row]
     __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
-    __shared__ double ob[SO][14];               // Jx 6 | f 2 | J_intr 4 | pad
+    __shared__ double ob[SO][4];                // J_intr nonzeros
+    __shared__ double vs[SO][10];               // per observation: Jx'Jx (6) | Jx'f (3) | pad
+    __shared__ double vsum[SP][10];             // per point: V (6) | g_E (3)
     __shared__ double obm[SO][6];               // M = Jx L^-T
     __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
@@ -495,37 +497,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
                 for (int a = 0; a < 3; ++a) L.Jx[r][a] *= sE[a];
             }
+            // this observation's share of its point's V = Jx'Jx and g_E = Jx'f
+            double cv[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // V00 V10 V11 V20 V21 V22 | b0 b1 b2
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
+            for (int r = 0; r < 2; ++r) {
+                const double j0 = L.Jx[r][0], j1 = L.Jx[r][1], j2 = L.Jx[r][2], fr = L.f[r];
+                cv[0] += j0 * j0; cv[1] += j1 * j0; cv[2] += j1 * j1;
+                cv[3] += j2 * j0; cv[4] += j2 * j1; cv[5] += j2 * j2;
+                cv[6] += j0 * fr; cv[7] += j1 * fr; cv[8] += j2 * fr;
+            }
 #pragma unroll
-                for (int a = 0; a < 3; ++a) ob[lane][3 * r + a] = L.Jx[r][a];
-            ob[lane][6] = L.f[0];
-            ob[lane][7] = L.f[1];
+            for (int e = 0; e < 9; ++e) vs[lane][e] = cv[e];
             // J_intr rows are [x s, 0, s, 0] and [0, y s, 0, s]: keep the 4 nonzeros
-            ob[lane][8] = L.Ji[0][0] * isc[is][4];
-            ob[lane][9] = L.Ji[1][1] * isc[is][5];
-            ob[lane][10] = L.Ji[0][2] * isc[is][6];
-            ob[lane][11] = L.Ji[1][3] * isc[is][7];
+            ob[lane][0] = L.Ji[0][0] * isc[is][4];
+            ob[lane][1] = L.Ji[1][1] * isc[is][5];
+            ob[lane][2] = L.Ji[0][2] * isc[is][6];
+            ob[lane][3] = L.Ji[1][3] * isc[is][7];
             orow[lane] = irow[is];
         }
         __syncthreads();
+        // per-point sums in observation order, one lane per (point, entry)
+        if (lane < 9 * npts) {
+            const int pt = lane / 9, e = lane - 9 * pt;
+            const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
+            double acc = 0.0;
+            for (int q = q0; q < q1; ++q) acc += vs[q][e];
+            vsum[pt][e] = acc;
+        }
+        __syncthreads();
         SFM_STAMP(1)
-        // ---- B: every observation lane forms its point's V + D^2 and g_E (sum
-        // in observation-then-row order: identical on all lanes of the point),
-        // factors it, and goes on to M = Jx L^-T and the camera rows of Z ----
+        // ---- B: every observation lane takes its point's V + D^2 and g_E (the
+        // per-point sums above: identical on all lanes of the point), factors
+        // it, and goes on to M = Jx L^-T and the camera rows of Z ----
         if (lane < nobs) {
-            const int q0 = cpoff[p0 + pl] - o0, q1 = cpoff[p0 + pl + 1] - o0;
-            double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};  // V00 V10 V11 V20 V21 V22
-            for (int q = q0; q < q1; ++q) {
+            const int q0 = cpoff[p0 + pl] - o0;
+            double V[6], b[3];   // V00 V10 V11 V20 V21 V22
 #pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const double j0 = ob[q][3 * r], j1 = ob[q][3 * r + 1], j2 = ob[q][3 * r + 2];
-                    const double fr = ob[q][6 + r];
-                    V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
-                    V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
-                    b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
-                }
-            }
+            for (int e = 0; e < 6; ++e) V[e] = vsum[pl][e];
+#pragma unroll
+            for (int e = 0; e < 3; ++e) b[e] = vsum[pl][6 + e];
             const bool first = lane == q0;
             if (first) {   // gradient / norm bookkeeping at x (used after a relinearisation)
 #pragma unroll
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                         z = 0.0;
                         row = rq;
                     }
-                    z = fma(ob[q][8 + k], obm[q][mo], z);
+                    z = fma(ob[q][k], obm[q][mo], z);
                 }
                 panel[3 * pt + a][row + k] += z;
             }
@@ -613,10 +623,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                     row = rq;
                 }
                 const double m0 = obm[q][a], m1 = obm[q][3 + a];
-                z0 += ob[q][8] * m0;
-                z1 += ob[q][9] * m1;
-                z2 += ob[q][10] * m0;
-                z3 += ob[q][11] * m1;
+                z0 += ob[q][0] * m0;
+                z1 += ob[q][1] * m1;
+                z2 += ob[q][2] * m0;
+                z3 += ob[q][3] * m1;
             }
             panel[3 * pt + a][row + 0] += z0; panel[3 * pt + a][row + 1] += z1;
             panel[3 * pt + a][row + 2] += z2; panel[3 * pt + a][row + 3] += z3;
