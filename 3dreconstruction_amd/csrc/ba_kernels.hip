@@ -521,7 +521,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             const int pt = lane / 9, e = lane - 9 * pt;
             const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
             double acc = 0.0;
-            for (int q = q0; q < q1; ++q) acc += vs[q][e];
+            int q = q0;
+            for (; q + 4 <= q1; q += 4) {   // loads in flight together, adds in order
+                const double v0 = vs[q][e], v1 = vs[q + 1][e], v2 = vs[q + 2][e], v3 = vs[q + 3][e];
+                acc += v0; acc += v1; acc += v2; acc += v3;
+            }
+            for (; q < q1; ++q) acc += vs[q][e];
             vsum[pt][e] = acc;
         }
         __syncthreads();
@@ -598,15 +603,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
                 const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
                 int row = orow[q0];
                 double z = 0.0;
-                for (int q = q0; q < q1; ++q) {
-                    const int rq = orow[q];
+                auto step = [&](int rq, double jv, double mv) {
                     if (rq != row) {
                         panel[3 * pt + a][row + k] += z;
                         z = 0.0;
                         row = rq;
                     }
-                    z = fma(ob[q][k], obm[q][mo], z);
+                    z = fma(jv, mv, z);
+                };
+                int q = q0;
+                for (; q + 4 <= q1; q += 4) {   // operands of 4 observations loaded together
+                    int rq[4];
+                    double jv[4], mv[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { rq[j] = orow[q + j]; jv[j] = ob[q + j][k]; mv[j] = obm[q + j][mo]; }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) step(rq[j], jv[j], mv[j]);
                 }
+                for (; q < q1; ++q) step(orow[q], ob[q][k], obm[q][mo]);
                 panel[3 * pt + a][row + k] += z;
             }
         } else if (lane < 3 * npts) {
