@@ -38,6 +38,14 @@ constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 // 1/sqrt(d): hardware estimate + two Newton steps (full fp64 accuracy)
+// 1/d: hardware estimate + two Newton steps
+__device__ __forceinline__ double rcp_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) y = fma(y, fma(-d, y, 1.0), y);
+    return y;
+}
+
 __device__ __forceinline__ double rsqrt_nr(double d) {
     double y = __builtin_amdgcn_rsq(d);
 #pragma unroll
@@ -438,6 +446,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int c = blockIdx.x, lane = threadIdx.x;
     const ChunkDesc& cd = P.chunks[c];
     const int pb = cd.pt_begin, np = cd.pt_end - pb, ob0 = cd.obs_begin;
+    const double inv_radius = 1.0 / radius;   // LM diagonal D^2 = clamp(diag) / radius (as step_kernel)
 
     for (int e = lane; e <= np; e += 64) cpoff[e] = P.pt_off[pb + e] - ob0;
     stage_campre(cd, cps, scp);
@@ -471,6 +480,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int e = lane; e < kPK * kPS / 2; e += 64)
             reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
+        if (NT == 4 && lane < kPK) wcol[lane] = 0.0;   // columns past 3 * npts stay zero
         int slot = 0, pl = 0;
         double u0 = 0.0, u1 = 0.0, Xp[3] = {0.0, 0.0, 0.0}, sE[3] = {1.0, 1.0, 1.0};
         if (lane < nobs) {
@@ -545,7 +555,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             if (first) {   // gradient / norm bookkeeping at x (used after a relinearisation)
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
-                    const double g = b[a] / sE[a];
+                    const double g = b[a] * rcp_nr(sE[a]);
                     xn2 += Xp[a] * Xp[a];
                     gmx = fmax(gmx, fabs(Xp[a] - (Xp[a] - g)));
                 }
@@ -553,7 +563,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             const int di[3] = {0, 2, 5};
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) / radius);
+                const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
                 V[di[a]] += lm * lm;
             }
             const double i00 = rsqrt_nr(V[0]);
@@ -661,8 +671,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
             for (int q = 0; q < kNTiles; ++q)
                 acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ks][kTi[q]], op[ks][kTj[q]], acc[q], 0, 0, 0);
-        if (NT == 4)
-            for (int k = 0; k < 3 * npts; ++k) wacc += panel[k][lane] * wcol[k];
+        if (NT == 4) {
+#pragma unroll
+            for (int k = 0; k < kPK; ++k) wacc += panel[k][lane] * wcol[k];
+        }
         __syncthreads();
         SFM_STAMP(4)
         p0 = p1;
@@ -1093,6 +1105,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
     __shared__ double csy[kCamSlots][12];       // camera scaleF | yF (0 for a constant image)
     __shared__ double isy[kIntrSlots][16];      // intrinsics | candidate | scaleF | yF
     const int c = blockIdx.x, tid = threadIdx.x;
+    const double inv_radius = 1.0 / radius;   // as schur_kernel
     const ChunkDesc& cd = P.chunks[c];
     {
         constexpr int kCpW = sizeof(CamPre) / 8;
@@ -1147,7 +1160,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
         const int di[3] = {0, 2, 5};
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) / radius);
+            const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
             V[di[a]] += lm * lm;
         }
         // y_E = (V + D^2)^-1 (g_E - W' y_F) via Cholesky
