@@ -214,12 +214,86 @@ __device__ __forceinline__ double wave_max(double v) {
 
 // ---------------------------------------------------------------------------
 // per-image Gram blocks: U = J_F' J_F (10x10), b = J_F' f, cost
-// One workgroup per image.  Each lane linearises one observation and stores
-// its two scaled rows [J_c (6) | J_i (4) | f | 0 ...] in wave-private LDS;
-// [J | f]' [J | f] is then a 16x16 fp64 MFMA tile (k = Jacobian rows), the
-// same LDS element feeding both operands.  Waves add in fixed order.
+// kGramSeg workgroups per image, one observation per lane per step.  Each lane
+// keeps its own running sums of the 62 structurally nonzero entries of
+// [J_c | J_i | f]' [J_c | J_i | f] (J_i row 0 = [x s, 0, s, 0], row 1 =
+// [0, y s, 0, s]) plus the cost on the VALU -- 90 FMAs per observation, no
+// LDS staging -- and the wave then reduce-scatters the 64 sums (permlane32 /
+// permlane16 swaps, then xor shuffles) so lane l ends with entry l; the four
+// waves add in fixed order.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
+namespace gram {
+constexpr bool in0(int i) { return i < 6 || i == 6 || i == 8 || i == 10; }   // nonzero in row 0
+constexpr bool in1(int i) { return i < 6 || i == 7 || i == 9 || i == 10; }   // nonzero in row 1
+struct Slots {
+    int i[64], j[64], id[11][11], n;
+};
+constexpr Slots make_slots() {
+    Slots t{};
+    t.n = 0;
+    for (int a = 0; a < 11; ++a)
+        for (int b = 0; b < 11; ++b) t.id[a][b] = -1;
+    for (int a = 0; a < 11; ++a)
+        for (int b = 0; b <= a; ++b)
+            if ((in0(a) && in0(b)) || (in1(a) && in1(b))) {
+                t.i[t.n] = a; t.j[t.n] = b;
+                t.id[a][b] = t.id[b][a] = t.n;
+                ++t.n;
+            }
+    return t;
+}
+constexpr Slots kS = make_slots();
+static_assert(kS.n == 62, "image Gram: 62 nonzero entries");
+constexpr int kCost = 62;   // slot of the cost; slot 63 stays zero
+
+__device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__double_as_longlong(v); }
+__device__ __forceinline__ unsigned hi32(double v) { return (unsigned)(__double_as_longlong(v) >> 32); }
+__device__ __forceinline__ double mk(unsigned lo, unsigned hi) {
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+// v[j] + partner's v[j] in the lanes that keep j, v[j+H] + partner's in the others
+template <int H>
+__device__ __forceinline__ void swap_add(double (&v)[64]) {
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        const double a = v[k], b = v[k + H];
+        double na, nb;
+        if (H == 32) {
+            const auto l = __builtin_amdgcn_permlane32_swap(lo32(a), lo32(b), false, false);
+            const auto h = __builtin_amdgcn_permlane32_swap(hi32(a), hi32(b), false, false);
+            na = mk(l[0], h[0]); nb = mk(l[1], h[1]);
+        } else {
+            const auto l = __builtin_amdgcn_permlane16_swap(lo32(a), lo32(b), false, false);
+            const auto h = __builtin_amdgcn_permlane16_swap(hi32(a), hi32(b), false, false);
+            na = mk(l[0], h[0]); nb = mk(l[1], h[1]);
+        }
+        v[k] = na + nb;
+    }
+}
+template <int M>
+__device__ __forceinline__ void xor_add(double (&v)[64], int lane) {
+    const bool up = (lane & M) != 0;
+#pragma unroll
+    for (int k = 0; k < M; ++k) {
+        const double send = up ? v[k] : v[k + M], keep = up ? v[k + M] : v[k];
+        v[k] = keep + __shfl_xor(send, M);
+    }
+}
+// after the call lane l holds the wave sum of v[l] in v[0]
+__device__ __forceinline__ void reduce_scatter64(double (&v)[64], int lane) {
+    swap_add<32>(v);   // lanes 0-31: entries 0..31, lanes 32-63: 32..63 (in v[0..31])
+    swap_add<16>(v);   // row r (16 lanes): entries 16 r + (0..15)
+    xor_add<8>(v, lane);
+    xor_add<4>(v, lane);
+    xor_add<2>(v, lane);
+    xor_add<1>(v, lane);
+}
+}  // namespace gram
+
+#ifndef SFM_GRAM_WPE
+#define SFM_GRAM_WPE 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WPE, SFM_GRAM_WPE))) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const double* __restrict__ X) {
     const int img = blockIdx.x / kGramSeg, seg = blockIdx.x - kGramSeg * img;   // slice of the image
@@ -229,10 +303,7 @@ __global__ __launch_bounds__(256) void image_gram_kernel(DevProblem P, const Cam
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ CamPre scp;
     __shared__ double sin_[4], ssc[10];
-    constexpr int kJ = 11;                     // [J_c | J_i | f]; MFMA columns 11..15 read as 0
-    __shared__ double jl[4][128 * kJ];         // per wave: 64 observations x 2 rows
-    // after the loop each wave's 16x16 tile reuses its own jl region
-    auto part = [&](int w, int i, int j) -> double& { return jl[w][i * 17 + j]; };
+    __shared__ double part[4][64], badw[4];
     if (threadIdx.x < sizeof(CamPre) / 8)
         reinterpret_cast<double*>(&scp)[threadIdx.x] = reinterpret_cast<const double*>(&cps[img])[threadIdx.x];
     if (threadIdx.x >= 64 && threadIdx.x < 68) sin_[threadIdx.x - 64] = intr[4 * P.img_intr[img] + threadIdx.x - 64];
@@ -241,9 +312,10 @@ __global__ __launch_bounds__(256) void image_gram_kernel(DevProblem P, const Cam
         ssc[a] = a < 6 ? (colc >= 0 ? P.scaleF[colc + a] : 0.0) : P.scaleF[coli + a - 6];
     }
     __syncthreads();
-    v4d acc = v4d{0.0, 0.0, 0.0, 0.0}, acc2 = acc;
-    double cost = 0.0, bad = 0.0;
-    const int kk = lane >> 4, ii = lane & 15;
+    double g[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) g[k] = 0.0;
+    double bad = 0.0;
     // software pipeline: point ids / measurements two iterations ahead, the
     // point itself one iteration ahead
     auto fetch_ids = [&](int base, int& p, double2& uv) {
@@ -269,64 +341,45 @@ __global__ __launch_bounds__(256) void image_gram_kernel(DevProblem P, const Cam
         p_c = p_n; uv_c = uv_n;
         fetch_x(p_c, x_c);
         fetch_ids(base + 512, p_n, uv_n);
-        double v[2][11];
+        // re-read the staged camera from LDS each step instead of keeping its
+        // 28 doubles live across the loop (register budget of 2 waves/SIMD)
+        asm volatile("" ::: "memory");
         if (p_cur >= 0) {
             Lin L;
             linearize<true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
-            cost += L.half_rho;
+            g[gram::kCost] += L.half_rho;
             bad = fmax(bad, L.ok ? 0.0 : 1.0);
+            // unscaled rows; the per-image column scales are applied to the sums
+            auto r = [&](int q, int i) -> double {
+                return i < 6 ? L.Jc[q][i] : i < 10 ? L.Ji[q][i - 6] : L.f[q];
+            };
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
-#pragma unroll
-                for (int a = 0; a < 6; ++a) v[r][a] = L.Jc[r][a] * ssc[a];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) v[r][6 + a] = L.Ji[r][a] * ssc[6 + a];
-                v[r][10] = L.f[r];
+            for (int s = 0; s < 62; ++s) {
+                const int i = gram::kS.i[s], j = gram::kS.j[s];
+                if (gram::in0(i) && gram::in0(j)) g[s] = fma(r(0, i), r(0, j), g[s]);
+                if (gram::in1(i) && gram::in1(j)) g[s] = fma(r(1, i), r(1, j), g[s]);
             }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (int a = 0; a < 11; ++a) v[r][a] = 0.0;
         }
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int a = 0; a < kJ; ++a) jl[wave][(2 * lane + r) * kJ + a] = v[r][a];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int nrow = 2 * min(64, o1 - base);
-        for (int k = 0; k < nrow; k += 8) {   // two independent chains (rows 0 mod 8 / 4 mod 8)
-            const double op0 = ii < kJ ? jl[wave][(k + kk) * kJ + ii] : 0.0;
-            const double op1 = (ii < kJ && k + 4 < nrow) ? jl[wave][(k + 4 + kk) * kJ + ii] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(op0, op0, acc, 0, 0, 0);
-            acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(op1, op1, acc2, 0, 0, 0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    double cs[1] = {cost};
-    wave_sum(cs);
+    gram::reduce_scatter64(g, lane);
     bad = wave_max(bad);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part(wave, kk + 4 * r, ii) = acc[r] + acc2[r];
-    if (lane == 0) { part(wave, 11, 16) = cs[0]; part(wave, 12, 16) = bad; }
+    part[wave][lane] = g[0];
+    if (lane == 0) badw[wave] = bad;
     __syncthreads();
+    auto tot = [&](int s) { return ((part[0][s] + part[1][s]) + part[2][s]) + part[3][s]; };
     if (threadIdx.x < 100) {
-        const int i = threadIdx.x / 10, j = threadIdx.x % 10;
-        const double u = ((part(0, i, j) + part(1, i, j)) + part(2, i, j)) + part(3, i, j);
+        const int i = threadIdx.x / 10, j = threadIdx.x % 10, s = gram::kS.id[i][j];
+        const double u = s >= 0 ? ssc[i] * ssc[j] * tot(s) : 0.0;
         P.U[(size_t)blockIdx.x * 100 + threadIdx.x] = u;
         if (i == j) P.Ucn[(size_t)blockIdx.x * 10 + i] = u;
     }
     if (threadIdx.x >= 128 && threadIdx.x < 138) {
         const int i = threadIdx.x - 128;
-        P.Ub[(size_t)blockIdx.x * 10 + i] = ((part(0, i, 10) + part(1, i, 10)) + part(2, i, 10)) + part(3, i, 10);
+        P.Ub[(size_t)blockIdx.x * 10 + i] = ssc[i] * tot(gram::kS.id[10][i]);
     }
     if (threadIdx.x == 192) {
-        P.part_u[2 * (size_t)blockIdx.x] = ((part(0, 11, 16) + part(1, 11, 16)) + part(2, 11, 16)) + part(3, 11, 16);
-        P.part_u[2 * (size_t)blockIdx.x + 1] = fmax(fmax(part(0, 12, 16), part(1, 12, 16)), fmax(part(2, 12, 16), part(3, 12, 16)));
+        P.part_u[2 * (size_t)blockIdx.x] = tot(gram::kCost);
+        P.part_u[2 * (size_t)blockIdx.x + 1] = fmax(fmax(badw[0], badw[1]), fmax(badw[2], badw[3]));
     }
 }
 
