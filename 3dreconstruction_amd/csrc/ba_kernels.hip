@@ -1155,8 +1155,8 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                                                          const double* __restrict__ X,
                                                          double* __restrict__ Xc, double radius) {
     __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
-    __shared__ double csy[kCamSlots][12];       // camera scaleF | yF (0 for a constant image)
-    __shared__ double isy[kIntrSlots][16];      // intrinsics | candidate | scaleF | yF
+    __shared__ double csy[kCamSlots][6];        // camera scaleF * yF (0 for a constant image)
+    __shared__ double isy[kIntrSlots][12];      // intrinsics | candidate | scaleF * yF
     const int c = blockIdx.x, tid = threadIdx.x;
     const double inv_radius = 1.0 / radius;   // as schur_kernel
     const ChunkDesc& cd = P.chunks[c];
@@ -1169,15 +1169,13 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
         }
         for (int e = tid; e < cd.n_cams * 6; e += blockDim.x) {
             const int t = e / 6, k = e - 6 * t, col = cd.cam_col[t];
-            csy[t][k] = col >= 0 ? P.scaleF[col + k] : 0.0;
-            csy[t][6 + k] = col >= 0 ? P.yF[col + k] : 0.0;
+            csy[t][k] = col >= 0 ? P.scaleF[col + k] * P.yF[col + k] : 0.0;
         }
         if (tid < 4 * cd.n_intr) {
             const int t = tid >> 2, k = tid & 3, col = cd.intr_col[t];
             isy[t][k] = intr[4 * cd.intr_id[t] + k];
             isy[t][4 + k] = intr_c[4 * cd.intr_id[t] + k];
-            isy[t][8 + k] = P.scaleF[col + k];
-            isy[t][12 + k] = P.yF[col + k];
+            isy[t][8 + k] = P.scaleF[col + k] * P.yF[col + k];
         }
     }
     __syncthreads();
@@ -1187,7 +1185,13 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
     if (p < cd.pt_end) {
         const double Xp[3] = {X[3 * (size_t)p], X[3 * (size_t)p + 1], X[3 * (size_t)p + 2]};
         const double sE[3] = {P.scaleE[3 * (size_t)p], P.scaleE[3 * (size_t)p + 1], P.scaleE[3 * (size_t)p + 2]};
-        double V[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+        // One linearisation per observation at x gathers everything the step
+        // needs: with j = J_E rows scaled by sE and q = J_F y_F (this row),
+        //   V = sum j j',  b = sum j (f - q) = bf - bq,
+        // and the model change sum m (f + m/2), m = -(q + j y_E), expands to
+        //   -(sum q f + y_E . bf) + (sum q^2 + 2 y_E . bq + y_E' V y_E) / 2.
+        double V[6] = {0, 0, 0, 0, 0, 0}, bf[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
+        double sqf = 0.0, sqq = 0.0;
         const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
         for (int o = o0; o < o1; ++o) {
             const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
@@ -1200,16 +1204,21 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                 double q = 0.0;  // (J_F y_F) for this row
                 if (cam)
 #pragma unroll
-                    for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * csy[cs][a] * csy[cs][6 + a];
+                    for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * csy[cs][a];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) q += L.Ji[r][a] * isy[is][8 + a] * isy[is][12 + a];
+                for (int a = 0; a < 4; ++a) q += L.Ji[r][a] * isy[is][8 + a];
                 const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
-                const double fr = L.f[r] - q;
+                const double fr = L.f[r];
                 V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
                 V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
-                b[0] += j0 * fr; b[1] += j1 * fr; b[2] += j2 * fr;
+                bf[0] += j0 * fr; bf[1] += j1 * fr; bf[2] += j2 * fr;
+                bq[0] += j0 * q; bq[1] += j1 * q; bq[2] += j2 * q;
+                sqf += q * fr;
+                sqq += q * q;
             }
         }
+        const double V0[6] = {V[0], V[1], V[2], V[3], V[4], V[5]};
+        const double b[3] = {bf[0] - bq[0], bf[1] - bq[1], bf[2] - bq[2]};
         const int di[3] = {0, 2, 5};
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -1232,24 +1241,19 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             Xc[3 * (size_t)p + a] = xc[a];
             if (!isfinite(xc[a])) bad = 1.0;
         }
+        {
+            const double ybf = yE[0] * bf[0] + yE[1] * bf[1] + yE[2] * bf[2];
+            const double ybq = yE[0] * bq[0] + yE[1] * bq[1] + yE[2] * bq[2];
+            const double Vy0 = V0[0] * yE[0] + V0[1] * yE[1] + V0[3] * yE[2];
+            const double Vy1 = V0[1] * yE[0] + V0[2] * yE[1] + V0[4] * yE[2];
+            const double Vy2 = V0[3] * yE[0] + V0[4] * yE[1] + V0[5] * yE[2];
+            const double yVy = yE[0] * Vy0 + yE[1] * Vy1 + yE[2] * Vy2;
+            acc[0] = -(sqf + ybf) + 0.5 * (sqq + 2.0 * ybq + yVy);
+        }
+        // candidate residuals at (x_c, candidate cameras / intrinsics)
         for (int o = o0; o < o1; ++o) {
             const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-            Lin L;
-            linearize<true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
-            const bool cam = crow_valid(cd, cs);
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                double m = 0.0;  // J_s step, step = -y
-                if (cam)
-#pragma unroll
-                    for (int a = 0; a < 6; ++a) m -= L.Jc[r][a] * csy[cs][a] * csy[cs][6 + a];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) m -= L.Ji[r][a] * isy[is][8 + a] * isy[is][12 + a];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) m -= L.Jx[r][a] * sE[a] * yE[a];
-                acc[0] += m * (L.f[r] + m / 2.0);
-            }
             Lin C;
             linearize<false, false, false>(scc[cs], &isy[is][4], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;
