@@ -330,7 +330,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         ba_finalize(P, s);
-        if (ctx->world > 1) {
+        if (ctx->world > 1 || ctx->comm) {
             ctx_allreduce(ctx, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);
             ctx_allreduce(ctx, P.scal + kScMaxBegin, kScMaxEnd - kScMaxBegin, 1, s);
         }

@@ -82,7 +82,7 @@ extern "C" const char* sfm_version(void) { return "sfmcore 0.1.0 (gfx950)"; }
 extern "C" const char* sfm_last_error(void) { return g_err.c_str(); }
 
 void sfm::ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStream_t s) {
-    if (ctx->world <= 1 || n == 0) return;
+    if (n == 0 || (ctx->world <= 1 && !ctx->comm)) return;   // a 1-rank RCCL comm still runs
     if (!ctx->host_allreduce) {
         SFM_REQUIRE(rccl_allreduce_f64(ctx->comm, dev_buf, n, op_max, s) == 0, SFM_ERR_COMM,
                     "RCCL all-reduce failed");
@@ -141,7 +141,7 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         if (c->world > 1 && opts->allreduce && !opts->comm_id) {
             c->host_allreduce = opts->allreduce;
             c->host_allreduce_user = opts->allreduce_user;
-        } else if (c->world > 1) {
+        } else if (c->world > 1 || opts->comm_id) {   // comm_id at world_size 1: a 1-rank RCCL comm
             SFM_REQUIRE(opts->comm_id, SFM_ERR_INVALID_ARG, "world_size>1 needs comm_id or an allreduce hook");
             try {
                 rccl_comm_init(&c->comm, c->world, opts->comm_id, c->rank);

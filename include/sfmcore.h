@@ -63,7 +63,9 @@ typedef struct sfm_ctx_opts {
     int32_t reserved;
     const uint8_t* comm_id;  /* 128-byte RCCL unique id from rank 0's
                                 sfm_comm_unique_id(); NULL when world_size==1
-                                or when `allreduce` is given                  */
+                                or when `allreduce` is given (at world_size 1
+                                it builds a 1-rank communicator: the RCCL
+                                exchanges run and are identities)             */
     sfm_allreduce_fn allreduce; /* optional (world_size > 1, comm_id NULL):
                                 the per-iteration exchanges are staged through
                                 pinned host memory and handed to this hook

@@ -245,3 +245,21 @@ def test_sharded_two_ranks_one_gpu(ctx, tmp_path, scene_args):
     assert abs(float(r["cost"]) / gs.final_cost - 1) < 2e-6
     np.testing.assert_allclose(r["e"], e, atol=2e-3)
     np.testing.assert_allclose(r["x"], x, atol=5e-3 * (np.abs(x).max() + 1))
+
+
+def test_rccl_single_rank_communicator(ctx):
+    """The RCCL binding end to end on one GPU: a 1-rank communicator runs every
+    per-iteration all-reduce (identities), so the solve must be bit-identical
+    to the communicator-free one."""
+    sc = H.Scene(n_cam=24, n_pt=2000, k=6, seed=5)
+    e0, i0, x0 = sc.params()
+    rc, s0 = api.ba_solve(ctx, sc.problem(), e0, i0, x0)
+    c1 = api.Context(device=0, rank=0, world_size=1, comm_id=api.comm_unique_id())
+    try:
+        e1, i1, x1 = sc.params()
+        rc1, s1 = api.ba_solve(c1, sc.problem(), e1, i1, x1)
+    finally:
+        c1.close()
+    assert rc == rc1 == 0
+    assert s1.iterations == s0.iterations and s1.final_cost == s0.final_cost
+    assert np.array_equal(e1, e0) and np.array_equal(x1, x0)
