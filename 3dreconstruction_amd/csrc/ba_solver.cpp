@@ -51,6 +51,8 @@ struct sfm_ba_plan {
     DBuf<double> img_uv;
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
     DBuf<unsigned long long> bcr_stamps;   // SFM_BCR_STAMPS=1 diagnostic
+    DBuf<double> scal_g;                   // [world][kScMaxEnd] gathered partial scalars
+    std::vector<double> scal_gh;
     BcrArgs bcr;
     bool use_bcr = false;
     int64_t rcs_n = 0;
@@ -167,6 +169,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->part_s.alloc(2 * std::max<size_t>(h.chunks.size(), 1));
     pl->scal.alloc(kScCount);
     pl->scal.zero(s);
+    if (ctx->comm) {
+        pl->scal_g.alloc((size_t)ctx->world * kScMaxEnd);
+        pl->scal_gh.assign(pl->scal_g.n, 0.0);
+    }
     SFM_HIP(hipHostMalloc((void**)&pl->scal_h, kScCount * sizeof(double), hipHostMallocDefault));
 
     DevProblem& P = pl->P;
@@ -330,12 +336,30 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         ba_finalize(P, s);
-        if (ctx->world > 1 || ctx->comm) {
-            ctx_allreduce(ctx, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);
-            ctx_allreduce(ctx, P.scal + kScMaxBegin, kScMaxEnd - kScMaxBegin, 1, s);
+        if (ctx->comm && !ctx->host_allreduce) {
+            // one RCCL collective: gather every rank's partial scalars, then sum
+            // (rank order) / max them on the host
+            SFM_REQUIRE(rccl_allgather_f64(ctx->comm, P.scal, pl->scal_g.p, kScMaxEnd, s) == 0, SFM_ERR_COMM,
+                        "RCCL all-gather failed");
+            SFM_HIP(hipMemcpyAsync(pl->scal_h, P.scal, kScCount * 8, hipMemcpyDeviceToHost, s));
+            SFM_HIP(hipMemcpyAsync(pl->scal_gh.data(), pl->scal_g.p, pl->scal_g.n * 8, hipMemcpyDeviceToHost, s));
+            SFM_HIP(hipStreamSynchronize(s));
+            for (int k = kScSumBegin; k < kScMaxEnd; ++k) {
+                double v = pl->scal_gh[k];
+                for (int r = 1; r < ctx->world; ++r) {
+                    const double w = pl->scal_gh[(size_t)r * kScMaxEnd + k];
+                    v = k < kScSumEnd ? v + w : std::max(v, w);
+                }
+                pl->scal_h[k] = v;
+            }
+        } else {
+            if (ctx->world > 1) {
+                ctx_allreduce(ctx, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);
+                ctx_allreduce(ctx, P.scal + kScMaxBegin, kScMaxEnd - kScMaxBegin, 1, s);
+            }
+            SFM_HIP(hipMemcpyAsync(pl->scal_h, P.scal, kScCount * 8, hipMemcpyDeviceToHost, s));
+            SFM_HIP(hipStreamSynchronize(s));
         }
-        SFM_HIP(hipMemcpyAsync(pl->scal_h, P.scal, kScCount * 8, hipMemcpyDeviceToHost, s));
-        SFM_HIP(hipStreamSynchronize(s));
         if (timed) {
             float ms = 0.f;
             SFM_HIP(hipEventElapsedTime(&ms, pl->ev[ev_i], pl->ev[ev_i + 1]));

@@ -57,6 +57,8 @@ int guarded(F&& body) {
 struct Rccl;
 const Rccl* rccl();  // throws SFM_ERR_COMM if unavailable
 int rccl_allreduce_f64(void* comm, double* buf, size_t n, int op_max, hipStream_t s);
+// out[world][n] <- every rank's in[n] (RCCL communicator only)
+int rccl_allgather_f64(void* comm, const double* in, double* out, size_t n, hipStream_t s);
 // All-reduce of a device buffer across the context's ranks (RCCL, or the
 // host hook through pinned memory); no-op at world 1.
 void ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStream_t s);

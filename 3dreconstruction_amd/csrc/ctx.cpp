@@ -26,6 +26,7 @@ struct Rccl {
     decltype(&ncclCommInitRank) comm_init_rank = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
@@ -42,8 +43,10 @@ const Rccl* rccl() {
         r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
         r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
         r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
         r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-        ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.error_string;
+        ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.all_gather &&
+             r.error_string;
     });
     SFM_REQUIRE(ok, SFM_ERR_COMM, "RCCL (librccl.so.1) not available");
     return &r;
@@ -70,6 +73,13 @@ int rccl_allreduce_f64(void* comm, double* buf, size_t n, int op_max, hipStream_
     ncclResult_t e = r->all_reduce(buf, buf, n, ncclFloat64, op_max ? ncclMax : ncclSum,
                                    (ncclComm_t)comm, s);
     SFM_REQUIRE(e == ncclSuccess, SFM_ERR_COMM, "ncclAllReduce: %s", r->error_string(e));
+    return SFM_OK;
+}
+
+int rccl_allgather_f64(void* comm, const double* in, double* out, size_t n, hipStream_t s) {
+    const Rccl* r = rccl();
+    ncclResult_t e = r->all_gather(in, out, n, ncclFloat64, (ncclComm_t)comm, s);
+    SFM_REQUIRE(e == ncclSuccess, SFM_ERR_COMM, "ncclAllGather: %s", r->error_string(e));
     return SFM_OK;
 }
 
