@@ -295,15 +295,17 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
 }
 
 // ---- pack: band (6x6 blocks) -> 64x64 super-blocks, D^2 added, identity pad --
+// One workgroup per 4 rows of a super-block (N * 16 workgroups).
 __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
-    const int I = blockIdx.x;
+    const int I = blockIdx.x >> 4, rg = blockIdx.x & 15;
     double* A = b.A + (size_t)I * M * M;
     double* Cm = b.C + (size_t)I * M * M;
     double* R = b.R + (size_t)I * M * b.nrhs;
     double* R0 = b.R0 + (size_t)I * M * b.nrhs;
     const int c0 = I * b.K, nreal = min(b.K, P.ncam - c0) * 6;
     const int Dp = P.D + 1;
-    for (int e = threadIdx.x; e < M * M; e += NT) {
+    {
+        const int e = 4 * rg * M + threadIdx.x;   // NT = 4 rows x 64 columns
         const int r = e / M, c = e % M;
         double a = 0.0, cc = 0.0;
         if (r < nreal) {
@@ -335,7 +337,7 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
         Cm[e] = cc;
     }
     // R: column 0 = rhs, columns 1 + 4k + a = arrow (intr k, row a) transposed
-    for (int e = threadIdx.x; e < M * b.nrhs; e += NT) {
+    for (int e = 4 * rg * b.nrhs + threadIdx.x; e < 4 * (rg + 1) * b.nrhs; e += NT) {
         const int r = e / b.nrhs, c = e % b.nrhs;
         double v = 0.0;
         if (r < nreal) {
@@ -349,7 +351,7 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
         R[e] = v;
         R0[e] = v;
     }
-    if (I == 0 && threadIdx.x == 0) *b.fail = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *b.fail = 0.0;
 }
 
 // ---- update of one 16-row tile w of an even block j after eliminating its odd
@@ -508,21 +510,45 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
 }
 
 // ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------
-__global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b) {
+// sp > 0: first block 0's update from its right neighbour sp, eliminated by
+// the last level (A_0 -= Wl_sp' Wl_sp, R_0 -= Wl_sp' z_sp; lower tiles only).
+__global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b, int sp) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int ldr = b.nrhs + 1;
     double* A = sm;
     double* X = A + M * LD;
     double* R = X + M * LD;
     double* T = R + M * ldr;
-    double* sc = T + M * ldr;
+    double* Wb = T + M * ldr;       // [64][LD] Wl_sp
+    double* Zb = Wb + M * LD;       // [64][ldr] z_sp
+    double* sc = Zb + M * ldr;
     double* bad = sc + 33;
     const int wave = threadIdx.x >> 6;
+    const bool upd = sp > 0 && sp < b.N;
     if (threadIdx.x == 0) bad[0] = 0.0;
     load_rows(A, LD, b.A, M, M);
     load_rows(R, ldr, b.R, b.nrhs, b.nrhs);
+    if (upd) {
+        load_rows(Wb, LD, b.Wl + (size_t)sp * M * M, M, M);
+        load_rows(Zb, ldr, b.Z + (size_t)sp * M * b.nrhs, b.nrhs, b.nrhs);
+    }
     for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
     __syncthreads();
+    if (upd) {
+        for (int q = wave; q < 10; q += 4) {
+            const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
+            const int tj = q - ti * (ti + 1) / 2;
+            v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
+            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, M);
+            tile_st(A, LD, 16 * ti, 16 * tj, acc);
+        }
+        for (int tj = 0; tj < b.nrhs / 16; ++tj) {
+            v4d acc = tile_ld(R, ldr, 16 * wave, 16 * tj);
+            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * wave, Zb, ldr, 16 * tj, 0, M);
+            tile_st(R, ldr, 16 * wave, 16 * tj, acc);
+        }
+        __syncthreads();
+    }
     chol_inv64(A, X, bad, sc);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     for (int tj = 0; tj < b.nrhs / 16; ++tj)
@@ -597,26 +623,36 @@ __global__ __launch_bounds__(64) void bcr_corner_part_kernel(BcrArgs b, int na4)
 __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
     const int na4 = 4 * P.nintr;
     __shared__ double Mc[16 * 16 + 16];
-    auto sum_parts = [&](int off) {   // fixed order; loads unrolled to overlap
+    // partials of super-blocks [g N/8, (g+1) N/8) per lane, the 8 lanes of an
+    // element then combined by a fixed xor butterfly (deterministic)
+    auto sum_parts = [&](int off, int g) {
+        const int I0 = b.N * g / 8, I1 = b.N * (g + 1) / 8;
         double t = 0.0;
-#pragma unroll 16
-        for (int I = 0; I < b.N; ++I) t += b.part[(size_t)I * 512 + off];
+#pragma unroll 4
+        for (int I = I0; I < I1; ++I) t += b.part[(size_t)I * 512 + off];
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o);
         return t;
     };
-    if (threadIdx.x < na4 * na4) {
-        const int a = threadIdx.x / na4, c = threadIdx.x % na4;
-        const double red = sum_parts(a * 16 + c);
-        double m = P.Scorner[(((size_t)(a / 4) * P.nintr + c / 4) * 16) + (a % 4) * 4 + c % 4];
-        if (a == c) {
-            const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
-            m += lm * lm;
+    const int el = threadIdx.x >> 3, g = threadIdx.x & 7;   // 32 elements x 8 lanes per pass
+    for (int base = 0; base < na4 * na4 + na4; base += NT / 8) {
+        const int k = base + el;
+        if (k < na4 * na4) {
+            const int a = k / na4, c = k % na4;
+            const double red = sum_parts(a * 16 + c, g);
+            if (g == 0) {
+                double m = P.Scorner[(((size_t)(a / 4) * P.nintr + c / 4) * 16) + (a % 4) * 4 + c % 4];
+                if (a == c) {
+                    const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
+                    m += lm * lm;
+                }
+                Mc[a * 16 + c] = m - red;
+            }
+        } else if (k < na4 * na4 + na4) {
+            const int a = k - na4 * na4;
+            const double red = sum_parts(256 + a * 16, g);
+            if (g == 0) Mc[256 + a] = P.rhs[P.nb + a] - red;
         }
-        Mc[a * 16 + c] = m - red;
-    }
-    if (threadIdx.x < na4) {
-        const int a = threadIdx.x;
-        const double red = sum_parts(256 + a * 16);
-        Mc[256 + a] = P.rhs[P.nb + a] - red;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -685,13 +721,13 @@ void bcr_bind(BcrArgs& b, double* base) {
 }
 
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s) {
-    hipLaunchKernelGGL(bcr_pack_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
+    hipLaunchKernelGGL(bcr_pack_kernel, dim3(16 * b.N), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());
     const size_t ldr = b.nrhs + 1;
     const size_t lds_odd = (2 * M * LD + 2 * M * M + 2 * M * 17 + 16 * LD + 18) * sizeof(double);
     const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);
     const size_t lds_l = std::max(lds_odd, lds_even);
-    const size_t lds_t = (2 * M * LD + 2 * M * ldr + 34) * sizeof(double);
+    const size_t lds_t = (3 * M * LD + 3 * M * ldr + 34) * sizeof(double);
     const size_t lds_b = (3 * M * LD + 3 * M * ldr) * sizeof(double);
     static bool attr = false;
     if (!attr) {   // sized for the largest nrhs (32)
@@ -709,11 +745,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
-    if (s_top > 1) {   // block 0's update from the last level
-        hipLaunchKernelGGL(bcr_level_kernel, dim3(4), dim3(NT), lds_l, s, b, s_top, 0);
-        SFM_HIP(hipGetLastError());
-    }
-    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NT), lds_t, s, b);
+    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NT), lds_t, s, b, s_top / 2);
     SFM_HIP(hipGetLastError());
     for (int stride = s_top / 2; stride >= 1; stride /= 2) {
         if (stride >= b.N) continue;

@@ -323,9 +323,12 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     };
 
     double prev_gmax = 0.0;
+    int step_no = 0;
     while (term < 0) {
         // ---- one step on the device ------------------------------------------
-        const bool timed = ev_i + 1 < (int)pl->ev.size();
+        // the Schur launch is timed with events on the first two steps of each
+        // solve only: an event pair costs ~12 us of stream serialisation
+        const bool timed = step_no++ < 2;
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p);
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
