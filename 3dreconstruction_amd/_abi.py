@@ -105,6 +105,21 @@ class MatchOptions(C.Structure):
     _fields_ = [("mode", C.c_int32), ("ratio", C.c_float)]
 
 
+class MvgView(C.Structure):
+    _fields_ = [("id_view", C.c_uint32), ("id_intrinsic", C.c_uint32), ("id_pose", C.c_uint32),
+                ("width", C.c_uint32), ("height", C.c_uint32), ("img_path", C.c_char * 500)]
+
+
+class SparseMatchOpts(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("ratio", C.c_float), ("force", C.c_int32),
+                ("dedup_xy", C.c_int32), ("reserved", C.c_int32 * 2)]
+
+
+class SparseMatchStats(C.Structure):
+    _fields_ = [("n_views", C.c_int64), ("n_pairs_in", C.c_int64), ("n_pairs_out", C.c_int64),
+                ("n_matches", C.c_int64), ("reloaded", C.c_int32), ("reserved", C.c_int32)]
+
+
 def default_options():
     o = BAOptions()
     o.max_num_iterations = 50
@@ -155,6 +170,19 @@ SIGNATURES = [
     ("sfm_match_plan_destroy", C.c_int, [C.c_void_p]),
     ("sfm_exhaustive_pairs", C.c_int, [C.c_int32, i32p]),
     ("sfm_synth_descriptors", C.c_int, [C.c_int32, C.c_int32, C.c_uint64, u8p]),
+    ("sfm_mvg_load_views", C.c_int, [C.c_char_p, C.POINTER(MvgView), C.c_int32, i32p]),
+    ("sfm_mvg_check_describer", C.c_int, [C.c_char_p]),
+    ("sfm_mvg_read_desc", C.c_int, [C.c_char_p, u8p, C.c_int64, i64p]),
+    ("sfm_mvg_write_desc", C.c_int, [C.c_char_p, u8p, C.c_int64]),
+    ("sfm_mvg_read_feat", C.c_int, [C.c_char_p, C.POINTER(C.c_float), C.c_int64, i64p]),
+    ("sfm_mvg_load_pairs", C.c_int, [C.c_char_p, C.c_int32, i32p, C.c_int64, i64p]),
+    ("sfm_mvg_save_pairs", C.c_int, [C.c_char_p, i32p, C.c_int64]),
+    ("sfm_mvg_save_matches", C.c_int, [C.c_char_p, i32p, C.c_int64, i64p, u32p, u32p]),
+    ("sfm_mvg_load_matches", C.c_int, [C.c_char_p, i32p, i64p, u32p, u32p, C.c_int64, C.c_int64,
+                                       i64p, i64p]),
+    ("sfm_sparse_match_pair", C.c_int, [C.c_char_p]),
+    ("sfm_sparse_match", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SparseMatchOpts),
+                                   C.POINTER(SparseMatchStats)]),
 ]
 
 _lib = None

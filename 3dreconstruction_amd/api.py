@@ -272,3 +272,119 @@ def ba_partition(problem, world_size):
     _check(lib.sfm_ba_partition(C.byref(problem), world_size, abi.ptr(order, abi.i64p),
                                 abi.ptr(bounds, abi.i64p)), "sfm_ba_partition")
     return order[:problem.n_pt], bounds
+
+
+# ---------------------------------------------------------------------------
+# file-staged sparseBuilder flow (OpenMVG stage-boundary formats)
+# ---------------------------------------------------------------------------
+def _b(path):
+    return str(path).encode()
+
+
+def mvg_load_views(path):
+    """sfm_data.json VIEWS -> list of dicts sorted by id_view."""
+    lib = abi.load()
+    n = C.c_int32()
+    _check(lib.sfm_mvg_load_views(_b(path), None, 0, C.byref(n)), "sfm_mvg_load_views")
+    v = (abi.MvgView * max(n.value, 1))()
+    _check(lib.sfm_mvg_load_views(_b(path), v, n.value, C.byref(n)), "sfm_mvg_load_views")
+    return [{"id_view": x.id_view, "id_intrinsic": x.id_intrinsic, "id_pose": x.id_pose,
+             "width": x.width, "height": x.height, "img_path": x.img_path.decode()}
+            for x in v[:n.value]]
+
+
+def mvg_check_describer(path):
+    _check(abi.load().sfm_mvg_check_describer(_b(path)), "sfm_mvg_check_describer")
+
+
+def mvg_read_desc(path):
+    lib = abi.load()
+    n = C.c_int64()
+    _check(lib.sfm_mvg_read_desc(_b(path), None, 0, C.byref(n)), "sfm_mvg_read_desc")
+    d = np.zeros((max(n.value, 1), 128), np.uint8)
+    _check(lib.sfm_mvg_read_desc(_b(path), abi.ptr(d, abi.u8p), n.value, C.byref(n)),
+           "sfm_mvg_read_desc")
+    return d[:n.value]
+
+
+def mvg_write_desc(path, desc):
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 128)
+    _check(abi.load().sfm_mvg_write_desc(_b(path), abi.ptr(d, abi.u8p), d.shape[0]),
+           "sfm_mvg_write_desc")
+
+
+def mvg_read_feat(path):
+    lib = abi.load()
+    n = C.c_int64()
+    _check(lib.sfm_mvg_read_feat(_b(path), None, 0, C.byref(n)), "sfm_mvg_read_feat")
+    f = np.zeros((max(n.value, 1), 4), np.float32)
+    _check(lib.sfm_mvg_read_feat(_b(path), f.ctypes.data_as(C.POINTER(C.c_float)), n.value,
+                                 C.byref(n)), "sfm_mvg_read_feat")
+    return f[:n.value]
+
+
+def mvg_load_pairs(path, n_views):
+    lib = abi.load()
+    n = C.c_int64()
+    _check(lib.sfm_mvg_load_pairs(_b(path), n_views, None, 0, C.byref(n)), "sfm_mvg_load_pairs")
+    p = np.zeros((max(n.value, 1), 2), np.int32)
+    _check(lib.sfm_mvg_load_pairs(_b(path), n_views, abi.ptr(p, abi.i32p), n.value, C.byref(n)),
+           "sfm_mvg_load_pairs")
+    return p[:n.value]
+
+
+def mvg_save_pairs(path, pairs):
+    p = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    _check(abi.load().sfm_mvg_save_pairs(_b(path), abi.ptr(p, abi.i32p), p.shape[0]),
+           "sfm_mvg_save_pairs")
+
+
+def mvg_save_matches(path, matches):
+    """matches: {(I, J): int array [n, 2] of (i, j)} -> PairWiseMatches file."""
+    keys = sorted(matches)
+    pairs = np.array(keys, np.int32).reshape(-1, 2)
+    counts = np.array([len(matches[k]) for k in keys], np.int64)
+    ij = np.concatenate([np.asarray(matches[k], np.uint32).reshape(-1, 2) for k in keys]) \
+        if keys else np.zeros((0, 2), np.uint32)
+    i = np.ascontiguousarray(ij[:, 0])
+    j = np.ascontiguousarray(ij[:, 1])
+    _check(abi.load().sfm_mvg_save_matches(_b(path), abi.ptr(pairs, abi.i32p), len(keys),
+                                           abi.ptr(counts, abi.i64p), abi.ptr(i, abi.u32p),
+                                           abi.ptr(j, abi.u32p)), "sfm_mvg_save_matches")
+
+
+def mvg_load_matches(path):
+    """PairWiseMatches file -> {(I, J): uint32 array [n, 2]} (map order)."""
+    lib = abi.load()
+    npair, nm = C.c_int64(), C.c_int64()
+    _check(lib.sfm_mvg_load_matches(_b(path), None, None, None, None, 0, 0, C.byref(npair),
+                                    C.byref(nm)), "sfm_mvg_load_matches")
+    pairs = np.zeros((max(npair.value, 1), 2), np.int32)
+    counts = np.zeros(max(npair.value, 1), np.int64)
+    i = np.zeros(max(nm.value, 1), np.uint32)
+    j = np.zeros(max(nm.value, 1), np.uint32)
+    _check(lib.sfm_mvg_load_matches(_b(path), abi.ptr(pairs, abi.i32p), abi.ptr(counts, abi.i64p),
+                                    abi.ptr(i, abi.u32p), abi.ptr(j, abi.u32p), npair.value,
+                                    nm.value, C.byref(npair), C.byref(nm)), "sfm_mvg_load_matches")
+    out, off = {}, 0
+    for k in range(npair.value):
+        c = int(counts[k])
+        out[(int(pairs[k, 0]), int(pairs[k, 1]))] = np.stack([i[off:off + c], j[off:off + c]], 1)
+        off += c
+    return out
+
+
+def sparse_match_pair(matches_dir):
+    """sparseBuilder::matchPair(): writes <matches_dir>/pairs.bin."""
+    _check(abi.load().sfm_sparse_match_pair(_b(matches_dir)), "sfm_sparse_match_pair")
+
+
+def sparse_match(ctx, matches_dir, mode=abi.SFM_MATCH_RATIO, ratio=0.8, force=False, dedup_xy=True):
+    """sparseBuilder::match(), file-staged, on the GPU matcher."""
+    o = abi.SparseMatchOpts()
+    o.mode, o.ratio, o.force, o.dedup_xy = mode, ratio, int(force), int(dedup_xy)
+    st = abi.SparseMatchStats()
+    _check(ctx.lib.sfm_sparse_match(ctx.h, _b(matches_dir), C.byref(o), C.byref(st)),
+           "sfm_sparse_match")
+    return {"n_views": st.n_views, "n_pairs_in": st.n_pairs_in, "n_pairs_out": st.n_pairs_out,
+            "n_matches": st.n_matches, "reloaded": bool(st.reloaded)}

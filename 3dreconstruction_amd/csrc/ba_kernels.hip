@@ -525,28 +525,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
     double xn2 = 0.0, gmx = 0.0;
     __syncthreads();
+    // A batch's observation stream (uv, slot) and point data (X, column scale)
+    // are fetched one batch ahead, so their HBM latency overlaps the current
+    // batch's compute instead of opening every batch.
+    struct BatchIn {
+        int npts, slot, pl;
+        double u0, u1, Xp[3], sE[3];
+    };
+    auto fetch = [&](int q0, BatchIn& in) {
+        in.npts = q0 < np ? batch_points<SP, SO>(cpoff, q0, np) : 0;
+        in.slot = 0; in.pl = 0; in.u0 = 0.0; in.u1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { in.Xp[k] = 0.0; in.sE[k] = 1.0; }
+        const int qo = cpoff[q0 < np ? q0 : np];
+        if (lane < cpoff[q0 + in.npts] - qo) {
+            const int o = ob0 + qo + lane;
+            in.slot = P.obs_slot[o];
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+            in.u0 = uv.x; in.u1 = uv.y;
+#pragma unroll
+            for (int j = 1; j < SP; ++j) in.pl += (j < in.npts && cpoff[q0 + j] - qo <= lane) ? 1 : 0;
+            const size_t g = 3 * (size_t)(pb + q0 + in.pl);   // same address for the point's lanes
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { in.Xp[k] = X[g + k]; in.sE[k] = P.scaleE[g + k]; }
+        }
+    };
+    BatchIn nx;
+    fetch(0, nx);
     for (int p0 = 0; p0 < np;) {
-        const int npts = batch_points<SP, SO>(cpoff, p0, np);   // batch [p0, p1)
+        const int npts = nx.npts;   // batch [p0, p1)
         if (npts == 0) break;   // a point above SO observations: excluded by the planner
         const int p1 = p0 + npts;
         const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
+        const int slot = nx.slot, pl = nx.pl;
+        const double u0 = nx.u0, u1 = nx.u1;
+        const double Xp[3] = {nx.Xp[0], nx.Xp[1], nx.Xp[2]}, sE[3] = {nx.sE[0], nx.sE[1], nx.sE[2]};
+        fetch(p1, nx);
 #pragma unroll
         for (int e = lane; e < kPK * kPS / 2; e += 64)
             reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
         if (NT == 4 && lane < kPK) wcol[lane] = 0.0;   // columns past 3 * npts stay zero
-        int slot = 0, pl = 0;
-        double u0 = 0.0, u1 = 0.0, Xp[3] = {0.0, 0.0, 0.0}, sE[3] = {1.0, 1.0, 1.0};
-        if (lane < nobs) {
-            const int o = ob0 + o0 + lane;
-            slot = P.obs_slot[o];
-            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-            u0 = uv.x; u1 = uv.y;
-#pragma unroll
-            for (int j = 1; j < SP; ++j) pl += (j < npts && cpoff[p0 + j] - o0 <= lane) ? 1 : 0;
-            const size_t g = 3 * (size_t)(pb + p0 + pl);   // same address for the point's lanes
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { Xp[k] = X[g + k]; sE[k] = P.scaleE[g + k]; }
-        }
         SFM_STAMP(0)
         // ---- A: observations -> scaled, corrected Jacobians -----------------
         Lin L;
@@ -1193,9 +1211,16 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
         double V[6] = {0, 0, 0, 0, 0, 0}, bf[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
         double sqf = 0.0, sqq = 0.0;
         const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+        // the next observation's (slot, uv) is loaded while this one is linearised
+        int nslot = o0 < o1 ? P.obs_slot[o0] : 0;
+        double2 nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
         for (int o = o0; o < o1; ++o) {
-            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
-            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+            const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
+            const double2 uv = nuv;
+            if (o + 1 < o1) {
+                nslot = P.obs_slot[o + 1];
+                nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
+            }
             Lin L;
             linearize<true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
             const bool cam = crow_valid(cd, cs);
@@ -1251,9 +1276,15 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             acc[0] = -(sqf + ybf) + 0.5 * (sqq + 2.0 * ybq + yVy);
         }
         // candidate residuals at (x_c, candidate cameras / intrinsics)
+        nslot = o0 < o1 ? P.obs_slot[o0] : 0;
+        nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
         for (int o = o0; o < o1; ++o) {
-            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
-            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+            const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
+            const double2 uv = nuv;
+            if (o + 1 < o1) {
+                nslot = P.obs_slot[o + 1];
+                nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
+            }
             Lin C;
             linearize<false, false, false>(scc[cs], &isy[is][4], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;

@@ -7,8 +7,8 @@
 //   sparse::sparseBuilder src/sparseBuilder/sparseBuilder.h:14-39 — matchPair()
 //                         (exhaustive pairs, .cpp:758-807) and match()
 //                         (Matcher_Regions(0.8, BRUTE_FORCE_L2), .cpp:809-1023)
-//                         on in-memory regions; the OpenMVG file formats of the
-//                         reference stages are out of this build's scope.
+//                         file-staged over <base>/output/matches in OpenMVG's
+//                         formats (csrc/mvg_io.cpp), or on in-memory regions.
 //
 // Header-only; link with -lsfmcore.  Errors: the reference prints and leaves
 // the world untouched on BA failure (BundleAdjuster.h:128-131); so does this
@@ -308,23 +308,47 @@ struct IndMatch {  // openMVG::matching::IndMatch
 using Pair = std::pair<uint32_t, uint32_t>;
 using PairWiseMatches = std::map<Pair, std::vector<IndMatch>>;
 
-// In-memory counterpart of the reference's file-staged sparseBuilder stages
-// matchPair() + match() (sparseBuilder.cpp:758-1023).
+// sparse::sparseBuilder (sparseBuilder.h:14-39).  Constructed on a base path
+// like the reference's, matchPair() / match() are the file-staged stages of
+// sparseBuilder.cpp:758-1023 over <base>/output/matches (sfm_data.json,
+// image_describer.json, <stem>.desc/.feat, pairs.bin -> matches.putative.bin,
+// preemptive_pairs.txt), with the GPU matcher in place of the OpenMVG
+// collection matcher.  Errors print and return, as the reference's
+// OPENMVG_LOG_ERROR + return does (:825-878); lastError() keeps the code.
+// exhaustive() / matchRegions() are the same stages on in-memory regions.
 class sparseBuilder {
    public:
     explicit sparseBuilder(Context& ctx = Context::thread_default()) : ctx_(&ctx) {}
-    // regions: per view, n x 128 uint8 descriptors
+    explicit sparseBuilder(const std::string& base_path, Context& ctx = Context::thread_default())
+        : ctx_(&ctx), matches_dir_(base_path + "/output/matches") {}
+
+    const std::string& matchesDir() const { return matches_dir_; }
+    int lastError() const { return last_rc_; }
+
+    // exhaustivePairs(#views) -> pairs.bin (:758-807)
+    void matchPair() {
+        last_rc_ = sfm_sparse_match_pair(matches_dir_.c_str());
+        if (last_rc_ != SFM_OK) std::fprintf(stderr, "matchPair failed: %s\n", sfm_last_error());
+    }
+    // Matcher_Regions(fDistRatio = 0.8f, BRUTE_FORCE_L2) over pairs.bin (:809-1023)
+    void match(float dist_ratio = 0.8f, bool force = false) {
+        sfm_sparse_match_opts o{SFM_MATCH_RATIO, dist_ratio, force ? 1 : 0, 1, {0, 0}};
+        last_rc_ = sfm_sparse_match(ctx_->get(), matches_dir_.c_str(), &o, &stats_);
+        if (last_rc_ != SFM_OK) std::fprintf(stderr, "match failed: %s\n", sfm_last_error());
+    }
+    const sfm_sparse_match_stats& stats() const { return stats_; }
+
+    // in-memory regions: per view, n x 128 uint8 descriptors
     void setRegions(std::vector<std::vector<uint8_t>> regions) { regions_ = std::move(regions); }
     // exhaustivePairs(N) (:786)
-    std::vector<Pair> matchPair() const {
+    std::vector<Pair> exhaustive() const {
         std::vector<Pair> p;
         const uint32_t n = (uint32_t)regions_.size();
         for (uint32_t i = 0; i < n; ++i)
             for (uint32_t j = i + 1; j < n; ++j) p.emplace_back(i, j);
         return p;
     }
-    // Matcher_Regions(fDistRatio = 0.8, BRUTE_FORCE_L2) (:812, :919-921)
-    PairWiseMatches match(const std::vector<Pair>& pairs, float dist_ratio = 0.8f) const {
+    PairWiseMatches matchRegions(const std::vector<Pair>& pairs, float dist_ratio = 0.8f) const {
         std::vector<uint8_t> desc;
         std::vector<int64_t> off(1, 0);
         for (auto& r : regions_) {
@@ -356,6 +380,9 @@ class sparseBuilder {
 
    private:
     Context* ctx_;
+    std::string matches_dir_;
+    int last_rc_ = SFM_OK;
+    sfm_sparse_match_stats stats_{};
     std::vector<std::vector<uint8_t>> regions_;
 };
 

@@ -281,6 +281,69 @@ int sfm_exhaustive_pairs(int32_t n_img, int32_t* pairs);
 int sfm_synth_descriptors(int32_t n_img, int32_t n_kp, uint64_t seed,
                           uint8_t* desc /* [n_img*n_kp*128] */);
 
+/* ------------------------------------------------------------------------ */
+/* File-staged sparseBuilder flow.                   */
+/* The reference's matchPair()/match() (sparseBuilder.cpp:758-1023) talk to  */
+/* each other through files in <base>/output/matches written by OpenMVG's    */
+/* Load/Save (cereal).  These functions read and write the same layouts      */
+/* natively (restated from OpenMVG's published code; OpenMVG is un-vendored, */
+/* so byte parity is unpinned — DESIGN.md §3).  Pass NULL output arrays to   */
+/* query sizes first.                                                        */
+/* ------------------------------------------------------------------------ */
+typedef struct sfm_mvg_view {  /* openMVG::sfm::View                         */
+    uint32_t id_view, id_intrinsic, id_pose, width, height;
+    char img_path[500];        /* View::s_Img_path = local_path/filename      */
+} sfm_mvg_view;
+
+/* [cpu] VIEWS of an sfm_data.json (Load(sfm_data, ..., VIEWS), :773, :835),
+ * sorted by id_view. */
+int sfm_mvg_load_views(const char* sfm_data_json, sfm_mvg_view* views,
+                       int32_t cap, int32_t* n_views);
+/* [cpu] image_describer.json names 128-D uint8 SIFT_Regions (:851-856);
+ * other region types return SFM_ERR_UNSUPPORTED. */
+int sfm_mvg_check_describer(const char* image_describer_json);
+/* [cpu] <stem>.desc: uint64 count, count x 128 uint8 (saveDescsToBinFile). */
+int sfm_mvg_read_desc(const char* path, uint8_t* desc, int64_t cap_rows, int64_t* n_rows);
+int sfm_mvg_write_desc(const char* path, const uint8_t* desc, int64_t n_rows);
+/* [cpu] <stem>.feat: text "x y scale orientation" per keypoint (SIOPointFeature). */
+int sfm_mvg_read_feat(const char* path, float* xyso /* [4*n] */, int64_t cap_rows, int64_t* n_rows);
+/* [cpu] pairs.bin (text despite its name): loadPairs(N, ...) / savePairs
+ * (:801, :948): lines "I J1 J2 ...", stored as sorted unique (min, max). */
+int sfm_mvg_load_pairs(const char* path, int32_t n_views, int32_t* pairs, int64_t cap,
+                       int64_t* n_pairs);
+int sfm_mvg_save_pairs(const char* path, const int32_t* pairs, int64_t n_pairs);
+/* [cpu] PairWiseMatches Save/Load (:986, :896): ".bin" = cereal
+ * PortableBinary (uint8 1; uint64 #pairs; per pair uint32 I, J, uint64 n,
+ * n x (uint32 i, j)), ".txt" = "I J\nn\ni j\n...".  pairs strictly increasing. */
+int sfm_mvg_save_matches(const char* path, const int32_t* pairs, int64_t n_pairs,
+                         const int64_t* counts, const uint32_t* i, const uint32_t* j);
+int sfm_mvg_load_matches(const char* path, int32_t* pairs, int64_t* counts,
+                         uint32_t* i, uint32_t* j, int64_t cap_pairs, int64_t cap_matches,
+                         int64_t* n_pairs, int64_t* n_matches);
+
+/* [cpu] sparseBuilder::matchPair(): <matches_dir>/pairs.bin =
+ * exhaustivePairs(#views of sfm_data.json). */
+int sfm_sparse_match_pair(const char* matches_dir);
+
+typedef struct sfm_sparse_match_opts {
+    int32_t mode;      /* SFM_MATCH_RATIO (the reference's)                   */
+    float ratio;       /* fDistRatio 0.8f (:812)                              */
+    int32_t force;     /* 0: reload an existing matches.putative.bin (:890)   */
+    int32_t dedup_xy;  /* 1: drop matches whose keypoint coordinates repeat
+                          (IndMatchDecorator, needs <stem>.feat)             */
+    int32_t reserved[2];
+} sfm_sparse_match_opts;
+typedef struct sfm_sparse_match_stats {
+    int64_t n_views, n_pairs_in, n_pairs_out, n_matches;
+    int32_t reloaded, reserved;
+} sfm_sparse_match_stats;
+/* sparseBuilder::match(), file-staged: sfm_data.json + image_describer.json
+ * + <stem>.desc/.feat + pairs.bin (exhaustive if absent) -> GPU matcher ->
+ * matches.putative.bin (non-empty pairs) + preemptive_pairs.txt.
+ * opts NULL = {RATIO, 0.8f, 0, 1}. */
+int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm_sparse_match_opts* opts,
+                     sfm_sparse_match_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../../3dreconstruction_amd/include/sfm/sfm.hpp"
@@ -112,9 +113,9 @@ int main() {
     std::vector<std::vector<uint8_t>> regions(4);
     for (int v = 0; v < 4; ++v) regions[v].assign(desc.begin() + v * 700 * 128, desc.begin() + (v + 1) * 700 * 128);
     sb.setRegions(regions);
-    auto pairs = sb.matchPair();
+    auto pairs = sb.exhaustive();
     CHECK(pairs.size() == 6);
-    auto pm = sb.match(pairs);
+    auto pm = sb.matchRegions(pairs);
     for (auto& [pr2, v] : pm) {
         std::vector<int32_t> ri(700), rd(700);
         orc_match_dense(regions[pr2.first].data(), 700, regions[pr2.second].data(), 700, SFM_MATCH_RATIO, 0.8f,
@@ -125,6 +126,62 @@ int main() {
         CHECK(exp.size() == v.size());
         for (std::size_t k = 0; k < v.size(); ++k) CHECK(exp[k].first == v[k].i_ && exp[k].second == v[k].j_);
     }
-    std::printf("sparseBuilder: %zu pairs matched, bit-exact vs oracle\nfacade ok\n", pm.size());
+    std::printf("sparseBuilder: %zu pairs matched, bit-exact vs oracle\n", pm.size());
+
+    // ---- file-staged sparseBuilder(base).matchPair() + match() --------------------
+    char tmpl[] = "/tmp/sfm_facade_XXXXXX";
+    CHECK(mkdtemp(tmpl) != nullptr);
+    const std::string base(tmpl), mdir = base + "/output/matches";
+    CHECK(std::system(("mkdir -p " + mdir).c_str()) == 0);
+    {
+        std::FILE* f = std::fopen((mdir + "/sfm_data.json").c_str(), "w");
+        std::fprintf(f, "{\"sfm_data_version\": \"0.3\", \"root_path\": \"%s/images\", \"views\": [", base.c_str());
+        for (int v = 0; v < 4; ++v)
+            std::fprintf(f, "%s{\"key\": %d, \"value\": {\"polymorphic_id\": 1073741824, \"ptr_wrapper\": "
+                         "{\"id\": %lld, \"data\": {\"local_path\": \"\", \"filename\": \"img%d.jpg\", "
+                         "\"width\": 640, \"height\": 480, \"id_view\": %d, \"id_intrinsic\": 0, \"id_pose\": %d}}}}",
+                         v ? ", " : "", v, (long long)(2147483649LL + v), v, v, v);
+        std::fprintf(f, "], \"intrinsics\": [], \"extrinsics\": [], \"structure\": []}\n");
+        std::fclose(f);
+        f = std::fopen((mdir + "/image_describer.json").c_str(), "w");
+        std::fprintf(f, "{\"image_describer\": {\"polymorphic_id\": 2147483649, \"polymorphic_name\": "
+                        "\"SIFT_Image_describer\", \"ptr_wrapper\": {\"id\": 2147483649, \"data\": {}}}, "
+                        "\"regions_type\": {\"polymorphic_id\": 2147483650, \"polymorphic_name\": \"SIFT_Regions\", "
+                        "\"ptr_wrapper\": {\"id\": 2147483650, \"data\": {}}}}\n");
+        std::fclose(f);
+        for (int v = 0; v < 4; ++v) {   // distinct keypoint positions: nothing is de-duplicated
+            const std::string stem = mdir + "/img" + std::to_string(v);
+            CHECK(sfm_mvg_write_desc((stem + ".desc").c_str(), regions[v].data(), 700) == SFM_OK);
+            f = std::fopen((stem + ".feat").c_str(), "w");
+            for (int k = 0; k < 700; ++k) std::fprintf(f, "%d %d 1.5 0.25\n", k, v);
+            std::fclose(f);
+        }
+    }
+    sfm::sparse::sparseBuilder fsb(base, ctx);
+    fsb.matchPair();
+    CHECK(fsb.lastError() == SFM_OK);
+    fsb.match();
+    CHECK(fsb.lastError() == SFM_OK && !fsb.stats().reloaded);
+    int64_t np = 0, nm = 0;
+    const std::string mfile = mdir + "/matches.putative.bin";
+    CHECK(sfm_mvg_load_matches(mfile.c_str(), nullptr, nullptr, nullptr, nullptr, 0, 0, &np, &nm) == SFM_OK);
+    std::vector<int32_t> fp(2 * np);
+    std::vector<int64_t> fc(np);
+    std::vector<uint32_t> fi(nm), fj(nm);
+    CHECK(sfm_mvg_load_matches(mfile.c_str(), fp.data(), fc.data(), fi.data(), fj.data(), np, nm, &np, &nm) == SFM_OK);
+    std::size_t nonempty = 0;
+    for (auto& [pr2, v] : pm) nonempty += !v.empty();
+    CHECK((std::size_t)np == nonempty);
+    int64_t k = 0;
+    for (int64_t q = 0; q < np; ++q) {
+        const auto& v = pm.at({(uint32_t)fp[2 * q], (uint32_t)fp[2 * q + 1]});
+        CHECK((int64_t)v.size() == fc[q]);
+        for (int64_t c = 0; c < fc[q]; ++c, ++k) CHECK(v[c].i_ == fi[k] && v[c].j_ == fj[k]);
+    }
+    fsb.match();   // existing matches.putative.bin is reloaded (bForce = false)
+    CHECK(fsb.lastError() == SFM_OK && fsb.stats().reloaded && fsb.stats().n_matches == nm);
+    if (std::system(("rm -rf " + base).c_str()) != 0) std::fprintf(stderr, "cleanup of %s failed\n", base.c_str());
+    std::printf("sparseBuilder(base): file-staged matchPair + match, %lld pairs, identical to in-memory\n"
+                "facade ok\n", (long long)np);
     return 0;
 }

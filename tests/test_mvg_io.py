@@ -1,0 +1,265 @@
+"""File-staged sparseBuilder flow: the OpenMVG
+stage-boundary formats read/written by libsfmcore (csrc/mvg_io.cpp) and the
+file-staged match() on the GPU matcher.
+
+The layouts are restated from OpenMVG's published code at the reference's call
+sites (sparseBuilder.cpp:758-1023); OpenMVG is un-vendored and absent, so the
+byte layouts below are the restatement itself (parity unpinned).
+The expected bytes are built here independently with `struct`.
+"""
+import importlib
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import _helpers as H
+
+abi = H.abi
+api = importlib.import_module("3dreconstruction_amd.api")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _view(idv, fname, local="", derived=False):
+    fields = {"local_path": local, "filename": fname, "width": 640, "height": 480,
+              "id_view": idv, "id_intrinsic": 0, "id_pose": idv}
+    if derived:   # ViewPriors: base fields nested one level down
+        data = {"value0": fields, "use_pose_center_prior": False}
+        return {"key": idv, "value": {"polymorphic_id": 2147483649, "polymorphic_name": "view_priors",
+                                      "ptr_wrapper": {"id": 2147483649 + idv, "data": data}}}
+    return {"key": idv, "value": {"polymorphic_id": 1073741824,
+                                  "ptr_wrapper": {"id": 2147483649 + idv, "data": fields}}}
+
+
+def write_sfm_data(path, names, derived_at=()):
+    doc = {"sfm_data_version": "0.3", "root_path": "/data/images",
+           "views": [_view(k, n, derived=k in derived_at) for k, n in enumerate(names)],
+           "intrinsics": [], "extrinsics": [], "structure": [], "control_points": []}
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=4)
+
+
+def write_describer(path, regions="SIFT_Regions"):
+    doc = {"image_describer": {"polymorphic_id": 2147483649, "polymorphic_name": "SIFT_Image_describer",
+                               "ptr_wrapper": {"id": 2147483649, "data": {"bOrientation": True}}},
+           "regions_type": {"polymorphic_id": 2147483650, "polymorphic_name": regions,
+                            "ptr_wrapper": {"id": 2147483650, "data": {}}}}
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=4)
+
+
+def write_feat(path, kp):
+    with open(path, "w") as f:
+        for x, y, s, o in np.asarray(kp, np.float32).reshape(-1, 4):
+            f.write(f"{float(x)!r} {float(y)!r} {float(s)!r} {float(o)!r}\n")
+
+
+def test_views_json(tmp_path):
+    p = tmp_path / "sfm_data.json"
+    write_sfm_data(p, ["a.JPG", "b.jpg", "c.png"], derived_at=(1,))
+    v = api.mvg_load_views(p)
+    assert [x["id_view"] for x in v] == [0, 1, 2]
+    assert [x["img_path"] for x in v] == ["a.JPG", "b.jpg", "c.png"]
+    assert v[1]["width"] == 640 and v[2]["id_pose"] == 2
+    # local_path joins like stlplus::create_filespec; unicode escapes decode
+    doc = json.load(open(p))
+    doc["views"][0]["value"]["ptr_wrapper"]["data"]["local_path"] = "sub"
+    doc["views"][2]["value"]["ptr_wrapper"]["data"]["filename"] = "été.png"
+    json.dump(doc, open(p, "w"), ensure_ascii=True)
+    v = api.mvg_load_views(p)
+    assert v[0]["img_path"] == "sub/a.JPG" and v[2]["img_path"] == "été.png"
+
+
+def test_views_json_errors(tmp_path):
+    p = tmp_path / "sfm_data.json"
+    p.write_text('{"views": [ {"key": 0, "value": {}} ]}')
+    with pytest.raises(api.SfmError):
+        api.mvg_load_views(p)
+    p.write_text('{"views": [ ')
+    with pytest.raises(api.SfmError):
+        api.mvg_load_views(p)
+    with pytest.raises(api.SfmError):
+        api.mvg_load_views(tmp_path / "missing.json")
+
+
+def test_describer(tmp_path):
+    p = tmp_path / "image_describer.json"
+    write_describer(p)
+    api.mvg_check_describer(p)
+    write_describer(p, "AKAZE_Binary_Regions")
+    with pytest.raises(api.SfmError) as ei:
+        api.mvg_check_describer(p)
+    assert ei.value.code == abi.SFM_ERR_UNSUPPORTED
+
+
+def test_desc_layout_and_roundtrip(tmp_path):
+    d = np.random.default_rng(1).integers(0, 256, (37, 128), dtype=np.uint8)
+    p = tmp_path / "x.desc"
+    api.mvg_write_desc(p, d)
+    raw = p.read_bytes()
+    assert raw[:8] == struct.pack("<Q", 37) and raw[8:] == d.tobytes()
+    assert np.array_equal(api.mvg_read_desc(p), d)
+    api.mvg_write_desc(p, np.zeros((0, 128), np.uint8))
+    assert api.mvg_read_desc(p).shape == (0, 128)
+    p.write_bytes(struct.pack("<Q", 5) + bytes(128 * 4))   # truncated
+    with pytest.raises(api.SfmError):
+        api.mvg_read_desc(p)
+
+
+def test_feat(tmp_path):
+    kp = np.fromfile(os.path.join(GOLDEN, "vlfeat_view0.kp"), np.float32).reshape(-1, 4)
+    p = tmp_path / "x.feat"
+    write_feat(p, kp)
+    assert np.array_equal(api.mvg_read_feat(p), kp)
+    p.write_text("1 2 3 4\n5 6 x 8\n")
+    with pytest.raises(api.SfmError):
+        api.mvg_read_feat(p)
+
+
+def test_pairs_text(tmp_path):
+    p = tmp_path / "pairs.bin"
+    p.write_text("3 1 2\n0 4\n2 1\n")   # adjacency lines, (min, max), set order
+    assert api.mvg_load_pairs(p, 5).tolist() == [[0, 4], [1, 2], [1, 3], [2, 3]]
+    api.mvg_save_pairs(p, [[2, 3], [0, 1], [0, 1]])
+    assert p.read_text() == "0 1\n2 3\n"
+    for bad in ("1 1\n", "0 5\n", "0\n", "0 x\n"):
+        p.write_text(bad)
+        with pytest.raises(api.SfmError):
+            api.mvg_load_pairs(p, 5)
+
+
+def _expected_bin(matches):
+    out = struct.pack("<B", 1) + struct.pack("<Q", len(matches))
+    for (I, J) in sorted(matches):
+        m = np.asarray(matches[(I, J)], np.uint32).reshape(-1, 2)
+        out += struct.pack("<IIQ", I, J, len(m))
+        for a, b in m:
+            out += struct.pack("<II", a, b)
+    return out
+
+
+def test_matches_bin_and_txt(tmp_path):
+    m = {(0, 2): [[5, 1], [7, 3]], (0, 1): [[0, 0]], (1, 2): np.zeros((0, 2))}
+    p = tmp_path / "matches.putative.bin"
+    api.mvg_save_matches(p, m)
+    assert p.read_bytes() == _expected_bin(m)
+    back = api.mvg_load_matches(p)
+    assert list(back) == [(0, 1), (0, 2), (1, 2)]
+    assert back[(0, 2)].tolist() == [[5, 1], [7, 3]] and back[(1, 2)].shape == (0, 2)
+    t = tmp_path / "matches.putative.txt"
+    api.mvg_save_matches(t, m)
+    assert t.read_text() == "0 1\n1\n0 0\n0 2\n2\n5 1\n7 3\n1 2\n0\n"
+    assert api.mvg_load_matches(t)[(0, 2)].tolist() == [[5, 1], [7, 3]]
+    p.write_bytes(_expected_bin(m)[:-3])
+    with pytest.raises(api.SfmError):
+        api.mvg_load_matches(p)
+
+
+def test_match_pair_stage(tmp_path):
+    write_sfm_data(tmp_path / "sfm_data.json", [f"im{k}.jpg" for k in range(5)])
+    api.sparse_match_pair(tmp_path)
+    lines = (tmp_path / "pairs.bin").read_text().splitlines()
+    assert lines == [f"{a} {b}" for a in range(5) for b in range(a + 1, 5)]
+
+
+# ---------------------------------------------------------------------------
+# the full file-staged match() on VLFeat descriptors of the reference's own SIFT
+# ---------------------------------------------------------------------------
+def vlfeat_views():
+    meta = json.load(open(os.path.join(GOLDEN, "vlfeat_matches.json")))
+    out = []
+    for k, n in enumerate(meta["views"]):
+        d = np.fromfile(os.path.join(GOLDEN, f"vlfeat_view{k}.u8"), np.uint8).reshape(n, 128)
+        kp = np.fromfile(os.path.join(GOLDEN, f"vlfeat_view{k}.kp"), np.float32).reshape(n, 4)
+        out.append((d, kp))
+    return out
+
+
+def make_stage_dir(d, views, with_pairs=True):
+    names = [f"frame_{k:03d}.JPG" for k in range(len(views))]
+    write_sfm_data(d / "sfm_data.json", names)
+    write_describer(d / "image_describer.json")
+    for name, (desc, kp) in zip(names, views):
+        stem = name.rsplit(".", 1)[0]
+        api.mvg_write_desc(d / f"{stem}.desc", desc)
+        write_feat(d / f"{stem}.feat", kp)
+    if with_pairs:
+        api.sparse_match_pair(d)
+
+
+def expected_matches(views, dedup=True):
+    """Oracle restatement: RATIO matching (exact brute force), (i, j)-sorted,
+    then drop matches whose (xI, yI, xJ, yJ) repeat an earlier one."""
+    out = {}
+    for I in range(len(views)):
+        for J in range(I + 1, len(views)):
+            (dI, kI), (dJ, kJ) = views[I], views[J]
+            idx, _ = H.oracle_match_dense(dI, dJ, abi.SFM_MATCH_RATIO)
+            m = sorted((int(i), int(j)) for j, i in enumerate(idx) if i >= 0)
+            if dedup:
+                seen, keep = set(), []
+                for i, j in m:
+                    key = (kI[i, 0], kI[i, 1], kJ[j, 0], kJ[j, 1])
+                    if key not in seen:
+                        seen.add(key)
+                        keep.append((i, j))
+                m = keep
+            if m:
+                out[(I, J)] = np.array(m, np.uint32)
+    return out
+
+
+def test_vlfeat_fixtures_have_repeated_keypoints():
+    # SIFT emits several orientations per keypoint, which is what dedup_xy is for
+    (d, kp) = vlfeat_views()[0]
+    assert len({(x, y) for x, y in kp[:, :2]}) < len(kp)
+
+
+def test_match_stage_without_device_fails_loudly(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    make_stage_dir(tmp_path, vlfeat_views())
+    with pytest.raises(api.SfmError):
+        api.sparse_match(api.Context(0), tmp_path)
+
+
+@pytest.mark.gpu
+def test_match_stage_gpu(tmp_path):
+    views = vlfeat_views()
+    make_stage_dir(tmp_path, views)
+    ctx = api.Context(0)
+    st = api.sparse_match(ctx, tmp_path)
+    got = api.mvg_load_matches(tmp_path / "matches.putative.bin")
+    exp = expected_matches(views)
+    assert list(got) == list(exp)
+    for k in exp:
+        assert np.array_equal(got[k], exp[k]), k
+    assert st["n_pairs_in"] == 3 and st["n_pairs_out"] == len(exp) and not st["reloaded"]
+    assert (tmp_path / "preemptive_pairs.txt").read_text().splitlines() == [f"{a} {b}" for a, b in exp]
+    # an existing matches file is reloaded, not recomputed (bForce = false)
+    assert api.sparse_match(ctx, tmp_path)["reloaded"]
+    # without dedup the raw ratio matches come out; forced recompute
+    st2 = api.sparse_match(ctx, tmp_path, force=True, dedup_xy=False)
+    raw = expected_matches(views, dedup=False)
+    got2 = api.mvg_load_matches(tmp_path / "matches.putative.bin")
+    assert list(got2) == list(raw) and all(np.array_equal(got2[k], raw[k]) for k in raw)
+    assert st2["n_matches"] >= st["n_matches"]
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_match_stage_gpu_pairs_file_and_empty_view(tmp_path):
+    views = vlfeat_views()
+    views.append((np.zeros((0, 128), np.uint8), np.zeros((0, 4), np.float32)))   # no regions
+    make_stage_dir(tmp_path, views, with_pairs=False)
+    (tmp_path / "pairs.bin").write_text("2 0\n3 1 0\n")   # (0,2), (0,3), (1,3)
+    ctx = api.Context(0)
+    st = api.sparse_match(ctx, tmp_path)
+    got = api.mvg_load_matches(tmp_path / "matches.putative.bin")
+    exp = {k: v for k, v in expected_matches(views[:3]).items() if k == (0, 2)}
+    assert list(got) == list(exp) and np.array_equal(got[(0, 2)], exp[(0, 2)])
+    assert st["n_pairs_in"] == 3 and st["n_pairs_out"] == 1
+    ctx.close()
