@@ -24,6 +24,9 @@ SFM_TERM_CONVERGENCE = 0
 SFM_TERM_NO_CONVERGENCE = 1
 SFM_TERM_FAILURE = 2
 
+SFM_CAM_PINHOLE = 0
+SFM_CAM_SNAVELY = 1
+
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1
 
@@ -49,7 +52,7 @@ class BAProblem(C.Structure):
     _fields_ = [("n_img", C.c_int32), ("n_intr", C.c_int32), ("n_pt", C.c_int64),
                 ("n_obs", C.c_int64), ("pt_offsets", i64p), ("obs_img", i32p),
                 ("obs_uv", f64p), ("img_intr", i32p), ("const_img", C.c_int32),
-                ("reserved", C.c_int32), ("huber_a", C.c_double)]
+                ("camera_model", C.c_int32), ("huber_a", C.c_double)]
 
 
 class BAOptions(C.Structure):
@@ -98,7 +101,7 @@ class SynthBAConfig(C.Structure):
                 ("noise_px", C.c_double), ("outlier_frac", C.c_double),
                 ("perturb_rot", C.c_double), ("perturb_t", C.c_double),
                 ("perturb_X", C.c_double), ("perturb_f", C.c_double),
-                ("const_img", C.c_int32), ("reserved", C.c_int32)]
+                ("const_img", C.c_int32), ("camera_model", C.c_int32)]
 
 
 class MatchOptions(C.Structure):

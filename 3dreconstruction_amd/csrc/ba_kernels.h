@@ -22,6 +22,7 @@ constexpr int kPartT = 5;  // per step block: model acc, cand cost, step norm^2,
 struct DevProblem {
     int32_t n_img, n_intr, n_spt, n_sobs, n_chunk, ncam, nintr, D;
     int32_t tile_nt;    // 16-row MFMA tiles per chunk side: 4 (64 F rows) or 5 (76 + w row)
+    int32_t cam_model;  // SFM_CAM_* residual model
     int64_t nb, nF;
     double huber_a, min_diag, max_diag;
     // shard data

@@ -118,7 +118,7 @@ struct Lin {
     bool ok;
 };
 
-template <bool JC, bool JI, bool JX>
+template <int CM, bool JC, bool JI, bool JX>
 __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, const double* X, double u0,
                                           double u1, double huber_a, Lin& L) {
     double P[3];
@@ -136,8 +136,43 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
     P[0] += cp.t[0]; P[1] += cp.t[1]; P[2] += cp.t[2];
     // one reciprocal for the projection and its Jacobian (x = P0/P2 to 1 ulp)
     const double iz = 1.0 / P[2];
-    const double x = P[0] * iz, y = P[1] * iz;
-    const double r0 = in[0] * x + in[2] - u0, r1 = in[1] * y + in[3] - u1;
+    double r0, r1;
+    // unscaled dr/dP (2x3) and dr/d(intrinsics) (2x4) of the model
+    double A[2][3], Ji[2][4];
+    if constexpr (CM == SFM_CAM_SNAVELY) {
+        // SnavelyReprojectionError.h:31-47: p = -P/P2, d = 1 + r2 (l1 + l2 r2),
+        // r = f d p - obs; dr/dP = f [d I + 2 (l1 + 2 l2 r2) p p'] dp/dP with
+        // dp/dP = -1/P2 [1 0 xp; 0 1 yp]
+        const double xp = -P[0] * iz, yp = -P[1] * iz;
+        const double r2 = xp * xp + yp * yp;
+        const double d = 1.0 + r2 * (in[1] + in[2] * r2);
+        r0 = in[0] * d * xp - u0;
+        r1 = in[0] * d * yp - u1;
+        if (JC || JI || JX) {
+            const double dd2 = 2.0 * (in[1] + 2.0 * in[2] * r2);
+            const double b01 = in[0] * dd2 * xp * yp;
+            const double B[2][2] = {{in[0] * (d + dd2 * xp * xp), b01}, {b01, in[0] * (d + dd2 * yp * yp)}};
+            const double pp[2] = {xp, yp};
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                A[r][0] = -iz * B[r][0];
+                A[r][1] = -iz * B[r][1];
+                A[r][2] = -iz * (B[r][0] * xp + B[r][1] * yp);
+                Ji[r][0] = d * pp[r];
+                Ji[r][1] = in[0] * r2 * pp[r];
+                Ji[r][2] = in[0] * r2 * r2 * pp[r];
+                Ji[r][3] = 0.0;
+            }
+        }
+    } else {
+        const double x = P[0] * iz, y = P[1] * iz;
+        r0 = in[0] * x + in[2] - u0;
+        r1 = in[1] * y + in[3] - u1;
+        A[0][0] = in[0] * iz; A[0][1] = 0.0; A[0][2] = -in[0] * x * iz;
+        A[1][0] = 0.0; A[1][1] = in[1] * iz; A[1][2] = -in[1] * y * iz;
+        Ji[0][0] = x; Ji[0][1] = 0.0; Ji[0][2] = 1.0; Ji[0][3] = 0.0;
+        Ji[1][0] = 0.0; Ji[1][1] = y; Ji[1][2] = 0.0; Ji[1][3] = 1.0;
+    }
     L.ok = isfinite(r0) && isfinite(r1);
     const double sq = r0 * r0 + r1 * r1;
     double rho0, sr = 1.0;   // Huber: rho' = 1 (inlier) needs no square root
@@ -151,11 +186,15 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
     L.half_rho = 0.5 * rho0;
     L.f[0] = r0 * sr; L.f[1] = r1 * sr;
     if (JC || JI || JX) {
-        const double A[2][3] = {{in[0] * iz * sr, 0.0, -in[0] * x * iz * sr},
-                                {0.0, in[1] * iz * sr, -in[1] * y * iz * sr}};
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) A[r][k] *= sr;
         if (JI) {
-            L.Ji[0][0] = x * sr; L.Ji[0][1] = 0.0; L.Ji[0][2] = sr; L.Ji[0][3] = 0.0;
-            L.Ji[1][0] = 0.0; L.Ji[1][1] = y * sr; L.Ji[1][2] = 0.0; L.Ji[1][3] = sr;
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) L.Ji[r][k] = Ji[r][k] * sr;
         }
         // dP/dX = R; dP/dw = -Al [X]x Ar with Al = R (Rodrigues) or I (small
         // angle), so the left factor A Al is J_X itself or A.
@@ -223,11 +262,17 @@ __device__ __forceinline__ double wave_max(double v) {
 // waves add in fixed order.
 // ---------------------------------------------------------------------------
 namespace gram {
-constexpr bool in0(int i) { return i < 6 || i == 6 || i == 8 || i == 10; }   // nonzero in row 0
-constexpr bool in1(int i) { return i < 6 || i == 7 || i == 9 || i == 10; }   // nonzero in row 1
+// structurally nonzero entries of [J_c | J_i | f] rows 0 / 1 (index 0..10)
+// PINHOLE: J_i row 0 = [x s, 0, s, 0], row 1 = [0, y s, 0, s];
+// SNAVELY: J_i rows = [d, f r2, f r2^2, 0] p_r s (column 9 is never a parameter)
+template <int CM>
+constexpr bool in0(int i) { return CM == SFM_CAM_SNAVELY ? i != 9 : (i < 6 || i == 6 || i == 8 || i == 10); }
+template <int CM>
+constexpr bool in1(int i) { return CM == SFM_CAM_SNAVELY ? i != 9 : (i < 6 || i == 7 || i == 9 || i == 10); }
 struct Slots {
     int i[64], j[64], id[11][11], n;
 };
+template <int CM>
 constexpr Slots make_slots() {
     Slots t{};
     t.n = 0;
@@ -235,16 +280,20 @@ constexpr Slots make_slots() {
         for (int b = 0; b < 11; ++b) t.id[a][b] = -1;
     for (int a = 0; a < 11; ++a)
         for (int b = 0; b <= a; ++b)
-            if ((in0(a) && in0(b)) || (in1(a) && in1(b))) {
+            if ((in0<CM>(a) && in0<CM>(b)) || (in1<CM>(a) && in1<CM>(b))) {
                 t.i[t.n] = a; t.j[t.n] = b;
                 t.id[a][b] = t.id[b][a] = t.n;
                 ++t.n;
             }
     return t;
 }
-constexpr Slots kS = make_slots();
-static_assert(kS.n == 62, "image Gram: 62 nonzero entries");
-constexpr int kCost = 62;   // slot of the cost; slot 63 stays zero
+template <int CM>
+struct SlotTable {
+    static constexpr Slots kS = make_slots<CM>();
+    static constexpr int kCost = kS.n;   // slot of the cost; later slots stay zero
+};
+static_assert(SlotTable<SFM_CAM_PINHOLE>::kS.n == 62, "image Gram: 62 nonzero entries (pinhole)");
+static_assert(SlotTable<SFM_CAM_SNAVELY>::kS.n == 55, "image Gram: 55 nonzero entries (Snavely)");
 
 __device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__double_as_longlong(v); }
 __device__ __forceinline__ unsigned hi32(double v) { return (unsigned)(__double_as_longlong(v) >> 32); }
@@ -293,9 +342,11 @@ __device__ __forceinline__ void reduce_scatter64(double (&v)[64], int lane) {
 #ifndef SFM_GRAM_WPE
 #define SFM_GRAM_WPE 2
 #endif
+template <int CM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WPE, SFM_GRAM_WPE))) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const double* __restrict__ X) {
+    using kT = gram::SlotTable<CM>;
     const int img = blockIdx.x / kGramSeg, seg = blockIdx.x - kGramSeg * img;   // slice of the image
     const int a0 = P.img_obs_ptr[img], n = P.img_obs_ptr[img + 1] - a0;
     const int o0 = a0 + (int)((int64_t)n * seg / kGramSeg), o1 = a0 + (int)((int64_t)n * (seg + 1) / kGramSeg);
@@ -346,18 +397,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         asm volatile("" ::: "memory");
         if (p_cur >= 0) {
             Lin L;
-            linearize<true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
-            g[gram::kCost] += L.half_rho;
+            linearize<CM, true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
+            g[kT::kCost] += L.half_rho;
             bad = fmax(bad, L.ok ? 0.0 : 1.0);
             // unscaled rows; the per-image column scales are applied to the sums
             auto r = [&](int q, int i) -> double {
                 return i < 6 ? L.Jc[q][i] : i < 10 ? L.Ji[q][i - 6] : L.f[q];
             };
 #pragma unroll
-            for (int s = 0; s < 62; ++s) {
-                const int i = gram::kS.i[s], j = gram::kS.j[s];
-                if (gram::in0(i) && gram::in0(j)) g[s] = fma(r(0, i), r(0, j), g[s]);
-                if (gram::in1(i) && gram::in1(j)) g[s] = fma(r(1, i), r(1, j), g[s]);
+            for (int s = 0; s < kT::kS.n; ++s) {
+                const int i = kT::kS.i[s], j = kT::kS.j[s];
+                if (gram::in0<CM>(i) && gram::in0<CM>(j)) g[s] = fma(r(0, i), r(0, j), g[s]);
+                if (gram::in1<CM>(i) && gram::in1<CM>(j)) g[s] = fma(r(1, i), r(1, j), g[s]);
             }
         }
     }
@@ -368,22 +419,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
     __syncthreads();
     auto tot = [&](int s) { return ((part[0][s] + part[1][s]) + part[2][s]) + part[3][s]; };
     if (threadIdx.x < 100) {
-        const int i = threadIdx.x / 10, j = threadIdx.x % 10, s = gram::kS.id[i][j];
+        const int i = threadIdx.x / 10, j = threadIdx.x % 10, s = kT::kS.id[i][j];
         const double u = s >= 0 ? ssc[i] * ssc[j] * tot(s) : 0.0;
         P.U[(size_t)blockIdx.x * 100 + threadIdx.x] = u;
         if (i == j) P.Ucn[(size_t)blockIdx.x * 10 + i] = u;
     }
     if (threadIdx.x >= 128 && threadIdx.x < 138) {
         const int i = threadIdx.x - 128;
-        P.Ub[(size_t)blockIdx.x * 10 + i] = ssc[i] * tot(gram::kS.id[10][i]);
+        P.Ub[(size_t)blockIdx.x * 10 + i] = ssc[i] * tot(kT::kS.id[10][i]);
     }
     if (threadIdx.x == 192) {
-        P.part_u[2 * (size_t)blockIdx.x] = tot(gram::kCost);
+        P.part_u[2 * (size_t)blockIdx.x] = tot(kT::kCost);
         P.part_u[2 * (size_t)blockIdx.x + 1] = fmax(fmax(badw[0], badw[1]), fmax(badw[2], badw[3]));
     }
 }
 
 // Jacobi scale of the point columns (iteration 0): 1 / (1 + |J col|).
+template <int CM>
 __global__ void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                    const double* __restrict__ intr, const double* __restrict__ X) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -392,7 +444,7 @@ __global__ void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
     for (int o = P.pt_off[p]; o < P.pt_off[p + 1]; ++o) {
         const int img = P.obs_img[o];
         Lin L;
-        linearize<false, false, true>(cps[img], intr + 4 * P.img_intr[img], X + 3 * p, P.obs_uv[2 * o],
+        linearize<CM, false, false, true>(cps[img], intr + 4 * P.img_intr[img], X + 3 * p, P.obs_uv[2 * o],
                                       P.obs_uv[2 * o + 1], P.huber_a, L);
 #pragma unroll
         for (int r = 0; r < 2; ++r)
@@ -466,7 +518,7 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 // NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
 // SP / SO: points / observations per wave batch.  The panel holds 3 columns
 // per point padded to the MFMA k of 4 and NT*16 rows (NT = 4 keeps w apart).
-template <int NT, int SP = kSubPts, int SO = kSubObs>
+template <int CM, int NT, int SP = kSubPts, int SO = kSubObs>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
@@ -485,7 +537,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT, kPS = kPR + 4;
     __shared__ double panel[kPK][kPS];          // [k][row]
     __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
-    __shared__ double ob[SO][4];                // J_intr nonzeros
+    constexpr int kOb = CM == SFM_CAM_SNAVELY ? 6 : 4;
+    __shared__ double ob[SO][kOb];              // J_intr nonzeros (scaled)
     __shared__ double vs[SO][10];               // per observation: Jx'Jx (6) | Jx'f (3) | pad
     __shared__ double vsum[SP][10];             // per point: V (6) | g_E (3)
     __shared__ double obm[SO][6];               // M = Jx L^-T
@@ -570,7 +623,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         Lin L;
         const int cs = slot & 255, is = (slot >> 8) & 255;
         if (lane < nobs) {
-            linearize<true, true, true>(scp[cs], &isc[is][0], Xp, u0, u1, P.huber_a, L);
+            linearize<CM, true, true, true>(scp[cs], &isc[is][0], Xp, u0, u1, P.huber_a, L);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
 #pragma unroll
@@ -590,10 +643,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
             for (int e = 0; e < 9; ++e) vs[lane][e] = cv[e];
             // J_intr rows are [x s, 0, s, 0] and [0, y s, 0, s]: keep the 4 nonzeros
-            ob[lane][0] = L.Ji[0][0] * isc[is][4];
-            ob[lane][1] = L.Ji[1][1] * isc[is][5];
-            ob[lane][2] = L.Ji[0][2] * isc[is][6];
-            ob[lane][3] = L.Ji[1][3] * isc[is][7];
+            if constexpr (CM == SFM_CAM_SNAVELY) {
+                // both rows of columns 0..2 (f, l1, l2); column 3 is not a parameter
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ob[lane][2 * k] = L.Ji[0][k] * isc[is][4 + k];
+                    ob[lane][2 * k + 1] = L.Ji[1][k] * isc[is][4 + k];
+                }
+            } else {
+                ob[lane][0] = L.Ji[0][0] * isc[is][4];
+                ob[lane][1] = L.Ji[1][1] * isc[is][5];
+                ob[lane][2] = L.Ji[0][2] * isc[is][6];
+                ob[lane][3] = L.Ji[1][3] * isc[is][7];
+            }
             orow[lane] = irow[is];
         }
         __syncthreads();
@@ -676,7 +738,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         SFM_STAMP(2)
         // ---- C2: intrinsics rows, ordered per point ---------------------------
         // (register sums per run of observations sharing an intrinsics block)
-        if constexpr (12 * SP <= 64) {
+        if constexpr (CM == SFM_CAM_SNAVELY) {
+            // one lane per (point, axis, intrinsics column k < 3):
+            // z_k = sum_q Ji[q][0][k] M[q][0][a] + Ji[q][1][k] M[q][1][a]
+            for (int e = lane; e < 9 * npts; e += 64) {
+                const int pt = e / 9, rem = e - 9 * pt, a = rem / 3, k = rem - 3 * a;
+                const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
+                int row = orow[q0];
+                double z = 0.0;
+                for (int q = q0; q < q1; ++q) {
+                    const int rq = orow[q];
+                    if (rq != row) {
+                        panel[3 * pt + a][row + k] += z;
+                        z = 0.0;
+                        row = rq;
+                    }
+                    z = fma(ob[q][2 * k], obm[q][a], z);
+                    z = fma(ob[q][2 * k + 1], obm[q][3 + a], z);
+                }
+                panel[3 * pt + a][row + k] += z;
+            }
+        } else if constexpr (12 * SP <= 64) {
             // one lane per (point, axis, intrinsics column): z_k = sum_q Ji[q][k] M[q][k & 1][a]
             if (lane < 12 * npts) {
                 const int pt = lane / 12, rem = lane - 12 * pt, a = rem >> 2, k = rem & 3;
@@ -1140,10 +1222,12 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
     } else if (t < P.n_img + P.n_intr) {
         const int q = t - P.n_img;
         const int c0 = P.intr_col[q];
+        // SNAVELY: the 4th double is not a parameter (not moved, not in the norms)
+        const int na = P.cam_model == SFM_CAM_SNAVELY ? 3 : 4;
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
             const double x = intr[4 * (size_t)q + a];
-            cand_intr[4 * (size_t)q + a] = c0 >= 0 ? col(x, (int64_t)c0 + a) : x;
+            cand_intr[4 * (size_t)q + a] = (c0 >= 0 && a < na) ? col(x, (int64_t)c0 + a) : x;
         }
     }
     wave_sum(v);
@@ -1166,6 +1250,7 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
 // and candidate cameras, intrinsics, column scales and y_F are staged in LDS
 // once, so the per-observation work gathers only the measurement.
 // ---------------------------------------------------------------------------
+template <int CM>
 __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const CamPre* __restrict__ cps_c,
@@ -1222,7 +1307,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
             }
             Lin L;
-            linearize<true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
+            linearize<CM, true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
             const bool cam = crow_valid(cd, cs);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
@@ -1286,7 +1371,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
             }
             Lin C;
-            linearize<false, false, false>(scc[cs], &isy[is][4], xc, uv.x, uv.y, P.huber_a, C);
+            linearize<CM, false, false, false>(scc[cs], &isy[is][4], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;
             if (!C.ok) cbad = 1.0;
         }
@@ -1367,16 +1452,30 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
     SFM_HIP(hipGetLastError());
 }
 
+// the residual model is a template parameter of every kernel that linearises
+#define SFM_BY_MODEL(P, CALL)                                  \
+    do {                                                       \
+        if ((P).cam_model == SFM_CAM_SNAVELY) {                \
+            constexpr int CM = SFM_CAM_SNAVELY;                \
+            CALL;                                              \
+        } else {                                               \
+            constexpr int CM = SFM_CAM_PINHOLE;                \
+            CALL;                                              \
+        }                                                      \
+    } while (0)
+
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                    hipStream_t s) {
-    hipLaunchKernelGGL(image_gram_kernel, dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp, intr, X);
+    SFM_BY_MODEL(P, hipLaunchKernelGGL(image_gram_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp,
+                                       intr, X));
     SFM_HIP(hipGetLastError());
 }
 
 void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                     hipStream_t s) {
     if (P.n_spt <= 0) return;
-    hipLaunchKernelGGL(point_scale_kernel, dim3((P.n_spt + 255) / 256), dim3(256), 0, s, P, cp, intr, X);
+    SFM_BY_MODEL(P, hipLaunchKernelGGL(point_scale_kernel<CM>, dim3((P.n_spt + 255) / 256), dim3(256), 0, s, P,
+                                       cp, intr, X));
     SFM_HIP(hipGetLastError());
 }
 
@@ -1392,10 +1491,11 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
     // 64-row tiles: 4-point batches (12 panel columns, no k padding) keep LDS
     // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
     if (P.tile_nt == 4)
-        hipLaunchKernelGGL((schur_kernel<4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>), dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X,
-                           radius, stamps);
+        SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>), dim3(P.n_chunk),
+                                           dim3(64), 0, s, P, cp, intr, X, radius, stamps));
     else
-        hipLaunchKernelGGL(schur_kernel<5>, dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps);
+        SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5>), dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X,
+                                           radius, stamps));
     SFM_HIP(hipGetLastError());
 }
 
@@ -1453,8 +1553,8 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
              const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
     const int nb = ba_step_blocks(P);
     if (nb <= 0) return;
-    hipLaunchKernelGGL(step_kernel, dim3(nb), dim3(kChunkPts), 0, s, P, cp, intr, cp_cand, intr_cand, X, X_cand,
-                       radius);
+    SFM_BY_MODEL(P, hipLaunchKernelGGL(step_kernel<CM>, dim3(nb), dim3(kChunkPts), 0, s, P, cp, intr, cp_cand,
+                                       intr_cand, X, X_cand, radius));
     SFM_HIP(hipGetLastError());
 }
 

@@ -93,6 +93,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         SFM_REQUIRE(P.img_intr[i] >= 0 && P.img_intr[i] < P.n_intr, SFM_ERR_INVALID_ARG,
                     "image %d references intrinsics %d", i, P.img_intr[i]);
     SFM_REQUIRE(P.const_img >= -1 && P.const_img < P.n_img, SFM_ERR_INVALID_ARG, "bad const_img");
+    SFM_REQUIRE(P.camera_model == SFM_CAM_PINHOLE || P.camera_model == SFM_CAM_SNAVELY, SFM_ERR_INVALID_ARG,
+                "unknown camera_model %d", P.camera_model);
 
     pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
     pl.rank = rank; pl.world = world;

@@ -183,6 +183,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D;
     P.nb = h.nb; P.nF = h.nF;
     P.huber_a = prob.huber_a;
+    P.cam_model = prob.camera_model;
     P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p; P.obs_pt = pl->obs_pt.p;
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
     P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;

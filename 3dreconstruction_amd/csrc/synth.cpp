@@ -62,10 +62,18 @@ void rotate(const double w[3], const double X[3], double out[3]) {
     }
 }
 
-void project(const double* intr, const double* extr, const double* X, double uv[2]) {
+void project(int model, const double* intr, const double* extr, const double* X, double uv[2]) {
     double P[3];
     rotate(extr, X, P);
     P[0] += extr[3]; P[1] += extr[4]; P[2] += extr[5];
+    if (model == SFM_CAM_SNAVELY) {   // SnavelyReprojectionError.h:27-47
+        const double xp = -P[0] / P[2], yp = -P[1] / P[2];
+        const double r2 = xp * xp + yp * yp;
+        const double d = 1.0 + r2 * (intr[1] + intr[2] * r2);
+        uv[0] = intr[0] * d * xp;
+        uv[1] = intr[0] * d * yp;
+        return;
+    }
     uv[0] = intr[0] * (P[0] / P[2]) + intr[2];
     uv[1] = intr[1] * (P[1] / P[2]) + intr[3];
 }
@@ -80,8 +88,10 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
                             double* extr, double* intr, double* X, double* gt_extr,
                             double* gt_intr, double* gt_X, int64_t* n_obs_out) {
     if (!cfg || cfg->n_cam < 1 || cfg->n_pt < 0 || cfg->k < 1 || cfg->k > cfg->n_cam ||
-        cfg->n_intr < 1 || cfg->n_intr > cfg->n_cam)
+        cfg->n_intr < 1 || cfg->n_intr > cfg->n_cam ||
+        (cfg->camera_model != SFM_CAM_PINHOLE && cfg->camera_model != SFM_CAM_SNAVELY))
         return SFM_ERR_INVALID_ARG;
+    const int model = cfg->camera_model;
     const int64_t n_obs = cfg->n_pt * cfg->k;
     if (n_obs_out) *n_obs_out = n_obs;
     if (!pt_offsets) return SFM_OK;  // size query
@@ -92,6 +102,11 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
     for (int q = 0; q < cfg->n_intr; ++q) {
         Rng r(entity_seed(seed, kStreamIntr, q));
         const double df = q == 0 ? 0.0 : 40.0 * (r.uni() - 0.5);
+        if (model == SFM_CAM_SNAVELY) {   // BAL-like: f, l1, l2 (principal point at 0)
+            gi[4 * q + 0] = 1000.0 + df; gi[4 * q + 1] = -0.08;
+            gi[4 * q + 2] = 0.02;         gi[4 * q + 3] = 0.0;
+            continue;
+        }
         gi[4 * q + 0] = 2905.88 + df; gi[4 * q + 1] = 2905.88 + df;
         gi[4 * q + 2] = 1416.0;       gi[4 * q + 3] = 1064.0;
     }
@@ -141,7 +156,7 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
         for (int a = 0; a < k; ++a) {
             const int c = cams[a];
             double uv[2];
-            project(&gi[4 * (size_t)img_intr[c]], &ge[6 * (size_t)c], Xg, uv);
+            project(model, &gi[4 * (size_t)img_intr[c]], &ge[6 * (size_t)c], Xg, uv);
             uv[0] += cfg->noise_px * r.gauss();
             uv[1] += cfg->noise_px * r.gauss();
             if (r.uni() < cfg->outlier_frac) {
@@ -174,7 +189,12 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
         for (int a = 0; a < 4; ++a) {
             const double g = gi[4 * (size_t)q + a];
             if (gt_intr) gt_intr[4 * (size_t)q + a] = g;
-            intr[4 * (size_t)q + a] = a < 2 ? g + cfg->perturb_f * r.gauss() : g;
+            if (model == SFM_CAM_SNAVELY)   // f by perturb_f, l1 / l2 by a proportional small amount
+                intr[4 * (size_t)q + a] = a == 0 ? g + cfg->perturb_f * r.gauss()
+                                        : a < 3  ? g + 2e-3 * cfg->perturb_f / 5.0 * r.gauss() / (a == 1 ? 1.0 : 4.0)
+                                                 : g;
+            else
+                intr[4 * (size_t)q + a] = a < 2 ? g + cfg->perturb_f * r.gauss() : g;
         }
     }
     return SFM_OK;

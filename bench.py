@@ -42,9 +42,10 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004):
+def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0):
     lib = abi.load()
     cfg = abi.SynthBAConfig()
+    cfg.camera_model = model
     cfg.n_cam, cfg.k, cfg.vis_mode, cfg.n_intr = n_cam, k, 0, 1
     cfg.n_pt, cfg.seed = n_pt, seed
     cfg.noise_px, cfg.outlier_frac = 0.5, 0.01
@@ -72,6 +73,7 @@ def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004):
     pr.obs_uv = p(sc["obs_uv"], abi.f64p)
     pr.img_intr = p(sc["img_intr"], abi.i32p)
     pr.const_img = 1
+    pr.camera_model = model
     pr.huber_a = 4.0
     sc["problem"] = pr
     sc["n_obs"] = no
@@ -147,6 +149,7 @@ def main():
     ap.add_argument("--match-frames", type=int, default=500)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
+    ap.add_argument("--no-snavely", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -245,6 +248,44 @@ def main():
     log(f"BA: {iters} LM iterations in {dt:.3f}s -> {value:.1f} it/s, rmse "
         f"{summ.rmse_initial:.4f}->{summ.rmse_final:.4f}, schur avg {schur_avg_ms:.3f} ms")
 
+    # ---------------- BA, BAL residual model ----------------
+    snav = None
+    if not args.no_snavely:
+        ssc = c4_scene(args.n_cam, args.n_pt, model=abi.SFM_CAM_SNAVELY)
+        splan = api.BAPlan(ctx, ssc["problem"], ssc["extr"], ssc["intr"], ssc["X"])
+        for _ in range(args.warmup):
+            splan.run()
+        ctx.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        s_iters, s_ms, s_n = 0, 0.0, 0
+        for _ in range(args.steps):
+            rc, ssum = splan.run()
+            s_iters += ssum.iterations
+            inf = splan.info()
+            s_ms += inf.schur_ms_total
+            s_n += inf.schur_launches
+        ctx.synchronize()
+        barrier()
+        sdt = max_over_ranks(time.perf_counter() - t0)
+        s_avg = s_ms / max(s_n, 1)
+        s_flops = splan.info().schur_flops_per_iter
+        s_ach = s_flops / (s_avg * 1e-3) / 1e12 if s_n else 0.0
+        snav = {"metric": "BA LM-iters/sec, SnavelyReprojectionError (BAL) residual model",
+                "value": s_iters / sdt, "unit": "LM-iters/s", "ms_per_step": sdt / args.steps * 1e3,
+                "obs_per_sec": s_iters * ssc["n_obs"] / sdt, "lm_iterations_per_solve": ssum.iterations,
+                "rmse_initial": ssum.rmse_initial, "rmse_final": ssum.rmse_final,
+                "config": {"workload": f"C4 geometry ({args.n_cam} cams / {args.n_pt} pts / "
+                                       f"{ssc['n_obs']} obs), SnavelyReprojectionError.h model "
+                                       "(f, l1, l2 per camera block; one shared block), HuberLoss(4)"},
+                "roofline": {"bound": "mfma", "achieved": s_ach, "peak": FP64_PEAK_TF, "unit": "TFLOP/s",
+                             "frac": s_ach / FP64_PEAK_TF, "kernel": "schur_kernel<SNAVELY>",
+                             "per_launch_ms": s_avg}}
+        log(f"BA snavely: {s_iters} LM iterations in {sdt:.3f}s -> {s_iters / sdt:.1f} it/s, rmse "
+            f"{ssum.rmse_initial:.4f}->{ssum.rmse_final:.4f}")
+        splan.close()
+        del ssc
+
     # ---------------- matching (C3) ----------------
     match = None
     if not args.no_match:
@@ -313,6 +354,7 @@ def main():
                          "algorithmic_flops_per_launch": flops},
             "cpu_baseline": cpu,
             "match": match,
+            "ba_snavely": snav,
         }
         print(json.dumps(out))
     plan.close()

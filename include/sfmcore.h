@@ -99,9 +99,21 @@ typedef struct sfm_ba_problem {
     const int32_t* img_intr; /* [n_img] intrinsic block of each image          */
     int32_t const_img;       /* gauge: image whose pose is held constant
                                 (BundleAdjuster.h:105); -1 for none          */
-    int32_t reserved;
+    int32_t camera_model;    /* SFM_CAM_* residual model (0 = the reference's
+                                ReprojectCost)                               */
     double huber_a;          /* HuberLoss scale a (reference: 4.0); <=0: none  */
 } sfm_ba_problem;
+
+/* Residual models (sfm_ba_problem.camera_model).  Every model keeps the
+ * 4-double intrinsics block layout of intr[]:
+ *   SFM_CAM_PINHOLE  BundleAdjuster.h:33-69 ReprojectCost, {fx, fy, cx, cy}:
+ *                    r = (fx P0/P2 + cx - u, fy P1/P2 + cy - v)
+ *   SFM_CAM_SNAVELY  src/adjuster/SnavelyReprojectionError.h:16-54 (BAL /
+ *                    Bundler), {f, l1, l2, -}: p = (-P0/P2, -P1/P2),
+ *                    r = f (1 + |p|^2 (l1 + l2 |p|^2)) p - (u, v); the 4th
+ *                    double is not a parameter (never read, never moved). */
+#define SFM_CAM_PINHOLE 0
+#define SFM_CAM_SNAVELY 1
 
 typedef struct sfm_ba_options {  /* ceres::Solver::Options semantics      */
     int32_t max_num_iterations;            /* 50   */
@@ -216,7 +228,8 @@ typedef struct sfm_synth_ba_config {
     double noise_px, outlier_frac;        /* 0.5, 0.01                         */
     double perturb_rot, perturb_t, perturb_X, perturb_f; /* .01,.05,.05,5      */
     int32_t const_img;                    /* gauge (1)                          */
-    int32_t reserved;
+    int32_t camera_model;                 /* SFM_CAM_*; SNAVELY: f 1000,
+                                             l1 -0.08, l2 0.02 (+ perturbation) */
 } sfm_synth_ba_config;
 int sfm_synth_ba(const sfm_synth_ba_config* cfg,
                  int64_t* pt_offsets, int32_t* obs_img, double* obs_uv,

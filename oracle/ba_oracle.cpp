@@ -1,7 +1,8 @@
 // CPU restatement of the reference bundle adjuster — TEST INFRASTRUCTURE
 // ONLY (see oracle.h; parity unpinned: Ceres is absent).
 //
-// Model (src/adjuster/BundleAdjuster.h):
+// Model (src/adjuster/BundleAdjuster.h; SFM_CAM_SNAVELY: the in-tree
+// src/adjuster/SnavelyReprojectionError.h:16-54 instead of ReprojectCost):
 //   ReprojectCost :40-65   P = AngleAxisRotatePoint(w, X) + t; x = P0/P2;
 //                          y = P1/P2; r = (fx x + cx - u, fy y + cy - v)
 //   HuberLoss(4)   :109    rho(s) = s (s <= 16), 2*4*sqrt(s) - 16 otherwise
@@ -50,7 +51,7 @@ constexpr double kEps = std::numeric_limits<double>::epsilon();
 // (Gallego & Yezzi 2015); small-angle branch of AngleAxisRotatePoint:
 // P = X + w x X, dP/dw = -[X]x, dP/dX = I + [w]x.
 // ---------------------------------------------------------------------------
-bool residual_jacobian(const double* in, const double* e, const double* X, const double* uv,
+bool residual_jacobian(int model, const double* in, const double* e, const double* X, const double* uv,
                        double r[2], double* J) {
     const double* w = e;
     const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
@@ -104,16 +105,47 @@ bool residual_jacobian(const double* in, const double* e, const double* X, const
         }
     }
     P[0] += e[3]; P[1] += e[4]; P[2] += e[5];
-    const double x = P[0] / P[2], y = P[1] / P[2];
-    r[0] = in[0] * x + in[2] - uv[0];
-    r[1] = in[1] * y + in[3] - uv[1];
+    double A[2][3], Ji[2][4];
+    if (model == SFM_CAM_SNAVELY) {
+        // SnavelyReprojectionError.h:31-47: p = -P/P2, d = 1 + r2 (l1 + l2 r2),
+        // r = f d p - obs.  dr/dP = f [d I + 2 (l1 + 2 l2 r2) p p'] dp/dP,
+        // dp/dP = -1/P2 [1 0 xp; 0 1 yp]
+        const double xp = -P[0] / P[2], yp = -P[1] / P[2];
+        const double r2 = xp * xp + yp * yp;
+        const double d = 1.0 + r2 * (in[1] + in[2] * r2);
+        r[0] = in[0] * d * xp - uv[0];
+        r[1] = in[0] * d * yp - uv[1];
+        if (J) {
+            const double iz = 1.0 / P[2], dd2 = 2.0 * (in[1] + 2.0 * in[2] * r2);
+            const double B[2][2] = {{in[0] * (d + dd2 * xp * xp), in[0] * dd2 * xp * yp},
+                                    {in[0] * dd2 * xp * yp, in[0] * (d + dd2 * yp * yp)}};
+            const double p[2] = {xp, yp};
+            for (int row = 0; row < 2; ++row) {
+                A[row][0] = -iz * B[row][0];
+                A[row][1] = -iz * B[row][1];
+                A[row][2] = -iz * (B[row][0] * xp + B[row][1] * yp);
+                Ji[row][0] = d * p[row];
+                Ji[row][1] = in[0] * r2 * p[row];
+                Ji[row][2] = in[0] * r2 * r2 * p[row];
+                Ji[row][3] = 0.0;
+            }
+        }
+    } else {
+        const double x = P[0] / P[2], y = P[1] / P[2];
+        r[0] = in[0] * x + in[2] - uv[0];
+        r[1] = in[1] * y + in[3] - uv[1];
+        if (J) {
+            const double iz = 1.0 / P[2];
+            const double A0[2][3] = {{in[0] * iz, 0.0, -in[0] * x * iz}, {0.0, in[1] * iz, -in[1] * y * iz}};
+            const double J0[2][4] = {{x, 0.0, 1.0, 0.0}, {0.0, y, 0.0, 1.0}};
+            std::memcpy(A, A0, sizeof A);
+            std::memcpy(Ji, J0, sizeof Ji);
+        }
+    }
     if (J) {
-        const double iz = 1.0 / P[2];
-        const double A[2][3] = {{in[0] * iz, 0.0, -in[0] * x * iz}, {0.0, in[1] * iz, -in[1] * y * iz}};
         for (int row = 0; row < 2; ++row) {
             double* Jr = J + row * 13;
-            Jr[0] = row == 0 ? x : 0.0; Jr[1] = row == 1 ? y : 0.0;
-            Jr[2] = row == 0 ? 1.0 : 0.0; Jr[3] = row == 1 ? 1.0 : 0.0;
+            for (int k = 0; k < 4; ++k) Jr[k] = Ji[row][k];
             for (int j = 0; j < 3; ++j) {
                 double a = 0, b = 0;
                 for (int k = 0; k < 3; ++k) { a += A[row][k] * dPdw[k * 3 + j]; b += A[row][k] * dPdX[k * 3 + j]; }
@@ -145,7 +177,7 @@ inline Jet jsqrt(const Jet& f) { const double t = std::sqrt(f.a), i2 = 1.0 / (2.
 inline Jet jcos(const Jet& f) { Jet r(std::cos(f.a)); const double s = -std::sin(f.a); for (int k = 0; k < 13; ++k) r.v[k] = s * f.v[k]; return r; }
 inline Jet jsin(const Jet& f) { Jet r(std::sin(f.a)); const double c = std::cos(f.a); for (int k = 0; k < 13; ++k) r.v[k] = c * f.v[k]; return r; }
 
-void residual_jet(const Jet* intr, const Jet* extr, const Jet* pt, const double* uv, Jet* res) {
+void residual_jet(int model, const Jet* intr, const Jet* extr, const Jet* pt, const double* uv, Jet* res) {
     const Jet* w = extr;
     Jet P[3];
     const Jet theta2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
@@ -160,6 +192,14 @@ void residual_jet(const Jet* intr, const Jet* extr, const Jet* pt, const double*
         for (int a = 0; a < 3; ++a) P[a] = pt[a] + cr[a];
     }
     P[0] = P[0] + extr[3]; P[1] = P[1] + extr[4]; P[2] = P[2] + extr[5];
+    if (model == SFM_CAM_SNAVELY) {   // SnavelyReprojectionError.h:31-47, term by term
+        const Jet xp = Jet(0.0) - P[0] / P[2], yp = Jet(0.0) - P[1] / P[2];
+        const Jet r2 = xp * xp + yp * yp;
+        const Jet dist = Jet(1.0) + r2 * (intr[1] + intr[2] * r2);
+        res[0] = intr[0] * dist * xp - Jet(uv[0]);
+        res[1] = intr[0] * dist * yp - Jet(uv[1]);
+        return;
+    }
     const Jet x = P[0] / P[2], y = P[1] / P[2];
     res[0] = intr[0] * x + intr[2] - Jet(uv[0]);
     res[1] = intr[1] * y + intr[3] - Jet(uv[1]);
@@ -352,7 +392,11 @@ struct Oracle {
         extr.assign(e, e + 6 * (size_t)P.n_img); intr.assign(in, in + 4 * (size_t)P.n_intr);
         xF.assign(nF, 0.0);
         for (int i = 0; i < P.n_img; ++i) if (cam_blk[i] >= 0) for (int a = 0; a < 6; ++a) xF[6 * cam_blk[i] + a] = extr[6 * i + a];
-        for (int q = 0; q < P.n_intr; ++q) if (intr_blk[q] >= 0) for (int a = 0; a < 4; ++a) xF[nb + 4 * intr_blk[q] + a] = intr[4 * q + a];
+        // SNAVELY: the 4th intrinsics double is not a parameter (held at 0, never written back)
+        for (int q = 0; q < P.n_intr; ++q)
+            if (intr_blk[q] >= 0)
+                for (int a = 0; a < 4; ++a)
+                    xF[nb + 4 * intr_blk[q] + a] = (P.camera_model == SFM_CAM_SNAVELY && a == 3) ? 0.0 : intr[4 * q + a];
         xE.resize(3 * pts.size());
         for (size_t k = 0; k < pts.size(); ++k) for (int a = 0; a < 3; ++a) xE[3 * k + a] = X[3 * pts[k] + a];
         f.assign(2 * n_sobs, 0.0); J.assign(26 * n_sobs, 0.0);
@@ -381,7 +425,7 @@ struct Oracle {
             for (int64_t o = P.pt_offsets[p], s = obs_ptr[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
                 const int img = P.obs_img[o];
                 double r[2], Jl[26];
-                const bool ok = residual_jacobian(&intr[4 * (size_t)P.img_intr[img]], &extr[6 * (size_t)img],
+                const bool ok = residual_jacobian(P.camera_model, &intr[4 * (size_t)P.img_intr[img]], &extr[6 * (size_t)img],
                                                   &xe[3 * k], &P.obs_uv[2 * o], r, jac ? Jl : nullptr);
                 if (!ok) { bad[tid] = 1; continue; }
                 const double sq = r[0] * r[0] + r[1] * r[1];
@@ -620,12 +664,18 @@ struct Oracle {
 
 extern "C" int orc_ba_jacobian(int32_t mode, const double* intr, const double* extr, const double* X,
                                const double* uv, double* r, double* J) {
-    if (mode == 0) return residual_jacobian(intr, extr, X, uv, r, J) ? SFM_OK : SFM_ERR_NOT_FINITE;
+    return orc_ba_jacobian_model(SFM_CAM_PINHOLE, mode, intr, extr, X, uv, r, J);
+}
+
+extern "C" int orc_ba_jacobian_model(int32_t model, int32_t mode, const double* intr, const double* extr,
+                                     const double* X, const double* uv, double* r, double* J) {
+    if (model != SFM_CAM_PINHOLE && model != SFM_CAM_SNAVELY) return SFM_ERR_INVALID_ARG;
+    if (mode == 0) return residual_jacobian(model, intr, extr, X, uv, r, J) ? SFM_OK : SFM_ERR_NOT_FINITE;
     Jet in[4], ex[6], pt[3], res[2];
     for (int a = 0; a < 4; ++a) in[a] = Jet(intr[a], a);
     for (int a = 0; a < 6; ++a) ex[a] = Jet(extr[a], 4 + a);
     for (int a = 0; a < 3; ++a) pt[a] = Jet(X[a], 10 + a);
-    residual_jet(in, ex, pt, uv, res);
+    residual_jet(model, in, ex, pt, uv, res);
     for (int row = 0; row < 2; ++row) {
         r[row] = res[row].a;
         for (int k = 0; k < 13; ++k) J[13 * row + k] = res[row].v[k];
@@ -641,7 +691,7 @@ extern "C" int orc_ba_cost(const sfm_ba_problem* P, const double* extr, const do
         for (int64_t o = P->pt_offsets[p]; o < P->pt_offsets[p + 1]; ++o) {
             const int img = P->obs_img[o];
             double r[2];
-            residual_jacobian(&intr[4 * (size_t)P->img_intr[img]], &extr[6 * (size_t)img], &X[3 * p],
+            residual_jacobian(P->camera_model, &intr[4 * (size_t)P->img_intr[img]], &extr[6 * (size_t)img], &X[3 * p],
                               &P->obs_uv[2 * o], r, nullptr);
             double rho[2];
             huber(P->huber_a, r[0] * r[0] + r[1] * r[1], rho);
@@ -658,6 +708,7 @@ extern "C" int orc_ba_solve(const sfm_ba_problem* P, double* extr, double* intr,
                             int64_t n_shard_pts, orc_allreduce_fn allreduce, void* user,
                             int32_t n_threads) {
     if (!P || !extr || !intr || !X || !sum || P->n_img < 0 || P->n_pt < 0) return SFM_ERR_INVALID_ARG;
+    if (P->camera_model != SFM_CAM_PINHOLE && P->camera_model != SFM_CAM_SNAVELY) return SFM_ERR_INVALID_ARG;
     sfm_ba_options O;
     if (opts) {
         O = *opts;
@@ -688,7 +739,10 @@ extern "C" int orc_ba_solve(const sfm_ba_problem* P, double* extr, double* intr,
         for (size_t k = 0; trace && k < iters.size() && (int32_t)k < trace_cap; ++k) trace[k] = iters[k];
         if (sum->usable) {  // BundleAdjuster::updateWorld only on a usable solution
             for (int i = 0; i < P->n_img; ++i) if (S.cam_blk[i] >= 0) for (int a = 0; a < 6; ++a) extr[6 * i + a] = S.xF[6 * S.cam_blk[i] + a];
-            for (int q = 0; q < P->n_intr; ++q) if (S.intr_blk[q] >= 0) for (int a = 0; a < 4; ++a) intr[4 * q + a] = S.xF[S.nb + 4 * S.intr_blk[q] + a];
+            for (int q = 0; q < P->n_intr; ++q)
+                if (S.intr_blk[q] >= 0)
+                    for (int a = 0; a < (P->camera_model == SFM_CAM_SNAVELY ? 3 : 4); ++a)
+                        intr[4 * q + a] = S.xF[S.nb + 4 * S.intr_blk[q] + a];
             for (size_t k = 0; k < S.pts.size(); ++k) for (int a = 0; a < 3; ++a) X[3 * S.pts[k] + a] = S.xE[3 * k + a];
         }
         return term == SFM_TERM_FAILURE ? SFM_ERR_SOLVER : SFM_OK;

@@ -12,7 +12,9 @@
  *   - src/adjuster/BundleAdjuster.h:33-69 (ReprojectCost), :109 (Huber 4),
  *     :105 (gauge), :125-139 (Solve + RMSE definition) with the published
  *     Ceres 2.2 TrustRegionMinimizer / LevenbergMarquardtStrategy /
- *     SchurEliminator control flow (documented in oracle/ba_oracle.cpp);
+ *     SchurEliminator control flow (documented in oracle/ba_oracle.cpp),
+ *     and src/adjuster/SnavelyReprojectionError.h:16-54 (BAL residual model,
+ *     SURVEY.md §8(f) row 4) as an alternative residual;
  *   - OpenMVG Matcher_Regions(BRUTE_FORCE_L2) ratio matching as selected by
  *     src/sparseBuilder/sparseBuilder.cpp:919-921 with fDistRatio 0.8 (:812);
  *   - OpenCV BFMatcher(NORM_L2, crossCheck) knnMatch(k=1) as used by
@@ -53,6 +55,11 @@ int orc_ba_cost(const sfm_ba_problem* prob, const double* extr, const double* in
  * ceres::AngleAxisRotatePoint (the Ceres AutoDiff path). */
 int orc_ba_jacobian(int32_t mode, const double* intr, const double* extr, const double* X,
                     const double* uv, double* r, double* J);
+
+/* Same for a residual model SFM_CAM_* (SNAVELY: SnavelyReprojectionError.h,
+ * intrinsics {f, l1, l2, -}, J column 3 is zero). */
+int orc_ba_jacobian_model(int32_t model, int32_t mode, const double* intr, const double* extr,
+                          const double* X, const double* uv, double* r, double* J);
 
 /* Dense single-pair matching: same contract as sfm_match_dense. */
 int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,

@@ -30,6 +30,9 @@ def oracle():
         lib.orc_ba_jacobian.restype = C.c_int
         lib.orc_ba_jacobian.argtypes = [C.c_int32, abi.f64p, abi.f64p, abi.f64p, abi.f64p,
                                         abi.f64p, abi.f64p]
+        lib.orc_ba_jacobian_model.restype = C.c_int
+        lib.orc_ba_jacobian_model.argtypes = [C.c_int32, C.c_int32, abi.f64p, abi.f64p, abi.f64p,
+                                              abi.f64p, abi.f64p, abi.f64p]
         lib.orc_match_dense.restype = C.c_int
         lib.orc_match_dense.argtypes = [abi.u8p, C.c_int32, abi.u8p, C.c_int32, C.c_int32,
                                         C.c_float, abi.i32p, abi.i32p]
@@ -51,7 +54,7 @@ class Scene:
 
     def __init__(self, n_cam, n_pt, k, vis_mode=0, n_intr=1, seed=0x5F3D0001, noise=0.5,
                  outliers=0.01, perturb=(0.01, 0.05, 0.05, 5.0), const_img=1, huber=4.0,
-                 lib=None):
+                 lib=None, model=0):
         lib = lib or oracle()
         cfg = abi.SynthBAConfig()
         cfg.n_cam, cfg.k, cfg.vis_mode, cfg.n_intr = n_cam, k, vis_mode, n_intr
@@ -59,6 +62,7 @@ class Scene:
         cfg.noise_px, cfg.outlier_frac = noise, outliers
         cfg.perturb_rot, cfg.perturb_t, cfg.perturb_X, cfg.perturb_f = perturb
         cfg.const_img = const_img
+        cfg.camera_model = model
         n_obs = C.c_int64()
         rc = lib.sfm_synth_ba(C.byref(cfg), None, None, None, None, None, None, None, None,
                               None, None, C.byref(n_obs))
@@ -82,7 +86,7 @@ class Scene:
                               p(self.gt_X, abi.f64p), C.byref(n_obs))
         assert rc == 0
         self.n_cam, self.n_intr, self.n_pt, self.n_obs = n_cam, n_intr, n_pt, no
-        self.const_img, self.huber = const_img, huber
+        self.const_img, self.huber, self.model = const_img, huber, model
 
     def problem(self):
         pr = abi.BAProblem()
@@ -92,6 +96,7 @@ class Scene:
         pr.obs_uv = abi.ptr(self.obs_uv, abi.f64p)
         pr.img_intr = abi.ptr(self.img_intr, abi.i32p)
         pr.const_img = self.const_img
+        pr.camera_model = self.model
         pr.huber_a = self.huber
         self._keep = pr
         return pr
