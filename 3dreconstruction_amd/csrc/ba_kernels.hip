@@ -482,11 +482,18 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 
 // copy the chunk's staged cameras' CamPre into LDS (one wave)
-__device__ __forceinline__ void stage_campre(const ChunkDesc& cd, const CamPre* __restrict__ cps, CamPre* dst) {
+// LDS copy of a CamPre padded to 240 B (60 dwords): lanes of a batch read up
+// to 10 different cameras' fields at once, and a 60-dword stride puts their
+// 16-byte reads on disjoint banks (224 B = 56 dwords collided: 56 * 8 = 0 mod 64)
+struct alignas(16) CamPreL {
+    CamPre cp;
+    double pad[2];
+};
+__device__ __forceinline__ void stage_campre(const ChunkDesc& cd, const CamPre* __restrict__ cps, CamPreL* dst) {
     constexpr int kCpW = sizeof(CamPre) / 8;
     for (int e = threadIdx.x; e < cd.n_cams * kCpW; e += 64) {
         const int t = e / kCpW;
-        reinterpret_cast<double*>(&dst[t])[e - t * kCpW] =
+        reinterpret_cast<double*>(&dst[t].cp)[e - t * kCpW] =
             reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
     }
 }
@@ -537,14 +544,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT, kPS = kPR + 4;
     __shared__ double panel[kPK][kPS];          // [k][row]
     __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
-    constexpr int kOb = CM == SFM_CAM_SNAVELY ? 6 : 4;
-    __shared__ double ob[SO][kOb];              // J_intr nonzeros (scaled)
-    __shared__ double vs[SO][10];               // per observation: Jx'Jx (6) | Jx'f (3) | pad
+    // per-observation rows use odd strides (in doubles): a wave's ds_*_b64 at
+    // lane-strided rows then hits 32 distinct bank pairs (even strides of 4,
+    // 6, 10 doubles were 2- to 4-way bank conflicts, SQ_LDS_BANK_CONFLICT)
+    constexpr int kOb = CM == SFM_CAM_SNAVELY ? 7 : 5;
+    __shared__ double ob[SO][kOb];              // J_intr nonzeros (scaled) | pad
+    __shared__ double vs[SO][9];                // per observation: Jx'Jx (6) | Jx'f (3)
     __shared__ double vsum[SP][10];             // per point: V (6) | g_E (3)
-    __shared__ double obm[SO][6];               // M = Jx L^-T
+    __shared__ double obm[SO][7];               // M = Jx L^-T | pad
     __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
-    __shared__ CamPre scp[kCamSlots];
+    __shared__ CamPreL scp[kCamSlots];
     __shared__ double csc[kCamSlots][6];        // camera column scales (0: constant image)
     __shared__ double isc[kIntrSlots][8];       // intrinsics | their column scales
     __shared__ int crow[kCamSlots], irow[kIntrSlots];
@@ -623,7 +633,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         Lin L;
         const int cs = slot & 255, is = (slot >> 8) & 255;
         if (lane < nobs) {
-            linearize<CM, true, true, true>(scp[cs], &isc[is][0], Xp, u0, u1, P.huber_a, L);
+            linearize<CM, true, true, true>(scp[cs].cp, &isc[is][0], Xp, u0, u1, P.huber_a, L);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
 #pragma unroll

@@ -150,8 +150,13 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // MFMA work per point; it is used unless it would need many more chunks.
     // 128 points per chunk: ~2x the co-resident waves of the chip at C4 size,
     // so the last round of chunks is short (256 measured 17% slower).
-    int chunk_pts = kChunkPts;   // tuning override (diagnostics)
-    if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));
+    // A shard too small to give every wave slot of the chip a 128-point chunk
+    // (a landmark shard at N = 4, 8) gets shorter chunks instead, down to 16
+    // points: the Schur pass takes about one chunk's latency once the chunks
+    // fit in one round, so 2048 chunks (8 waves per CU) keep it dividing by N.
+    constexpr int64_t kTargetChunks = 2048;
+    int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_spt + kTargetChunks - 1) / kTargetChunks));
+    if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));   // tuning override
     auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, std::vector<int32_t>& slot_out) -> int64_t {
         int64_t flops = 0;
         slot_out.assign(pl.n_sobs, 0);
