@@ -210,20 +210,25 @@ __device__ __forceinline__ void diag16_xrow(const double (&a)[16], const double 
                                             std::integer_sequence<int, P...>) {
     ((P & 1 ? fmac_bc<false>(u1, a[P], x[P], K) : fmac_bc<P == 0>(u0, a[P], x[P], K)), ...);
 }
+// The wave is VALU-issue bound here (one wave, fp64: ~8 cycles per
+// instruction), so each pivot is kept to few instructions: no select for the
+// new column (lane K's a_KK is d, so lk = a_iK rinv is L_KK on lane K, L_iK
+// below it, and only the never-read upper triangle above) and no per-pivot
+// definiteness test (a pivot d <= 0 or NaN leaves a non-positive or NaN L_KK,
+// checked once at the end).
 template <int K>
-__device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], bool& ok, int i) {
+__device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], int i) {
     const double d = row_bcast(a[K], K);
-    ok = ok && d > 0.0;
     const double rinv = rsqrt_nr(d);
-    const double lk = a[K] * rinv;       // L_ik (i > K)
+    const double lk = a[K] * rinv;       // L_iK (i >= K)
     const double nt = -(lk * rinv);      // -a_iK / d_K
     diag16_update<K>(a, nt, std::make_integer_sequence<int, 15 - K>{});
-    a[K] = i == K ? d * rinv : (i > K ? lk : a[K]);
+    a[K] = lk;
     // row K of L is final: lane c gets x_K = (delta_Kc - sum_p L_Kp x_p) / L_KK
     double u0 = 0.0, u1 = 0.0;
     diag16_xrow<K>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
     x[K] = ((K == i ? 1.0 : 0.0) - (u0 + u1)) * rinv;
-    if constexpr (K < 15) diag16_step<K + 1>(a, x, ok, i);
+    if constexpr (K < 15) diag16_step<K + 1>(a, x, i);
 }
 
 __device__ void diag16(double* A, double* X, double* bad, double* col) {
@@ -233,9 +238,11 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
     double a[16], x[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? A[i * LD + j] : 0.0;
-    bool ok = true;
-    diag16_step<0>(a, x, ok, i);
-    if (lane == 0 && !ok) bad[0] = 1.0;
+    diag16_step<0>(a, x, i);
+    double lii = 1.0;   // this lane's L_ii (a[i], extracted without dynamic indexing)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) lii = j == i ? a[j] : lii;
+    if (__ballot(act && !(lii > 0.0)) != 0 && lane == 0) bad[0] = 1.0;
     if (act) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
@@ -246,45 +253,66 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
 
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
 // the caller).  All 256 threads; ends synchronised.
+//
+// Look-ahead schedule: the critical path is the four wave-local diagonal
+// factors (VALU-issue bound) joined by one tile product each way:
+//   P(k)   panels L_ik = A_ik X_kk' (i > k) and X_kj = -X_kk T_kj (j < k):
+//          at most three tiles, one MFMA product each, waves 0..2
+//   D(k+1) wave 0: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}', then diag16(k+1);
+//          waves 1..3 meanwhile: the other trailing tiles of step k and the
+//          partial inverse rows T_{k+1,j} = sum_{m=j..k} L_{k+1,m} X_mj
 __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
                            unsigned long long* st = nullptr) {
     const int wave = threadIdx.x >> 6;
-    unsigned long long t0 = 0, td = 0;
+    unsigned long long t0 = 0, td = 0, ta = 0;
     if (st) t0 = stamp();
-    for (int k = 0; k < 4; ++k) {
-        unsigned long long ta = 0;
-        if (st) ta = stamp();
-        if (wave == 0) diag16(A + 16 * k * (LD + 1), X + 16 * k * (LD + 1), bad, col);
-        __syncthreads();
-        if (st) td += stamp() - ta;
-
-        if (wave < 3 - k) {   // panel: L_ik = A_ik X_kk'
-            const int i = k + 1 + wave;
-            const v4d t = tile_mm<false, true, false>(zero4(), A, LD, 16 * i, X, LD, 16 * k, 16 * k, 16 * k + 16);
-            tile_st(A, LD, 16 * i, 16 * k, t);
+    if (wave == 0) {
+        diag16(A, X, bad, col);
+        if (st) td += stamp() - t0;
+    }
+    __syncthreads();
+    for (int k = 0;; ++k) {
+        // ---- P(k): 3 - k panels, then k inverse tiles ----------------------
+        if (wave < 3) {
+            if (wave < 3 - k) {
+                const int i = k + 1 + wave;
+                tile_st(A, LD, 16 * i, 16 * k,
+                        tile_mm<false, true, false>(zero4(), A, LD, 16 * i, X, LD, 16 * k, 16 * k, 16 * k + 16));
+            } else {
+                const int j = wave - (3 - k);   // T_kj sits in X tile (k, j)
+                tile_st(X, LD, 16 * k, 16 * j,
+                        tile_mm<false, false, true>(zero4(), X, LD, 16 * k, X, LD, 16 * j, 16 * k, 16 * k + 16));
+            }
         }
         __syncthreads();
-        int t = 0;            // trailing: A_ij -= L_ik L_jk', k < j <= i
-        for (int i = k + 1; i < 4; ++i)
-            for (int j = k + 1; j <= i; ++j, ++t)
-                if ((t & 3) == wave) {
-                    v4d acc = tile_ld(A, LD, 16 * i, 16 * j);
-                    acc = tile_mm<false, true, true>(acc, A, LD, 16 * i, A, LD, 16 * j, 16 * k, 16 * k + 16);
-                    tile_st(A, LD, 16 * i, 16 * j, acc);
-                }
-        __syncthreads();
-    }
-    // X_ij = -X_ii sum_{m=j}^{i-1} L_im X_mj, by distance from the diagonal
-    for (int dd = 1; dd < 4; ++dd) {
-        if (wave < 4 - dd) {
-            const int i = dd + wave, j = i - dd;
-            v4d acc = zero4();
-            for (int m = j; m < i; ++m)
-                acc = tile_mm<false, false, false>(acc, A, LD, 16 * i, X, LD, 16 * j, 16 * m, 16 * m + 16);
-            tile_st(X, LD, 16 * i, 16 * j, acc);
+        if (k == 3) break;
+        // ---- D(k+1) ---------------------------------------------------------
+        const int n = k + 1;
+        if (wave == 0) {
+            if (st) ta = stamp();
+            v4d acc = tile_ld(A, LD, 16 * n, 16 * n);
+            acc = tile_mm<false, true, true>(acc, A, LD, 16 * n, A, LD, 16 * n, 16 * k, 16 * k + 16);
+            tile_st(A, LD, 16 * n, 16 * n, acc);
             wave_sync();
-            acc = tile_mm<false, false, true>(zero4(), X, LD, 16 * i, X, LD, 16 * j, 16 * i, 16 * i + 16);
-            tile_st(X, LD, 16 * i, 16 * j, acc);
+            diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+            if (st) td += stamp() - ta;
+        } else {
+            // items: trailing tiles (i, j), n <= j <= i < 4, (i, j) != (n, n);
+            // then T_nj, j < n
+            int t = 0;
+            for (int i = n; i < 4; ++i)
+                for (int j = n; j <= i; ++j) {
+                    if (i == n && j == n) continue;
+                    if (t++ % 3 == wave - 1) {
+                        v4d acc = tile_ld(A, LD, 16 * i, 16 * j);
+                        acc = tile_mm<false, true, true>(acc, A, LD, 16 * i, A, LD, 16 * j, 16 * k, 16 * k + 16);
+                        tile_st(A, LD, 16 * i, 16 * j, acc);
+                    }
+                }
+            for (int j = 0; j < n; ++j)
+                if (t++ % 3 == wave - 1)   // X is lower triangular: m runs j..n-1
+                    tile_st(X, LD, 16 * n, 16 * j,
+                            tile_mm<false, false, false>(zero4(), A, LD, 16 * n, X, LD, 16 * j, 16 * j, 16 * n));
         }
         __syncthreads();
     }
@@ -482,23 +510,34 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
     if (st) t1 = stamp();
     chol_inv64(A, X, bad, col, st);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
-    if (w == 0) {
-        double* Xg = b.L + (size_t)i * M * M;
-        for (int e = threadIdx.x; e < M * M; e += NT) Xg[e] = X[(e / M) * LD + e % M];
+    {   // X for the back substitution: each of the block's 4 workgroups stores 16 rows
+        double* Xg = b.L + (size_t)i * M * M + 16 * w * M;
+        for (int e = threadIdx.x; e < 16 * M; e += NT) Xg[e] = X[(16 * w + e / M) * LD + e % M];
     }
     if (st) {
         __syncthreads();
         if (threadIdx.x == 0) atomicAdd(st + 6, stamp() - t0);   // through the X copy
     }
-    const int kend = 16 * (wave + 1);   // X is lower triangular
-    tile_st(b.Wl + (size_t)i * M * M, M, 16 * wave, 16 * w,
-            tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Cc, L16, 0, 0, kend));
-    if (hr)   // op(B)[k][n] = C_r[16w + n][k]
-        tile_st(b.Wr + (size_t)i * M * M, M, 16 * wave, 16 * w,
-                tile_mm<false, true, false>(zero4(), X, LD, 16 * wave, Cr, LD, 0, 0, kend));
-    if (hz)
-        tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * wave, 16 * w,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, Rc, L16, 0, 0, kend));
+    // column tile w of Wl = X C_i, Wr = X C_r', z = X R_i: product p of row
+    // tile r costs r + 1 k-chunks (X is lower triangular); the 12 (p, r) items
+    // are split 8 / 8 / 8 / 6 chunks over the waves instead of 12 for row 3
+    constexpr int8_t kItems[4][4][2] = {{{0, 3}, {1, 3}, {-1, 0}, {-1, 0}},
+                                        {{2, 3}, {0, 2}, {0, 0}, {-1, 0}},
+                                        {{1, 2}, {2, 2}, {1, 1}, {-1, 0}},
+                                        {{0, 1}, {2, 1}, {1, 0}, {2, 0}}};
+    for (int q = 0; q < 4; ++q) {
+        const int pr = kItems[wave][q][0], r = kItems[wave][q][1], kend = 16 * (r + 1);
+        if (pr < 0) break;
+        if (pr == 0)
+            tile_st(b.Wl + (size_t)i * M * M, M, 16 * r, 16 * w,
+                    tile_mm<false, false, false>(zero4(), X, LD, 16 * r, Cc, L16, 0, 0, kend));
+        else if (pr == 1 && hr)   // op(B)[k][n] = C_r[16w + n][k]
+            tile_st(b.Wr + (size_t)i * M * M, M, 16 * r, 16 * w,
+                    tile_mm<false, true, false>(zero4(), X, LD, 16 * r, Cr, LD, 0, 0, kend));
+        else if (pr == 2 && hz)
+            tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * r, 16 * w,
+                    tile_mm<false, false, false>(zero4(), X, LD, 16 * r, Rc, L16, 0, 0, kend));
+    }
     if (st) {
         __syncthreads();
         if (threadIdx.x == 0) {
