@@ -1405,19 +1405,24 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
 }
 
 // fixed-order reduction of the per-block partials
-__global__ __launch_bounds__(256) void finalize_kernel(DevProblem P, int n_step_blocks) {
+// 1024 threads: each strides over ~4 partials per list instead of ~16 (the
+// pass is a chain of dependent global loads); fixed order, so deterministic
+constexpr int kFinThreads = 1024;
+__global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks) {
     double s[7] = {0, 0, 0, 0, 0, 0, 0};
     double m[5] = {0, 0, 0, 0, 0};
 #pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_fblk; i += 256) {
+    for (int i = threadIdx.x; i < P.n_fblk; i += kFinThreads) {
         s[5] += P.part_f[3 * i]; s[6] += P.part_f[3 * i + 1]; m[4] = fmax(m[4], P.part_f[3 * i + 2]);
     }
 #pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_img * kGramSeg; i += 256) { s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]); }
+    for (int i = threadIdx.x; i < P.n_img * kGramSeg; i += kFinThreads) {
+        s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]);
+    }
 #pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_chunk; i += 256) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
+    for (int i = threadIdx.x; i < P.n_chunk; i += kFinThreads) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
 #pragma unroll 4
-    for (int i = threadIdx.x; i < n_step_blocks; i += 256) {
+    for (int i = threadIdx.x; i < n_step_blocks; i += kFinThreads) {
         s[2] += P.part_t[kPartT * i]; s[3] += P.part_t[kPartT * i + 1]; s[4] += P.part_t[kPartT * i + 2];
         m[2] = fmax(m[2], P.part_t[kPartT * i + 4]);
         m[3] = fmax(m[3], P.part_t[kPartT * i + 3]);
@@ -1425,29 +1430,21 @@ __global__ __launch_bounds__(256) void finalize_kernel(DevProblem P, int n_step_
     wave_sum(s);
 #pragma unroll
     for (int k = 0; k < 5; ++k) m[k] = wave_max(m[k]);
-    __shared__ double red[4][12];
+    constexpr int kW = kFinThreads / 64;
+    __shared__ double red[kW][12];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) {
         for (int k = 0; k < 7; ++k) red[wave][k] = s[k];
         for (int k = 0; k < 5; ++k) red[wave][7 + k] = m[k];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double t[12];
-        for (int k = 0; k < 7; ++k) t[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
-        for (int k = 7; k < 12; ++k) t[k] = fmax(fmax(red[0][k], red[1][k]), fmax(red[2][k], red[3][k]));
-        P.scal[kScCost] = t[0];
-        P.scal[kScXnorm2E] = t[1];
-        P.scal[kScModelAcc] = t[2];
-        P.scal[kScCandCost] = t[3];
-        P.scal[kScStepnorm2E] = t[4];
-        P.scal[kScXnorm2F] = t[5];
-        P.scal[kScStepnorm2F] = t[6];
-        P.scal[kScBadX] = t[7];
-        P.scal[kScGmaxE] = t[8];
-        P.scal[kScCandBad] = t[9];
-        P.scal[kScStepBad] = t[10];
-        P.scal[kScGmaxF] = t[11];
+    if (threadIdx.x < 12) {   // one thread per scalar, waves in order
+        const int k = threadIdx.x;
+        double t = red[0][k];
+        for (int w = 1; w < kW; ++w) t = k < 7 ? t + red[w][k] : fmax(t, red[w][k]);
+        constexpr int kSlot[12] = {kScCost, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E, kScXnorm2F,
+                                   kScStepnorm2F, kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScGmaxF};
+        P.scal[kSlot[k]] = t;
     }
 }
 
@@ -1569,7 +1566,7 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
 }
 
 void ba_finalize(const DevProblem& P, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, P, ba_step_blocks(P));
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinThreads), 0, s, P, ba_step_blocks(P));
     SFM_HIP(hipGetLastError());
 }
 
