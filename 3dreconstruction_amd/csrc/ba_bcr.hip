@@ -133,28 +133,6 @@ __device__ __forceinline__ void load_rows(double* dst, int ld_dst, const double*
     else load_tile<16>(dst, ld_dst, src, ld_src);
 }
 
-// value of v in lane l (l wave-uniform): two v_readlane_b32
-__device__ __forceinline__ double rdlane(double v, int l) {
-    const long long bits = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)bits, l);
-    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// 1/d: hardware estimate + two Newton steps (full fp64 accuracy)
-__device__ __forceinline__ double rcp_nr(double d) {
-    double y = __builtin_amdgcn_rcp(d);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) y = fma(y, fma(-d, y, 1.0), y);
-    return y;
-}
-
 // value of v in lane l of this lane's 16-lane row (DPP row_newbcast, 64-bit);
 // l must fold to a constant
 __device__ __forceinline__ double row_bcast(double v, int l) {
