@@ -903,15 +903,24 @@ __global__ void reduce_kernel(DevProblem P, int min_kind) {
     if (e >= T.rows * T.cols) return;
     const int r = e / T.cols, cc = e % T.cols;
     const bool vec = T.cols == 1;
-    // batches of 8 independent loads, summed in term order (deterministic)
+    // batches of 16 (then 4) independent loads, summed in term order
+    // (deterministic); a target is a chain of dependent global round trips
+    // (term descriptor, then data), so the batch width sets its latency
     double s = 0.0;
     int k = T.c_begin;
-    for (; k + 8 <= T.c_end; k += 8) {
-        double v[8];
+    for (; k + 16 <= T.c_end; k += 16) {
+        double v[16];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = term_value(P, P.terms[k + j], r, cc);
+        for (int j = 0; j < 16; ++j) v[j] = term_value(P, P.terms[k + j], r, cc);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += v[j];
+        for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; k + 4 <= T.c_end; k += 4) {
+        double v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = term_value(P, P.terms[k + j], r, cc);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += v[j];
     }
     for (; k < T.c_end; ++k) s += term_value(P, P.terms[k], r, cc);
     double* dst;

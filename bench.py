@@ -150,6 +150,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--no-snavely", action="store_true")
+    # diagnostic: rank 0's shard of an N-way landmark partition on this one GPU,
+    # with a no-op all-reduce (per-rank kernel times of the N-GPU run; the
+    # solve itself is then not the global one, so the result is not a bench line)
+    ap.add_argument("--fake-world", type=int, default=0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,6 +212,10 @@ def main():
             ctx = api.Context(device=local_rank, rank=rank, world_size=world, allreduce=host_allreduce)
             transport = "gloo-host (RCCL unavailable)"
             log("falling back to the host-staged gloo all-reduce")
+    elif args.fake_world > 1:
+        ctx = api.Context(device=local_rank, rank=0, world_size=args.fake_world,
+                          allreduce=lambda a, op: None)
+        transport = f"none (diagnostic: shard 0 of {args.fake_world}, no-op all-reduce)"
     else:
         ctx = api.Context(device=local_rank)
 
