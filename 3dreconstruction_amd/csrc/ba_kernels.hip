@@ -455,6 +455,11 @@ __global__ void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
     for (int a = 0; a < 3; ++a) P.scaleE[3 * (size_t)p + a] = 1.0 / (1.0 + sqrt(cn[a]));
 }
 
+__global__ void fill_kernel(double* p, int64_t n, double v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
 __global__ void fscale_kernel(DevProblem P) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c < P.nF) P.scaleF[c] = 1.0 / (1.0 + sqrt(P.cnF[c]));
@@ -1492,6 +1497,12 @@ void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, c
     if (P.n_spt <= 0) return;
     SFM_BY_MODEL(P, hipLaunchKernelGGL(point_scale_kernel<CM>, dim3((P.n_spt + 255) / 256), dim3(256), 0, s, P,
                                        cp, intr, X));
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_fill(double* p, int64_t n, double v, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, n, v);
     SFM_HIP(hipGetLastError());
 }
 
