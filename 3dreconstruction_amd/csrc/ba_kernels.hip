@@ -435,17 +435,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
 }
 
 // Jacobi scale of the point columns (iteration 0): 1 / (1 + |J col|).
+// One workgroup per Schur chunk, one thread per point, the chunk's cameras and
+// intrinsics staged in LDS (gathering each observation's CamPre from global
+// memory made this pass latency bound: 111 us at C4).
 template <int CM>
-__global__ void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
-                                   const double* __restrict__ intr, const double* __restrict__ X) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P.n_spt) return;
+__global__ __launch_bounds__(kChunkPts) void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                                const double* __restrict__ intr,
+                                                                const double* __restrict__ X) {
+    __shared__ CamPre scp[kCamSlots];
+    __shared__ double sin_[kIntrSlots][4];
+    const ChunkDesc& cd = P.chunks[blockIdx.x];
+    const int tid = threadIdx.x;
+    constexpr int kCpW = sizeof(CamPre) / 8;
+    for (int e = tid; e < cd.n_cams * kCpW; e += blockDim.x) {
+        const int t = e / kCpW;
+        reinterpret_cast<double*>(&scp[t])[e - t * kCpW] =
+            reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
+    }
+    if (tid < 4 * cd.n_intr) sin_[tid >> 2][tid & 3] = intr[4 * cd.intr_id[tid >> 2] + (tid & 3)];
+    __syncthreads();
+    const int p = cd.pt_begin + tid;
+    if (p >= cd.pt_end) return;
+    const double Xp[3] = {X[3 * (size_t)p], X[3 * (size_t)p + 1], X[3 * (size_t)p + 2]};
     double cn[3] = {0, 0, 0};
     for (int o = P.pt_off[p]; o < P.pt_off[p + 1]; ++o) {
-        const int img = P.obs_img[o];
+        const int slot = P.obs_slot[o];
+        const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
         Lin L;
-        linearize<CM, false, false, true>(cps[img], intr + 4 * P.img_intr[img], X + 3 * p, P.obs_uv[2 * o],
-                                      P.obs_uv[2 * o + 1], P.huber_a, L);
+        linearize<CM, false, false, true>(scp[slot & 255], sin_[(slot >> 8) & 255], Xp, uv.x, uv.y, P.huber_a, L);
 #pragma unroll
         for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -1495,8 +1512,8 @@ void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, co
 void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                     hipStream_t s) {
     if (P.n_spt <= 0) return;
-    SFM_BY_MODEL(P, hipLaunchKernelGGL(point_scale_kernel<CM>, dim3((P.n_spt + 255) / 256), dim3(256), 0, s, P,
-                                       cp, intr, X));
+    SFM_BY_MODEL(P, hipLaunchKernelGGL(point_scale_kernel<CM>, dim3(P.n_chunk), dim3(kChunkPts), 0, s, P, cp,
+                                       intr, X));
     SFM_HIP(hipGetLastError());
 }
 
