@@ -14,12 +14,29 @@
 #include <climits>
 #include <map>
 #include <numeric>
+#include <thread>
 
 #include "common.h"
 
 namespace sfm {
 
 namespace {
+
+// Split [0, n) into contiguous ranges over up to 16 host threads (results are
+// independent of the split: every range writes its own outputs).
+template <class F>
+void parallel_ranges(int64_t n, F&& fn) {
+    const int64_t hw = std::max<int64_t>(1, std::min<int64_t>(16, std::thread::hardware_concurrency()));
+    const int64_t nt = n < 65536 ? 1 : hw;
+    if (nt <= 1) {
+        fn(0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 1; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt, (int)t); });
+    fn(0, n / nt, 0);
+    for (auto& x : th) x.join();
+}
 
 void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
     pl.cam_blk.assign(P.n_img, -1);
@@ -133,15 +150,17 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     pl.obs_pt.resize(pl.n_sobs);
     pl.obs_uv.resize(2 * pl.n_sobs);
     pl.obs_slot.assign(pl.n_sobs, 0);
-    for (int64_t k = 0; k < pl.n_spt; ++k) {
-        const int64_t p = pl.spt_global[k];
-        for (int64_t o = P.pt_offsets[p], s = pl.pt_off[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
-            pl.obs_img[s] = P.obs_img[o];
-            pl.obs_pt[s] = (int32_t)k;
-            pl.obs_uv[2 * s] = P.obs_uv[2 * o];
-            pl.obs_uv[2 * s + 1] = P.obs_uv[2 * o + 1];
+    parallel_ranges(pl.n_spt, [&](int64_t k0, int64_t k1, int) {
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t p = pl.spt_global[k];
+            for (int64_t o = P.pt_offsets[p], s = pl.pt_off[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
+                pl.obs_img[s] = P.obs_img[o];
+                pl.obs_pt[s] = (int32_t)k;
+                pl.obs_uv[2 * s] = P.obs_uv[2 * o];
+                pl.obs_uv[2 * s + 1] = P.obs_uv[2 * o + 1];
+            }
         }
-    }
+    });
 
     // ---- Schur chunks --------------------------------------------------------
     // Greedy over shard points: a chunk's F blocks (camera 6 rows, intrinsics 4
@@ -162,6 +181,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         slot_out.assign(pl.n_sobs, 0);
         ChunkDesc cd{};
         std::vector<int> cams, intrs, dcams;  // F-slot images / intrinsics, staged images
+        // O(1) membership for the open chunk: image -> F slot / staged index,
+        // intrinsics -> staged index (-1 = absent); reset through the lists
+        std::vector<int> cam_slot(P.n_img, -1), dcam_idx(P.n_img, -1), intr_idx(P.n_intr, -1);
         int rows = 0;
         auto reset = [&](int32_t p) {
             cd = ChunkDesc{};
@@ -170,6 +192,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             for (int s = 0; s < kMaxSlots; ++s) { cd.slot_img[s] = -1; cd.slot_intr[s] = -1; cd.slot_row[s] = -1; cd.slot_col[s] = -1; }
             for (int s = 0; s < kCamSlots; ++s) { cd.cam_img[s] = -1; cd.cam_row[s] = -1; cd.cam_col[s] = -1; }
             for (int s = 0; s < kIntrSlots; ++s) { cd.intr_id[s] = -1; cd.intr_row[s] = -1; cd.intr_col[s] = -1; }
+            for (int img : cams) cam_slot[img] = -1;
+            for (int img : dcams) dcam_idx[img] = -1;
+            for (int q : intrs) intr_idx[q] = -1;
             cams.clear(); intrs.clear(); dcams.clear(); rows = 0;
         };
         auto close = [&](int32_t p_end) {
@@ -180,19 +205,29 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             cd.n_intr = (int32_t)intrs.size();
             chunks_out.push_back(cd);
         };
-        auto has = [](const std::vector<int>& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); };
+        // per-point image lists in fixed storage (<= kSubObs each): this loop
+        // runs once per point, and heap vectors here dominated planning time
+        struct Small {
+            int v[kSubObs];
+            int n = 0;
+            void push_back(int x) { v[n++] = x; }
+            const int* begin() const { return v; }
+            const int* end() const { return v + n; }
+            size_t size() const { return (size_t)n; }
+            bool has(int x) const { return std::find(v, v + n, x) != v + n; }
+        };
         if (pl.n_spt > 0) reset(0);
         for (int32_t k = 0; k < (int32_t)pl.n_spt; ++k) {
             const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
             SFM_REQUIRE(nobs <= kSubObs, SFM_ERR_UNSUPPORTED, "point with %d observations (> %d)",
                         nobs, kSubObs);
-            std::vector<int> pc, pi, pd;
+            Small pc, pi, pd;
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
                 const int img = pl.obs_img[s];
                 if (pl.cam_blk[img] >= 0) pc.push_back(img);
                 pd.push_back(img);
                 const int q = P.img_intr[img];
-                if (!has(pi, q)) pi.push_back(q);
+                if (!pi.has(q)) pi.push_back(q);
             }
             const int own = 6 * (int)pc.size() + 4 * (int)pi.size();
             SFM_REQUIRE(own <= cap && (int)pd.size() <= kCamSlots && (int)pi.size() <= kIntrSlots,
@@ -200,9 +235,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                         "point %lld spans %d F rows / %d images (> %d / %d): track too long for this build",
                         (long long)pl.spt_global[k], own, (int)pd.size(), cap, kCamSlots);
             int add = 0, add_slots = 0, add_d = 0, add_i = 0;
-            for (int img : pc) if (!has(cams, img)) { add += 6; ++add_slots; }
-            for (int q : pi) if (!has(intrs, q)) { add += 4; ++add_slots; ++add_i; }
-            for (int img : pd) if (!has(dcams, img)) ++add_d;
+            for (int img : pc) if (cam_slot[img] < 0) { add += 6; ++add_slots; }
+            for (int q : pi) if (intr_idx[q] < 0) { add += 4; ++add_slots; ++add_i; }
+            for (int img : pd) if (dcam_idx[img] < 0) ++add_d;
             const bool full = k > cd.pt_begin &&
                               (rows + add > cap || k - cd.pt_begin >= chunk_pts ||
                                (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots ||
@@ -210,36 +245,37 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                                (int)intrs.size() + add_i > kIntrSlots);
             if (full) { close(k); reset(k); }
             for (int img : pc)
-                if (!has(cams, img)) {
+                if (cam_slot[img] < 0) {
                     const int s = (int)(cams.size() + intrs.size());
                     cams.push_back(img);
+                    cam_slot[img] = s;
                     cd.slot_img[s] = img; cd.slot_row[s] = rows; cd.slot_col[s] = pl.img_colc[img];
                     rows += 6;
                 }
             for (int q : pi)
-                if (!has(intrs, q)) {
+                if (intr_idx[q] < 0) {
                     const int s = (int)(cams.size() + intrs.size());
                     const int t = (int)intrs.size();
                     intrs.push_back(q);
+                    intr_idx[q] = t;
                     cd.slot_intr[s] = q; cd.slot_row[s] = rows;
                     cd.slot_col[s] = (int32_t)(pl.nb + 4 * pl.intr_blk[q]);
                     cd.intr_id[t] = q; cd.intr_row[t] = rows; cd.intr_col[t] = cd.slot_col[s];
                     rows += 4;
                 }
             for (int img : pd)
-                if (!has(dcams, img)) {
+                if (dcam_idx[img] < 0) {
                     const int t = (int)dcams.size();
                     dcams.push_back(img);
+                    dcam_idx[img] = t;
                     cd.cam_img[t] = img;
-                    for (int s = 0; s < kMaxSlots; ++s)
-                        if (cd.slot_img[s] == img) { cd.cam_row[t] = cd.slot_row[s]; cd.cam_col[t] = cd.slot_col[s]; }
+                    const int s = cam_slot[img];   // constant images have no F slot
+                    if (s >= 0) { cd.cam_row[t] = cd.slot_row[s]; cd.cam_col[t] = cd.slot_col[s]; }
                 }
             // observation -> staged camera | staged intrinsics << 8
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
                 const int img = pl.obs_img[s];
-                const int cs = (int)(std::find(dcams.begin(), dcams.end(), img) - dcams.begin());
-                const int is = (int)(std::find(intrs.begin(), intrs.end(), P.img_intr[img]) - intrs.begin());
-                slot_out[s] = cs | (is << 8);
+                slot_out[s] = dcam_idx[img] | (intr_idx[P.img_intr[img]] << 8);
             }
             const int64_t nfp = own;
             flops += 2LL * 3 * nfp * nfp + 600LL * nobs;   // Z Z' over the point's F rows + linearisation
@@ -263,12 +299,24 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     pl.tile_nt = 5;
     // the 64-row kernel walks 48-observation batches (ba_kernels.hip)
     if (max_own <= 64 && max_obs <= 48 && !std::getenv("SFM_BA_TILE80")) {
-        std::vector<ChunkDesc> c4;
-        std::vector<int32_t> s4;
-        const int64_t f4 = make_chunks(64, c4, s4);
-        std::vector<ChunkDesc> c5;
-        std::vector<int32_t> s5;
-        const int64_t f5 = make_chunks(kTileRowsUsed, c5, s5);
+        // both tile heights are planned concurrently (independent, read-only inputs)
+        std::vector<ChunkDesc> c4, c5;
+        std::vector<int32_t> s4, s5;
+        int64_t f4 = 0, f5 = 0;
+        int rc5 = SFM_OK;
+        std::thread t5([&] {
+            rc5 = guarded([&] {
+                f5 = make_chunks(kTileRowsUsed, c5, s5);
+                return SFM_OK;
+            });
+        });
+        int rc4 = guarded([&] {
+            f4 = make_chunks(64, c4, s4);
+            return SFM_OK;
+        });
+        t5.join();
+        if (rc4 != SFM_OK) throw SfmError{rc4};
+        if (rc5 != SFM_OK) throw SfmError{rc5};
         if (c4.size() * 4 <= c5.size() * 5) {
             pl.tile_nt = 4; pl.chunks.swap(c4); pl.obs_slot.swap(s4); flops = f4;
         } else {
@@ -282,21 +330,47 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                      (int64_t)pl.chunks.size() * kTileR * kTileR * 8;
 
     // ---- image CSR of shard observations ------------------------------------
+    // counting sort by image, in parallel: per-range counts, then each range
+    // scatters from its own offsets (ranges in order => shard order per image)
     pl.img_obs_ptr.assign(P.n_img + 1, 0);
-    for (int64_t s = 0; s < pl.n_sobs; ++s) pl.img_obs_ptr[pl.obs_img[s] + 1]++;
-    for (int i = 0; i < P.n_img; ++i) pl.img_obs_ptr[i + 1] += pl.img_obs_ptr[i];
     pl.img_obs.resize(pl.n_sobs);
     pl.img_pt.resize(pl.n_sobs);
     pl.img_uv.resize(2 * pl.n_sobs);
     {
-        std::vector<int32_t> fill(pl.img_obs_ptr.begin(), pl.img_obs_ptr.end() - 1);
-        for (int64_t s = 0; s < pl.n_sobs; ++s) {
-            const int32_t q = fill[pl.obs_img[s]]++;
-            pl.img_obs[q] = (int32_t)s;
-            pl.img_pt[q] = pl.obs_pt[s];
-            pl.img_uv[2 * q] = pl.obs_uv[2 * s];
-            pl.img_uv[2 * q + 1] = pl.obs_uv[2 * s + 1];
+        constexpr int kMaxT = 16;
+        std::vector<std::vector<int32_t>> cnt(kMaxT);
+        std::vector<std::pair<int64_t, int64_t>> rng(kMaxT, {0, 0});
+        parallel_ranges(pl.n_sobs, [&](int64_t s0, int64_t s1, int t) {
+            rng[t] = {s0, s1};
+            cnt[t].assign(P.n_img, 0);
+            for (int64_t s = s0; s < s1; ++s) cnt[t][pl.obs_img[s]]++;
+        });
+        for (int i = 0; i < P.n_img; ++i) {
+            int32_t tot = 0;
+            for (int t = 0; t < kMaxT; ++t)
+                if (!cnt[t].empty()) tot += cnt[t][i];
+            pl.img_obs_ptr[i + 1] = pl.img_obs_ptr[i] + tot;
         }
+        // per-range write cursors: image start + counts of earlier ranges
+        for (int i = 0; i < P.n_img; ++i) {
+            int32_t at = pl.img_obs_ptr[i];
+            for (int t = 0; t < kMaxT; ++t)
+                if (!cnt[t].empty()) {
+                    const int32_t c = cnt[t][i];
+                    cnt[t][i] = at;
+                    at += c;
+                }
+        }
+        parallel_ranges(pl.n_sobs, [&](int64_t s0, int64_t s1, int t) {
+            std::vector<int32_t>& fill = cnt[t];
+            for (int64_t s = s0; s < s1; ++s) {
+                const int32_t q = fill[pl.obs_img[s]]++;
+                pl.img_obs[q] = (int32_t)s;
+                pl.img_pt[q] = pl.obs_pt[s];
+                pl.img_uv[2 * q] = pl.obs_uv[2 * s];
+                pl.img_uv[2 * q + 1] = pl.obs_uv[2 * s + 1];
+            }
+        });
     }
 
     // ---- reduce plan -----------------------------------------------------------

@@ -343,6 +343,22 @@ def main():
                  "digest": mplan.digest()}
         log(f"match: {len(pairs)} pairs in {mdt:.3f}s -> {len(pairs) / mdt:.0f} pairs/s, "
             f"{tops:.0f} TOP/s")
+        # the legacy exact matcher (LocalFrame/GlobalFrame crossCheck):
+        # MUTUAL mode on the first tenth of the pair list (two top-1 passes per pair)
+        msub = pairs[: max(1, len(pairs) // 10)]
+        mlo, mhi = len(msub) * rank // world, len(msub) * (rank + 1) // world
+        ctx.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        mplan.run(msub[mlo:mhi], mode=abi.SFM_MATCH_MUTUAL, count=False)
+        ctx.synchronize()
+        barrier()
+        udt = max_over_ranks(time.perf_counter() - t1)
+        match["mutual"] = {"metric": "SIFT mutual (crossCheck) match pairs/sec", "value": len(msub) / udt,
+                           "unit": "pairs/s", "pairs": len(msub),
+                           "workload": "first 10% of the C3 pair list, BFMatcher(NORM_L2, crossCheck) "
+                                       "semantics (LocalFrame.h:31-47), exact"}
+        log(f"match mutual: {len(msub)} pairs in {udt:.3f}s -> {len(msub) / udt:.0f} pairs/s")
 
     cpu = None
     cpu_match = None
