@@ -5,4 +5,4 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_ba_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/q_tests.log 2>&1 || { tail -30 gpurun_out/q_tests.log; exit 1; }
 tail -1 gpurun_out/q_tests.log
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-match 2> gpurun_out/q_b.err | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', d['value'], 'ms/step', d['ms_per_step'], 'schur ms', d['roofline']['per_launch_ms'], 'frac', d['roofline']['frac'], d['rmse_final'], d['lm_iterations_per_solve'])"
-bash gpurun_prof.sh
+bash tools/gpurun/gpurun_prof.sh

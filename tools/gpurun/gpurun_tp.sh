@@ -4,4 +4,4 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -m pytest tests/test_ba_gpu.py -q -m gpu -x > gpurun_out/diag_tests.log 2>&1 || { tail -40 gpurun_out/diag_tests.log; exit 1; }
 tail -1 gpurun_out/diag_tests.log
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-match 2> gpurun_out/diagb.err | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['per_launch_ms'], d['roofline']['frac'])"
-bash gpurun_prof.sh
+bash tools/gpurun/gpurun_prof.sh
