@@ -79,19 +79,34 @@ def main():
     with open(os.path.join(HERE, "vlfeat_matches.json"), "w") as f:
         json.dump(expected, f)
 
-    sc = H.Scene(20, 2000, 4, seed=0x5F3D0001)
+    n = write_ba_pins()
+    print("golden fixtures written:", expected["views"], "BA iterations", n)
+
+
+def write_ba_pin(name, model):
+    """Oracle trajectory of the C1 scene (20 cams / 2000 pts / k 4), one thread."""
+    sc = H.Scene(20, 2000, 4, seed=0x5F3D0001, model=model)
     rc, s, tr, (e, i, x) = H.oracle_solve(sc)
-    ba = {"scene": {"n_cam": 20, "n_pt": 2000, "k": 4, "seed": 0x5F3D0001},
+    ba = {"scene": {"n_cam": 20, "n_pt": 2000, "k": 4, "seed": 0x5F3D0001, "camera_model": model},
           "rc": rc, "iterations": s.iterations, "successful_steps": s.successful_steps,
           "unsuccessful_steps": s.unsuccessful_steps, "termination": s.termination,
           "initial_cost": s.initial_cost, "final_cost": s.final_cost,
           "rmse_initial": s.rmse_initial, "rmse_final": s.rmse_final,
           "trace": [[t.iteration, t.step_is_valid, t.step_is_successful, t.cost,
                      t.trust_region_radius] for t in tr]}
-    with open(os.path.join(HERE, "ba_c1_oracle.json"), "w") as f:
+    with open(os.path.join(HERE, name), "w") as f:
         json.dump(ba, f, indent=1)
-    print("golden fixtures written:", expected["views"], "BA iterations", s.iterations)
+    return s.iterations
+
+
+def write_ba_pins():
+    n = write_ba_pin("ba_c1_oracle.json", 0)
+    write_ba_pin("ba_c1_snavely_oracle.json", 1)   # SnavelyReprojectionError.h model
+    return n
 
 
 if __name__ == "__main__":
-    main()
+    if "--ba-only" in sys.argv:   # trajectories only (no VLFeat rebuild)
+        write_ba_pins()
+    else:
+        main()

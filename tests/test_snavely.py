@@ -147,3 +147,17 @@ def test_snavely_gpu_unused_slot(ctx):
 def test_snavely_gpu_c2(ctx):
     sc = H.Scene(200, 50_000, 10, model=SNAV, seed=0x5F3D0002)
     _compare(ctx, sc)
+
+
+def test_snavely_regression_pin_c1():
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ba_c1_snavely_oracle.json")))
+    sc = H.Scene(g["scene"]["n_cam"], g["scene"]["n_pt"], g["scene"]["k"], seed=g["scene"]["seed"], model=SNAV)
+    rc, s, tr, _ = H.oracle_solve(sc, threads=1)
+    assert rc == g["rc"] and s.iterations == g["iterations"]
+    assert s.successful_steps == g["successful_steps"]
+    assert abs(s.final_cost / g["final_cost"] - 1) < 1e-9
+    for t, gt in zip(tr, g["trace"]):
+        assert [t.iteration, t.step_is_valid, t.step_is_successful] == gt[:3]
+        assert abs(t.cost / gt[3] - 1) < 1e-9
