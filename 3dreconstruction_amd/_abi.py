@@ -29,10 +29,12 @@ SFM_CAM_SNAVELY = 1
 
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1
+SFM_MATCH_CASCADE = 2
 
 i32p = C.POINTER(C.c_int32)
 i64p = C.POINTER(C.c_int64)
 u32p = C.POINTER(C.c_uint32)
+f32p = C.POINTER(C.c_float)
 u64p = C.POINTER(C.c_uint64)
 u8p = C.POINTER(C.c_uint8)
 f64p = C.POINTER(C.c_double)

@@ -90,7 +90,7 @@ def comm_unique_id():
 def match_dense(ctx, a, b, mode=abi.SFM_MATCH_RATIO, ratio=0.8):
     a = np.ascontiguousarray(a, np.uint8).reshape(-1, 128)
     b = np.ascontiguousarray(b, np.uint8).reshape(-1, 128)
-    n_out = len(b) if mode == abi.SFM_MATCH_RATIO else len(a)
+    n_out = len(a) if mode == abi.SFM_MATCH_MUTUAL else len(b)
     idx = np.zeros(max(n_out, 1), np.int32)
     d2 = np.zeros(max(n_out, 1), np.int32)
     o = abi.MatchOptions(mode, ratio)

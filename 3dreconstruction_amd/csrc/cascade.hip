@@ -1,0 +1,372 @@
+// Cascade-hashing descriptor matching on CDNA4 (gfx950): the live default
+// matcher of the reference, OpenMVG Cascade_Hashing_Matcher_Regions(0.8)
+// selected by "AUTO" (src/sparseBuilder/sparseBuilder.cpp:811-814,911-914).
+//
+// Algorithm (OpenMVG cascade_hasher.hpp, after Cheng et al. 2014; restated
+// in oracle/cascade_oracle.cpp, which is the bit-exact spec of this file):
+//   * every descriptor x (uint8 -> float, minus the collection's zero-mean
+//     descriptor) gets a 128-bit code sign(P x) and 6 bucket ids of 10 bits,
+//     sign(S_g x) MSB first, from fixed Gaussian projections;
+//   * a query q of image J collects the descriptors of image I sharing one of
+//     its 6 buckets (first occurrence wins), orders them by Hamming distance
+//     of the codes (stable), re-ranks the first 10 by exact L2^2 and keeps
+//     the best if d1 < fl32(ratio^2) * d2; fewer than 3 collected candidates
+//     or fewer than 2 distinct ones give no match.
+// The projections are fp32 dot products with a fixed fma order (k = 0..127),
+// so the hash bits are reproducible on the CPU; distances are exact integers.
+//
+// Kernels:
+//   casc_colsum_kernel  per image column sums (zero-mean input), HBM-bound.
+//   casc_hash_kernel    188 x 128 fp32 FMAs per descriptor, projections in
+//                       LDS (broadcast reads), descriptor in 128 VGPRs.
+//   casc_bucket_kernel  one wave per (image, group): LDS histogram, scan and
+//                       a stable ballot-ranked scatter (lists stay ascending).
+//   casc_match_kernel   one thread per query; candidates of image I are read
+//                       from L2 (blockIdx is XCD-aware so one pair's query
+//                       blocks share an XCD); re-rank with v_dot4_i32_i8.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <random>
+#include <utility>
+
+#include "cascade.h"
+#include "common.h"
+
+namespace sfm {
+
+void casc_projections(std::vector<float>& proj) {
+    // CascadeHasher::Init(gen, 128): d(gen) for primary(i, j), i-major, then
+    // secondary[g](k, j) for g, k, j.
+    std::mt19937 gen(std::mt19937::default_seed);
+    std::normal_distribution<> d(0, 1);
+    proj.assign((size_t)kCascProjRows * kCascCode, 0.f);
+    for (int r = 0; r < kCascProjRows; ++r)
+        for (int j = 0; j < kCascCode; ++j) proj[(size_t)r * kCascCode + j] = (float)d(gen);
+}
+
+void casc_zero_mean(const int64_t* colsum, const int32_t* img_n, const std::vector<int32_t>& used,
+                    float* zm) {
+    // GetZeroMeanDescriptor(per-image matrix) = float column sums / float(n)
+    // (sums of <= 2^16 uint8 values are exact in float); then the mean of the
+    // per-image means (empty images contribute zero rows), accumulated here
+    // in double in ascending image order.
+    for (int c = 0; c < kCascCode; ++c) {
+        double acc = 0.0;
+        for (const int32_t I : used) {
+            const int32_t n = img_n[I];
+            if (n > 0) acc += (double)((float)colsum[(int64_t)I * kCascCode + c] / (float)n);
+        }
+        zm[c] = used.empty() ? 0.f : (float)(acc / (double)used.size());
+    }
+}
+
+namespace {
+
+__global__ __launch_bounds__(128) void casc_colsum_kernel(const int8_t* __restrict__ desc,
+                                                          const int64_t* __restrict__ img_row0,
+                                                          const int32_t* __restrict__ img_n,
+                                                          int64_t* __restrict__ colsum) {
+    const int I = blockIdx.x, c = threadIdx.x;
+    const int8_t* d = desc + img_row0[I] * 128 + c;
+    const int n = img_n[I];
+    int64_t s = 0;
+    for (int r = 0; r < n; ++r) s += (int)d[(int64_t)r * 128] + 128;
+    colsum[(int64_t)I * 128 + c] = s;
+}
+
+constexpr int kHashThreads = 256;
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void casc_hash_kernel(
+    const int8_t* __restrict__ desc, const int64_t* __restrict__ img_row0,
+    const int32_t* __restrict__ img_n, const int32_t* __restrict__ img_list,
+    const float* __restrict__ proj, const float* __restrict__ zm, uint32_t* __restrict__ code,
+    uint16_t* __restrict__ bkt) {
+    extern __shared__ __attribute__((aligned(16))) float4 sP[];  // [188][32]
+    __shared__ float sZ[kCascCode];
+    for (int i = threadIdx.x; i < kCascProjRows * 32; i += kHashThreads)
+        sP[i] = reinterpret_cast<const float4*>(proj)[i];
+    if (threadIdx.x < kCascCode) sZ[threadIdx.x] = zm[threadIdx.x];
+    __syncthreads();
+    const int I = img_list[blockIdx.y];
+    const int r = blockIdx.x * kHashThreads + threadIdx.x;
+    if (r >= img_n[I]) return;
+    const int64_t row = img_row0[I] + r;
+
+    // x lives in 128 VGPRs: every index below is a compile-time constant
+    // (static_for), so the array is promoted before loop unrolling runs.
+    float x[kCascCode];
+    const int4* src = reinterpret_cast<const int4*>(desc + row * 128);
+    static_for<8>([&](auto w) {
+        const int4 v = src[w.value];
+        const int wv[4] = {v.x, v.y, v.z, v.w};
+        static_for<16>([&](auto e) {
+            constexpr int k = 16 * decltype(w)::value + decltype(e)::value;
+            const int u = (int)(int8_t)(wv[e.value >> 2] >> (8 * (e.value & 3))) + 128;  // uint8
+            x[k] = (float)u - sZ[k];
+        });
+    });
+
+    // four projection rows at a time: independent fma chains, k = 0..127 each
+    auto proj4 = [&](int p0, float* acc) {
+        acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
+        static_for<32>([&](auto k4) {
+            constexpr int k = 4 * decltype(k4)::value;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 w = sP[(p0 + q) * 32 + k / 4];
+                acc[q] = __builtin_fmaf(w.x, x[k + 0], acc[q]);
+                acc[q] = __builtin_fmaf(w.y, x[k + 1], acc[q]);
+                acc[q] = __builtin_fmaf(w.z, x[k + 2], acc[q]);
+                acc[q] = __builtin_fmaf(w.w, x[k + 3], acc[q]);
+            }
+        });
+    };
+    uint32_t cw[4];
+#pragma unroll
+    for (int wd = 0; wd < 4; ++wd) {
+        uint32_t bits = 0;
+        for (int p = 0; p < 32; p += 4) {
+            float acc[4];
+            proj4(32 * wd + p, acc);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bits |= (uint32_t)(acc[q] > 0.f) << (p + q);
+        }
+        cw[wd] = bits;
+    }
+    uint64_t sec = 0;  // bit s = sign of secondary row s (g * 10 + k)
+    for (int p = 0; p < kCascGroups * kCascBucketBits; p += 4) {
+        float acc[4];
+        proj4(kCascCode + p, acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sec |= (uint64_t)(acc[q] > 0.f) << (p + q);
+    }
+    uint32_t b[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < kCascGroups; ++g) {
+        uint32_t id = 0;
+#pragma unroll
+        for (int k = 0; k < kCascBucketBits; ++k)
+            id = (id << 1) | (uint32_t)((sec >> (g * kCascBucketBits + k)) & 1);
+        b[g >> 1] |= id << (16 * (g & 1));
+    }
+    reinterpret_cast<uint4*>(code)[row] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    reinterpret_cast<uint4*>(bkt)[row] = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
+// One wave per (image, group): counting sort of the image's descriptors by
+// bucket id; within a bucket the ids stay ascending (the order OpenMVG's
+// push_back over j = 0..n-1 leaves them in).
+__global__ __launch_bounds__(64) void casc_bucket_kernel(const uint16_t* __restrict__ bkt,
+                                                         const int64_t* __restrict__ img_row0,
+                                                         const int32_t* __restrict__ img_n,
+                                                         const int32_t* __restrict__ img_list,
+                                                         int64_t rows, int32_t* __restrict__ boff,
+                                                         int32_t* __restrict__ blist) {
+    const int g = blockIdx.x, I = img_list[blockIdx.y], lane = threadIdx.x;
+    __shared__ int hist[kCascBuckets];
+    for (int b = lane; b < kCascBuckets; b += 64) hist[b] = 0;
+    __syncthreads();
+    const int n = img_n[I];
+    const int64_t row0 = img_row0[I];
+    for (int r = lane; r < n; r += 64) atomicAdd(&hist[bkt[(row0 + r) * 8 + g]], 1);
+    __syncthreads();
+    int loc[16], s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { loc[k] = s; s += hist[16 * lane + k]; }
+    int incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    const int excl = incl - s;
+    int32_t* off = boff + ((int64_t)I * kCascGroups + g) * (kCascBuckets + 1);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        hist[16 * lane + k] = excl + loc[k];
+        off[16 * lane + k] = excl + loc[k];
+    }
+    if (lane == 63) off[kCascBuckets] = incl;
+    __syncthreads();
+    int32_t* dst = blist + (int64_t)g * rows + row0;
+    for (int base = 0; base < n; base += 64) {
+        const int r = base + lane;
+        const bool valid = r < n;
+        const int b = valid ? bkt[(row0 + r) * 8 + g] : 0;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < kCascBucketBits; ++bit) {
+            const bool on = (b >> bit) & 1;
+            const uint64_t bb = __ballot(on);
+            m &= on ? bb : ~bb;
+        }
+        const int rank = __popcll(m & ((1ull << lane) - 1));
+        int pos = 0;
+        if (valid) pos = hist[b] + rank;
+        __syncthreads();  // every lane has read its cursor before the leaders move it
+        if (valid) {
+            dst[pos] = r;
+            if (rank == 0) hist[b] += __popcll(m);
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ bool sorted_contains(const int32_t* __restrict__ l, int lo, int hi,
+                                                int v) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const int x = l[mid];
+        if (x == v) return true;
+        if (x < v) lo = mid + 1; else hi = mid;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(kCascQB) void casc_match_kernel(CascMatchArgs a) {
+    // XCD-aware bijective remap of the flat workgroup id (as match_top2_kernel)
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int pair = work / a.qblocks;
+    const int qblk = work - pair * a.qblocks;
+    if (pair >= a.n_pairs) return;
+    const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
+    const int q = qblk * kCascQB + threadIdx.x;
+    if (q >= a.t.img_n[J]) return;
+    const int64_t qrow = a.t.img_row0[J] + q;
+    const int64_t row0I = a.t.img_row0[I];
+
+    const uint4 qb = reinterpret_cast<const uint4*>(a.t.bkt)[qrow];
+    const uint32_t qbw[4] = {qb.x, qb.y, qb.z, qb.w};
+    const int32_t* offI = a.t.boff + (int64_t)I * kCascGroups * (kCascBuckets + 1);
+    int lo[kCascGroups], hi[kCascGroups], total = 0;
+#pragma unroll
+    for (int g = 0; g < kCascGroups; ++g) {
+        const int b = (qbw[g >> 1] >> (16 * (g & 1))) & 0xffff;
+        lo[g] = offI[g * (kCascBuckets + 1) + b];
+        hi[g] = offI[g * (kCascBuckets + 1) + b + 1];
+        total += hi[g] - lo[g];
+    }
+    int idx = -1, dd = -1;
+    if (total > 2) {   // candidate_descriptors.size() <= NN: skip
+        const uint4 qc = reinterpret_cast<const uint4*>(a.t.code)[qrow];
+        const uint4* codeI = reinterpret_cast<const uint4*>(a.t.code) + row0I;
+        int th[kCascTop], tc[kCascTop];
+#pragma unroll
+        for (int k = 0; k < kCascTop; ++k) { th[k] = INT_MAX; tc[k] = -1; }
+        int uniq = 0;
+#pragma unroll
+        for (int g = 0; g < kCascGroups; ++g) {
+            const int32_t* L = a.t.blist + (int64_t)g * a.t.rows + row0I;
+            for (int e = lo[g]; e < hi[g]; ++e) {
+                const int c = L[e];
+                bool dup = false;
+#pragma unroll
+                for (int g2 = 0; g2 < g; ++g2)
+                    dup = dup || sorted_contains(a.t.blist + (int64_t)g2 * a.t.rows + row0I, lo[g2],
+                                                 hi[g2], c);
+                if (dup) continue;
+                ++uniq;
+                const uint4 cc = codeI[c];
+                int h = __popc(qc.x ^ cc.x) + __popc(qc.y ^ cc.y) + __popc(qc.z ^ cc.z) +
+                        __popc(qc.w ^ cc.w);
+                int hc = c;
+                // stable insertion: equal distances keep their arrival order
+#pragma unroll
+                for (int k = 0; k < kCascTop; ++k) {
+                    const bool lt = h < th[k];
+                    const int oh = th[k], oc = tc[k];
+                    th[k] = lt ? h : oh;
+                    tc[k] = lt ? hc : oc;
+                    h = lt ? oh : h;
+                    hc = lt ? oc : hc;
+                }
+            }
+        }
+        if (uniq >= 2) {
+            const int4* qd = reinterpret_cast<const int4*>(a.t.desc + qrow * 128);
+            int4 qv[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) qv[w] = qd[w];
+            const int nq = a.t.nrm[qrow];
+            int d1 = INT_MAX, c1 = INT_MAX, d2 = INT_MAX, c2 = INT_MAX;
+#pragma unroll
+            for (int k = 0; k < kCascTop; ++k) {
+                if (k < uniq) {
+                    const int c = tc[k];
+                    const int4* cd = reinterpret_cast<const int4*>(a.t.desc + (row0I + c) * 128);
+                    int dot = 0;
+#pragma unroll
+                    for (int w = 0; w < 8; ++w) {
+                        const int4 v = cd[w];
+                        dot = __builtin_amdgcn_sdot4(qv[w].x, v.x, dot, false);
+                        dot = __builtin_amdgcn_sdot4(qv[w].y, v.y, dot, false);
+                        dot = __builtin_amdgcn_sdot4(qv[w].z, v.z, dot, false);
+                        dot = __builtin_amdgcn_sdot4(qv[w].w, v.w, dot, false);
+                    }
+                    const int d = nq + a.t.nrm[row0I + c] - 2 * dot;
+                    // partial_sort of (distance, id) pairs: lexicographic
+                    if (d < d1 || (d == d1 && c < c1)) {
+                        d2 = d1; c2 = c1; d1 = d; c1 = c;
+                    } else if (d < d2 || (d == d2 && c < c2)) {
+                        d2 = d; c2 = c;
+                    }
+                }
+            }
+            if ((float)d1 < a.r2 * (float)d2) { idx = c1; dd = d1; }
+        }
+    }
+    a.out_idx[(int64_t)pair * a.out_stride + q] = idx;
+    a.out_d[(int64_t)pair * a.out_stride + q] = dd;
+}
+
+}  // namespace
+
+void casc_colsum(const CascTables& t, int n_img, int64_t* colsum, hipStream_t s) {
+    if (n_img == 0) return;
+    hipLaunchKernelGGL(casc_colsum_kernel, dim3(n_img), dim3(128), 0, s, t.desc, t.img_row0,
+                       t.img_n, colsum);
+    SFM_HIP(hipGetLastError());
+}
+
+void casc_hash(const CascTables& t, const float* proj, const float* zm, const int32_t* img, int n,
+               int max_n, hipStream_t s) {
+    if (n == 0 || max_n == 0) return;
+    const size_t lds = (size_t)kCascProjRows * kCascCode * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+        SFM_HIP(hipFuncSetAttribute((const void*)casc_hash_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+    }
+    SFM_REQUIRE(n <= 65535, SFM_ERR_UNSUPPORTED, "cascade hashing over %d images", n);
+    hipLaunchKernelGGL(casc_hash_kernel, dim3((max_n + kHashThreads - 1) / kHashThreads, n),
+                       dim3(kHashThreads), lds, s, t.desc, t.img_row0, t.img_n, img, proj, zm,
+                       t.code, t.bkt);
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(casc_bucket_kernel, dim3(kCascGroups, n), dim3(64), 0, s, t.bkt, t.img_row0,
+                       t.img_n, img, t.rows, t.boff, t.blist);
+    SFM_HIP(hipGetLastError());
+}
+
+void casc_match(const CascMatchArgs& a, hipStream_t s) {
+    const int64_t nwg = (int64_t)a.n_pairs * a.qblocks;
+    if (nwg == 0) return;
+    hipLaunchKernelGGL(casc_match_kernel, dim3((unsigned)nwg), dim3(kCascQB), 0, s, a);
+    SFM_HIP(hipGetLastError());
+}
+
+}  // namespace sfm

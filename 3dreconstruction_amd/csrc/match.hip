@@ -29,6 +29,7 @@
 #include <cstring>
 #include <vector>
 
+#include "cascade.h"
 #include "common.h"
 
 namespace sfm {
@@ -277,13 +278,14 @@ __global__ void digest_kernel(const int32_t* __restrict__ idx, const int32_t* __
     const int pair = blockIdx.x;
     if (pair >= n_pairs) return;
     const int I = pairs[2 * pair], J = pairs[2 * pair + 1];
-    const int n_out = mode == SFM_MATCH_RATIO ? img_n[J] : img_n[I];
+    const bool qJ = mode != SFM_MATCH_MUTUAL;   // outputs per query of J
+    const int n_out = qJ ? img_n[J] : img_n[I];
     uint64_t h = 0, cnt = 0;
     for (int q = threadIdx.x; q < n_out; q += blockDim.x) {
         const int m = idx[(int64_t)pair * stride + q];
         if (m < 0) continue;
-        const uint32_t ii = mode == SFM_MATCH_RATIO ? (uint32_t)m : (uint32_t)q;
-        const uint32_t jj = mode == SFM_MATCH_RATIO ? (uint32_t)q : (uint32_t)m;
+        const uint32_t ii = qJ ? (uint32_t)m : (uint32_t)q;
+        const uint32_t jj = qJ ? (uint32_t)q : (uint32_t)m;
         h += mix64(((uint64_t)ii << 32 | jj) ^ ((uint64_t)(uint32_t)d[(int64_t)pair * stride + q] << 21));
         ++cnt;
     }
@@ -312,6 +314,7 @@ struct sfm_match_plan {
     std::vector<int64_t> row0;   // padded row start per image
     std::vector<int32_t> nrows;
     int32_t max_n = 0;
+    int64_t rows = 0;            // padded rows in total
     DBuf<uint8_t> desc;
     DBuf<int32_t> nrm, ntr, img_n;
     DBuf<int64_t> img_row0;
@@ -321,6 +324,15 @@ struct sfm_match_plan {
     std::vector<int32_t> pairs_h;
     DBuf<int32_t> pairs_d, out_idx, out_d, tmp_idx, tmp_d;
     DBuf<unsigned long long> digest;
+    // cascade hashing tables, built by the first CASCADE run and rebuilt when
+    // the set of images in the pair list (the zero-mean input) changes
+    std::vector<int32_t> casc_used;
+    bool casc_ready = false;
+    DBuf<float> casc_proj, casc_zm;
+    DBuf<int64_t> casc_colsum;
+    DBuf<uint32_t> casc_code;
+    DBuf<uint16_t> casc_bkt;
+    DBuf<int32_t> casc_boff, casc_blist, casc_img;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
     int64_t launches = 0;
@@ -344,6 +356,7 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
         rows += (n + kRowPad - 1) / kRowPad * kRowPad;
     }
     rows += kRowPad;  // guard rows for tile over-reads
+    p->rows = rows;
     std::vector<uint8_t> staging((size_t)rows * 128, 128);  // pad rows -> a' = 0
     std::vector<int64_t> rstart(rows, 0);
     std::vector<int32_t> rvalid(rows, 0);
@@ -373,6 +386,20 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
     p->img_row0.alloc(n_img);
     p->img_row0.upload(p->row0.data(), n_img, s);
     SFM_HIP(hipStreamSynchronize(s));  // staging buffers die here
+}
+
+CascTables casc_tables(sfm_match_plan* p) {
+    CascTables t;
+    t.desc = reinterpret_cast<const int8_t*>(p->desc.p);
+    t.nrm = p->nrm.p;
+    t.img_row0 = p->img_row0.p;
+    t.img_n = p->img_n.p;
+    t.rows = p->rows;
+    t.code = p->casc_code.p;
+    t.bkt = p->casc_bkt.p;
+    t.boff = p->casc_boff.p;
+    t.blist = p->casc_blist.p;
+    return t;
 }
 
 // Run the top-2 kernel over pairs [0, n_pairs) in launch batches.
@@ -406,14 +433,76 @@ void run_top2(sfm_match_plan* p, const int32_t* pairs_d, int64_t n_pairs, int sw
     }
 }
 
+// Hash tables for the images of this pair list (zero-mean over exactly those
+// images, as Cascade_Hashing_Matcher_Regions' used_index).
+void casc_prepare(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs) {
+    hipStream_t s = p->ctx->stream;
+    std::vector<char> seen(p->n_img, 0);
+    for (int64_t q = 0; q < 2 * n_pairs; ++q) seen[pairs[q]] = 1;
+    std::vector<int32_t> used;
+    for (int i = 0; i < p->n_img; ++i)
+        if (seen[i]) used.push_back(i);
+    if (p->casc_ready && used == p->casc_used) return;
+    CascTables t = casc_tables(p);
+    if (!p->casc_proj.p) {
+        std::vector<float> proj;
+        casc_projections(proj);
+        p->casc_proj.alloc(proj.size());
+        p->casc_proj.upload(proj.data(), proj.size(), s);
+        p->casc_zm.alloc(kCascCode);
+        p->casc_colsum.alloc((size_t)std::max(1, p->n_img) * kCascCode);
+        p->casc_code.alloc((size_t)p->rows * 4);
+        p->casc_bkt.alloc((size_t)p->rows * 8);
+        p->casc_boff.alloc((size_t)std::max(1, p->n_img) * kCascGroups * (kCascBuckets + 1));
+        p->casc_blist.alloc((size_t)p->rows * kCascGroups);
+        p->casc_img.alloc(std::max(1, p->n_img));
+        t = casc_tables(p);
+        casc_colsum(t, p->n_img, p->casc_colsum.p, s);
+    }
+    std::vector<int64_t> colsum((size_t)p->n_img * kCascCode);
+    if (p->n_img)
+        SFM_HIP(hipMemcpyAsync(colsum.data(), p->casc_colsum.p, colsum.size() * 8,
+                               hipMemcpyDeviceToHost, s));
+    SFM_HIP(hipStreamSynchronize(s));
+    float zm[kCascCode];
+    casc_zero_mean(colsum.data(), p->nrows.data(), used, zm);
+    p->casc_zm.upload(zm, kCascCode, s);
+    if (!used.empty()) p->casc_img.upload(used.data(), used.size(), s);
+    casc_hash(t, p->casc_proj.p, p->casc_zm.p, p->casc_img.p, (int)used.size(), p->max_n, s);
+    SFM_HIP(hipStreamSynchronize(s));   // host zm / image list die here
+    p->casc_used = std::move(used);
+    p->casc_ready = true;
+}
+
+void run_cascade(sfm_match_plan* p, int64_t n_pairs, float r2) {
+    const int qblocks = std::max(1, (p->max_n + kCascQB - 1) / kCascQB);
+    const int64_t batch = std::max<int64_t>(1, (int64_t)(1 << 22) / qblocks);
+    for (int64_t b0 = 0; b0 < n_pairs; b0 += batch) {
+        const int64_t nb = std::min(batch, n_pairs - b0);
+        CascMatchArgs a;
+        a.t = casc_tables(p);
+        a.pairs = p->pairs_d.p + 2 * b0;
+        a.n_pairs = (int32_t)nb;
+        a.qblocks = qblocks;
+        a.r2 = r2;
+        a.out_stride = p->stride;
+        a.out_idx = p->out_idx.p + b0 * p->stride;
+        a.out_d = p->out_d.p + b0 * p->stride;
+        casc_match(a, p->ctx->stream);
+        ++p->launches;
+    }
+}
+
 void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const sfm_match_options* o) {
     hipStream_t s = p->ctx->stream;
-    SFM_REQUIRE(o && (o->mode == SFM_MATCH_RATIO || o->mode == SFM_MATCH_MUTUAL),
+    SFM_REQUIRE(o && (o->mode == SFM_MATCH_RATIO || o->mode == SFM_MATCH_MUTUAL ||
+                      o->mode == SFM_MATCH_CASCADE),
                 SFM_ERR_INVALID_ARG, "bad match options");
     for (int64_t q = 0; q < n_pairs; ++q)
         SFM_REQUIRE(pairs[2 * q] >= 0 && pairs[2 * q] < p->n_img && pairs[2 * q + 1] >= 0 &&
                         pairs[2 * q + 1] < p->n_img,
                     SFM_ERR_INVALID_ARG, "pair %lld out of range", (long long)q);
+    if (o->mode == SFM_MATCH_CASCADE) casc_prepare(p, pairs, n_pairs);
     p->mode = o->mode;
     p->n_pairs = n_pairs;
     p->stride = std::max<int64_t>(1, p->max_n);
@@ -426,7 +515,9 @@ void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const s
     if (!p->ev0) { SFM_HIP(hipEventCreate(&p->ev0)); SFM_HIP(hipEventCreate(&p->ev1)); }
     SFM_HIP(hipEventRecord(p->ev0, s));
     if (n_pairs > 0) {
-        if (o->mode == SFM_MATCH_RATIO) {
+        if (o->mode == SFM_MATCH_CASCADE) {
+            run_cascade(p, n_pairs, o->ratio * o->ratio);
+        } else if (o->mode == SFM_MATCH_RATIO) {
             run_top2(p, p->pairs_d.p, n_pairs, 0, 1, o->ratio * o->ratio, p->out_idx.p, p->out_d.p,
                      p->stride);
         } else {
@@ -537,13 +628,14 @@ extern "C" int sfm_match_plan_fetch(sfm_match_plan* p, int64_t* counts, uint32_t
         std::vector<std::pair<uint64_t, int32_t>> v;
         for (int64_t q = 0; q < p->n_pairs; ++q) {
             const int I = p->pairs_h[2 * q], J = p->pairs_h[2 * q + 1];
-            const int n_out = p->mode == SFM_MATCH_RATIO ? p->nrows[J] : p->nrows[I];
+            const bool qJ = p->mode != SFM_MATCH_MUTUAL;
+            const int n_out = qJ ? p->nrows[J] : p->nrows[I];
             v.clear();
             for (int t = 0; t < n_out; ++t) {
                 const int m = hi[(size_t)q * p->stride + t];
                 if (m < 0) continue;
-                const uint32_t ii = p->mode == SFM_MATCH_RATIO ? (uint32_t)m : (uint32_t)t;
-                const uint32_t jj = p->mode == SFM_MATCH_RATIO ? (uint32_t)t : (uint32_t)m;
+                const uint32_t ii = qJ ? (uint32_t)m : (uint32_t)t;
+                const uint32_t jj = qJ ? (uint32_t)t : (uint32_t)m;
                 v.emplace_back(((uint64_t)ii << 32) | jj, hd[(size_t)q * p->stride + t]);
             }
             std::sort(v.begin(), v.end());  // IndMatch::getDeduplicated order
@@ -603,7 +695,7 @@ extern "C" int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a, cons
         upload_collection(&plan, desc.data(), off, 2);
         const int32_t pair[2] = {0, 1};
         run_pairs(&plan, pair, 1, o);
-        const int32_t n_out = o->mode == SFM_MATCH_RATIO ? n_b : n_a;
+        const int32_t n_out = o->mode != SFM_MATCH_MUTUAL ? n_b : n_a;
         if (n_out) {
             SFM_HIP(hipMemcpyAsync(match_idx, plan.out_idx.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
             SFM_HIP(hipMemcpyAsync(match_d2, plan.out_d.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -245,6 +245,14 @@ int sfm_synth_ba(const sfm_synth_ba_config* cfg,
                                  if d1 < fl32(ratio*ratio)*d2; emit (i, j)   */
 #define SFM_MATCH_MUTUAL  1   /* BFMatcher(NORM_L2, crossCheck) knnMatch k=1:
                                  keep (i, j) iff j = NN_J(i) and i = NN_I(j) */
+#define SFM_MATCH_CASCADE 2   /* Cascade_Hashing_Matcher_Regions(0.8), the
+                                 "AUTO" default (sparseBuilder.cpp:811-814,
+                                 911-914): per query j of J, candidates of I
+                                 sharing one of 6 hash buckets, top-10 by
+                                 Hamming distance re-ranked by exact L2^2,
+                                 ratio test as RATIO; emit (i, j).  The
+                                 zero-mean descriptor is taken over the
+                                 images of the run's pair list.             */
 
 typedef struct sfm_match_options {
     int32_t mode;            /* SFM_MATCH_*                                    */

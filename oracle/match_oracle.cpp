@@ -79,6 +79,15 @@ extern "C" int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, 
         }
         return SFM_OK;
     }
+    if (mode == SFM_MATCH_CASCADE) {   // a 2-image collection, pair (0, 1)
+        std::vector<uint8_t> d((size_t)(n_a + n_b) * 128);
+        if (n_a) std::memcpy(d.data(), a, (size_t)n_a * 128);
+        if (n_b) std::memcpy(d.data() + (size_t)n_a * 128, b, (size_t)n_b * 128);
+        const int64_t off[3] = {0, n_a, (int64_t)n_a + n_b};
+        const int32_t pair[2] = {0, 1};
+        return orc_cascade_pairs(d.data(), off, 2, pair, 1, ratio, 1, std::max(1, n_b), match_idx,
+                                 match_d2);
+    }
     return SFM_ERR_INVALID_ARG;
 }
 
@@ -89,25 +98,42 @@ extern "C" int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int3
     if (n_pairs < 0 || !counts) return SFM_ERR_INVALID_ARG;
     std::vector<std::vector<std::pair<uint64_t, int32_t>>> res(n_pairs);
     int err = SFM_OK;
-#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : 1)
-    for (int64_t p = 0; p < n_pairs; ++p) {
-        const int32_t I = pairs[2 * p], J = pairs[2 * p + 1];
-        if (I < 0 || J < 0 || I >= n_img || J >= n_img) { err = SFM_ERR_INVALID_ARG; continue; }
-        const int32_t nI = (int32_t)(offsets[I + 1] - offsets[I]);
-        const int32_t nJ = (int32_t)(offsets[J + 1] - offsets[J]);
-        const uint8_t* dI = desc + offsets[I] * 128;
-        const uint8_t* dJ = desc + offsets[J] * 128;
-        const int32_t n_out = mode == SFM_MATCH_RATIO ? nJ : nI;
-        std::vector<int32_t> idx(n_out), dd(n_out);
-        orc_match_dense(dI, nI, dJ, nJ, mode, ratio, idx.data(), dd.data());
-        auto& v = res[p];
-        for (int32_t t = 0; t < n_out; ++t) {
-            if (idx[t] < 0) continue;
-            const uint32_t ii = mode == SFM_MATCH_RATIO ? (uint32_t)idx[t] : (uint32_t)t;
-            const uint32_t jj = mode == SFM_MATCH_RATIO ? (uint32_t)t : (uint32_t)idx[t];
-            v.emplace_back(((uint64_t)ii << 32) | jj, dd[t]);
+    if (mode == SFM_MATCH_CASCADE) {   // hashing needs the whole pair list at once
+        int64_t stride = 1;
+        for (int32_t k = 0; k < n_img; ++k) stride = std::max(stride, offsets[k + 1] - offsets[k]);
+        std::vector<int32_t> idx((size_t)(n_pairs * stride)), dd((size_t)(n_pairs * stride));
+        const int e = orc_cascade_pairs(desc, offsets, n_img, pairs, n_pairs, ratio, n_threads,
+                                        stride, idx.data(), dd.data());
+        if (e) return e;
+        for (int64_t p = 0; p < n_pairs; ++p) {
+            const int32_t J = pairs[2 * p + 1];
+            for (int64_t t = 0; t < offsets[J + 1] - offsets[J]; ++t)
+                if (idx[p * stride + t] >= 0)
+                    res[p].emplace_back(((uint64_t)(uint32_t)idx[p * stride + t] << 32) | (uint32_t)t,
+                                        dd[p * stride + t]);
+            std::sort(res[p].begin(), res[p].end());
         }
-        std::sort(v.begin(), v.end());
+    } else {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads > 0 ? n_threads : 1)
+        for (int64_t p = 0; p < n_pairs; ++p) {
+            const int32_t I = pairs[2 * p], J = pairs[2 * p + 1];
+            if (I < 0 || J < 0 || I >= n_img || J >= n_img) { err = SFM_ERR_INVALID_ARG; continue; }
+            const int32_t nI = (int32_t)(offsets[I + 1] - offsets[I]);
+            const int32_t nJ = (int32_t)(offsets[J + 1] - offsets[J]);
+            const uint8_t* dI = desc + offsets[I] * 128;
+            const uint8_t* dJ = desc + offsets[J] * 128;
+            const int32_t n_out = mode == SFM_MATCH_RATIO ? nJ : nI;
+            std::vector<int32_t> idx(n_out), dd(n_out);
+            orc_match_dense(dI, nI, dJ, nJ, mode, ratio, idx.data(), dd.data());
+            auto& v = res[p];
+            for (int32_t t = 0; t < n_out; ++t) {
+                if (idx[t] < 0) continue;
+                const uint32_t ii = mode == SFM_MATCH_RATIO ? (uint32_t)idx[t] : (uint32_t)t;
+                const uint32_t jj = mode == SFM_MATCH_RATIO ? (uint32_t)t : (uint32_t)idx[t];
+                v.emplace_back(((uint64_t)ii << 32) | jj, dd[t]);
+            }
+            std::sort(v.begin(), v.end());
+        }
     }
     if (err) return err;
     int64_t off = 0;

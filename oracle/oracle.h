@@ -17,6 +17,8 @@
  *     SURVEY.md §8(f) row 4) as an alternative residual;
  *   - OpenMVG Matcher_Regions(BRUTE_FORCE_L2) ratio matching as selected by
  *     src/sparseBuilder/sparseBuilder.cpp:919-921 with fDistRatio 0.8 (:812);
+ *   - OpenMVG Cascade_Hashing_Matcher_Regions(0.8), the "AUTO" default of
+ *     src/sparseBuilder/sparseBuilder.cpp:811-814,911-914 (cascade_oracle.cpp);
  *   - OpenCV BFMatcher(NORM_L2, crossCheck) knnMatch(k=1) as used by
  *     src/frame/LocalFrame.h:31-47 and src/frame/GlobalFrame.h:22-43.
  * The only reference-produced artefacts available are VLFeat descriptors
@@ -70,6 +72,14 @@ int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b
 int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,
                     const int32_t* pairs, int64_t n_pairs, int32_t mode, float ratio,
                     int32_t n_threads, int64_t* counts, uint32_t* i, uint32_t* j, int32_t* d2);
+
+/* Cascade hashing (SFM_MATCH_CASCADE, cascade_oracle.cpp): per query of J,
+ * idx/dist[p * stride + q] = matched row of I or -1 / its L2^2 or -1. */
+int orc_cascade_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,
+                      const int32_t* pairs, int64_t n_pairs, float ratio, int32_t n_threads,
+                      int64_t stride, int32_t* idx, int32_t* dist);
+/* CascadeHasher::Init projections, float [188][128]. */
+int orc_cascade_projections(float* out);
 
 #ifdef __cplusplus
 }

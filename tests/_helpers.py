@@ -36,6 +36,8 @@ def oracle():
         lib.orc_match_dense.restype = C.c_int
         lib.orc_match_dense.argtypes = [abi.u8p, C.c_int32, abi.u8p, C.c_int32, C.c_int32,
                                         C.c_float, abi.i32p, abi.i32p]
+        lib.orc_cascade_projections.restype = C.c_int
+        lib.orc_cascade_projections.argtypes = [abi.f32p]
         lib.orc_match_pairs.restype = C.c_int
         lib.orc_match_pairs.argtypes = [abi.u8p, abi.i64p, C.c_int32, abi.i32p, C.c_int64,
                                         C.c_int32, C.c_float, C.c_int32, abi.i64p, abi.u32p,
@@ -133,13 +135,33 @@ def oracle_match_dense(a, b, mode, ratio=0.8):
     lib = oracle()
     a = np.ascontiguousarray(a, np.uint8)
     b = np.ascontiguousarray(b, np.uint8)
-    n_out = len(b) if mode == abi.SFM_MATCH_RATIO else len(a)
+    n_out = len(a) if mode == abi.SFM_MATCH_MUTUAL else len(b)
     idx = np.zeros(n_out, np.int32)
     d2 = np.zeros(n_out, np.int32)
     rc = lib.orc_match_dense(abi.ptr(a, abi.u8p), len(a), abi.ptr(b, abi.u8p), len(b), mode,
                              ratio, abi.ptr(idx, abi.i32p), abi.ptr(d2, abi.i32p))
     assert rc == 0
     return idx, d2
+
+
+def oracle_match_pairs(desc, offsets, pairs, mode, ratio=0.8, threads=8):
+    """Compacted all-pairs oracle matches: (counts, i, j, d2)."""
+    lib = oracle()
+    desc = np.ascontiguousarray(desc, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+    n = len(pairs)
+    counts = np.zeros(max(n, 1), np.int64)
+    args = (abi.ptr(desc, abi.u8p), abi.ptr(offsets, abi.i64p), len(offsets) - 1,
+            abi.ptr(pairs, abi.i32p), n, mode, ratio, threads)
+    assert lib.orc_match_pairs(*args, abi.ptr(counts, abi.i64p), None, None, None) == 0
+    tot = int(counts[:n].sum())
+    i = np.zeros(max(tot, 1), np.uint32)
+    j = np.zeros(max(tot, 1), np.uint32)
+    d = np.zeros(max(tot, 1), np.int32)
+    assert lib.orc_match_pairs(*args, abi.ptr(counts, abi.i64p), abi.ptr(i, abi.u32p),
+                               abi.ptr(j, abi.u32p), abi.ptr(d, abi.i32p)) == 0
+    return counts[:n], i[:tot], j[:tot], d[:tot]
 
 
 def oracle_cost(scene, e, i, x):
