@@ -170,6 +170,7 @@ SIGNATURES = [
     ("sfm_match_plan_run", C.c_int, [C.c_void_p, i32p, C.c_int64, C.POINTER(MatchOptions),
                                      i64p]),
     ("sfm_match_plan_fetch", C.c_int, [C.c_void_p, i64p, u32p, u32p, i32p]),
+    ("sfm_match_plan_cascade_index", C.c_int, [C.c_void_p, i32p, C.c_int64]),
     ("sfm_match_plan_digest", C.c_int, [C.c_void_p, u64p]),
     ("sfm_match_plan_get_last_ms", C.c_int, [C.c_void_p, f64p, i64p]),
     ("sfm_match_plan_destroy", C.c_int, [C.c_void_p]),

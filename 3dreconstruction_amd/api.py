@@ -140,6 +140,13 @@ class MatchPlan:
                                                  abi.ptr(d, abi.i32p)), "sfm_match_plan_fetch")
         return counts, i[:tot], j[:tot], d[:tot]
 
+    def cascade_index(self, pairs):
+        """Hash tables for the images of `pairs` (SFM_MATCH_CASCADE); later
+        cascade runs over any part of that list reuse them."""
+        pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        _check(self.ctx.lib.sfm_match_plan_cascade_index(self.h, abi.ptr(pairs, abi.i32p),
+                                                         len(pairs)), "sfm_match_plan_cascade_index")
+
     def digest(self):
         v = C.c_uint64()
         _check(self.ctx.lib.sfm_match_plan_digest(self.h, C.byref(v)), "sfm_match_plan_digest")
@@ -379,8 +386,10 @@ def sparse_match_pair(matches_dir):
     _check(abi.load().sfm_sparse_match_pair(_b(matches_dir)), "sfm_sparse_match_pair")
 
 
-def sparse_match(ctx, matches_dir, mode=abi.SFM_MATCH_RATIO, ratio=0.8, force=False, dedup_xy=True):
-    """sparseBuilder::match(), file-staged, on the GPU matcher."""
+def sparse_match(ctx, matches_dir, mode=abi.SFM_MATCH_CASCADE, ratio=0.8, force=False, dedup_xy=True):
+    """sparseBuilder::match(), file-staged, on the GPU matcher.  The default
+    mode is the reference's "AUTO" (cascade hashing, sparseBuilder.cpp:814,
+    911-914); SFM_MATCH_RATIO is its "BRUTEFORCEL2" (:919-921)."""
     o = abi.SparseMatchOpts()
     o.mode, o.ratio, o.force, o.dedup_xy = mode, ratio, int(force), int(dedup_xy)
     st = abi.SparseMatchStats()

@@ -37,7 +37,7 @@ struct CascTables {
     const int32_t* img_n;     // rows per image
     int64_t rows;             // padded rows in total
     uint32_t* code;           // [rows][4]   128-bit hash code
-    uint16_t* bkt;            // [rows][8]   6 bucket ids (+2 unused)
+    uint64_t* bkt;            // [rows]      6 bucket ids, group g in bits [10g, 10g+10)
     int32_t* boff;            // [n_img][6][1025] bucket start per image and group
     int32_t* blist;           // [6][rows]   descriptor ids per bucket, ascending
 };
@@ -58,7 +58,10 @@ struct CascMatchArgs {
     int32_t* out_idx;         // per query of J: matched row of I or -1
     int32_t* out_d;           // its squared L2 distance or -1
 };
-constexpr int kCascQB = 256;  // queries per workgroup
-void casc_match(const CascMatchArgs& a, hipStream_t s);
+constexpr int kCascQB = 256;          // queries per workgroup (tables in global memory)
+constexpr int kCascLdsThreads = 1024; // one workgroup per pair (tables in LDS)
+constexpr int kCascLdsMaxN = 4200;    // largest image whose tables fit 160 KB of LDS
+// max_n: most rows of any image; picks the LDS-staged kernel when it fits
+void casc_match(const CascMatchArgs& a, int max_n, hipStream_t s);
 
 }  // namespace sfm

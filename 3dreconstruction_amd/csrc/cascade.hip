@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(1,
     const int8_t* __restrict__ desc, const int64_t* __restrict__ img_row0,
     const int32_t* __restrict__ img_n, const int32_t* __restrict__ img_list,
     const float* __restrict__ proj, const float* __restrict__ zm, uint32_t* __restrict__ code,
-    uint16_t* __restrict__ bkt) {
+    uint64_t* __restrict__ bkt) {
     extern __shared__ __attribute__((aligned(16))) float4 sP[];  // [188][32]
     __shared__ float sZ[kCascCode];
     for (int i = threadIdx.x; i < kCascProjRows * 32; i += kHashThreads)
@@ -150,23 +150,27 @@ __global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
         for (int q = 0; q < 4; ++q) sec |= (uint64_t)(acc[q] > 0.f) << (p + q);
     }
-    uint32_t b[4] = {0, 0, 0, 0};
+    uint64_t b = 0;   // bucket id of group g in bits [10g, 10g + 10)
 #pragma unroll
     for (int g = 0; g < kCascGroups; ++g) {
         uint32_t id = 0;
 #pragma unroll
         for (int k = 0; k < kCascBucketBits; ++k)
             id = (id << 1) | (uint32_t)((sec >> (g * kCascBucketBits + k)) & 1);
-        b[g >> 1] |= id << (16 * (g & 1));
+        b |= (uint64_t)id << (kCascBucketBits * g);
     }
     reinterpret_cast<uint4*>(code)[row] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-    reinterpret_cast<uint4*>(bkt)[row] = make_uint4(b[0], b[1], b[2], b[3]);
+    bkt[row] = b;
 }
 
 // One wave per (image, group): counting sort of the image's descriptors by
 // bucket id; within a bucket the ids stay ascending (the order OpenMVG's
 // push_back over j = 0..n-1 leaves them in).
-__global__ __launch_bounds__(64) void casc_bucket_kernel(const uint16_t* __restrict__ bkt,
+__device__ __forceinline__ int bucket_of(uint64_t b, int g) {
+    return (int)(b >> (kCascBucketBits * g)) & (kCascBuckets - 1);
+}
+
+__global__ __launch_bounds__(64) void casc_bucket_kernel(const uint64_t* __restrict__ bkt,
                                                          const int64_t* __restrict__ img_row0,
                                                          const int32_t* __restrict__ img_n,
                                                          const int32_t* __restrict__ img_list,
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(64) void casc_bucket_kernel(const uint16_t* __restr
     __syncthreads();
     const int n = img_n[I];
     const int64_t row0 = img_row0[I];
-    for (int r = lane; r < n; r += 64) atomicAdd(&hist[bkt[(row0 + r) * 8 + g]], 1);
+    for (int r = lane; r < n; r += 64) atomicAdd(&hist[bucket_of(bkt[row0 + r], g)], 1);
     __syncthreads();
     int loc[16], s = 0;
 #pragma unroll
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(64) void casc_bucket_kernel(const uint16_t* __restr
     for (int base = 0; base < n; base += 64) {
         const int r = base + lane;
         const bool valid = r < n;
-        const int b = valid ? bkt[(row0 + r) * 8 + g] : 0;
+        const int b = valid ? bucket_of(bkt[row0 + r], g) : 0;
         uint64_t m = __ballot(valid);
 #pragma unroll
         for (int bit = 0; bit < kCascBucketBits; ++bit) {
@@ -223,76 +227,80 @@ __global__ __launch_bounds__(64) void casc_bucket_kernel(const uint16_t* __restr
     }
 }
 
-__device__ __forceinline__ bool sorted_contains(const int32_t* __restrict__ l, int lo, int hi,
-                                                int v) {
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const int x = l[mid];
-        if (x == v) return true;
-        if (x < v) lo = mid + 1; else hi = mid;
-    }
-    return false;
-}
+// Bucket tables of the database image, read from global memory (L2) ...
+struct GlobalTabs {
+    const int32_t* list;   // blist + row0I; group g at g * rows
+    int64_t rows;
+    const int32_t* off;    // [6][1025] of image I
+    const uint4* code;     // codes of image I
+    const uint64_t* bk;    // bucket ids of image I
+    __device__ __forceinline__ int at(int g, int e) const { return list[(int64_t)g * rows + e]; }
+    __device__ __forceinline__ int bucket(int g, int b) const { return off[g * (kCascBuckets + 1) + b]; }
+    __device__ __forceinline__ uint4 cd(int c) const { return code[c]; }
+    __device__ __forceinline__ uint64_t bid(int c) const { return bk[c]; }
+};
+// ... or staged in LDS once per workgroup (u16 ids: images of < 65536 rows)
+struct LdsTabs {
+    const uint16_t* list;  // [6][n]
+    int n;
+    const uint16_t* off;   // [6][1025]
+    const uint4* code;     // [n]
+    const uint64_t* bk;    // [n]
+    __device__ __forceinline__ int at(int g, int e) const { return list[g * n + e]; }
+    __device__ __forceinline__ int bucket(int g, int b) const { return off[g * (kCascBuckets + 1) + b]; }
+    __device__ __forceinline__ uint4 cd(int c) const { return code[c]; }
+    __device__ __forceinline__ uint64_t bid(int c) const { return bk[c]; }
+};
 
-__global__ __launch_bounds__(kCascQB) void casc_match_kernel(CascMatchArgs a) {
-    // XCD-aware bijective remap of the flat workgroup id (as match_top2_kernel)
-    const int nwg = gridDim.x;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int work = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int pair = work / a.qblocks;
-    const int qblk = work - pair * a.qblocks;
-    if (pair >= a.n_pairs) return;
-    const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
-    const int q = qblk * kCascQB + threadIdx.x;
-    if (q >= a.t.img_n[J]) return;
-    const int64_t qrow = a.t.img_row0[J] + q;
-    const int64_t row0I = a.t.img_row0[I];
-
-    const uint4 qb = reinterpret_cast<const uint4*>(a.t.bkt)[qrow];
-    const uint32_t qbw[4] = {qb.x, qb.y, qb.z, qb.w};
-    const int32_t* offI = a.t.boff + (int64_t)I * kCascGroups * (kCascBuckets + 1);
+// One query q (row qrow of image J) against database image I (first row
+// row0I): Match_HashedDescriptions + NNdistanceRatio for that query.
+//   * candidate c of group g was collected before iff it shares the query's
+//     bucket in an earlier group g2 (bucket lists hold every descriptor once
+//     per group), so first occurrences are found by comparing bucket ids;
+//   * the stable Hamming ranking is a sort on the packed key
+//     (h << 24) | (g << 21) | e, e = position in group g's list: arrival
+//     order is (g, e) order; the ten smallest keys are kept by a min/max
+//     network (2 VALU per slot) and mapped back to ids at the end.
+template <class T>
+__device__ __forceinline__ void casc_query(const T& tb, const CascMatchArgs& a, int64_t qrow,
+                                           int64_t row0I, int64_t o) {
+    const uint64_t qb = a.t.bkt[qrow];
     int lo[kCascGroups], hi[kCascGroups], total = 0;
 #pragma unroll
     for (int g = 0; g < kCascGroups; ++g) {
-        const int b = (qbw[g >> 1] >> (16 * (g & 1))) & 0xffff;
-        lo[g] = offI[g * (kCascBuckets + 1) + b];
-        hi[g] = offI[g * (kCascBuckets + 1) + b + 1];
+        const int b = bucket_of(qb, g);
+        lo[g] = tb.bucket(g, b);
+        hi[g] = tb.bucket(g, b + 1);
         total += hi[g] - lo[g];
     }
     int idx = -1, dd = -1;
     if (total > 2) {   // candidate_descriptors.size() <= NN: skip
         const uint4 qc = reinterpret_cast<const uint4*>(a.t.code)[qrow];
-        const uint4* codeI = reinterpret_cast<const uint4*>(a.t.code) + row0I;
-        int th[kCascTop], tc[kCascTop];
+        uint32_t key[kCascTop];
 #pragma unroll
-        for (int k = 0; k < kCascTop; ++k) { th[k] = INT_MAX; tc[k] = -1; }
+        for (int k = 0; k < kCascTop; ++k) key[k] = 0xffffffffu;
         int uniq = 0;
 #pragma unroll
         for (int g = 0; g < kCascGroups; ++g) {
-            const int32_t* L = a.t.blist + (int64_t)g * a.t.rows + row0I;
             for (int e = lo[g]; e < hi[g]; ++e) {
-                const int c = L[e];
+                const int c = tb.at(g, e);
                 bool dup = false;
+                if (g > 0) {
+                    const uint64_t x = tb.bid(c) ^ qb;
 #pragma unroll
-                for (int g2 = 0; g2 < g; ++g2)
-                    dup = dup || sorted_contains(a.t.blist + (int64_t)g2 * a.t.rows + row0I, lo[g2],
-                                                 hi[g2], c);
+                    for (int g2 = 0; g2 < g; ++g2) dup = dup || bucket_of(x, g2) == 0;
+                }
                 if (dup) continue;
                 ++uniq;
-                const uint4 cc = codeI[c];
-                int h = __popc(qc.x ^ cc.x) + __popc(qc.y ^ cc.y) + __popc(qc.z ^ cc.z) +
-                        __popc(qc.w ^ cc.w);
-                int hc = c;
-                // stable insertion: equal distances keep their arrival order
+                const uint4 cc = tb.cd(c);
+                const uint32_t h = __popc(qc.x ^ cc.x) + __popc(qc.y ^ cc.y) + __popc(qc.z ^ cc.z) +
+                                   __popc(qc.w ^ cc.w);
+                uint32_t kk = (h << 24) | ((uint32_t)g << 21) | (uint32_t)e;
 #pragma unroll
                 for (int k = 0; k < kCascTop; ++k) {
-                    const bool lt = h < th[k];
-                    const int oh = th[k], oc = tc[k];
-                    th[k] = lt ? h : oh;
-                    tc[k] = lt ? hc : oc;
-                    h = lt ? oh : h;
-                    hc = lt ? oc : hc;
+                    const uint32_t t = key[k];
+                    key[k] = min(t, kk);
+                    kk = max(t, kk);
                 }
             }
         }
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(kCascQB) void casc_match_kernel(CascMatchArgs a) {
 #pragma unroll
             for (int k = 0; k < kCascTop; ++k) {
                 if (k < uniq) {
-                    const int c = tc[k];
+                    const int c = tb.at((int)(key[k] >> 21) & 7, (int)(key[k] & 0x1fffff));
                     const int4* cd = reinterpret_cast<const int4*>(a.t.desc + (row0I + c) * 128);
                     int dot = 0;
 #pragma unroll
@@ -329,8 +337,63 @@ __global__ __launch_bounds__(kCascQB) void casc_match_kernel(CascMatchArgs a) {
             if ((float)d1 < a.r2 * (float)d2) { idx = c1; dd = d1; }
         }
     }
-    a.out_idx[(int64_t)pair * a.out_stride + q] = idx;
-    a.out_d[(int64_t)pair * a.out_stride + q] = dd;
+    a.out_idx[o] = idx;
+    a.out_d[o] = dd;
+}
+
+__device__ __forceinline__ int xcd_work(int bid, int nwg) {
+    // XCD-aware bijective remap of the flat workgroup id (as match_top2_kernel):
+    // each XCD gets a contiguous range of work items, so the pairs of one
+    // database image share that XCD's L2
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// Tables of I from global memory: one thread per query, kCascQB per workgroup.
+__global__ __launch_bounds__(kCascQB) void casc_match_kernel(CascMatchArgs a) {
+    const int work = xcd_work(blockIdx.x, gridDim.x);
+    const int pair = work / a.qblocks;
+    const int qblk = work - pair * a.qblocks;
+    if (pair >= a.n_pairs) return;
+    const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
+    const int q = qblk * kCascQB + threadIdx.x;
+    if (q >= a.t.img_n[J]) return;
+    const int64_t row0I = a.t.img_row0[I];
+    GlobalTabs tb{a.t.blist + row0I, a.t.rows,
+                  a.t.boff + (int64_t)I * kCascGroups * (kCascBuckets + 1),
+                  reinterpret_cast<const uint4*>(a.t.code) + row0I, a.t.bkt + row0I};
+    casc_query(tb, a, a.t.img_row0[J] + q, row0I, (int64_t)pair * a.out_stride + q);
+}
+
+// Tables of I staged in LDS: one workgroup per pair, every query of J.
+__global__ __launch_bounds__(kCascLdsThreads) void casc_match_lds_kernel(CascMatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    const int pair = xcd_work(blockIdx.x, gridDim.x);
+    if (pair >= a.n_pairs) return;
+    const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
+    const int nI = a.t.img_n[I], nJ = a.t.img_n[J];
+    const int64_t row0I = a.t.img_row0[I];
+    uint4* sCode = smem;
+    uint64_t* sBk = reinterpret_cast<uint64_t*>(sCode + nI);
+    uint16_t* sList = reinterpret_cast<uint16_t*>(sBk + nI);
+    uint16_t* sOff = sList + kCascGroups * nI;
+    const uint4* gCode = reinterpret_cast<const uint4*>(a.t.code) + row0I;
+    for (int i = threadIdx.x; i < nI; i += kCascLdsThreads) {
+        sCode[i] = gCode[i];
+        sBk[i] = a.t.bkt[row0I + i];
+    }
+    for (int g = 0; g < kCascGroups; ++g) {
+        const int32_t* L = a.t.blist + (int64_t)g * a.t.rows + row0I;
+        for (int i = threadIdx.x; i < nI; i += kCascLdsThreads) sList[g * nI + i] = (uint16_t)L[i];
+    }
+    const int32_t* gOff = a.t.boff + (int64_t)I * kCascGroups * (kCascBuckets + 1);
+    for (int i = threadIdx.x; i < kCascGroups * (kCascBuckets + 1); i += kCascLdsThreads)
+        sOff[i] = (uint16_t)gOff[i];
+    __syncthreads();
+    LdsTabs tb{sList, nI, sOff, sCode, sBk};
+    const int64_t qrow0 = a.t.img_row0[J];
+    for (int q = threadIdx.x; q < nJ; q += kCascLdsThreads)
+        casc_query(tb, a, qrow0 + q, row0I, (int64_t)pair * a.out_stride + q);
 }
 
 }  // namespace
@@ -362,10 +425,27 @@ void casc_hash(const CascTables& t, const float* proj, const float* zm, const in
     SFM_HIP(hipGetLastError());
 }
 
-void casc_match(const CascMatchArgs& a, hipStream_t s) {
-    const int64_t nwg = (int64_t)a.n_pairs * a.qblocks;
-    if (nwg == 0) return;
-    hipLaunchKernelGGL(casc_match_kernel, dim3((unsigned)nwg), dim3(kCascQB), 0, s, a);
+size_t casc_lds_bytes(int max_n) {
+    return (size_t)max_n * (16 + 8 + 2 * kCascGroups) + (size_t)kCascGroups * (kCascBuckets + 1) * 2;
+}
+
+void casc_match(const CascMatchArgs& a, int max_n, hipStream_t s) {
+    if (a.n_pairs == 0) return;
+    const size_t lds = casc_lds_bytes(max_n);
+    if (max_n <= kCascLdsMaxN) {
+        static bool attr = false;
+        if (!attr) {
+            SFM_HIP(hipFuncSetAttribute((const void*)casc_match_lds_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)casc_lds_bytes(kCascLdsMaxN)));
+            attr = true;
+        }
+        hipLaunchKernelGGL(casc_match_lds_kernel, dim3((unsigned)a.n_pairs), dim3(kCascLdsThreads),
+                           lds, s, a);
+    } else {
+        const int64_t nwg = (int64_t)a.n_pairs * a.qblocks;
+        hipLaunchKernelGGL(casc_match_kernel, dim3((unsigned)nwg), dim3(kCascQB), 0, s, a);
+    }
     SFM_HIP(hipGetLastError());
 }
 

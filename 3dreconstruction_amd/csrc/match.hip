@@ -328,10 +328,11 @@ struct sfm_match_plan {
     // the set of images in the pair list (the zero-mean input) changes
     std::vector<int32_t> casc_used;
     bool casc_ready = false;
+    bool casc_pinned = false;    // set by sfm_match_plan_cascade_index
     DBuf<float> casc_proj, casc_zm;
     DBuf<int64_t> casc_colsum;
     DBuf<uint32_t> casc_code;
-    DBuf<uint16_t> casc_bkt;
+    DBuf<uint64_t> casc_bkt;
     DBuf<int32_t> casc_boff, casc_blist, casc_img;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
@@ -435,14 +436,25 @@ void run_top2(sfm_match_plan* p, const int32_t* pairs_d, int64_t n_pairs, int sw
 
 // Hash tables for the images of this pair list (zero-mean over exactly those
 // images, as Cascade_Hashing_Matcher_Regions' used_index).
-void casc_prepare(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs) {
+void casc_prepare(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, bool pin) {
     hipStream_t s = p->ctx->stream;
     std::vector<char> seen(p->n_img, 0);
     for (int64_t q = 0; q < 2 * n_pairs; ++q) seen[pairs[q]] = 1;
     std::vector<int32_t> used;
     for (int i = 0; i < p->n_img; ++i)
         if (seen[i]) used.push_back(i);
-    if (p->casc_ready && used == p->casc_used) return;
+    if (p->casc_ready) {
+        if (used == p->casc_used) {
+            p->casc_pinned = p->casc_pinned || pin;
+            return;
+        }
+        if (!pin && p->casc_pinned &&
+            std::includes(p->casc_used.begin(), p->casc_used.end(), used.begin(), used.end()))
+            return;   // a part of the indexed list
+    }
+    p->casc_pinned = pin;
+    SFM_REQUIRE(p->max_n < (1 << 21), SFM_ERR_UNSUPPORTED,
+                "cascade hashing: %d descriptors in one image (limit 2^21)", p->max_n);
     CascTables t = casc_tables(p);
     if (!p->casc_proj.p) {
         std::vector<float> proj;
@@ -452,7 +464,7 @@ void casc_prepare(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs) {
         p->casc_zm.alloc(kCascCode);
         p->casc_colsum.alloc((size_t)std::max(1, p->n_img) * kCascCode);
         p->casc_code.alloc((size_t)p->rows * 4);
-        p->casc_bkt.alloc((size_t)p->rows * 8);
+        p->casc_bkt.alloc((size_t)p->rows);
         p->casc_boff.alloc((size_t)std::max(1, p->n_img) * kCascGroups * (kCascBuckets + 1));
         p->casc_blist.alloc((size_t)p->rows * kCascGroups);
         p->casc_img.alloc(std::max(1, p->n_img));
@@ -488,7 +500,7 @@ void run_cascade(sfm_match_plan* p, int64_t n_pairs, float r2) {
         a.out_stride = p->stride;
         a.out_idx = p->out_idx.p + b0 * p->stride;
         a.out_d = p->out_d.p + b0 * p->stride;
-        casc_match(a, p->ctx->stream);
+        casc_match(a, p->max_n, p->ctx->stream);
         ++p->launches;
     }
 }
@@ -502,7 +514,7 @@ void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const s
         SFM_REQUIRE(pairs[2 * q] >= 0 && pairs[2 * q] < p->n_img && pairs[2 * q + 1] >= 0 &&
                         pairs[2 * q + 1] < p->n_img,
                     SFM_ERR_INVALID_ARG, "pair %lld out of range", (long long)q);
-    if (o->mode == SFM_MATCH_CASCADE) casc_prepare(p, pairs, n_pairs);
+    if (o->mode == SFM_MATCH_CASCADE) casc_prepare(p, pairs, n_pairs, false);
     p->mode = o->mode;
     p->n_pairs = n_pairs;
     p->stride = std::max<int64_t>(1, p->max_n);
@@ -586,6 +598,19 @@ extern "C" int sfm_match_plan_run(sfm_match_plan* p, const int32_t* pairs, int64
             SFM_HIP(hipStreamSynchronize(p->ctx->stream));
             *total = (int64_t)h[1];
         }
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_cascade_index(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs) {
+    return guarded([&] {
+        SFM_REQUIRE(p && (pairs || n_pairs == 0) && n_pairs >= 0, SFM_ERR_INVALID_ARG,
+                    "bad arguments");
+        for (int64_t q = 0; q < 2 * n_pairs; ++q)
+            SFM_REQUIRE(pairs[q] >= 0 && pairs[q] < p->n_img, SFM_ERR_INVALID_ARG,
+                        "pair %lld out of range", (long long)(q / 2));
+        SFM_HIP(hipSetDevice(p->ctx->device));
+        casc_prepare(p, pairs, n_pairs, true);
         return SFM_OK;
     });
 }

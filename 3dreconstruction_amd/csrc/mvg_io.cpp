@@ -682,10 +682,12 @@ extern "C" int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm
                                 sfm_sparse_match_stats* stats) {
     return guarded([&] {
         SFM_REQUIRE(ctx && matches_dir, SFM_ERR_INVALID_ARG, "null argument");
-        sfm_sparse_match_opts o{SFM_MATCH_RATIO, 0.8f, 0, 1, {0, 0}};
+        // NULL opts: the reference's own settings, "AUTO" on SIFT regions ->
+        // cascade hashing (:811-814,911-914), fDistRatio 0.8f, bForce false
+        sfm_sparse_match_opts o{SFM_MATCH_CASCADE, 0.8f, 0, 1, {0, 0}};
         if (opts) o = *opts;
-        SFM_REQUIRE(o.mode == SFM_MATCH_RATIO || o.mode == SFM_MATCH_MUTUAL, SFM_ERR_INVALID_ARG, "bad mode %d",
-                    o.mode);
+        SFM_REQUIRE(o.mode == SFM_MATCH_RATIO || o.mode == SFM_MATCH_MUTUAL || o.mode == SFM_MATCH_CASCADE,
+                    SFM_ERR_INVALID_ARG, "bad mode %d", o.mode);
         sfm_sparse_match_stats st{};
         const std::string dir(matches_dir), out = filespec(dir, "matches.putative.bin");
         if (!o.force && is_file(out)) {
@@ -728,13 +730,17 @@ extern "C" int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm
         }
         st.n_views = (int64_t)views.size();
         st.n_pairs_in = (int64_t)pairs.size();
-        // pairs whose views have no regions are skipped (Matcher_Regions :continue)
+        // pairs whose views have no regions are skipped by Matcher_Regions
+        // (:continue); the cascade matcher keeps them, since every view of the
+        // pair list enters its zero-mean descriptor (an empty one as zeros)
         std::vector<std::pair<uint32_t, uint32_t>> run;
         std::vector<int32_t> pv;
         for (const auto& p : pairs) {
             auto a = slot.find(p.first), b = slot.find(p.second);
             if (a == slot.end() || b == slot.end()) continue;
-            if (off[a->second + 1] == off[a->second] || off[b->second + 1] == off[b->second]) continue;
+            if (o.mode != SFM_MATCH_CASCADE &&
+                (off[a->second + 1] == off[a->second] || off[b->second + 1] == off[b->second]))
+                continue;
             run.push_back(p);
             pv.push_back(a->second);
             pv.push_back(b->second);

@@ -330,9 +330,24 @@ class sparseBuilder {
         last_rc_ = sfm_sparse_match_pair(matches_dir_.c_str());
         if (last_rc_ != SFM_OK) std::fprintf(stderr, "matchPair failed: %s\n", sfm_last_error());
     }
-    // Matcher_Regions(fDistRatio = 0.8f, BRUTE_FORCE_L2) over pairs.bin (:809-1023)
-    void match(float dist_ratio = 0.8f, bool force = false) {
-        sfm_sparse_match_opts o{SFM_MATCH_RATIO, dist_ratio, force ? 1 : 0, 1, {0, 0}};
+    // sNearestMatchingMethod (:814, :911-925) -> SFM_MATCH_*: "AUTO" on SIFT
+    // regions is Cascade_Hashing_Matcher_Regions, "BRUTEFORCEL2" is
+    // Matcher_Regions(BRUTE_FORCE_L2); others are not provided (-1).
+    static int matchingMode(const std::string& method) {
+        if (method == "AUTO" || method == "CASCADEHASHINGL2" || method == "FASTCASCADEHASHINGL2")
+            return SFM_MATCH_CASCADE;
+        if (method == "BRUTEFORCEL2") return SFM_MATCH_RATIO;
+        return -1;
+    }
+    // match() over pairs.bin (:809-1023), fDistRatio = 0.8f, method "AUTO"
+    void match(float dist_ratio = 0.8f, bool force = false, const std::string& method = "AUTO") {
+        const int mode = matchingMode(method);
+        if (mode < 0) {
+            last_rc_ = SFM_ERR_UNSUPPORTED;
+            std::fprintf(stderr, "match failed: unsupported nearest matching method %s\n", method.c_str());
+            return;
+        }
+        sfm_sparse_match_opts o{mode, dist_ratio, force ? 1 : 0, 1, {0, 0}};
         last_rc_ = sfm_sparse_match(ctx_->get(), matches_dir_.c_str(), &o, &stats_);
         if (last_rc_ != SFM_OK) std::fprintf(stderr, "match failed: %s\n", sfm_last_error());
     }
@@ -348,7 +363,10 @@ class sparseBuilder {
             for (uint32_t j = i + 1; j < n; ++j) p.emplace_back(i, j);
         return p;
     }
-    PairWiseMatches matchRegions(const std::vector<Pair>& pairs, float dist_ratio = 0.8f) const {
+    PairWiseMatches matchRegions(const std::vector<Pair>& pairs, float dist_ratio = 0.8f,
+                                 const std::string& method = "AUTO") const {
+        const int mode = matchingMode(method);
+        if (mode < 0) throw Error(SFM_ERR_UNSUPPORTED, "unsupported nearest matching method " + method);
         std::vector<uint8_t> desc;
         std::vector<int64_t> off(1, 0);
         for (auto& r : regions_) {
@@ -360,7 +378,7 @@ class sparseBuilder {
               "sfm_match_plan_create");
         std::vector<int32_t> pv;
         for (auto& p : pairs) { pv.push_back((int32_t)p.first); pv.push_back((int32_t)p.second); }
-        sfm_match_options o{SFM_MATCH_RATIO, dist_ratio};
+        sfm_match_options o{mode, dist_ratio};
         int64_t total = 0;
         int rc = sfm_match_plan_run(plan, pv.data(), (int64_t)pairs.size(), &o, &total);
         std::vector<int64_t> counts(pairs.size());

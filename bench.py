@@ -119,6 +119,27 @@ def cpu_baseline_match(desc, n_kp, pairs, n_pairs=24, threads=1):
             "sample": f"first {n_pairs} pairs of C3, exact integer brute force, {dt:.1f} s wall"}
 
 
+def cpu_baseline_cascade(desc, n_kp, n_img=16, threads=1):
+    """The oracle on every pair among the first n_img images (hashing
+    included, so the sample is hashing-heavier than the full list)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _helpers as H
+    lib = H.oracle()
+    off = np.arange(desc.shape[0] // n_kp + 1, dtype=np.int64) * n_kp
+    sub = np.array([(i, j) for i in range(n_img) for j in range(i + 1, n_img)], np.int32)
+    n_pairs = len(sub)
+    counts = np.zeros(n_pairs, np.int64)
+    t = time.time()
+    lib.orc_match_pairs(abi.ptr(desc, abi.u8p), abi.ptr(off, abi.i64p), len(off) - 1,
+                        abi.ptr(sub, abi.i32p), n_pairs, abi.SFM_MATCH_CASCADE, 0.8, threads,
+                        abi.ptr(counts, abi.i64p), None, None, None)
+    dt = time.time() - t
+    n_used = len(np.unique(sub))
+    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"all {n_pairs} pairs among the first {n_used} C3 images, incl. hashing "
+                      f"them, cascade-hashing restatement, {dt:.1f} s wall"}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
     summary of this configuration (profiles/r*/pmc_summary.json, written by
@@ -359,6 +380,40 @@ def main():
                            "workload": "first 10% of the C3 pair list, BFMatcher(NORM_L2, crossCheck) "
                                        "semantics (LocalFrame.h:31-47), exact"}
         log(f"match mutual: {len(msub)} pairs in {udt:.3f}s -> {len(msub) / udt:.0f} pairs/s")
+        # the reference's live default, "AUTO" -> cascade hashing (SURVEY §8(f)
+        # row 1): index (zero-mean, codes, buckets of every image of the list;
+        # replicated per rank) + this rank's part of the pair list, timed together
+        mplan.run(pairs[:64], mode=abi.SFM_MATCH_CASCADE, count=False)   # warm-up
+        ctx.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        mplan.cascade_index(pairs)
+        ctx.synchronize()
+        t_idx = time.perf_counter() - t1
+        mplan.run(pairs[lo:hi], mode=abi.SFM_MATCH_CASCADE, count=False)
+        ctx.synchronize()
+        barrier()
+        cdt = max_over_ranks(time.perf_counter() - t1)
+        ckms, ckl = mplan.last_ms()
+        # algorithmic bytes per pair: both images' hashed tables read once
+        # (database I: descriptors, codes, 6 bucket lists, bucket offsets;
+        # queries J: descriptors, codes, bucket ids) + the per-query result
+        bpp = nkp * (128 + 16 + 6 * 4) + 6 * 1025 * 4 + nkp * (128 + 16 + 16) + nkp * 8
+        cgbs = (hi - lo) * bpp / (ckms * 1e-3) / 1e9
+        match["cascade"] = {
+            "metric": "SIFT cascade-hashing match pairs/sec", "value": len(pairs) / cdt,
+            "unit": "pairs/s", "pairs": len(pairs), "index_ms": t_idx * 1e3,
+            "workload": "C3 pair list, Cascade_Hashing_Matcher_Regions(0.8) semantics "
+                        "(sparseBuilder.cpp:911-914, the reference's AUTO default); "
+                        "time includes hashing every image",
+            "roofline": {"bound": "hbm", "achieved": cgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": cgbs / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic("casc_match_kernel") if pmc_ok else None,
+                         "kernel": "casc_match_kernel", "per_launch_ms": ckms / max(ckl, 1),
+                         "algorithmic_bytes_per_pair": bpp},
+            "digest": mplan.digest()}
+        log(f"match cascade: {len(pairs)} pairs in {cdt:.3f}s (index {t_idx * 1e3:.1f} ms) -> "
+            f"{len(pairs) / cdt:.0f} pairs/s, match kernels {ckms:.1f} ms")
 
     cpu = None
     cpu_match = None
@@ -369,6 +424,8 @@ def main():
             if match is not None:
                 cpu_match = cpu_baseline_match(desc, 4096, pairs, n_pairs=8, threads=1)
                 match["cpu_baseline"] = cpu_match
+                match["cascade"]["cpu_baseline"] = cpu_baseline_cascade(desc, 4096)
+                log(f"cpu baseline cascade: {match['cascade']['cpu_baseline']['value']:.3f} pairs/s")
         except Exception as ex:  # oracle missing: baseline unmeasured, not faked
             log(f"cpu baseline unavailable: {ex}")
 

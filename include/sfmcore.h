@@ -280,6 +280,13 @@ int sfm_match_plan_create(sfm_ctx* ctx, const uint8_t* desc,
 int sfm_match_plan_run(sfm_match_plan* plan, const int32_t* pairs,
                        int64_t n_pairs, const sfm_match_options* opts,
                        int64_t* total_matches);
+/* SFM_MATCH_CASCADE tables (codes, buckets, zero-mean descriptor) for the
+ * images of this pair list, as Cascade_Hashing_Matcher_Regions::Match builds
+ * them for its whole pair list.  Later CASCADE runs whose images are a subset
+ * reuse them, so a list split over ranks or batches matches exactly as the
+ * whole list does; a run touching other images re-hashes for its own list. */
+int sfm_match_plan_cascade_index(sfm_match_plan* plan, const int32_t* pairs,
+                                 int64_t n_pairs);
 /* Fetch: counts[n_pairs]; i/j/d2[total] pair-ordered, each pair's matches
  * sorted by (i, j) as openMVG IndMatch::getDeduplicated leaves them. */
 int sfm_match_plan_fetch(sfm_match_plan* plan, int64_t* counts,
@@ -347,7 +354,9 @@ int sfm_mvg_load_matches(const char* path, int32_t* pairs, int64_t* counts,
 int sfm_sparse_match_pair(const char* matches_dir);
 
 typedef struct sfm_sparse_match_opts {
-    int32_t mode;      /* SFM_MATCH_RATIO (the reference's)                   */
+    int32_t mode;      /* SFM_MATCH_CASCADE = "AUTO", the reference's default
+                          (:814, :911-914); SFM_MATCH_RATIO = "BRUTEFORCEL2"
+                          (:919-921); NULL opts select CASCADE             */
     float ratio;       /* fDistRatio 0.8f (:812)                              */
     int32_t force;     /* 0: reload an existing matches.putative.bin (:890)   */
     int32_t dedup_xy;  /* 1: drop matches whose keypoint coordinates repeat

@@ -115,7 +115,7 @@ int main() {
     sb.setRegions(regions);
     auto pairs = sb.exhaustive();
     CHECK(pairs.size() == 6);
-    auto pm = sb.matchRegions(pairs);
+    auto pm = sb.matchRegions(pairs, 0.8f, "BRUTEFORCEL2");
     for (auto& [pr2, v] : pm) {
         std::vector<int32_t> ri(700), rd(700);
         orc_match_dense(regions[pr2.first].data(), 700, regions[pr2.second].data(), 700, SFM_MATCH_RATIO, 0.8f,
@@ -127,6 +127,33 @@ int main() {
         for (std::size_t k = 0; k < v.size(); ++k) CHECK(exp[k].first == v[k].i_ && exp[k].second == v[k].j_);
     }
     std::printf("sparseBuilder: %zu pairs matched, bit-exact vs oracle\n", pm.size());
+    // "AUTO" (the reference's default): cascade hashing over the collection
+    auto pmc = sb.matchRegions(pairs);
+    {
+        std::vector<int32_t> pv;
+        for (auto& p : pairs) { pv.push_back((int32_t)p.first); pv.push_back((int32_t)p.second); }
+        const int64_t off[5] = {0, 700, 1400, 2100, 2800};
+        std::vector<int64_t> cnt(pairs.size());
+        CHECK(orc_match_pairs(desc.data(), off, 4, pv.data(), (int64_t)pairs.size(), SFM_MATCH_CASCADE, 0.8f, 4,
+                              cnt.data(), nullptr, nullptr, nullptr) == SFM_OK);
+        int64_t tot = 0;
+        for (auto c : cnt) tot += c;
+        std::vector<uint32_t> ci(tot + 1), cj(tot + 1);
+        std::vector<int32_t> cd(tot + 1);
+        CHECK(orc_match_pairs(desc.data(), off, 4, pv.data(), (int64_t)pairs.size(), SFM_MATCH_CASCADE, 0.8f, 4,
+                              cnt.data(), ci.data(), cj.data(), cd.data()) == SFM_OK);
+        int64_t k = 0;
+        for (std::size_t p = 0; p < pairs.size(); ++p) {
+            const auto& v = pmc.at(pairs[p]);
+            CHECK((int64_t)v.size() == cnt[p]);
+            for (int64_t c = 0; c < cnt[p]; ++c, ++k) CHECK(v[c].i_ == ci[k] && v[c].j_ == cj[k]);
+        }
+        CHECK(tot > 0);
+        std::printf("sparseBuilder AUTO: cascade hashing, %lld matches, bit-exact vs oracle\n", (long long)tot);
+    }
+    bool threw = false;
+    try { sb.matchRegions(pairs, 0.8f, "HNSWL2"); } catch (const sfm::Error& e) { threw = e.code == SFM_ERR_UNSUPPORTED; }
+    CHECK(threw);
 
     // ---- file-staged sparseBuilder(base).matchPair() + match() --------------------
     char tmpl[] = "/tmp/sfm_facade_XXXXXX";
@@ -160,7 +187,7 @@ int main() {
     sfm::sparse::sparseBuilder fsb(base, ctx);
     fsb.matchPair();
     CHECK(fsb.lastError() == SFM_OK);
-    fsb.match();
+    fsb.match(0.8f, false, "BRUTEFORCEL2");
     CHECK(fsb.lastError() == SFM_OK && !fsb.stats().reloaded);
     int64_t np = 0, nm = 0;
     const std::string mfile = mdir + "/matches.putative.bin";
@@ -180,6 +207,25 @@ int main() {
     }
     fsb.match();   // existing matches.putative.bin is reloaded (bForce = false)
     CHECK(fsb.lastError() == SFM_OK && fsb.stats().reloaded && fsb.stats().n_matches == nm);
+    fsb.match(0.8f, true);   // forced, "AUTO": cascade hashing, same as in memory
+    CHECK(fsb.lastError() == SFM_OK && !fsb.stats().reloaded);
+    {
+        int64_t cp = 0, cm = 0;
+        CHECK(sfm_mvg_load_matches(mfile.c_str(), nullptr, nullptr, nullptr, nullptr, 0, 0, &cp, &cm) == SFM_OK);
+        std::vector<int32_t> cpv(2 * cp);
+        std::vector<int64_t> ccn(cp);
+        std::vector<uint32_t> cii(cm), cjj(cm);
+        CHECK(sfm_mvg_load_matches(mfile.c_str(), cpv.data(), ccn.data(), cii.data(), cjj.data(), cp, cm, &cp, &cm) ==
+              SFM_OK);
+        int64_t kk = 0;
+        for (int64_t q = 0; q < cp; ++q) {
+            const auto& v = pmc.at({(uint32_t)cpv[2 * q], (uint32_t)cpv[2 * q + 1]});
+            CHECK((int64_t)v.size() == ccn[q]);
+            for (int64_t c = 0; c < ccn[q]; ++c, ++kk) CHECK(v[c].i_ == cii[kk] && v[c].j_ == cjj[kk]);
+        }
+    }
+    fsb.match(0.8f, true, "HNSWL1");
+    CHECK(fsb.lastError() == SFM_ERR_UNSUPPORTED);
     if (std::system(("rm -rf " + base).c_str()) != 0) std::fprintf(stderr, "cleanup of %s failed\n", base.c_str());
     std::printf("sparseBuilder(base): file-staged matchPair + match, %lld pairs, identical to in-memory\n"
                 "facade ok\n", (long long)np);

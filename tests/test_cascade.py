@@ -173,13 +173,16 @@ def test_gpu_dense_vlfeat(ctx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("na,nb,hi", [(0, 5, 256), (5, 0, 256), (1, 7, 256), (2, 2, 256),
                                       (3, 3, 256), (37, 300, 256), (513, 1000, 130),
-                                      (600, 600, 3), (300, 300, 1)])
+                                      (600, 600, 3), (300, 300, 1),
+                                      # > kCascLdsMaxN rows: the global-table kernel
+                                      (6000, 700, 130)])
 def test_gpu_dense_random(ctx, na, nb, hi):
     rng = np.random.default_rng(na * 7919 + nb + hi)
     a = rng.integers(0, hi, (na, 128), dtype=np.uint8)
     b = rng.integers(0, hi, (nb, 128), dtype=np.uint8)
-    if na == nb and hi == 130:
-        b[: na // 2] = a[: na // 2]
+    if hi == 130:
+        m = min(na, nb) // 2
+        b[:m] = a[:m]
     gi, gd = _api().match_dense(ctx, a, b, CASC)
     oi, od = H.oracle_match_dense(a, b, CASC)
     np.testing.assert_array_equal(gi, oi)
@@ -209,5 +212,16 @@ def test_gpu_plan_vs_oracle_ragged_and_rehash(ctx):
             np.testing.assert_array_equal(i, oi)
             np.testing.assert_array_equal(j, oj)
             np.testing.assert_array_equal(dd, od)
+        # a list split into parts (ranks / batches) after cascade_index(full)
+        # matches exactly as the whole list
+        plan.cascade_index(full)
+        oc, oi, oj, od = H.oracle_match_pairs(desc, off, full, CASC)
+        got = [[], [], [], []]
+        for part in (full[:7], full[7:30], full[30:]):
+            plan.run(part, mode=CASC)
+            for k, v in enumerate(plan.fetch()):
+                got[k].append(v)
+        for k, v in enumerate((oc, oi, oj, od)):
+            np.testing.assert_array_equal(np.concatenate(got[k]), v)
     finally:
         plan.close()

@@ -189,15 +189,31 @@ def make_stage_dir(d, views, with_pairs=True):
         api.sparse_match_pair(d)
 
 
-def expected_matches(views, dedup=True):
-    """Oracle restatement: RATIO matching (exact brute force), (i, j)-sorted,
-    then drop matches whose (xI, yI, xJ, yJ) repeat an earlier one."""
+def expected_matches(views, dedup=True, mode=abi.SFM_MATCH_RATIO, pairs=None):
+    """Oracle restatement: RATIO (exact brute force) or CASCADE matching over
+    the collection, (i, j)-sorted, then drop matches whose (xI, yI, xJ, yJ)
+    repeat an earlier one."""
+    n = len(views)
+    if pairs is None:
+        pairs = [(I, J) for I in range(n) for J in range(I + 1, n)]
+    per = {}
+    if mode == abi.SFM_MATCH_CASCADE:
+        desc = np.concatenate([v[0] for v in views])
+        off = np.cumsum([0] + [len(v[0]) for v in views]).astype(np.int64)
+        c, ii, jj, _ = H.oracle_match_pairs(desc, off, pairs, mode)
+        k = 0
+        for (I, J), cnt in zip(pairs, c):
+            per[(I, J)] = list(zip(ii[k:k + cnt].tolist(), jj[k:k + cnt].tolist()))
+            k += cnt
     out = {}
-    for I in range(len(views)):
-        for J in range(I + 1, len(views)):
+    for (I, J) in pairs:
+        if True:
             (dI, kI), (dJ, kJ) = views[I], views[J]
-            idx, _ = H.oracle_match_dense(dI, dJ, abi.SFM_MATCH_RATIO)
-            m = sorted((int(i), int(j)) for j, i in enumerate(idx) if i >= 0)
+            if mode == abi.SFM_MATCH_CASCADE:
+                m = per[(I, J)]
+            else:
+                idx, _ = H.oracle_match_dense(dI, dJ, mode)
+                m = sorted((int(i), int(j)) for j, i in enumerate(idx) if i >= 0)
             if dedup:
                 seen, keep = set(), []
                 for i, j in m:
@@ -231,7 +247,7 @@ def test_match_stage_gpu(tmp_path):
     views = vlfeat_views()
     make_stage_dir(tmp_path, views)
     ctx = api.Context(0)
-    st = api.sparse_match(ctx, tmp_path)
+    st = api.sparse_match(ctx, tmp_path, mode=abi.SFM_MATCH_RATIO)
     got = api.mvg_load_matches(tmp_path / "matches.putative.bin")
     exp = expected_matches(views)
     assert list(got) == list(exp)
@@ -242,7 +258,7 @@ def test_match_stage_gpu(tmp_path):
     # an existing matches file is reloaded, not recomputed (bForce = false)
     assert api.sparse_match(ctx, tmp_path)["reloaded"]
     # without dedup the raw ratio matches come out; forced recompute
-    st2 = api.sparse_match(ctx, tmp_path, force=True, dedup_xy=False)
+    st2 = api.sparse_match(ctx, tmp_path, mode=abi.SFM_MATCH_RATIO, force=True, dedup_xy=False)
     raw = expected_matches(views, dedup=False)
     got2 = api.mvg_load_matches(tmp_path / "matches.putative.bin")
     assert list(got2) == list(raw) and all(np.array_equal(got2[k], raw[k]) for k in raw)
@@ -257,9 +273,30 @@ def test_match_stage_gpu_pairs_file_and_empty_view(tmp_path):
     make_stage_dir(tmp_path, views, with_pairs=False)
     (tmp_path / "pairs.bin").write_text("2 0\n3 1 0\n")   # (0,2), (0,3), (1,3)
     ctx = api.Context(0)
-    st = api.sparse_match(ctx, tmp_path)
+    st = api.sparse_match(ctx, tmp_path, mode=abi.SFM_MATCH_RATIO)
     got = api.mvg_load_matches(tmp_path / "matches.putative.bin")
     exp = {k: v for k, v in expected_matches(views[:3]).items() if k == (0, 2)}
     assert list(got) == list(exp) and np.array_equal(got[(0, 2)], exp[(0, 2)])
     assert st["n_pairs_in"] == 3 and st["n_pairs_out"] == 1
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_match_stage_gpu_auto_is_cascade(tmp_path):
+    """Default (NULL-equivalent) options = the reference's "AUTO": cascade
+    hashing over the collection, with the pairs file and an empty view (the
+    empty view still counts in the zero-mean descriptor)."""
+    views = vlfeat_views()
+    views.append((np.zeros((0, 128), np.uint8), np.zeros((0, 4), np.float32)))
+    make_stage_dir(tmp_path, views, with_pairs=False)
+    (tmp_path / "pairs.bin").write_text("1 2\n2 0\n3 1 0\n")
+    ctx = api.Context(0)
+    st = api.sparse_match(ctx, tmp_path)
+    got = api.mvg_load_matches(tmp_path / "matches.putative.bin")
+    pairs = sorted([(1, 2), (0, 2), (1, 3), (0, 3)])
+    exp = expected_matches(views, mode=abi.SFM_MATCH_CASCADE, pairs=pairs)
+    assert list(got) == list(exp) and len(exp) >= 2
+    for k in exp:
+        assert np.array_equal(got[k], exp[k]), k
+    assert st["n_pairs_in"] == 4 and st["n_pairs_out"] == len(exp)
     ctx.close()
