@@ -140,7 +140,7 @@ def cpu_baseline_cascade(desc, n_kp, n_img=16, threads=1):
                       f"them, cascade-hashing restatement, {dt:.1f} s wall"}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, largest=False):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
     summary of this configuration (profiles/r*/pmc_summary.json, written by
     tools/pmc_summary.py: FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE).
@@ -156,7 +156,7 @@ def pmc_traffic(kernel):
         return None
     for name, e in ks.items():
         if name.startswith(kernel) and "traffic_bytes" in e:
-            return e["traffic_bytes"]
+            return e.get("traffic_bytes_max", e["traffic_bytes"]) if largest else e["traffic_bytes"]
     return None
 
 
@@ -358,7 +358,7 @@ def main():
                  "dtype": "u8 (i8 MFMA, i32 accumulate: exact)",
                  "roofline": {"bound": "mfma", "achieved": tops, "peak": I8_PEAK_TOPS,
                               "unit": "TOP/s", "frac": tops / I8_PEAK_TOPS,
-                              "traffic": pmc_traffic("match_top2_kernel") if pmc_ok else None,
+                              "traffic": pmc_traffic("match_top2_kernel", largest=True) if pmc_ok else None,
                               "kernel": "match_top2_kernel",
                               "per_launch_ms": kms / max(kl, 1)},
                  "digest": mplan.digest()}
@@ -408,8 +408,8 @@ def main():
                         "time includes hashing every image",
             "roofline": {"bound": "hbm", "achieved": cgbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": cgbs / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic("casc_match_kernel") if pmc_ok else None,
-                         "kernel": "casc_match_kernel", "per_launch_ms": ckms / max(ckl, 1),
+                         "traffic": pmc_traffic("casc_match_lds_kernel", largest=True) if pmc_ok else None,
+                         "kernel": "casc_match_lds_kernel", "per_launch_ms": ckms / max(ckl, 1),
                          "algorithmic_bytes_per_pair": bpp},
             "digest": mplan.digest()}
         log(f"match cascade: {len(pairs)} pairs in {cdt:.3f}s (index {t_idx * 1e3:.1f} ms) -> "

@@ -13,7 +13,7 @@ cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_r1 -o bench -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof_bench.err || { tail -20 $R/gpurun_out/prof_bench.err; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU"; do
   N=$(echo $C | cut -d' ' -f1)
-  timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "schur_kernel|match_top2_kernel|step_kernel|image_gram_kernel|bcr_level_kernel" --kernel-trace --output-format csv -d $R/gpurun_out/pmc3/$N -o p -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc3/$N.json 2> $R/gpurun_out/pmc3/$N.err || { tail -20 $R/gpurun_out/pmc3/$N.err; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "schur_kernel|match_top2_kernel|step_kernel|image_gram_kernel|bcr_level_kernel|casc_match_lds_kernel|casc_hash_kernel" --kernel-trace --output-format csv -d $R/gpurun_out/pmc3/$N -o p -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc3/$N.json 2> $R/gpurun_out/pmc3/$N.err || { tail -20 $R/gpurun_out/pmc3/$N.err; exit 1; }
   echo "pass $N done"
 done
 python3 $R/tools/pmc_summary.py $R/gpurun_out/pmc3 $R/gpurun_out/pmc3/pmc_summary.json

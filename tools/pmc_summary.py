@@ -33,6 +33,10 @@ def main(src, out):
             e["write_bytes"] = 1024.0 * sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
         if "fetch_bytes" in e and "write_bytes" in e:
             e["traffic_bytes"] = e["fetch_bytes"] + e["write_bytes"]
+            if len(d["FETCH_SIZE"]) == len(d["WRITE_SIZE"]):
+                # the largest launch (passes replay the same launch sequence)
+                e["traffic_bytes_max"] = max(1024.0 * (2.0 * f + w)
+                                             for f, w in zip(d["FETCH_SIZE"], d["WRITE_SIZE"]))
         for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU"):
             if c in d:
                 e[c] = sum(d[c]) / len(d[c])
