@@ -262,8 +262,9 @@ struct LdsTabs {
 //     order is (g, e) order; the ten smallest keys are kept by a min/max
 //     network (2 VALU per slot) and mapped back to ids at the end.
 template <class T>
-__device__ __forceinline__ void casc_query(const T& tb, const CascMatchArgs& a, int64_t qrow,
-                                           int64_t row0I, int64_t o) {
+__device__ __forceinline__ int casc_collect(const T& tb, const CascMatchArgs& a, int64_t qrow,
+                                            uint32_t (&key)[kCascTop]) {
+    // returns the number of distinct candidates (0 when <= 2 were collected)
     const uint64_t qb = a.t.bkt[qrow];
     int lo[kCascGroups], hi[kCascGroups], total = 0;
 #pragma unroll
@@ -273,19 +274,21 @@ __device__ __forceinline__ void casc_query(const T& tb, const CascMatchArgs& a, 
         hi[g] = tb.bucket(g, b + 1);
         total += hi[g] - lo[g];
     }
-    int idx = -1, dd = -1;
+#pragma unroll
+    for (int k = 0; k < kCascTop; ++k) key[k] = 0xffffffffu;
+    int uniq = 0;
     if (total > 2) {   // candidate_descriptors.size() <= NN: skip
         const uint4 qc = reinterpret_cast<const uint4*>(a.t.code)[qrow];
-        uint32_t key[kCascTop];
-#pragma unroll
-        for (int k = 0; k < kCascTop; ++k) key[k] = 0xffffffffu;
-        int uniq = 0;
 #pragma unroll
         for (int g = 0; g < kCascGroups; ++g) {
             for (int e = lo[g]; e < hi[g]; ++e) {
                 const int c = tb.at(g, e);
                 bool dup = false;
+#ifndef CASC_DIAG_NODEDUP   // A/B diagnostic builds only
                 if (g > 0) {
+#else
+                if (false) {
+#endif
                     const uint64_t x = tb.bid(c) ^ qb;
 #pragma unroll
                     for (int g2 = 0; g2 < g; ++g2) dup = dup || bucket_of(x, g2) == 0;
@@ -304,38 +307,79 @@ __device__ __forceinline__ void casc_query(const T& tb, const CascMatchArgs& a, 
                 }
             }
         }
-        if (uniq >= 2) {
-            const int4* qd = reinterpret_cast<const int4*>(a.t.desc + qrow * 128);
-            int4 qv[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) qv[w] = qd[w];
-            const int nq = a.t.nrm[qrow];
-            int d1 = INT_MAX, c1 = INT_MAX, d2 = INT_MAX, c2 = INT_MAX;
-#pragma unroll
-            for (int k = 0; k < kCascTop; ++k) {
-                if (k < uniq) {
-                    const int c = tb.at((int)(key[k] >> 21) & 7, (int)(key[k] & 0x1fffff));
-                    const int4* cd = reinterpret_cast<const int4*>(a.t.desc + (row0I + c) * 128);
-                    int dot = 0;
-#pragma unroll
-                    for (int w = 0; w < 8; ++w) {
-                        const int4 v = cd[w];
-                        dot = __builtin_amdgcn_sdot4(qv[w].x, v.x, dot, false);
-                        dot = __builtin_amdgcn_sdot4(qv[w].y, v.y, dot, false);
-                        dot = __builtin_amdgcn_sdot4(qv[w].z, v.z, dot, false);
-                        dot = __builtin_amdgcn_sdot4(qv[w].w, v.w, dot, false);
-                    }
-                    const int d = nq + a.t.nrm[row0I + c] - 2 * dot;
-                    // partial_sort of (distance, id) pairs: lexicographic
-                    if (d < d1 || (d == d1 && c < c1)) {
-                        d2 = d1; c2 = c1; d1 = d; c1 = c;
-                    } else if (d < d2 || (d == d2 && c < c2)) {
-                        d2 = d; c2 = c;
-                    }
-                }
-            }
-            if ((float)d1 < a.r2 * (float)d2) { idx = c1; dd = d1; }
+    }
+    return uniq;
+}
+
+template <class T>
+__device__ __forceinline__ int key_id(const T& tb, uint32_t key) {
+    return tb.at((int)(key >> 21) & 7, (int)(key & 0x1fffff));
+}
+
+// partial_sort of (distance, id) pairs + NNdistanceRatio
+struct Best2 {
+    int d1 = INT_MAX, c1 = INT_MAX, d2 = INT_MAX, c2 = INT_MAX;
+    __device__ __forceinline__ void add(int d, int c) {
+        if (d < d1 || (d == d1 && c < c1)) {
+            d2 = d1; c2 = c1; d1 = d; c1 = c;
+        } else if (d < d2 || (d == d2 && c < c2)) {
+            d2 = d; c2 = c;
         }
+    }
+};
+
+// One query q (row qrow of image J) against database image I (first row
+// row0I), every lane on its own: Match_HashedDescriptions + NNdistanceRatio.
+template <class T>
+__device__ __forceinline__ void casc_query(const T& tb, const CascMatchArgs& a, int64_t qrow,
+                                           int64_t row0I, int64_t o) {
+    uint32_t key[kCascTop];
+    const int uniq = casc_collect(tb, a, qrow, key);
+    int idx = -1, dd = -1;
+    if (uniq >= 2) {
+        // rows of the re-ranked candidates: ids and norms first, then the
+        // 128-byte rows double-buffered (loads of k+1 in flight during the
+        // dot product of k; slots past uniq re-read candidate 0, unused)
+        int cid[kCascTop], cn[kCascTop];
+#pragma unroll
+        for (int k = 0; k < kCascTop; ++k) cid[k] = key_id(tb, key[k < uniq ? k : 0]);
+#pragma unroll
+        for (int k = 0; k < kCascTop; ++k) cn[k] = a.t.nrm[row0I + cid[k]];
+        const int4* qd = reinterpret_cast<const int4*>(a.t.desc + qrow * 128);
+        int4 qv[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) qv[w] = qd[w];
+        const int nq = a.t.nrm[qrow];
+        Best2 b;
+        int4 cur[8];
+        {
+            const int4* cd = reinterpret_cast<const int4*>(a.t.desc + (row0I + cid[0]) * 128);
+#pragma unroll
+            for (int w = 0; w < 8; ++w) cur[w] = cd[w];
+        }
+#pragma unroll
+        for (int k = 0; k < kCascTop; ++k) {
+            int4 nxt[8];
+            if (k + 1 < kCascTop) {
+                const int4* cd = reinterpret_cast<const int4*>(a.t.desc + (row0I + cid[k + 1]) * 128);
+#pragma unroll
+                for (int w = 0; w < 8; ++w) nxt[w] = cd[w];
+            }
+            int dot = 0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                dot = __builtin_amdgcn_sdot4(qv[w].x, cur[w].x, dot, false);
+                dot = __builtin_amdgcn_sdot4(qv[w].y, cur[w].y, dot, false);
+                dot = __builtin_amdgcn_sdot4(qv[w].z, cur[w].z, dot, false);
+                dot = __builtin_amdgcn_sdot4(qv[w].w, cur[w].w, dot, false);
+            }
+            if (k < uniq) b.add(nq + cn[k] - 2 * dot, cid[k]);
+            if (k + 1 < kCascTop) {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) cur[w] = nxt[w];
+            }
+        }
+        if ((float)b.d1 < a.r2 * (float)b.d2) { idx = b.c1; dd = b.d1; }
     }
     a.out_idx[o] = idx;
     a.out_d[o] = dd;
