@@ -263,3 +263,53 @@ def test_rccl_single_rank_communicator(ctx):
     assert rc == rc1 == 0
     assert s1.iterations == s0.iterations and s1.final_cost == s0.final_cost
     assert np.array_equal(e1, e0) and np.array_equal(x1, x0)
+
+
+def _subset(sc, keep_fn):
+    """Keep, per point, the observations keep_fn(p, obs ids) returns."""
+    keep, off = [], [0]
+    for p in range(sc.n_pt):
+        ids = keep_fn(p, list(range(sc.pt_offsets[p], sc.pt_offsets[p + 1])))
+        keep.extend(ids)
+        off.append(off[-1] + len(ids))
+    keep = np.array(keep, np.int64)
+    sc.obs_img = np.ascontiguousarray(sc.obs_img[keep])
+    sc.obs_uv = np.ascontiguousarray(sc.obs_uv.reshape(-1, 2)[keep].reshape(-1))
+    sc.pt_offsets = np.array(off, np.int64)
+    sc.n_obs = len(keep)
+    return sc
+
+
+def test_single_observation_tracks_and_unobserved_blocks(ctx):
+    # points seen once (V of rank 2, held up by the LM diagonal), points and a
+    # camera with no observation at all (their blocks are dropped, as Ceres
+    # never sees a parameter block no residual touches), ragged elsewhere
+    sc = H.Scene(14, 900, 5, seed=21)
+    obs_img = sc.obs_img.copy()
+
+    def keep(p, ids):
+        ids = [o for o in ids if obs_img[o] != 9]
+        if p < 120:
+            return ids[:1]
+        if p < 160:
+            return []
+        return ids
+    # Points seen once leave a depth direction held only by the LM diagonal:
+    # the tail of the trajectory follows summation order (the oracle alone
+    # takes 17 or 18 iterations across 1/2/3/8 threads, same final cost to
+    # 1e-12), so the cost bar holds and the iteration count is not compared.
+    _compare(ctx, _subset(sc, keep), check_trace=False)
+
+
+def test_no_observations(ctx):
+    sc = _subset(H.Scene(6, 50, 3, seed=5), lambda p, ids: [])
+    orc_rc, os_, _, _ = H.oracle_solve(sc)
+    e, i, x = sc.params()
+    e0, i0, x0 = e.copy(), i.copy(), x.copy()
+    rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
+    assert rc == orc_rc
+    assert gs.num_residuals == os_.num_residuals == 0
+    assert gs.final_cost == os_.final_cost == 0.0
+    np.testing.assert_array_equal(e, e0)
+    np.testing.assert_array_equal(i, i0)
+    np.testing.assert_array_equal(x, x0)
