@@ -85,6 +85,8 @@ void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, co
 void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                     hipStream_t s);
 void ba_fscale(const DevProblem& P, hipStream_t s);
+// U / Ub / Ucn of a unit-scale ba_image_gram pass -> the same pass at scaleF
+void ba_gram_rescale(const DevProblem& P, hipStream_t s);
 void ba_fill(double* p, int64_t n, double v, hipStream_t s);
 // stamps (diagnostic builds only, else nullptr): per chunk 6 phase cycle sums
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,

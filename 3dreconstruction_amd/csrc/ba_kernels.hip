@@ -434,6 +434,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
     }
 }
 
+// Iteration 0 after the Jacobi scales are known: the image Gram pass applies
+// the per-image column scales to its sums (u = (s_i s_j) * sum), so the
+// scaled blocks follow from the unit-scale pass's exactly, without a second
+// linearisation of every observation (bit-identical to re-running the pass).
+template <int CM>
+__global__ __launch_bounds__(128) void gram_rescale_kernel(DevProblem P) {
+    using kT = gram::SlotTable<CM>;
+    const int b = blockIdx.x, img = b / kGramSeg;
+    const int colc = P.img_colc[img], coli = P.img_coli[img];
+    __shared__ double ssc[10];
+    if (threadIdx.x < 10) {
+        const int a = threadIdx.x;
+        ssc[a] = a < 6 ? (colc >= 0 ? P.scaleF[colc + a] : 0.0) : P.scaleF[coli + a - 6];
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int i = threadIdx.x / 10, j = threadIdx.x % 10, s = kT::kS.id[i][j];
+        const double u = s >= 0 ? ssc[i] * ssc[j] * P.U[(size_t)b * 100 + threadIdx.x] : 0.0;
+        P.U[(size_t)b * 100 + threadIdx.x] = u;
+        if (i == j) P.Ucn[(size_t)b * 10 + i] = u;
+    }
+    if (threadIdx.x >= 100 && threadIdx.x < 110) {
+        const int i = threadIdx.x - 100;
+        P.Ub[(size_t)b * 10 + i] = ssc[i] * P.Ub[(size_t)b * 10 + i];
+    }
+}
+
 // Jacobi scale of the point columns (iteration 0): 1 / (1 + |J col|).
 // One workgroup per Schur chunk, one thread per point, the chunk's cameras and
 // intrinsics staged in LDS (gathering each observation's CamPre from global
@@ -1506,6 +1533,12 @@ void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, co
                    hipStream_t s) {
     SFM_BY_MODEL(P, hipLaunchKernelGGL(image_gram_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp,
                                        intr, X));
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_gram_rescale(const DevProblem& P, hipStream_t s) {
+    if (P.n_img <= 0) return;
+    SFM_BY_MODEL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(128), 0, s, P));
     SFM_HIP(hipGetLastError());
 }
 

@@ -298,8 +298,10 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         allreduce_rcs();
         ba_fscale(P, s);
         ba_point_scale(P, S.cp, S.in, S.X, s);
+        ba_gram_rescale(P, s);         // = relinearize() at the new scales
+    } else {
+        relinearize();
     }
-    relinearize();
 
     double radius = O.initial_trust_region_radius, decrease_factor = 2.0;
     int consecutive_invalid = 0;
