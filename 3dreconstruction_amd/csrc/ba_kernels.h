@@ -74,6 +74,7 @@ struct DevProblem {
     double* part_f;     // [n_fblk][3] candidate-kernel partials
     int32_t n_fblk;
     double* scal;       // [kScCount]
+    double* scal_host;  // device view of host-mapped [kScCount + 1] (+ sequence word), or null
 };
 
 void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s);
@@ -102,7 +103,8 @@ void ba_cand(const DevProblem& P, const double* extr, const double* intr, double
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius,
              hipStream_t s);
-void ba_finalize(const DevProblem& P, hipStream_t s);
+// seq: written to scal_host[kScCount] after the scalars when scal_host is set
+void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq = 0);
 size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
 size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);

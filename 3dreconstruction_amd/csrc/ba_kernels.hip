@@ -1466,7 +1466,8 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
 // 1024 threads: each strides over ~4 partials per list instead of ~16 (the
 // pass is a chain of dependent global loads); fixed order, so deterministic
 constexpr int kFinThreads = 1024;
-__global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks) {
+__global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks,
+                                                               unsigned long long seq) {
     double s[7] = {0, 0, 0, 0, 0, 0, 0};
     double m[5] = {0, 0, 0, 0, 0};
 #pragma unroll 4
@@ -1503,6 +1504,17 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
         constexpr int kSlot[12] = {kScCost, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E, kScXnorm2F,
                                    kScStepnorm2F, kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScGmaxF};
         P.scal[kSlot[k]] = t;
+        if (P.scal_host) P.scal_host[kSlot[k]] = t;
+    }
+    if (P.scal_host) {
+        // publish to host-mapped memory: every scalar, a system-scope fence,
+        // then the sequence word the host polls (no blit, no stream sync)
+        if (threadIdx.x == 12) P.scal_host[kScSolveFail] = P.scal[kScSolveFail];
+        if (threadIdx.x < 13) __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.scal_host + kScCount), seq,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1635,8 +1647,8 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
     SFM_HIP(hipGetLastError());
 }
 
-void ba_finalize(const DevProblem& P, hipStream_t s) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinThreads), 0, s, P, ba_step_blocks(P));
+void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinThreads), 0, s, P, ba_step_blocks(P), seq);
     SFM_HIP(hipGetLastError());
 }
 

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -56,7 +57,9 @@ struct sfm_ba_plan {
     BcrArgs bcr;
     bool use_bcr = false;
     int64_t rcs_n = 0;
-    double* scal_h = nullptr;  // pinned
+    double* scal_h = nullptr;  // pinned, host-mapped: [kScCount] + finalize sequence word
+    double* scal_dev = nullptr;   // its device address
+    unsigned long long fin_seq = 0;
     std::vector<sfm_ba_iter> trace;
     double last_ms[8] = {0};
     double schur_ms_total = 0;
@@ -173,7 +176,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->scal_g.alloc((size_t)ctx->world * kScMaxEnd);
         pl->scal_gh.assign(pl->scal_g.n, 0.0);
     }
-    SFM_HIP(hipHostMalloc((void**)&pl->scal_h, kScCount * sizeof(double), hipHostMallocDefault));
+    SFM_HIP(hipHostMalloc((void**)&pl->scal_h, (kScCount + 1) * sizeof(double),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(pl->scal_h, 0, (kScCount + 1) * sizeof(double));
+    SFM_HIP(hipHostGetDevicePointer((void**)&pl->scal_dev, pl->scal_h, 0));
 
     DevProblem& P = pl->P;
     P.n_img = prob.n_img; P.n_intr = prob.n_intr;
@@ -254,6 +260,25 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     SFM_HIP(hipStreamSynchronize(s));
 }
 
+// Wait for finalize_kernel's publish of the iteration scalars (sequence word
+// after the values, system-scope release): a host spin on pinned memory
+// instead of a blit + stream synchronisation per LM iteration.  A long wait
+// falls back to the stream synchronisation, which also reports a failed launch.
+void wait_scalars(const double* host, unsigned long long seq, hipStream_t s) {
+    const auto* word = reinterpret_cast<const unsigned long long*>(host + kScCount);
+    auto published = [&] { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == seq; };
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 0; !published(); ++spins) {
+        __builtin_ia32_pause();
+        if ((spins & 1023) == 1023 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            SFM_HIP(hipStreamSynchronize(s));
+            SFM_REQUIRE(published(), SFM_ERR_DEVICE, "iteration scalars were not published");
+            break;
+        }
+    }
+}
+
 struct IterState {
     double* X; double* Xc; double* e; double* ec; double* in; double* inc; CamPre* cp; CamPre* cpc;
 };
@@ -303,6 +328,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         relinearize();
     }
 
+    // one rank: the scalars come back through host-mapped memory (wait_scalars);
+    // several: the device all-gather / host all-reduce below
+    P.scal_host = ctx->world == 1 ? pl->scal_dev : nullptr;
     double radius = O.initial_trust_region_radius, decrease_factor = 2.0;
     int consecutive_invalid = 0;
     double x_cost = 0.0, x_norm = 0.0;
@@ -339,8 +367,11 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         else ba_solve(P, radius, s);
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
-        ba_finalize(P, s);
-        if (ctx->comm && !ctx->host_allreduce) {
+        const unsigned long long seq = ++pl->fin_seq;
+        ba_finalize(P, s, seq);
+        if (P.scal_host) {
+            wait_scalars(pl->scal_h, seq, s);
+        } else if (ctx->comm && !ctx->host_allreduce) {
             // one RCCL collective: gather every rank's partial scalars, then sum
             // (rank order) / max them on the host
             SFM_REQUIRE(rccl_allgather_f64(ctx->comm, P.scal, pl->scal_g.p, kScMaxEnd, s) == 0, SFM_ERR_COMM,
@@ -365,6 +396,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             SFM_HIP(hipStreamSynchronize(s));
         }
         if (timed) {
+            SFM_HIP(hipEventSynchronize(pl->ev[ev_i + 1]));
             float ms = 0.f;
             SFM_HIP(hipEventElapsedTime(&ms, pl->ev[ev_i], pl->ev[ev_i + 1]));
             pl->schur_ms_total += ms;
