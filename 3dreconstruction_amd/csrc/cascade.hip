@@ -261,6 +261,12 @@ struct LdsTabs {
 //     (h << 24) | (g << 21) | e, e = position in group g's list: arrival
 //     order is (g, e) order; the ten smallest keys are kept by a min/max
 //     network (2 VALU per slot) and mapped back to ids at the end.
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 template <class T>
 __device__ __forceinline__ int casc_collect(const T& tb, const CascMatchArgs& a, int64_t qrow,
                                             uint32_t (&key)[kCascTop]) {
@@ -279,32 +285,47 @@ __device__ __forceinline__ int casc_collect(const T& tb, const CascMatchArgs& a,
     int uniq = 0;
     if (total > 2) {   // candidate_descriptors.size() <= NN: skip
         const uint4 qc = reinterpret_cast<const uint4*>(a.t.code)[qrow];
+        // software pipeline per group: the id of entry e+2 and the code /
+        // bucket ids of entry e+1 are read while entry e is ranked, so the
+        // two dependent LDS round trips per candidate overlap the VALU work
 #pragma unroll
         for (int g = 0; g < kCascGroups; ++g) {
-            for (int e = lo[g]; e < hi[g]; ++e) {
-                const int c = tb.at(g, e);
+            const int e0 = lo[g], e1 = hi[g];
+            if (e0 >= e1) continue;
+            int c = tb.at(g, e0);
+            int cn = e0 + 1 < e1 ? tb.at(g, e0 + 1) : c;
+            uint4 cc = tb.cd(c);
+            uint64_t cb = tb.bid(c);
+            for (int e = e0; e < e1; ++e) {
+                const int c1 = cn;
+                const uint4 cc1 = tb.cd(c1);
+                const uint64_t cb1 = g > 0 ? tb.bid(c1) : 0;
+                cn = e + 2 < e1 ? tb.at(g, e + 2) : c1;
                 bool dup = false;
 #ifndef CASC_DIAG_NODEDUP   // A/B diagnostic builds only
                 if (g > 0) {
 #else
                 if (false) {
 #endif
-                    const uint64_t x = tb.bid(c) ^ qb;
+                    const uint64_t x = cb ^ qb;
 #pragma unroll
                     for (int g2 = 0; g2 < g; ++g2) dup = dup || bucket_of(x, g2) == 0;
                 }
-                if (dup) continue;
-                ++uniq;
-                const uint4 cc = tb.cd(c);
-                const uint32_t h = __popc(qc.x ^ cc.x) + __popc(qc.y ^ cc.y) + __popc(qc.z ^ cc.z) +
-                                   __popc(qc.w ^ cc.w);
-                uint32_t kk = (h << 24) | ((uint32_t)g << 21) | (uint32_t)e;
+                if (!dup) {
+                    ++uniq;
+                    const uint32_t h = __popc(qc.x ^ cc.x) + __popc(qc.y ^ cc.y) + __popc(qc.z ^ cc.z) +
+                                       __popc(qc.w ^ cc.w);
+                    const uint32_t kk = (h << 24) | ((uint32_t)g << 21) | (uint32_t)e;
+                    // sorted insertion, one VALU per slot: the new k-th smallest
+                    // of {key, kk} is med3(key[k-1], kk, key[k]) (keys ascending),
+                    // so updating from the top down reads only old neighbours
 #pragma unroll
-                for (int k = 0; k < kCascTop; ++k) {
-                    const uint32_t t = key[k];
-                    key[k] = min(t, kk);
-                    kk = max(t, kk);
+                    for (int k = kCascTop - 1; k > 0; --k) key[k] = umed3(key[k - 1], kk, key[k]);
+                    key[0] = min(key[0], kk);
                 }
+                c = c1;
+                cc = cc1;
+                cb = cb1;
             }
         }
     }
