@@ -17,8 +17,9 @@
 //
 // Kernels:
 //   casc_colsum_kernel  per image column sums (zero-mean input), HBM-bound.
-//   casc_hash_kernel    188 x 128 fp32 FMAs per descriptor, projections in
-//                       LDS (broadcast reads), descriptor in 128 VGPRs.
+//   casc_hash_mfma_kernel  the 188 projections of 16 descriptors per wave as a
+//                       [16 x 128] x [128 x 192] product on v_mfma_f32_16x16x4_f32
+//                       (exact k-ordered fmaf chain), signs gathered by ballot.
 //   casc_bucket_kernel  one wave per (image, group): LDS histogram, scan and
 //                       a stable ballot-ranked scatter (lists stay ascending).
 //   casc_match_kernel   one thread per query; candidates of image I are read
@@ -26,6 +27,7 @@
 //                       blocks share an XCD); re-rank with v_dot4_i32_i8.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <random>
 #include <utility>
@@ -75,7 +77,6 @@ __global__ __launch_bounds__(128) void casc_colsum_kernel(const int8_t* __restri
     colsum[(int64_t)I * 128 + c] = s;
 }
 
-constexpr int kHashThreads = 256;
 
 template <typename F, int... I>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -86,81 +87,98 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-__global__ __launch_bounds__(kHashThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void casc_hash_kernel(
+// Projections on the f32 MFMA (v_mfma_f32_16x16x4_f32): the result
+// of one instruction is the k-ordered fmaf chain fma(a3,b3, .. fma(a0,b0,C)),
+// and chaining the 32 k-steps in k order reproduces the sequential
+// k = 0..127 fmaf chain of the oracle bit for bit.
+//   A = 16 descriptors x 4 k (lane l: descriptor l & 15, k = 4s + (l >> 4)),
+//   B = 4 k x 16 projections, from an LDS image P'[k][208] (row stride 208
+//   = 16 mod 64 banks: the wave's 64 reads hit 64 distinct banks),
+//   12 column tiles (188 projections padded to 192 with zeros) per wave tile;
+// the signs come out of __ballot per accumulator register.
+constexpr int kHashMThreads = 512;
+constexpr int kPtStride = 208;
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(kHashMThreads) void casc_hash_mfma_kernel(
     const int8_t* __restrict__ desc, const int64_t* __restrict__ img_row0,
     const int32_t* __restrict__ img_n, const int32_t* __restrict__ img_list,
     const float* __restrict__ proj, const float* __restrict__ zm, uint32_t* __restrict__ code,
     uint64_t* __restrict__ bkt) {
-    extern __shared__ __attribute__((aligned(16))) float4 sP[];  // [188][32]
+    extern __shared__ __attribute__((aligned(16))) float sPt[];   // [128][kPtStride]
     __shared__ float sZ[kCascCode];
-    for (int i = threadIdx.x; i < kCascProjRows * 32; i += kHashThreads)
-        sP[i] = reinterpret_cast<const float4*>(proj)[i];
+    // coalesced reads of proj[p][k], transposed into P'[k][p]; columns 188..207 zero
+    for (int i = threadIdx.x; i < kCascProjRows * kCascCode; i += kHashMThreads)
+        sPt[(i & (kCascCode - 1)) * kPtStride + (i >> 7)] = proj[i];
+    for (int i = threadIdx.x; i < kCascCode * (kPtStride - kCascProjRows); i += kHashMThreads) {
+        const int k = i / (kPtStride - kCascProjRows), pj = kCascProjRows + i % (kPtStride - kCascProjRows);
+        sPt[k * kPtStride + pj] = 0.f;
+    }
     if (threadIdx.x < kCascCode) sZ[threadIdx.x] = zm[threadIdx.x];
     __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int d = lane & 15, j = lane >> 4;
+    constexpr int kWaves = kHashMThreads / 64;
     const int I = img_list[blockIdx.y];
-    const int r = blockIdx.x * kHashThreads + threadIdx.x;
-    if (r >= img_n[I]) return;
-    const int64_t row = img_row0[I] + r;
-
-    // x lives in 128 VGPRs: every index below is a compile-time constant
-    // (static_for), so the array is promoted before loop unrolling runs.
-    float x[kCascCode];
-    const int4* src = reinterpret_cast<const int4*>(desc + row * 128);
-    static_for<8>([&](auto w) {
-        const int4 v = src[w.value];
-        const int wv[4] = {v.x, v.y, v.z, v.w};
-        static_for<16>([&](auto e) {
-            constexpr int k = 16 * decltype(w)::value + decltype(e)::value;
-            const int u = (int)(int8_t)(wv[e.value >> 2] >> (8 * (e.value & 3))) + 128;  // uint8
-            x[k] = (float)u - sZ[k];
+    const int n = img_n[I];
+    const int64_t row0 = img_row0[I];
+    for (int tile = blockIdx.x * kWaves + wave; tile * 16 < n; tile += gridDim.x * kWaves) {
+        const int r = min(tile * 16 + d, n - 1);
+        // this lane's A column: x[k] for k = 4s + j, s = 0..31
+        float x[32];
+        const int* src = reinterpret_cast<const int*>(desc + (row0 + r) * 128);
+        static_for<32>([&](auto sv) {
+            constexpr int sI = decltype(sv)::value;
+            const int wv = src[sI];   // bytes 4s .. 4s+3
+            const int u = (int)(int8_t)(wv >> (8 * j)) + 128;
+            x[sI] = (float)u - sZ[4 * sI + j];
         });
-    });
-
-    // four projection rows at a time: independent fma chains, k = 0..127 each
-    auto proj4 = [&](int p0, float* acc) {
-        acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
-        static_for<32>([&](auto k4) {
-            constexpr int k = 4 * decltype(k4)::value;
+        v4f acc[12];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 w = sP[(p0 + q) * 32 + k / 4];
-                acc[q] = __builtin_fmaf(w.x, x[k + 0], acc[q]);
-                acc[q] = __builtin_fmaf(w.y, x[k + 1], acc[q]);
-                acc[q] = __builtin_fmaf(w.z, x[k + 2], acc[q]);
-                acc[q] = __builtin_fmaf(w.w, x[k + 3], acc[q]);
+        for (int ct = 0; ct < 12; ++ct) acc[ct] = v4f{0.f, 0.f, 0.f, 0.f};
+        static_for<32>([&](auto sv) {
+            constexpr int sI = decltype(sv)::value;
+            const float* brow = sPt + (4 * sI + j) * kPtStride + d;
+            float bv[12];
+#pragma unroll
+            for (int ct = 0; ct < 12; ++ct) bv[ct] = brow[16 * ct];
+#pragma unroll
+            for (int ct = 0; ct < 12; ++ct)
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[sI], bv[ct], acc[ct], 0, 0, 0);
+            asm volatile("" ::: "memory");   // keep each k-step's 12 LDS reads beside its MFMAs
+        });
+        // acc[ct][q] = projection 16 ct + (lane & 15) of descriptor 4 (lane >> 4) + q;
+        // lane t < 16 collects descriptor t = 4 g + q from the 64-bit ballots
+        const int g = (lane >> 2) & 3, q = lane & 3, sh = 16 * g;
+        uint32_t cw[4] = {0, 0, 0, 0};
+        uint64_t sec = 0;
+#pragma unroll
+        for (int ct = 0; ct < 12; ++ct) {
+            uint32_t mine = 0;
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const uint64_t bl = __ballot(acc[ct][qq] > 0.f);
+                if (q == qq) mine = (uint32_t)(bl >> sh) & 0xffffu;
             }
-        });
-    };
-    uint32_t cw[4];
-#pragma unroll
-    for (int wd = 0; wd < 4; ++wd) {
-        uint32_t bits = 0;
-        for (int p = 0; p < 32; p += 4) {
-            float acc[4];
-            proj4(32 * wd + p, acc);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bits |= (uint32_t)(acc[q] > 0.f) << (p + q);
+            if (ct < 8) cw[ct >> 1] |= mine << (16 * (ct & 1));
+            else sec |= (uint64_t)mine << (16 * (ct - 8));
         }
-        cw[wd] = bits;
-    }
-    uint64_t sec = 0;  // bit s = sign of secondary row s (g * 10 + k)
-    for (int p = 0; p < kCascGroups * kCascBucketBits; p += 4) {
-        float acc[4];
-        proj4(kCascCode + p, acc);
+        if (lane < 16 && tile * 16 + lane < n) {
+            uint64_t b = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sec |= (uint64_t)(acc[q] > 0.f) << (p + q);
-    }
-    uint64_t b = 0;   // bucket id of group g in bits [10g, 10g + 10)
+            for (int gg = 0; gg < kCascGroups; ++gg) {
+                uint32_t id = 0;
 #pragma unroll
-    for (int g = 0; g < kCascGroups; ++g) {
-        uint32_t id = 0;
-#pragma unroll
-        for (int k = 0; k < kCascBucketBits; ++k)
-            id = (id << 1) | (uint32_t)((sec >> (g * kCascBucketBits + k)) & 1);
-        b |= (uint64_t)id << (kCascBucketBits * g);
+                for (int k = 0; k < kCascBucketBits; ++k)
+                    id = (id << 1) | (uint32_t)((sec >> (gg * kCascBucketBits + k)) & 1);
+                b |= (uint64_t)id << (kCascBucketBits * gg);
+            }
+            const int64_t row = row0 + tile * 16 + lane;
+            reinterpret_cast<uint4*>(code)[row] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+            bkt[row] = b;
+        }
     }
-    reinterpret_cast<uint4*>(code)[row] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-    bkt[row] = b;
 }
 
 // One wave per (image, group): counting sort of the image's descriptors by
@@ -473,17 +491,23 @@ void casc_colsum(const CascTables& t, int n_img, int64_t* colsum, hipStream_t s)
 void casc_hash(const CascTables& t, const float* proj, const float* zm, const int32_t* img, int n,
                int max_n, hipStream_t s) {
     if (n == 0 || max_n == 0) return;
-    const size_t lds = (size_t)kCascProjRows * kCascCode * sizeof(float);
-    static bool attr = false;
-    if (!attr) {
-        SFM_HIP(hipFuncSetAttribute((const void*)casc_hash_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = true;
-    }
     SFM_REQUIRE(n <= 65535, SFM_ERR_UNSUPPORTED, "cascade hashing over %d images", n);
-    hipLaunchKernelGGL(casc_hash_kernel, dim3((max_n + kHashThreads - 1) / kHashThreads, n),
-                       dim3(kHashThreads), lds, s, t.desc, t.img_row0, t.img_n, img, proj, zm,
-                       t.code, t.bkt);
+    {
+        const size_t mlds = (size_t)kCascCode * kPtStride * sizeof(float);
+        static bool mattr = false;
+        if (!mattr) {
+            SFM_HIP(hipFuncSetAttribute((const void*)casc_hash_mfma_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds));
+            mattr = true;
+        }
+        // every workgroup stages the 106 KB projection image once: enough
+        // workgroups to fill the chip (~1024), not one per 8 tiles
+        const int tiles = (max_n + 15) / 16;
+        const int per_wg = kHashMThreads / 64;
+        const int gx = std::max(1, std::min((tiles + per_wg - 1) / per_wg, std::max(1, 1024 / n)));
+        hipLaunchKernelGGL(casc_hash_mfma_kernel, dim3(gx, n), dim3(kHashMThreads), mlds, s, t.desc,
+                           t.img_row0, t.img_n, img, proj, zm, t.code, t.bkt);
+    }
     SFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(casc_bucket_kernel, dim3(kCascGroups, n), dim3(64), 0, s, t.bkt, t.img_row0,
                        t.img_n, img, t.rows, t.boff, t.blist);
