@@ -81,17 +81,17 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s);
 // U blocks, cost and non-finite flag at (cp, intr, X); scaled with scaleF.
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                    hipStream_t s);
-// Jacobi scaling at iteration 0: scaleE from per-point column norms,
-// scaleF from the reduced cnF (must run after ba_reduce of an unscaled pass).
-void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
-                    hipStream_t s);
+// Jacobi scaling at iteration 0: scaleF from the reduced cnF (after ba_reduce
+// of an unscaled pass); scaleE comes from ba_schur(..., scale_e = true).
 void ba_fscale(const DevProblem& P, hipStream_t s);
 // U / Ub / Ucn of a unit-scale ba_image_gram pass -> the same pass at scaleF
 void ba_gram_rescale(const DevProblem& P, hipStream_t s);
 void ba_fill(double* p, int64_t n, double v, hipStream_t s);
 // stamps (diagnostic builds only, else nullptr): per chunk 6 phase cycle sums
+// scale_e: also form the Jacobi point scales (scaleE) in this pass (the
+// solve's first pass, replacing ba_point_scale)
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
-              double radius, hipStream_t s, unsigned long long* stamps = nullptr);
+              double radius, hipStream_t s, unsigned long long* stamps = nullptr, bool scale_e = false);
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s);
 void ba_solve(const DevProblem& P, double radius, hipStream_t s);
 // candidate cameras/intrinsics and their CamPre; F-part norm/gradient partials

@@ -461,44 +461,6 @@ __global__ __launch_bounds__(128) void gram_rescale_kernel(DevProblem P) {
     }
 }
 
-// Jacobi scale of the point columns (iteration 0): 1 / (1 + |J col|).
-// One workgroup per Schur chunk, one thread per point, the chunk's cameras and
-// intrinsics staged in LDS (gathering each observation's CamPre from global
-// memory made this pass latency bound: 111 us at C4).
-template <int CM>
-__global__ __launch_bounds__(kChunkPts) void point_scale_kernel(DevProblem P, const CamPre* __restrict__ cps,
-                                                                const double* __restrict__ intr,
-                                                                const double* __restrict__ X) {
-    __shared__ CamPre scp[kCamSlots];
-    __shared__ double sin_[kIntrSlots][4];
-    const ChunkDesc& cd = P.chunks[blockIdx.x];
-    const int tid = threadIdx.x;
-    constexpr int kCpW = sizeof(CamPre) / 8;
-    for (int e = tid; e < cd.n_cams * kCpW; e += blockDim.x) {
-        const int t = e / kCpW;
-        reinterpret_cast<double*>(&scp[t])[e - t * kCpW] =
-            reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
-    }
-    if (tid < 4 * cd.n_intr) sin_[tid >> 2][tid & 3] = intr[4 * cd.intr_id[tid >> 2] + (tid & 3)];
-    __syncthreads();
-    const int p = cd.pt_begin + tid;
-    if (p >= cd.pt_end) return;
-    const double Xp[3] = {X[3 * (size_t)p], X[3 * (size_t)p + 1], X[3 * (size_t)p + 2]};
-    double cn[3] = {0, 0, 0};
-    for (int o = P.pt_off[p]; o < P.pt_off[p + 1]; ++o) {
-        const int slot = P.obs_slot[o];
-        const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-        Lin L;
-        linearize<CM, false, false, true>(scp[slot & 255], sin_[(slot >> 8) & 255], Xp, uv.x, uv.y, P.huber_a, L);
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int a = 0; a < 3; ++a) cn[a] += L.Jx[r][a] * L.Jx[r][a];
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) P.scaleE[3 * (size_t)p + a] = 1.0 / (1.0 + sqrt(cn[a]));
-}
-
 __global__ void fill_kernel(double* p, int64_t n, double v) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
@@ -574,7 +536,10 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 // NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
 // SP / SO: points / observations per wave batch.  The panel holds 3 columns
 // per point padded to the MFMA k of 4 and NT*16 rows (NT = 4 keeps w apart).
-template <int CM, int NT, int SP = kSubPts, int SO = kSubObs>
+// SE: the solve's first pass also forms the Jacobi point scales (what
+// point_scale_kernel computes) from the unscaled Jx it linearises anyway,
+// writes them to scaleE and uses them, instead of a separate pass.
+template <int CM, int NT, int SP = kSubPts, int SO = kSubObs, bool SE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
@@ -671,7 +636,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         const int o0 = cpoff[p0], nobs = cpoff[p1] - o0;
         const int slot = nx.slot, pl = nx.pl;
         const double u0 = nx.u0, u1 = nx.u1;
-        const double Xp[3] = {nx.Xp[0], nx.Xp[1], nx.Xp[2]}, sE[3] = {nx.sE[0], nx.sE[1], nx.sE[2]};
+        const double Xp[3] = {nx.Xp[0], nx.Xp[1], nx.Xp[2]};
+        double sE[3] = {nx.sE[0], nx.sE[1], nx.sE[2]};
         fetch(p1, nx);
 #pragma unroll
         for (int e = lane; e < kPK * kPS / 2; e += 64)
@@ -681,8 +647,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         // ---- A: observations -> scaled, corrected Jacobians -----------------
         Lin L;
         const int cs = slot & 255, is = (slot >> 8) & 255;
+        if (lane < nobs) linearize<CM, true, true, true>(scp[cs].cp, &isc[is][0], Xp, u0, u1, P.huber_a, L);
+        if constexpr (SE) {
+            // column norms of the point's unscaled Jx, in observation and row
+            // order (as point_scale_kernel): raw Jx staged in obm (free until B)
+            if (lane < nobs) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) obm[lane][3 * r + a] = L.Jx[r][a];
+            }
+            __syncthreads();
+            if (lane < 3 * npts) {
+                const int pt = lane / 3, a = lane - 3 * pt;
+                const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
+                double cn = 0.0;
+                for (int q = q0; q < q1; ++q) {
+                    cn = fma(obm[q][a], obm[q][a], cn);
+                    cn = fma(obm[q][3 + a], obm[q][3 + a], cn);
+                }
+                const double se = 1.0 / (1.0 + sqrt(cn));
+                vsum[pt][a] = se;   // vsum is rewritten after phase A
+                P.scaleE[3 * (size_t)(pb + p0 + pt) + a] = se;
+            }
+            __syncthreads();
+            if (lane < nobs) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) sE[a] = vsum[pl][a];
+            }
+            __syncthreads();   // vsum is reused by the per-point sums below
+        }
         if (lane < nobs) {
-            linearize<CM, true, true, true>(scp[cs].cp, &isc[is][0], Xp, u0, u1, P.huber_a, L);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
 #pragma unroll
@@ -1554,13 +1549,6 @@ void ba_gram_rescale(const DevProblem& P, hipStream_t s) {
     SFM_HIP(hipGetLastError());
 }
 
-void ba_point_scale(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
-                    hipStream_t s) {
-    if (P.n_spt <= 0) return;
-    SFM_BY_MODEL(P, hipLaunchKernelGGL(point_scale_kernel<CM>, dim3(P.n_chunk), dim3(kChunkPts), 0, s, P, cp,
-                                       intr, X));
-    SFM_HIP(hipGetLastError());
-}
 
 void ba_fill(double* p, int64_t n, double v, hipStream_t s) {
     if (n <= 0) return;
@@ -1575,16 +1563,25 @@ void ba_fscale(const DevProblem& P, hipStream_t s) {
 }
 
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
-              hipStream_t s, unsigned long long* stamps) {
+              hipStream_t s, unsigned long long* stamps, bool scale_e) {
     if (P.n_chunk <= 0) return;
     // 64-row tiles: 4-point batches (12 panel columns, no k padding) keep LDS
     // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
-    if (P.tile_nt == 4)
-        SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>), dim3(P.n_chunk),
-                                           dim3(64), 0, s, P, cp, intr, X, radius, stamps));
-    else
-        SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5>), dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X,
-                                           radius, stamps));
+    if (P.tile_nt == 4) {
+        if (scale_e)
+            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO, true>),
+                                               dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+        else
+            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>),
+                                               dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+    } else {
+        if (scale_e)
+            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, kSubPts, kSubObs, true>), dim3(P.n_chunk),
+                                               dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+        else
+            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5>), dim3(P.n_chunk), dim3(64), 0, s, P, cp,
+                                               intr, X, radius, stamps));
+    }
     SFM_HIP(hipGetLastError());
 }
 

@@ -322,8 +322,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         ba_reduce(P, true, s);
         allreduce_rcs();
         ba_fscale(P, s);
-        ba_point_scale(P, S.cp, S.in, S.X, s);
         ba_gram_rescale(P, s);         // = relinearize() at the new scales
+        // the point scales come from the first Schur pass (schur_kernel<SE>)
     } else {
         relinearize();
     }
@@ -355,11 +355,14 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     int step_no = 0;
     while (term < 0) {
         // ---- one step on the device ------------------------------------------
-        // the Schur launch is timed with events on the first two steps of each
+        // the Schur launch is timed with events on the second and third steps of each
         // solve only: an event pair costs ~12 us of stream serialisation
-        const bool timed = step_no++ < 2;
+        // (the first pass, which also forms the point scales, is not timed)
+        const bool first = step_no == 0;
+        const bool timed = step_no == 1 || step_no == 2;
+        ++step_no;
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i], s));
-        ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p);
+        ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
         ba_reduce(P, false, s);
         allreduce_rcs();
