@@ -108,18 +108,18 @@ __device__ __forceinline__ v4d zero4() { return v4d{0.0, 0.0, 0.0, 0.0}; }
 
 // global [R][ld_src] -> LDS [R][ld_dst], first NC columns: every thread
 // issues all its 16-byte loads before the first LDS store
-template <int NC, int R = M>
+template <int NC, int R = M, int TH = NT>
 __device__ __forceinline__ void load_tile(double* dst, int ld_dst, const double* __restrict__ src, int ld_src) {
-    constexpr int n2 = R * NC / 2, per = (n2 + NT - 1) / NT;
+    constexpr int n2 = R * NC / 2, per = (n2 + TH - 1) / TH;
     double2 v[per];
 #pragma unroll
     for (int q = 0; q < per; ++q) {
-        const int e = threadIdx.x + q * NT;
+        const int e = threadIdx.x + q * TH;
         if (e < n2) v[q] = *reinterpret_cast<const double2*>(src + (e / (NC / 2)) * ld_src + 2 * (e % (NC / 2)));
     }
 #pragma unroll
     for (int q = 0; q < per; ++q) {
-        const int e = threadIdx.x + q * NT;
+        const int e = threadIdx.x + q * TH;
         if (e < n2) {
             double* d = dst + (e / (NC / 2)) * ld_dst + 2 * (e % (NC / 2));
             d[0] = v[q].x;
@@ -127,10 +127,11 @@ __device__ __forceinline__ void load_tile(double* dst, int ld_dst, const double*
         }
     }
 }
+template <int TH = NT>
 __device__ __forceinline__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src, int nc) {
-    if (nc == 64) load_tile<64>(dst, ld_dst, src, ld_src);
-    else if (nc == 32) load_tile<32>(dst, ld_dst, src, ld_src);
-    else load_tile<16>(dst, ld_dst, src, ld_src);
+    if (nc == 64) load_tile<64, M, TH>(dst, ld_dst, src, ld_src);
+    else if (nc == 32) load_tile<32, M, TH>(dst, ld_dst, src, ld_src);
+    else load_tile<16, M, TH>(dst, ld_dst, src, ld_src);
 }
 
 // value of v in lane l of this lane's 16-lane row (DPP row_newbcast, 64-bit);
@@ -239,6 +240,7 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
 //   D(k+1) wave 0: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}', then diag16(k+1);
 //          waves 1..3 meanwhile: the other trailing tiles of step k and the
 //          partial inverse rows T_{k+1,j} = sum_{m=j..k} L_{k+1,m} X_mj
+template <int NW = NT / 64>
 __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
                            unsigned long long* st = nullptr) {
     const int wave = threadIdx.x >> 6;
@@ -281,14 +283,14 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
             for (int i = n; i < 4; ++i)
                 for (int j = n; j <= i; ++j) {
                     if (i == n && j == n) continue;
-                    if (t++ % 3 == wave - 1) {
+                    if (t++ % (NW - 1) == wave - 1) {
                         v4d acc = tile_ld(A, LD, 16 * i, 16 * j);
                         acc = tile_mm<false, true, true>(acc, A, LD, 16 * i, A, LD, 16 * j, 16 * k, 16 * k + 16);
                         tile_st(A, LD, 16 * i, 16 * j, acc);
                     }
                 }
             for (int j = 0; j < n; ++j)
-                if (t++ % 3 == wave - 1)   // X is lower triangular: m runs j..n-1
+                if (t++ % (NW - 1) == wave - 1)   // X is lower triangular: m runs j..n-1
                     tile_st(X, LD, 16 * n, 16 * j,
                             tile_mm<false, false, false>(zero4(), A, LD, 16 * n, X, LD, 16 * j, 16 * j, 16 * n));
         }
@@ -364,6 +366,7 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
 // neighbours at stride s (they hold Wl = L^-1 C, Wr = L^-1 C_r', z = L^-1 R):
 // A_j -= Wr_{j-s}' Wr_{j-s} + Wl_{j+s}' Wl_{j+s};  R_j -= Wr' z + Wl' z;
 // new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}.  Wave v: tile (w, v).
+template <int TH>
 __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* sm) {
     const int ldr = b.nrhs + 1;
     double* Wa = sm;               // Wr_{j-s}
@@ -371,24 +374,26 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
     double* Wc = Wb + M * LD;      // Wl_{j-s}
     double* Za = Wc + M * LD;      // z_{j-s}
     double* Zb = Za + M * ldr;     // z_{j+s}
-    const int il = j - s, ir = j + s, v = threadIdx.x >> 6;
+    // waves 0..3: A tile (w, v); waves 4..7: R and C tiles (w, v - 4)
+    const int il = j - s, ir = j + s, wv = threadIdx.x >> 6, v = wv & 3;
     const bool hl = il >= 0, hr = ir < b.N, hc = hl && j - 2 * s >= 0;
     if (hl) {
-        load_rows(Wa, LD, b.Wr + (size_t)il * M * M, M, M);
-        load_rows(Za, ldr, b.Z + (size_t)il * M * b.nrhs, b.nrhs, b.nrhs);
+        load_rows<TH>(Wa, LD, b.Wr + (size_t)il * M * M, M, M);
+        load_rows<TH>(Za, ldr, b.Z + (size_t)il * M * b.nrhs, b.nrhs, b.nrhs);
     }
     if (hr) {
-        load_rows(Wb, LD, b.Wl + (size_t)ir * M * M, M, M);
-        load_rows(Zb, ldr, b.Z + (size_t)ir * M * b.nrhs, b.nrhs, b.nrhs);
+        load_rows<TH>(Wb, LD, b.Wl + (size_t)ir * M * M, M, M);
+        load_rows<TH>(Zb, ldr, b.Z + (size_t)ir * M * b.nrhs, b.nrhs, b.nrhs);
     }
-    if (hc) load_rows(Wc, LD, b.Wl + (size_t)il * M * M, M, M);
+    if (hc) load_rows<TH>(Wc, LD, b.Wl + (size_t)il * M * M, M, M);
     __syncthreads();
     double* Aj = b.A + (size_t)j * M * M;
-    {
+    if (wv < 4) {
         v4d acc = tile_ld(Aj, M, 16 * w, 16 * v);
         if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * w, Wa, LD, 16 * v, 0, M);
         if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * w, Wb, LD, 16 * v, 0, M);
         tile_st(Aj, M, 16 * w, 16 * v, acc);
+        return;
     }
     if (16 * v < b.nrhs) {
         double* Rj = b.R + (size_t)j * M * b.nrhs;
@@ -412,12 +417,14 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
 //     Wl = X C_i, Wr = X C_r', z = X R_i.
 //   even block j (items >= n_odd, s > 1): update(s/2) of its row tile w, stored.
 // At s = 1 the inputs come straight from bcr_pack.
-__global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_odd) {
+constexpr int NTL = 512, NWL = NTL / 64;   // level kernel: 8 waves
+
+__global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_odd) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int item = blockIdx.x >> 2, w = blockIdx.x & 3, sp = s >> 1;
     if (item >= n_odd) {
         const int j = 2 * s * (item - n_odd);
-        if (sp > 0 && j < b.N) update_tile_rows(b, sp, j, w, sm);
+        if (sp > 0 && j < b.N) update_tile_rows<NTL>(b, sp, j, w, sm);
         return;
     }
     const int i = s + 2 * s * item;
@@ -438,10 +445,10 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
     unsigned long long t0 = 0, t1 = 0;
     if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
-    load_rows(A, LD, b.A + (size_t)i * M * M, M, M);
-    load_rows(Cc, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
-    if (hr) load_tile<64, 16>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
-    if (hz) load_rows(Rc, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
+    load_rows<NTL>(A, LD, b.A + (size_t)i * M * M, M, M);
+    load_rows<NTL>(Cc, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
+    if (hr) load_tile<64, 16, NTL>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
+    if (hz) load_rows<NTL>(Rc, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
     if (sp > 0) {
         // neighbours eliminated at stride sp: i-sp (always there) and i+sp
         const int il = i - sp, ir = i + sp;
@@ -452,19 +459,19 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
         double* Z2 = Z1 + M * 16;
         double* WL = Z2 + M * 16;
         double* WR = WL + M * 16;
-        load_tile<64, 64>(Wa, M, b.Wr + (size_t)il * M * M, M);
-        load_tile<16>(WL, 16, b.Wl + (size_t)il * M * M + 16 * w, M);
-        if (hz) load_tile<16>(Z1, 16, b.Z + (size_t)il * M * b.nrhs + 16 * w, b.nrhs);
+        load_tile<64, 64, NTL>(Wa, M, b.Wr + (size_t)il * M * M, M);
+        load_tile<16, M, NTL>(WL, 16, b.Wl + (size_t)il * M * M + 16 * w, M);
+        if (hz) load_tile<16, M, NTL>(Z1, 16, b.Z + (size_t)il * M * b.nrhs + 16 * w, b.nrhs);
         if (hir) {
-            load_tile<64, 64>(Wb, M, b.Wl + (size_t)ir * M * M, M);
-            if (hz) load_tile<16>(Z2, 16, b.Z + (size_t)ir * M * b.nrhs + 16 * w, b.nrhs);
-            if (hr) load_tile<16>(WR, 16, b.Wr + (size_t)ir * M * M + 16 * w, M);
+            load_tile<64, 64, NTL>(Wb, M, b.Wl + (size_t)ir * M * M, M);
+            if (hz) load_tile<16, M, NTL>(Z2, 16, b.Z + (size_t)ir * M * b.nrhs + 16 * w, b.nrhs);
+            if (hr) load_tile<16, M, NTL>(WR, 16, b.Wr + (size_t)ir * M * M + 16 * w, M);
         }
         __syncthreads();
         if (st && threadIdx.x == 0) atomicAdd(st + 5, stamp() - t0);   // loads
         // A_i -= Wa' Wa + Wb' Wb on the 10 lower tiles (the factorisation reads
         // nothing above the diagonal): wave v takes tiles v, v+4, v+8
-        for (int q = wave; q < 10; q += 4) {
+        for (int q = wave; q < 10; q += NWL) {
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
@@ -472,25 +479,29 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
             if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * ti, Wb, M, 16 * tj, 0, M);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         }
-        // R_i[:, w] -= Wa' z_{i-sp}[:, w] + Wb' z_{i+sp}[:, w]
-        if (hz) {
-            v4d acc = tile_ld(Rc, L16, 16 * wave, 0);
-            acc = tile_mm<true, false, true>(acc, Wa, M, 16 * wave, Z1, 16, 0, 0, M);
-            if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * wave, Z2, 16, 0, 0, M);
-            tile_st(Rc, L16, 16 * wave, 0, acc);
+        const int v = wave & 3;   // row tile; waves 0..3: R_i and C_i, waves 4..7: C_r
+        if (wave < 4) {
+            // R_i[:, w] -= Wa' z_{i-sp}[:, w] + Wb' z_{i+sp}[:, w]
+            if (hz) {
+                v4d acc = tile_ld(Rc, L16, 16 * v, 0);
+                acc = tile_mm<true, false, true>(acc, Wa, M, 16 * v, Z1, 16, 0, 0, M);
+                if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * v, Z2, 16, 0, 0, M);
+                tile_st(Rc, L16, 16 * v, 0, acc);
+            }
+            // C_i[:, w] = -Wa' Wl_{i-sp}[:, w]   (block (i, i-2sp) = (i, i-s))
+            tile_st(Cc, L16, 16 * v, 0, tile_mm<true, false, true>(zero4(), Wa, M, 16 * v, WL, 16, 0, 0, M));
+        } else if (hr && hir) {
+            // C_r[w rows, :] = -(Wr_{i+sp}[:, w])' Wl_{i+sp}   (block (r, r-s) = (r, i))
+            tile_st(Cr, LD, 0, 16 * v, tile_mm<true, false, true>(zero4(), WR, 16, 0, Wb, M, 16 * v, 0, M));
         }
-        // C_i[:, w] = -Wa' Wl_{i-sp}[:, w]   (block (i, i-2sp) = (i, i-s))
-        tile_st(Cc, L16, 16 * wave, 0, tile_mm<true, false, true>(zero4(), Wa, M, 16 * wave, WL, 16, 0, 0, M));
-        // C_r[w rows, :] = -(Wr_{i+sp}[:, w])' Wl_{i+sp}   (block (r, r-s) = (r, i))
-        if (hr && hir) tile_st(Cr, LD, 0, 16 * wave, tile_mm<true, false, true>(zero4(), WR, 16, 0, Wb, M, 16 * wave, 0, M));
     }
     __syncthreads();
     if (st) t1 = stamp();
-    chol_inv64(A, X, bad, col, st);
+    chol_inv64<NWL>(A, X, bad, col, st);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     {   // X for the back substitution: each of the block's 4 workgroups stores 16 rows
         double* Xg = b.L + (size_t)i * M * M + 16 * w * M;
-        for (int e = threadIdx.x; e < 16 * M; e += NT) Xg[e] = X[(16 * w + e / M) * LD + e % M];
+        for (int e = threadIdx.x; e < 16 * M; e += NTL) Xg[e] = X[(16 * w + e / M) * LD + e % M];
     }
     if (st) {
         __syncthreads();
@@ -498,12 +509,11 @@ __global__ __launch_bounds__(NT) void bcr_level_kernel(BcrArgs b, int s, int n_o
     }
     // column tile w of Wl = X C_i, Wr = X C_r', z = X R_i: product p of row
     // tile r costs r + 1 k-chunks (X is lower triangular); the 12 (p, r) items
-    // are split 8 / 8 / 8 / 6 chunks over the waves instead of 12 for row 3
-    constexpr int8_t kItems[4][4][2] = {{{0, 3}, {1, 3}, {-1, 0}, {-1, 0}},
-                                        {{2, 3}, {0, 2}, {0, 0}, {-1, 0}},
-                                        {{1, 2}, {2, 2}, {1, 1}, {-1, 0}},
-                                        {{0, 1}, {2, 1}, {1, 0}, {2, 0}}};
-    for (int q = 0; q < 4; ++q) {
+    // (30 chunks) are split at most 4 chunks per wave over the 8 waves
+    constexpr int8_t kItems[NWL][2][2] = {{{0, 3}, {-1, 0}}, {{1, 3}, {-1, 0}}, {{2, 3}, {-1, 0}},
+                                          {{0, 2}, {0, 0}},  {{1, 2}, {1, 0}},  {{2, 2}, {2, 0}},
+                                          {{0, 1}, {1, 1}},  {{2, 1}, {-1, 0}}};
+    for (int q = 0; q < 2; ++q) {
         const int pr = kItems[wave][q][0], r = kItems[wave][q][1], kend = 16 * (r + 1);
         if (pr < 0) break;
         if (pr == 0)
@@ -758,7 +768,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     for (int stride = 1; stride < b.N; stride *= 2) {
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
         const int n_even = stride > 1 ? (b.N + 2 * stride - 1) / (2 * stride) : 0;
-        hipLaunchKernelGGL(bcr_level_kernel, dim3(4 * (n_odd + n_even)), dim3(NT), lds_l, s, b, stride, n_odd);
+        hipLaunchKernelGGL(bcr_level_kernel, dim3(4 * (n_odd + n_even)), dim3(NTL), lds_l, s, b, stride, n_odd);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
