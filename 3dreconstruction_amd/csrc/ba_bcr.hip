@@ -539,7 +539,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
 // ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------
 // sp > 0: first block 0's update from its right neighbour sp, eliminated by
 // the last level (A_0 -= Wl_sp' Wl_sp, R_0 -= Wl_sp' z_sp; lower tiles only).
-__global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b, int sp) {
+__global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int ldr = b.nrhs + 1;
     double* A = sm;
@@ -553,38 +553,44 @@ __global__ __launch_bounds__(NT) void bcr_top_kernel(BcrArgs b, int sp) {
     const int wave = threadIdx.x >> 6;
     const bool upd = sp > 0 && sp < b.N;
     if (threadIdx.x == 0) bad[0] = 0.0;
-    load_rows(A, LD, b.A, M, M);
-    load_rows(R, ldr, b.R, b.nrhs, b.nrhs);
+    load_rows<NTL>(A, LD, b.A, M, M);
+    load_rows<NTL>(R, ldr, b.R, b.nrhs, b.nrhs);
     if (upd) {
-        load_rows(Wb, LD, b.Wl + (size_t)sp * M * M, M, M);
-        load_rows(Zb, ldr, b.Z + (size_t)sp * M * b.nrhs, b.nrhs, b.nrhs);
+        load_rows<NTL>(Wb, LD, b.Wl + (size_t)sp * M * M, M, M);
+        load_rows<NTL>(Zb, ldr, b.Z + (size_t)sp * M * b.nrhs, b.nrhs, b.nrhs);
     }
-    for (int e = threadIdx.x; e < M * LD; e += NT) X[e] = 0.0;
+    for (int e = threadIdx.x; e < M * LD; e += NTL) X[e] = 0.0;
     __syncthreads();
     if (upd) {
-        for (int q = wave; q < 10; q += 4) {
+        // 8 waves: the 10 lower A tiles, and the R rows on waves 4..7
+        for (int q = wave; q < 10; q += NWL) {
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
             acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, M);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         }
-        for (int tj = 0; tj < b.nrhs / 16; ++tj) {
-            v4d acc = tile_ld(R, ldr, 16 * wave, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * wave, Zb, ldr, 16 * tj, 0, M);
-            tile_st(R, ldr, 16 * wave, 16 * tj, acc);
+        if (wave >= 4) {
+            const int v = wave - 4;
+            for (int tj = 0; tj < b.nrhs / 16; ++tj) {
+                v4d acc = tile_ld(R, ldr, 16 * v, 16 * tj);
+                acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, M);
+                tile_st(R, ldr, 16 * v, 16 * tj, acc);
+            }
         }
         __syncthreads();
     }
-    chol_inv64(A, X, bad, sc);
+    chol_inv64<NWL>(A, X, bad, sc);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj)
-        tile_st(T, ldr, 16 * wave, 16 * tj,
-                tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
+    if (wave < 4)
+        for (int tj = 0; tj < b.nrhs / 16; ++tj)
+            tile_st(T, ldr, 16 * wave, 16 * tj,
+                    tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
     __syncthreads();
-    for (int tj = 0; tj < b.nrhs / 16; ++tj)   // X' is upper triangular
-        tile_st(b.Y, b.nrhs, 16 * wave, 16 * tj,
-                tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
+    if (wave < 4)
+        for (int tj = 0; tj < b.nrhs / 16; ++tj)   // X' is upper triangular
+            tile_st(b.Y, b.nrhs, 16 * wave, 16 * tj,
+                    tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
 }
 
 // ---- back substitution at level l: y_i = X_i' (z_i - Wl y_l - Wr y_r) ----------
@@ -772,7 +778,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
-    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NT), lds_t, s, b, s_top / 2);
+    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NTL), lds_t, s, b, s_top / 2);
     SFM_HIP(hipGetLastError());
     for (int stride = s_top / 2; stride >= 1; stride /= 2) {
         if (stride >= b.N) continue;
