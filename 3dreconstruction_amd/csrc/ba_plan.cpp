@@ -277,8 +277,12 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 const int img = pl.obs_img[s];
                 slot_out[s] = dcam_idx[img] | (intr_idx[P.img_intr[img]] << 8);
             }
+            // algorithmic flops: the symmetric Z Z' over the
+            // point's own F rows (r(r+1)/2 entries x 3 x 2 = 3 r (r+1)), the
+            // linearisation (600 per observation) and the point block (V, its
+            // factor, M = Jx L^-T, Z = J' M: 180 per observation + 30)
             const int64_t nfp = own;
-            flops += 2LL * 3 * nfp * nfp + 600LL * nobs;   // Z Z' over the point's F rows + linearisation
+            flops += 3LL * nfp * (nfp + 1) + 780LL * nobs + 30;
         }
         if (pl.n_spt > 0) close((int32_t)pl.n_spt);
         return flops;

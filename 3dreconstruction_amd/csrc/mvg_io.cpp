@@ -484,21 +484,40 @@ MatchSet load_matches(const char* path) {
     return m;
 }
 
-// IndMatchDecorator<float>::getDeduplicated restated: matches whose keypoint
-// coordinates (xI, yI, xJ, yJ) coincide with an earlier match's are dropped
-// (SIFT emits up to 4 orientations per keypoint); the survivors keep their
-// (i, j) order.  OpenMVG's own set ordering is not pinned.
+// IndMatchDecorator<float>::getDeduplicated (openMVG matching/
+// indMatchDecoratorXY.hpp, un-vendored: SURVEY §8c) restated: every match is
+// decorated with its keypoint coordinates (xI, yI, xJ, yJ) and the decorated
+// list -- in (i, j) order, as IndMatch::getDeduplicated leaves it -- is copied
+// into a std::set ordered by the decorator's operator<, whose iteration order
+// is the output.  That comparator is not a strict weak order (x1 only picks
+// which branch compares y1), so the survivors and their order are those of
+// libstdc++'s set built from the range: the same container, comparator and
+// insertion sequence as the reference's build, hence the same tree walk.
+struct DecoratedMatch {
+    float x1, y1, x2, y2;
+    uint32_t i, j;
+};
+struct DecoratorLess {
+    static bool same(const DecoratedMatch& a, const DecoratedMatch& b) {
+        return a.x1 == b.x1 && a.y1 == b.y1 && a.x2 == b.x2 && a.y2 == b.y2;
+    }
+    bool operator()(const DecoratedMatch& a, const DecoratedMatch& b) const {
+        if (same(a, b)) return false;
+        if (a.x1 < b.x1) return a.y1 < b.y1;
+        if (a.x1 > b.x1) return a.y1 < b.y1;
+        return a.x2 < b.x2 && a.y2 < b.y2;
+    }
+};
 void dedup_xy(std::vector<std::pair<uint32_t, uint32_t>>& v, const std::vector<float>& fi,
               const std::vector<float>& fj) {
-    std::set<std::array<float, 4>> seen;
-    size_t w = 0;
-    for (size_t k = 0; k < v.size(); ++k) {
-        const uint32_t a = v[k].first, b = v[k].second;
-        const std::array<float, 4> key{fi[4 * (size_t)a], fi[4 * (size_t)a + 1], fj[4 * (size_t)b],
-                                       fj[4 * (size_t)b + 1]};
-        if (seen.insert(key).second) v[w++] = v[k];
-    }
-    v.resize(w);
+    std::vector<DecoratedMatch> dec;
+    dec.reserve(v.size());
+    for (const auto& m : v)
+        dec.push_back(DecoratedMatch{fi[4 * (size_t)m.first], fi[4 * (size_t)m.first + 1], fj[4 * (size_t)m.second],
+                                     fj[4 * (size_t)m.second + 1], m.first, m.second});
+    const std::set<DecoratedMatch, DecoratorLess> uniq(dec.begin(), dec.end());
+    v.clear();
+    for (const auto& d : uniq) v.emplace_back(d.i, d.j);
 }
 
 }  // namespace
@@ -722,12 +741,9 @@ extern "C" int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm
         }
         std::set<std::pair<uint32_t, uint32_t>> pairs;
         const std::string pf = filespec(dir, "pairs.bin");
-        if (is_file(pf)) {
-            pairs = load_pairs(pf.c_str(), (int64_t)views.size());
-        } else {
-            for (uint32_t a = 0; a < views.size(); ++a)
-                for (uint32_t b = a + 1; b < views.size(); ++b) pairs.insert({a, b});
-        }
+        // loadPairs(pairs.bin) failing is an error in the reference (:957-960)
+        SFM_REQUIRE(is_file(pf), SFM_ERR_INVALID_ARG, "%s: no pairs file (run matchPair first)", pf.c_str());
+        pairs = load_pairs(pf.c_str(), (int64_t)views.size());
         st.n_views = (int64_t)views.size();
         st.n_pairs_in = (int64_t)pairs.size();
         // pairs whose views have no regions are skipped by Matcher_Regions

@@ -180,6 +180,10 @@ class BundleAdjuster {
     struct Options {
         bool fixed_writeback = false;  // false: reproduce Image::setIntrinsic's ZYX-Euler quirk
         bool verbose = true;           // print the reference's statistics block
+        // A solve that could not run at all (bad input, device, RCCL) is not
+        // the reference's "solution not usable" outcome: it is always reported
+        // on stderr with sfm_last_error(), and thrown as sfm::Error when set.
+        bool throw_on_error = false;
         sfm_ba_options solver{};
         Options() { sfm_ba_default_options(&solver); }
     };
@@ -192,6 +196,7 @@ class BundleAdjuster {
         clear();
     }
     const sfm_ba_summary& summary() const { return summary_; }
+    int lastError() const { return last_rc_; }   // SFM_OK or the last sfm_ba_solve code
 
    private:
     // loadDataFromWorld (:82-98) + problem assembly (:100-123)
@@ -259,7 +264,13 @@ class BundleAdjuster {
         pr.huber_a = 4.0;
         if (pr.n_img == 0 || pr.n_intr == 0) return false;
         const int rc = sfm_ba_solve(ctx_->get(), &pr, extr_.data(), intr_.data(), X_.data(), &opt_.solver, &summary_);
-        if (rc != SFM_OK || !summary_.usable) {
+        last_rc_ = rc;
+        if (rc != SFM_OK && rc != SFM_ERR_SOLVER && rc != SFM_ERR_NOT_FINITE) {
+            std::fprintf(stderr, "Bundle Adjustment failed: %s (code %d)\n", sfm_last_error(), rc);
+            if (opt_.throw_on_error) throw Error(rc, "sfm_ba_solve");
+            return false;
+        }
+        if (rc != SFM_OK || !summary_.usable) {   // !IsSolutionUsable (:128-131)
             if (opt_.verbose) std::printf("Bundle Adjustment failed.\n");
             return false;
         }
@@ -297,6 +308,7 @@ class BundleAdjuster {
     std::vector<double> extr_, intr_, X_, uv_;
     std::vector<int64_t> off_;
     int32_t const_img_ = -1;
+    int last_rc_ = SFM_OK;
     sfm_ba_summary summary_{};
 };
 

@@ -80,35 +80,73 @@ def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0):
     return sc
 
 
-def cpu_baseline_ba(sc, iters=2, threads=1):
-    """Oracle (CPU restatement) on the same C4 scene, first `iters` LM iterations."""
+def host_cpu():
+    """CPU model and the thread budget of this process (OMP_NUM_THREADS on the
+    GPU box is this GPU's share of the host)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return model, max(1, min(n, 64))
+
+
+def cpu_baseline_ba(sc):
+    """Oracle (CPU restatement of the reference Ceres semantics) on the same C4
+    scene: a full solve to termination on all of this process's host threads
+    (value), and the first LM iterations on one thread, as the reference runs
+    Ceres (num_threads = 1, BundleAdjuster.h:170)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _helpers as H  # test infrastructure: the oracle is only the baseline here
     lib = H.oracle()
-    o = abi.default_options()
-    o.max_num_iterations = iters
-    e, i, x = sc["extr"].copy(), sc["intr"].copy(), sc["X"].copy()
-    s = abi.BASummary()
-    tr = (abi.BAIter * 8)()
-    tn = C.c_int32()
-    t = time.time()
-    lib.orc_ba_solve(C.byref(sc["problem"]), abi.ptr(e, abi.f64p), abi.ptr(i, abi.f64p),
-                     abi.ptr(x, abi.f64p), C.byref(o), C.byref(s), tr, 8, C.byref(tn), None, 0,
-                     H.ALLREDUCE_FN(), None, threads)
-    dt = time.time() - t
-    return {"value": s.iterations / dt, "unit": "LM-iters/s", "cores": threads, "kind": "port",
-            "sample": f"C4 scene (1000 cams/500k pts/5M obs), first {s.iterations} LM iterations "
-                      f"incl. iteration-0 linearisation and Jacobi scaling, {dt:.1f} s wall; "
-                      "oracle = CPU restatement of the reference Ceres semantics, not Ceres itself",
-            "obs_per_sec": s.iterations * sc["n_obs"] / dt}
+    model, threads = host_cpu()
+
+    def solve(max_iters, nthreads):
+        o = abi.default_options()
+        o.max_num_iterations = max_iters
+        e, i, x = sc["extr"].copy(), sc["intr"].copy(), sc["X"].copy()
+        s = abi.BASummary()
+        tr = (abi.BAIter * 64)()
+        tn = C.c_int32()
+        t = time.time()
+        lib.orc_ba_solve(C.byref(sc["problem"]), abi.ptr(e, abi.f64p), abi.ptr(i, abi.f64p),
+                         abi.ptr(x, abi.f64p), C.byref(o), C.byref(s), tr, 64, C.byref(tn), None, 0,
+                         H.ALLREDUCE_FN(), None, nthreads)
+        return s, time.time() - t
+
+    s_all, dt_all = solve(50, threads)
+    s_one, dt_one = solve(2, 1)
+    return {"value": s_all.iterations / dt_all, "unit": "LM-iters/s", "cores": threads, "kind": "port",
+            "cpu_model": model,
+            "sample": f"C4 scene (1000 cams/500k pts/5M obs), full solve to termination "
+                      f"({s_all.iterations} LM iterations incl. iteration-0 linearisation and Jacobi "
+                      f"scaling) on {threads} threads, {dt_all:.1f} s wall; oracle = CPU restatement of the "
+                      "reference Ceres semantics, not Ceres itself",
+            "obs_per_sec": s_all.iterations * sc["n_obs"] / dt_all,
+            "rmse_final": s_all.rmse_final,
+            "single_thread": {"value": s_one.iterations / dt_one, "unit": "LM-iters/s", "cores": 1,
+                              "sample": f"first {s_one.iterations} LM iterations incl. iteration 0, "
+                                        f"{dt_one:.1f} s wall (Ceres num_threads = 1)"}}
 
 
-def cpu_baseline_match(desc, n_kp, pairs, n_pairs=24, threads=1):
+def cpu_baseline_match(desc, n_kp, pairs, n_pairs=96):
+    """The oracle (exact integer brute force) on pairs spread over the whole C3
+    list, on all of this process's host threads."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _helpers as H
     lib = H.oracle()
+    model, threads = host_cpu()
     off = np.arange(desc.shape[0] // n_kp + 1, dtype=np.int64) * n_kp
-    sub = np.ascontiguousarray(pairs[:n_pairs])
+    pick = np.linspace(0, len(pairs) - 1, n_pairs).astype(np.int64)
+    sub = np.ascontiguousarray(pairs[pick])
     counts = np.zeros(n_pairs, np.int64)
     t = time.time()
     lib.orc_match_pairs(abi.ptr(desc, abi.u8p), abi.ptr(off, abi.i64p), len(off) - 1,
@@ -116,15 +154,18 @@ def cpu_baseline_match(desc, n_kp, pairs, n_pairs=24, threads=1):
                         abi.ptr(counts, abi.i64p), None, None, None)
     dt = time.time() - t
     return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"first {n_pairs} pairs of C3, exact integer brute force, {dt:.1f} s wall"}
+            "cpu_model": model,
+            "sample": f"{n_pairs} pairs evenly spaced over the C3 list, exact integer brute force, "
+                      f"{dt:.1f} s wall"}
 
 
-def cpu_baseline_cascade(desc, n_kp, n_img=16, threads=1):
+def cpu_baseline_cascade(desc, n_kp, n_img=24):
     """The oracle on every pair among the first n_img images (hashing
     included, so the sample is hashing-heavier than the full list)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _helpers as H
     lib = H.oracle()
+    model, threads = host_cpu()
     off = np.arange(desc.shape[0] // n_kp + 1, dtype=np.int64) * n_kp
     sub = np.array([(i, j) for i in range(n_img) for j in range(i + 1, n_img)], np.int32)
     n_pairs = len(sub)
@@ -135,7 +176,7 @@ def cpu_baseline_cascade(desc, n_kp, n_img=16, threads=1):
                         abi.ptr(counts, abi.i64p), None, None, None)
     dt = time.time() - t
     n_used = len(np.unique(sub))
-    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+    return {"value": n_pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port", "cpu_model": model,
             "sample": f"all {n_pairs} pairs among the first {n_used} C3 images, incl. hashing "
                       f"them, cascade-hashing restatement, {dt:.1f} s wall"}
 
@@ -160,6 +201,76 @@ def pmc_traffic(kernel, largest=False):
     return None
 
 
+# rocprofv3 counter passes run by this benchmark on itself (a child process
+# per pass, the program directly after `--`).  gfx950 slot limits
+# (MI355X_MICROARCH.md §rocprofv3 PMC slots): FETCH_SIZE uses 3 of the 4 TCC
+# slots and WRITE_SIZE 2, so they take separate passes.
+PMC_PASSES = [["FETCH_SIZE"],
+              ["WRITE_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]]
+
+
+def pmc_child(args):
+    """--pmc-child: the C4 plan and two solves, nothing else (profiled by the
+    parent's rocprofv3 passes)."""
+    ctx = api.Context(0)
+    sc = c4_scene(args.n_cam, args.n_pt)
+    plan = api.BAPlan(ctx, sc["problem"], sc["extr"], sc["intr"], sc["X"])
+    for _ in range(2):
+        plan.run()
+    ctx.synchronize()
+    plan.close()
+    ctx.close()
+
+
+def pmc_measure(args, kernel_regex="schur_kernel"):
+    """HBM bytes and MFMA-busy cycles per launch of the Schur kernel, measured
+    now by rocprofv3 --pmc passes over a child run of the same C4 plan.
+    Returns None when rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="sfm_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for k, counters in enumerate(PMC_PASSES):
+            d = os.path.join(tmp, f"pass{k}")
+            cmd = [prof, "--pmc", *counters, "--kernel-include-regex", kernel_regex, "--output-format", "csv",
+                   "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
+                   "--n-cam", str(args.n_cam), "--n-pt", str(args.n_pt)]
+            try:
+                r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+            except subprocess.TimeoutExpired:
+                log(f"pmc pass {counters} timed out")
+                return None
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                log(f"pmc pass {counters} failed (rc {r.returncode}): {r.stderr[-400:]}")
+                return None
+            for row in csv.DictReader(open(files[0])):
+                name = row.get("Kernel_Name", "")
+                if ", true>" in name:   # the solve's first pass also forms the point scales
+                    continue
+                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
+        return None
+    mean = {c: sum(v) / len(v) for c, v in vals.items()}
+    out = {"fetch_bytes": 2.0 * 1024.0 * mean["FETCH_SIZE"],   # gfx950: FETCH_SIZE counts half (guide §HBM)
+           "write_bytes": 1024.0 * mean["WRITE_SIZE"], "launches": len(vals["FETCH_SIZE"])}
+    out["traffic"] = out["fetch_bytes"] + out["write_bytes"]
+    for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+        if c in mean:
+            out[c] = mean[c]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,7 +286,15 @@ def main():
     # with a no-op all-reduce (per-rank kernel times of the N-GPU run; the
     # solve itself is then not the global one, so the result is not a bench line)
     ap.add_argument("--fake-world", type=int, default=0)
+    # N > 1 without an RCCL communicator: the host-staged gloo all-reduce only
+    # when asked for (the number is then labelled in config.transport)
+    ap.add_argument("--allow-host-allreduce", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        pmc_child(args)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -228,6 +347,9 @@ def main():
         if int(ok.item()) == 0:
             if ctx is not None:
                 ctx.close()
+            if not args.allow_host_allreduce:
+                raise RuntimeError("RCCL communicator unavailable on some rank; refusing to benchmark over the "
+                                   "host gloo all-reduce (pass --allow-host-allreduce to measure that transport)")
 
             def host_allreduce(a, op):
                 dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM)
@@ -419,16 +541,46 @@ def main():
     cpu_match = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline_ba(sc, iters=2, threads=1)
-            log(f"cpu baseline BA: {cpu['value']:.4f} it/s")
+            cpu = cpu_baseline_ba(sc)
+            log(f"cpu baseline BA: {cpu['value']:.4f} it/s on {cpu['cores']} threads, "
+                f"{cpu['single_thread']['value']:.4f} it/s on 1")
             if match is not None:
-                cpu_match = cpu_baseline_match(desc, 4096, pairs, n_pairs=8, threads=1)
+                cpu_match = cpu_baseline_match(desc, 4096, pairs)
                 match["cpu_baseline"] = cpu_match
                 match["cascade"]["cpu_baseline"] = cpu_baseline_cascade(desc, 4096)
                 log(f"cpu baseline cascade: {match['cascade']['cpu_baseline']['value']:.3f} pairs/s")
         except Exception as ex:  # oracle missing: baseline unmeasured, not faked
             log(f"cpu baseline unavailable: {ex}")
 
+    # HBM traffic and MFMA busy of the Schur kernel, measured now (rocprofv3
+    # --pmc passes over a child run of the same C4 plan), N = 1 only
+    pmc = None
+    if world == 1 and rank == 0 and not args.no_pmc and args.fake_world <= 1:
+        t1 = time.time()
+        pmc = pmc_measure(args)
+        log(f"pmc passes: {time.time() - t1:.1f}s -> {pmc}")
+    roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TF,
+            "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TF,
+            "traffic": None, "kernel": "schur_kernel", "per_launch_ms": schur_avg_ms,
+            "algorithmic_flops_per_launch": flops,
+            "flops_formula": "sum over points of 3 r (r+1) + 780 k + 30 (r = F rows of the point, "
+                             "k = its observations; DESIGN.md §5)"}
+    if pmc is not None:
+        roof["traffic"] = pmc["traffic"]
+        roof["traffic_source"] = (f"rocprofv3 --pmc in this run: FETCH_SIZE x2 (gfx950) + WRITE_SIZE, mean of "
+                                  f"{pmc['launches']} launches")
+        # what the pass must read: per observation uv (16 B) + slot (4 B), per
+        # point X and its Jacobi scale (48 B); the RCS band it produces is < 3 MB
+        roof["algorithmic_bytes_per_launch"] = 20 * sc["n_obs"] + 48 * args.n_pt
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in pmc and schur_avg_ms > 0:
+            # busy cycles summed over the 1024 SIMDs / (SIMDs x launch time x 2.4 GHz)
+            roof["mfma_busy"] = pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * schur_avg_ms * 1e-3 * 2.4e9)
+            if pmc.get("GRBM_GUI_ACTIVE"):
+                # against the cycles the chip actually ran (GRBM_GUI_ACTIVE sums the 8 XCDs)
+                roof["mfma_busy_clk"] = pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * pmc["GRBM_GUI_ACTIVE"] / 8)
+    elif pmc_ok:
+        roof["traffic"] = pmc_traffic("schur_kernel")
+        roof["traffic_source"] = "committed profiles/r*/pmc_summary.json (not measured in this run)"
     if rank == 0:
         out = {
             "metric": "BA LM-iters/sec + obs/sec, 1k cams/500k pts/5M obs; SIFT match pairs/sec",
@@ -444,11 +596,7 @@ def main():
             "obs_per_sec": obs_per_sec,
             "lm_iterations_per_solve": summ.iterations,
             "rmse_initial": summ.rmse_initial, "rmse_final": summ.rmse_final,
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TF,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TF,
-                         "traffic": pmc_traffic("schur_kernel") if pmc_ok else None,
-                         "kernel": "schur_kernel", "per_launch_ms": schur_avg_ms,
-                         "algorithmic_flops_per_launch": flops},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "match": match,
             "ba_snavely": snav,

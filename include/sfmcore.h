@@ -288,7 +288,8 @@ int sfm_match_plan_run(sfm_match_plan* plan, const int32_t* pairs,
 int sfm_match_plan_cascade_index(sfm_match_plan* plan, const int32_t* pairs,
                                  int64_t n_pairs);
 /* Fetch: counts[n_pairs]; i/j/d2[total] pair-ordered, each pair's matches
- * sorted by (i, j) as openMVG IndMatch::getDeduplicated leaves them. */
+ * sorted by (i, j) as openMVG IndMatch::getDeduplicated leaves them (the
+ * keypoint-coordinate decorator is applied by sfm_sparse_match only). */
 int sfm_match_plan_fetch(sfm_match_plan* plan, int64_t* counts,
                          uint32_t* i, uint32_t* j, int32_t* d2);
 /* Order-independent digest of the last run's results (checksum of per-pair
@@ -368,9 +369,13 @@ typedef struct sfm_sparse_match_stats {
     int32_t reloaded, reserved;
 } sfm_sparse_match_stats;
 /* sparseBuilder::match(), file-staged: sfm_data.json + image_describer.json
- * + <stem>.desc/.feat + pairs.bin (exhaustive if absent) -> GPU matcher ->
+ * + <stem>.desc/.feat + pairs.bin -> GPU matcher ->
  * matches.putative.bin (non-empty pairs) + preemptive_pairs.txt.
- * opts NULL = {RATIO, 0.8f, 0, 1}. */
+ * pairs.bin must exist (the reference's loadPairs fails without it, :957-960:
+ * SFM_ERR_INVALID_ARG).  opts NULL = {CASCADE ("AUTO"), 0.8f, 0, 1}.
+ * dedup_xy keeps the survivors in the order OpenMVG's
+ * IndMatchDecorator::getDeduplicated leaves them (std::set over its
+ * coordinate comparator, inserted in (i, j) order). */
 int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm_sparse_match_opts* opts,
                      sfm_sparse_match_stats* stats);
 

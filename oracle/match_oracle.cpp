@@ -150,3 +150,43 @@ extern "C" int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int3
     }
     return SFM_OK;
 }
+
+// OpenMVG IndMatchDecorator<float>::getDeduplicated (matching/
+// indMatchDecoratorXY.hpp, un-vendored; parity unpinned): the (i, j)-sorted
+// matches, decorated with (xI, yI, xJ, yJ), are copied into a std::set keyed
+// by the decorator's operator<; the set's iteration order is the result.
+// That operator< is the upstream one verbatim in meaning: equal coordinates
+// compare false; otherwise a differing x1 only selects a y1 comparison, and
+// an equal x1 requires both x2 and y2 to be smaller.
+namespace {
+struct OrcDecorated {
+    float x1, y1, x2, y2;
+    uint32_t i, j;
+    friend bool operator==(const OrcDecorated& m1, const OrcDecorated& m2) {
+        return m1.x1 == m2.x1 && m1.y1 == m2.y1 && m1.x2 == m2.x2 && m1.y2 == m2.y2;
+    }
+    friend bool operator<(const OrcDecorated& m1, const OrcDecorated& m2) {
+        if (m1 == m2) return false;
+        if (m1.x1 < m2.x1)
+            return m1.y1 < m2.y1;
+        else if (m1.x1 > m2.x1)
+            return m1.y1 < m2.y1;
+        return m1.x2 < m2.x2 && m1.y2 < m2.y2;
+    }
+};
+}  // namespace
+
+#include <set>
+extern "C" int orc_dedup_decorator(const uint32_t* i, const uint32_t* j, int64_t n, const float* feat_i,
+                                   const float* feat_j, uint32_t* out_i, uint32_t* out_j, int64_t* n_out) {
+    if ((n > 0 && (!i || !j || !feat_i || !feat_j || !out_i || !out_j)) || !n_out) return SFM_ERR_INVALID_ARG;
+    std::vector<OrcDecorated> v;
+    for (int64_t k = 0; k < n; ++k)
+        v.push_back(OrcDecorated{feat_i[4 * (size_t)i[k]], feat_i[4 * (size_t)i[k] + 1], feat_j[4 * (size_t)j[k]],
+                                 feat_j[4 * (size_t)j[k] + 1], i[k], j[k]});
+    std::set<OrcDecorated> s(v.begin(), v.end());
+    int64_t w = 0;
+    for (const auto& d : s) { out_i[w] = d.i; out_j[w] = d.j; ++w; }
+    *n_out = w;
+    return SFM_OK;
+}

@@ -78,6 +78,11 @@ int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,
 int orc_cascade_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,
                       const int32_t* pairs, int64_t n_pairs, float ratio, int32_t n_threads,
                       int64_t stride, int32_t* idx, int32_t* dist);
+/* IndMatchDecorator<float>::getDeduplicated: (i, j)-sorted matches and
+ * [n][4] keypoints (x, y, scale, orientation) of both images -> survivors in
+ * the decorator's std::set order. */
+int orc_dedup_decorator(const uint32_t* i, const uint32_t* j, int64_t n, const float* feat_i,
+                        const float* feat_j, uint32_t* out_i, uint32_t* out_j, int64_t* n_out);
 /* CascadeHasher::Init projections, float [188][128]. */
 int orc_cascade_projections(float* out);
 

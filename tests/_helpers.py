@@ -36,6 +36,9 @@ def oracle():
         lib.orc_match_dense.restype = C.c_int
         lib.orc_match_dense.argtypes = [abi.u8p, C.c_int32, abi.u8p, C.c_int32, C.c_int32,
                                         C.c_float, abi.i32p, abi.i32p]
+        lib.orc_dedup_decorator.restype = C.c_int
+        lib.orc_dedup_decorator.argtypes = [abi.u32p, abi.u32p, C.c_int64, abi.f32p, abi.f32p,
+                                            abi.u32p, abi.u32p, abi.i64p]
         lib.orc_cascade_projections.restype = C.c_int
         lib.orc_cascade_projections.argtypes = [abi.f32p]
         lib.orc_match_pairs.restype = C.c_int
@@ -171,3 +174,20 @@ def oracle_cost(scene, e, i, x):
                          abi.ptr(x, abi.f64p), C.byref(c), None)
     assert rc == 0
     return c.value
+
+
+def oracle_dedup_decorator(m, kp_i, kp_j):
+    """OpenMVG IndMatchDecorator::getDeduplicated on (i, j)-sorted matches m."""
+    lib = oracle()
+    m = np.asarray(m, np.uint32).reshape(-1, 2)
+    i = np.ascontiguousarray(m[:, 0])
+    j = np.ascontiguousarray(m[:, 1])
+    fi = np.ascontiguousarray(kp_i, np.float32)
+    fj = np.ascontiguousarray(kp_j, np.float32)
+    oi = np.zeros(max(len(m), 1), np.uint32)
+    oj = np.zeros(max(len(m), 1), np.uint32)
+    n = C.c_int64()
+    assert lib.orc_dedup_decorator(abi.ptr(i, abi.u32p), abi.ptr(j, abi.u32p), len(m), abi.ptr(fi, abi.f32p),
+                                   abi.ptr(fj, abi.f32p), abi.ptr(oi, abi.u32p), abi.ptr(oj, abi.u32p),
+                                   C.byref(n)) == 0
+    return list(zip(oi[:n.value].tolist(), oj[:n.value].tolist()))

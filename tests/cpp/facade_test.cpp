@@ -176,11 +176,14 @@ int main() {
                         "\"regions_type\": {\"polymorphic_id\": 2147483650, \"polymorphic_name\": \"SIFT_Regions\", "
                         "\"ptr_wrapper\": {\"id\": 2147483650, \"data\": {}}}}\n");
         std::fclose(f);
-        for (int v = 0; v < 4; ++v) {   // distinct keypoint positions: nothing is de-duplicated
+        // distinct keypoint positions with x and y both increasing in the
+        // keypoint index: OpenMVG's decorator set then keeps every match, in
+        // (i, j) order
+        for (int v = 0; v < 4; ++v) {
             const std::string stem = mdir + "/img" + std::to_string(v);
             CHECK(sfm_mvg_write_desc((stem + ".desc").c_str(), regions[v].data(), 700) == SFM_OK);
             f = std::fopen((stem + ".feat").c_str(), "w");
-            for (int k = 0; k < 700; ++k) std::fprintf(f, "%d %d 1.5 0.25\n", k, v);
+            for (int k = 0; k < 700; ++k) std::fprintf(f, "%d %d 1.5 0.25\n", k, k + 1000 * v);
             std::fclose(f);
         }
     }

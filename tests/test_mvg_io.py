@@ -191,8 +191,8 @@ def make_stage_dir(d, views, with_pairs=True):
 
 def expected_matches(views, dedup=True, mode=abi.SFM_MATCH_RATIO, pairs=None):
     """Oracle restatement: RATIO (exact brute force) or CASCADE matching over
-    the collection, (i, j)-sorted, then drop matches whose (xI, yI, xJ, yJ)
-    repeat an earlier one."""
+    the collection, (i, j)-sorted, then OpenMVG's IndMatchDecorator
+    de-duplication (its std::set order over the keypoint coordinates)."""
     n = len(views)
     if pairs is None:
         pairs = [(I, J) for I in range(n) for J in range(I + 1, n)]
@@ -215,16 +215,34 @@ def expected_matches(views, dedup=True, mode=abi.SFM_MATCH_RATIO, pairs=None):
                 idx, _ = H.oracle_match_dense(dI, dJ, mode)
                 m = sorted((int(i), int(j)) for j, i in enumerate(idx) if i >= 0)
             if dedup:
-                seen, keep = set(), []
-                for i, j in m:
-                    key = (kI[i, 0], kI[i, 1], kJ[j, 0], kJ[j, 1])
-                    if key not in seen:
-                        seen.add(key)
-                        keep.append((i, j))
-                m = keep
+                m = H.oracle_dedup_decorator(m, kI, kJ)
             if m:
                 out[(I, J)] = np.array(m, np.uint32)
     return out
+
+
+def test_decorator_dedup_order():
+    """The decorator set drops repeated (xI, yI, xJ, yJ) and orders the rest by
+    its comparator: with x and y both increasing in the index the order is
+    (i, j); with one y for every keypoint of I the comparator calls all of
+    them equivalent and only the first match survives (the upstream quirk)."""
+    kI = np.array([[k, k, 1, 0] for k in range(6)], np.float32)
+    kJ = np.array([[k, 2 * k, 1, 0] for k in range(6)], np.float32)
+    m = [(0, 1), (1, 0), (1, 3), (4, 2), (5, 5)]
+    assert H.oracle_dedup_decorator(m, kI, kJ) == m
+    kJ2 = kJ.copy()
+    kJ2[3] = kJ2[0]          # (1, 3) repeats (1, 0)'s coordinates
+    assert H.oracle_dedup_decorator(m, kI, kJ2) == [(0, 1), (1, 0), (4, 2), (5, 5)]
+    flat = kI.copy()
+    flat[:, 1] = 7.0
+    assert H.oracle_dedup_decorator(m, flat, kJ) == [(0, 1)]
+    # survivors never repeat a coordinate tuple on the VLFeat views
+    (dI, pI), (dJ, pJ) = vlfeat_views()[:2]
+    idx, _ = H.oracle_match_dense(dI, dJ, abi.SFM_MATCH_RATIO)
+    raw = sorted((int(i), int(j)) for j, i in enumerate(idx) if i >= 0)
+    got = H.oracle_dedup_decorator(raw, pI, pJ)
+    keys = {(pI[i, 0], pI[i, 1], pJ[j, 0], pJ[j, 1]) for i, j in got}
+    assert len(keys) == len(got) and set(got) <= set(raw) and 0 < len(got) < len(raw)
 
 
 def test_vlfeat_fixtures_have_repeated_keypoints():
