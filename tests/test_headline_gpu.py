@@ -61,15 +61,16 @@ def test_c4_bench_scene_full_solve_vs_oracle(ctx):
 
 
 def _c3_sample(n_img, n):
+    """n pairs: half neighbouring frames (shared landmarks), half far apart,
+    always including the first and the last pair of the exhaustive list."""
     rng = np.random.default_rng(0xC3)
-    near = [(i, i + 1) for i in rng.choice(n_img - 1, n // 2, replace=False)]
-    far = set()
-    while len(far) < n - len(near) - 2:
+    pairs = {(0, 1), (n_img - 2, n_img - 1)}
+    pairs |= {(int(i), int(i) + 1) for i in rng.choice(n_img - 1, n // 2, replace=False)}
+    while len(pairs) < n:
         a, b = sorted(rng.choice(n_img, 2, replace=False).tolist())
         if b - a > 4:
-            far.add((a, b))
-    pairs = sorted(set(near) | far | {(0, 1), (n_img - 2, n_img - 1)})
-    return np.array(pairs, np.int32)
+            pairs.add((a, b))
+    return np.array(sorted(pairs), np.int32)
 
 
 @pytest.mark.parametrize("mode", [abi.SFM_MATCH_RATIO, abi.SFM_MATCH_MUTUAL])
