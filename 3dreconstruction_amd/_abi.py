@@ -97,6 +97,13 @@ class BAPlanInfo(C.Structure):
                 ("schur_launches", C.c_int64), ("schur_ms_total", C.c_double)]
 
 
+class BAPlanShape(C.Structure):
+    _fields_ = [("n_chunks", C.c_int32), ("band_blocks", C.c_int32), ("dense", C.c_int32),
+                ("n_cam_active", C.c_int32), ("n_intr_active", C.c_int32), ("tile_rows", C.c_int32),
+                ("n_chunk_pts", C.c_int64), ("n_general_pts", C.c_int64), ("rcs_dim", C.c_int64),
+                ("n_targets", C.c_int64), ("n_terms", C.c_int64), ("n_pterms", C.c_int64)]
+
+
 class SynthBAConfig(C.Structure):
     _fields_ = [("n_cam", C.c_int32), ("k", C.c_int32), ("vis_mode", C.c_int32),
                 ("n_intr", C.c_int32), ("n_pt", C.c_int64), ("seed", C.c_uint64),
@@ -161,6 +168,7 @@ SIGNATURES = [
     ("sfm_ba_plan_get_info", C.c_int, [C.c_void_p, C.POINTER(BAPlanInfo)]),
     ("sfm_ba_plan_get_trace", C.c_int, [C.c_void_p, C.POINTER(BAIter), C.c_int32, i32p]),
     ("sfm_ba_partition", C.c_int, [C.POINTER(BAProblem), C.c_int32, i64p, i64p]),
+    ("sfm_ba_describe", C.c_int, [C.POINTER(BAProblem), C.c_int32, C.c_int32, C.POINTER(BAPlanShape)]),
     ("sfm_synth_ba", C.c_int, [C.POINTER(SynthBAConfig), i64p, i32p, f64p, i32p, f64p,
                                f64p, f64p, f64p, f64p, f64p, i64p]),
     ("sfm_match_dense", C.c_int, [C.c_void_p, u8p, C.c_int32, u8p, C.c_int32,

@@ -210,6 +210,14 @@ def synth_descriptors(n_img, n_kp, seed=0xC3):
     return d[:n_img * n_kp * 128].reshape(-1, 128)
 
 
+def ba_describe(problem, rank=0, world=1):
+    """[cpu] The planner's structure for a problem (sfm_ba_describe)."""
+    lib = abi.load()
+    out = abi.BAPlanShape()
+    _check(lib.sfm_ba_describe(C.byref(problem), rank, world, C.byref(out)), "sfm_ba_describe")
+    return out
+
+
 class BAPlan:
     """Resident BA problem (sfm_ba_plan): upload once, run many times."""
 

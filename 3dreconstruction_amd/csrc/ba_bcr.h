@@ -18,6 +18,17 @@ struct BcrArgs {
     unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums
 };
 
+// Dense RCS solve (blocked Cholesky on 64x64 tiles, same file).
+struct DenseArgs {
+    int nt = 0;          // tiles per side
+    int64_t np = 0;      // padded order nt * 64
+    double *A = nullptr, *X = nullptr, *b = nullptr, *y = nullptr, *x = nullptr, *fail = nullptr;
+};
+void dense_setup(DenseArgs& d, const DevProblem& P);
+size_t dense_doubles(const DenseArgs& d);
+void dense_bind(DenseArgs& d, double* base);
+void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s);
+
 bool bcr_supported(const DevProblem& P);
 void bcr_setup(BcrArgs& b, const DevProblem& P);
 size_t bcr_doubles(const BcrArgs& b);

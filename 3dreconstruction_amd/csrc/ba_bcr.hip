@@ -794,4 +794,202 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     SFM_HIP(hipGetLastError());
 }
 
+
+// ===========================================================================
+// Dense reduced camera system (RCS) solve: blocked right-looking Cholesky on
+// 64x64 fp64 tiles.  Used when the cameras do not form a narrow band (random
+// visibility, long tracks, many intrinsics blocks) -- Ceres' SPARSE_SCHUR +
+// EIGEN_SPARSE (BundleAdjuster.h:171-173) factors the same matrix.
+//   pack      A = lower(S) + D^2 (Ceres' LM diagonal), identity padding; b = rhs
+//   step k    panel: every workgroup of column k factors A_kk (chol_inv64:
+//             L_kk and X_kk = L_kk^-1, MFMA) and forms L_ik = A_ik X_kk';
+//             the k-th one stores L_kk, X_kk and y_k = X_kk b_k
+//   update k  A_ij -= L_ik L_jk' for k < j <= i (one workgroup per tile, MFMA),
+//             b_i -= L_ik y_k (forward substitution, fused)
+//   back      x_k = X_kk' (y_k - sum_{j>k} L_jk' x_j), one workgroup
+// ===========================================================================
+namespace {
+
+constexpr int kDM = 64;   // tile
+
+__global__ __launch_bounds__(256) void dense_pack_kernel(DenseArgs d, DevProblem P, double radius) {
+    const int64_t np = d.np;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e < np * np) {
+        const int64_t i = e / np, j = e % np;
+        double v = 0.0;
+        if (i < P.nF && j < P.nF) {
+            if (j <= i) v = P.Sdense[i * P.nF + j];
+            if (i == j) {
+                const double lm = sqrt(clampd(P.cnF[i], P.min_diag, P.max_diag) / radius);
+                v += lm * lm;
+            }
+        } else if (i == j) {
+            v = 1.0;
+        }
+        d.A[e] = v;
+    }
+    if (e < np) d.b[e] = e < P.nF ? P.rhs[e] : 0.0;
+    if (e == 0) d.fail[0] = 0.0;
+}
+
+// column k: workgroup w handles row tile i = k + w
+__global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Akk = sm;                 // [64][LD]
+    double* Xkk = Akk + M * LD;       // [64][LD]
+    double* Aik = Xkk + M * LD;       // [64][LD]
+    double* flag = Aik + M * LD;      // [2]
+    const int i = k + blockIdx.x;
+    const int64_t np = d.np;
+    const double* src = d.A + (int64_t)k * kDM * np + (int64_t)k * kDM;
+    load_tile<64>(Akk, LD, src, (int)np);
+    for (int e = threadIdx.x; e < M * LD; e += NT) Xkk[e] = 0.0;
+    if (threadIdx.x == 0) flag[0] = 0.0;
+    if (i > k) load_tile<64>(Aik, LD, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
+    __syncthreads();
+    chol_inv64(Akk, Xkk, flag, flag + 1);
+    const int wave = threadIdx.x >> 6;
+    if (i == k) {
+        double* dst = d.A + (int64_t)k * kDM * np + (int64_t)k * kDM;
+        double* xd = d.X + (int64_t)k * kDM * kDM;
+        for (int e = threadIdx.x; e < M * M; e += NT) {
+            const int r = e / M, c = e % M;
+            dst[(int64_t)r * np + c] = Akk[r * LD + c];
+            xd[e] = Xkk[r * LD + c];
+        }
+        // y_k = X_kk b_k (b_k final: every earlier column's update is done)
+        if (threadIdx.x < M) {
+            const int r = threadIdx.x;
+            const double* bk = d.b + (int64_t)k * kDM;
+            double s = 0.0;
+            for (int c = 0; c <= r; ++c) s += Xkk[r * LD + c] * bk[c];
+            d.y[(int64_t)k * kDM + r] = s;
+        }
+        if (threadIdx.x == 0 && flag[0] != 0.0) d.fail[0] = 1.0;
+        return;
+    }
+    // L_ik = A_ik X_kk' (X lower: column c of X' needs m <= c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int t = wave * 4 + q, ti = t >> 2, tj = t & 3;
+        const v4d acc = tile_mm<false, true, false>(zero4(), Aik, LD, 16 * ti, Xkk, LD, 16 * tj, 0, 16 * tj + 16);
+        tile_st(d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np, 16 * ti, 16 * tj, acc);
+    }
+}
+
+// trailing update of column k: tiles (i, j), k < j <= i, plus rhs tiles
+__global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k, int n_tiles) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Li = sm;
+    double* Lj = sm + M * LD;
+    const int64_t np = d.np;
+    const int m = d.nt - k - 1;
+    const int t = blockIdx.x;
+    if (t >= n_tiles) {   // rhs tile i: b_i -= L_ik y_k
+        const int i = k + 1 + (t - n_tiles);
+        if (threadIdx.x < M) {
+            const int r = threadIdx.x;
+            const double* L = d.A + ((int64_t)i * kDM + r) * np + (int64_t)k * kDM;
+            const double* yk = d.y + (int64_t)k * kDM;
+            double s = 0.0;
+            for (int c = 0; c < M; ++c) s += L[c] * yk[c];
+            d.b[(int64_t)i * kDM + r] -= s;
+        }
+        return;
+    }
+    // t -> (i, j) over the lower triangle of the m x m trailing tile grid
+    int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((a + 1) * (a + 2) / 2 <= t) ++a;
+    while (a * (a + 1) / 2 > t) --a;
+    const int i = k + 1 + a, j = k + 1 + (t - a * (a + 1) / 2);
+    (void)m;
+    load_tile<64>(Li, LD, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
+    if (i != j) load_tile<64>(Lj, LD, d.A + (int64_t)j * kDM * np + (int64_t)k * kDM, (int)np);
+    __syncthreads();
+    const double* Lb = i != j ? Lj : Li;
+    double* C = d.A + (int64_t)i * kDM * np + (int64_t)j * kDM;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
+        if (i == j && tj > ti) continue;   // the diagonal tile's lower half (and its diagonal sub-tiles)
+        v4d acc = tile_ld(C, (int)np, 16 * ti, 16 * tj);
+        acc = tile_mm<false, true, true>(acc, Li, LD, 16 * ti, Lb, LD, 16 * tj, 0, M);
+        tile_st(C, (int)np, 16 * ti, 16 * tj, acc);
+    }
+}
+
+// back substitution L' x = y, one workgroup: x_k = X_kk' (y_k - sum_{j>k} L_jk' x_j)
+__global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem P) {
+    __shared__ double part[4][M], t[M];
+    const int64_t np = d.np;
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    for (int k = d.nt - 1; k >= 0; --k) {
+        // column c of block k: sum over rows r > this block of L[r][k*64 + c] x[r]
+        double s = 0.0;
+        for (int64_t r = (int64_t)(k + 1) * kDM + g; r < np; r += 4) s += d.A[r * np + (int64_t)k * kDM + c] * d.x[r];
+        part[g][c] = s;
+        __syncthreads();
+        if (threadIdx.x < M) t[c] = d.y[(int64_t)k * kDM + c] - (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+        __syncthreads();
+        if (threadIdx.x < M) {   // x_k = X_kk' t: X lower, so rows m >= c
+            const double* X = d.X + (int64_t)k * kDM * kDM;
+            double v = 0.0;
+            for (int mm = c; mm < M; ++mm) v += X[mm * M + c] * t[mm];
+            d.x[(int64_t)k * kDM + c] = v;
+        }
+        __syncthreads();
+    }
+    for (int64_t e = threadIdx.x; e < P.nF; e += NT) P.yF[e] = d.x[e];
+    if (threadIdx.x == 0) P.scal[kScSolveFail] = d.fail[0];
+}
+
+}  // namespace
+
+void dense_setup(DenseArgs& d, const DevProblem& P) {
+    d.nt = (int)((P.nF + kDM - 1) / kDM);
+    d.np = (int64_t)d.nt * kDM;
+}
+
+size_t dense_doubles(const DenseArgs& d) {
+    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8;
+}
+
+void dense_bind(DenseArgs& d, double* base) {
+    d.A = base;
+    d.X = d.A + (size_t)d.np * d.np;
+    d.b = d.X + (size_t)d.nt * kDM * kDM;
+    d.y = d.b + d.np;
+    d.x = d.y + d.np;
+    d.fail = d.x + d.np;
+}
+
+void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s) {
+    const int64_t n2 = d.np * d.np;
+    hipLaunchKernelGGL(dense_pack_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d, P, radius);
+    SFM_HIP(hipGetLastError());
+    const size_t lds_p = (3 * M * LD + 2) * sizeof(double), lds_u = 2 * M * LD * sizeof(double);
+    static bool attr = false;
+    if (!attr) {
+        SFM_HIP(hipFuncSetAttribute((const void*)dense_panel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_p));
+        SFM_HIP(hipFuncSetAttribute((const void*)dense_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_u));
+        attr = true;
+    }
+    for (int k = 0; k < d.nt; ++k) {
+        hipLaunchKernelGGL(dense_panel_kernel, dim3(d.nt - k), dim3(NT), lds_p, s, d, k);
+        SFM_HIP(hipGetLastError());
+        const int m = d.nt - k - 1;
+        if (m > 0) {
+            const int n_tiles = m * (m + 1) / 2;
+            hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m), dim3(NT), lds_u, s, d, k, n_tiles);
+            SFM_HIP(hipGetLastError());
+        }
+    }
+    hipLaunchKernelGGL(dense_back_kernel, dim3(1), dim3(NT), 0, s, d, P);
+    SFM_HIP(hipGetLastError());
+}
+
 }  // namespace sfm

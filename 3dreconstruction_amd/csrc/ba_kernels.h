@@ -21,6 +21,9 @@ constexpr int kPartT = 5;  // per step block: model acc, cand cost, step norm^2,
 
 struct DevProblem {
     int32_t n_img, n_intr, n_spt, n_sobs, n_chunk, ncam, nintr, D;
+    int32_t n_cpt, n_gpt;           // chunk points [0, n_cpt), general points [n_cpt, n_spt)
+    int32_t gz_max;                 // Z doubles of the largest general point
+    int32_t dense;                  // RCS stored dense (Sdense) rather than band + arrow
     int32_t tile_nt;    // 16-row MFMA tiles per chunk side: 4 (64 F rows) or 5 (76 + w row)
     int32_t cam_model;  // SFM_CAM_* residual model
     int64_t nb, nF;
@@ -50,6 +53,13 @@ struct DevProblem {
     const int32_t* lseg_off;        // [n_long+1] segment ranges per long target
     const int32_t* lseg;            // [n_lseg][2] (long index, first term)
     double* lpart;                  // [n_lseg][36] segment partial sums
+    // general points (ba_plan.h): blocks, Z layout, product terms
+    const int32_t* gblk_off;        // [n_gpt+1]
+    const int32_t* gblk_col;        // F column of each block
+    const int32_t* gblk_z;          // block's offset within the point's Z
+    const int64_t* gz_off;          // [n_gpt+1]
+    const PTerm* pterms;
+    double* Z;                      // general points' eliminated rows, w after each point's blocks
     // state
     double* scaleE;     // [3*n_spt]
     double* scaleF;     // [nF]
@@ -60,6 +70,7 @@ struct DevProblem {
     double* Sband;      // [ncam][D+1][36]
     double* Sarrow;     // [nintr][ncam][24]
     double* Scorner;    // [nintr][nintr][16]
+    double* Sdense;     // [nF][nF], lower triangle (dense mode)
     double* rhs;        // [nF]
     double* bF;         // [nF]
     double* cnF;        // [nF]
@@ -69,7 +80,7 @@ struct DevProblem {
     double* yF;         // [nF]
     double* Wglobal;    // solve window when it does not fit LDS
     double* part_u;     // [n_img][2]
-    double* part_s;     // [n_chunk][2]
+    double* part_s;     // [n_chunk + n_gpt][2]
     double* part_t;     // [n_step_blocks][kPartT]
     double* part_f;     // [n_fblk][3] candidate-kernel partials
     int32_t n_fblk;
@@ -108,6 +119,7 @@ void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq = 0)
 size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
 size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);
+constexpr int kGStepThreads = 128;   // general points per step workgroup
 int reduce_long_threshold();
 constexpr int kReduceSeg = 256;   // terms per long-target segment (one workgroup)
 

@@ -928,7 +928,8 @@ __device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {
         case 2: return P.Scorner;
         case 3: return P.rhs;
         case 4: return P.bF;
-        default: return P.cnF;
+        case 5: return P.cnF;
+        default: return P.Sdense;
     }
 }
 
@@ -938,12 +939,17 @@ __device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {
 // intrinsics corner one per chunk (thousands).
 constexpr int kLongTerms = 256;
 
-__global__ void reduce_kernel(DevProblem P, int min_kind) {
+// vectors_only (iteration 0, before the Jacobi scales): bF and cnF only
+__device__ __forceinline__ bool skip_kind(int kind, int vectors_only) {
+    return vectors_only && kind != kDstBF && kind != kDstCnF;
+}
+
+__global__ void reduce_kernel(DevProblem P, int vectors_only) {
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int e = threadIdx.x & 63;
     if (t >= P.n_targets) return;
     const ReduceTarget T = P.targets[t];
-    if (T.dst_kind < min_kind || T.c_end - T.c_begin > kLongTerms) return;
+    if (skip_kind(T.dst_kind, vectors_only) || T.c_end - T.c_begin > kLongTerms) return;
     if (e >= T.rows * T.cols) return;
     const int r = e / T.cols, cc = e % T.cols;
     const bool vec = T.cols == 1;
@@ -975,11 +981,11 @@ __global__ void reduce_kernel(DevProblem P, int min_kind) {
 // Long targets, pass 1: one workgroup per kReduceSeg-term segment, one term
 // per thread (every element of the block, <= 36, in registers); the 256
 // partial blocks are combined by xor-butterflies and wave order (fixed).
-__global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int min_kind) {
+__global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int vectors_only) {
     const int sg = blockIdx.x;
     const int j = P.lseg[2 * sg], k0 = P.lseg[2 * sg + 1];
     const ReduceTarget T = P.targets[P.long_targets[j]];
-    if (T.dst_kind < min_kind) return;
+    if (skip_kind(T.dst_kind, vectors_only)) return;
     const int E = T.rows * T.cols;
     double s[36];
 #pragma unroll
@@ -1006,10 +1012,10 @@ __global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int min_k
 }
 
 // pass 2: segment partials added in segment order
-__global__ __launch_bounds__(64) void reduce_long_kernel(DevProblem P, int min_kind) {
+__global__ __launch_bounds__(64) void reduce_long_kernel(DevProblem P, int vectors_only) {
     const int j = blockIdx.x;
     const ReduceTarget T = P.targets[P.long_targets[j]];
-    if (T.dst_kind < min_kind) return;
+    if (skip_kind(T.dst_kind, vectors_only)) return;
     const int E = T.rows * T.cols, e = threadIdx.x;
     if (e >= E) return;
     double t = 0.0;
@@ -1457,6 +1463,337 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
     }
 }
 
+// ---------------------------------------------------------------------------
+// General points (ba_plan.h): one wavefront per point -- any number of
+// observations (rounds of 64), repeated views of one image, any number of
+// intrinsics blocks.  The point is eliminated as in schur_kernel (V + D^2, its
+// Cholesky L, w = L^-1 g_E, M = Jx L^-T per observation) and its eliminated
+// rows Z_b = sum over the observations of block b of J_b' M (camera 6 x 3,
+// intrinsics 4 x 3) plus w go to the Z buffer; preduce_kernel forms the RCS
+// contributions -Z_a Z_b' and -Z_a w.  The point's Z is accumulated in LDS
+// (dynamic: 64 x 19 staging doubles + the largest point's Z) in a fixed order:
+// a camera block sums its adjacent run of observations (the planner sorts a
+// general point's observations by image), an intrinsics block one masked
+// wave sum per 64-observation round, rounds in order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kZStage = 19;   // doubles per staged observation row (18 used, odd stride)
+
+template <int CM, bool SE>
+__global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                    const double* __restrict__ intr, const double* __restrict__ X,
+                                                    double radius) {
+    extern __shared__ __attribute__((aligned(16))) double zlds[];
+    double* zc = zlds;                       // [64][kZStage] camera rows J_c' M of this round
+    double* Zl = zlds + 64 * kZStage;        // the point's Z (blocks), accumulated
+    __shared__ int cbl[64];
+    const int lane = threadIdx.x, g = blockIdx.x;
+    const int k = P.n_cpt + g;
+    const int o0 = P.pt_off[k], o1 = P.pt_off[k + 1];
+    const int b0 = P.gblk_off[g];
+    const int zn = (int)(P.gz_off[g + 1] - P.gz_off[g]) - 3;
+    const double Xp[3] = {X[3 * (size_t)k], X[3 * (size_t)k + 1], X[3 * (size_t)k + 2]};
+    double sE[3];
+    // observation o at x: loss-corrected Jacobians, unscaled
+    auto lin = [&](int o, Lin& L) {
+        const int img = P.obs_img[o];
+        const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+        linearize<CM, true, true, true>(cps[img], intr + 4 * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
+    };
+    if constexpr (SE) {
+        // the solve's first pass: Ceres' Jacobi point scales from the column
+        // norms of the unscaled point Jacobian
+        double cn[3] = {0.0, 0.0, 0.0};
+        for (int o = o0 + lane; o < o1; o += 64) {
+            Lin L;
+            lin(o, L);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) cn[a] += L.Jx[0][a] * L.Jx[0][a] + L.Jx[1][a] * L.Jx[1][a];
+        }
+        wave_sum(cn);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) sE[a] = 1.0 / (1.0 + sqrt(cn[a]));
+        if (lane < 3) P.scaleE[3 * (size_t)k + lane] = sE[lane];
+    } else {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) sE[a] = P.scaleE[3 * (size_t)k + a];
+    }
+    // V = Jx' Jx, g_E = Jx' f over the point (scaled), summed by the wave
+    double v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // V00 V10 V11 V20 V21 V22 | b0 b1 b2
+    for (int o = o0 + lane; o < o1; o += 64) {
+        Lin L;
+        lin(o, L);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2], fr = L.f[r];
+            v9[0] += j0 * j0; v9[1] += j1 * j0; v9[2] += j1 * j1;
+            v9[3] += j2 * j0; v9[4] += j2 * j1; v9[5] += j2 * j2;
+            v9[6] += j0 * fr; v9[7] += j1 * fr; v9[8] += j2 * fr;
+        }
+    }
+    wave_sum(v9);
+    double V[6] = {v9[0], v9[1], v9[2], v9[3], v9[4], v9[5]};
+    const double b[3] = {v9[6], v9[7], v9[8]};
+    if (lane == 0) {   // gradient / norm bookkeeping at x
+        double xn2 = 0.0, gmx = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double gg = b[a] * rcp_nr(sE[a]);
+            xn2 += Xp[a] * Xp[a];
+            gmx = fmax(gmx, fabs(Xp[a] - (Xp[a] - gg)));
+        }
+        P.part_s[2 * (size_t)(P.n_chunk + g)] = xn2;
+        P.part_s[2 * (size_t)(P.n_chunk + g) + 1] = gmx;
+    }
+    const double inv_radius = 1.0 / radius;
+    const int di[3] = {0, 2, 5};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
+        V[di[a]] += lm * lm;
+    }
+    const double i00 = rsqrt_nr(V[0]);
+    const double l10 = V[1] * i00, l20 = V[3] * i00;
+    const double i11 = rsqrt_nr(V[2] - l10 * l10);
+    const double l21 = (V[4] - l20 * l10) * i11;
+    const double i22 = rsqrt_nr(V[5] - l20 * l20 - l21 * l21);
+    const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    for (int e = lane; e < zn; e += 64) Zl[e] = 0.0;
+    int prev_cb = -1;   // camera block of the previous round's last observation
+    for (int base = o0; base < o1; base += 64) {
+        const int o = base + lane;
+        const bool act = o < o1;
+        int cb = 0xffff, ib = -1;
+        double zi[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) zi[e] = 0.0;
+        if (act) {
+            Lin L;
+            lin(o, L);
+            const int img = P.obs_img[o];
+            const int slot = P.obs_slot[o];
+            cb = slot & 0xffff;
+            ib = slot >> 16;
+            double M[2][3];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
+                M[r][0] = j0 * i00;
+                M[r][1] = j0 * i10 + j1 * i11;
+                M[r][2] = j0 * i20 + j1 * i21 + j2 * i22;
+            }
+            const int colc = P.img_colc[img], coli = P.img_coli[img];
+            if (cb != 0xffff) {
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const double s = P.scaleF[colc + r];
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        zc[lane * kZStage + 3 * r + a] = (L.Jc[0][r] * s) * M[0][a] + (L.Jc[1][r] * s) * M[1][a];
+                }
+            }
+            const int ni = CM == SFM_CAM_SNAVELY ? 3 : 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (r >= ni) continue;
+                const double s = P.scaleF[coli + r];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) zi[3 * r + a] = (L.Ji[0][r] * s) * M[0][a] + (L.Ji[1][r] * s) * M[1][a];
+            }
+        }
+        cbl[lane] = act ? cb : -2;
+        wsync();
+        // camera blocks: the first observation of each run sums the run in order
+        const bool head = act && cb != 0xffff && (lane == 0 || cbl[lane - 1] != cb);
+        if (head) {
+            double acc[18];
+#pragma unroll
+            for (int e = 0; e < 18; ++e) acc[e] = zc[lane * kZStage + e];
+            for (int q = lane + 1; q < 64 && cbl[q] == cb; ++q)
+#pragma unroll
+                for (int e = 0; e < 18; ++e) acc[e] += zc[q * kZStage + e];
+            double* dst = Zl + P.gblk_z[b0 + cb];
+            const bool cont = lane == 0 && cb == prev_cb;   // run continued from the previous round
+#pragma unroll
+            for (int e = 0; e < 18; ++e) dst[e] = cont ? dst[e] + acc[e] : acc[e];
+        }
+        prev_cb = cbl[63] >= 0 ? cbl[63] : -1;
+        // intrinsics blocks: one masked wave sum per distinct block of the round
+        unsigned long long pend = __ballot(act);
+        while (pend) {
+            const int src = __builtin_ctzll(pend);
+            const int j = __shfl(ib, src);
+            const bool mine = act && ib == j;
+            double v[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) v[e] = mine ? zi[e] : 0.0;
+            wave_sum(v);
+            const int nz = 3 * (CM == SFM_CAM_SNAVELY ? 3 : 4);
+            double mine_v = 0.0;   // v[lane] without a dynamically indexed register array
+#pragma unroll
+            for (int e = 0; e < 12; ++e) mine_v = lane == e ? v[e] : mine_v;
+            if (lane < nz) Zl[P.gblk_z[b0 + j] + lane] += mine_v;
+            pend &= ~__ballot(mine);
+        }
+        wsync();
+    }
+    double* Zg = P.Z + P.gz_off[g];
+    for (int e = lane; e < zn; e += 64) Zg[e] = Zl[e];
+    if (lane < 3) {
+        const double w3[3] = {i00 * b[0], i10 * b[0] + i11 * b[1], i20 * b[0] + i21 * b[1] + i22 * b[2]};
+        Zg[zn + lane] = lane == 0 ? w3[0] : lane == 1 ? w3[1] : w3[2];
+    }
+}
+
+// Product terms of the general points: target element (r, c) -= sum over the
+// target's terms (in order) of Z_a[r] . Z_b[c] (3-vectors).  One wave per
+// target, one lane per element; runs after reduce_kernel has written the sum
+// terms.
+__global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int e = threadIdx.x & 63;
+    if (t >= P.n_targets) return;
+    const ReduceTarget T = P.targets[t];
+    if (T.p_end == T.p_begin || e >= T.rows * T.cols) return;
+    const int r = e / T.cols, cc = e % T.cols;
+    const bool vec = T.cols == 1;
+    const double* Z = P.Z;
+    double s = 0.0;
+    int q = T.p_begin;
+    for (; q + 4 <= T.p_end; q += 4) {   // 4 terms' loads in flight, sums in order
+        double a[4][3], bb[4][3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const PTerm pt = P.pterms[q + j];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                a[j][k] = Z[pt.za + 3 * r + k];
+                bb[j][k] = Z[pt.zb + (vec ? 0 : 3 * cc) + k];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += a[j][0] * bb[j][0] + a[j][1] * bb[j][1] + a[j][2] * bb[j][2];
+    }
+    for (; q < T.p_end; ++q) {
+        const PTerm pt = P.pterms[q];
+        const double* za = Z + pt.za + 3 * r;
+        const double* zb = Z + pt.zb + (vec ? 0 : 3 * cc);
+        s += za[0] * zb[0] + za[1] * zb[1] + za[2] * zb[2];
+    }
+    double* dst = target_base(P, T.dst_kind) + T.dst + (vec ? r : (int64_t)r * T.ld + cc);
+    *dst -= s;
+}
+
+// Step for general points: one thread per point, the same arithmetic as
+// step_kernel with cameras and column scales read from global memory.
+template <int CM>
+__global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
+    DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr, const CamPre* __restrict__ cps_c,
+    const double* __restrict__ intr_c, const double* __restrict__ X, double* __restrict__ Xc, double radius) {
+    const int tid = threadIdx.x, g = blockIdx.x * kGStepThreads + tid;
+    const double inv_radius = 1.0 / radius;
+    double acc[3] = {0.0, 0.0, 0.0};
+    double bad = 0.0, cbad = 0.0;
+    if (g < P.n_gpt) {
+        const int p = P.n_cpt + g;
+        const double Xp[3] = {X[3 * (size_t)p], X[3 * (size_t)p + 1], X[3 * (size_t)p + 2]};
+        const double sE[3] = {P.scaleE[3 * (size_t)p], P.scaleE[3 * (size_t)p + 1], P.scaleE[3 * (size_t)p + 2]};
+        double V[6] = {0, 0, 0, 0, 0, 0}, bf[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
+        double sqf = 0.0, sqq = 0.0;
+        const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+        for (int o = o0; o < o1; ++o) {
+            const int img = P.obs_img[o];
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+            const int colc = P.img_colc[img], coli = P.img_coli[img];
+            Lin L;
+            linearize<CM, true, true, true>(cps[img], intr + 4 * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double q = 0.0;
+                if (colc >= 0)
+#pragma unroll
+                    for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * (P.scaleF[colc + a] * P.yF[colc + a]);
+                const int ni = CM == SFM_CAM_SNAVELY ? 3 : 4;
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+                    if (a < ni) q += L.Ji[r][a] * (P.scaleF[coli + a] * P.yF[coli + a]);
+                const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
+                const double fr = L.f[r];
+                V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
+                V[3] += j2 * j0; V[4] += j2 * j1; V[5] += j2 * j2;
+                bf[0] += j0 * fr; bf[1] += j1 * fr; bf[2] += j2 * fr;
+                bq[0] += j0 * q; bq[1] += j1 * q; bq[2] += j2 * q;
+                sqf += q * fr;
+                sqq += q * q;
+            }
+        }
+        const double V0[6] = {V[0], V[1], V[2], V[3], V[4], V[5]};
+        const double b[3] = {bf[0] - bq[0], bf[1] - bq[1], bf[2] - bq[2]};
+        const int di[3] = {0, 2, 5};
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
+            V[di[a]] += lm * lm;
+        }
+        const double l00 = sqrt(V[0]), l10 = V[1] / l00, l20 = V[3] / l00;
+        const double l11 = sqrt(V[2] - l10 * l10), l21 = (V[4] - l20 * l10) / l11;
+        const double l22 = sqrt(V[5] - l20 * l20 - l21 * l21);
+        const double z0 = b[0] / l00, z1 = (b[1] - l10 * z0) / l11, z2 = (b[2] - l20 * z0 - l21 * z1) / l22;
+        const double y2 = z2 / l22, y1 = (z1 - l21 * y2) / l11, y0 = (z0 - l10 * y1 - l20 * y2) / l00;
+        const double yE[3] = {y0, y1, y2};
+        double xc[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            xc[a] = Xp[a] + (-yE[a]) * sE[a];
+            const double d = Xp[a] - xc[a];
+            acc[2] += d * d;
+            Xc[3 * (size_t)p + a] = xc[a];
+            if (!isfinite(xc[a])) bad = 1.0;
+        }
+        {
+            const double ybf = yE[0] * bf[0] + yE[1] * bf[1] + yE[2] * bf[2];
+            const double ybq = yE[0] * bq[0] + yE[1] * bq[1] + yE[2] * bq[2];
+            const double Vy0 = V0[0] * yE[0] + V0[1] * yE[1] + V0[3] * yE[2];
+            const double Vy1 = V0[1] * yE[0] + V0[2] * yE[1] + V0[4] * yE[2];
+            const double Vy2 = V0[3] * yE[0] + V0[4] * yE[1] + V0[5] * yE[2];
+            const double yVy = yE[0] * Vy0 + yE[1] * Vy1 + yE[2] * Vy2;
+            acc[0] = -(sqf + ybf) + 0.5 * (sqq + 2.0 * ybq + yVy);
+        }
+        for (int o = o0; o < o1; ++o) {
+            const int img = P.obs_img[o];
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+            Lin C;
+            linearize<CM, false, false, false>(cps_c[img], intr_c + 4 * (size_t)P.img_intr[img], xc, uv.x, uv.y,
+                                               P.huber_a, C);
+            acc[1] += C.half_rho;
+            if (!C.ok) cbad = 1.0;
+        }
+        if (!isfinite(acc[0])) bad = 1.0;
+    }
+    wave_sum(acc);
+    bad = wave_max(bad);
+    cbad = wave_max(cbad);
+    constexpr int kW = kGStepThreads / 64;
+    __shared__ double red[kW][kPartT];
+    const int wave = tid >> 6, lane = tid & 63;
+    if (lane == 0) {
+        red[wave][0] = acc[0]; red[wave][1] = acc[1]; red[wave][2] = acc[2];
+        red[wave][3] = bad; red[wave][4] = cbad;
+    }
+    __syncthreads();
+    if (tid < kPartT) {
+        double v = red[0][tid];
+        for (int w = 1; w < kW; ++w) v = tid < 3 ? v + red[w][tid] : fmax(v, red[w][tid]);
+        P.part_t[kPartT * (size_t)(P.n_chunk + blockIdx.x) + tid] = v;
+    }
+}
+
 // fixed-order reduction of the per-block partials
 // 1024 threads: each strides over ~4 partials per list instead of ~16 (the
 // pass is a chain of dependent global loads); fixed order, so deterministic
@@ -1474,7 +1811,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
         s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]);
     }
 #pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_chunk; i += kFinThreads) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
+    for (int i = threadIdx.x; i < P.n_chunk + P.n_gpt; i += kFinThreads) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
 #pragma unroll 4
     for (int i = threadIdx.x; i < n_step_blocks; i += kFinThreads) {
         s[2] += P.part_t[kPartT * i]; s[3] += P.part_t[kPartT * i + 1]; s[4] += P.part_t[kPartT * i + 2];
@@ -1564,6 +1901,24 @@ void ba_fscale(const DevProblem& P, hipStream_t s) {
 
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
               hipStream_t s, unsigned long long* stamps, bool scale_e) {
+    if (P.n_gpt > 0) {
+        const size_t lds = (64 * kZStage + (size_t)P.gz_max) * sizeof(double);
+        if (scale_e)
+            SFM_BY_MODEL(P, {
+                if (lds > 64 * 1024)
+                    SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                hipLaunchKernelGGL((zpoint_kernel<CM, true>), dim3(P.n_gpt), dim3(64), lds, s, P, cp, intr, X, radius);
+            });
+        else
+            SFM_BY_MODEL(P, {
+                if (lds > 64 * 1024)
+                    SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, false>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                hipLaunchKernelGGL((zpoint_kernel<CM, false>), dim3(P.n_gpt), dim3(64), lds, s, P, cp, intr, X, radius);
+            });
+        SFM_HIP(hipGetLastError());
+    }
     if (P.n_chunk <= 0) return;
     // 64-row tiles: 4-point batches (12 panel columns, no k padding) keep LDS
     // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
@@ -1587,12 +1942,17 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
 
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     if (P.n_targets <= 0) return;
-    hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P, vectors_only ? 4 : 0);
+    hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P, vectors_only ? 1 : 0);
     SFM_HIP(hipGetLastError());
     if (P.n_long > 0) {
-        hipLaunchKernelGGL(reduce_seg_kernel, dim3(P.n_lseg), dim3(256), 0, s, P, vectors_only ? 4 : 0);
+        hipLaunchKernelGGL(reduce_seg_kernel, dim3(P.n_lseg), dim3(256), 0, s, P, vectors_only ? 1 : 0);
         SFM_HIP(hipGetLastError());
-        hipLaunchKernelGGL(reduce_long_kernel, dim3(P.n_long), dim3(64), 0, s, P, vectors_only ? 4 : 0);
+        hipLaunchKernelGGL(reduce_long_kernel, dim3(P.n_long), dim3(64), 0, s, P, vectors_only ? 1 : 0);
+        SFM_HIP(hipGetLastError());
+    }
+    // product terms (general points) land on the matrix and rhs targets
+    if (P.n_gpt > 0 && !vectors_only) {
+        hipLaunchKernelGGL(preduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P);
         SFM_HIP(hipGetLastError());
     }
 }
@@ -1633,15 +1993,21 @@ void ba_cand(const DevProblem& P, const double* extr, const double* intr, double
     SFM_HIP(hipGetLastError());
 }
 
-int ba_step_blocks(const DevProblem& P) { return P.n_chunk; }
+int ba_step_blocks(const DevProblem& P) { return P.n_chunk + (P.n_gpt + kGStepThreads - 1) / kGStepThreads; }
 
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
-    const int nb = ba_step_blocks(P);
-    if (nb <= 0) return;
-    SFM_BY_MODEL(P, hipLaunchKernelGGL(step_kernel<CM>, dim3(nb), dim3(kChunkPts), 0, s, P, cp, intr, cp_cand,
-                                       intr_cand, X, X_cand, radius));
-    SFM_HIP(hipGetLastError());
+    if (P.n_chunk > 0) {
+        SFM_BY_MODEL(P, hipLaunchKernelGGL(step_kernel<CM>, dim3(P.n_chunk), dim3(kChunkPts), 0, s, P, cp, intr,
+                                           cp_cand, intr_cand, X, X_cand, radius));
+        SFM_HIP(hipGetLastError());
+    }
+    if (P.n_gpt > 0) {
+        const int nb = (P.n_gpt + kGStepThreads - 1) / kGStepThreads;
+        SFM_BY_MODEL(P, hipLaunchKernelGGL(step_general_kernel<CM>, dim3(nb), dim3(kGStepThreads), 0, s, P, cp, intr,
+                                           cp_cand, intr_cand, X, X_cand, radius));
+        SFM_HIP(hipGetLastError());
+    }
 }
 
 void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq) {

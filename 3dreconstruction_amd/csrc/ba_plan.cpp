@@ -10,9 +10,8 @@
 #include "ba_plan.h"
 
 #include <algorithm>
-#include <cstdlib>
 #include <climits>
-#include <map>
+#include <cstdlib>
 #include <numeric>
 #include <thread>
 
@@ -38,21 +37,124 @@ void parallel_ranges(int64_t n, F&& fn) {
     for (auto& x : th) x.join();
 }
 
-void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
-    pl.cam_blk.assign(P.n_img, -1);
-    pl.intr_blk.assign(P.n_intr, -1);
-    std::vector<char> cu(P.n_img, 0), iu(P.n_intr, 0);
-    for (int64_t o = 0; o < P.n_obs; ++o) {
-        cu[P.obs_img[o]] = 1;
-        iu[P.img_intr[P.obs_img[o]]] = 1;
+// block half-bandwidth of the points' camera spans under the order cam_blk
+int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk) {
+    int32_t D = 0;
+    for (int64_t p = 0; p < P.n_pt; ++p) {
+        int lo = INT_MAX, hi = -1;
+        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+            const int b = cam_blk[P.obs_img[o]];
+            if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+        }
+        if (hi >= 0) D = std::max(D, hi - lo);
     }
+    return D;
+}
+
+// Reverse Cuthill-McKee over the camera co-visibility graph (cameras that
+// share a point are adjacent): a closed orbit, whose first and last images
+// see the same points, gets a band of ~2k blocks instead of the whole RCS.
+// Long tracks contribute a chain of nearest neighbours only.  Returns the new
+// block of every natural block.
+std::vector<int32_t> rcm_order(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int32_t ncam) {
+    std::vector<uint64_t> edges;
+    std::vector<int32_t> cs;
+    for (int64_t p = 0; p < P.n_pt; ++p) {
+        cs.clear();
+        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o)
+            if (cam_blk[P.obs_img[o]] >= 0) cs.push_back(cam_blk[P.obs_img[o]]);
+        std::sort(cs.begin(), cs.end());
+        cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+        const size_t n = cs.size(), reach = n <= 24 ? n : 4;
+        for (size_t a = 0; a < n; ++a)
+            for (size_t b = a + 1; b < std::min(n, a + 1 + reach); ++b) {
+                edges.push_back(((uint64_t)cs[a] << 32) | (uint32_t)cs[b]);
+                edges.push_back(((uint64_t)cs[b] << 32) | (uint32_t)cs[a]);
+            }
+    }
+    std::sort(edges.begin(), edges.end());
+    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+    std::vector<int64_t> ptr(ncam + 1, 0);
+    for (uint64_t e : edges) ptr[(e >> 32) + 1]++;
+    for (int32_t c = 0; c < ncam; ++c) ptr[c + 1] += ptr[c];
+    std::vector<int32_t> adj(edges.size());
+    for (size_t k = 0; k < edges.size(); ++k) adj[k] = (int32_t)(edges[k] & 0xffffffffu);
+    auto deg = [&](int32_t c) { return ptr[c + 1] - ptr[c]; };
+    std::vector<int32_t> seq;
+    std::vector<char> seen(ncam, 0);
+    auto bfs = [&](int32_t s, std::vector<int32_t>& out, std::vector<char>& mark) {
+        out.clear();
+        out.push_back(s);
+        mark[s] = 1;
+        std::vector<int32_t> nb;
+        for (size_t h = 0; h < out.size(); ++h) {
+            const int32_t c = out[h];
+            nb.assign(adj.begin() + ptr[c], adj.begin() + ptr[c + 1]);
+            std::stable_sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) { return deg(a) < deg(b); });
+            for (int32_t n : nb)
+                if (!mark[n]) { mark[n] = 1; out.push_back(n); }
+        }
+    };
+    std::vector<int32_t> byd(ncam);
+    std::iota(byd.begin(), byd.end(), 0);
+    std::stable_sort(byd.begin(), byd.end(), [&](int32_t a, int32_t b) { return deg(a) < deg(b); });
+    std::vector<int32_t> comp;
+    for (int32_t s0 : byd) {
+        if (seen[s0]) continue;
+        // pseudo-peripheral start: the last-reached node of a BFS from s0
+        std::vector<char> tmp(seen);
+        bfs(s0, comp, tmp);
+        int32_t s = comp.back();
+        bfs(s, comp, seen);
+        seq.insert(seq.end(), comp.begin(), comp.end());
+    }
+    std::reverse(seq.begin(), seq.end());
+    std::vector<int32_t> newpos(ncam);
+    for (int32_t k = 0; k < ncam; ++k) newpos[seq[k]] = k;
+    return newpos;
+}
+
+}  // namespace
+
+std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, int32_t* D_out) {
+    std::vector<int32_t> cam_blk(P.n_img, -1);
+    std::vector<char> used(P.n_img, 0);
+    for (int64_t o = 0; o < P.n_obs; ++o) used[P.obs_img[o]] = 1;
+    int32_t ncam = 0;
     for (int i = 0; i < P.n_img; ++i)
-        if (cu[i] && i != P.const_img) { pl.cam_blk[i] = pl.ncam++; pl.blk_img.push_back(i); }
+        if (used[i] && i != P.const_img) cam_blk[i] = ncam++;
+    int32_t D = half_bandwidth(P, cam_blk);
+    // reorder only when the image order does not give a band the BCR solver
+    // takes, and the co-visibility graph is small enough to build quickly
+    if (D > kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20 && !std::getenv("SFM_BA_NO_RCM")) {
+        const std::vector<int32_t> pos = rcm_order(P, cam_blk, ncam);
+        std::vector<int32_t> alt(cam_blk);
+        for (auto& b : alt)
+            if (b >= 0) b = pos[b];
+        const int32_t D2 = half_bandwidth(P, alt);
+        if (D2 < D) { cam_blk.swap(alt); D = D2; }
+    }
+    if (ncam_out) *ncam_out = ncam;
+    if (D_out) *D_out = D;
+    return cam_blk;
+}
+
+namespace {
+
+void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
+    pl.cam_blk = camera_blocks(P, &pl.ncam, &pl.D);
+    pl.blk_img.assign(pl.ncam, -1);
+    for (int i = 0; i < P.n_img; ++i)
+        if (pl.cam_blk[i] >= 0) pl.blk_img[pl.cam_blk[i]] = i;
+    pl.intr_blk.assign(P.n_intr, -1);
+    std::vector<char> iu(P.n_intr, 0);
+    for (int64_t o = 0; o < P.n_obs; ++o) iu[P.img_intr[P.obs_img[o]]] = 1;
     for (int q = 0; q < P.n_intr; ++q)
         if (iu[q]) { pl.intr_blk[q] = pl.nintr++; pl.blk_intr.push_back(q); }
     pl.nb = 6LL * pl.ncam;
     pl.na = 4LL * pl.nintr;
     pl.nF = pl.nb + pl.na;
+    pl.nFB = pl.ncam + pl.nintr;
     pl.img_colc.assign(P.n_img, -1);
     pl.img_coli.assign(P.n_img, -1);
     pl.img_intr.assign(P.img_intr, P.img_intr + P.n_img);
@@ -92,6 +194,35 @@ void partition_points(const sfm_ba_problem& P, const std::vector<int32_t>& cam_b
     }
 }
 
+namespace {
+
+// A point goes through the Schur chunk kernel when its F rows fit a chunk
+// tile and its observations one wave batch; everything else is a general
+// point (Ceres takes any track length, any number of camera
+// intrinsics and repeated (point, image) observations).
+bool chunkable(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t p) {
+    const int64_t o0 = P.pt_offsets[p], o1 = P.pt_offsets[p + 1];
+    if (o1 - o0 > kSubObs) return false;
+    int nc = 0, ni = 0;
+    int32_t intrs[kIntrSlots];
+    for (int64_t o = o0; o < o1; ++o) {
+        const int img = P.obs_img[o];
+        for (int64_t o2 = o0; o2 < o; ++o2)
+            if (P.obs_img[o2] == img) return false;      // the same image twice
+        if (pl.cam_blk[img] >= 0) ++nc;
+        const int q = P.img_intr[img];
+        bool have = false;
+        for (int t = 0; t < ni; ++t) have |= intrs[t] == q;
+        if (!have) {
+            if (ni == kIntrSlots) return false;
+            intrs[ni++] = q;
+        }
+    }
+    return o1 - o0 <= kCamSlots && 6 * nc + 4 * ni <= kTileRowsUsed;
+}
+
+}  // namespace
+
 void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     SFM_REQUIRE(P.n_img >= 1 && P.n_intr >= 1 && P.n_pt >= 0 && P.n_obs >= 0 &&
                     P.pt_offsets && (P.n_obs == 0 || (P.obs_img && P.obs_uv)) && P.img_intr,
@@ -116,30 +247,28 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
     pl.rank = rank; pl.world = world;
     active_sets(P, pl);
-    SFM_REQUIRE(pl.nintr <= 4, SFM_ERR_UNSUPPORTED,
-                "%d active intrinsic blocks; this build supports up to 4 (dense arrow)", pl.nintr);
-
-    // band half-width (blocks) over active cameras; duplicate views rejected
-    int32_t D = 0;
-    for (int64_t p = 0; p < P.n_pt; ++p) {
-        int lo = INT_MAX, hi = -1;
-        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
-            for (int64_t o2 = P.pt_offsets[p]; o2 < o; ++o2)
-                SFM_REQUIRE(P.obs_img[o2] != P.obs_img[o], SFM_ERR_UNSUPPORTED,
-                            "point %lld observed twice by image %d", (long long)p, P.obs_img[o]);
-            const int b = pl.cam_blk[P.obs_img[o]];
-            if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
-        }
-        if (hi >= 0) D = std::max(D, hi - lo);
+    // RCS storage and solver, identical on every rank: the block-banded form
+    // (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
+    // and a few intrinsics blocks, else dense (blocked Cholesky, ba_dense.hip)
+    pl.dense = !(pl.D <= kBandMaxD && 1 + 4 * pl.nintr <= 32) || std::getenv("SFM_BA_DENSE") != nullptr;
+    if (pl.dense) {
+        SFM_REQUIRE(pl.nF <= 40000, SFM_ERR_UNSUPPORTED, "dense reduced camera system of %lld columns",
+                    (long long)pl.nF);
+        pl.n_sdense = pl.nF * pl.nF;
     }
-    pl.D = D;
 
     partition_points(P, pl.cam_blk, world, pl.order, pl.bounds);
 
-    // ---- shard arrays ------------------------------------------------------
+    // ---- shard arrays: chunkable points first, then general points ---------
     const int64_t b0 = pl.bounds[rank], b1 = pl.bounds[rank + 1];
+    {
+        std::vector<int64_t> cpts, gpts;
+        for (int64_t k = b0; k < b1; ++k) (chunkable(P, pl, pl.order[k]) ? cpts : gpts).push_back(pl.order[k]);
+        pl.n_cpt = (int64_t)cpts.size();
+        pl.spt_global = std::move(cpts);
+        pl.spt_global.insert(pl.spt_global.end(), gpts.begin(), gpts.end());
+    }
     pl.n_spt = b1 - b0;
-    pl.spt_global.assign(pl.order.begin() + b0, pl.order.begin() + b1);
     pl.pt_off.assign(pl.n_spt + 1, 0);
     for (int64_t k = 0; k < pl.n_spt; ++k) {
         const int64_t p = pl.spt_global[k];
@@ -162,7 +291,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
     });
 
-    // ---- Schur chunks --------------------------------------------------------
+    // ---- Schur chunks over [0, n_cpt) ------------------------------------------
     // Greedy over shard points: a chunk's F blocks (camera 6 rows, intrinsics 4
     // rows) must fit `cap` rows of its tile: 64 (4x4 MFMA tiles, -Zw on the
     // VALU) or 76 (5x5 tiles, -Zw in row 79).  The 64-row form does 2/3 of the
@@ -174,11 +303,19 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // points: the Schur pass takes about one chunk's latency once the chunks
     // fit in one round, so 2048 chunks (8 waves per CU) keep it dividing by N.
     constexpr int64_t kTargetChunks = 2048;
-    int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_spt + kTargetChunks - 1) / kTargetChunks));
+    int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
     if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));   // tuning override
+    const int32_t ncp = (int32_t)pl.n_cpt;
+    auto point_flops = [](int64_t rows, int64_t nobs) {
+        // algorithmic flops: the symmetric Z Z' over the
+        // point's own F rows (r(r+1)/2 entries x 3 x 2 = 3 r (r+1)), the
+        // linearisation (600 per observation) and the point block (V, its
+        // factor, M = Jx L^-T, Z = J' M: 180 per observation + 30)
+        return 3 * rows * (rows + 1) + 780 * nobs + 30;
+    };
     auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, std::vector<int32_t>& slot_out) -> int64_t {
         int64_t flops = 0;
-        slot_out.assign(pl.n_sobs, 0);
+        slot_out.assign(pl.pt_off[ncp], 0);
         ChunkDesc cd{};
         std::vector<int> cams, intrs, dcams;  // F-slot images / intrinsics, staged images
         // O(1) membership for the open chunk: image -> F slot / staged index,
@@ -216,11 +353,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             size_t size() const { return (size_t)n; }
             bool has(int x) const { return std::find(v, v + n, x) != v + n; }
         };
-        if (pl.n_spt > 0) reset(0);
-        for (int32_t k = 0; k < (int32_t)pl.n_spt; ++k) {
+        if (ncp > 0) reset(0);
+        for (int32_t k = 0; k < ncp; ++k) {
             const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
-            SFM_REQUIRE(nobs <= kSubObs, SFM_ERR_UNSUPPORTED, "point with %d observations (> %d)",
-                        nobs, kSubObs);
             Small pc, pi, pd;
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
                 const int img = pl.obs_img[s];
@@ -230,10 +365,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 if (!pi.has(q)) pi.push_back(q);
             }
             const int own = 6 * (int)pc.size() + 4 * (int)pi.size();
-            SFM_REQUIRE(own <= cap && (int)pd.size() <= kCamSlots && (int)pi.size() <= kIntrSlots,
-                        SFM_ERR_UNSUPPORTED,
-                        "point %lld spans %d F rows / %d images (> %d / %d): track too long for this build",
-                        (long long)pl.spt_global[k], own, (int)pd.size(), cap, kCamSlots);
+            SFM_REQUIRE(own <= cap, SFM_ERR_INVALID_ARG, "internal: chunk point over %d rows", cap);
             int add = 0, add_slots = 0, add_d = 0, add_i = 0;
             for (int img : pc) if (cam_slot[img] < 0) { add += 6; ++add_slots; }
             for (int q : pi) if (intr_idx[q] < 0) { add += 4; ++add_slots; ++add_i; }
@@ -277,29 +409,26 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 const int img = pl.obs_img[s];
                 slot_out[s] = dcam_idx[img] | (intr_idx[P.img_intr[img]] << 8);
             }
-            // algorithmic flops: the symmetric Z Z' over the
-            // point's own F rows (r(r+1)/2 entries x 3 x 2 = 3 r (r+1)), the
-            // linearisation (600 per observation) and the point block (V, its
-            // factor, M = Jx L^-T, Z = J' M: 180 per observation + 30)
-            const int64_t nfp = own;
-            flops += 3LL * nfp * (nfp + 1) + 780LL * nobs + 30;
+            flops += point_flops(own, nobs);
         }
-        if (pl.n_spt > 0) close((int32_t)pl.n_spt);
+        if (ncp > 0) close(ncp);
         return flops;
     };
     int max_own = 0, max_obs = 0;
-    for (int64_t k = 0; k < pl.n_spt; ++k) {
+    for (int64_t k = 0; k < ncp; ++k) {
         max_obs = std::max(max_obs, pl.pt_off[k + 1] - pl.pt_off[k]);
         int nc = 0;
-        std::vector<int> pi;
+        int32_t pi[kIntrSlots];
+        int ni = 0;
         for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
             if (pl.cam_blk[pl.obs_img[s]] >= 0) ++nc;
             const int q = P.img_intr[pl.obs_img[s]];
-            if (std::find(pi.begin(), pi.end(), q) == pi.end()) pi.push_back(q);
+            if (std::find(pi, pi + ni, q) == pi + ni) pi[ni++] = q;
         }
-        max_own = std::max(max_own, 6 * nc + 4 * (int)pi.size());
+        max_own = std::max(max_own, 6 * nc + 4 * ni);
     }
     int64_t flops = 0;
+    std::vector<int32_t> cslot;
     pl.tile_nt = 5;
     // the 64-row kernel walks 48-observation batches (ba_kernels.hip)
     if (max_own <= 64 && max_obs <= 48 && !std::getenv("SFM_BA_TILE80")) {
@@ -322,12 +451,90 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         if (rc4 != SFM_OK) throw SfmError{rc4};
         if (rc5 != SFM_OK) throw SfmError{rc5};
         if (c4.size() * 4 <= c5.size() * 5) {
-            pl.tile_nt = 4; pl.chunks.swap(c4); pl.obs_slot.swap(s4); flops = f4;
+            pl.tile_nt = 4; pl.chunks.swap(c4); cslot.swap(s4); flops = f4;
         } else {
-            pl.chunks.swap(c5); pl.obs_slot.swap(s5); flops = f5;
+            pl.chunks.swap(c5); cslot.swap(s5); flops = f5;
         }
     } else {
-        flops = make_chunks(kTileRowsUsed, pl.chunks, pl.obs_slot);
+        flops = make_chunks(kTileRowsUsed, pl.chunks, cslot);
+    }
+    // Chunks pay off when camera windows are shared by many consecutive
+    // points (sequences, orbits); under random visibility a chunk holds one
+    // or two points and its tile traffic exceeds the general path's
+    if (pl.n_cpt > 0 && (int64_t)pl.chunks.size() * 4 > pl.n_cpt) {
+        pl.chunks.clear();
+        cslot.clear();
+        pl.n_cpt = 0;
+        flops = 0;
+    }
+    std::copy(cslot.begin(), cslot.end(), pl.obs_slot.begin());
+    pl.n_gpt = pl.n_spt - pl.n_cpt;
+    // a general point's observations in image order, so that repeated views
+    // of one image are adjacent (the Z kernel sums runs of one camera block)
+    parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+        std::vector<int32_t> idx;
+        std::vector<int32_t> img;
+        std::vector<double> uv;
+        for (int64_t g = g0; g < g1; ++g) {
+            const int64_t k = pl.n_cpt + g;
+            const int32_t s0 = pl.pt_off[k], n = pl.pt_off[k + 1] - s0;
+            idx.resize(n);
+            std::iota(idx.begin(), idx.end(), 0);
+            std::stable_sort(idx.begin(), idx.end(),
+                             [&](int32_t a, int32_t b) { return pl.obs_img[s0 + a] < pl.obs_img[s0 + b]; });
+            img.assign(pl.obs_img.begin() + s0, pl.obs_img.begin() + s0 + n);
+            uv.assign(pl.obs_uv.begin() + 2 * s0, pl.obs_uv.begin() + 2 * (s0 + n));
+            for (int32_t q = 0; q < n; ++q) {
+                pl.obs_img[s0 + q] = img[idx[q]];
+                pl.obs_uv[2 * (s0 + q)] = uv[2 * idx[q]];
+                pl.obs_uv[2 * (s0 + q) + 1] = uv[2 * idx[q] + 1];
+            }
+        }
+    });
+
+    // ---- general points: their F blocks and Z buffer layout --------------------
+    // blocks in F-column order; obs_slot = local camera block (0xffff: constant
+    // image) | local intrinsics block << 16
+    pl.gblk_off.assign(pl.n_gpt + 1, 0);
+    pl.gz_off.assign(pl.n_gpt + 1, 0);
+    pl.gblk_col.clear();
+    pl.gblk_z.clear();
+    {
+        std::vector<int32_t> cols;
+        for (int64_t g = 0; g < pl.n_gpt; ++g) {
+            const int64_t k = pl.n_cpt + g;
+            cols.clear();
+            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                const int img = pl.obs_img[s];
+                if (pl.img_colc[img] >= 0) cols.push_back(pl.img_colc[img]);
+                cols.push_back(pl.img_coli[img]);
+            }
+            std::sort(cols.begin(), cols.end());
+            cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+            SFM_REQUIRE(cols.size() < 0xffff, SFM_ERR_UNSUPPORTED, "point with %zu parameter blocks", cols.size());
+            int32_t z = 0;
+            for (int32_t c : cols) {
+                pl.gblk_col.push_back(c);
+                pl.gblk_z.push_back(z);
+                z += 3 * (c < pl.nb ? 6 : 4);
+            }
+            pl.gblk_off[g + 1] = (int32_t)pl.gblk_col.size();
+            pl.gz_off[g + 1] = pl.gz_off[g] + z + 3;   // + w = L^-1 g_E
+            pl.gz_max = std::max<int64_t>(pl.gz_max, z + 3);
+            SFM_REQUIRE(z + 3 <= kZMaxDoubles, SFM_ERR_UNSUPPORTED,
+                        "point %lld observed by %zu parameter blocks (more than the %d rows one wavefront eliminates)",
+                        (long long)pl.spt_global[k], cols.size(), kZMaxDoubles / 3);
+            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                const int img = pl.obs_img[s];
+                const int32_t cb = pl.img_colc[img] >= 0
+                                       ? (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_colc[img]) - cols.begin())
+                                       : 0xffff;
+                const int32_t ib = (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_coli[img]) - cols.begin());
+                pl.obs_slot[s] = cb | (ib << 16);
+            }
+            flops += point_flops(z / 3, pl.pt_off[k + 1] - pl.pt_off[k]);
+        }
+        pl.n_z = pl.gz_off[pl.n_gpt];
     }
     pl.schur_flops = flops;
     pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +
@@ -378,94 +585,166 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     }
 
     // ---- reduce plan -----------------------------------------------------------
-    const int Dp = pl.D + 1;
-    pl.n_sband = (int64_t)pl.ncam * Dp * 36;
-    pl.n_sarrow = (int64_t)pl.nintr * pl.ncam * 24;
-    pl.n_scorner = (int64_t)pl.nintr * pl.nintr * 16;
-    // chunk slot lookups: block -> (chunk, row)
-    std::map<int64_t, std::vector<ReduceTerm>> band, arrow, corner, rhs;  // keyed by target
+    // Every matrix block (a, b), a >= b in F-block order (cameras, then
+    // intrinsics), collects sum terms (image Gram slices first, then chunk tile
+    // sub-blocks in chunk order) and product terms (general points in order);
+    // vectors (rhs, bF, cnF) likewise per block.  Terms are gathered as (key,
+    // term) pairs and stably sorted by key: a fixed order, so every sum is
+    // bit-reproducible.
+    const int32_t nFB = pl.nFB;
+    auto fb_of_col = [&](int64_t col) -> int32_t {
+        return col < pl.nb ? (int32_t)(col / 6) : (int32_t)(pl.ncam + (col - pl.nb) / 4);
+    };
+    auto col_of_fb = [&](int32_t b) -> int64_t { return b < pl.ncam ? 6LL * b : pl.nb + 4LL * (b - pl.ncam); };
+    auto size_of_fb = [&](int32_t b) { return b < pl.ncam ? 6 : 4; };
+    std::vector<std::pair<int64_t, ReduceTerm>> mterms, vterms;
+    std::vector<std::pair<int64_t, PTerm>> mprod, vprod;
+    // image Gram blocks (kGramSeg partial slices per image)
+    auto add_u = [&](std::vector<std::pair<int64_t, ReduceTerm>>& out, int64_t key, int32_t kind, int img,
+                     int16_t ro, int16_t co) {
+        for (int g = 0; g < kGramSeg; ++g) out.push_back({key, ReduceTerm{kind, img * kGramSeg + g, ro, co, 1.f}});
+    };
+    for (int img = 0; img < P.n_img; ++img) {
+        const int cb = pl.cam_blk[img], q = pl.intr_blk[P.img_intr[img]];
+        if (pl.img_obs_ptr[img + 1] == pl.img_obs_ptr[img] && cb < 0 && q < 0) continue;
+        const int32_t fq = q >= 0 ? pl.ncam + q : -1;
+        if (cb >= 0) {
+            add_u(mterms, (int64_t)cb * nFB + cb, kSrcU, img, 0, 0);
+            if (fq >= 0) add_u(mterms, (int64_t)fq * nFB + cb, kSrcU, img, 6, 0);
+            add_u(vterms, cb, kSrcUb, img, 0, 0);
+        }
+        if (fq >= 0) {
+            add_u(mterms, (int64_t)fq * nFB + fq, kSrcU, img, 6, 6);
+            add_u(vterms, fq, kSrcUb, img, 6, 0);
+        }
+    }
+    // cnF: per block, image slices only (never a tile term)
+    std::vector<std::pair<int64_t, ReduceTerm>> cterms;
+    for (const auto& t : vterms) {
+        ReduceTerm q = t.second;
+        q.kind = kSrcUcn;
+        cterms.push_back({t.first, q});
+    }
+    // chunk tiles
     for (int32_t c = 0; c < (int32_t)pl.chunks.size(); ++c) {
         const ChunkDesc& cd = pl.chunks[c];
         for (int a = 0; a < cd.n_slots; ++a) {
+            const int32_t fa = fb_of_col(cd.slot_col[a]);
             // rhs contribution (-Z w) from tile row 79
-            rhs[cd.slot_col[a]].push_back(ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f});
+            vterms.push_back({fa, ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}});
             for (int b = 0; b < cd.n_slots; ++b) {
-                const bool ac = cd.slot_img[a] >= 0, bc = cd.slot_img[b] >= 0;
-                if (ac && bc) {
-                    const int ia = pl.cam_blk[cd.slot_img[a]], ib = pl.cam_blk[cd.slot_img[b]];
-                    if (ia < ib) continue;
-                    band[(int64_t)ia * Dp + (ia - ib)].push_back(
-                        ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
-                } else if (!ac && bc) {
-                    const int k = pl.intr_blk[cd.slot_intr[a]], ib = pl.cam_blk[cd.slot_img[b]];
-                    arrow[(int64_t)k * pl.ncam + ib].push_back(
-                        ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
-                } else if (!ac && !bc) {
-                    const int k = pl.intr_blk[cd.slot_intr[a]], l = pl.intr_blk[cd.slot_intr[b]];
-                    corner[(int64_t)k * pl.nintr + l].push_back(
-                        ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
-                }
+                const int32_t fb = fb_of_col(cd.slot_col[b]);
+                if (fa < fb) continue;
+                mterms.push_back({(int64_t)fa * nFB + fb,
+                                  ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f}});
             }
         }
     }
-    auto emit = [&](int32_t kind, int64_t dst, int rows, int cols, int ld, std::vector<ReduceTerm>* tl,
-                    std::vector<ReduceTerm> extra) {
+    // general points
+    for (int64_t g = 0; g < pl.n_gpt; ++g) {
+        const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
+        const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
+        for (int32_t a = k0; a < k1; ++a) {
+            const int32_t fa = fb_of_col(pl.gblk_col[a]);
+            vprod.push_back({fa, PTerm{zb + pl.gblk_z[a], wz}});
+            for (int32_t b = k0; b <= a; ++b)
+                mprod.push_back({(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}});
+        }
+    }
+    auto by_key = [](const auto& x, const auto& y) { return x.first < y.first; };
+    std::stable_sort(mterms.begin(), mterms.end(), by_key);
+    std::stable_sort(vterms.begin(), vterms.end(), by_key);
+    std::stable_sort(cterms.begin(), cterms.end(), by_key);
+    std::stable_sort(mprod.begin(), mprod.end(), by_key);
+    std::stable_sort(vprod.begin(), vprod.end(), by_key);
+
+    const int Dp = pl.D + 1;
+    if (!pl.dense) {
+        pl.n_sband = (int64_t)pl.ncam * Dp * 36;
+        pl.n_sarrow = (int64_t)pl.nintr * pl.ncam * 24;
+        pl.n_scorner = (int64_t)pl.nintr * pl.nintr * 16;
+    }
+    size_t im = 0, ipm = 0, iv = 0, ipv = 0, ic = 0;
+    auto emit = [&](int64_t key, int32_t kind, int64_t dst, int rows, int cols, int ld,
+                    std::vector<std::pair<int64_t, ReduceTerm>>& st, size_t& is,
+                    std::vector<std::pair<int64_t, PTerm>>* pt, size_t* ip) {
         ReduceTarget t{};
         t.dst = dst; t.dst_kind = kind; t.rows = rows; t.cols = cols; t.ld = ld;
+        while (is < st.size() && st[is].first < key) ++is;   // (keys with no target: none by construction)
         t.c_begin = (int32_t)pl.terms.size();
-        for (const auto& e : extra)   // image Gram blocks come in kGramSeg partial slices
-            for (int g = 0; g < (e.kind == kSrcTile ? 1 : kGramSeg); ++g) {
-                ReduceTerm q = e;
-                if (e.kind != kSrcTile) q.index = e.index * kGramSeg + g;
-                pl.terms.push_back(q);
-            }
-        if (tl) for (const auto& e : *tl) pl.terms.push_back(e);
+        for (; is < st.size() && st[is].first == key; ++is) pl.terms.push_back(st[is].second);
         t.c_end = (int32_t)pl.terms.size();
+        t.p_begin = t.p_end = (int32_t)pl.pterms.size();
+        if (pt) {
+            while (*ip < pt->size() && (*pt)[*ip].first < key) ++*ip;
+            for (; *ip < pt->size() && (*pt)[*ip].first == key; ++*ip) pl.pterms.push_back((*pt)[*ip].second);
+            t.p_end = (int32_t)pl.pterms.size();
+        }
         pl.targets.push_back(t);
     };
-    for (int i = 0; i < pl.ncam; ++i) {
-        const int img = pl.blk_img[i];
-        for (int d = 0; d <= std::min(pl.D, i); ++d) {
-            auto it = band.find((int64_t)i * Dp + d);
-            std::vector<ReduceTerm> ex;
-            if (d == 0) ex.push_back(ReduceTerm{kSrcU, img, 0, 0, 1.f});
-            emit(0, ((int64_t)i * Dp + d) * 36, 6, 6, 6, it == band.end() ? nullptr : &it->second, ex);
+    if (!pl.dense) {
+        // every band block (i, i-d), d <= D, then the arrow and the corner, in
+        // key order within each family
+        std::vector<std::pair<int64_t, std::pair<int32_t, int64_t>>> tl;   // key -> (kind, dst)
+        for (int i = 0; i < pl.ncam; ++i)
+            for (int d = std::min(pl.D, i); d >= 0; --d)
+                tl.push_back({(int64_t)i * nFB + (i - d), {kDstBand, ((int64_t)i * Dp + d) * 36}});
+        for (int k = 0; k < pl.nintr; ++k)
+            for (int i = 0; i < pl.ncam; ++i)
+                tl.push_back({(int64_t)(pl.ncam + k) * nFB + i, {kDstArrow, ((int64_t)k * pl.ncam + i) * 24}});
+        for (int k = 0; k < pl.nintr; ++k)
+            for (int l = 0; l < pl.nintr; ++l)
+                tl.push_back({(int64_t)(pl.ncam + std::max(k, l)) * nFB + pl.ncam + std::min(k, l),
+                              {kDstCorner, ((int64_t)k * pl.nintr + l) * 16}});
+        std::stable_sort(tl.begin(), tl.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        // the corner is stored whole: block (k, l) with k < l is the transpose
+        // of (l, k) and is gathered separately with swapped source offsets
+        for (size_t x = 0; x < tl.size(); ++x) {
+            const int64_t key = tl[x].first;
+            const int32_t kind = tl[x].second.first;
+            const int64_t dst = tl[x].second.second;
+            if (kind == kDstCorner) {
+                const int k = (int)(dst / 16) / pl.nintr, l = (int)(dst / 16) % pl.nintr;
+                if (k < l) {
+                    // transpose of the (l, k) block: same terms, row/column swapped
+                    const size_t t0 = pl.terms.size(), p0 = pl.pterms.size();
+                    size_t js = 0, jp = 0;
+                    emit(key, kind, dst, 4, 4, 4, mterms, js, &mprod, &jp);
+                    for (size_t q = t0; q < pl.terms.size(); ++q) std::swap(pl.terms[q].roff, pl.terms[q].coff);
+                    for (size_t q = p0; q < pl.pterms.size(); ++q) std::swap(pl.pterms[q].za, pl.pterms[q].zb);
+                    continue;
+                }
+                emit(key, kind, dst, 4, 4, 4, mterms, im, &mprod, &ipm);
+                continue;
+            }
+            const int rows = kind == kDstBand ? 6 : 4;
+            emit(key, kind, dst, rows, 6, 6, mterms, im, &mprod, &ipm);
+        }
+    } else {
+        // dense: every block that receives a term (the rest stays zero)
+        std::vector<int64_t> keys;
+        for (const auto& t : mterms) keys.push_back(t.first);
+        for (const auto& t : mprod) keys.push_back(t.first);
+        std::sort(keys.begin(), keys.end());
+        keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+        for (int64_t key : keys) {
+            const int32_t a = (int32_t)(key / nFB), b = (int32_t)(key % nFB);
+            emit(key, kDstDense, col_of_fb(a) * pl.nF + col_of_fb(b), size_of_fb(a), size_of_fb(b), (int32_t)pl.nF,
+                 mterms, im, &mprod, &ipm);
         }
     }
-    for (int k = 0; k < pl.nintr; ++k)
-        for (int i = 0; i < pl.ncam; ++i) {
-            const int img = pl.blk_img[i];
-            auto it = arrow.find((int64_t)k * pl.ncam + i);
-            std::vector<ReduceTerm> ex;
-            if (pl.intr_blk[P.img_intr[img]] == k) ex.push_back(ReduceTerm{kSrcU, img, 6, 0, 1.f});
-            emit(1, ((int64_t)k * pl.ncam + i) * 24, 4, 6, 6, it == arrow.end() ? nullptr : &it->second, ex);
-        }
-    for (int k = 0; k < pl.nintr; ++k)
-        for (int l = 0; l < pl.nintr; ++l) {
-            auto it = corner.find((int64_t)k * pl.nintr + l);
-            std::vector<ReduceTerm> ex;
-            if (k == l)
-                for (int img = 0; img < P.n_img; ++img)
-                    if (pl.intr_blk[P.img_intr[img]] == k) ex.push_back(ReduceTerm{kSrcU, img, 6, 6, 1.f});
-            emit(2, ((int64_t)k * pl.nintr + l) * 16, 4, 4, 4, it == corner.end() ? nullptr : &it->second, ex);
-        }
-    // vectors: rhs = bF - Z w, bF, cnF
-    for (int vk = 3; vk <= 5; ++vk) {
-        for (int i = 0; i < pl.ncam; ++i) {
-            const int img = pl.blk_img[i];
-            std::vector<ReduceTerm> ex{ReduceTerm{vk == 5 ? kSrcUcn : kSrcUb, img, 0, 0, 1.f}};
-            auto it = rhs.find(6LL * i);
-            emit(vk, 6LL * i, 6, 1, 1, (vk == 3 && it != rhs.end()) ? &it->second : nullptr, ex);
-        }
-        for (int k = 0; k < pl.nintr; ++k) {
-            std::vector<ReduceTerm> ex;
-            for (int img = 0; img < P.n_img; ++img)
-                if (pl.intr_blk[P.img_intr[img]] == k)
-                    ex.push_back(ReduceTerm{vk == 5 ? kSrcUcn : kSrcUb, img, 6, 0, 1.f});
-            auto it = rhs.find(pl.nb + 4LL * k);
-            emit(vk, pl.nb + 4LL * k, 4, 1, 1, (vk == 3 && it != rhs.end()) ? &it->second : nullptr, ex);
-        }
+    // vectors: rhs = bF - Z w, bF, cnF, per F block in order
+    for (int32_t fb = 0; fb < nFB; ++fb)
+        emit(fb, kDstRhs, col_of_fb(fb), size_of_fb(fb), 1, 1, vterms, iv, &vprod, &ipv);
+    {
+        // bF: the image slices of vterms only (no tile, no product term)
+        std::vector<std::pair<int64_t, ReduceTerm>> bterms;
+        for (const auto& t : vterms)
+            if (t.second.kind == kSrcUb) bterms.push_back(t);
+        size_t ib = 0;
+        for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstBF, col_of_fb(fb), size_of_fb(fb), 1, 1, bterms, ib, nullptr, nullptr);
     }
+    for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstCnF, col_of_fb(fb), size_of_fb(fb), 1, 1, cterms, ic, nullptr, nullptr);
 }
 
 }  // namespace sfm
@@ -475,17 +754,36 @@ extern "C" int sfm_ba_partition(const sfm_ba_problem* prob, int32_t world_size, 
     using namespace sfm;
     return guarded([&] {
         SFM_REQUIRE(prob && order && bounds && world_size >= 1, SFM_ERR_INVALID_ARG, "bad arguments");
-        BAHostPlan tmp;
-        std::vector<int32_t> cam_blk(prob->n_img, -1);
-        int nc = 0;
-        std::vector<char> used(prob->n_img, 0);
-        for (int64_t o = 0; o < prob->n_obs; ++o) used[prob->obs_img[o]] = 1;
-        for (int i = 0; i < prob->n_img; ++i)
-            if (used[i] && i != prob->const_img) cam_blk[i] = nc++;
+        const std::vector<int32_t> cam_blk = camera_blocks(*prob, nullptr, nullptr);
         std::vector<int64_t> ord, bnd;
         partition_points(*prob, cam_blk, world_size, ord, bnd);
         std::copy(ord.begin(), ord.end(), order);
         std::copy(bnd.begin(), bnd.end(), bounds);
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_ba_describe(const sfm_ba_problem* prob, int32_t rank, int32_t world_size,
+                               sfm_ba_plan_shape* out) {
+    using namespace sfm;
+    return guarded([&] {
+        SFM_REQUIRE(prob && out && world_size >= 1 && rank >= 0 && rank < world_size, SFM_ERR_INVALID_ARG,
+                    "bad arguments");
+        BAHostPlan h;
+        build_plan(*prob, rank, world_size, h);
+        *out = sfm_ba_plan_shape{};
+        out->n_chunks = (int32_t)h.chunks.size();
+        out->band_blocks = h.D;
+        out->dense = h.dense ? 1 : 0;
+        out->n_cam_active = h.ncam;
+        out->n_intr_active = h.nintr;
+        out->tile_rows = 16 * h.tile_nt;
+        out->n_chunk_pts = h.n_cpt;
+        out->n_general_pts = h.n_gpt;
+        out->rcs_dim = h.nF;
+        out->n_targets = (int64_t)h.targets.size();
+        out->n_terms = (int64_t)h.terms.size();
+        out->n_pterms = (int64_t)h.pterms.size();
         return SFM_OK;
     });
 }

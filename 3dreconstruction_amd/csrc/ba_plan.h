@@ -24,8 +24,22 @@ struct BAHostPlan {
     std::vector<int64_t> order, bounds;  // sorted points / rank ranges
     int32_t rank = 0, world = 1;
 
+    int32_t nFB = 0;                 // F blocks: cameras 0..ncam-1, intrinsics ncam..
+    bool dense = false;              // RCS storage + solver: dense (true) or band + arrow (BCR)
+    int64_t n_sdense = 0;            // nF * nF when dense
+
     // ---- shard ------------------------------------------------------------
+    // Shard points [0, n_cpt) are handled by Schur chunks (tile rows, LDS
+    // staging); [n_cpt, n_spt) are general points (any track length,
+    // duplicate views, many intrinsics), one wavefront each, whose
+    // eliminated rows Z go to a buffer and reach the RCS as product terms.
     int64_t n_spt = 0, n_sobs = 0;
+    int64_t n_cpt = 0, n_gpt = 0;
+    std::vector<int32_t> gblk_off;   // [n_gpt+1] block range of a general point
+    std::vector<int32_t> gblk_col;   // F column of each of its blocks (6 rows: camera, 4: intrinsics)
+    std::vector<int32_t> gblk_z;     // element offset of the block's Z rows within the point's Z
+    std::vector<int64_t> gz_off;     // [n_gpt+1] Z buffer range of a point: blocks, then w (3)
+    int64_t n_z = 0, gz_max = 0;     // Z doubles in all / of the largest point
     std::vector<int64_t> spt_global;  // shard point -> global point id
     std::vector<int32_t> pt_off;      // [n_spt+1]
     std::vector<int32_t> obs_img, obs_pt, obs_slot;
@@ -39,6 +53,7 @@ struct BAHostPlan {
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;
     std::vector<ReduceTerm> terms;
+    std::vector<PTerm> pterms;
     int64_t n_sband = 0, n_sarrow = 0, n_scorner = 0;
     int64_t schur_flops = 0;    // algorithmic flops of one Schur pass
     int64_t schur_bytes = 0;    // algorithmic HBM bytes of one Schur pass
@@ -50,5 +65,13 @@ void build_plan(const sfm_ba_problem& prob, int rank, int world, BAHostPlan& pla
 // Landmark-block partition (sfm_ba_partition).
 void partition_points(const sfm_ba_problem& prob, const std::vector<int32_t>& cam_blk, int world,
                       std::vector<int64_t>& order, std::vector<int64_t>& bounds);
+
+// Image -> active camera block (-1: constant or unobserved) in the RCS order:
+// image order, or reverse Cuthill-McKee over the camera co-visibility graph
+// when that gives a narrower band.  *D_out = the block half-bandwidth.
+std::vector<int32_t> camera_blocks(const sfm_ba_problem& prob, int32_t* ncam_out, int32_t* D_out);
+
+// Largest camera half-bandwidth the block-cyclic-reduction solver takes.
+constexpr int kBandMaxD = 10;
 
 }  // namespace sfm

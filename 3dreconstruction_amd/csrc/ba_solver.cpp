@@ -47,6 +47,11 @@ struct sfm_ba_plan {
     DBuf<double> scaleE, scaleF, gram, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
         part_t, part_f, scal, bcr_buf;
     DBuf<int32_t> long_targets;
+    DBuf<int32_t> gblk_off, gblk_col, gblk_z;   // general points
+    DBuf<int64_t> gz_off;
+    DBuf<PTerm> pterms;
+    DBuf<double> Zbuf, dense_buf;
+    DenseArgs dense;
     DBuf<double> lpart;           // long-target segment partials [n_lseg][36]
     DBuf<int32_t> img_pt;         // image-ordered observations (image Gram pass)
     DBuf<double> img_uv;
@@ -108,6 +113,12 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->blk_img, h.blk_img, s);
     up(pl->blk_intr, h.blk_intr, s);
     up(pl->targets, h.targets, s);
+    up(pl->gblk_off, h.gblk_off, s);
+    up(pl->gblk_col, h.gblk_col, s);
+    up(pl->gblk_z, h.gblk_z, s);
+    up(pl->gz_off, h.gz_off, s);
+    up(pl->pterms, h.pterms, s);
+    pl->Zbuf.alloc(std::max<int64_t>(h.n_z, 1));
     std::vector<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
     for (int64_t k = 0; k < h.n_spt; ++k)
         for (int a = 0; a < 3; ++a) xs[3 * k + a] = X[3 * h.spt_global[k] + a];
@@ -160,16 +171,20 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         }
         up(pl->terms, ft, s);
     }
-    pl->rcs_n = h.n_sband + h.n_sarrow + h.n_scorner + 3 * h.nF + 1;
+    // RCS: band + arrow + corner, or dense; the parts of a dense S no target
+    // writes stay zero from here on
+    pl->rcs_n = h.n_sband + h.n_sarrow + h.n_scorner + h.n_sdense + 3 * h.nF + 1;
     pl->rcs.alloc(pl->rcs_n);
     pl->rcs.zero(s);
     const int Dp = h.D + 1;
-    pl->Lcol.alloc(std::max<size_t>((size_t)h.ncam * Dp * 36, 1));
-    pl->Larrow.alloc(std::max<size_t>((size_t)h.ncam * h.nintr * 24, 1));
+    if (!h.dense) {
+        pl->Lcol.alloc(std::max<size_t>((size_t)h.ncam * Dp * 36, 1));
+        pl->Larrow.alloc(std::max<size_t>((size_t)h.ncam * h.nintr * 24, 1));
+    }
     pl->zF.alloc(nF);
     pl->yF.alloc(nF);
     pl->part_u.alloc(2 * (size_t)prob.n_img * kGramSeg);
-    pl->part_s.alloc(2 * std::max<size_t>(h.chunks.size(), 1));
+    pl->part_s.alloc(2 * std::max<size_t>(h.chunks.size() + h.n_gpt, 1));
     pl->scal.alloc(kScCount);
     pl->scal.zero(s);
     if (ctx->comm) {
@@ -185,6 +200,11 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.n_img = prob.n_img; P.n_intr = prob.n_intr;
     P.n_spt = (int32_t)h.n_spt; P.n_sobs = (int32_t)h.n_sobs;
     P.n_chunk = (int32_t)h.chunks.size();
+    P.n_cpt = (int32_t)h.n_cpt; P.n_gpt = (int32_t)h.n_gpt;
+    P.gz_max = (int32_t)h.gz_max;
+    P.dense = h.dense ? 1 : 0;
+    P.gblk_off = pl->gblk_off.p; P.gblk_col = pl->gblk_col.p; P.gblk_z = pl->gblk_z.p;
+    P.gz_off = pl->gz_off.p; P.pterms = pl->pterms.p; P.Z = pl->Zbuf.p;
     P.tile_nt = h.tile_nt;
     P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D;
     P.nb = h.nb; P.nF = h.nF;
@@ -228,13 +248,16 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.Sband = pl->rcs.p;
     P.Sarrow = P.Sband + h.n_sband;
     P.Scorner = P.Sarrow + h.n_sarrow;
-    P.rhs = P.Scorner + h.n_scorner;
+    P.Sdense = P.Scorner + h.n_scorner;
+    P.rhs = P.Sdense + h.n_sdense;
     P.bF = P.rhs + h.nF;
     P.cnF = P.bF + h.nF;
     P.Lcol = pl->Lcol.p; P.Larrow = pl->Larrow.p; P.zF = pl->zF.p; P.yF = pl->yF.p;
-    bool lds = true;
-    solve_lds_bytes(P, &lds);
-    if (!lds) pl->Wg.alloc(solve_window_doubles(P));
+    if (!h.dense) {
+        bool lds = true;
+        solve_lds_bytes(P, &lds);
+        if (!lds) pl->Wg.alloc(solve_window_doubles(P));
+    }
     P.Wglobal = pl->Wg.p;
     P.part_u = pl->part_u.p; P.part_s = pl->part_s.p;
     pl->part_t.alloc((size_t)kPartT * std::max(ba_step_blocks(P), 1));
@@ -243,7 +266,12 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->part_f.alloc(3 * (size_t)P.n_fblk);
     P.part_f = pl->part_f.p;
     P.scal = pl->scal.p;
-    pl->use_bcr = bcr_supported(P) && std::getenv("SFM_BA_BAND_SOLVER") == nullptr;
+    pl->use_bcr = !h.dense && bcr_supported(P) && std::getenv("SFM_BA_BAND_SOLVER") == nullptr;
+    if (h.dense) {
+        dense_setup(pl->dense, P);
+        pl->dense_buf.alloc(dense_doubles(pl->dense));
+        dense_bind(pl->dense, pl->dense_buf.p);
+    }
     if (pl->use_bcr) {
         bcr_setup(pl->bcr, P);
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
@@ -366,7 +394,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
         ba_reduce(P, false, s);
         allreduce_rcs();
-        if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s);
+        if (P.dense) dense_solve(pl->dense, P, radius, s);
+        else if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s);
         else ba_solve(P, radius, s);
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);

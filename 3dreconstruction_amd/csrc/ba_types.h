@@ -28,6 +28,8 @@ constexpr int kGramSeg = 3;               // workgroups per image in the image G
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
 constexpr int kCamSlots = 14;             // staged cameras per chunk (incl. constant images)
 constexpr int kIntrSlots = 4;             // staged intrinsics blocks per chunk
+constexpr int kZMaxDoubles = 18432;       // LDS Z accumulator of one general point (144 KB):
+                                          // ~1000 parameter blocks per point
 
 // Per-camera precomputed rotation terms (for current or candidate params).
 //   Rodrigues branch: P = X c + (u x X) s + u (u.X)(1-c) + t,
@@ -65,11 +67,25 @@ enum : int32_t { kSrcTile = 0, kSrcU = 1, kSrcUb = 2, kSrcUcn = 3 };
 
 struct ReduceTarget {
     int64_t dst;        // element offset of the block in its destination array
-    int32_t dst_kind;   // 0 Sband, 1 Sarrow, 2 Scorner, 3 rhs, 4 bF, 5 cnF
+    int32_t dst_kind;   // 0 Sband, 1 Sarrow, 2 Scorner, 3 rhs, 4 bF, 5 cnF, 6 Sdense
     int32_t rows, cols; // block shape (vectors: cols = 1)
     int32_t ld;         // destination row stride
-    int32_t c_begin, c_end;  // contribution range
+    int32_t c_begin, c_end;  // sum-term range (chunk tiles, image Gram blocks)
+    int32_t p_begin, p_end;  // product-term range (general points, PTerm)
 };
+
+// Product term of a general point (one not handled by a Schur chunk): the
+// target block gets -Z_a Z_b' (rows x cols, inner dimension 3), Z_a and Z_b
+// the point's eliminated rows of blocks a and b, row-major [rows][3] at
+// element offsets za / zb of the Z buffer; for a vector target Z_b is the
+// point's w = L^-1 g_E (one row of 3).
+struct PTerm {
+    int64_t za, zb;
+};
+
+// Kinds of dst_kind.
+enum : int32_t { kDstBand = 0, kDstArrow = 1, kDstCorner = 2, kDstRhs = 3, kDstBF = 4, kDstCnF = 5,
+                 kDstDense = 6 };
 
 // ReduceTerm resolved against the contiguous [tiles | U | Ub | Ucn] buffer:
 // element (r, c) of the source block is src[off + r * rs + c].

@@ -142,6 +142,12 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
         if (cfg->vis_mode == 0) {
             const int64_t c0 = cfg->n_pt > 0 ? (p * (int64_t)(nc - k + 1)) / cfg->n_pt : 0;
             for (int a = 0; a < k; ++a) cams[a] = (int)c0 + a;
+        } else if (cfg->vis_mode == 2) {
+            // closed orbit: k consecutive cameras modulo n_cam (the last
+            // images see the first images' points)
+            const int64_t c0 = cfg->n_pt > 0 ? (p * (int64_t)nc) / cfg->n_pt : 0;
+            for (int a = 0; a < k; ++a) cams[a] = (int)((c0 + a) % nc);
+            std::sort(cams.begin(), cams.end());
         } else {
             int got = 0;
             while (got < k) {

@@ -210,6 +210,17 @@ int sfm_ba_plan_get_info(sfm_ba_plan* plan, sfm_ba_plan_info* info);
 /* Iteration log of the last sfm_ba_plan_run (n <= cap entries written). */
 int sfm_ba_plan_get_trace(sfm_ba_plan* plan, sfm_ba_iter* out, int32_t cap, int32_t* n);
 
+/* [cpu] Structure the planner chooses for a problem (no device needed):
+ * Schur chunks vs general points (any track length, repeated views, many
+ * intrinsics blocks), camera half-bandwidth after ordering, and the reduced
+ * camera system's form (dense = 1: blocked dense Cholesky; 0: block-banded
+ * cyclic reduction). */
+typedef struct sfm_ba_plan_shape {
+    int32_t n_chunks, band_blocks, dense, n_cam_active, n_intr_active, tile_rows;
+    int64_t n_chunk_pts, n_general_pts, rcs_dim, n_targets, n_terms, n_pterms;
+} sfm_ba_plan_shape;
+int sfm_ba_describe(const sfm_ba_problem* prob, int32_t rank, int32_t world_size, sfm_ba_plan_shape* out);
+
 /* [cpu] Landmark-block partition: contiguous point ranges of the
  * (min-camera)-sorted point order with ~equal observation counts.
  * order[n_pt] receives the sorted point order, bounds[world_size+1] the
@@ -219,7 +230,8 @@ int sfm_ba_partition(const sfm_ba_problem* prob, int32_t world_size,
 
 /* [cpu] Deterministic synthetic scenes.  Two calls: first with
  * NULL arrays to get sizes, then with caller-allocated arrays.  vis_mode 0 =
- * banded orbit visibility (k consecutive cameras), 1 = random k cameras.
+ * banded orbit visibility (k consecutive cameras), 1 = random k cameras,
+ * 2 = closed orbit (k consecutive cameras modulo n_cam).
  * gt_* receive ground truth, extr/intr/X the perturbed initial point. */
 typedef struct sfm_synth_ba_config {
     int32_t n_cam, k, vis_mode, n_intr;   /* n_intr 1 = shared intrinsics      */
