@@ -392,6 +392,10 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
         if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
+        // dense S across ranks: each rank writes only the blocks its own
+        // points touch, so the summed S of the last iteration is cleared first
+        if (P.dense && ctx->world > 1)
+            SFM_HIP(hipMemsetAsync(P.Sdense, 0, (size_t)h.n_sdense * sizeof(double), s));
         ba_reduce(P, false, s);
         allreduce_rcs();
         if (P.dense) dense_solve(pl->dense, P, radius, s);
