@@ -132,6 +132,38 @@ class SparseMatchStats(C.Structure):
                 ("n_matches", C.c_int64), ("reloaded", C.c_int32), ("reserved", C.c_int32)]
 
 
+class SeqImage(C.Structure):
+    _fields_ = [("n_kp", C.c_int32), ("reserved", C.c_int32), ("kp_xy", f64p), ("desc", u8p),
+                ("pose_prior", C.c_double * 6)]
+
+
+class SeqOptions(C.Structure):
+    _fields_ = [("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+                ("epipolar_px", C.c_double), ("pnp_reproj_px", C.c_double),
+                ("max_depth", C.c_double), ("min_pnp_inliers", C.c_int64),
+                ("fixed_writeback", C.c_int32), ("reserved", C.c_int32), ("ba", BAOptions)]
+
+
+class SeqStep(C.Structure):
+    _fields_ = [("image", C.c_int32), ("kept", C.c_int32),
+                ("local_raw", C.c_int64), ("local_kept", C.c_int64),
+                ("global_raw", C.c_int64), ("global_kept", C.c_int64),
+                ("pnp_inliers", C.c_int64), ("epipolar_inliers", C.c_int64),
+                ("new_points", C.c_int64), ("extended_obs", C.c_int64),
+                ("world_points", C.c_int64), ("world_observations", C.c_int64),
+                ("ba", BASummary), ("ba_rc", C.c_int32), ("reserved", C.c_int32),
+                ("ba_images", C.c_int64), ("ba_points", C.c_int64), ("ba_observations", C.c_int64),
+                ("seconds_local_match", C.c_double), ("seconds_global_match", C.c_double),
+                ("seconds_geometry", C.c_double), ("seconds_ba", C.c_double)]
+
+
+class SynthOrbitConfig(C.Structure):
+    _fields_ = [("n_img", C.c_int32), ("n_clutter", C.c_int32), ("n_landmarks", C.c_int64),
+                ("track_mean", C.c_double), ("detect_prob", C.c_double), ("noise_px", C.c_double),
+                ("desc_noise_dims", C.c_int32), ("desc_noise_amp", C.c_int32),
+                ("prior_rot", C.c_double), ("prior_t", C.c_double), ("seed", C.c_uint64)]
+
+
 def default_options():
     o = BAOptions()
     o.max_num_iterations = 50
@@ -194,6 +226,18 @@ SIGNATURES = [
     ("sfm_mvg_save_matches", C.c_int, [C.c_char_p, i32p, C.c_int64, i64p, u32p, u32p]),
     ("sfm_mvg_load_matches", C.c_int, [C.c_char_p, i32p, i64p, u32p, u32p, C.c_int64, C.c_int64,
                                        i64p, i64p]),
+    ("sfm_seq_default_options", None, [C.POINTER(SeqOptions)]),
+    ("sfm_seq_create", C.c_int, [C.c_void_p, C.POINTER(SeqOptions), C.POINTER(C.c_void_p)]),
+    ("sfm_seq_init", C.c_int, [C.c_void_p, C.POINTER(SeqImage), C.POINTER(SeqImage)]),
+    ("sfm_seq_add_image", C.c_int, [C.c_void_p, C.POINTER(SeqImage), i32p]),
+    ("sfm_seq_bundle_adjust", C.c_int, [C.c_void_p, C.POINTER(BASummary)]),
+    ("sfm_seq_last_step", C.c_int, [C.c_void_p, C.POINTER(SeqStep)]),
+    ("sfm_seq_matches", C.c_int, [C.c_void_p, C.c_int32, i32p, i32p, f32p, C.c_int64, i64p]),
+    ("sfm_seq_world", C.c_int, [C.c_void_p, f64p, i64p, C.c_int64, i64p, f64p, C.c_int32, i32p,
+                                f64p]),
+    ("sfm_seq_destroy", C.c_int, [C.c_void_p]),
+    ("sfm_synth_orbit_image", C.c_int, [C.POINTER(SynthOrbitConfig), C.c_int32, i32p, f64p, u8p,
+                                        f64p, i64p, f64p]),
     ("sfm_sparse_match_pair", C.c_int, [C.c_char_p]),
     ("sfm_sparse_match", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SparseMatchOpts),
                                    C.POINTER(SparseMatchStats)]),

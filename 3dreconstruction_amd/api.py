@@ -290,6 +290,142 @@ def ba_partition(problem, world_size):
 
 
 # ---------------------------------------------------------------------------
+# incremental SequentialActuator loop (config C5)
+# ---------------------------------------------------------------------------
+def seq_default_options():
+    o = abi.SeqOptions()
+    abi.load().sfm_seq_default_options(C.byref(o))
+    return o
+
+
+class OrbitSequence:
+    """[cpu] The synthetic closed-orbit image sequence (sfm_synth_orbit_image)."""
+
+    def __init__(self, n_img=300, n_landmarks=60000, n_clutter=1000, track_mean=10.0,
+                 detect_prob=0.95, noise_px=0.5, desc_noise_dims=24, desc_noise_amp=3,
+                 prior_rot=2e-4, prior_t=1e-3, seed=0x5F3D0005):
+        c = abi.SynthOrbitConfig()
+        c.n_img, c.n_clutter, c.n_landmarks = n_img, n_clutter, n_landmarks
+        c.track_mean, c.detect_prob, c.noise_px = track_mean, detect_prob, noise_px
+        c.desc_noise_dims, c.desc_noise_amp = desc_noise_dims, desc_noise_amp
+        c.prior_rot, c.prior_t, c.seed = prior_rot, prior_t, seed
+        self.cfg = c
+        self.n_img = n_img
+
+    def image(self, k, gt=False):
+        """dict(kp [n,2] f64, desc [n,128] u8, prior [6], landmark [n] (gt))"""
+        lib = abi.load()
+        n = C.c_int32()
+        _check(lib.sfm_synth_orbit_image(C.byref(self.cfg), k, C.byref(n), None, None, None, None,
+                                         None), "sfm_synth_orbit_image")
+        kp = np.zeros((n.value, 2))
+        d = np.zeros((max(n.value, 1), 128), np.uint8)
+        prior = np.zeros(6)
+        lm = np.zeros(max(n.value, 1), np.int64)
+        _check(lib.sfm_synth_orbit_image(C.byref(self.cfg), k, C.byref(n), abi.ptr(kp, abi.f64p),
+                                         abi.ptr(d, abi.u8p), abi.ptr(prior, abi.f64p),
+                                         abi.ptr(lm, abi.i64p), None), "sfm_synth_orbit_image")
+        out = {"kp": kp, "desc": d[:n.value], "prior": prior}
+        if gt:
+            out["landmark"] = lm[:n.value]
+        return out
+
+    def gt_points(self):
+        lib = abi.load()
+        n = C.c_int32()
+        X = np.zeros(3 * max(self.cfg.n_landmarks, 1))
+        _check(lib.sfm_synth_orbit_image(C.byref(self.cfg), 0, C.byref(n), None, None, None, None,
+                                         abi.ptr(X, abi.f64p)), "sfm_synth_orbit_image")
+        return X[:3 * self.cfg.n_landmarks].reshape(-1, 3)
+
+
+def seq_image(img):
+    """numpy image dict -> SeqImage (keeps the arrays referenced)."""
+    si = abi.SeqImage()
+    kp = np.ascontiguousarray(img["kp"], np.float64)
+    d = np.ascontiguousarray(img["desc"], np.uint8)
+    si.n_kp = len(kp)
+    si.kp_xy = abi.ptr(kp, abi.f64p)
+    si.desc = abi.ptr(d, abi.u8p)
+    for a in range(6):
+        si.pose_prior[a] = float(img["prior"][a])
+    si._keep = (kp, d)
+    return si
+
+
+class _SeqCalls:
+    """init / add / bundle_adjust / step / matches / world over the sfm_seq_*
+    (product) or orc_seq_* (oracle, tests only) entry points."""
+
+    def _f(self, name):
+        return getattr(self.lib, self.prefix + name)
+
+    def init(self, a, b):
+        _check(self._f("init")(self.h, C.byref(seq_image(a)), C.byref(seq_image(b))), self.prefix + "init")
+
+    def add(self, img):
+        kept = C.c_int32()
+        _check(self._f("add_image")(self.h, C.byref(seq_image(img)), C.byref(kept)), self.prefix + "add_image")
+        return bool(kept.value)
+
+    def bundle_adjust(self):
+        s = abi.BASummary()
+        _check(self._f("bundle_adjust")(self.h, C.byref(s)), self.prefix + "bundle_adjust")
+        return s
+
+    def step(self):
+        st = abi.SeqStep()
+        _check(self._f("last_step")(self.h, C.byref(st)), self.prefix + "last_step")
+        return st
+
+    def matches(self, which):
+        n = C.c_int64()
+        self._f("matches")(self.h, which, None, None, None, 0, C.byref(n))
+        q = np.zeros(max(n.value, 1), np.int32)
+        t = np.zeros_like(q)
+        d = np.zeros(len(q), np.float32)
+        _check(self._f("matches")(self.h, which, abi.ptr(q, abi.i32p), abi.ptr(t, abi.i32p),
+                                  abi.ptr(d, abi.f32p), n.value, C.byref(n)), self.prefix + "matches")
+        return q[:n.value], t[:n.value], d[:n.value]
+
+    def world(self):
+        n_pts, n_img = C.c_int64(), C.c_int32()
+        self._f("world")(self.h, None, None, 0, C.byref(n_pts), None, 0, C.byref(n_img), None)
+        X = np.zeros(3 * max(n_pts.value, 1))
+        nobs = np.zeros(max(n_pts.value, 1), np.int64)
+        poses = np.zeros(6 * max(n_img.value, 1))
+        intr = np.zeros(4)
+        _check(self._f("world")(self.h, abi.ptr(X, abi.f64p), abi.ptr(nobs, abi.i64p), n_pts.value,
+                                C.byref(n_pts), abi.ptr(poses, abi.f64p), n_img.value, C.byref(n_img),
+                                abi.ptr(intr, abi.f64p)), self.prefix + "world")
+        return {"X": X[:3 * n_pts.value].reshape(-1, 3), "n_obs": nobs[:n_pts.value],
+                "poses": poses[:6 * n_img.value].reshape(-1, 6), "intr": intr}
+
+    def close(self):
+        if self.h:
+            self._f("destroy")(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SeqLoop(_SeqCalls):
+    """SequentialActuator on the GPU (sfm_seq_*)."""
+
+    def __init__(self, ctx, opts=None):
+        self.ctx, self.lib, self.prefix = ctx, ctx.lib, "sfm_seq_"
+        o = opts or seq_default_options()
+        h = C.c_void_p()
+        _check(self.lib.sfm_seq_create(ctx.h, C.byref(o), C.byref(h)), "sfm_seq_create")
+        self.h = h
+        ctx._adopt(self)
+
+
+# ---------------------------------------------------------------------------
 # file-staged sparseBuilder flow (OpenMVG stage-boundary formats)
 # ---------------------------------------------------------------------------
 def _b(path):

@@ -259,3 +259,129 @@ extern "C" int sfm_exhaustive_pairs(int32_t n_img, int32_t* pairs) {
         for (int32_t j = i + 1; j < n_img; ++j) { pairs[2 * q] = i; pairs[2 * q + 1] = j; ++q; }
     return SFM_OK;
 }
+
+// ---------------------------------------------------------------------------
+// C5: closed-orbit image sequence for the SequentialActuator loop
+// (src/main.cpp:99-108).  See include/sfmcore.h sfm_synth_orbit_image.
+// ---------------------------------------------------------------------------
+namespace {
+
+enum : uint64_t { kStreamOrbLm = 11, kStreamOrbDesc = 12, kStreamOrbObs = 13, kStreamOrbClutter = 14,
+                  kStreamOrbPrior = 15 };
+
+// ground-truth Tcw of orbit camera c: centre on the circle of radius 10 in
+// the XZ plane, looking at the origin, image y axis along world y
+void orbit_pose(int c, int n, double R[9], double t[3]) {
+    const double phi = 2.0 * M_PI * c / n;
+    const double C[3] = {10.0 * std::cos(phi), 0.0, 10.0 * std::sin(phi)};
+    const double z[3] = {-C[0] / 10.0, 0.0, -C[2] / 10.0};
+    const double up[3] = {0.0, 1.0, 0.0};
+    double x[3] = {z[1] * up[2] - z[2] * up[1], z[2] * up[0] - z[0] * up[2], z[0] * up[1] - z[1] * up[0]};
+    const double xn = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+    for (double& v : x) v /= xn;
+    const double y[3] = {z[1] * x[2] - z[2] * x[1], z[2] * x[0] - z[0] * x[2], z[0] * x[1] - z[1] * x[0]};
+    const double Rm[9] = {x[0], x[1], x[2], y[0], y[1], y[2], z[0], z[1], z[2]};
+    for (int a = 0; a < 9; ++a) R[a] = Rm[a];
+    for (int a = 0; a < 3; ++a) t[a] = -(R[3 * a] * C[0] + R[3 * a + 1] * C[1] + R[3 * a + 2] * C[2]);
+}
+
+struct OrbitLandmark {
+    double X[3];     // ground truth, orbit frame
+    double psi, h;   // facing direction, half-arc of the cameras that see it
+};
+
+OrbitLandmark orbit_landmark(const sfm_synth_orbit_config* cfg, int64_t l) {
+    Rng r(entity_seed(cfg->seed, kStreamOrbLm, (uint64_t)l));
+    OrbitLandmark L;
+    for (double& v : L.X) v = 4.0 * r.uni() - 2.0;
+    L.psi = 2.0 * M_PI * r.uni();
+    const double dphi = 2.0 * M_PI / cfg->n_img;
+    L.h = dphi * std::max(0.0, cfg->track_mean - 1.0) * 0.5 * (0.5 + r.uni());
+    return L;
+}
+
+}  // namespace
+
+extern "C" int sfm_synth_orbit_image(const sfm_synth_orbit_config* cfg, int32_t img, int32_t* n_kp,
+                                     double* kp_xy, uint8_t* desc, double* pose_prior, int64_t* landmark,
+                                     double* gt_X) {
+    if (!cfg || !n_kp || cfg->n_img < 2 || img < 0 || img >= cfg->n_img || cfg->n_landmarks < 0 ||
+        cfg->n_clutter < 0 || cfg->desc_noise_dims < 0 || cfg->desc_noise_amp < 0)
+        return SFM_ERR_INVALID_ARG;
+    const double fx = 2905.88, fy = 2905.88, cx = 1416.0, cy = 1064.0;   // src/main.cpp:59,124
+    const int n = cfg->n_img;
+    double R0[9], t0[3], Rc[9], tc[3];
+    orbit_pose(0, n, R0, t0);
+    orbit_pose(img, n, Rc, tc);
+    const double phi = 2.0 * M_PI * img / n;
+    // items: (shuffle key, landmark id or -1 - clutter slot)
+    std::vector<std::pair<uint64_t, int64_t>> items;
+    for (int64_t l = 0; l < cfg->n_landmarks; ++l) {
+        const OrbitLandmark L = orbit_landmark(cfg, l);
+        if (std::fabs(std::remainder(phi - L.psi, 2.0 * M_PI)) > L.h) continue;
+        Rng r(entity_seed(cfg->seed, kStreamOrbObs, (uint64_t)l * (uint64_t)n + (uint64_t)img));
+        if (r.uni() >= cfg->detect_prob) continue;
+        items.push_back({r.next(), l});
+    }
+    for (int32_t s = 0; s < cfg->n_clutter; ++s) {
+        Rng r(entity_seed(cfg->seed, kStreamOrbClutter, ((uint64_t)img << 32) | (uint32_t)s));
+        items.push_back({r.next(), -1 - (int64_t)s});
+    }
+    std::sort(items.begin(), items.end());
+    *n_kp = (int32_t)items.size();
+    if (gt_X)
+        for (int64_t l = 0; l < cfg->n_landmarks; ++l) {
+            const OrbitLandmark L = orbit_landmark(cfg, l);
+            for (int a = 0; a < 3; ++a)
+                gt_X[3 * l + a] = R0[3 * a] * L.X[0] + R0[3 * a + 1] * L.X[1] + R0[3 * a + 2] * L.X[2] + t0[a];
+        }
+    if (pose_prior) {
+        // Tcw relative to image 0: R = Rc R0^T, t = tc - R t0
+        double R[9], w[3], t[3];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c)
+                R[3 * r + c] = Rc[3 * r] * R0[3 * c] + Rc[3 * r + 1] * R0[3 * c + 1] + Rc[3 * r + 2] * R0[3 * c + 2];
+        for (int a = 0; a < 3; ++a) t[a] = tc[a] - (R[3 * a] * t0[0] + R[3 * a + 1] * t0[1] + R[3 * a + 2] * t0[2]);
+        mat_to_angle_axis(R, w);
+        if (img == 0) { w[0] = w[1] = w[2] = 0.0; t[0] = t[1] = t[2] = 0.0; }
+        Rng r(entity_seed(cfg->seed, kStreamOrbPrior, (uint64_t)img));
+        for (int a = 0; a < 3; ++a) {
+            pose_prior[a] = w[a] + (img ? cfg->prior_rot * r.gauss() : 0.0);
+            pose_prior[3 + a] = t[a] + (img ? cfg->prior_t * r.gauss() : 0.0);
+        }
+    }
+    if (!kp_xy && !desc && !landmark) return SFM_OK;
+    for (size_t k = 0; k < items.size(); ++k) {
+        const int64_t id = items[k].second;
+        double uv[2];
+        uint8_t d[128];
+        if (id >= 0) {
+            const OrbitLandmark L = orbit_landmark(cfg, id);
+            double P[3];
+            for (int a = 0; a < 3; ++a)
+                P[a] = Rc[3 * a] * L.X[0] + Rc[3 * a + 1] * L.X[1] + Rc[3 * a + 2] * L.X[2] + tc[a];
+            Rng r(entity_seed(cfg->seed, kStreamOrbObs, (uint64_t)id * (uint64_t)n + (uint64_t)img));
+            r.uni(); r.next();   // the draws the visibility test made
+            uv[0] = fx * P[0] / P[2] + cx + cfg->noise_px * r.gauss();
+            uv[1] = fy * P[1] / P[2] + cy + cfg->noise_px * r.gauss();
+            Rng dr(entity_seed(cfg->seed, kStreamOrbDesc, (uint64_t)id));
+            rootsift_like(dr, d);
+            for (int q = 0; q < cfg->desc_noise_dims; ++q) {
+                const int dim = (int)(r.next() % 128);
+                const int v = (int)d[dim] + (int)(r.next() % (uint64_t)(2 * cfg->desc_noise_amp + 1)) -
+                              cfg->desc_noise_amp;
+                d[dim] = (uint8_t)std::min(255, std::max(0, v));
+            }
+        } else {
+            Rng r(entity_seed(cfg->seed, kStreamOrbClutter, ((uint64_t)img << 32) | (uint32_t)(-1 - id)));
+            r.next();
+            uv[0] = 2832.0 * r.uni();
+            uv[1] = 2128.0 * r.uni();
+            rootsift_like(r, d);
+        }
+        if (kp_xy) { kp_xy[2 * k] = uv[0]; kp_xy[2 * k + 1] = uv[1]; }
+        if (desc) std::memcpy(desc + 128 * k, d, 128);
+        if (landmark) landmark[k] = id >= 0 ? id : -1;
+    }
+    return SFM_OK;
+}

@@ -1,0 +1,186 @@
+// BundleAdjuster (src/adjuster/BundleAdjuster.h:32-188) over a solver policy.
+//
+// BasicBundleAdjuster<Solver> does what the reference's class does around
+// ceres::Solve: loadDataFromWorld (:82-98) + problem assembly (:100-123) into
+// plain SoA arrays, the solve, updateWorld (:143-156) only when the solution
+// is usable (:128-131, :179-184), clear (:158-164).  The solver policy is
+//   int  solve(const sfm_ba_problem&, double* extr, double* intr, double* X,
+//              const sfm_ba_options&, sfm_ba_summary&);   // SFM_OK / SFM_ERR_*
+//   const char* last_error() const;
+// sfm.hpp binds it to the GPU (sfm_ba_solve); the loop oracle binds it to the
+// CPU restatement.  Header-only.
+#pragma once
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "../../../include/sfmcore.h"
+#include "frames.hpp"
+#include "world.hpp"
+
+namespace sfm {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& where, const char* msg = "")
+        : std::runtime_error(where + ": " + std::to_string(c) + " " + msg), code(c) {}
+};
+
+struct BundleAdjusterOptions {
+    bool fixed_writeback = false;  // false: reproduce Image::setIntrinsic's ZYX-Euler quirk
+    bool verbose = true;           // print the reference's statistics block
+    // A solve that could not run at all (bad input, device, RCCL, a shape the
+    // build does not take) is not the reference's "solution not usable"
+    // outcome: it is always reported on stderr with the solver's message, and
+    // thrown as sfm::Error when set.
+    bool throw_on_error = false;
+    sfm_ba_options solver{};
+    BundleAdjusterOptions() {
+        solver.max_num_iterations = 50; solver.max_num_consecutive_invalid_steps = 5;
+        solver.jacobi_scaling = 1; solver.reserved = 0;
+        solver.function_tolerance = 1e-6; solver.gradient_tolerance = 1e-10;
+        solver.parameter_tolerance = 1e-8; solver.initial_trust_region_radius = 1e4;
+        solver.max_trust_region_radius = 1e16; solver.min_trust_region_radius = 1e-32;
+        solver.min_relative_decrease = 1e-3; solver.min_lm_diagonal = 1e-6;
+        solver.max_lm_diagonal = 1e32;
+    }
+};
+
+template <class Solver>
+class BasicBundleAdjuster {
+   public:
+    using Options = BundleAdjusterOptions;
+    explicit BasicBundleAdjuster(Solver solver, Options opt = Options()) : solver_(std::move(solver)), opt_(opt) {}
+
+    void operator()(WorldStructure::Ptr& world) {  // :176-186
+        load(world);
+        if (solve()) update();
+        clear();
+    }
+    const sfm_ba_summary& summary() const { return summary_; }
+    int lastError() const { return last_rc_; }   // SFM_OK or the last solve code
+    // size of the last problem (images with a pose block, points, observations)
+    int64_t lastImages() const { return last_n_img_; }
+    int64_t lastPoints() const { return last_n_pt_; }
+    int64_t lastObservations() const { return last_n_obs_; }
+    Options& options() { return opt_; }
+
+   private:
+    // loadDataFromWorld (:82-98) + problem assembly (:100-123)
+    void load(const WorldStructure::Ptr& world) {
+        images_.clear(); cams_.clear(); extr_.clear(); intr_.clear();
+        img_index_.clear(); cam_index_.clear(); img_cam_.clear();
+        auto add_cam = [&](const Camera::Ptr& c, bool zero) {
+            auto it = cam_index_.find(c.get());
+            if (it != cam_index_.end()) return it->second;
+            const int k = (int)cams_.size();
+            cam_index_[c.get()] = k;
+            cams_.push_back(c);
+            const auto v = zero ? std::array<double, 4>{0, 0, 0, 0} : c->getIntrinsic();
+            intr_.insert(intr_.end(), v.begin(), v.end());
+            return k;
+        };
+        auto add_img = [&](const Image::Ptr& im, bool zero_pose) {
+            auto it = img_index_.find(im.get());
+            if (it != img_index_.end()) return it->second;
+            const int k = (int)images_.size();
+            img_index_[im.get()] = k;
+            images_.push_back(im);
+            const auto p = zero_pose ? std::array<double, 6>{} : im->pose();
+            extr_.insert(extr_.end(), p.begin(), p.end());
+            img_cam_.push_back(-1);
+            return k;
+        };
+        for (auto& f : world->local_frames_) {
+            const int k = add_img(f->getImage2(), false);
+            img_cam_[k] = add_cam(f->getImage2()->getCamera(), false);
+        }
+        const_img_ = world->local_frames_.empty() ? -1 : 0;
+        std::vector<std::pair<WorldPoint::Idx, WorldPoint::Ptr>> pts(world->world_points_.begin(),
+                                                                     world->world_points_.end());
+        std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
+        points_.clear(); X_.clear(); off_.assign(1, 0); obs_img_.clear(); uv_.clear();
+        for (auto& [idx, p] : pts) {
+            points_.push_back(p);
+            X_.insert(X_.end(), p->world_pos_.begin(), p->world_pos_.end());
+            for (auto& [im, uv] : p->observed_frames_) {
+                // image_extrinsic_[image] / camera_intrinsics_[camera] are
+                // operator[]: unseen blocks are inserted as zeros (:118-119)
+                const int k = add_img(im, true);
+                if (img_cam_[k] < 0) img_cam_[k] = add_cam(im->getCamera(), true);
+                obs_img_.push_back(k);
+                uv_.push_back(uv.x);
+                uv_.push_back(uv.y);
+            }
+            off_.push_back((int64_t)obs_img_.size());
+        }
+    }
+    bool solve() {
+        sfm_ba_problem pr{};
+        pr.n_img = (int32_t)images_.size();
+        pr.n_intr = (int32_t)cams_.size();
+        pr.n_pt = (int64_t)points_.size();
+        pr.n_obs = (int64_t)obs_img_.size();
+        pr.pt_offsets = off_.data();
+        pr.obs_img = obs_img_.data();
+        pr.obs_uv = uv_.data();
+        pr.img_intr = img_cam_.data();
+        pr.const_img = const_img_;
+        pr.huber_a = 4.0;
+        last_n_img_ = pr.n_img; last_n_pt_ = pr.n_pt; last_n_obs_ = pr.n_obs;
+        summary_ = sfm_ba_summary{};
+        if (pr.n_img == 0 || pr.n_intr == 0) return false;
+        const int rc = solver_.solve(pr, extr_.data(), intr_.data(), X_.data(), opt_.solver, summary_);
+        last_rc_ = rc;
+        if (rc != SFM_OK && rc != SFM_ERR_SOLVER && rc != SFM_ERR_NOT_FINITE) {
+            std::fprintf(stderr, "Bundle Adjustment failed: %s (code %d)\n", solver_.last_error(), rc);
+            if (opt_.throw_on_error) throw Error(rc, "bundle adjustment", solver_.last_error());
+            return false;
+        }
+        if (rc != SFM_OK || !summary_.usable) {   // !IsSolutionUsable (:128-131)
+            if (opt_.verbose) std::printf("Bundle Adjustment failed.\n");
+            return false;
+        }
+        if (opt_.verbose)
+            std::printf("Bundle Adjustment statistics (approximated RMSE):\n    #views: %zu\n    #residuals: %lld\n"
+                        "    Initial RMSE: %g\n    Final RMSE: %g\n    Time (s): %g\n",
+                        images_.size(), (long long)summary_.num_residuals, summary_.rmse_initial,
+                        summary_.rmse_final, summary_.seconds);
+        return true;
+    }
+    void update() {  // updateWorld (:143-156)
+        for (std::size_t k = 0; k < points_.size(); ++k) points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
+        for (std::size_t k = 0; k < images_.size(); ++k) {
+            std::array<double, 6> p;
+            for (int a = 0; a < 6; ++a) p[a] = extr_[6 * k + a];
+            images_[k]->setIntrinsic(p, opt_.fixed_writeback);
+        }
+        for (std::size_t k = 0; k < cams_.size(); ++k)
+            cams_[k]->setIntrinsic({intr_[4 * k], intr_[4 * k + 1], intr_[4 * k + 2], intr_[4 * k + 3]});
+    }
+    void clear() {  // :158-164
+        images_.clear(); cams_.clear(); points_.clear();
+    }
+
+    Solver solver_;
+    Options opt_;
+    std::vector<Image::Ptr> images_;
+    std::vector<Camera::Ptr> cams_;
+    std::vector<WorldPoint::Ptr> points_;
+    std::unordered_map<const Image*, int> img_index_;
+    std::unordered_map<const Camera*, int> cam_index_;
+    std::vector<int32_t> img_cam_, obs_img_;
+    std::vector<double> extr_, intr_, X_, uv_;
+    std::vector<int64_t> off_;
+    int32_t const_img_ = -1;
+    int last_rc_ = SFM_OK;
+    int64_t last_n_img_ = 0, last_n_pt_ = 0, last_n_obs_ = 0;
+    sfm_ba_summary summary_{};
+};
+
+}  // namespace sfm

@@ -25,18 +25,15 @@
 #include <vector>
 
 #include "../../../include/sfmcore.h"
+#include "actuator.hpp"
+#include "adjuster.hpp"
+#include "frames.hpp"
 #include "world.hpp"
 
 namespace sfm {
 
-struct Error : std::runtime_error {
-    int code;
-    Error(int c, const std::string& where)
-        : std::runtime_error(where + ": " + std::to_string(c) + " " + sfm_last_error()), code(c) {}
-};
-
 inline void check(int rc, const char* where) {
-    if (rc != SFM_OK) throw Error(rc, where);
+    if (rc != SFM_OK) throw Error(rc, where, sfm_last_error());
 }
 
 // One HIP device (+ RCCL communicator for landmark-sharded BA).
@@ -59,26 +56,6 @@ class Context {
 
    private:
     sfm_ctx* ctx_ = nullptr;
-};
-
-class LocalFrame {
-   public:
-    using Ptr = std::shared_ptr<LocalFrame>;
-    LocalFrame(Image::Ptr image1, Image::Ptr image2) : image1_(std::move(image1)), image2_(std::move(image2)) {}
-    Image::Ptr getImage1() const { return image1_; }
-    Image::Ptr getImage2() const { return image2_; }
-    const std::vector<DMatch>& getMatches() const { return matches_; }
-    template <class M> std::size_t matchFeature(M& matcher);
-    std::vector<DMatch> filterMatches() const;
-    template <class M> std::size_t matchFeatureAndFilter(M& matcher) {
-        matchFeature(matcher);
-        matches_ = filterMatches();
-        return matches_.size();
-    }
-
-   private:
-    Image::Ptr image1_, image2_;
-    std::vector<DMatch> matches_;
 };
 
 // ---------------------------------------------------------------------------
@@ -107,209 +84,40 @@ class Matcher {
     Context* ctx_;
 };
 
-template <class M>
-std::size_t LocalFrame::matchFeature(M& matcher) {
-    if (!matches_.empty()) matches_.clear();  // "Rematch feature" warning in the reference
-    std::vector<std::vector<DMatch>> v;
-    matcher.knnMatch(image1_->descriptors, image2_->descriptors, v, 1);
-    for (auto& row : v)
-        if (!row.empty()) matches_.push_back(row[0]);
-    return matches_.size();
-}
+// ---------------------------------------------------------------------------
+// BundleAdjuster (BundleAdjuster.h:32-188) on the GPU solver
+// ---------------------------------------------------------------------------
+struct GpuSolver {
+    Context* ctx;
+    int solve(const sfm_ba_problem& pr, double* extr, double* intr, double* X, const sfm_ba_options& o,
+              sfm_ba_summary& s) const {
+        return sfm_ba_solve(ctx->get(), &pr, extr, intr, X, &o, &s);
+    }
+    const char* last_error() const { return sfm_last_error(); }
+};
 
-// keep d <= 4 * min d (LocalFrame.h:49-64); empty input -> empty (the
-// reference dereferences min_element of an empty vector)
-inline std::vector<DMatch> LocalFrame::filterMatches() const {
-    std::vector<DMatch> good;
-    if (matches_.empty()) return good;
-    const float mn = std::min_element(matches_.begin(), matches_.end(),
-                                      [](const DMatch& a, const DMatch& b) { return a.distance < b.distance; })
-                         ->distance;
-    for (const auto& m : matches_)
-        if (m.distance <= 4 * mn) good.push_back(m);
-    return good;
-}
-
-class GlobalFrame {
+class BundleAdjuster : public BasicBundleAdjuster<GpuSolver> {
    public:
-    GlobalFrame(const WorldStructure::Ptr& world, Image::Ptr image) : image_(std::move(image)) {
-        std::vector<std::pair<WorldPoint::Idx, WorldPoint::Ptr>> pts(world->world_points_.begin(),
-                                                                     world->world_points_.end());
-        std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
-        for (auto& p : pts) world_points_.push_back(p.second);
-    }
-    template <class M> std::size_t matchFeature(M& matcher) {
-        matches_.clear();
-        std::vector<uint8_t> q;
-        for (auto& p : world_points_) q.insert(q.end(), p->last_descriptor_.begin(), p->last_descriptor_.end());
-        std::vector<std::vector<DMatch>> v;
-        matcher.knnMatch(q, image_->descriptors, v, 1);
-        for (auto& row : v)
-            if (!row.empty()) matches_.push_back(row[0]);
-        return matches_.size();
-    }
-    // drop d > 3 * min d (GlobalFrame.h:45-60)
-    std::vector<DMatch> filterMatches() const {
-        std::vector<DMatch> good;
-        if (matches_.empty()) return good;
-        float mn = matches_[0].distance;
-        for (auto& m : matches_) mn = std::min(mn, m.distance);
-        for (auto& m : matches_)
-            if (!(m.distance > 3 * mn)) good.push_back(m);
-        return good;
-    }
-    template <class M> std::size_t matchFeatureAndFilter(M& matcher) {
-        matchFeature(matcher);
-        matches_ = filterMatches();
-        return matches_.size();
-    }
-    const std::vector<WorldPoint::Ptr>& get_world_points() const { return world_points_; }
-    const std::vector<DMatch>& getMatches() const { return matches_; }
-
-   private:
-    std::vector<DMatch> matches_;
-    Image::Ptr image_;
-    std::vector<WorldPoint::Ptr> world_points_;
+    explicit BundleAdjuster(Context& ctx = Context::thread_default(), Options opt = Options())
+        : BasicBundleAdjuster<GpuSolver>(GpuSolver{&ctx}, opt) {}
 };
 
 // ---------------------------------------------------------------------------
-// BundleAdjuster (BundleAdjuster.h:32-188)
+// SequentialActuator (SequentialActuator.h:16-236) on the GPU matcher and
+// adjuster (BASELINE.json config C5)
 // ---------------------------------------------------------------------------
-class BundleAdjuster {
+struct GpuSeqBackend {
+    Matcher m;
+    Context* ctx;
+    Matcher& matcher() { return m; }
+    BundleAdjuster make_adjuster(const BundleAdjusterOptions& o) const { return BundleAdjuster(*ctx, o); }
+};
+
+class SequentialActuator : public BasicSequentialActuator<GpuSeqBackend> {
    public:
-    struct Options {
-        bool fixed_writeback = false;  // false: reproduce Image::setIntrinsic's ZYX-Euler quirk
-        bool verbose = true;           // print the reference's statistics block
-        // A solve that could not run at all (bad input, device, RCCL) is not
-        // the reference's "solution not usable" outcome: it is always reported
-        // on stderr with sfm_last_error(), and thrown as sfm::Error when set.
-        bool throw_on_error = false;
-        sfm_ba_options solver{};
-        Options() { sfm_ba_default_options(&solver); }
-    };
-    explicit BundleAdjuster(Context& ctx = Context::thread_default(), Options opt = Options())
-        : ctx_(&ctx), opt_(opt) {}
-
-    void operator()(WorldStructure::Ptr& world) {  // :176-186
-        load(world);
-        if (solve()) update();
-        clear();
-    }
-    const sfm_ba_summary& summary() const { return summary_; }
-    int lastError() const { return last_rc_; }   // SFM_OK or the last sfm_ba_solve code
-
-   private:
-    // loadDataFromWorld (:82-98) + problem assembly (:100-123)
-    void load(const WorldStructure::Ptr& world) {
-        world_ = world;
-        images_.clear(); cams_.clear(); extr_.clear(); intr_.clear();
-        img_index_.clear(); cam_index_.clear();
-        auto add_cam = [&](const Camera::Ptr& c, bool zero) {
-            auto it = cam_index_.find(c.get());
-            if (it != cam_index_.end()) return it->second;
-            const int k = (int)cams_.size();
-            cam_index_[c.get()] = k;
-            cams_.push_back(c);
-            const auto v = zero ? std::array<double, 4>{0, 0, 0, 0} : c->getIntrinsic();
-            intr_.insert(intr_.end(), v.begin(), v.end());
-            return k;
-        };
-        auto add_img = [&](const Image::Ptr& im, bool zero_pose) {
-            auto it = img_index_.find(im.get());
-            if (it != img_index_.end()) return it->second;
-            const int k = (int)images_.size();
-            img_index_[im.get()] = k;
-            images_.push_back(im);
-            const auto p = zero_pose ? std::array<double, 6>{} : im->pose();
-            extr_.insert(extr_.end(), p.begin(), p.end());
-            img_cam_.push_back(-1);
-            return k;
-        };
-        img_cam_.clear();
-        for (auto& f : world->local_frames_) {
-            const int k = add_img(f->getImage2(), false);
-            img_cam_[k] = add_cam(f->getImage2()->getCamera(), false);
-        }
-        const_img_ = world->local_frames_.empty() ? -1 : 0;
-        std::vector<std::pair<WorldPoint::Idx, WorldPoint::Ptr>> pts(world->world_points_.begin(),
-                                                                     world->world_points_.end());
-        std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
-        points_.clear(); X_.clear(); off_.assign(1, 0); obs_img_.clear(); uv_.clear();
-        for (auto& [idx, p] : pts) {
-            points_.push_back(p);
-            X_.insert(X_.end(), p->world_pos_.begin(), p->world_pos_.end());
-            for (auto& [im, uv] : p->observed_frames_) {
-                // image_extrinsic_[image] / camera_intrinsics_[camera] are
-                // operator[]: unseen blocks are inserted as zeros (:118-119)
-                const int k = add_img(im, true);
-                if (img_cam_[k] < 0) img_cam_[k] = add_cam(im->getCamera(), true);
-                obs_img_.push_back(k);
-                uv_.push_back(uv.x);
-                uv_.push_back(uv.y);
-            }
-            off_.push_back((int64_t)obs_img_.size());
-        }
-    }
-    bool solve() {
-        sfm_ba_problem pr{};
-        pr.n_img = (int32_t)images_.size();
-        pr.n_intr = (int32_t)cams_.size();
-        pr.n_pt = (int64_t)points_.size();
-        pr.n_obs = (int64_t)obs_img_.size();
-        pr.pt_offsets = off_.data();
-        pr.obs_img = obs_img_.data();
-        pr.obs_uv = uv_.data();
-        pr.img_intr = img_cam_.data();
-        pr.const_img = const_img_;
-        pr.huber_a = 4.0;
-        if (pr.n_img == 0 || pr.n_intr == 0) return false;
-        const int rc = sfm_ba_solve(ctx_->get(), &pr, extr_.data(), intr_.data(), X_.data(), &opt_.solver, &summary_);
-        last_rc_ = rc;
-        if (rc != SFM_OK && rc != SFM_ERR_SOLVER && rc != SFM_ERR_NOT_FINITE) {
-            std::fprintf(stderr, "Bundle Adjustment failed: %s (code %d)\n", sfm_last_error(), rc);
-            if (opt_.throw_on_error) throw Error(rc, "sfm_ba_solve");
-            return false;
-        }
-        if (rc != SFM_OK || !summary_.usable) {   // !IsSolutionUsable (:128-131)
-            if (opt_.verbose) std::printf("Bundle Adjustment failed.\n");
-            return false;
-        }
-        if (opt_.verbose)
-            std::printf("Bundle Adjustment statistics (approximated RMSE):\n    #views: %zu\n    #residuals: %lld\n"
-                        "    Initial RMSE: %g\n    Final RMSE: %g\n    Time (s): %g\n",
-                        images_.size(), (long long)summary_.num_residuals, summary_.rmse_initial,
-                        summary_.rmse_final, summary_.seconds);
-        return true;
-    }
-    void update() {  // updateWorld (:143-156)
-        for (std::size_t k = 0; k < points_.size(); ++k) points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
-        for (std::size_t k = 0; k < images_.size(); ++k) {
-            std::array<double, 6> p;
-            for (int a = 0; a < 6; ++a) p[a] = extr_[6 * k + a];
-            images_[k]->setIntrinsic(p, opt_.fixed_writeback);
-        }
-        for (std::size_t k = 0; k < cams_.size(); ++k)
-            cams_[k]->setIntrinsic({intr_[4 * k], intr_[4 * k + 1], intr_[4 * k + 2], intr_[4 * k + 3]});
-    }
-    void clear() {
-        world_ = nullptr;
-        images_.clear(); cams_.clear(); points_.clear();
-    }
-
-    Context* ctx_;
-    Options opt_;
-    WorldStructure::Ptr world_;
-    std::vector<Image::Ptr> images_;
-    std::vector<Camera::Ptr> cams_;
-    std::vector<WorldPoint::Ptr> points_;
-    std::unordered_map<const Image*, int> img_index_;
-    std::unordered_map<const Camera*, int> cam_index_;
-    std::vector<int32_t> img_cam_, obs_img_;
-    std::vector<double> extr_, intr_, X_, uv_;
-    std::vector<int64_t> off_;
-    int32_t const_img_ = -1;
-    int last_rc_ = SFM_OK;
-    sfm_ba_summary summary_{};
+    explicit SequentialActuator(Camera::Ptr camera, Context& ctx = Context::thread_default(),
+                                SeqOptions opt = SeqOptions())
+        : BasicSequentialActuator<GpuSeqBackend>(GpuSeqBackend{Matcher(ctx), &ctx}, std::move(camera), opt) {}
 };
 
 namespace sparse {

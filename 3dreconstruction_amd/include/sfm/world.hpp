@@ -129,6 +129,7 @@ struct WorldPoint {
 };
 
 class LocalFrame;
+template <class Solver> class BasicBundleAdjuster;
 
 class WorldStructure {
    public:
@@ -152,7 +153,7 @@ class WorldStructure {
     std::vector<std::shared_ptr<LocalFrame>> local_frames_;
     std::unordered_map<Image::Idx, Image::Ptr> images_;
     std::unordered_map<WorldPoint::Idx, WorldPoint::Ptr> world_points_;
-    friend class BundleAdjuster;
+    template <class> friend class BasicBundleAdjuster;
     friend class GlobalFrame;
 };
 

@@ -271,6 +271,78 @@ def pmc_measure(args, kernel_regex="schur_kernel"):
     return out
 
 
+def bench_loop(ctx, n_img, cpu=True, cpu_images=16):
+    """C5: SequentialActuator over the synthetic closed orbit (src/main.cpp:99-108):
+    init + BA, then addSingleImage + BA per image, a fresh BundleAdjuster per
+    call.  Images are generated before the timed region (they stand for what
+    detectAndCompute leaves behind); the timed region is the whole loop."""
+    seq = api.OrbitSequence(n_img=n_img)
+    t0 = time.time()
+    imgs = [seq.image(k) for k in range(n_img)]
+    log(f"loop: {n_img} images generated in {time.time() - t0:.1f}s "
+        f"({np.mean([len(i['kp']) for i in imgs]):.0f} keypoints each)")
+    lp = api.SeqLoop(ctx)
+    steps = []
+    t0 = time.perf_counter()
+    lp.init(imgs[0], imgs[1])
+    lp.bundle_adjust()
+    steps.append(lp.step())
+    for k in range(2, n_img):
+        lp.add(imgs[k])
+        lp.bundle_adjust()
+        steps.append(lp.step())
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    lp.close()
+    stage = {f: sum(getattr(s, "seconds_" + f) for s in steps)
+             for f in ("local_match", "global_match", "geometry", "ba")}
+    iters = sum(s.ba.iterations for s in steps)
+    last = steps[-1]
+    out = {"metric": "C5 incremental loop images/sec", "value": n_img / dt, "unit": "images/s",
+           "seconds": dt, "stage_seconds": stage,
+           "ba_calls": len(steps), "ba_lm_iterations": iters,
+           "ba_lm_iters_per_sec_in_loop": iters / max(stage["ba"], 1e-12),
+           "kept_images": 1 + sum(s.kept for s in steps),
+           "world_points": last.world_points, "world_observations": last.world_observations,
+           "final_ba": {"rmse_initial": last.ba.rmse_initial, "rmse_final": last.ba.rmse_final,
+                        "iterations": last.ba.iterations, "observations": last.ba_observations},
+           "config": {"workload": f"C5 SequentialActuator loop, {n_img}-image synthetic closed orbit "
+                                  f"({seq.cfg.n_landmarks} landmarks, tracks ~{seq.cfg.track_mean:g} images, "
+                                  f"{seq.cfg.n_clutter} clutter keypoints/image), LocalFrame + GlobalFrame "
+                                  "mutual matching and a fresh BundleAdjuster per image, "
+                                  "Image::setIntrinsic quirk on (reference write-back)"}}
+    log(f"loop: {n_img} images in {dt:.2f}s ({n_img / dt:.1f} images/s), stages "
+        + ", ".join(f"{k} {v:.2f}s" for k, v in stage.items())
+        + f"; {iters} LM iterations; world {last.world_points} pts / {last.world_observations} obs")
+    if cpu:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import _helpers as H   # oracle loader (test infrastructure: the CPU baseline only)
+            model, nth = host_cpu()
+            n = min(cpu_images, n_img)
+            ol = H.OracleSeqLoop(threads=nth)
+            t1 = time.perf_counter()
+            ol.init(imgs[0], imgs[1])
+            ol.bundle_adjust()
+            for k in range(2, n):
+                ol.add(imgs[k])
+                ol.bundle_adjust()
+            cdt = time.perf_counter() - t1
+            ol.close()
+            gpu_first = sum(s.seconds_local_match + s.seconds_global_match + s.seconds_geometry + s.seconds_ba
+                            for s in steps[:n - 1])
+            out["cpu_baseline"] = {"value": n / cdt, "unit": "images/s", "cores": nth, "kind": "port",
+                                   "cpu_model": model,
+                                   "sample": f"the first {n} images of the same sequence through the loop oracle "
+                                             f"(CPU matcher + Ceres-semantics solver, {nth} threads), "
+                                             f"{cdt:.1f} s wall; the GPU loop spent {gpu_first:.2f} s on "
+                                             "those images"}
+            log(f"cpu baseline loop: {n} images in {cdt:.1f}s")
+        except Exception as ex:
+            log(f"cpu baseline loop unavailable: {ex}")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -282,6 +354,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--no-snavely", action="store_true")
+    ap.add_argument("--no-loop", action="store_true")
+    ap.add_argument("--loop-images", type=int, default=300)
     # diagnostic: rank 0's shard of an N-way landmark partition on this one GPU,
     # with a no-op all-reduce (per-rank kernel times of the N-GPU run; the
     # solve itself is then not the global one, so the result is not a bench line)
@@ -537,6 +611,11 @@ def main():
         log(f"match cascade: {len(pairs)} pairs in {cdt:.3f}s (index {t_idx * 1e3:.1f} ms) -> "
             f"{len(pairs) / cdt:.0f} pairs/s, match kernels {ckms:.1f} ms")
 
+    # ---------------- incremental loop (C5) ----------------
+    loop = None
+    if world == 1 and rank == 0 and not args.no_loop and args.fake_world <= 1:
+        loop = bench_loop(ctx, args.loop_images, cpu=not args.no_cpu_baseline)
+
     cpu = None
     cpu_match = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -601,6 +680,7 @@ def main():
             "match": match,
             "ba_snavely": snav,
             "ba_pcie_inclusive": pcie,
+            "loop": loop,
         }
         print(json.dumps(out))
     plan.close()

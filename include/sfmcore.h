@@ -323,6 +323,104 @@ int sfm_synth_descriptors(int32_t n_img, int32_t n_kp, uint64_t seed,
                           uint8_t* desc /* [n_img*n_kp*128] */);
 
 /* ------------------------------------------------------------------------ */
+/* Incremental loop: SequentialActuator (src/actuator/SequentialActuator.h)  */
+/* as src/main.cpp:99-108 drives it (BASELINE.json config C5):               */
+/*   init(img0, img1); bundleAdjustment();                                  */
+/*   for i >= 2 { addSingleImage(img_i); bundleAdjustment(); }               */
+/* LocalFrame mutual matching + 4*min filter and GlobalFrame world-point     */
+/* matching + 3*min filter run on the GPU matcher (sfm_match_dense MUTUAL);  */
+/* bundleAdjustment is a fresh BundleAdjuster over the whole world per call  */
+/* (:226-229) on the GPU solver (sfm_ba_solve).  The OpenCV geometry          */
+/* (findEssentialMat / recoverPose / solvePnPRansac) is out of scope: each   */
+/* image carries the pose that solver would return (pose_prior) and the      */
+/* inlier masks are geometric checks against the current poses (the C++      */
+/* header include/sfm/actuator.hpp documents each stand-in).                 */
+/* ------------------------------------------------------------------------ */
+typedef struct sfm_seq_image {
+    int32_t n_kp;
+    int32_t reserved;
+    const double* kp_xy;     /* [2*n_kp] keypoint pixel coordinates           */
+    const uint8_t* desc;     /* [n_kp*128] descriptors (RootSIFT uchar)       */
+    double pose_prior[6];    /* Tcw as angle-axis + t (the geometric solver's
+                                output; image 0's is ignored: Tcw = I)       */
+} sfm_seq_image;
+
+typedef struct sfm_seq_options {
+    double fx, fy, cx, cy;   /* the one shared Camera (main.cpp:91,124)       */
+    double epipolar_px;      /* essential-matrix inlier threshold, px (4.0)   */
+    double pnp_reproj_px;    /* solvePnPRansac reprojectionError (8.0, :179)  */
+    double max_depth;        /* recoverPose distanceThresh (100)              */
+    int64_t min_pnp_inliers; /* drop the image below this (30, :191)          */
+    int32_t fixed_writeback; /* 0: Image::setIntrinsic ZYX-Euler quirk (the
+                                reference); 1: store the angle-axis          */
+    int32_t reserved;
+    sfm_ba_options ba;       /* BundleAdjuster() solver options               */
+} sfm_seq_options;
+
+/* What one init / addSingleImage (+ the following bundleAdjustment) did. */
+typedef struct sfm_seq_step {
+    int32_t image;              /* sequence index of the new image           */
+    int32_t kept;               /* 0: dropped (< min_pnp_inliers)            */
+    int64_t local_raw, local_kept;     /* LocalFrame matches before / after
+                                          the 4*min filter                  */
+    int64_t global_raw, global_kept;   /* GlobalFrame, 3*min filter          */
+    int64_t pnp_inliers, epipolar_inliers;
+    int64_t new_points, extended_obs;  /* savePointCloudToWorld             */
+    int64_t world_points, world_observations;
+    sfm_ba_summary ba;          /* last bundleAdjustment of this step        */
+    int32_t ba_rc;              /* its return code (1: not run yet)          */
+    int32_t reserved;
+    int64_t ba_images, ba_points, ba_observations;   /* its problem size    */
+    double seconds_local_match, seconds_global_match, seconds_geometry, seconds_ba;
+} sfm_seq_step;
+
+typedef struct sfm_seq sfm_seq;
+/* [cpu] SequentialActuator defaults + BundleAdjuster() options. */
+void sfm_seq_default_options(sfm_seq_options* opts);
+int sfm_seq_create(sfm_ctx* ctx, const sfm_seq_options* opts, sfm_seq** out);
+int sfm_seq_init(sfm_seq* seq, const sfm_seq_image* img0, const sfm_seq_image* img1);
+/* *kept = 0 when the image was dropped (fewer than min_pnp_inliers). */
+int sfm_seq_add_image(sfm_seq* seq, const sfm_seq_image* img, int32_t* kept);
+int sfm_seq_bundle_adjust(sfm_seq* seq, sfm_ba_summary* summary);
+int sfm_seq_last_step(sfm_seq* seq, sfm_seq_step* step);
+/* The last step's filtered matches: which 0 = LocalFrame (query = image1
+ * keypoint, train = image2 keypoint), 1 = GlobalFrame (query = world point in
+ * index order, train = image keypoint).  dist = sqrt of the exact L2^2. */
+int sfm_seq_matches(sfm_seq* seq, int32_t which, int32_t* query, int32_t* train,
+                    float* dist, int64_t cap, int64_t* n);
+/* World state: points in index order (X[3*n]), the observation count of
+ * each (n_obs[n]), every image's pose in sequence order (poses[6*n_img]) and
+ * the shared camera's {fx, fy, cx, cy}.  NULL arrays: sizes only. */
+int sfm_seq_world(sfm_seq* seq, double* X, int64_t* n_obs, int64_t cap_pts, int64_t* n_pts,
+                  double* poses, int32_t cap_img, int32_t* n_img, double* intr4);
+int sfm_seq_destroy(sfm_seq* seq);
+
+/* [cpu] Synthetic closed-orbit image sequence for C5: cameras on a circle of
+ * radius 10 around a cube of landmarks (side 4), looking at its centre, all
+ * with the reference intrinsics (fx = fy = 2905.88, cx 1416, cy 1064).  Each
+ * landmark faces a direction and is seen from an arc of consecutive images
+ * (tracks of ~track_mean images), detected with detect_prob; its observed
+ * descriptor is a RootSIFT-like base with desc_noise_dims entries moved by up
+ * to +-desc_noise_amp.  n_clutter unmatched keypoints per image.  Keypoint
+ * order is shuffled per image.  pose_prior = ground-truth Tcw relative to
+ * image 0 (the reconstruction's world frame) + N(0, prior_rot^2) rad /
+ * N(0, prior_t^2) noise; image 0's is exactly zero. */
+typedef struct sfm_synth_orbit_config {
+    int32_t n_img, n_clutter;
+    int64_t n_landmarks;
+    double track_mean, detect_prob, noise_px;
+    int32_t desc_noise_dims, desc_noise_amp;
+    double prior_rot, prior_t;
+    uint64_t seed;
+} sfm_synth_orbit_config;
+/* Two calls: NULL arrays return *n_kp only.  landmark[n_kp] (optional):
+ * ground-truth landmark of each keypoint or -1 for clutter; gt_X (optional,
+ * [3*n_landmarks]) landmark positions in the image-0 frame. */
+int sfm_synth_orbit_image(const sfm_synth_orbit_config* cfg, int32_t img, int32_t* n_kp,
+                          double* kp_xy, uint8_t* desc, double* pose_prior,
+                          int64_t* landmark, double* gt_X);
+
+/* ------------------------------------------------------------------------ */
 /* File-staged sparseBuilder flow.                   */
 /* The reference's matchPair()/match() (sparseBuilder.cpp:758-1023) talk to  */
 /* each other through files in <base>/output/matches written by OpenMVG's    */

@@ -36,7 +36,8 @@ inline int32_t l2sq(const uint8_t* a, const uint8_t* b) {
 
 // For every row of q: best and second-best (value) over rows of db.
 void top2(const uint8_t* db, int32_t n_db, const uint8_t* q, int32_t n_q,
-          int32_t* best_idx, int32_t* best_d, int32_t* second_d) {
+          int32_t* best_idx, int32_t* best_d, int32_t* second_d, int n_threads = 1) {
+#pragma omp parallel for schedule(static, 64) num_threads(n_threads > 0 ? n_threads : 1) if (n_threads > 1)
     for (int32_t t = 0; t < n_q; ++t) {
         int32_t b1 = INT32_MAX, b2 = INT32_MAX, i1 = -1;
         const uint8_t* qt = q + (int64_t)t * 128;
@@ -55,10 +56,16 @@ void top2(const uint8_t* db, int32_t n_db, const uint8_t* q, int32_t n_q,
 extern "C" int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,
                                int32_t mode, float ratio, int32_t* match_idx,
                                int32_t* match_d2) {
+    return orc_match_dense_mt(a, n_a, b, n_b, mode, ratio, 1, match_idx, match_d2);
+}
+
+extern "C" int orc_match_dense_mt(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,
+                                  int32_t mode, float ratio, int32_t n_threads, int32_t* match_idx,
+                                  int32_t* match_d2) {
     if (n_a < 0 || n_b < 0) return SFM_ERR_INVALID_ARG;
     if (mode == SFM_MATCH_RATIO) {
         std::vector<int32_t> bi(n_b), bd(n_b), sd(n_b);
-        top2(a, n_a, b, n_b, bi.data(), bd.data(), sd.data());
+        top2(a, n_a, b, n_b, bi.data(), bd.data(), sd.data(), n_threads);
         const float r2 = ratio * ratio;  // Square(f_dist_ratio) in float
         for (int32_t t = 0; t < n_b; ++t) {
             bool keep = n_a >= 2 && (float)bd[t] < r2 * (float)sd[t];
@@ -69,8 +76,8 @@ extern "C" int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, 
     }
     if (mode == SFM_MATCH_MUTUAL) {
         std::vector<int32_t> nq(n_a), dq(n_a), nt(n_b), dt(n_b);
-        top2(b, n_b, a, n_a, nq.data(), dq.data(), nullptr);  // per query row of a
-        top2(a, n_a, b, n_b, nt.data(), dt.data(), nullptr);  // per train row of b
+        top2(b, n_b, a, n_a, nq.data(), dq.data(), nullptr, n_threads);  // per query row of a
+        top2(a, n_a, b, n_b, nt.data(), dt.data(), nullptr, n_threads);  // per train row of b
         for (int32_t q = 0; q < n_a; ++q) {
             const int32_t t = nq[q];
             const bool keep = t >= 0 && nt[t] == q;

@@ -67,6 +67,25 @@ int orc_ba_jacobian_model(int32_t model, int32_t mode, const double* intr, const
 int orc_match_dense(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,
                     int32_t mode, float ratio, int32_t* match_idx, int32_t* match_d2);
 
+/* The same on n_threads OpenMP threads. */
+int orc_match_dense_mt(const uint8_t* a, int32_t n_a, const uint8_t* b, int32_t n_b,
+                       int32_t mode, float ratio, int32_t n_threads, int32_t* match_idx,
+                       int32_t* match_d2);
+
+/* Incremental loop oracle (seq_oracle.cpp): sfm_seq_* semantics with the CPU
+ * matcher and solver. */
+typedef struct orc_seq orc_seq;
+int orc_seq_create(const sfm_seq_options* opts, int32_t n_threads, orc_seq** out);
+int orc_seq_init(orc_seq* s, const sfm_seq_image* a, const sfm_seq_image* b);
+int orc_seq_add_image(orc_seq* s, const sfm_seq_image* im, int32_t* kept);
+int orc_seq_bundle_adjust(orc_seq* s, sfm_ba_summary* summary);
+int orc_seq_last_step(orc_seq* s, sfm_seq_step* step);
+int orc_seq_matches(orc_seq* s, int32_t which, int32_t* query, int32_t* train, float* dist,
+                    int64_t cap, int64_t* n);
+int orc_seq_world(orc_seq* s, double* X, int64_t* n_obs, int64_t cap_pts, int64_t* n_pts,
+                  double* poses, int32_t cap_img, int32_t* n_img, double* intr4);
+int orc_seq_destroy(orc_seq* s);
+
 /* All-pairs, compacted (counts per pair; matches sorted by (i,j)).
  * Two calls: counts only when i/j/d2 are NULL. */
 int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,

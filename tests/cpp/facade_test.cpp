@@ -86,6 +86,27 @@ int main() {
     CHECK(std::fabs(cam->fx - i2[0]) < 1e-3 * i2[0]);
     std::printf("BA: rmse %.6f -> %.6f (%d iterations), oracle %.6f\n", s.rmse_initial, s.rmse_final, s.iterations,
                 os.rmse_final);
+    // written-back poses: Image::setIntrinsic reads the angle-axis as ZYX Euler
+    // angles (Image.h:131-141); the façade's world holds quirk(solved pose)
+    {
+        double worst = 0, moved = 0;
+        for (int c = 0; c < cfg.n_cam; ++c) {
+            const double* e = &e2[6 * pos[c]];
+            double R[9], w[3];
+            sfm::rot::zyx_euler_to_matrix(e[0], e[1], e[2], R);
+            sfm::rot::matrix_to_aa(R, w);
+            const auto& p = imgs[c]->pose();
+            for (int a = 0; a < 3; ++a) {
+                worst = std::max(worst, std::fabs(p[a] - w[a]));
+                moved = std::max(moved, std::fabs(p[a] - e[a]));
+            }
+            for (int a = 3; a < 6; ++a) worst = std::max(worst, std::fabs(p[a] - e[a]));
+        }
+        CHECK(worst < 2e-3);    // parameter agreement bar (gauge-null direction)
+        CHECK(moved > 1e-2);    // the quirk visibly changed written-back rotations
+        std::printf("BA write-back: poses = quirk(solved) within %.2e (quirk moved them by up to %.3f)\n", worst,
+                    moved);
+    }
 
     // ---- LocalFrame / GlobalFrame matching --------------------------------------
     std::vector<uint8_t> desc(4 * 700 * 128);
@@ -107,6 +128,61 @@ int main() {
     CHECK(n == nref && n > 0);
     for (auto& m : lf.getMatches()) CHECK(oi[m.queryIdx] == m.trainIdx);
     std::printf("LocalFrame: %zu matches after the 4*min filter\n", n);
+
+    // ---- SequentialActuator: init + BA, addSingleImage + BA (main.cpp:99-108) -----
+    {
+        sfm_synth_orbit_config oc{};
+        oc.n_img = 300; oc.n_clutter = 300; oc.n_landmarks = 12000; oc.track_mean = 10; oc.detect_prob = 0.95;
+        oc.noise_px = 0.5; oc.desc_noise_dims = 24; oc.desc_noise_amp = 3; oc.prior_rot = 2e-4; oc.prior_t = 1e-3;
+        oc.seed = 5;
+        const int n_seq = 6;
+        std::vector<sfm::SeqImage> simgs(n_seq);
+        std::vector<std::vector<double>> kps(n_seq);
+        std::vector<sfm_seq_image> cimgs(n_seq);
+        for (int k = 0; k < n_seq; ++k) {
+            int32_t nk = 0;
+            CHECK(sfm_synth_orbit_image(&oc, k, &nk, nullptr, nullptr, nullptr, nullptr, nullptr) == SFM_OK);
+            kps[k].resize(2 * nk);
+            simgs[k].descriptors.resize((size_t)nk * 128);
+            CHECK(sfm_synth_orbit_image(&oc, k, &nk, kps[k].data(), simgs[k].descriptors.data(),
+                                        simgs[k].pose_prior.data(), nullptr, nullptr) == SFM_OK);
+            for (int q = 0; q < nk; ++q) simgs[k].keypoints.push_back({kps[k][2 * q], kps[k][2 * q + 1]});
+            cimgs[k] = sfm_seq_image{nk, 0, kps[k].data(), simgs[k].descriptors.data(), {}};
+            for (int a = 0; a < 6; ++a) cimgs[k].pose_prior[a] = simgs[k].pose_prior[a];
+        }
+        auto seq_cam = std::make_shared<sfm::Camera>(2905.88, 2905.88, 1416.0, 1064.0);
+        sfm::SequentialActuator act(seq_cam, ctx);
+        sfm_seq_options so;
+        sfm_seq_default_options(&so);
+        orc_seq* os2 = nullptr;
+        CHECK(orc_seq_create(&so, 4, &os2) == SFM_OK);
+        act.init(simgs[0], simgs[1]);
+        act.bundleAdjustment();
+        CHECK(orc_seq_init(os2, &cimgs[0], &cimgs[1]) == SFM_OK);
+        sfm_ba_summary ob{};
+        CHECK(orc_seq_bundle_adjust(os2, &ob) == SFM_OK);
+        for (int k = 2; k < n_seq; ++k) {
+            int32_t kept = 0;
+            CHECK(act.addSingleImage(simgs[k]));
+            act.bundleAdjustment();
+            CHECK(orc_seq_add_image(os2, &cimgs[k], &kept) == SFM_OK && kept);
+            CHECK(orc_seq_bundle_adjust(os2, &ob) == SFM_OK);
+            sfm_seq_step og{};
+            orc_seq_last_step(os2, &og);
+            const auto& g = act.lastStep();
+            CHECK(g.local_kept == og.local_kept && g.global_kept == og.global_kept && g.new_points == og.new_points);
+            CHECK(g.world_points == og.world_points && g.world_observations == og.world_observations);
+            CHECK(g.ba.iterations == og.ba.iterations && std::fabs(g.ba.rmse_final / og.ba.rmse_final - 1) < 1e-6);
+        }
+        std::vector<double> oposes(6 * n_seq);
+        int32_t oni = 0;
+        CHECK(orc_seq_world(os2, nullptr, nullptr, 0, nullptr, oposes.data(), n_seq, &oni, nullptr) == SFM_OK);
+        for (int k = 0; k < n_seq; ++k)
+            for (int a = 0; a < 6; ++a) CHECK(std::fabs(act.images()[k]->pose()[a] - oposes[6 * k + a]) < 1e-8);
+        orc_seq_destroy(os2);
+        std::printf("SequentialActuator: %d images, %lld world points, same as the loop oracle\n", n_seq,
+                    (long long)act.lastStep().world_points);
+    }
 
     // ---- sparseBuilder::matchPair + match -------------------------------------------
     sfm::sparse::sparseBuilder sb(ctx);

@@ -1,0 +1,102 @@
+"""GPU parity of the incremental SequentialActuator loop (BASELINE.json config
+C5; src/actuator/SequentialActuator.h:85-229 driven as src/main.cpp:99-108).
+
+The first images of the C5 closed-orbit sequence go through the product loop
+(LocalFrame / GlobalFrame matching on the GPU matcher, a fresh GPU
+BundleAdjuster per call) and through the loop oracle (the same loop on the
+CPU restatements).  Asserted at every step: the same LocalFrame matches after
+the 4*min filter (LocalFrame.h:49-64) and the same GlobalFrame matches after
+the 3*min filter (GlobalFrame.h:45-60) — query, train and distance bit-exact
+—, the same kept/dropped decision, the same world growth, and a bundle
+adjustment with the same iteration count and "RMSE" (BundleAdjuster.h:137-138)
+within 1e-6 relative.  The written-back poses (Image::setIntrinsic's ZYX-Euler
+quirk, Image.h:131-141) and points agree at the end."""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+import _helpers as H
+
+pytestmark = pytest.mark.gpu
+api = importlib.import_module("3dreconstruction_amd.api")
+THREADS = max(1, min(16, os.cpu_count() or 1))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = api.Context(0)
+    yield c
+    c.close()
+
+
+def _same_step(g, o, k):
+    for f in ("kept", "local_raw", "local_kept", "global_raw", "global_kept", "pnp_inliers",
+              "epipolar_inliers", "new_points", "extended_obs", "world_points", "world_observations",
+              "ba_images", "ba_points", "ba_observations", "ba_rc"):
+        assert getattr(g, f) == getattr(o, f), (k, f, getattr(g, f), getattr(o, f))
+
+
+def _same_matches(gl, ol, k):
+    for which in (0, 1):
+        gq, gt, gd = gl.matches(which)
+        oq, ot, od = ol.matches(which)
+        assert np.array_equal(gq, oq) and np.array_equal(gt, ot), (k, which)
+        assert np.array_equal(gd.view(np.uint32), od.view(np.uint32)), (k, which)
+
+
+def _same_ba(g, o, k):
+    assert g.usable == o.usable and g.termination == o.termination, k
+    assert g.iterations == o.iterations and g.successful_steps == o.successful_steps, \
+        (k, g.iterations, o.iterations)
+    assert abs(g.initial_cost / o.initial_cost - 1) < 1e-9, k
+    assert abs(g.rmse_final / o.rmse_final - 1) < 1e-6, (k, g.rmse_final, o.rmse_final)
+
+
+def _run_both(ctx, seq, n, opts, imgs=None):
+    imgs = imgs or [seq.image(k) for k in range(n)]
+    gl = api.SeqLoop(ctx, opts)
+    ol = H.OracleSeqLoop(opts, threads=THREADS)
+    gl.init(imgs[0], imgs[1])
+    ol.init(imgs[0], imgs[1])
+    steps = []
+    for k in range(1, n):
+        if k >= 2:
+            assert gl.add(imgs[k]) == ol.add(imgs[k]), k
+        gs, os_ = gl.bundle_adjust(), ol.bundle_adjust()
+        g, o = gl.step(), ol.step()
+        _same_step(g, o, k)
+        _same_matches(gl, ol, k)
+        _same_ba(gs, os_, k)
+        steps.append(g)
+    return gl, ol, steps
+
+
+def test_c5_loop_20_images_vs_oracle(ctx):
+    seq = api.OrbitSequence()          # the C5 sequence (300 images); its first 20
+    gl, ol, steps = _run_both(ctx, seq, 20, api.seq_default_options())
+    gw, ow = gl.world(), ol.world()
+    assert len(gw["X"]) == len(ow["X"]) and np.array_equal(gw["n_obs"], ow["n_obs"])
+    np.testing.assert_allclose(gw["X"], ow["X"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(gw["poses"], ow["poses"], rtol=0, atol=1e-8)
+    np.testing.assert_allclose(gw["intr"], ow["intr"], rtol=1e-9)
+    # the loop did real work: tracks extended, GlobalFrame matched, BA improved
+    assert all(s.kept for s in steps) and steps[-1].world_points > 5000
+    assert sum(s.extended_obs for s in steps) > 10 * steps[-1].new_points
+    assert all(s.global_kept >= 30 for s in steps[1:])
+    assert all(s.ba.usable and s.ba.rmse_final < s.ba.rmse_initial for s in steps)
+    gl.close()
+    ol.close()
+
+
+def test_c5_loop_fixed_writeback_and_drop(ctx):
+    # fixed (non-quirk) write-back and a dropped image
+    # (SequentialActuator.h:191-194): the next image pairs with the last kept one
+    seq = api.OrbitSequence(n_landmarks=20000, n_clutter=400, seed=77)
+    o = api.seq_default_options()
+    o.fixed_writeback = 1
+    gl, ol, steps = _run_both(ctx, seq, 12, o, H.corrupted_sequence(seq, 12, 6))
+    assert [s.kept for s in steps] == [1] * 5 + [0] + [1] * 5
+    assert steps[6].local_kept > 100     # image 7 matched against image 5
+    np.testing.assert_allclose(gl.world()["poses"], ol.world()["poses"], rtol=0, atol=1e-8)
