@@ -85,6 +85,10 @@ int orc_seq_matches(orc_seq* s, int32_t which, int32_t* query, int32_t* train, f
 int orc_seq_world(orc_seq* s, double* X, int64_t* n_obs, int64_t cap_pts, int64_t* n_pts,
                   double* poses, int32_t cap_img, int32_t* n_img, double* intr4);
 int orc_seq_destroy(orc_seq* s);
+/* Overwrite the numeric state (X[3*n_pts] in point-index order, poses[6*n_img]
+ * in sequence order, the camera's intr4) of a loop with identical topology. */
+int orc_seq_set_state(orc_seq* s, const double* X, int64_t n_pts, const double* poses, int32_t n_img,
+                      const double* intr4);
 
 /* All-pairs, compacted (counts per pair; matches sorted by (i,j)).
  * Two calls: counts only when i/j/d2 are NULL. */

@@ -6,8 +6,10 @@
 // (include/sfm/actuator.hpp): what this checks is that the GPU matcher and
 // GPU solver, driven through the same loop, make the same decisions — the
 // same filtered match lists, the same dropped images, the same world, and
-// per-call "RMSE" within 1e-6.  Same C signatures as sfm_seq_* (sfmcore.h)
-// with orc_ names, plus a thread count.
+// per-call "RMSE" within 1e-6 on identical inputs (orc_seq_set_state adopts
+// the product loop's numeric state after each call: the reference problem's
+// scale gauge is free, so two correct solvers part along it).  Same C
+// signatures as sfm_seq_* (sfmcore.h) with orc_ names, plus a thread count.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -142,5 +144,28 @@ extern "C" int orc_seq_world(orc_seq* s, double* X, int64_t* n_obs, int64_t cap_
 
 extern "C" int orc_seq_destroy(orc_seq* s) {
     delete s;
+    return SFM_OK;
+}
+
+// Re-synchronise the numeric state (point positions in index order, image
+// poses in sequence order, the shared camera) with another run of the loop
+// whose topology is identical.  Used by the loop parity test: each bundle
+// adjustment of the reference problem leaves its scale gauge (only image 1's
+// pose is held constant, BundleAdjuster.h:105) to rounding, so two correct
+// solvers part along it; per-call parity is checked on identical inputs.
+extern "C" int orc_seq_set_state(orc_seq* s, const double* X, int64_t n_pts, const double* poses, int32_t n_img,
+                                 const double* intr4) {
+    auto w = s->act->getWorld();
+    std::vector<std::pair<sfm::WorldPoint::Idx, sfm::WorldPoint::Ptr>> pts(w->points().begin(), w->points().end());
+    std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    const auto& ims = s->act->images();
+    if (n_pts != (int64_t)pts.size() || n_img != (int32_t)ims.size()) return SFM_ERR_INVALID_ARG;
+    for (int64_t k = 0; k < n_pts; ++k) pts[k].second->setPos({X[3 * k], X[3 * k + 1], X[3 * k + 2]});
+    for (int32_t k = 0; k < n_img; ++k) {
+        std::array<double, 6> p;
+        for (int a = 0; a < 6; ++a) p[a] = poses[6 * k + a];
+        ims[k]->setPose(p);
+    }
+    s->act->camera()->setIntrinsic({intr4[0], intr4[1], intr4[2], intr4[3]});
     return SFM_OK;
 }

@@ -59,7 +59,8 @@ def oracle():
                                               abi.i64p]),
                 ("orc_seq_world", C.c_int, [vp, abi.f64p, abi.i64p, C.c_int64, abi.i64p, abi.f64p,
                                             C.c_int32, abi.i32p, abi.f64p]),
-                ("orc_seq_destroy", C.c_int, [vp])]:
+                ("orc_seq_destroy", C.c_int, [vp]),
+                ("orc_seq_set_state", C.c_int, [vp, abi.f64p, C.c_int64, abi.f64p, C.c_int32, abi.f64p])]:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -225,6 +226,15 @@ class OracleSeqLoop(api._SeqCalls):
         rc = self.lib.orc_seq_create(C.byref(o), threads, C.byref(h))
         assert rc == 0
         self.h = h
+
+    def set_state(self, w):
+        """adopt another loop's numeric state (same topology)"""
+        X = np.ascontiguousarray(w["X"]).reshape(-1)
+        P = np.ascontiguousarray(w["poses"]).reshape(-1)
+        I = np.ascontiguousarray(w["intr"])
+        rc = self.lib.orc_seq_set_state(self.h, abi.ptr(X, abi.f64p), len(X) // 3, abi.ptr(P, abi.f64p),
+                                        len(P) // 6, abi.ptr(I, abi.f64p))
+        assert rc == 0
 
 
 def corrupted_sequence(seq, n, bad):
