@@ -235,6 +235,7 @@ SIGNATURES = [
     ("sfm_seq_matches", C.c_int, [C.c_void_p, C.c_int32, i32p, i32p, f32p, C.c_int64, i64p]),
     ("sfm_seq_world", C.c_int, [C.c_void_p, f64p, i64p, C.c_int64, i64p, f64p, C.c_int32, i32p,
                                 f64p]),
+    ("sfm_seq_observations", C.c_int, [C.c_void_p, i32p, f64p, C.c_int64, i64p]),
     ("sfm_seq_destroy", C.c_int, [C.c_void_p]),
     ("sfm_synth_orbit_image", C.c_int, [C.POINTER(SynthOrbitConfig), C.c_int32, i32p, f64p, u8p,
                                         f64p, i64p, f64p]),

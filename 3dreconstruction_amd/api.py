@@ -401,6 +401,17 @@ class _SeqCalls:
         return {"X": X[:3 * n_pts.value].reshape(-1, 3), "n_obs": nobs[:n_pts.value],
                 "poses": poses[:6 * n_img.value].reshape(-1, 6), "intr": intr}
 
+    def observations(self):
+        """(image sequence index [n], uv [n, 2]) of every observation, points
+        in index order (counts: world()["n_obs"])"""
+        n = C.c_int64()
+        self._f("observations")(self.h, None, None, 0, C.byref(n))
+        img = np.zeros(max(n.value, 1), np.int32)
+        uv = np.zeros((max(n.value, 1), 2))
+        _check(self._f("observations")(self.h, abi.ptr(img, abi.i32p), abi.ptr(uv, abi.f64p), n.value,
+                                       C.byref(n)), self.prefix + "observations")
+        return img[:n.value], uv[:n.value]
+
     def close(self):
         if self.h:
             self._f("destroy")(self.h)

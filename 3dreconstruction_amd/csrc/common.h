@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/sfmcore.h"
@@ -89,6 +90,13 @@ struct DBuf {
             throw SfmError{SFM_ERR_OOM};
         }
         n = count;
+        // SFM_POISON_ALLOC=1 (tests): every fresh buffer starts as 0xFF bytes
+        // (NaN doubles, -1 integers), so a read before the first write shows
+        if (poison_alloc()) SFM_HIP(hipMemset(p, 0xFF, count * sizeof(T)));
+    }
+    static bool poison_alloc() {
+        static const bool on = std::getenv("SFM_POISON_ALLOC") != nullptr;
+        return on;
     }
     void upload(const T* h, size_t count, hipStream_t s) {
         if (count) SFM_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));

@@ -178,6 +178,11 @@ extern "C" int sfm_seq_world(sfm_seq* s, double* X, int64_t* n_obs, int64_t cap_
     return SFM_OK;
 }
 
+extern "C" int sfm_seq_observations(sfm_seq* s, int32_t* img, double* uv, int64_t cap, int64_t* n) {
+    if (!s || !n) return SFM_ERR_INVALID_ARG;
+    return seq_observations(*s->act, img, uv, cap, n);
+}
+
 extern "C" int sfm_seq_destroy(sfm_seq* s) {
     delete s;
     return SFM_OK;

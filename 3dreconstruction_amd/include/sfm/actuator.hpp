@@ -28,8 +28,10 @@
 // (knnMatch shape, frames.hpp) and a fresh bundle adjuster per call.  The
 // product (sfm.hpp) binds the GPU; the loop oracle binds the CPU restatement.
 #pragma once
+#include <algorithm>
 #include <array>
 #include <chrono>
+#include <unordered_map>
 #include <cmath>
 #include <cstdint>
 #include <memory>
@@ -486,5 +488,27 @@ class BasicSequentialActuator {
     std::vector<DMatch> local_, global_;
     sfm_seq_step step_{};
 };
+
+// Every world point's observations in point-index order: the sequence index
+// of the observing image and the observed pixel (sfm_seq_observations).
+template <class Act>
+int seq_observations(const Act& act, int32_t* img, double* uv, int64_t cap, int64_t* n) {
+    auto w = act.getWorld();
+    std::vector<std::pair<WorldPoint::Idx, WorldPoint::Ptr>> pts(w->points().begin(), w->points().end());
+    std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    std::unordered_map<const Image*, int32_t> seq_idx;
+    for (std::size_t k = 0; k < act.images().size(); ++k) seq_idx[act.images()[k].get()] = (int32_t)k;
+    int64_t m = 0;
+    for (auto& [i, p] : pts)
+        for (auto& [im, o] : p->observed_frames_) {
+            if (m < cap) {
+                if (img) img[m] = seq_idx.at(im.get());
+                if (uv) { uv[2 * m] = o.x; uv[2 * m + 1] = o.y; }
+            }
+            ++m;
+        }
+    *n = m;
+    return SFM_OK;
+}
 
 }  // namespace sfm

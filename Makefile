@@ -8,7 +8,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -mcode-object-version=5 
             -Wall -Wno-unused-result -I/opt/rocm/include
 SRCS := $(wildcard $(CSRC)/*.cpp $(CSRC)/*.hip)
 OBJS := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
-HDRS := $(wildcard $(CSRC)/*.h) include/sfmcore.h
+HDRS := $(wildcard $(CSRC)/*.h) include/sfmcore.h $(wildcard $(PKG)/include/sfm/*.hpp)
 
 all: $(LIB) oracle/liboracle.so tests/cpp/facade_test
 
@@ -18,7 +18,7 @@ build/%.hip.o: $(CSRC)/%.hip $(HDRS)
 
 build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -fvisibility=hidden -fvisibility-inlines-hidden -x hip -c $< -o $@
 
 $(LIB): $(OBJS)
 	@mkdir -p $(PKG)/lib

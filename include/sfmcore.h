@@ -33,6 +33,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* the C-ABI is the only exported surface (libraries build with hidden default visibility) */
+#pragma GCC visibility push(default)
 
 #define SFM_OK                 0
 #define SFM_ERR_INVALID_ARG   -1
@@ -393,6 +395,9 @@ int sfm_seq_matches(sfm_seq* seq, int32_t which, int32_t* query, int32_t* train,
  * the shared camera's {fx, fy, cx, cy}.  NULL arrays: sizes only. */
 int sfm_seq_world(sfm_seq* seq, double* X, int64_t* n_obs, int64_t cap_pts, int64_t* n_pts,
                   double* poses, int32_t cap_img, int32_t* n_img, double* intr4);
+/* Every world point's observations, points in index order (counts from
+ * sfm_seq_world's n_obs): the observing image's sequence index and the pixel. */
+int sfm_seq_observations(sfm_seq* seq, int32_t* img, double* uv, int64_t cap, int64_t* n);
 int sfm_seq_destroy(sfm_seq* seq);
 
 /* [cpu] Synthetic closed-orbit image sequence for C5: cameras on a circle of
@@ -489,6 +494,7 @@ typedef struct sfm_sparse_match_stats {
 int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm_sparse_match_opts* opts,
                      sfm_sparse_match_stats* stats);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif

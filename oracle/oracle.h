@@ -33,6 +33,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* the C-ABI is the only exported surface (libraries build with hidden default visibility) */
+#pragma GCC visibility push(default)
 
 /* op: 0 = sum, 1 = max.  In-place over buf[n]. */
 typedef void (*orc_allreduce_fn)(void* user, double* buf, int64_t n, int32_t op);
@@ -84,6 +86,7 @@ int orc_seq_matches(orc_seq* s, int32_t which, int32_t* query, int32_t* train, f
                     int64_t cap, int64_t* n);
 int orc_seq_world(orc_seq* s, double* X, int64_t* n_obs, int64_t cap_pts, int64_t* n_pts,
                   double* poses, int32_t cap_img, int32_t* n_img, double* intr4);
+int orc_seq_observations(orc_seq* s, int32_t* img, double* uv, int64_t cap, int64_t* n);
 int orc_seq_destroy(orc_seq* s);
 /* Overwrite the numeric state (X[3*n_pts] in point-index order, poses[6*n_img]
  * in sequence order, the camera's intr4) of a loop with identical topology. */
@@ -109,6 +112,7 @@ int orc_dedup_decorator(const uint32_t* i, const uint32_t* j, int64_t n, const f
 /* CascadeHasher::Init projections, float [188][128]. */
 int orc_cascade_projections(float* out);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif

@@ -142,6 +142,10 @@ extern "C" int orc_seq_world(orc_seq* s, double* X, int64_t* n_obs, int64_t cap_
     return SFM_OK;
 }
 
+extern "C" int orc_seq_observations(orc_seq* s, int32_t* img, double* uv, int64_t cap, int64_t* n) {
+    return seq_observations(*s->act, img, uv, cap, n);
+}
+
 extern "C" int orc_seq_destroy(orc_seq* s) {
     delete s;
     return SFM_OK;

@@ -60,6 +60,7 @@ def oracle():
                 ("orc_seq_world", C.c_int, [vp, abi.f64p, abi.i64p, C.c_int64, abi.i64p, abi.f64p,
                                             C.c_int32, abi.i32p, abi.f64p]),
                 ("orc_seq_destroy", C.c_int, [vp]),
+                ("orc_seq_observations", C.c_int, [vp, abi.i32p, abi.f64p, C.c_int64, abi.i64p]),
                 ("orc_seq_set_state", C.c_int, [vp, abi.f64p, C.c_int64, abi.f64p, C.c_int32, abi.f64p])]:
             fn = getattr(lib, name)
             fn.restype = res
