@@ -92,7 +92,11 @@ struct DBuf {
         n = count;
         // SFM_POISON_ALLOC=1 (tests): every fresh buffer starts as 0xFF bytes
         // (NaN doubles, -1 integers), so a read before the first write shows
-        if (poison_alloc()) SFM_HIP(hipMemset(p, 0xFF, count * sizeof(T)));
+        // (completed before any stream can use the buffer)
+        if (poison_alloc()) {
+            SFM_HIP(hipMemset(p, 0xFF, count * sizeof(T)));
+            SFM_HIP(hipDeviceSynchronize());
+        }
     }
     static bool poison_alloc() {
         static const bool on = std::getenv("SFM_POISON_ALLOC") != nullptr;
