@@ -806,7 +806,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
 //             the k-th one stores L_kk, X_kk and y_k = X_kk b_k
 //   update k  A_ij -= L_ik L_jk' for k < j <= i (one workgroup per tile, MFMA),
 //             b_i -= L_ik y_k (forward substitution, fused)
-//   back      x_k = X_kk' (y_k - sum_{j>k} L_jk' x_j), one workgroup
+//   back      x_k = X_kk' y_k, then y_i -= L_ki' x_k for i < k (one launch per k)
 // ===========================================================================
 namespace {
 
@@ -920,29 +920,48 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k, in
     }
 }
 
-// back substitution L' x = y, one workgroup: x_k = X_kk' (y_k - sum_{j>k} L_jk' x_j)
-__global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem P) {
-    __shared__ double part[4][M], t[M];
+// back substitution L' x = y, right-looking by block column, one launch per
+// k (descending): every workgroup forms x_k = X_kk' y_k (y_k is final: the
+// launches for j > k have subtracted their L_jk' x_j), then workgroup i < k
+// applies y_i -= L_ki' x_k from row block k (contiguous rows).  The k = 0
+// launch also publishes x to yF.
+__global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem P, int k) {
+    __shared__ double Xs[M * (M + 1)], yk[M], xk[M], part[4][M];
     const int64_t np = d.np;
     const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    for (int k = d.nt - 1; k >= 0; --k) {
-        // column c of block k: sum over rows r > this block of L[r][k*64 + c] x[r]
-        double s = 0.0;
-        for (int64_t r = (int64_t)(k + 1) * kDM + g; r < np; r += 4) s += d.A[r * np + (int64_t)k * kDM + c] * d.x[r];
-        part[g][c] = s;
-        __syncthreads();
-        if (threadIdx.x < M) t[c] = d.y[(int64_t)k * kDM + c] - (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
-        __syncthreads();
-        if (threadIdx.x < M) {   // x_k = X_kk' t: X lower, so rows m >= c
-            const double* X = d.X + (int64_t)k * kDM * kDM;
-            double v = 0.0;
-            for (int mm = c; mm < M; ++mm) v += X[mm * M + c] * t[mm];
-            d.x[(int64_t)k * kDM + c] = v;
-        }
-        __syncthreads();
+    {   // X_kk and y_k into LDS: all loads in flight at once
+        const double* X = d.X + (int64_t)k * kDM * kDM;
+        double v[M / 4];
+#pragma unroll
+        for (int q = 0; q < M / 4; ++q) v[q] = X[(4 * q + g) * M + c];
+#pragma unroll
+        for (int q = 0; q < M / 4; ++q) Xs[(4 * q + g) * (M + 1) + c] = v[q];
+        if (threadIdx.x < M) yk[c] = d.y[(int64_t)k * kDM + c];
     }
-    for (int64_t e = threadIdx.x; e < P.nF; e += NT) P.yF[e] = d.x[e];
-    if (threadIdx.x == 0) P.scal[kScSolveFail] = d.fail[0];
+    __syncthreads();
+    if (threadIdx.x < M) {   // x_k = X_kk' y_k: X lower, so rows m >= c
+        double v = 0.0;
+        for (int mm = c; mm < M; ++mm) v += Xs[mm * (M + 1) + c] * yk[mm];
+        xk[c] = v;
+        if (blockIdx.x == 0) d.x[(int64_t)k * kDM + c] = v;
+    }
+    __syncthreads();
+    if (k == 0) {
+        for (int64_t e = threadIdx.x; e < P.nF; e += NT) P.yF[e] = e < M ? xk[e] : d.x[e];
+        if (threadIdx.x == 0) P.scal[kScSolveFail] = d.fail[0];
+        return;
+    }
+    const int i = blockIdx.x;   // < k
+    const double* L = d.A + (int64_t)k * kDM * np + (int64_t)i * kDM + c;
+    double lv[M / 4];
+#pragma unroll
+    for (int q = 0; q < M / 4; ++q) lv[q] = L[(int64_t)(4 * q + g) * np];
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < M / 4; ++q) s += lv[q] * xk[4 * q + g];
+    part[g][c] = s;
+    __syncthreads();
+    if (threadIdx.x < M) d.y[(int64_t)i * kDM + c] -= ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
 }
 
 }  // namespace
@@ -988,8 +1007,10 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
             SFM_HIP(hipGetLastError());
         }
     }
-    hipLaunchKernelGGL(dense_back_kernel, dim3(1), dim3(NT), 0, s, d, P);
-    SFM_HIP(hipGetLastError());
+    for (int k = d.nt - 1; k >= 0; --k) {
+        hipLaunchKernelGGL(dense_back_kernel, dim3(k > 0 ? k : 1), dim3(NT), 0, s, d, P, k);
+        SFM_HIP(hipGetLastError());
+    }
 }
 
 }  // namespace sfm

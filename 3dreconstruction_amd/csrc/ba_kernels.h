@@ -60,6 +60,12 @@ struct DevProblem {
     const int64_t* gz_off;          // [n_gpt+1]
     const PTerm* pterms;
     double* Z;                      // general points' eliminated rows, w after each point's blocks
+    int32_t n_plong;                // targets with > preduce_long_threshold() product terms
+    const int32_t* plong_targets;   // [n_plong] target ids
+    int32_t n_plseg;                // kReduceSeg-term segments of their product-term lists
+    const int32_t* plseg_off;       // [n_plong+1]
+    const int32_t* plseg;           // [n_plseg][2] (long index, first product term)
+    double* plpart;                 // [n_plseg][36]
     // state
     double* scaleE;     // [3*n_spt]
     double* scaleF;     // [nF]
@@ -121,6 +127,7 @@ size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);
 constexpr int kGStepThreads = 128;   // general points per step workgroup
 int reduce_long_threshold();
+int preduce_long_threshold();
 constexpr int kReduceSeg = 256;   // terms per long-target segment (one workgroup)
 
 }  // namespace sfm

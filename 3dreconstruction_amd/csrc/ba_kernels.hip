@@ -1655,12 +1655,16 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
 // target's terms (in order) of Z_a[r] . Z_b[c] (3-vectors).  One wave per
 // target, one lane per element; runs after reduce_kernel has written the sum
 // terms.
+// Lists longer than this (the intrinsics arrow and corner collect one term
+// per general point) go through preduce_seg_kernel + preduce_long_kernel.
+constexpr int kLongPTerms = 64;
+
 __global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int e = threadIdx.x & 63;
     if (t >= P.n_targets) return;
     const ReduceTarget T = P.targets[t];
-    if (T.p_end == T.p_begin || e >= T.rows * T.cols) return;
+    if (T.p_end == T.p_begin || T.p_end - T.p_begin > kLongPTerms || e >= T.rows * T.cols) return;
     const int r = e / T.cols, cc = e % T.cols;
     const bool vec = T.cols == 1;
     const double* Z = P.Z;
@@ -1688,6 +1692,62 @@ __global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
     }
     double* dst = target_base(P, T.dst_kind) + T.dst + (vec ? r : (int64_t)r * T.ld + cc);
     *dst -= s;
+}
+
+// Long product-term lists, pass 1: one workgroup per kReduceSeg-term segment,
+// one term per thread (all <= 36 elements of the block in registers), the
+// partial blocks combined by xor-butterflies and wave order (fixed).
+__global__ __launch_bounds__(256) void preduce_seg_kernel(DevProblem P) {
+    const int sg = blockIdx.x;
+    const int j = P.plseg[2 * sg], k0 = P.plseg[2 * sg + 1];
+    const ReduceTarget T = P.targets[P.plong_targets[j]];
+    const int E = T.rows * T.cols;
+    const bool vec = T.cols == 1;
+    double s[36];
+#pragma unroll
+    for (int e = 0; e < 36; ++e) s[e] = 0.0;
+    const int k = k0 + (int)threadIdx.x;
+    if (k < T.p_end && k - k0 < kReduceSeg) {
+        const PTerm pt = P.pterms[k];
+        double a[18], b[18];
+#pragma unroll
+        for (int e = 0; e < 18; ++e) {
+            a[e] = e < 3 * T.rows ? P.Z[pt.za + e] : 0.0;
+            b[e] = e < (vec ? 3 : 3 * T.cols) ? P.Z[pt.zb + e] : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 36; ++e) {
+            if (e < E) {
+                const int r = e / T.cols, cc = vec ? 0 : e % T.cols;
+                s[e] = a[3 * r] * b[3 * cc] + a[3 * r + 1] * b[3 * cc + 1] + a[3 * r + 2] * b[3 * cc + 2];
+            }
+        }
+    }
+    wave_sum(s);
+    __shared__ double part[4][36];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+#pragma unroll
+        for (int e = 0; e < 36; ++e) part[wave][e] = s[e];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < E) {
+        const int e = threadIdx.x;
+        P.plpart[(size_t)sg * 36 + e] = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
+    }
+}
+
+// pass 2: segment partials added in segment order, subtracted from the target
+__global__ __launch_bounds__(64) void preduce_long_kernel(DevProblem P) {
+    const int j = blockIdx.x;
+    const ReduceTarget T = P.targets[P.plong_targets[j]];
+    const int E = T.rows * T.cols, e = threadIdx.x;
+    if (e >= E) return;
+    double t = 0.0;
+#pragma unroll 8
+    for (int sg = P.plseg_off[j]; sg < P.plseg_off[j + 1]; ++sg) t += P.plpart[(size_t)sg * 36 + e];
+    const int r = e / T.cols, cc = e % T.cols;
+    target_base(P, T.dst_kind)[T.dst + (T.cols == 1 ? r : (int64_t)r * T.ld + cc)] -= t;
 }
 
 // Step for general points: one thread per point, the same arithmetic as
@@ -1954,10 +2014,17 @@ void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     if (P.n_gpt > 0 && !vectors_only) {
         hipLaunchKernelGGL(preduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P);
         SFM_HIP(hipGetLastError());
+        if (P.n_plong > 0) {
+            hipLaunchKernelGGL(preduce_seg_kernel, dim3(P.n_plseg), dim3(256), 0, s, P);
+            SFM_HIP(hipGetLastError());
+            hipLaunchKernelGGL(preduce_long_kernel, dim3(P.n_plong), dim3(64), 0, s, P);
+            SFM_HIP(hipGetLastError());
+        }
     }
 }
 
 int reduce_long_threshold() { return kLongTerms; }
+int preduce_long_threshold() { return kLongPTerms; }
 
 size_t solve_window_doubles(const DevProblem& P) {
     const size_t Dp = P.D + 1;

@@ -57,28 +57,49 @@ int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_
 // Long tracks contribute a chain of nearest neighbours only.  Returns the new
 // block of every natural block.
 std::vector<int32_t> rcm_order(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int32_t ncam) {
-    std::vector<uint64_t> edges;
-    std::vector<int32_t> cs;
-    for (int64_t p = 0; p < P.n_pt; ++p) {
-        cs.clear();
-        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o)
-            if (cam_blk[P.obs_img[o]] >= 0) cs.push_back(cam_blk[P.obs_img[o]]);
-        std::sort(cs.begin(), cs.end());
-        cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
-        const size_t n = cs.size(), reach = n <= 24 ? n : 4;
-        for (size_t a = 0; a < n; ++a)
-            for (size_t b = a + 1; b < std::min(n, a + 1 + reach); ++b) {
-                edges.push_back(((uint64_t)cs[a] << 32) | (uint32_t)cs[b]);
-                edges.push_back(((uint64_t)cs[b] << 32) | (uint32_t)cs[a]);
-            }
-    }
-    std::sort(edges.begin(), edges.end());
-    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+    // adjacency rows in ascending neighbour order: a bit matrix while it is
+    // small (ncam <= 8192: <= 8 MB), else a sorted, de-duplicated edge list
     std::vector<int64_t> ptr(ncam + 1, 0);
-    for (uint64_t e : edges) ptr[(e >> 32) + 1]++;
-    for (int32_t c = 0; c < ncam; ++c) ptr[c + 1] += ptr[c];
-    std::vector<int32_t> adj(edges.size());
-    for (size_t k = 0; k < edges.size(); ++k) adj[k] = (int32_t)(edges[k] & 0xffffffffu);
+    std::vector<int32_t> adj;
+    auto each_pair = [&](auto&& emit) {
+        std::vector<int32_t> cs;
+        for (int64_t p = 0; p < P.n_pt; ++p) {
+            cs.clear();
+            for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o)
+                if (cam_blk[P.obs_img[o]] >= 0) cs.push_back(cam_blk[P.obs_img[o]]);
+            std::sort(cs.begin(), cs.end());
+            cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+            const size_t n = cs.size(), reach = n <= 24 ? n : 4;
+            for (size_t a = 0; a < n; ++a)
+                for (size_t b = a + 1; b < std::min(n, a + 1 + reach); ++b) emit(cs[a], cs[b]);
+        }
+    };
+    if (ncam <= 8192) {
+        const int64_t words = (ncam + 63) / 64;
+        std::vector<uint64_t> bits((size_t)(ncam * words), 0);
+        each_pair([&](int32_t a, int32_t b) {
+            bits[(size_t)(a * words + (b >> 6))] |= 1ull << (b & 63);
+            bits[(size_t)(b * words + (a >> 6))] |= 1ull << (a & 63);
+        });
+        for (int32_t c = 0; c < ncam; ++c) {
+            for (int64_t w = 0; w < words; ++w)
+                for (uint64_t m = bits[(size_t)(c * words + w)]; m; m &= m - 1)
+                    adj.push_back((int32_t)(64 * w + __builtin_ctzll(m)));
+            ptr[c + 1] = (int64_t)adj.size();
+        }
+    } else {
+        std::vector<uint64_t> edges;
+        each_pair([&](int32_t a, int32_t b) {
+            edges.push_back(((uint64_t)a << 32) | (uint32_t)b);
+            edges.push_back(((uint64_t)b << 32) | (uint32_t)a);
+        });
+        std::sort(edges.begin(), edges.end());
+        edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+        for (uint64_t e : edges) ptr[(e >> 32) + 1]++;
+        for (int32_t c = 0; c < ncam; ++c) ptr[c + 1] += ptr[c];
+        adj.resize(edges.size());
+        for (size_t k = 0; k < edges.size(); ++k) adj[k] = (int32_t)(edges[k] & 0xffffffffu);
+    }
     auto deg = [&](int32_t c) { return ptr[c + 1] - ptr[c]; };
     std::vector<int32_t> seq;
     std::vector<char> seen(ncam, 0);
@@ -117,22 +138,27 @@ std::vector<int32_t> rcm_order(const sfm_ba_problem& P, const std::vector<int32_
 }  // namespace
 
 std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, int32_t* D_out) {
+    PhaseTimer tm("camera_blocks");
     std::vector<int32_t> cam_blk(P.n_img, -1);
     std::vector<char> used(P.n_img, 0);
     for (int64_t o = 0; o < P.n_obs; ++o) used[P.obs_img[o]] = 1;
     int32_t ncam = 0;
     for (int i = 0; i < P.n_img; ++i)
         if (used[i] && i != P.const_img) cam_blk[i] = ncam++;
+    tm.mark("used");
     int32_t D = half_bandwidth(P, cam_blk);
     // reorder only when the image order does not give a band the BCR solver
     // takes, and the co-visibility graph is small enough to build quickly
+    tm.mark("bandwidth");
     if (D > kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20 && !std::getenv("SFM_BA_NO_RCM")) {
         const std::vector<int32_t> pos = rcm_order(P, cam_blk, ncam);
+        tm.mark("rcm");
         std::vector<int32_t> alt(cam_blk);
         for (auto& b : alt)
             if (b >= 0) b = pos[b];
         const int32_t D2 = half_bandwidth(P, alt);
         if (D2 < D) { cam_blk.swap(alt); D = D2; }
+        tm.mark("bandwidth2");
     }
     if (ncam_out) *ncam_out = ncam;
     if (D_out) *D_out = D;
@@ -244,9 +270,12 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     SFM_REQUIRE(P.camera_model == SFM_CAM_PINHOLE || P.camera_model == SFM_CAM_SNAVELY, SFM_ERR_INVALID_ARG,
                 "unknown camera_model %d", P.camera_model);
 
+    PhaseTimer tm("build_plan");
+    tm.mark("validate");
     pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
     pl.rank = rank; pl.world = world;
     active_sets(P, pl);
+    tm.mark("active");
     // RCS storage and solver, identical on every rank: the block-banded form
     // (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
     // and a few intrinsics blocks, else dense (blocked Cholesky, ba_dense.hip)
@@ -258,6 +287,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     }
 
     partition_points(P, pl.cam_blk, world, pl.order, pl.bounds);
+    tm.mark("partition");
 
     // ---- shard arrays: chunkable points first, then general points ---------
     const int64_t b0 = pl.bounds[rank], b1 = pl.bounds[rank + 1];
@@ -291,6 +321,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
     });
 
+    tm.mark("shard");
     // ---- Schur chunks over [0, n_cpt) ------------------------------------------
     // Greedy over shard points: a chunk's F blocks (camera 6 rows, intrinsics 4
     // rows) must fit `cap` rows of its tile: 64 (4x4 MFMA tiles, -Zw on the
@@ -467,6 +498,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         pl.n_cpt = 0;
         flops = 0;
     }
+    tm.mark("chunks");
     std::copy(cslot.begin(), cslot.end(), pl.obs_slot.begin());
     pl.n_gpt = pl.n_spt - pl.n_cpt;
     // a general point's observations in image order, so that repeated views
@@ -536,6 +568,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
         pl.n_z = pl.gz_off[pl.n_gpt];
     }
+    tm.mark("general");
     pl.schur_flops = flops;
     pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +
                      (int64_t)pl.chunks.size() * kTileR * kTileR * 8;
@@ -584,6 +617,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         });
     }
 
+    tm.mark("image_csr");
     // ---- reduce plan -----------------------------------------------------------
     // Every matrix block (a, b), a >= b in F-block order (cameras, then
     // intrinsics), collects sum terms (image Gram slices first, then chunk tile
@@ -652,12 +686,14 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
     }
     auto by_key = [](const auto& x, const auto& y) { return x.first < y.first; };
+    tm.mark("terms");
     std::stable_sort(mterms.begin(), mterms.end(), by_key);
     std::stable_sort(vterms.begin(), vterms.end(), by_key);
     std::stable_sort(cterms.begin(), cterms.end(), by_key);
     std::stable_sort(mprod.begin(), mprod.end(), by_key);
     std::stable_sort(vprod.begin(), vprod.end(), by_key);
 
+    tm.mark("term_sort");
     const int Dp = pl.D + 1;
     if (!pl.dense) {
         pl.n_sband = (int64_t)pl.ncam * Dp * 36;
@@ -745,6 +781,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstBF, col_of_fb(fb), size_of_fb(fb), 1, 1, bterms, ib, nullptr, nullptr);
     }
     for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstCnF, col_of_fb(fb), size_of_fb(fb), 1, 1, cterms, ic, nullptr, nullptr);
+    tm.mark("targets");
 }
 
 }  // namespace sfm

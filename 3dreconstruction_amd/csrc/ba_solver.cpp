@@ -53,6 +53,8 @@ struct sfm_ba_plan {
     DBuf<double> Zbuf, dense_buf;
     DenseArgs dense;
     DBuf<double> lpart;           // long-target segment partials [n_lseg][36]
+    DBuf<int32_t> plong_targets;  // long product-term targets, offsets, segments
+    DBuf<double> plpart;          // their segment partials [n_plseg][36]
     DBuf<int32_t> img_pt;         // image-ordered observations (image Gram pass)
     DBuf<double> img_uv;
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
@@ -72,7 +74,7 @@ struct sfm_ba_plan {
     std::vector<hipEvent_t> ev;
     bool cur_is_a = true;
     ~sfm_ba_plan() {
-        if (scal_h) (void)hipHostFree(scal_h);
+        if (scal_h) pinned_free(scal_h);
         for (auto e : ev) (void)hipEventDestroy(e);
     }
 };
@@ -90,7 +92,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     sfm_ctx* ctx = pl->ctx;
     hipStream_t s = ctx->stream;
     BAHostPlan& h = pl->hp;
+    PhaseTimer tm("create_plan");
     build_plan(prob, ctx->rank, ctx->world, h);
+    tm.mark("build_plan");
     up(pl->pt_off, h.pt_off, s);
     up(pl->obs_img, h.obs_img, s);
     up(pl->obs_pt, h.obs_pt, s);
@@ -191,8 +195,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->scal_g.alloc((size_t)ctx->world * kScMaxEnd);
         pl->scal_gh.assign(pl->scal_g.n, 0.0);
     }
-    SFM_HIP(hipHostMalloc((void**)&pl->scal_h, (kScCount + 1) * sizeof(double),
-                          hipHostMallocMapped | hipHostMallocCoherent));
+    pl->scal_h = static_cast<double*>(pinned_alloc((kScCount + 1) * sizeof(double)));
     std::memset(pl->scal_h, 0, (kScCount + 1) * sizeof(double));
     SFM_HIP(hipHostGetDevicePointer((void**)&pl->scal_dev, pl->scal_h, 0));
 
@@ -242,6 +245,31 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->lpart.alloc(36 * std::max<size_t>(P.n_lseg, 1));
         P.lpart = pl->lpart.p;
     }
+    {
+        // the same for long product-term lists (general points)
+        std::vector<int32_t> lt, off{0}, seg;
+        for (size_t t = 0; t < h.targets.size(); ++t) {
+            const int32_t b0 = h.targets[t].p_begin, n = h.targets[t].p_end - b0;
+            if (n <= preduce_long_threshold()) continue;
+            for (int32_t k = 0; k < n; k += kReduceSeg) {
+                seg.push_back((int32_t)lt.size());
+                seg.push_back(b0 + k);
+            }
+            lt.push_back((int32_t)t);
+            off.push_back((int32_t)(seg.size() / 2));
+        }
+        P.n_plong = (int32_t)lt.size();
+        P.n_plseg = (int32_t)(seg.size() / 2);
+        std::vector<int32_t> all(lt);
+        all.insert(all.end(), off.begin(), off.end());
+        all.insert(all.end(), seg.begin(), seg.end());
+        up(pl->plong_targets, all, s);
+        P.plong_targets = pl->plong_targets.p;
+        P.plseg_off = P.plong_targets + P.n_plong;
+        P.plseg = P.plseg_off + P.n_plong + 1;
+        pl->plpart.alloc(36 * std::max<size_t>(P.n_plseg, 1));
+        P.plpart = pl->plpart.p;
+    }
     P.scaleE = pl->scaleE.p; P.scaleF = pl->scaleF.p; P.tiles = pl->gram.p;
     P.U = P.tiles + o_u; P.Ub = P.tiles + o_ub; P.Ucn = P.tiles + o_ucn;
     P.src = pl->gram.p;
@@ -283,9 +311,11 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         }
     }
     if (std::getenv("SFM_SCHUR_STAMPS")) pl->stamps.alloc(6 * std::max<size_t>(h.chunks.size(), 1));
-    pl->ev.resize(16);
+    pl->ev.resize(2);   // the Schur launch timing of steps 1 and 2
     for (auto& e2 : pl->ev) SFM_HIP(hipEventCreate(&e2));
+    tm.mark("alloc+upload");
     SFM_HIP(hipStreamSynchronize(s));
+    tm.mark("sync");
 }
 
 // Wait for finalize_kernel's publish of the iteration scalars (sequence word
@@ -581,7 +611,7 @@ extern "C" int sfm_ba_plan_create(sfm_ctx* ctx, const sfm_ba_problem* prob, cons
     return guarded([&] {
         SFM_REQUIRE(ctx && prob && extr && intr && (X || prob->n_pt == 0) && out, SFM_ERR_INVALID_ARG,
                     "null argument");
-        SFM_HIP(hipSetDevice(ctx->device));
+        CtxScope scope_(ctx);
         auto* pl = new sfm_ba_plan;
         pl->ctx = ctx;
         try {
@@ -598,7 +628,7 @@ extern "C" int sfm_ba_plan_create(sfm_ctx* ctx, const sfm_ba_problem* prob, cons
 extern "C" int sfm_ba_plan_run(sfm_ba_plan* pl, const sfm_ba_options* opts, sfm_ba_summary* sum) {
     return guarded([&] {
         SFM_REQUIRE(pl && sum, SFM_ERR_INVALID_ARG, "null argument");
-        SFM_HIP(hipSetDevice(pl->ctx->device));
+        CtxScope scope_(pl->ctx);
         sfm_ba_options O;
         if (opts) O = *opts; else sfm_ba_default_options(&O);
         return run_plan(pl, O, sum);
@@ -608,7 +638,7 @@ extern "C" int sfm_ba_plan_run(sfm_ba_plan* pl, const sfm_ba_options* opts, sfm_
 extern "C" int sfm_ba_plan_download(sfm_ba_plan* pl, double* extr, double* intr, double* X) {
     return guarded([&] {
         SFM_REQUIRE(pl, SFM_ERR_INVALID_ARG, "null plan");
-        SFM_HIP(hipSetDevice(pl->ctx->device));
+        CtxScope scope_(pl->ctx);
         download(pl, extr, intr, X);
         return SFM_OK;
     });
@@ -617,7 +647,7 @@ extern "C" int sfm_ba_plan_download(sfm_ba_plan* pl, double* extr, double* intr,
 extern "C" int sfm_ba_plan_destroy(sfm_ba_plan* pl) {
     return guarded([&] {
         if (!pl) return SFM_OK;
-        (void)hipSetDevice(pl->ctx->device);
+        CtxScope scope_(pl->ctx);
         (void)hipStreamSynchronize(pl->ctx->stream);
         delete pl;
         return SFM_OK;
@@ -658,13 +688,18 @@ extern "C" int sfm_ba_plan_get_trace(sfm_ba_plan* pl, sfm_ba_iter* out, int32_t 
 extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* extr, double* intr,
                             double* X, const sfm_ba_options* opts, sfm_ba_summary* sum) {
     sfm_ba_plan* pl = nullptr;
+    sfm::PhaseTimer tm("sfm_ba_solve");
     int rc = sfm_ba_plan_create(ctx, prob, extr, intr, X, &pl);
+    tm.mark("create");
     if (rc != SFM_OK) return rc;
     rc = sfm_ba_plan_run(pl, opts, sum);
+    tm.mark("run");
     if (sum && sum->usable) {  // BundleAdjuster::updateWorld only on success (:179-184)
         const int rc2 = sfm_ba_plan_download(pl, extr, intr, X);
         if (rc == SFM_OK) rc = rc2;
     }
+    tm.mark("download");
     sfm_ba_plan_destroy(pl);
+    tm.mark("destroy");
     return rc;
 }

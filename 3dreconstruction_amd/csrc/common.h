@@ -7,8 +7,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <ctime>
 
 #include "../../include/sfmcore.h"
+
+struct sfm_ctx;
 
 namespace sfm {
 
@@ -66,6 +69,27 @@ void ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStrea
 int rccl_comm_init(void** comm, int world, const uint8_t* id128, int rank);
 void rccl_comm_destroy(void* comm);
 
+// Device memory cache (ctx.cpp).  A block freed while a context is bound to
+// the calling thread (CtxScope) is kept for later allocations under the same
+// context stream instead of going back through hipFree, which synchronises
+// the whole device and dominated small solves (a fresh plan per
+// BundleAdjuster call).  Reuse is stream-ordered, so no extra synchronisation
+// is needed; without a bound context blocks go straight to hipMalloc/hipFree.
+void* dev_alloc(size_t bytes);   // throws SFM_ERR_OOM
+void dev_free(void* p);
+void dev_cache_release(hipStream_t s);   // hipFree every cached block of s
+// Page-locked, device-mapped host memory, cached the same way.
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p);
+
+// Binds a context to the calling thread for the duration of an API call:
+// its device, and its stream as the key of the device memory cache.
+struct CtxScope {
+    hipStream_t prev;
+    explicit CtxScope(const sfm_ctx* c);
+    ~CtxScope();
+};
+
 // Device buffer RAII.
 template <class T>
 struct DBuf {
@@ -76,24 +100,20 @@ struct DBuf {
     DBuf& operator=(const DBuf&) = delete;
     ~DBuf() { reset(); }
     void reset() {
-        if (p) (void)hipFree(p);
+        if (p) dev_free(p);
         p = nullptr;
         n = 0;
     }
     void alloc(size_t count) {
         reset();
         if (count == 0) return;
-        hipError_t e = hipMalloc(&p, count * sizeof(T));
-        if (e != hipSuccess) {
-            p = nullptr;
-            set_error("hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
-            throw SfmError{SFM_ERR_OOM};
-        }
+        p = static_cast<T*>(dev_alloc(count * sizeof(T)));
         n = count;
         // SFM_POISON_ALLOC=1 (tests): every fresh buffer starts as 0xFF bytes
         // (NaN doubles, -1 integers), so a read before the first write shows
         // (completed before any stream can use the buffer)
         if (poison_alloc()) {
+            SFM_HIP(hipDeviceSynchronize());   // a cached block's last user may still run
             SFM_HIP(hipMemset(p, 0xFF, count * sizeof(T)));
             SFM_HIP(hipDeviceSynchronize());
         }
@@ -107,6 +127,35 @@ struct DBuf {
     }
     void zero(hipStream_t s) {
         if (n) SFM_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
+    }
+};
+
+// SFM_TIMING=1 (diagnostic): host wall time per phase of a call, printed to
+// stderr as "[timing] <what>: a 1.2 ms, b 3.4 ms".
+struct PhaseTimer {
+    static bool on() {
+        static const bool v = std::getenv("SFM_TIMING") != nullptr;
+        return v;
+    }
+    const char* what;
+    double t_last;
+    std::string line;
+    explicit PhaseTimer(const char* w) : what(w), t_last(now()) {}
+    static double now() {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+    }
+    void mark(const char* phase) {
+        if (!on()) return;
+        const double t = now();
+        char b[96];
+        std::snprintf(b, sizeof b, "%s%s %.2f ms", line.empty() ? "" : ", ", phase, t - t_last);
+        line += b;
+        t_last = t;
+    }
+    ~PhaseTimer() {
+        if (on() && !line.empty()) std::fprintf(stderr, "[timing] %s: %s\n", what, line.c_str());
     }
 };
 

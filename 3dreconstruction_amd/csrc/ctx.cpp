@@ -4,7 +4,12 @@
 
 #include <cstdarg>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <tuple>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
 
 #include "common.h"
 
@@ -83,6 +88,132 @@ int rccl_allgather_f64(void* comm, const double* in, double* out, size_t n, hipS
     return SFM_OK;
 }
 
+// ---- device memory cache ----------------------------------------------------
+namespace {
+
+thread_local hipStream_t tl_stream = nullptr;   // key of the bound context
+
+// Size classes: 256 B granules up to 64 KB, above that eight classes per
+// power of two (<= 12.5 % slack), so regrown buffers of a growing problem
+// (the incremental loop) still find their class.
+size_t size_class(size_t b) {
+    if (b <= 65536) return (b + 255) & ~size_t(255);
+    int e = 63 - __builtin_clzll(b - 1);          // 2^e < b <= 2^(e+1)
+    const size_t step = size_t(1) << (e - 2);     // 2^(e+1) / 8
+    return (b + step - 1) / step * step;
+}
+
+struct Block {
+    hipStream_t key;
+    size_t bytes;
+    bool pinned;
+};
+
+struct MemCache {
+    std::mutex mu;
+    std::unordered_map<void*, Block> live;
+    // (key, pinned, class) -> free blocks
+    std::map<std::tuple<hipStream_t, bool, size_t>, std::vector<void*>> free;
+    std::unordered_set<hipStream_t> streams;   // contexts alive (their keys)
+    size_t cached = 0;
+    static constexpr size_t kCap = size_t(32) << 30;   // cached bytes kept at most
+};
+
+MemCache& cache() {
+    static MemCache* c = new MemCache;   // never destroyed: frees may run at exit
+    return *c;
+}
+
+void raw_free(void* p, bool pinned) {
+    if (pinned) (void)hipHostFree(p);
+    else (void)hipFree(p);
+}
+
+void release_all_locked(MemCache& c, hipStream_t only, bool all) {
+    for (auto it = c.free.begin(); it != c.free.end();) {
+        if (all || std::get<0>(it->first) == only) {
+            for (void* p : it->second) {
+                raw_free(p, std::get<1>(it->first));
+                c.cached -= std::get<2>(it->first);
+            }
+            it = c.free.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+void* cached_alloc(size_t bytes, bool pinned) {
+    MemCache& c = cache();
+    const hipStream_t key = tl_stream;
+    const size_t cls = size_class(bytes);
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (key && c.streams.count(key)) {
+        auto it = c.free.find({key, pinned, cls});
+        if (it != c.free.end() && !it->second.empty()) {
+            void* p = it->second.back();
+            it->second.pop_back();
+            c.cached -= cls;
+            c.live[p] = Block{key, cls, pinned};
+            return p;
+        }
+    }
+    void* p = nullptr;
+    auto get = [&] {
+        return pinned ? hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent) : hipMalloc(&p, cls);
+    };
+    hipError_t e = get();
+    if (e != hipSuccess && c.cached) {   // give the cache back and retry once
+        (void)hipGetLastError();
+        release_all_locked(c, nullptr, true);
+        e = get();
+    }
+    if (e != hipSuccess) {
+        set_error("%s(%zu bytes) failed: %s", pinned ? "hipHostMalloc" : "hipMalloc", cls, hipGetErrorString(e));
+        throw SfmError{SFM_ERR_OOM};
+    }
+    c.live[p] = Block{key, cls, pinned};
+    return p;
+}
+
+void cached_free(void* p) {
+    if (!p) return;
+    MemCache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return;
+    const Block b = it->second;
+    c.live.erase(it);
+    // reuse only under the stream the block was last used on
+    const hipStream_t key = tl_stream ? tl_stream : b.key;
+    if (key && c.streams.count(key) && c.cached + b.bytes <= MemCache::kCap) {
+        c.free[{key, b.pinned, b.bytes}].push_back(p);
+        c.cached += b.bytes;
+        return;
+    }
+    raw_free(p, b.pinned);
+}
+
+}  // namespace
+
+void* dev_alloc(size_t bytes) { return cached_alloc(bytes, false); }
+void dev_free(void* p) { cached_free(p); }
+void* pinned_alloc(size_t bytes) { return cached_alloc(bytes, true); }
+void pinned_free(void* p) { cached_free(p); }
+
+void dev_cache_release(hipStream_t s) {
+    MemCache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    release_all_locked(c, s, false);
+    c.streams.erase(s);
+}
+
+CtxScope::CtxScope(const sfm_ctx* ctx) : prev(tl_stream) {
+    SFM_HIP(hipSetDevice(ctx->device));
+    tl_stream = ctx->stream;
+}
+CtxScope::~CtxScope() { tl_stream = prev; }
+
 }  // namespace sfm
 
 using namespace sfm;
@@ -148,6 +279,11 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         c->cu_count = prop.multiProcessorCount;
         SFM_HIP(hipSetDevice(c->device));
         SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        {
+            MemCache& mc = cache();
+            std::lock_guard<std::mutex> lk(mc.mu);
+            mc.streams.insert(c->stream);
+        }
         if (c->world > 1 && opts->allreduce && !opts->comm_id) {
             c->host_allreduce = opts->allreduce;
             c->host_allreduce_user = opts->allreduce_user;
@@ -173,7 +309,10 @@ extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         rccl_comm_destroy(ctx->comm);
         if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
-        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        if (ctx->stream) {
+            dev_cache_release(ctx->stream);
+            (void)hipStreamDestroy(ctx->stream);
+        }
         delete ctx;
         return SFM_OK;
     });
@@ -182,7 +321,7 @@ extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
 extern "C" int sfm_ctx_synchronize(sfm_ctx* ctx) {
     return guarded([&] {
         SFM_REQUIRE(ctx, SFM_ERR_INVALID_ARG, "null ctx");
-        SFM_HIP(hipSetDevice(ctx->device));
+        CtxScope scope(ctx);
         SFM_HIP(hipStreamSynchronize(ctx->stream));
         return SFM_OK;
     });

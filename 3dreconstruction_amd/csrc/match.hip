@@ -505,7 +505,8 @@ void run_cascade(sfm_match_plan* p, int64_t n_pairs, float r2) {
     }
 }
 
-void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const sfm_match_options* o) {
+void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const sfm_match_options* o,
+               bool timed = true) {
     hipStream_t s = p->ctx->stream;
     SFM_REQUIRE(o && (o->mode == SFM_MATCH_RATIO || o->mode == SFM_MATCH_MUTUAL ||
                       o->mode == SFM_MATCH_CASCADE),
@@ -524,8 +525,8 @@ void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const s
     const size_t need = (size_t)std::max<int64_t>(1, n_pairs * p->stride);
     if (p->out_idx.n < need) { p->out_idx.alloc(need); p->out_d.alloc(need); }
     p->launches = 0;
-    if (!p->ev0) { SFM_HIP(hipEventCreate(&p->ev0)); SFM_HIP(hipEventCreate(&p->ev1)); }
-    SFM_HIP(hipEventRecord(p->ev0, s));
+    if (timed && !p->ev0) { SFM_HIP(hipEventCreate(&p->ev0)); SFM_HIP(hipEventCreate(&p->ev1)); }
+    if (timed) SFM_HIP(hipEventRecord(p->ev0, s));
     if (n_pairs > 0) {
         if (o->mode == SFM_MATCH_CASCADE) {
             run_cascade(p, n_pairs, o->ratio * o->ratio);
@@ -549,7 +550,7 @@ void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const s
             }
         }
     }
-    SFM_HIP(hipEventRecord(p->ev1, s));
+    if (timed) SFM_HIP(hipEventRecord(p->ev1, s));
 }
 
 }  // namespace
@@ -559,7 +560,7 @@ extern "C" int sfm_match_plan_create(sfm_ctx* ctx, const uint8_t* desc, const in
     return guarded([&] {
         SFM_REQUIRE(ctx && out && offsets && n_img >= 0, SFM_ERR_INVALID_ARG, "null argument");
         SFM_REQUIRE(desc || offsets[n_img] == 0, SFM_ERR_INVALID_ARG, "null descriptors");
-        SFM_HIP(hipSetDevice(ctx->device));
+        CtxScope scope_(ctx);
         auto* p = new sfm_match_plan;
         p->ctx = ctx;
         try {
@@ -578,7 +579,7 @@ extern "C" int sfm_match_plan_run(sfm_match_plan* p, const int32_t* pairs, int64
     return guarded([&] {
         SFM_REQUIRE(p && (pairs || n_pairs == 0) && n_pairs >= 0, SFM_ERR_INVALID_ARG,
                     "bad arguments");
-        SFM_HIP(hipSetDevice(p->ctx->device));
+        CtxScope scope_(p->ctx);
         run_pairs(p, pairs, n_pairs, o);
         if (total) {
             uint64_t dg;
@@ -609,7 +610,7 @@ extern "C" int sfm_match_plan_cascade_index(sfm_match_plan* p, const int32_t* pa
         for (int64_t q = 0; q < 2 * n_pairs; ++q)
             SFM_REQUIRE(pairs[q] >= 0 && pairs[q] < p->n_img, SFM_ERR_INVALID_ARG,
                         "pair %lld out of range", (long long)(q / 2));
-        SFM_HIP(hipSetDevice(p->ctx->device));
+        CtxScope scope_(p->ctx);
         casc_prepare(p, pairs, n_pairs, true);
         return SFM_OK;
     });
@@ -618,7 +619,7 @@ extern "C" int sfm_match_plan_cascade_index(sfm_match_plan* p, const int32_t* pa
 extern "C" int sfm_match_plan_digest(sfm_match_plan* p, uint64_t* digest) {
     return guarded([&] {
         SFM_REQUIRE(p && digest, SFM_ERR_INVALID_ARG, "null argument");
-        SFM_HIP(hipSetDevice(p->ctx->device));
+        CtxScope scope_(p->ctx);
         if (!p->digest.p) p->digest.alloc(2);
         p->digest.zero(p->ctx->stream);
         for (int64_t b0 = 0; b0 < p->n_pairs; b0 += 65535) {
@@ -641,7 +642,7 @@ extern "C" int sfm_match_plan_fetch(sfm_match_plan* p, int64_t* counts, uint32_t
                                     int32_t* d2) {
     return guarded([&] {
         SFM_REQUIRE(p && counts, SFM_ERR_INVALID_ARG, "null argument");
-        SFM_HIP(hipSetDevice(p->ctx->device));
+        CtxScope scope_(p->ctx);
         const size_t n = (size_t)(p->n_pairs * p->stride);
         std::vector<int32_t> hi(n), hd(n);
         if (n) {
@@ -695,7 +696,7 @@ extern "C" int sfm_match_plan_get_last_ms(sfm_match_plan* p, double* ms, int64_t
 extern "C" int sfm_match_plan_destroy(sfm_match_plan* p) {
     return guarded([&] {
         if (!p) return SFM_OK;
-        (void)hipSetDevice(p->ctx->device);
+        CtxScope scope_(p->ctx);
         (void)hipStreamSynchronize(p->ctx->stream);
         if (p->ev0) { (void)hipEventDestroy(p->ev0); (void)hipEventDestroy(p->ev1); }
         delete p;
@@ -710,23 +711,27 @@ extern "C" int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a, cons
         SFM_REQUIRE(ctx && o && match_idx && match_d2 && n_a >= 0 && n_b >= 0 &&
                         (a || n_a == 0) && (b || n_b == 0),
                     SFM_ERR_INVALID_ARG, "bad arguments");
-        SFM_HIP(hipSetDevice(ctx->device));
+        CtxScope scope_(ctx);
+        PhaseTimer tm("sfm_match_dense");
         std::vector<uint8_t> desc((size_t)(n_a + n_b) * 128);
         if (n_a) std::memcpy(desc.data(), a, (size_t)n_a * 128);
         if (n_b) std::memcpy(desc.data() + (size_t)n_a * 128, b, (size_t)n_b * 128);
         const int64_t off[3] = {0, n_a, (int64_t)n_a + n_b};
         sfm_match_plan plan;
         plan.ctx = ctx;
+        tm.mark("stage");
         upload_collection(&plan, desc.data(), off, 2);
+        tm.mark("upload");
         const int32_t pair[2] = {0, 1};
-        run_pairs(&plan, pair, 1, o);
+        run_pairs(&plan, pair, 1, o, false);
+        tm.mark("launch");
         const int32_t n_out = o->mode != SFM_MATCH_MUTUAL ? n_b : n_a;
         if (n_out) {
             SFM_HIP(hipMemcpyAsync(match_idx, plan.out_idx.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
             SFM_HIP(hipMemcpyAsync(match_d2, plan.out_d.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
         }
         SFM_HIP(hipStreamSynchronize(ctx->stream));
-        if (plan.ev0) { (void)hipEventDestroy(plan.ev0); (void)hipEventDestroy(plan.ev1); plan.ev0 = nullptr; }
+        tm.mark("sync+download");
         return SFM_OK;
     });
 }
