@@ -164,6 +164,20 @@ class SynthOrbitConfig(C.Structure):
                 ("prior_rot", C.c_double), ("prior_t", C.c_double), ("seed", C.c_uint64)]
 
 
+class FMatrixOpts(C.Structure):
+    _fields_ = [("precision", C.c_double), ("max_iterations", C.c_int32), ("reserved", C.c_int32)]
+
+
+class FMatrixResult(C.Structure):
+    _fields_ = [("F", C.c_double * 9), ("error_max", C.c_double), ("min_nfa", C.c_double),
+                ("n_inliers", C.c_int32), ("iterations", C.c_int32)]
+
+
+class SparseFilterStats(C.Structure):
+    _fields_ = [("n_pairs_in", C.c_int64), ("n_pairs_out", C.c_int64), ("n_matches_in", C.c_int64),
+                ("n_matches_out", C.c_int64)]
+
+
 def default_options():
     o = BAOptions()
     o.max_num_iterations = 50
@@ -242,6 +256,10 @@ SIGNATURES = [
     ("sfm_sparse_match_pair", C.c_int, [C.c_char_p]),
     ("sfm_sparse_match", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(SparseMatchOpts),
                                    C.POINTER(SparseMatchStats)]),
+    ("sfm_fmatrix_ac", C.c_int, [C.c_void_p, C.c_int64, i64p, f64p, i32p, C.POINTER(FMatrixOpts),
+                                 C.POINTER(FMatrixResult), i32p]),
+    ("sfm_sparse_filter", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(FMatrixOpts),
+                                    C.POINTER(SparseFilterStats)]),
 ]
 
 _lib = None

@@ -552,3 +552,53 @@ def sparse_match(ctx, matches_dir, mode=abi.SFM_MATCH_CASCADE, ratio=0.8, force=
            "sfm_sparse_match")
     return {"n_views": st.n_views, "n_pairs_in": st.n_pairs_in, "n_pairs_out": st.n_pairs_out,
             "n_matches": st.n_matches, "reloaded": bool(st.reloaded)}
+
+
+# ---- geometric filter (GeometricFilter_FMatrix_AC) ----------
+def fmatrix_opts(precision=4.0, max_iterations=2048):
+    o = abi.FMatrixOpts()
+    o.precision, o.max_iterations = precision, max_iterations
+    return o
+
+
+def _fmatrix_inputs(xy_list, wh):
+    counts = np.array([len(x) for x in xy_list], np.int64)
+    off = np.zeros(len(xy_list) + 1, np.int64)
+    off[1:] = np.cumsum(counts)
+    xy = np.ascontiguousarray(np.concatenate([np.asarray(x, np.float64).reshape(-1, 4) for x in xy_list])
+                              if len(xy_list) and off[-1] else np.zeros((1, 4)), np.float64)
+    wh = np.ascontiguousarray(np.asarray(wh, np.int32).reshape(-1, 4))
+    return off, xy, wh
+
+
+def _fmatrix_outputs(off, res, inl):
+    out = []
+    for q in range(len(off) - 1):
+        r = res[q]
+        out.append({"F": np.array(r.F[:]).reshape(3, 3), "error_max": r.error_max, "min_nfa": r.min_nfa,
+                    "n_inliers": r.n_inliers, "iterations": r.iterations,
+                    "inliers": inl[off[q]:off[q] + r.n_inliers].copy()})
+    return out
+
+
+def fmatrix_ac(ctx, xy_list, wh, opts=None):
+    """sfm_fmatrix_ac over a list of pairs: xy_list[q] is an (n_q, 4) array of
+    (x_I, y_I, x_J, y_J) pixels, wh[q] = (w_I, h_I, w_J, h_J).  Returns one
+    dict per pair (F, error_max, min_nfa, n_inliers, iterations, inliers)."""
+    lib = abi.load()
+    off, xy, wh = _fmatrix_inputs(xy_list, wh)
+    n_pairs = len(off) - 1
+    res = (abi.FMatrixResult * max(n_pairs, 1))()
+    inl = np.full(max(int(off[-1]), 1), -1, np.int32)
+    _check(lib.sfm_fmatrix_ac(ctx.h, n_pairs, abi.ptr(off, abi.i64p), abi.ptr(xy, abi.f64p),
+                              abi.ptr(wh, abi.i32p), C.byref(opts or fmatrix_opts()), res,
+                              abi.ptr(inl, abi.i32p)), "sfm_fmatrix_ac")
+    return _fmatrix_outputs(off, res, inl)
+
+
+def sparse_filter(ctx, matches_dir, opts=None):
+    lib = abi.load()
+    st = abi.SparseFilterStats()
+    _check(lib.sfm_sparse_filter(ctx.h, _b(matches_dir), C.byref(opts or fmatrix_opts()), C.byref(st)),
+           "sfm_sparse_filter")
+    return st

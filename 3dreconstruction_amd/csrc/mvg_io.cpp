@@ -799,3 +799,78 @@ extern "C" int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm
         return SFM_OK;
     });
 }
+
+extern "C" int sfm_sparse_filter(sfm_ctx* ctx, const char* matches_dir, const sfm_fmatrix_opts* opts,
+                                 sfm_sparse_filter_stats* stats) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && matches_dir, SFM_ERR_INVALID_ARG, "null argument");
+        sfm_fmatrix_opts o{4.0, 2048, 0};   // GeometricFilter_FMatrix_AC(4.0, imax_iteration = 2048)
+        if (opts) o = *opts;
+        const std::string dir(matches_dir);
+        std::string root;
+        // Load(sfm_data, VIEWS | INTRINSICS) (:1095), putative matches (:1138)
+        const auto views = load_views(filespec(dir, "sfm_data.json").c_str(), &root);
+        std::map<uint32_t, size_t> vix;
+        for (size_t k = 0; k < views.size(); ++k) vix[views[k].id_view] = k;
+        const MatchSet put = load_matches(filespec(dir, "matches.putative.bin").c_str());
+        std::map<size_t, std::vector<float>> feats;   // MatchesPairToMat: feature positions per view
+        auto feat_of = [&](uint32_t id) -> const std::vector<float>& {
+            auto it = vix.find(id);
+            SFM_REQUIRE(it != vix.end(), SFM_ERR_INVALID_ARG, "matches reference view %u not in sfm_data.json", id);
+            auto f = feats.find(it->second);
+            if (f != feats.end()) return f->second;
+            const std::string stem = basename_part(filespec(root, views[it->second].img_path));
+            return feats[it->second] = read_feat(filespec(dir, stem + ".feat").c_str());
+        };
+        const int64_t np = (int64_t)put.pairs.size();
+        std::vector<int64_t> off(np + 1, 0);
+        std::vector<double> xy(4 * std::max<size_t>(put.i.size(), 1));
+        std::vector<int32_t> wh(4 * std::max<int64_t>(np, 1));
+        for (int64_t q = 0; q < np; ++q) {
+            const auto& fi = feat_of(put.pairs[q].first);
+            const auto& fj = feat_of(put.pairs[q].second);
+            const View& vi = views[vix[put.pairs[q].first]];
+            const View& vj = views[vix[put.pairs[q].second]];
+            wh[4 * q] = (int32_t)vi.width; wh[4 * q + 1] = (int32_t)vi.height;
+            wh[4 * q + 2] = (int32_t)vj.width; wh[4 * q + 3] = (int32_t)vj.height;
+            off[q + 1] = off[q] + put.counts[q];
+            for (int64_t k = off[q]; k < off[q + 1]; ++k) {
+                const uint32_t a = put.i[k], b = put.j[k];
+                SFM_REQUIRE((size_t)a < fi.size() / 4 && (size_t)b < fj.size() / 4, SFM_ERR_INVALID_ARG,
+                            "pair (%u, %u): match (%u, %u) outside the features", put.pairs[q].first,
+                            put.pairs[q].second, a, b);
+                xy[4 * k] = fi[4 * (size_t)a];
+                xy[4 * k + 1] = fi[4 * (size_t)a + 1];
+                xy[4 * k + 2] = fj[4 * (size_t)b];
+                xy[4 * k + 3] = fj[4 * (size_t)b + 1];
+            }
+        }
+        std::vector<sfm_fmatrix_result> res((size_t)std::max<int64_t>(np, 1));
+        std::vector<int32_t> inl(std::max<size_t>(put.i.size(), 1));
+        if (np) {
+            const int rc = sfm_fmatrix_ac(ctx, np, off.data(), xy.data(), wh.data(), &o, res.data(), inl.data());
+            if (rc != SFM_OK) throw SfmError{rc};
+        }
+        // Robust_model_estimation keeps the pairs whose estimation succeeded,
+        // each with putative[index] for index in vec_inliers order
+        MatchSet out;
+        for (int64_t q = 0; q < np; ++q) {
+            if (res[q].n_inliers <= 0) continue;
+            out.pairs.push_back(put.pairs[q]);
+            out.counts.push_back(res[q].n_inliers);
+            for (int32_t t = 0; t < res[q].n_inliers; ++t) {
+                const int64_t k = off[q] + inl[off[q] + t];
+                out.i.push_back(put.i[k]);
+                out.j.push_back(put.j[k]);
+            }
+        }
+        save_matches(filespec(dir, "matches.f.bin").c_str(), out);
+        if (stats) {
+            stats->n_pairs_in = np;
+            stats->n_matches_in = (int64_t)put.i.size();
+            stats->n_pairs_out = (int64_t)out.pairs.size();
+            stats->n_matches_out = (int64_t)out.i.size();
+        }
+        return SFM_OK;
+    });
+}

@@ -494,6 +494,49 @@ typedef struct sfm_sparse_match_stats {
 int sfm_sparse_match(sfm_ctx* ctx, const char* matches_dir, const sfm_sparse_match_opts* opts,
                      sfm_sparse_match_stats* stats);
 
+/* ------------------------------------------------------------------------ */
+/* Geometric filter                                  */
+/* sparseBuilder::filter() (sparseBuilder.cpp:1025-1280) runs                */
+/* GeometricFilter_FMatrix_AC(4.0, 2048) (:1179-1186) over every putative    */
+/* pair: OpenMVG's a-contrario RANSAC (ACRANSAC) with the 7-point            */
+/* fundamental-matrix solver, keeping a pair iff it has > 2.5 * 7 inliers.   */
+/* Restated from OpenMVG's published code (un-vendored: parity unpinned,     */
+/* DESIGN.md §3); the GPU runs one workgroup per pair.                       */
+/* ------------------------------------------------------------------------ */
+typedef struct sfm_fmatrix_opts {
+    double precision;         /* 4.0 px: upper bound of the a-contrario threshold */
+    int32_t max_iterations;   /* 2048 (imax_iteration, :1040)                     */
+    int32_t reserved;
+} sfm_fmatrix_opts;
+typedef struct sfm_fmatrix_result {
+    double F[9];          /* row-major, pixels: x_J' F x_I = 0 (when n_inliers > 0)  */
+    double error_max;     /* a-contrario threshold in px (ACRANSAC .first)          */
+    double min_nfa;       /* log10 NFA of the best model (ACRANSAC .second)         */
+    int32_t n_inliers;    /* > 17 when the pair is kept, else 0                     */
+    int32_t iterations;   /* RANSAC iterations run                                  */
+} sfm_fmatrix_result;
+/* n_pairs independent pairs.  Pair q's putative correspondences are
+ * k = off[q] .. off[q+1]-1 with xy[4k..4k+3] = (x_I, y_I, x_J, y_J) in pixels
+ * (MatchesPairToMat order = the putative IndMatch order); wh[4q..4q+3] =
+ * (width_I, height_I, width_J, height_J).  inliers[off[q] + t],
+ * t < results[q].n_inliers: the kept correspondences (indices into the pair's
+ * list) in OpenMVG's vec_inliers order (ascending residual).  opts NULL =
+ * {4.0, 2048}.  A pair with more than 16384 correspondences returns
+ * SFM_ERR_UNSUPPORTED. */
+int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off, const double* xy,
+                   const int32_t* wh, const sfm_fmatrix_opts* opts,
+                   sfm_fmatrix_result* results, int32_t* inliers);
+
+/* sparseBuilder::filter(), file-staged: sfm_data.json (view sizes) +
+ * <stem>.feat + matches.putative.bin -> sfm_fmatrix_ac ->
+ * matches.f.bin (kept pairs, each pair's IndMatches in vec_inliers order).
+ * opts NULL = {4.0, 2048}. */
+typedef struct sfm_sparse_filter_stats {
+    int64_t n_pairs_in, n_pairs_out, n_matches_in, n_matches_out;
+} sfm_sparse_filter_stats;
+int sfm_sparse_filter(sfm_ctx* ctx, const char* matches_dir, const sfm_fmatrix_opts* opts,
+                      sfm_sparse_filter_stats* stats);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

@@ -112,6 +112,18 @@ int orc_dedup_decorator(const uint32_t* i, const uint32_t* j, int64_t n, const f
 /* CascadeHasher::Init projections, float [188][128]. */
 int orc_cascade_projections(float* out);
 
+/* sfm_fmatrix_ac semantics (fmat_oracle.cpp: OpenMVG GeometricFilter_FMatrix_AC
+ * + ACRANSAC restated), OpenMP over pairs. */
+int orc_fmatrix_ac(int64_t n_pairs, const int64_t* off, const double* xy, const int32_t* wh,
+                   const sfm_fmatrix_opts* opts, sfm_fmatrix_result* results, int32_t* inliers,
+                   int32_t n_threads);
+/* std::mt19937(default_seed) + std::uniform_int_distribution<uint32_t>(lo[k], hi[k]) */
+int orc_uniform_draws(const uint32_t* lo, const uint32_t* hi, int64_t n, uint32_t* out);
+/* fn 0: the filter's log10, 1: its cube root */
+int orc_det_math(int32_t fn, const double* x, int64_t n, double* out);
+/* seven-point solver on 7 normalised correspondences: F[9 * n_models] */
+int orc_seven_point(const double* x1, const double* x2, double* F, int32_t* n_models);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }
