@@ -31,12 +31,10 @@ struct DevProblem {
     // shard data
     const int32_t* pt_off;
     const int32_t* obs_img;
-    const int32_t* obs_pt;
     const int32_t* obs_slot;
     const double* obs_uv;
     const ChunkDesc* chunks;
     const int32_t* img_obs_ptr;
-    const int32_t* img_obs;
     const int32_t* img_pt;          // image order (img_obs_ptr): point, measurement
     const double* img_uv;
     const int32_t* img_colc;

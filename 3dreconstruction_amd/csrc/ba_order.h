@@ -1,0 +1,17 @@
+// Device-side planning helpers (ba_order.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.h"
+
+namespace sfm {
+
+// Image order of a shard's observations (stable by image, shard order within
+// one): img_pt[q] = owning shard point, img_uv[2q..] = measurement.  Inputs
+// and outputs are device arrays; runs on stream s.
+void ba_image_order(const int32_t* obs_img, const double* obs_uv, const int32_t* pt_off, int32_t n_sobs,
+                    int32_t n_spt, int32_t n_img, int32_t* img_pt, double* img_uv, hipStream_t s);
+
+}  // namespace sfm

@@ -1,0 +1,73 @@
+// Device-side part of BA planning: the image-ordered copy of a shard's
+// observations that the image Gram pass (image_gram_kernel) walks.
+//
+// The host planner used to build it with a counting sort and upload three
+// more observation-sized arrays (120 MB at C4); here the observations already
+// resident in HBM are stably radix-sorted by image (rocPRIM through hipCUB:
+// shard order is kept within an image, the order the host sort produced) and
+// the point index and measurement gathered in that order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "ba_order.h"
+
+namespace sfm {
+namespace {
+
+// obs_pt[s] = the shard point owning observation s
+__global__ __launch_bounds__(256) void obs_point_kernel(const int32_t* __restrict__ pt_off, int32_t n_spt,
+                                                        int32_t* __restrict__ obs_pt) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n_spt) return;
+    for (int s = pt_off[k]; s < pt_off[k + 1]; ++s) obs_pt[s] = k;
+}
+
+__global__ __launch_bounds__(256) void iota_kernel(int32_t* __restrict__ v, int32_t n) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s < n) v[s] = s;
+}
+
+// image order: point and measurement of the observation at each position
+__global__ __launch_bounds__(256) void image_gather_kernel(const int32_t* __restrict__ order,
+                                                           const int32_t* __restrict__ obs_pt,
+                                                           const double2* __restrict__ obs_uv, int32_t n,
+                                                           int32_t* __restrict__ img_pt, double2* __restrict__ img_uv) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= n) return;
+    const int s = order[q];
+    img_pt[q] = obs_pt[s];
+    img_uv[q] = obs_uv[s];
+}
+
+}  // namespace
+
+void ba_image_order(const int32_t* obs_img, const double* obs_uv, const int32_t* pt_off, int32_t n_sobs,
+                    int32_t n_spt, int32_t n_img, int32_t* img_pt, double* img_uv, hipStream_t s) {
+    if (n_sobs <= 0) return;
+    DBuf<int32_t> obs_pt, idx, order, keys_out;
+    obs_pt.alloc(n_sobs);
+    idx.alloc(n_sobs);
+    order.alloc(n_sobs);
+    keys_out.alloc(n_sobs);
+    const unsigned gs = (unsigned)((n_sobs + 255) / 256);
+    hipLaunchKernelGGL(obs_point_kernel, dim3((unsigned)((n_spt + 255) / 256)), dim3(256), 0, s, pt_off, n_spt,
+                       obs_pt.p);
+    SFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(iota_kernel, dim3(gs), dim3(256), 0, s, idx.p, n_sobs);
+    SFM_HIP(hipGetLastError());
+    int end_bit = 1;
+    while (end_bit < 31 && (1 << end_bit) < n_img) ++end_bit;
+    size_t tmp_bytes = 0;
+    SFM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, obs_img, keys_out.p, idx.p, order.p, n_sobs, 0,
+                                               end_bit, s));
+    DBuf<uint8_t> tmp;
+    tmp.alloc(std::max<size_t>(tmp_bytes, 1));
+    SFM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, obs_img, keys_out.p, idx.p, order.p, n_sobs, 0,
+                                               end_bit, s));
+    hipLaunchKernelGGL(image_gather_kernel, dim3(gs), dim3(256), 0, s, order.p, obs_pt.p,
+                       reinterpret_cast<const double2*>(obs_uv), n_sobs, img_pt, reinterpret_cast<double2*>(img_uv));
+    SFM_HIP(hipGetLastError());
+    // the temporaries go back to the context's cache, stream-ordered
+}
+
+}  // namespace sfm

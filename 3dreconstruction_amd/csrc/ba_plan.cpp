@@ -39,16 +39,34 @@ void parallel_ranges(int64_t n, F&& fn) {
 
 // block half-bandwidth of the points' camera spans under the order cam_blk
 int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk) {
-    int32_t D = 0;
-    for (int64_t p = 0; p < P.n_pt; ++p) {
-        int lo = INT_MAX, hi = -1;
-        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
-            const int b = cam_blk[P.obs_img[o]];
-            if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+    int32_t Dt[16] = {0};
+    parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int t) {
+        int32_t D = 0;
+        for (int64_t p = p0; p < p1; ++p) {
+            int lo = INT_MAX, hi = -1;
+            for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+                const int b = cam_blk[P.obs_img[o]];
+                if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+            }
+            if (hi >= 0) D = std::max(D, hi - lo);
         }
-        if (hi >= 0) D = std::max(D, hi - lo);
-    }
+        Dt[t] = D;
+    });
+    int32_t D = 0;
+    for (int32_t d : Dt) D = std::max(D, d);
     return D;
+}
+
+// flags[i] = 1 for every value i = idx[o] (o < n): a per-thread pass each
+void mark_used(const int32_t* idx, int64_t n, int32_t m, std::vector<char>& flags) {
+    std::vector<std::vector<char>> part(16);
+    parallel_ranges(n, [&](int64_t o0, int64_t o1, int t) {
+        part[t].assign(m, 0);
+        for (int64_t o = o0; o < o1; ++o) part[t][idx[o]] = 1;
+    });
+    flags.assign(m, 0);
+    for (const auto& f : part)
+        for (int32_t i = 0; i < (int32_t)f.size(); ++i) flags[i] |= f[i];
 }
 
 // Reverse Cuthill-McKee over the camera co-visibility graph (cameras that
@@ -140,8 +158,8 @@ std::vector<int32_t> rcm_order(const sfm_ba_problem& P, const std::vector<int32_
 std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, int32_t* D_out) {
     PhaseTimer tm("camera_blocks");
     std::vector<int32_t> cam_blk(P.n_img, -1);
-    std::vector<char> used(P.n_img, 0);
-    for (int64_t o = 0; o < P.n_obs; ++o) used[P.obs_img[o]] = 1;
+    std::vector<char> used;
+    mark_used(P.obs_img, P.n_obs, P.n_img, used);
     int32_t ncam = 0;
     for (int i = 0; i < P.n_img; ++i)
         if (used[i] && i != P.const_img) cam_blk[i] = ncam++;
@@ -173,8 +191,11 @@ void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
     for (int i = 0; i < P.n_img; ++i)
         if (pl.cam_blk[i] >= 0) pl.blk_img[pl.cam_blk[i]] = i;
     pl.intr_blk.assign(P.n_intr, -1);
-    std::vector<char> iu(P.n_intr, 0);
-    for (int64_t o = 0; o < P.n_obs; ++o) iu[P.img_intr[P.obs_img[o]]] = 1;
+    // intrinsics blocks of observed images
+    std::vector<char> iu(P.n_intr, 0), im;
+    mark_used(P.obs_img, P.n_obs, P.n_img, im);
+    for (int i = 0; i < P.n_img; ++i)
+        if (im[i]) iu[P.img_intr[i]] = 1;
     for (int q = 0; q < P.n_intr; ++q)
         if (iu[q]) { pl.intr_blk[q] = pl.nintr++; pl.blk_intr.push_back(q); }
     pl.nb = 6LL * pl.ncam;
@@ -195,21 +216,36 @@ void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
 
 void partition_points(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int world,
                       std::vector<int64_t>& order, std::vector<int64_t>& bounds) {
-    struct Key { int32_t lo, hi; int64_t id; };
-    std::vector<Key> keys(P.n_pt);
-    for (int64_t p = 0; p < P.n_pt; ++p) {
-        int lo = INT_MAX, hi = -1;
-        for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
-            const int b = cam_blk[P.obs_img[o]];
-            if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+    // stable order by (first, last) active camera block: two stable counting
+    // passes (last, then first) over ncam + 1 buckets (no active camera sorts
+    // last), the order std::stable_sort on the pair gives
+    int32_t ncam = 0;
+    for (int32_t b : cam_blk) ncam = std::max(ncam, b + 1);
+    std::vector<int32_t> lo(P.n_pt), hi(P.n_pt);
+    parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int) {
+        for (int64_t p = p0; p < p1; ++p) {
+            int l = ncam, h = 0;
+            for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+                const int b = cam_blk[P.obs_img[o]];
+                if (b >= 0) { l = std::min(l, b); h = std::max(h, b + 1); }
+            }
+            lo[p] = l;
+            hi[p] = h;
         }
-        keys[p] = {lo, hi, p};
-    }
-    std::stable_sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
-        return a.lo != b.lo ? a.lo < b.lo : a.hi < b.hi;
     });
+    std::vector<int64_t> tmp(P.n_pt), cnt(ncam + 2);
+    auto pass = [&](const std::vector<int32_t>& key, const int64_t* in, int64_t* out) {
+        std::fill(cnt.begin(), cnt.end(), 0);
+        for (int64_t k = 0; k < P.n_pt; ++k) cnt[key[in ? in[k] : k] + 1]++;
+        for (int32_t b = 0; b <= ncam; ++b) cnt[b + 1] += cnt[b];
+        for (int64_t k = 0; k < P.n_pt; ++k) {
+            const int64_t p = in ? in[k] : k;
+            out[cnt[key[p]]++] = p;
+        }
+    };
     order.resize(P.n_pt);
-    for (int64_t k = 0; k < P.n_pt; ++k) order[k] = keys[k].id;
+    pass(hi, nullptr, tmp.data());
+    pass(lo, tmp.data(), order.data());
     bounds.assign(world + 1, P.n_pt);
     bounds[0] = 0;
     int64_t acc = 0, r = 1;
@@ -257,12 +293,22 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 "pt_offsets must run from 0 to n_obs");
     SFM_REQUIRE(P.n_obs < INT32_MAX && P.n_pt < INT32_MAX, SFM_ERR_UNSUPPORTED,
                 "more than 2^31 observations per process");
-    for (int64_t p = 0; p < P.n_pt; ++p)
-        SFM_REQUIRE(P.pt_offsets[p + 1] >= P.pt_offsets[p], SFM_ERR_INVALID_ARG,
-                    "pt_offsets not monotone at point %lld", (long long)p);
-    for (int64_t o = 0; o < P.n_obs; ++o)
-        SFM_REQUIRE(P.obs_img[o] >= 0 && P.obs_img[o] < P.n_img, SFM_ERR_INVALID_ARG,
-                    "obs %lld references image %d", (long long)o, P.obs_img[o]);
+    {
+        // first offending point / observation per host range, reported in order
+        std::vector<int64_t> bad_p(16, -1), bad_o(16, -1);
+        parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int t) {
+            for (int64_t p = p0; p < p1 && bad_p[t] < 0; ++p)
+                if (P.pt_offsets[p + 1] < P.pt_offsets[p]) bad_p[t] = p;
+        });
+        parallel_ranges(P.n_obs, [&](int64_t o0, int64_t o1, int t) {
+            for (int64_t o = o0; o < o1 && bad_o[t] < 0; ++o)
+                if (P.obs_img[o] < 0 || P.obs_img[o] >= P.n_img) bad_o[t] = o;
+        });
+        for (int64_t p : bad_p)
+            SFM_REQUIRE(p < 0, SFM_ERR_INVALID_ARG, "pt_offsets not monotone at point %lld", (long long)p);
+        for (int64_t o : bad_o)
+            SFM_REQUIRE(o < 0, SFM_ERR_INVALID_ARG, "obs %lld references image %d", (long long)o, P.obs_img[o]);
+    }
     for (int i = 0; i < P.n_img; ++i)
         SFM_REQUIRE(P.img_intr[i] >= 0 && P.img_intr[i] < P.n_intr, SFM_ERR_INVALID_ARG,
                     "image %d references intrinsics %d", i, P.img_intr[i]);
@@ -292,12 +338,17 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // ---- shard arrays: chunkable points first, then general points ---------
     const int64_t b0 = pl.bounds[rank], b1 = pl.bounds[rank + 1];
     {
+        std::vector<char> ck(b1 - b0);
+        parallel_ranges(b1 - b0, [&](int64_t k0, int64_t k1, int) {
+            for (int64_t k = k0; k < k1; ++k) ck[k] = chunkable(P, pl, pl.order[b0 + k]);
+        });
         std::vector<int64_t> cpts, gpts;
-        for (int64_t k = b0; k < b1; ++k) (chunkable(P, pl, pl.order[k]) ? cpts : gpts).push_back(pl.order[k]);
+        for (int64_t k = b0; k < b1; ++k) (ck[k - b0] ? cpts : gpts).push_back(pl.order[k]);
         pl.n_cpt = (int64_t)cpts.size();
         pl.spt_global = std::move(cpts);
         pl.spt_global.insert(pl.spt_global.end(), gpts.begin(), gpts.end());
     }
+    tm.mark("classify");
     pl.n_spt = b1 - b0;
     pl.pt_off.assign(pl.n_spt + 1, 0);
     for (int64_t k = 0; k < pl.n_spt; ++k) {
@@ -305,8 +356,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         pl.pt_off[k + 1] = pl.pt_off[k] + (int32_t)(P.pt_offsets[p + 1] - P.pt_offsets[p]);
     }
     pl.n_sobs = pl.pt_off[pl.n_spt];
+    tm.mark("pt_off");
     pl.obs_img.resize(pl.n_sobs);
-    pl.obs_pt.resize(pl.n_sobs);
     pl.obs_uv.resize(2 * pl.n_sobs);
     pl.obs_slot.assign(pl.n_sobs, 0);
     parallel_ranges(pl.n_spt, [&](int64_t k0, int64_t k1, int) {
@@ -314,7 +365,6 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             const int64_t p = pl.spt_global[k];
             for (int64_t o = P.pt_offsets[p], s = pl.pt_off[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
                 pl.obs_img[s] = P.obs_img[o];
-                pl.obs_pt[s] = (int32_t)k;
                 pl.obs_uv[2 * s] = P.obs_uv[2 * o];
                 pl.obs_uv[2 * s + 1] = P.obs_uv[2 * o + 1];
             }
@@ -344,9 +394,11 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         // factor, M = Jx L^-T, Z = J' M: 180 per observation + 30)
         return 3 * rows * (rows + 1) + 780 * nobs + 30;
     };
-    auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, std::vector<int32_t>& slot_out) -> int64_t {
+    // greedy chunking of shard points [k_begin, k_end); slot_out is indexed by
+    // shard observation (each range writes its own)
+    auto make_chunks_range = [&](int cap, int32_t k_begin, int32_t k_end, std::vector<ChunkDesc>& chunks_out,
+                                 HostVec<int32_t>& slot_out) -> int64_t {
         int64_t flops = 0;
-        slot_out.assign(pl.pt_off[ncp], 0);
         ChunkDesc cd{};
         std::vector<int> cams, intrs, dcams;  // F-slot images / intrinsics, staged images
         // O(1) membership for the open chunk: image -> F slot / staged index,
@@ -384,8 +436,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             size_t size() const { return (size_t)n; }
             bool has(int x) const { return std::find(v, v + n, x) != v + n; }
         };
-        if (ncp > 0) reset(0);
-        for (int32_t k = 0; k < ncp; ++k) {
+        if (k_end > k_begin) reset(k_begin);
+        for (int32_t k = k_begin; k < k_end; ++k) {
             const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
             Small pc, pi, pd;
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
@@ -442,45 +494,72 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             }
             flops += point_flops(own, nobs);
         }
-        if (ncp > 0) close(ncp);
+        if (k_end > k_begin) close(k_end);
         return flops;
     };
-    int max_own = 0, max_obs = 0;
-    for (int64_t k = 0; k < ncp; ++k) {
-        max_obs = std::max(max_obs, pl.pt_off[k + 1] - pl.pt_off[k]);
-        int nc = 0;
-        int32_t pi[kIntrSlots];
-        int ni = 0;
-        for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
-            if (pl.cam_blk[pl.obs_img[s]] >= 0) ++nc;
-            const int q = P.img_intr[pl.obs_img[s]];
-            if (std::find(pi, pi + ni, q) == pi + ni) pi[ni++] = q;
+    // Large shards are chunked in 16 fixed point ranges on host threads (a
+    // chunk never spans two ranges: at most 15 extra chunks out of thousands;
+    // the split depends on the shard only, never on the host)
+    auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, HostVec<int32_t>& slot_out) -> int64_t {
+        slot_out.resize(pl.pt_off[ncp]);   // every entry written by its range
+        const int nseg = ncp >= 65536 ? 16 : 1;
+        std::vector<std::vector<ChunkDesc>> seg_chunks(nseg);
+        std::vector<int64_t> seg_flops(nseg, 0);
+        std::vector<int> seg_rc(nseg, SFM_OK);
+        auto run = [&](int g) {
+            seg_rc[g] = guarded([&] {
+                const int32_t k0 = (int32_t)((int64_t)ncp * g / nseg), k1 = (int32_t)((int64_t)ncp * (g + 1) / nseg);
+                seg_flops[g] = make_chunks_range(cap, k0, k1, seg_chunks[g], slot_out);
+                return SFM_OK;
+            });
+        };
+        std::vector<std::thread> th;
+        for (int g = 1; g < nseg; ++g) th.emplace_back(run, g);
+        run(0);
+        for (auto& t : th) t.join();
+        int64_t flops = 0;
+        chunks_out.clear();
+        for (int g = 0; g < nseg; ++g) {
+            if (seg_rc[g] != SFM_OK) throw SfmError{seg_rc[g]};
+            chunks_out.insert(chunks_out.end(), seg_chunks[g].begin(), seg_chunks[g].end());
+            flops += seg_flops[g];
         }
-        max_own = std::max(max_own, 6 * nc + 4 * ni);
+        return flops;
+    };
+    tm.mark("shard_copy");
+    int max_own = 0, max_obs = 0;
+    {
+        int mo[16] = {0}, mb[16] = {0};
+        parallel_ranges(ncp, [&](int64_t k0, int64_t k1, int t) {
+            int lo_own = 0, lo_obs = 0;   // thread-local (the arrays share a cache line)
+            for (int64_t k = k0; k < k1; ++k) {
+                lo_obs = std::max(lo_obs, pl.pt_off[k + 1] - pl.pt_off[k]);
+                int nc = 0;
+                int32_t pi[kIntrSlots];
+                int ni = 0;
+                for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                    if (pl.cam_blk[pl.obs_img[s]] >= 0) ++nc;
+                    const int q = P.img_intr[pl.obs_img[s]];
+                    if (std::find(pi, pi + ni, q) == pi + ni) pi[ni++] = q;
+                }
+                lo_own = std::max(lo_own, 6 * nc + 4 * ni);
+            }
+            mo[t] = lo_own;
+            mb[t] = lo_obs;
+        });
+        for (int t = 0; t < 16; ++t) { max_own = std::max(max_own, mo[t]); max_obs = std::max(max_obs, mb[t]); }
     }
+    tm.mark("chunk_shape");
     int64_t flops = 0;
-    std::vector<int32_t> cslot;
+    HostVec<int32_t> cslot;
     pl.tile_nt = 5;
     // the 64-row kernel walks 48-observation batches (ba_kernels.hip)
     if (max_own <= 64 && max_obs <= 48 && !std::getenv("SFM_BA_TILE80")) {
-        // both tile heights are planned concurrently (independent, read-only inputs)
+        // both tile heights are planned (each over the host threads)
         std::vector<ChunkDesc> c4, c5;
-        std::vector<int32_t> s4, s5;
-        int64_t f4 = 0, f5 = 0;
-        int rc5 = SFM_OK;
-        std::thread t5([&] {
-            rc5 = guarded([&] {
-                f5 = make_chunks(kTileRowsUsed, c5, s5);
-                return SFM_OK;
-            });
-        });
-        int rc4 = guarded([&] {
-            f4 = make_chunks(64, c4, s4);
-            return SFM_OK;
-        });
-        t5.join();
-        if (rc4 != SFM_OK) throw SfmError{rc4};
-        if (rc5 != SFM_OK) throw SfmError{rc5};
+        HostVec<int32_t> s4, s5;
+        const int64_t f5 = make_chunks(kTileRowsUsed, c5, s5);
+        const int64_t f4 = make_chunks(64, c4, s4);
         if (c4.size() * 4 <= c5.size() * 5) {
             pl.tile_nt = 4; pl.chunks.swap(c4); cslot.swap(s4); flops = f4;
         } else {
@@ -573,19 +652,13 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +
                      (int64_t)pl.chunks.size() * kTileR * kTileR * 8;
 
-    // ---- image CSR of shard observations ------------------------------------
-    // counting sort by image, in parallel: per-range counts, then each range
-    // scatters from its own offsets (ranges in order => shard order per image)
+    // ---- observations per image (the image-ordered copy itself is built on
+    // the device from the uploaded shard arrays: ba_image_order) -------------
     pl.img_obs_ptr.assign(P.n_img + 1, 0);
-    pl.img_obs.resize(pl.n_sobs);
-    pl.img_pt.resize(pl.n_sobs);
-    pl.img_uv.resize(2 * pl.n_sobs);
     {
         constexpr int kMaxT = 16;
         std::vector<std::vector<int32_t>> cnt(kMaxT);
-        std::vector<std::pair<int64_t, int64_t>> rng(kMaxT, {0, 0});
         parallel_ranges(pl.n_sobs, [&](int64_t s0, int64_t s1, int t) {
-            rng[t] = {s0, s1};
             cnt[t].assign(P.n_img, 0);
             for (int64_t s = s0; s < s1; ++s) cnt[t][pl.obs_img[s]]++;
         });
@@ -595,28 +668,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 if (!cnt[t].empty()) tot += cnt[t][i];
             pl.img_obs_ptr[i + 1] = pl.img_obs_ptr[i] + tot;
         }
-        // per-range write cursors: image start + counts of earlier ranges
-        for (int i = 0; i < P.n_img; ++i) {
-            int32_t at = pl.img_obs_ptr[i];
-            for (int t = 0; t < kMaxT; ++t)
-                if (!cnt[t].empty()) {
-                    const int32_t c = cnt[t][i];
-                    cnt[t][i] = at;
-                    at += c;
-                }
-        }
-        parallel_ranges(pl.n_sobs, [&](int64_t s0, int64_t s1, int t) {
-            std::vector<int32_t>& fill = cnt[t];
-            for (int64_t s = s0; s < s1; ++s) {
-                const int32_t q = fill[pl.obs_img[s]]++;
-                pl.img_obs[q] = (int32_t)s;
-                pl.img_pt[q] = pl.obs_pt[s];
-                pl.img_uv[2 * q] = pl.obs_uv[2 * s];
-                pl.img_uv[2 * q + 1] = pl.obs_uv[2 * s + 1];
-            }
-        });
     }
-
     tm.mark("image_csr");
     // ---- reduce plan -----------------------------------------------------------
     // Every matrix block (a, b), a >= b in F-block order (cameras, then
@@ -685,13 +737,28 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 mprod.push_back({(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}});
         }
     }
-    auto by_key = [](const auto& x, const auto& y) { return x.first < y.first; };
+    // stable by key: a counting sort over the block-pair keys (< nFB^2) when
+    // they fit a count array, else std::stable_sort (the same order)
+    auto sort_terms = [&](auto& v) {
+        using E = typename std::decay_t<decltype(v)>::value_type;
+        const int64_t kmax = (int64_t)nFB * nFB + 1;
+        if (kmax > ((int64_t)1 << 25) || v.size() < 4096) {
+            std::stable_sort(v.begin(), v.end(), [](const E& x, const E& y) { return x.first < y.first; });
+            return;
+        }
+        std::vector<int32_t> cnt((size_t)kmax + 1, 0);
+        for (const E& e : v) cnt[(size_t)e.first + 1]++;
+        for (int64_t k = 0; k < kmax; ++k) cnt[(size_t)k + 1] += cnt[(size_t)k];
+        std::vector<E> out(v.size());
+        for (const E& e : v) out[(size_t)cnt[(size_t)e.first]++] = e;
+        v.swap(out);
+    };
     tm.mark("terms");
-    std::stable_sort(mterms.begin(), mterms.end(), by_key);
-    std::stable_sort(vterms.begin(), vterms.end(), by_key);
-    std::stable_sort(cterms.begin(), cterms.end(), by_key);
-    std::stable_sort(mprod.begin(), mprod.end(), by_key);
-    std::stable_sort(vprod.begin(), vprod.end(), by_key);
+    sort_terms(mterms);
+    sort_terms(vterms);
+    sort_terms(cterms);
+    sort_terms(mprod);
+    sort_terms(vprod);
 
     tm.mark("term_sort");
     const int Dp = pl.D + 1;
@@ -758,11 +825,20 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
     } else {
         // dense: every block that receives a term (the rest stays zero)
+        // keys of both (sorted) term lists, merged without duplicates
         std::vector<int64_t> keys;
-        for (const auto& t : mterms) keys.push_back(t.first);
-        for (const auto& t : mprod) keys.push_back(t.first);
-        std::sort(keys.begin(), keys.end());
-        keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+        {
+            size_t a = 0, b = 0;
+            int64_t last = -1;
+            while (a < mterms.size() || b < mprod.size()) {
+                const int64_t ka = a < mterms.size() ? mterms[a].first : INT64_MAX;
+                const int64_t kb = b < mprod.size() ? mprod[b].first : INT64_MAX;
+                const int64_t k = std::min(ka, kb);
+                if (k != last) keys.push_back(last = k);
+                if (ka == k) ++a;
+                else ++b;
+            }
+        }
         for (int64_t key : keys) {
             const int32_t a = (int32_t)(key / nFB), b = (int32_t)(key % nFB);
             emit(key, kDstDense, col_of_fb(a) * pl.nF + col_of_fb(b), size_of_fb(a), size_of_fb(b), (int32_t)pl.nF,

@@ -5,6 +5,7 @@
 
 #include "../../include/sfmcore.h"
 #include "ba_types.h"
+#include "common.h"
 
 namespace sfm {
 
@@ -41,14 +42,14 @@ struct BAHostPlan {
     std::vector<int64_t> gz_off;     // [n_gpt+1] Z buffer range of a point: blocks, then w (3)
     int64_t n_z = 0, gz_max = 0;     // Z doubles in all / of the largest point
     std::vector<int64_t> spt_global;  // shard point -> global point id
-    std::vector<int32_t> pt_off;      // [n_spt+1]
-    std::vector<int32_t> obs_img, obs_pt, obs_slot;
-    std::vector<double> obs_uv;
+    // observation-sized arrays live in page-locked staging memory while a
+    // context is bound (HostVec, common.h): uploaded, then released
+    HostVec<int32_t> pt_off;          // [n_spt+1]
+    HostVec<int32_t> obs_img, obs_slot;
+    HostVec<double> obs_uv;
     std::vector<ChunkDesc> chunks;
     int32_t tile_nt = 5;              // 16-row MFMA tiles per chunk side (4 or 5)
-    std::vector<int32_t> img_obs_ptr, img_obs;
-    std::vector<int32_t> img_pt;      // image order: point of each observation
-    std::vector<double> img_uv;       // image order: its measurement
+    std::vector<int32_t> img_obs_ptr;  // [n_img+1] shard observations per image (prefix)
 
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;

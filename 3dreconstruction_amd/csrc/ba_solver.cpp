@@ -27,6 +27,7 @@
 
 #include "ba_bcr.h"
 #include "ba_kernels.h"
+#include "ba_order.h"
 #include "ba_plan.h"
 #include "common.h"
 
@@ -36,7 +37,7 @@ struct sfm_ba_plan {
     sfm_ctx* ctx = nullptr;
     BAHostPlan hp;
     DevProblem P{};
-    DBuf<int32_t> pt_off, obs_img, obs_pt, obs_slot, img_obs_ptr, img_obs, img_colc,
+    DBuf<int32_t> pt_off, obs_img, obs_slot, img_obs_ptr, img_colc,
         img_coli, img_intr, intr_col, blk_img, blk_intr;
     DBuf<double> obs_uv;
     DBuf<ChunkDesc> chunks;
@@ -81,8 +82,8 @@ struct sfm_ba_plan {
 
 namespace {
 
-template <class T>
-void up(DBuf<T>& d, const std::vector<T>& h, hipStream_t s) {
+template <class T, class V>
+void up(DBuf<T>& d, const V& h, hipStream_t s) {
     d.alloc(std::max<size_t>(h.size(), 1));
     d.upload(h.data(), h.size(), s);
 }
@@ -97,14 +98,14 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     tm.mark("build_plan");
     up(pl->pt_off, h.pt_off, s);
     up(pl->obs_img, h.obs_img, s);
-    up(pl->obs_pt, h.obs_pt, s);
     up(pl->obs_slot, h.obs_slot, s);
     up(pl->obs_uv, h.obs_uv, s);
     up(pl->chunks, h.chunks, s);
     up(pl->img_obs_ptr, h.img_obs_ptr, s);
-    up(pl->img_obs, h.img_obs, s);
-    up(pl->img_pt, h.img_pt, s);
-    up(pl->img_uv, h.img_uv, s);
+    pl->img_pt.alloc(std::max<int64_t>(h.n_sobs, 1));
+    pl->img_uv.alloc(2 * std::max<int64_t>(h.n_sobs, 1));
+    ba_image_order(pl->obs_img.p, pl->obs_uv.p, pl->pt_off.p, (int32_t)h.n_sobs, (int32_t)h.n_spt, prob.n_img,
+                   pl->img_pt.p, pl->img_uv.p, s);
     up(pl->img_colc, h.img_colc, s);
     up(pl->img_coli, h.img_coli, s);
     {
@@ -213,9 +214,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.nb = h.nb; P.nF = h.nF;
     P.huber_a = prob.huber_a;
     P.cam_model = prob.camera_model;
-    P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p; P.obs_pt = pl->obs_pt.p;
+    P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p;
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
-    P.img_obs_ptr = pl->img_obs_ptr.p; P.img_obs = pl->img_obs.p;
+    P.img_obs_ptr = pl->img_obs_ptr.p;
     P.img_pt = pl->img_pt.p; P.img_uv = pl->img_uv.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.intr_col = pl->intr_col.p;
@@ -315,6 +316,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     for (auto& e2 : pl->ev) SFM_HIP(hipEventCreate(&e2));
     tm.mark("alloc+upload");
     SFM_HIP(hipStreamSynchronize(s));
+    // the observation staging goes back to the cache (the uploads are done)
+    h.obs_img = HostVec<int32_t>();
+    h.obs_slot = HostVec<int32_t>();
+    h.obs_uv = HostVec<double>();
     tm.mark("sync");
 }
 
@@ -648,8 +653,11 @@ extern "C" int sfm_ba_plan_destroy(sfm_ba_plan* pl) {
     return guarded([&] {
         if (!pl) return SFM_OK;
         CtxScope scope_(pl->ctx);
+        PhaseTimer tm("sfm_ba_plan_destroy");
         (void)hipStreamSynchronize(pl->ctx->stream);
+        tm.mark("sync");
         delete pl;
+        tm.mark("delete");
         return SFM_OK;
     });
 }

@@ -4,7 +4,7 @@
 // HBM layout (DESIGN.md §BA data layout), per rank:
 //   points   : X[3*n_spt] in shard order (landmark-major, sorted by first
 //              active camera), scaleE[3*n_spt] (Jacobi scale, fixed at iter 0)
-//   obs      : obs_uv[2*n_sobs], obs_img[n_sobs], obs_pt[n_sobs], pt_off[n_spt+1]
+//   obs      : obs_uv[2*n_sobs], obs_img[n_sobs], pt_off[n_spt+1]
 //              (observations of a point contiguous)
 //   cameras  : extr[6*n_img], intr[4*n_intr] (full tables, replicated),
 //              CamPre[n_img] (per-camera rotation terms), scaleF[nF]

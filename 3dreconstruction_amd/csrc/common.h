@@ -6,8 +6,12 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
-#include <string>
 #include <ctime>
+#include <new>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "../../include/sfmcore.h"
 
@@ -81,6 +85,37 @@ void dev_cache_release(hipStream_t s);   // hipFree every cached block of s
 // Page-locked, device-mapped host memory, cached the same way.
 void* pinned_alloc(size_t bytes);
 void pinned_free(void* p);
+// Host staging memory for uploads: page-locked and cached like the above
+// while a context is bound (no page faults on reuse, DMA uploads), plain
+// malloc otherwise.  host_free takes either kind.
+void* host_alloc(size_t bytes);
+void host_free(void* p);
+
+// std::vector allocator over host_alloc that default-initialises (resize
+// does not zero-fill what the planner overwrites anyway)
+template <class T>
+struct HostAlloc {
+    using value_type = T;
+    HostAlloc() = default;
+    template <class U>
+    HostAlloc(const HostAlloc<U>&) noexcept {}
+    T* allocate(size_t n) { return static_cast<T*>(host_alloc(n * sizeof(T))); }
+    void deallocate(T* p, size_t) noexcept { host_free(p); }
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    bool operator==(const HostAlloc<U>&) const noexcept { return true; }
+    template <class U>
+    bool operator!=(const HostAlloc<U>&) const noexcept { return false; }
+};
+template <class T>
+using HostVec = std::vector<T, HostAlloc<T>>;
 
 // Binds a context to the calling thread for the duration of an API call:
 // its device, and its stream as the key of the device memory cache.

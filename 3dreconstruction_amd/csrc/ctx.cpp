@@ -2,7 +2,9 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -103,17 +105,19 @@ size_t size_class(size_t b) {
     return (b + step - 1) / step * step;
 }
 
+// kind 0: device, 1: pinned mapped + coherent (polled scalars), 2: pinned
+// staging for uploads
 struct Block {
     hipStream_t key;
     size_t bytes;
-    bool pinned;
+    int kind;
 };
 
 struct MemCache {
     std::mutex mu;
     std::unordered_map<void*, Block> live;
-    // (key, pinned, class) -> free blocks
-    std::map<std::tuple<hipStream_t, bool, size_t>, std::vector<void*>> free;
+    // (key, kind, class) -> free blocks
+    std::map<std::tuple<hipStream_t, int, size_t>, std::vector<void*>> free;
     std::unordered_set<hipStream_t> streams;   // contexts alive (their keys)
     size_t cached = 0;
     static constexpr size_t kCap = size_t(32) << 30;   // cached bytes kept at most
@@ -124,8 +128,8 @@ MemCache& cache() {
     return *c;
 }
 
-void raw_free(void* p, bool pinned) {
-    if (pinned) (void)hipHostFree(p);
+void raw_free(void* p, int kind) {
+    if (kind) (void)hipHostFree(p);
     else (void)hipFree(p);
 }
 
@@ -143,24 +147,26 @@ void release_all_locked(MemCache& c, hipStream_t only, bool all) {
     }
 }
 
-void* cached_alloc(size_t bytes, bool pinned) {
+void* cached_alloc(size_t bytes, int kind) {
     MemCache& c = cache();
     const hipStream_t key = tl_stream;
     const size_t cls = size_class(bytes);
     std::lock_guard<std::mutex> lk(c.mu);
     if (key && c.streams.count(key)) {
-        auto it = c.free.find({key, pinned, cls});
+        auto it = c.free.find({key, kind, cls});
         if (it != c.free.end() && !it->second.empty()) {
             void* p = it->second.back();
             it->second.pop_back();
             c.cached -= cls;
-            c.live[p] = Block{key, cls, pinned};
+            c.live[p] = Block{key, cls, kind};
             return p;
         }
     }
     void* p = nullptr;
     auto get = [&] {
-        return pinned ? hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent) : hipMalloc(&p, cls);
+        return kind == 1   ? hipHostMalloc(&p, cls, hipHostMallocMapped | hipHostMallocCoherent)
+               : kind == 2 ? hipHostMalloc(&p, cls, hipHostMallocDefault)
+                           : hipMalloc(&p, cls);
     };
     hipError_t e = get();
     if (e != hipSuccess && c.cached) {   // give the cache back and retry once
@@ -169,37 +175,48 @@ void* cached_alloc(size_t bytes, bool pinned) {
         e = get();
     }
     if (e != hipSuccess) {
-        set_error("%s(%zu bytes) failed: %s", pinned ? "hipHostMalloc" : "hipMalloc", cls, hipGetErrorString(e));
+        set_error("%s(%zu bytes) failed: %s", kind ? "hipHostMalloc" : "hipMalloc", cls, hipGetErrorString(e));
         throw SfmError{SFM_ERR_OOM};
     }
-    c.live[p] = Block{key, cls, pinned};
+    c.live[p] = Block{key, cls, kind};
     return p;
 }
 
-void cached_free(void* p) {
-    if (!p) return;
+// false when p is not a block of the cache
+bool cached_free(void* p) {
+    if (!p) return true;
     MemCache& c = cache();
     std::lock_guard<std::mutex> lk(c.mu);
     auto it = c.live.find(p);
-    if (it == c.live.end()) return;
+    if (it == c.live.end()) return false;
     const Block b = it->second;
     c.live.erase(it);
     // reuse only under the stream the block was last used on
     const hipStream_t key = tl_stream ? tl_stream : b.key;
     if (key && c.streams.count(key) && c.cached + b.bytes <= MemCache::kCap) {
-        c.free[{key, b.pinned, b.bytes}].push_back(p);
+        c.free[{key, b.kind, b.bytes}].push_back(p);
         c.cached += b.bytes;
-        return;
+        return true;
     }
-    raw_free(p, b.pinned);
+    raw_free(p, b.kind);
+    return true;
 }
 
 }  // namespace
 
-void* dev_alloc(size_t bytes) { return cached_alloc(bytes, false); }
-void dev_free(void* p) { cached_free(p); }
-void* pinned_alloc(size_t bytes) { return cached_alloc(bytes, true); }
-void pinned_free(void* p) { cached_free(p); }
+void* dev_alloc(size_t bytes) { return cached_alloc(bytes, 0); }
+void dev_free(void* p) { (void)cached_free(p); }
+void* pinned_alloc(size_t bytes) { return cached_alloc(bytes, 1); }
+void pinned_free(void* p) { (void)cached_free(p); }
+void* host_alloc(size_t bytes) {
+    if (tl_stream) return cached_alloc(bytes, 2);
+    void* p = std::malloc(std::max<size_t>(bytes, 1));
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+void host_free(void* p) {
+    if (!cached_free(p)) std::free(p);
+}
 
 void dev_cache_release(hipStream_t s) {
     MemCache& c = cache();

@@ -358,6 +358,11 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
     }
     rows += kRowPad;  // guard rows for tile over-reads
     p->rows = rows;
+    PhaseTimer tm("upload_collection");
+    if (PhaseTimer::on()) {   // diagnostic: is anything still queued before this call?
+        SFM_HIP(hipStreamSynchronize(s));
+        tm.mark("presync");
+    }
     std::vector<uint8_t> staging((size_t)rows * 128, 128);  // pad rows -> a' = 0
     std::vector<int64_t> rstart(rows, 0);
     std::vector<int32_t> rvalid(rows, 0);
@@ -369,8 +374,12 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
             rvalid[p->row0[i] + r] = r < p->nrows[i];
         }
     }
+    tm.mark("stage");
     p->desc.alloc(staging.size());
+    tm.mark("alloc");
     p->desc.upload(staging.data(), staging.size(), s);
+    if (PhaseTimer::on()) SFM_HIP(hipStreamSynchronize(s));
+    tm.mark("copy");
     DBuf<int64_t> rs;
     DBuf<int32_t> rv;
     rs.alloc(rows);
@@ -386,7 +395,9 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
     p->img_n.upload(p->nrows.data(), n_img, s);
     p->img_row0.alloc(n_img);
     p->img_row0.upload(p->row0.data(), n_img, s);
+    tm.mark("rest");
     SFM_HIP(hipStreamSynchronize(s));  // staging buffers die here
+    tm.mark("sync");
 }
 
 CascTables casc_tables(sfm_match_plan* p) {

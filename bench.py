@@ -343,6 +343,78 @@ def bench_loop(ctx, n_img, cpu=True, cpu_images=16):
     return out
 
 
+def synth_fpairs(n_pairs, n_match, outlier_frac=0.3, seed=0xF3, w=1920, h=1080, f=1400.0):
+    """Synthetic putative matches for the geometric filter: per pair, n_match
+    projections of random points into two views (0.5 px noise), a fraction
+    replaced by uniform clutter in the second view."""
+    rng = np.random.default_rng(seed)
+    K = np.array([[f, 0, w / 2], [0, f, h / 2], [0, 0, 1.0]])
+    xs = []
+    for _ in range(n_pairs):
+        wv = rng.normal(0, 0.15, 3)
+        th = np.linalg.norm(wv)
+        k = wv / th
+        Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+        R = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+        t = np.array([-0.6, rng.normal(0, 0.1), rng.normal(0, 0.1)])
+        X = np.stack([rng.uniform(-3, 3, n_match), rng.uniform(-2, 2, n_match), rng.uniform(5, 12, n_match)], 1)
+        p1 = (K @ X.T).T
+        p2 = (K @ (R @ X.T + t[:, None])).T
+        u1 = p1[:, :2] / p1[:, 2:] + rng.normal(0, 0.5, (n_match, 2))
+        u2 = p2[:, :2] / p2[:, 2:] + rng.normal(0, 0.5, (n_match, 2))
+        out = rng.random(n_match) < outlier_frac
+        u2[out] = np.stack([rng.uniform(0, w, out.sum()), rng.uniform(0, h, out.sum())], 1)
+        xs.append(np.concatenate([u1, u2], 1))
+    return xs, [(w, h, w, h)] * n_pairs
+
+
+def bench_filter(ctx, n_pairs, n_match, cpu=True, cpu_pairs=32):
+    """sparseBuilder::filter()'s GeometricFilter_FMatrix_AC(4.0, 2048) over a
+    synthetic collection of putative pairs."""
+    xs, whs = synth_fpairs(n_pairs, n_match)
+    api.fmatrix_ac(ctx, xs[:8], whs[:8])   # warm-up (code object, caches)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    res = api.fmatrix_ac(ctx, xs, whs)
+    dt = time.perf_counter() - t0
+    iters = sum(r["iterations"] for r in res)
+    kept = sum(r["n_inliers"] > 0 for r in res)
+    out = {"metric": "geometric filter pairs/sec (F-matrix AC-RANSAC, 2048 iterations)", "value": n_pairs / dt,
+           "unit": "pairs/s", "seconds": dt, "pairs": n_pairs, "matches_per_pair": n_match,
+           "ransac_iterations_per_sec": iters / dt, "pairs_kept": kept,
+           "inliers": int(sum(r["n_inliers"] for r in res)),
+           "workload": f"{n_pairs} pairs x {n_match} putative matches (30% clutter), 1920x1080 views, "
+                       "GeometricFilter_FMatrix_AC(4.0, 2048) semantics (sparseBuilder.cpp:1179-1186); "
+                       "time includes upload, normalisation and download"}
+    log(f"filter: {n_pairs} pairs in {dt:.3f}s -> {n_pairs / dt:.0f} pairs/s ({iters / dt:.3g} RANSAC it/s), "
+        f"{kept} kept")
+    if cpu:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import _helpers as H   # oracle loader (test infrastructure: the CPU baseline only)
+            lib = H.oracle()
+            lib.orc_fmatrix_ac.restype = C.c_int
+            lib.orc_fmatrix_ac.argtypes = [C.c_int64, abi.i64p, abi.f64p, abi.i32p, C.POINTER(abi.FMatrixOpts),
+                                           C.POINTER(abi.FMatrixResult), abi.i32p, C.c_int32]
+            model, nth = host_cpu()
+            n = min(cpu_pairs, n_pairs)
+            off, xy, wh = api._fmatrix_inputs(xs[:n], whs[:n])
+            r = (abi.FMatrixResult * n)()
+            inl = np.zeros(int(off[-1]), np.int32)
+            t1 = time.perf_counter()
+            lib.orc_fmatrix_ac(n, abi.ptr(off, abi.i64p), abi.ptr(xy, abi.f64p), abi.ptr(wh, abi.i32p),
+                               C.byref(api.fmatrix_opts()), r, abi.ptr(inl, abi.i32p), nth)
+            cdt = time.perf_counter() - t1
+            out["cpu_baseline"] = {"value": n / cdt, "unit": "pairs/s", "cores": nth, "kind": "port",
+                                   "cpu_model": model,
+                                   "sample": f"the first {n} pairs of the same collection through the filter "
+                                             f"oracle (OpenMP over pairs, {nth} threads), {cdt:.1f} s wall"}
+            log(f"cpu baseline filter: {n} pairs in {cdt:.1f}s")
+        except Exception as ex:
+            log(f"cpu baseline filter unavailable: {ex}")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -356,6 +428,9 @@ def main():
     ap.add_argument("--no-snavely", action="store_true")
     ap.add_argument("--no-loop", action="store_true")
     ap.add_argument("--loop-images", type=int, default=300)
+    ap.add_argument("--no-filter", action="store_true")
+    ap.add_argument("--filter-pairs", type=int, default=2000)
+    ap.add_argument("--filter-matches", type=int, default=1000)
     # diagnostic: rank 0's shard of an N-way landmark partition on this one GPU,
     # with a no-op all-reduce (per-rank kernel times of the N-GPU run; the
     # solve itself is then not the global one, so the result is not a bench line)
@@ -616,6 +691,11 @@ def main():
     if world == 1 and rank == 0 and not args.no_loop and args.fake_world <= 1:
         loop = bench_loop(ctx, args.loop_images, cpu=not args.no_cpu_baseline)
 
+    # ---------------- geometric filter ----------------
+    filt = None
+    if world == 1 and rank == 0 and not args.no_filter and args.fake_world <= 1:
+        filt = bench_filter(ctx, args.filter_pairs, args.filter_matches, cpu=not args.no_cpu_baseline)
+
     cpu = None
     cpu_match = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -681,6 +761,7 @@ def main():
             "ba_snavely": snav,
             "ba_pcie_inclusive": pcie,
             "loop": loop,
+            "filter": filt,
         }
         print(json.dumps(out))
     plan.close()
