@@ -72,11 +72,9 @@ struct sfm_ba_plan {
     double last_ms[8] = {0};
     double schur_ms_total = 0;
     int64_t schur_launches = 0;
-    std::vector<hipEvent_t> ev;
     bool cur_is_a = true;
     ~sfm_ba_plan() {
         if (scal_h) pinned_free(scal_h);
-        for (auto e : ev) (void)hipEventDestroy(e);
     }
 };
 
@@ -312,8 +310,6 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         }
     }
     if (std::getenv("SFM_SCHUR_STAMPS")) pl->stamps.alloc(6 * std::max<size_t>(h.chunks.size(), 1));
-    pl->ev.resize(2);   // the Schur launch timing of steps 1 and 2
-    for (auto& e2 : pl->ev) SFM_HIP(hipEventCreate(&e2));
     tm.mark("alloc+upload");
     SFM_HIP(hipStreamSynchronize(s));
     // the observation staging goes back to the cache (the uploads are done)
@@ -401,7 +397,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     sfm_ba_iter pending{};
     pending.iteration = 0; pending.step_is_valid = 1; pending.step_is_successful = 1;
     int term = -1;
-    int ev_i = 0;
+    hipEvent_t* ev = ctx_events(ctx);   // the Schur launch timing of steps 1 and 2
     int last_iter = 0;
 
     auto finalize = [&](const sfm_ba_iter& cur, double gmax) -> int {
@@ -424,9 +420,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         const bool first = step_no == 0;
         const bool timed = step_no == 1 || step_no == 2;
         ++step_no;
-        if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i], s));
+        if (timed) SFM_HIP(hipEventRecord(ev[0], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
-        if (timed) SFM_HIP(hipEventRecord(pl->ev[ev_i + 1], s));
+        if (timed) SFM_HIP(hipEventRecord(ev[1], s));
         // dense S across ranks: each rank writes only the blocks its own
         // points touch, so the summed S of the last iteration is cleared first
         if (P.dense && ctx->world > 1)
@@ -467,9 +463,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             SFM_HIP(hipStreamSynchronize(s));
         }
         if (timed) {
-            SFM_HIP(hipEventSynchronize(pl->ev[ev_i + 1]));
+            SFM_HIP(hipEventSynchronize(ev[1]));
             float ms = 0.f;
-            SFM_HIP(hipEventElapsedTime(&ms, pl->ev[ev_i], pl->ev[ev_i + 1]));
+            SFM_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
             pl->schur_ms_total += ms;
             pl->schur_launches++;
             pl->last_ms[0] = ms;

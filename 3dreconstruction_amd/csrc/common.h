@@ -207,4 +207,16 @@ struct sfm_ctx {
     double* host_buf = nullptr;                  // pinned staging for host_allreduce
     size_t host_cap = 0;
     int cu_count = 0;
+    hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
 };
+
+namespace sfm {
+// the context's two timing events (created once, destroyed with the context)
+inline hipEvent_t* ctx_events(sfm_ctx* ctx) {
+    if (!ctx->ev[0]) {
+        SFM_HIP(hipEventCreate(&ctx->ev[0]));
+        SFM_HIP(hipEventCreate(&ctx->ev[1]));
+    }
+    return ctx->ev;
+}
+}  // namespace sfm

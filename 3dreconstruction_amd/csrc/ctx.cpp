@@ -326,6 +326,8 @@ extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         rccl_comm_destroy(ctx->comm);
         if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
+        for (hipEvent_t e : ctx->ev)
+            if (e) (void)hipEventDestroy(e);
         if (ctx->stream) {
             dev_cache_release(ctx->stream);
             (void)hipStreamDestroy(ctx->stream);
