@@ -525,6 +525,9 @@ __device__ __forceinline__ bool crow_valid(const ChunkDesc& cd, int t) { return 
 __device__ constexpr int kTi[15] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4};
 __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4};
 
+#ifndef SFM_SCHUR_WPE   // waves per SIMD the Schur kernel is compiled for
+#define SFM_SCHUR_WPE 2
+#endif
 #ifndef SFM_SCHUR4_SP   // points / observations per batch of the 64-row variant
 #define SFM_SCHUR4_SP 4
 #endif
@@ -540,7 +543,7 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 // point_scale_kernel computes) from the unscaled Jx it linearises anyway,
 // writes them to scaleE and uses them, instead of a separate pass.
 template <int CM, int NT, int SP = kSubPts, int SO = kSubObs, bool SE = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void schur_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WPE, SFM_SCHUR_WPE))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
     unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;

@@ -42,11 +42,11 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0):
+def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0, vis=0):
     lib = abi.load()
     cfg = abi.SynthBAConfig()
     cfg.camera_model = model
-    cfg.n_cam, cfg.k, cfg.vis_mode, cfg.n_intr = n_cam, k, 0, 1
+    cfg.n_cam, cfg.k, cfg.vis_mode, cfg.n_intr = n_cam, k, vis, 1
     cfg.n_pt, cfg.seed = n_pt, seed
     cfg.noise_px, cfg.outlier_frac = 0.5, 0.01
     cfg.perturb_rot, cfg.perturb_t, cfg.perturb_X, cfg.perturb_f = 0.01, 0.05, 0.05, 5.0
@@ -368,6 +368,39 @@ def synth_fpairs(n_pairs, n_match, outlier_frac=0.3, seed=0xF3, w=1920, h=1080, 
     return xs, [(w, h, w, h)] * n_pairs
 
 
+def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2):
+    """SURVEY §8(d)'s dense-S stress case: random-k visibility (vis_mode 1),
+    so every camera pair can share points, the reduced camera system is dense
+    (nF = 6 (n_cam - 1) + 4) and the general-point path plus the blocked dense
+    Cholesky (ba_bcr.hip dense_*) carry the solve.  C4's sizes."""
+    t0 = time.time()
+    sc = c4_scene(n_cam, n_pt, k=k, seed=0x5F3D0014, vis=1)
+    plan = api.BAPlan(ctx, sc["problem"], sc["extr"], sc["intr"], sc["X"])
+    t_plan = time.time() - t0
+    info = plan.info()
+    plan.run()   # warm-up
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    iters = 0
+    for _ in range(steps):
+        rc, summ = plan.run()
+        iters += summ.iterations
+    ctx.synchronize()
+    dt = time.perf_counter() - t1
+    plan.close()
+    nF = info.rcs_dim
+    out = {"metric": "BA LM-iters/sec, dense reduced camera system (random-k visibility)",
+           "value": iters / dt, "unit": "LM-iters/s", "ms_per_iteration": dt / max(iters, 1) * 1e3,
+           "lm_iterations_per_solve": summ.iterations, "rmse_initial": summ.rmse_initial,
+           "rmse_final": summ.rmse_final, "rcs_dim": nF, "dense": True,
+           "rcs_factor_flops_per_iteration": nF ** 3 / 3.0, "host_plan_seconds": t_plan,
+           "config": {"workload": f"{n_cam} cams / {n_pt} pts / {sc['n_obs']} obs, random k={k} visibility "
+                                  "(SURVEY §8(d) dense-S stress variant of C4), HuberLoss(4)"}}
+    log(f"BA dense-S: {iters} LM iterations in {dt:.3f}s -> {iters / dt:.1f} it/s, rcs {nF}, plan {t_plan:.1f}s, "
+        f"rmse {summ.rmse_initial:.4f}->{summ.rmse_final:.4f}")
+    return out
+
+
 def bench_filter(ctx, n_pairs, n_match, cpu=True, cpu_pairs=32):
     """sparseBuilder::filter()'s GeometricFilter_FMatrix_AC(4.0, 2048) over a
     synthetic collection of putative pairs."""
@@ -429,6 +462,7 @@ def main():
     ap.add_argument("--no-loop", action="store_true")
     ap.add_argument("--loop-images", type=int, default=300)
     ap.add_argument("--no-filter", action="store_true")
+    ap.add_argument("--no-dense", action="store_true")
     ap.add_argument("--filter-pairs", type=int, default=2000)
     ap.add_argument("--filter-matches", type=int, default=1000)
     # diagnostic: rank 0's shard of an N-way landmark partition on this one GPU,
@@ -691,6 +725,11 @@ def main():
     if world == 1 and rank == 0 and not args.no_loop and args.fake_world <= 1:
         loop = bench_loop(ctx, args.loop_images, cpu=not args.no_cpu_baseline)
 
+    # ---------------- dense-S stress case ----------------
+    dense_s = None
+    if world == 1 and rank == 0 and not args.no_dense and args.fake_world <= 1:
+        dense_s = bench_dense_s(ctx)
+
     # ---------------- geometric filter ----------------
     filt = None
     if world == 1 and rank == 0 and not args.no_filter and args.fake_world <= 1:
@@ -762,6 +801,7 @@ def main():
             "ba_pcie_inclusive": pcie,
             "loop": loop,
             "filter": filt,
+            "ba_dense_s": dense_s,
         }
         print(json.dumps(out))
     plan.close()
