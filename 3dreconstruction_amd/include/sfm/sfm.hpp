@@ -173,6 +173,16 @@ class sparseBuilder {
     }
     const sfm_sparse_match_stats& stats() const { return stats_; }
 
+    // filter() (:1025-1280) with its settings: sGeometricModel "f" ->
+    // GeometricFilter_FMatrix_AC(4.0, imax_iteration = 2048), no guided
+    // matching: matches.putative.bin -> matches.f.bin
+    void filter(double precision = 4.0, int max_iterations = 2048) {
+        sfm_fmatrix_opts o{precision, max_iterations, 0};
+        last_rc_ = sfm_sparse_filter(ctx_->get(), matches_dir_.c_str(), &o, &filter_stats_);
+        if (last_rc_ != SFM_OK) std::fprintf(stderr, "filter failed: %s\n", sfm_last_error());
+    }
+    const sfm_sparse_filter_stats& filterStats() const { return filter_stats_; }
+
     // in-memory regions: per view, n x 128 uint8 descriptors
     void setRegions(std::vector<std::vector<uint8_t>> regions) { regions_ = std::move(regions); }
     // exhaustivePairs(N) (:786)
@@ -221,6 +231,7 @@ class sparseBuilder {
     std::string matches_dir_;
     int last_rc_ = SFM_OK;
     sfm_sparse_match_stats stats_{};
+    sfm_sparse_filter_stats filter_stats_{};
     std::vector<std::vector<uint8_t>> regions_;
 };
 
