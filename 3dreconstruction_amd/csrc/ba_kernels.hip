@@ -889,7 +889,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
         SFM_STAMP(4)
         p0 = p1;
     }
-    // ---- write the negated tile (full symmetric 80x80) -----------------------
+    // ---- write the negated tile: its lower 16x16 tiles only (the gather reads
+    // upper blocks at their symmetric partner, FlatTerm modes), row-contiguous
     double* out = P.tiles + (size_t)c * kTileR * kTileR;
     if (NT == 4) out[kTileWRow * kTileR + lane] = -wacc;
 #pragma unroll
@@ -898,9 +899,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = 16 * ti + (lane >> 4) + 4 * r, col = 16 * tj + (lane & 15);
-            const double v = -acc[q][r];
-            out[row * kTileR + col] = v;
-            if (ti != tj) out[col * kTileR + row] = v;
+            out[row * kTileR + col] = -acc[q][r];
         }
     }
     // ---- point partials (fixed-order wave reduction) --------------------------
@@ -921,7 +920,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 // static gather-reduce: one wave per target block
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double term_value(const DevProblem& P, const FlatTerm& q, int r, int cc) {
-    return (double)q.sign * P.src[q.off + (int64_t)r * q.rs + cc];
+    // all three index forms computed and selected without branches, so the
+    // reduce loops keep a batch of term loads in flight
+    const int t = q.rs;   // kFlatSym: the origin's offset within the tile
+    const int R = t / kTileR + r, C = t % kTileR + cc;
+    const int64_t i_rows = q.off + (int64_t)r * q.rs + cc;
+    const int64_t i_trans = q.off + (int64_t)cc * kTileR + r;
+    const int64_t i_sym = q.off - t + (R >= C ? R * kTileR + C : C * kTileR + R);
+    const int64_t idx = q.mode == kFlatRows ? i_rows : q.mode == kFlatTrans ? i_trans : i_sym;
+    return (double)q.sign * P.src[idx];
 }
 
 __device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {

@@ -152,11 +152,26 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
                 const ReduceTerm& q = h.terms[k];
                 FlatTerm& f = ft[k];
                 f.sign = q.sign;
+                f.mode = kFlatRows;
                 switch (q.kind) {
-                    case kSrcTile:
-                        f.off = (int64_t)q.index * kTileR * kTileR + q.roff * kTileR + q.coff;
-                        f.rs = vec ? 1 : kTileR;
+                    case kSrcTile: {
+                        // slot blocks occupy disjoint tile rows, so a block of two
+                        // slots is wholly below or wholly above the diagonal
+                        const int64_t base = (int64_t)q.index * kTileR * kTileR;
+                        if (vec || q.roff > q.coff) {
+                            f.off = base + q.roff * kTileR + q.coff;
+                            f.rs = vec ? 1 : kTileR;
+                        } else if (q.roff < q.coff) {
+                            f.off = base + q.coff * kTileR + q.roff;
+                            f.rs = 1;
+                            f.mode = kFlatTrans;
+                        } else {   // rs = the origin's offset within the tile
+                            f.off = base + q.roff * kTileR + q.coff;
+                            f.rs = (int16_t)(q.roff * kTileR + q.coff);
+                            f.mode = kFlatSym;
+                        }
                         break;
+                    }
                     case kSrcU:
                         f.off = (int64_t)o_u + (int64_t)q.index * 100 + q.roff * 10 + q.coff;
                         f.rs = 10;

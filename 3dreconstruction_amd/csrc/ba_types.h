@@ -87,11 +87,20 @@ struct PTerm {
 enum : int32_t { kDstBand = 0, kDstArrow = 1, kDstCorner = 2, kDstRhs = 3, kDstBF = 4, kDstCnF = 5,
                  kDstDense = 6 };
 
-// ReduceTerm resolved against the contiguous [tiles | U | Ub | Ucn] buffer:
-// element (r, c) of the source block is src[off + r * rs + c].
+// ReduceTerm resolved against the contiguous [tiles | U | Ub | Ucn] buffer.
+// Chunk tiles hold only their lower 16x16 tiles (diagonal tiles whole), so a
+// tile block is read in one of three modes:
+//   kFlatRows  element (r, c) at src[off + r * rs + c]       (lower blocks, U, vectors)
+//   kFlatTrans element (r, c) at src[off + c * kTileR + r]   (upper blocks: the
+//              symmetric partner; off addresses the partner's origin)
+//   kFlatSym   element (r, c) of a diagonal slot block: tile position
+//              (R, C) = origin + (r, c) read at (max, min); off addresses
+//              the origin, rs holds its offset within the chunk tile
+enum : int16_t { kFlatRows = 0, kFlatTrans = 1, kFlatSym = 2 };
 struct FlatTerm {
     int64_t off;
-    int32_t rs;
+    int16_t rs;
+    int16_t mode;
     float sign;
 };
 
