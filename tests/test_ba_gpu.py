@@ -327,3 +327,29 @@ def test_no_observations(ctx):
     np.testing.assert_array_equal(e, e0)
     np.testing.assert_array_equal(i, i0)
     np.testing.assert_array_equal(x, x0)
+
+
+def test_memory_cache_across_contexts_and_shapes(ctx):
+    """Device / staging memory is cached per context stream (ctx.cpp): solves
+    of growing and shrinking problems interleaved on two contexts, and a
+    context destroyed in between, give the same bits as fresh solves."""
+    scenes = [H.Scene(12, 800, 4, seed=40), H.Scene(30, 5000, 6, seed=41), H.Scene(8, 200, 3, seed=42)]
+    ref = []
+    for sc in scenes:
+        e, i, x = sc.params()
+        rc, s = api.ba_solve(ctx, sc.problem(), e, i, x)
+        assert rc == 0
+        ref.append((s.final_cost, s.iterations, x.copy()))
+    c2 = api.Context(0)
+    for rep in range(2):
+        for k, sc in enumerate(scenes[::-1] + scenes):
+            idx = scenes.index(sc)
+            e, i, x = sc.params()
+            rc, s = api.ba_solve(c2 if (k + rep) % 2 else ctx, sc.problem(), e, i, x)
+            assert rc == 0
+            assert (s.final_cost, s.iterations) == ref[idx][:2]
+            np.testing.assert_array_equal(x, ref[idx][2])
+        if rep == 0:
+            c2.close()
+            c2 = api.Context(0)
+    c2.close()
