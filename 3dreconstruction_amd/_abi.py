@@ -26,6 +26,7 @@ SFM_TERM_FAILURE = 2
 
 SFM_CAM_PINHOLE = 0
 SFM_CAM_SNAVELY = 1
+SFM_CAM_RADIAL3 = 2
 
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1
@@ -213,6 +214,7 @@ SIGNATURES = [
     ("sfm_ba_plan_destroy", C.c_int, [C.c_void_p]),
     ("sfm_ba_plan_get_info", C.c_int, [C.c_void_p, C.POINTER(BAPlanInfo)]),
     ("sfm_ba_plan_get_trace", C.c_int, [C.c_void_p, C.POINTER(BAIter), C.c_int32, i32p]),
+    ("sfm_ba_intr_width", C.c_int, [C.c_int32]),
     ("sfm_ba_partition", C.c_int, [C.POINTER(BAProblem), C.c_int32, i64p, i64p]),
     ("sfm_ba_describe", C.c_int, [C.POINTER(BAProblem), C.c_int32, C.c_int32, C.POINTER(BAPlanShape)]),
     ("sfm_synth_ba", C.c_int, [C.POINTER(SynthBAConfig), i64p, i32p, f64p, i32p, f64p,

@@ -26,6 +26,7 @@ struct DevProblem {
     int32_t dense;                  // RCS stored dense (Sdense) rather than band + arrow
     int32_t tile_nt;    // 16-row MFMA tiles per chunk side: 4 (64 F rows) or 5 (76 + w row)
     int32_t cam_model;  // SFM_CAM_* residual model
+    int32_t iw;         // doubles per intrinsics block (4; RADIAL3 6)
     int64_t nb, nF;
     double huber_a, min_diag, max_diag;
     // shard data
@@ -68,9 +69,9 @@ struct DevProblem {
     double* scaleE;     // [3*n_spt]
     double* scaleF;     // [nF]
     double* tiles;      // [n_chunk][80][80]
-    double* U;          // [n_img][100]
-    double* Ub;         // [n_img][10]
-    double* Ucn;        // [n_img][10]
+    double* U;          // [n_img * kGramSeg][FW * FW], FW = 6 + iw
+    double* Ub;         // [n_img * kGramSeg][FW]
+    double* Ucn;        // [n_img * kGramSeg][FW]
     double* Sband;      // [ncam][D+1][36]
     double* Sarrow;     // [nintr][ncam][24]
     double* Scorner;    // [nintr][nintr][16]

@@ -37,6 +37,10 @@ constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+// doubles per intrinsics block of a residual model (RADIAL3: f, ppx, ppy, k1-k3)
+template <int CM>
+constexpr int kIW = CM == SFM_CAM_RADIAL3 ? 6 : 4;
+
 // 1/sqrt(d): hardware estimate + two Newton steps (full fp64 accuracy)
 // 1/d: hardware estimate + two Newton steps
 __device__ __forceinline__ double rcp_nr(double d) {
@@ -109,18 +113,22 @@ __global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __
 // (BundleAdjuster.h:40-65 model; ceres Corrector with rho'' <= 0: r and J
 // scaled by sqrt(rho'))
 // ---------------------------------------------------------------------------
-struct Lin {
+template <int IW>
+struct LinW {
     double f[2];
     double Jc[2][6];
-    double Ji[2][4];
+    double Ji[2][IW];
     double Jx[2][3];
     double half_rho;
     bool ok;
 };
+using Lin = LinW<4>;
+template <int CM>
+using LinT = LinW<kIW<CM>>;
 
 template <int CM, bool JC, bool JI, bool JX>
 __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, const double* X, double u0,
-                                          double u1, double huber_a, Lin& L) {
+                                          double u1, double huber_a, LinT<CM>& L) {
     double P[3];
     const double* u = cp.u;
     const double cr0 = u[1] * X[2] - u[2] * X[1], cr1 = u[2] * X[0] - u[0] * X[2],
@@ -137,9 +145,37 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
     // one reciprocal for the projection and its Jacobian (x = P0/P2 to 1 ulp)
     const double iz = 1.0 / P[2];
     double r0, r1;
-    // unscaled dr/dP (2x3) and dr/d(intrinsics) (2x4) of the model
-    double A[2][3], Ji[2][4];
-    if constexpr (CM == SFM_CAM_SNAVELY) {
+    // unscaled dr/dP (2x3) and dr/d(intrinsics) (2 x kIW) of the model
+    double A[2][3], Ji[2][kIW<CM>];
+    if constexpr (CM == SFM_CAM_RADIAL3) {
+        // OpenMVG ResidualErrorFunctor_Pinhole_Intrinsic_Radial_K3: (x, y) = P/P2,
+        // c = 1 + k1 r2 + k2 r2^2 + k3 r2^3, r = pp + f c (x, y) - obs;
+        // dr/dP = f [c I + D (x, y)(x, y)'] dp/dP with D = 2 (k1 + 2 k2 r2 + 3 k3 r2^2),
+        // dp/dP = 1/P2 [1 0 -x; 0 1 -y]
+        const double xu = P[0] * iz, yu = P[1] * iz;
+        const double r2 = xu * xu + yu * yu, r4 = r2 * r2, r6 = r4 * r2;
+        const double rc = 1.0 + in[3] * r2 + in[4] * r4 + in[5] * r6;
+        r0 = in[1] + in[0] * (xu * rc) - u0;
+        r1 = in[2] + in[0] * (yu * rc) - u1;
+        if (JC || JI || JX) {
+            const double dd = 2.0 * (in[3] + 2.0 * in[4] * r2 + 3.0 * in[5] * r4);
+            const double b01 = in[0] * dd * xu * yu;
+            const double B[2][2] = {{in[0] * (rc + dd * xu * xu), b01}, {b01, in[0] * (rc + dd * yu * yu)}};
+            const double pu[2] = {xu, yu};
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                A[r][0] = iz * B[r][0];
+                A[r][1] = iz * B[r][1];
+                A[r][2] = -iz * (B[r][0] * xu + B[r][1] * yu);
+                Ji[r][0] = pu[r] * rc;
+                Ji[r][1] = r == 0 ? 1.0 : 0.0;
+                Ji[r][2] = r == 1 ? 1.0 : 0.0;
+                Ji[r][3] = in[0] * pu[r] * r2;
+                Ji[r][4] = in[0] * pu[r] * r4;
+                Ji[r][5] = in[0] * pu[r] * r6;
+            }
+        }
+    } else if constexpr (CM == SFM_CAM_SNAVELY) {
         // SnavelyReprojectionError.h:31-47: p = -P/P2, d = 1 + r2 (l1 + l2 r2),
         // r = f d p - obs; dr/dP = f [d I + 2 (l1 + 2 l2 r2) p p'] dp/dP with
         // dp/dP = -1/P2 [1 0 xp; 0 1 yp]
@@ -194,7 +230,7 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
 #pragma unroll
             for (int r = 0; r < 2; ++r)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) L.Ji[r][k] = Ji[r][k] * sr;
+                for (int k = 0; k < kIW<CM>; ++k) L.Ji[r][k] = Ji[r][k] * sr;
         }
         // dP/dX = R; dP/dw = -Al [X]x Ar with Al = R (Rodrigues) or I (small
         // angle), so the left factor A Al is J_X itself or A.
@@ -262,23 +298,32 @@ __device__ __forceinline__ double wave_max(double v) {
 // waves add in fixed order.
 // ---------------------------------------------------------------------------
 namespace gram {
-// structurally nonzero entries of [J_c | J_i | f] rows 0 / 1 (index 0..10)
+// F columns of an image block: pose 6 | intrinsics kIW; index FW is f
+template <int CM>
+constexpr int FW = 6 + kIW<CM>;
+// structurally nonzero entries of [J_c | J_i | f] rows 0 / 1 (index 0..FW)
 // PINHOLE: J_i row 0 = [x s, 0, s, 0], row 1 = [0, y s, 0, s];
-// SNAVELY: J_i rows = [d, f r2, f r2^2, 0] p_r s (column 9 is never a parameter)
+// SNAVELY: J_i rows = [d, f r2, f r2^2, 0] p_r s (column 9 is never a parameter);
+// RADIAL3: J_i row 0 = [x c, 1, 0, f x r2, f x r4, f x r6] s, row 1 the same
+//          with y and (0, 1) at the principal point
 template <int CM>
-constexpr bool in0(int i) { return CM == SFM_CAM_SNAVELY ? i != 9 : (i < 6 || i == 6 || i == 8 || i == 10); }
+constexpr bool in0(int i) {
+    return CM == SFM_CAM_RADIAL3 ? i != 8 : CM == SFM_CAM_SNAVELY ? i != 9 : (i < 6 || i == 6 || i == 8 || i == 10);
+}
 template <int CM>
-constexpr bool in1(int i) { return CM == SFM_CAM_SNAVELY ? i != 9 : (i < 6 || i == 7 || i == 9 || i == 10); }
+constexpr bool in1(int i) {
+    return CM == SFM_CAM_RADIAL3 ? i != 7 : CM == SFM_CAM_SNAVELY ? i != 9 : (i < 6 || i == 7 || i == 9 || i == 10);
+}
 struct Slots {
-    int i[64], j[64], id[11][11], n;
+    int i[128], j[128], id[13][13], n;
 };
 template <int CM>
 constexpr Slots make_slots() {
     Slots t{};
     t.n = 0;
-    for (int a = 0; a < 11; ++a)
-        for (int b = 0; b < 11; ++b) t.id[a][b] = -1;
-    for (int a = 0; a < 11; ++a)
+    for (int a = 0; a < 13; ++a)
+        for (int b = 0; b < 13; ++b) t.id[a][b] = -1;
+    for (int a = 0; a <= FW<CM>; ++a)
         for (int b = 0; b <= a; ++b)
             if ((in0<CM>(a) && in0<CM>(b)) || (in1<CM>(a) && in1<CM>(b))) {
                 t.i[t.n] = a; t.j[t.n] = b;
@@ -291,9 +336,12 @@ template <int CM>
 struct SlotTable {
     static constexpr Slots kS = make_slots<CM>();
     static constexpr int kCost = kS.n;   // slot of the cost; later slots stay zero
+    static constexpr int kPasses = (kS.n + 1 + 63) / 64;   // 64 register sums per lane and pass
 };
 static_assert(SlotTable<SFM_CAM_PINHOLE>::kS.n == 62, "image Gram: 62 nonzero entries (pinhole)");
 static_assert(SlotTable<SFM_CAM_SNAVELY>::kS.n == 55, "image Gram: 55 nonzero entries (Snavely)");
+static_assert(SlotTable<SFM_CAM_RADIAL3>::kS.n == 90 && SlotTable<SFM_CAM_RADIAL3>::kPasses == 2,
+              "image Gram: 90 nonzero entries in two passes (RADIAL3)");
 
 __device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__double_as_longlong(v); }
 __device__ __forceinline__ unsigned hi32(double v) { return (unsigned)(__double_as_longlong(v) >> 32); }
@@ -342,23 +390,28 @@ __device__ __forceinline__ void reduce_scatter64(double (&v)[64], int lane) {
 #ifndef SFM_GRAM_WPE
 #define SFM_GRAM_WPE 2
 #endif
-template <int CM>
+// PASS: which 64 slots this launch sums (RADIAL3's 91 sums take two passes,
+// each re-linearising the image's observations; the other models one).
+template <int CM, int PASS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WPE, SFM_GRAM_WPE))) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const double* __restrict__ X) {
     using kT = gram::SlotTable<CM>;
+    constexpr int IW = kIW<CM>, FW = gram::FW<CM>, S0 = 64 * PASS;
+    constexpr bool kHasCost = kT::kCost >= S0 && kT::kCost < S0 + 64;
     const int img = blockIdx.x / kGramSeg, seg = blockIdx.x - kGramSeg * img;   // slice of the image
     const int a0 = P.img_obs_ptr[img], n = P.img_obs_ptr[img + 1] - a0;
     const int o0 = a0 + (int)((int64_t)n * seg / kGramSeg), o1 = a0 + (int)((int64_t)n * (seg + 1) / kGramSeg);
     const int colc = P.img_colc[img], coli = P.img_coli[img];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ CamPre scp;
-    __shared__ double sin_[4], ssc[10];
+    __shared__ double sin_[IW], ssc[FW];
     __shared__ double part[4][64], badw[4];
     if (threadIdx.x < sizeof(CamPre) / 8)
         reinterpret_cast<double*>(&scp)[threadIdx.x] = reinterpret_cast<const double*>(&cps[img])[threadIdx.x];
-    if (threadIdx.x >= 64 && threadIdx.x < 68) sin_[threadIdx.x - 64] = intr[4 * P.img_intr[img] + threadIdx.x - 64];
-    if (threadIdx.x >= 96 && threadIdx.x < 106) {
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + IW)
+        sin_[threadIdx.x - 64] = intr[IW * (size_t)P.img_intr[img] + threadIdx.x - 64];
+    if (threadIdx.x >= 96 && threadIdx.x < 96 + FW) {
         const int a = threadIdx.x - 96;
         ssc[a] = a < 6 ? (colc >= 0 ? P.scaleF[colc + a] : 0.0) : P.scaleF[coli + a - 6];
     }
@@ -396,17 +449,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         // 28 doubles live across the loop (register budget of 2 waves/SIMD)
         asm volatile("" ::: "memory");
         if (p_cur >= 0) {
-            Lin L;
+            LinT<CM> L;
             linearize<CM, true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
-            g[kT::kCost] += L.half_rho;
+            if constexpr (kHasCost) g[kT::kCost - S0] += L.half_rho;
             bad = fmax(bad, L.ok ? 0.0 : 1.0);
             // unscaled rows; the per-image column scales are applied to the sums
             auto r = [&](int q, int i) -> double {
-                return i < 6 ? L.Jc[q][i] : i < 10 ? L.Ji[q][i - 6] : L.f[q];
+                return i < 6 ? L.Jc[q][i] : i < FW ? L.Ji[q][i - 6] : L.f[q];
             };
 #pragma unroll
-            for (int s = 0; s < kT::kS.n; ++s) {
-                const int i = kT::kS.i[s], j = kT::kS.j[s];
+            for (int s = 0; s < 64; ++s) {
+                if (S0 + s >= kT::kS.n) break;
+                const int i = kT::kS.i[S0 + s], j = kT::kS.j[S0 + s];
                 if (gram::in0<CM>(i) && gram::in0<CM>(j)) g[s] = fma(r(0, i), r(0, j), g[s]);
                 if (gram::in1<CM>(i) && gram::in1<CM>(j)) g[s] = fma(r(1, i), r(1, j), g[s]);
             }
@@ -417,18 +471,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
     part[wave][lane] = g[0];
     if (lane == 0) badw[wave] = bad;
     __syncthreads();
-    auto tot = [&](int s) { return ((part[0][s] + part[1][s]) + part[2][s]) + part[3][s]; };
-    if (threadIdx.x < 100) {
-        const int i = threadIdx.x / 10, j = threadIdx.x % 10, s = kT::kS.id[i][j];
-        const double u = s >= 0 ? ssc[i] * ssc[j] * tot(s) : 0.0;
-        P.U[(size_t)blockIdx.x * 100 + threadIdx.x] = u;
-        if (i == j) P.Ucn[(size_t)blockIdx.x * 10 + i] = u;
+    // slot s of this pass (S0 <= s < S0 + 64) summed over the four waves
+    auto tot = [&](int s) { return ((part[0][s - S0] + part[1][s - S0]) + part[2][s - S0]) + part[3][s - S0]; };
+    auto mine = [&](int s) { return s >= S0 && s < S0 + 64; };
+    if (threadIdx.x < FW * FW) {
+        const int i = threadIdx.x / FW, j = threadIdx.x % FW, s = kT::kS.id[i][j];
+        if (s >= 0 ? mine(s) : PASS == 0) {
+            const double u = s >= 0 ? ssc[i] * ssc[j] * tot(s) : 0.0;
+            P.U[(size_t)blockIdx.x * (FW * FW) + threadIdx.x] = u;
+            if (i == j) P.Ucn[(size_t)blockIdx.x * FW + i] = u;
+        }
     }
-    if (threadIdx.x >= 128 && threadIdx.x < 138) {
-        const int i = threadIdx.x - 128;
-        P.Ub[(size_t)blockIdx.x * 10 + i] = ssc[i] * tot(kT::kS.id[10][i]);
+    if (threadIdx.x >= 160 && threadIdx.x < 160 + FW) {
+        const int i = threadIdx.x - 160, s = kT::kS.id[FW][i];
+        if (mine(s)) P.Ub[(size_t)blockIdx.x * FW + i] = ssc[i] * tot(s);
     }
-    if (threadIdx.x == 192) {
+    if (kHasCost && threadIdx.x == 192) {
         P.part_u[2 * (size_t)blockIdx.x] = tot(kT::kCost);
         P.part_u[2 * (size_t)blockIdx.x + 1] = fmax(fmax(badw[0], badw[1]), fmax(badw[2], badw[3]));
     }
@@ -441,23 +499,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
 template <int CM>
 __global__ __launch_bounds__(128) void gram_rescale_kernel(DevProblem P) {
     using kT = gram::SlotTable<CM>;
+    constexpr int FW = gram::FW<CM>;
     const int b = blockIdx.x, img = b / kGramSeg;
     const int colc = P.img_colc[img], coli = P.img_coli[img];
-    __shared__ double ssc[10];
-    if (threadIdx.x < 10) {
+    __shared__ double ssc[FW];
+    if (threadIdx.x < FW) {
         const int a = threadIdx.x;
         ssc[a] = a < 6 ? (colc >= 0 ? P.scaleF[colc + a] : 0.0) : P.scaleF[coli + a - 6];
     }
     __syncthreads();
-    if (threadIdx.x < 100) {
-        const int i = threadIdx.x / 10, j = threadIdx.x % 10, s = kT::kS.id[i][j];
-        const double u = s >= 0 ? ssc[i] * ssc[j] * P.U[(size_t)b * 100 + threadIdx.x] : 0.0;
-        P.U[(size_t)b * 100 + threadIdx.x] = u;
-        if (i == j) P.Ucn[(size_t)b * 10 + i] = u;
+    for (int e = threadIdx.x; e < FW * FW; e += 128) {
+        const int i = e / FW, j = e % FW, s = kT::kS.id[i][j];
+        const double u = s >= 0 ? ssc[i] * ssc[j] * P.U[(size_t)b * (FW * FW) + e] : 0.0;
+        P.U[(size_t)b * (FW * FW) + e] = u;
+        if (i == j) P.Ucn[(size_t)b * FW + i] = u;
     }
-    if (threadIdx.x >= 100 && threadIdx.x < 110) {
-        const int i = threadIdx.x - 100;
-        P.Ub[(size_t)b * 10 + i] = ssc[i] * P.Ub[(size_t)b * 10 + i];
+    if (threadIdx.x < FW) {
+        const int i = threadIdx.x;
+        P.Ub[(size_t)b * FW + i] = ssc[i] * P.Ub[(size_t)b * FW + i];
     }
 }
 
@@ -546,6 +605,7 @@ template <int CM, int NT, int SP = kSubPts, int SO = kSubObs, bool SE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WPE, SFM_SCHUR_WPE))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
+    static_assert(kIW<CM> == 4, "chunk tiles hold 4-wide intrinsics blocks");
     unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
     if (stamps) tprev = stamp();
 #define SFM_STAMP(k)                                      \
@@ -1302,11 +1362,10 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
         const int q = t - P.n_img;
         const int c0 = P.intr_col[q];
         // SNAVELY: the 4th double is not a parameter (not moved, not in the norms)
-        const int na = P.cam_model == SFM_CAM_SNAVELY ? 3 : 4;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            const double x = intr[4 * (size_t)q + a];
-            cand_intr[4 * (size_t)q + a] = (c0 >= 0 && a < na) ? col(x, (int64_t)c0 + a) : x;
+        const int iw = P.iw, na = P.cam_model == SFM_CAM_SNAVELY ? 3 : iw;
+        for (int a = 0; a < iw; ++a) {
+            const double x = intr[iw * (size_t)q + a];
+            cand_intr[iw * (size_t)q + a] = (c0 >= 0 && a < na) ? col(x, (int64_t)c0 + a) : x;
         }
     }
     wave_sum(v);
@@ -1336,6 +1395,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                                                          const double* __restrict__ intr_c,
                                                          const double* __restrict__ X,
                                                          double* __restrict__ Xc, double radius) {
+    static_assert(kIW<CM> == 4, "chunk points carry 4-wide intrinsics blocks");
     __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
     __shared__ double csy[kCamSlots][6];        // camera scaleF * yF (0 for a constant image)
     __shared__ double isy[kIntrSlots][12];      // intrinsics | candidate | scaleF * yF
@@ -1510,17 +1570,18 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
     const double Xp[3] = {X[3 * (size_t)k], X[3 * (size_t)k + 1], X[3 * (size_t)k + 2]};
     double sE[3];
     // observation o at x: loss-corrected Jacobians, unscaled
-    auto lin = [&](int o, Lin& L) {
+    constexpr int IW = kIW<CM>;
+    auto lin = [&](int o, LinT<CM>& L) {
         const int img = P.obs_img[o];
         const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-        linearize<CM, true, true, true>(cps[img], intr + 4 * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
+        linearize<CM, true, true, true>(cps[img], intr + IW * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
     };
     if constexpr (SE) {
         // the solve's first pass: Ceres' Jacobi point scales from the column
         // norms of the unscaled point Jacobian
         double cn[3] = {0.0, 0.0, 0.0};
         for (int o = o0 + lane; o < o1; o += 64) {
-            Lin L;
+            LinT<CM> L;
             lin(o, L);
 #pragma unroll
             for (int a = 0; a < 3; ++a) cn[a] += L.Jx[0][a] * L.Jx[0][a] + L.Jx[1][a] * L.Jx[1][a];
@@ -1536,7 +1597,7 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
     // V = Jx' Jx, g_E = Jx' f over the point (scaled), summed by the wave
     double v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};   // V00 V10 V11 V20 V21 V22 | b0 b1 b2
     for (int o = o0 + lane; o < o1; o += 64) {
-        Lin L;
+        LinT<CM> L;
         lin(o, L);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -1580,11 +1641,11 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
         const int o = base + lane;
         const bool act = o < o1;
         int cb = 0xffff, ib = -1;
-        double zi[12];
+        double zi[3 * IW];
 #pragma unroll
-        for (int e = 0; e < 12; ++e) zi[e] = 0.0;
+        for (int e = 0; e < 3 * IW; ++e) zi[e] = 0.0;
         if (act) {
-            Lin L;
+            LinT<CM> L;
             lin(o, L);
             const int img = P.obs_img[o];
             const int slot = P.obs_slot[o];
@@ -1608,9 +1669,9 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
                         zc[lane * kZStage + 3 * r + a] = (L.Jc[0][r] * s) * M[0][a] + (L.Jc[1][r] * s) * M[1][a];
                 }
             }
-            const int ni = CM == SFM_CAM_SNAVELY ? 3 : 4;
+            const int ni = CM == SFM_CAM_SNAVELY ? 3 : IW;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < IW; ++r) {
                 if (r >= ni) continue;
                 const double s = P.scaleF[coli + r];
 #pragma unroll
@@ -1640,14 +1701,14 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
             const int src = __builtin_ctzll(pend);
             const int j = __shfl(ib, src);
             const bool mine = act && ib == j;
-            double v[12];
+            double v[3 * IW];
 #pragma unroll
-            for (int e = 0; e < 12; ++e) v[e] = mine ? zi[e] : 0.0;
+            for (int e = 0; e < 3 * IW; ++e) v[e] = mine ? zi[e] : 0.0;
             wave_sum(v);
-            const int nz = 3 * (CM == SFM_CAM_SNAVELY ? 3 : 4);
+            const int nz = 3 * (CM == SFM_CAM_SNAVELY ? 3 : IW);
             double mine_v = 0.0;   // v[lane] without a dynamically indexed register array
 #pragma unroll
-            for (int e = 0; e < 12; ++e) mine_v = lane == e ? v[e] : mine_v;
+            for (int e = 0; e < 3 * IW; ++e) mine_v = lane == e ? v[e] : mine_v;
             if (lane < nz) Zl[P.gblk_z[b0 + j] + lane] += mine_v;
             pend &= ~__ballot(mine);
         }
@@ -1766,6 +1827,7 @@ template <int CM>
 __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr, const CamPre* __restrict__ cps_c,
     const double* __restrict__ intr_c, const double* __restrict__ X, double* __restrict__ Xc, double radius) {
+    constexpr int IW = kIW<CM>;
     const int tid = threadIdx.x, g = blockIdx.x * kGStepThreads + tid;
     const double inv_radius = 1.0 / radius;
     double acc[3] = {0.0, 0.0, 0.0};
@@ -1781,17 +1843,17 @@ __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
             const int img = P.obs_img[o];
             const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
             const int colc = P.img_colc[img], coli = P.img_coli[img];
-            Lin L;
-            linearize<CM, true, true, true>(cps[img], intr + 4 * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
+            LinT<CM> L;
+            linearize<CM, true, true, true>(cps[img], intr + IW * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 double q = 0.0;
                 if (colc >= 0)
 #pragma unroll
                     for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * (P.scaleF[colc + a] * P.yF[colc + a]);
-                const int ni = CM == SFM_CAM_SNAVELY ? 3 : 4;
+                const int ni = CM == SFM_CAM_SNAVELY ? 3 : IW;
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < IW; ++a)
                     if (a < ni) q += L.Ji[r][a] * (P.scaleF[coli + a] * P.yF[coli + a]);
                 const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
                 const double fr = L.f[r];
@@ -1838,8 +1900,8 @@ __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
         for (int o = o0; o < o1; ++o) {
             const int img = P.obs_img[o];
             const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-            Lin C;
-            linearize<CM, false, false, false>(cps_c[img], intr_c + 4 * (size_t)P.img_intr[img], xc, uv.x, uv.y,
+            LinT<CM> C;
+            linearize<CM, false, false, false>(cps_c[img], intr_c + IW * (size_t)P.img_intr[img], xc, uv.x, uv.y,
                                                P.huber_a, C);
             acc[1] += C.half_rho;
             if (!C.ok) cbad = 1.0;
@@ -1932,6 +1994,8 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
 }
 
 // the residual model is a template parameter of every kernel that linearises
+// (chunk kernels: the 4-wide intrinsics models only; the planner sends
+// RADIAL3 points through the general path)
 #define SFM_BY_MODEL(P, CALL)                                  \
     do {                                                       \
         if ((P).cam_model == SFM_CAM_SNAVELY) {                \
@@ -1942,17 +2006,33 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
             CALL;                                              \
         }                                                      \
     } while (0)
+#define SFM_BY_MODEL_ALL(P, CALL)                              \
+    do {                                                       \
+        if ((P).cam_model == SFM_CAM_RADIAL3) {                \
+            constexpr int CM = SFM_CAM_RADIAL3;                \
+            CALL;                                              \
+        } else if ((P).cam_model == SFM_CAM_SNAVELY) {         \
+            constexpr int CM = SFM_CAM_SNAVELY;                \
+            CALL;                                              \
+        } else {                                               \
+            constexpr int CM = SFM_CAM_PINHOLE;                \
+            CALL;                                              \
+        }                                                      \
+    } while (0)
 
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                    hipStream_t s) {
-    SFM_BY_MODEL(P, hipLaunchKernelGGL(image_gram_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp,
-                                       intr, X));
+    SFM_BY_MODEL_ALL(P, {
+        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp, intr, X);
+        if constexpr (gram::SlotTable<CM>::kPasses > 1)
+            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp, intr, X);
+    });
     SFM_HIP(hipGetLastError());
 }
 
 void ba_gram_rescale(const DevProblem& P, hipStream_t s) {
     if (P.n_img <= 0) return;
-    SFM_BY_MODEL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(128), 0, s, P));
+    SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(128), 0, s, P));
     SFM_HIP(hipGetLastError());
 }
 
@@ -1974,14 +2054,14 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
     if (P.n_gpt > 0) {
         const size_t lds = (64 * kZStage + (size_t)P.gz_max) * sizeof(double);
         if (scale_e)
-            SFM_BY_MODEL(P, {
+            SFM_BY_MODEL_ALL(P, {
                 if (lds > 64 * 1024)
                     SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, true>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL((zpoint_kernel<CM, true>), dim3(P.n_gpt), dim3(64), lds, s, P, cp, intr, X, radius);
             });
         else
-            SFM_BY_MODEL(P, {
+            SFM_BY_MODEL_ALL(P, {
                 if (lds > 64 * 1024)
                     SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, false>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2081,7 +2161,7 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
     }
     if (P.n_gpt > 0) {
         const int nb = (P.n_gpt + kGStepThreads - 1) / kGStepThreads;
-        SFM_BY_MODEL(P, hipLaunchKernelGGL(step_general_kernel<CM>, dim3(nb), dim3(kGStepThreads), 0, s, P, cp, intr,
+        SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(step_general_kernel<CM>, dim3(nb), dim3(kGStepThreads), 0, s, P, cp, intr,
                                            cp_cand, intr_cand, X, X_cand, radius));
         SFM_HIP(hipGetLastError());
     }

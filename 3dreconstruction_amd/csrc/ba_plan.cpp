@@ -198,8 +198,9 @@ void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
         if (im[i]) iu[P.img_intr[i]] = 1;
     for (int q = 0; q < P.n_intr; ++q)
         if (iu[q]) { pl.intr_blk[q] = pl.nintr++; pl.blk_intr.push_back(q); }
+    pl.iw = sfm_ba_intr_width(P.camera_model);
     pl.nb = 6LL * pl.ncam;
-    pl.na = 4LL * pl.nintr;
+    pl.na = (int64_t)pl.iw * pl.nintr;
     pl.nF = pl.nb + pl.na;
     pl.nFB = pl.ncam + pl.nintr;
     pl.img_colc.assign(P.n_img, -1);
@@ -208,7 +209,7 @@ void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
     for (int i = 0; i < P.n_img; ++i) {
         if (pl.cam_blk[i] >= 0) pl.img_colc[i] = 6 * pl.cam_blk[i];
         const int q = pl.intr_blk[P.img_intr[i]];
-        if (q >= 0) pl.img_coli[i] = (int32_t)(pl.nb + 4 * q);
+        if (q >= 0) pl.img_coli[i] = (int32_t)(pl.nb + (int64_t)pl.iw * q);
     }
 }
 
@@ -264,7 +265,7 @@ namespace {
 // intrinsics and repeated (point, image) observations).
 bool chunkable(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t p) {
     const int64_t o0 = P.pt_offsets[p], o1 = P.pt_offsets[p + 1];
-    if (o1 - o0 > kSubObs) return false;
+    if (o1 - o0 > kSubObs || pl.iw != 4) return false;   // chunk tiles: 4-wide intrinsics blocks
     int nc = 0, ni = 0;
     int32_t intrs[kIntrSlots];
     for (int64_t o = o0; o < o1; ++o) {
@@ -313,8 +314,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         SFM_REQUIRE(P.img_intr[i] >= 0 && P.img_intr[i] < P.n_intr, SFM_ERR_INVALID_ARG,
                     "image %d references intrinsics %d", i, P.img_intr[i]);
     SFM_REQUIRE(P.const_img >= -1 && P.const_img < P.n_img, SFM_ERR_INVALID_ARG, "bad const_img");
-    SFM_REQUIRE(P.camera_model == SFM_CAM_PINHOLE || P.camera_model == SFM_CAM_SNAVELY, SFM_ERR_INVALID_ARG,
-                "unknown camera_model %d", P.camera_model);
+    SFM_REQUIRE(sfm_ba_intr_width(P.camera_model) > 0, SFM_ERR_INVALID_ARG, "unknown camera_model %d",
+                P.camera_model);
 
     PhaseTimer tm("build_plan");
     tm.mark("validate");
@@ -325,7 +326,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // RCS storage and solver, identical on every rank: the block-banded form
     // (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
     // and a few intrinsics blocks, else dense (blocked Cholesky, ba_dense.hip)
-    pl.dense = !(pl.D <= kBandMaxD && 1 + 4 * pl.nintr <= 32) || std::getenv("SFM_BA_DENSE") != nullptr;
+    // (the band solver's arrow holds 4-wide intrinsics blocks: RADIAL3 is dense)
+    pl.dense = !(pl.D <= kBandMaxD && 1 + 4 * pl.nintr <= 32) || pl.iw != 4 || std::getenv("SFM_BA_DENSE") != nullptr;
     if (pl.dense) {
         SFM_REQUIRE(pl.nF <= 40000, SFM_ERR_UNSUPPORTED, "dense reduced camera system of %lld columns",
                     (long long)pl.nF);
@@ -627,7 +629,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             for (int32_t c : cols) {
                 pl.gblk_col.push_back(c);
                 pl.gblk_z.push_back(z);
-                z += 3 * (c < pl.nb ? 6 : 4);
+                z += 3 * (c < pl.nb ? 6 : pl.iw);
             }
             pl.gblk_off[g + 1] = (int32_t)pl.gblk_col.size();
             pl.gz_off[g + 1] = pl.gz_off[g] + z + 3;   // + w = L^-1 g_E
@@ -679,10 +681,10 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // bit-reproducible.
     const int32_t nFB = pl.nFB;
     auto fb_of_col = [&](int64_t col) -> int32_t {
-        return col < pl.nb ? (int32_t)(col / 6) : (int32_t)(pl.ncam + (col - pl.nb) / 4);
+        return col < pl.nb ? (int32_t)(col / 6) : (int32_t)(pl.ncam + (col - pl.nb) / pl.iw);
     };
-    auto col_of_fb = [&](int32_t b) -> int64_t { return b < pl.ncam ? 6LL * b : pl.nb + 4LL * (b - pl.ncam); };
-    auto size_of_fb = [&](int32_t b) { return b < pl.ncam ? 6 : 4; };
+    auto col_of_fb = [&](int32_t b) -> int64_t { return b < pl.ncam ? 6LL * b : pl.nb + (int64_t)pl.iw * (b - pl.ncam); };
+    auto size_of_fb = [&](int32_t b) { return b < pl.ncam ? 6 : pl.iw; };
     std::vector<std::pair<int64_t, ReduceTerm>> mterms, vterms;
     std::vector<std::pair<int64_t, PTerm>> mprod, vprod;
     // image Gram blocks (kGramSeg partial slices per image)
@@ -861,6 +863,14 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
 }
 
 }  // namespace sfm
+
+extern "C" int sfm_ba_intr_width(int32_t camera_model) {
+    switch (camera_model) {
+        case SFM_CAM_PINHOLE: case SFM_CAM_SNAVELY: return 4;
+        case SFM_CAM_RADIAL3: return 6;
+        default: return 0;
+    }
+}
 
 extern "C" int sfm_ba_partition(const sfm_ba_problem* prob, int32_t world_size, int64_t* order,
                                 int64_t* bounds) {

@@ -22,6 +22,7 @@ struct BAHostPlan {
     std::vector<int32_t> img_intr;
     int32_t ncam = 0, nintr = 0, D = 0;
     int64_t nb = 0, na = 0, nF = 0;
+    int32_t iw = 4;                  // doubles per intrinsics block (RADIAL3: 6)
     std::vector<int64_t> order, bounds;  // sorted points / rank ranges
     int32_t rank = 0, world = 1;
 

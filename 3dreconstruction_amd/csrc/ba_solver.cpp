@@ -109,7 +109,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     {
         std::vector<int32_t> ic(std::max(prob.n_intr, 1), -1);
         for (int q = 0; q < prob.n_intr; ++q)
-            if (h.intr_blk[q] >= 0) ic[q] = (int32_t)(h.nb + 4 * (int64_t)h.intr_blk[q]);
+            if (h.intr_blk[q] >= 0) ic[q] = (int32_t)(h.nb + (int64_t)h.iw * h.intr_blk[q]);
         up(pl->intr_col, ic, s);
     }
     up(pl->img_intr, h.img_intr, s);
@@ -128,7 +128,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->X0, xs, s);
     pl->Xa.alloc(xs.size());
     pl->Xb.alloc(xs.size());
-    std::vector<double> e(extr, extr + 6 * (size_t)prob.n_img), in(intr, intr + 4 * (size_t)prob.n_intr);
+    std::vector<double> e(extr, extr + 6 * (size_t)prob.n_img), in(intr, intr + (size_t)h.iw * prob.n_intr);
     up(pl->extr0, e, s);
     up(pl->intr0, in, s);
     pl->ea.alloc(e.size()); pl->eb.alloc(e.size());
@@ -140,9 +140,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     // per-chunk Schur tiles and per-image Gram slices share one buffer so the
     // reduction terms address every source with a single offset
     const size_t n_tiles = std::max<size_t>(h.chunks.size(), 1) * kTileR * kTileR;
-    const size_t o_u = n_tiles, o_ub = o_u + 100 * (size_t)prob.n_img * kGramSeg,
-                 o_ucn = o_ub + 10 * (size_t)prob.n_img * kGramSeg,
-                 n_gram = o_ucn + 10 * (size_t)prob.n_img * kGramSeg;
+    const size_t fw = 6 + (size_t)h.iw;   // F columns of an image block
+    const size_t o_u = n_tiles, o_ub = o_u + fw * fw * (size_t)prob.n_img * kGramSeg,
+                 o_ucn = o_ub + fw * (size_t)prob.n_img * kGramSeg,
+                 n_gram = o_ucn + fw * (size_t)prob.n_img * kGramSeg;
     pl->gram.alloc(n_gram);
     {
         std::vector<FlatTerm> ft(std::max<size_t>(h.terms.size(), 1));
@@ -173,15 +174,15 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
                         break;
                     }
                     case kSrcU:
-                        f.off = (int64_t)o_u + (int64_t)q.index * 100 + q.roff * 10 + q.coff;
-                        f.rs = 10;
+                        f.off = (int64_t)o_u + (int64_t)(q.index * fw * fw + q.roff * fw + q.coff);
+                        f.rs = (int16_t)fw;
                         break;
                     case kSrcUb:
-                        f.off = (int64_t)o_ub + (int64_t)q.index * 10 + q.roff;
+                        f.off = (int64_t)o_ub + (int64_t)(q.index * fw + q.roff);
                         f.rs = 1;
                         break;
                     default:
-                        f.off = (int64_t)o_ucn + (int64_t)q.index * 10 + q.roff;
+                        f.off = (int64_t)o_ucn + (int64_t)(q.index * fw + q.roff);
                         f.rs = 1;
                         break;
                 }
@@ -227,6 +228,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.nb = h.nb; P.nF = h.nF;
     P.huber_a = prob.huber_a;
     P.cam_model = prob.camera_model;
+    P.iw = h.iw;
     P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p;
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
     P.img_obs_ptr = pl->img_obs_ptr.p;
@@ -373,7 +375,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
 
     // working buffers: a = current point, b = candidate
     IterState S{pl->Xa.p, pl->Xb.p, pl->ea.p, pl->eb.p, pl->ia.p, pl->ib.p, pl->cpa.p, pl->cpb.p};
-    const size_t ne = 6 * (size_t)h.n_img, ni = 4 * (size_t)h.n_intr, nx = 3 * (size_t)h.n_spt;
+    const size_t ne = 6 * (size_t)h.n_img, ni = (size_t)h.iw * h.n_intr, nx = 3 * (size_t)h.n_spt;
     if (nx) SFM_HIP(hipMemcpyAsync(S.X, pl->X0.p, nx * 8, hipMemcpyDeviceToDevice, s));
     SFM_HIP(hipMemcpyAsync(S.e, pl->extr0.p, ne * 8, hipMemcpyDeviceToDevice, s));
     SFM_HIP(hipMemcpyAsync(S.in, pl->intr0.p, ni * 8, hipMemcpyDeviceToDevice, s));
@@ -594,7 +596,7 @@ void download(sfm_ba_plan* pl, double* extr, double* intr, double* X) {
     const double* in = pl->cur_is_a ? pl->ia.p : pl->ib.p;
     const double* x = pl->cur_is_a ? pl->Xa.p : pl->Xb.p;
     if (extr) SFM_HIP(hipMemcpyAsync(extr, e, 6 * (size_t)h.n_img * 8, hipMemcpyDeviceToHost, s));
-    if (intr) SFM_HIP(hipMemcpyAsync(intr, in, 4 * (size_t)h.n_intr * 8, hipMemcpyDeviceToHost, s));
+    if (intr) SFM_HIP(hipMemcpyAsync(intr, in, (size_t)h.iw * h.n_intr * 8, hipMemcpyDeviceToHost, s));
     std::vector<double> xs(3 * (size_t)h.n_spt);
     if (X && h.n_spt) SFM_HIP(hipMemcpyAsync(xs.data(), x, xs.size() * 8, hipMemcpyDeviceToHost, s));
     SFM_HIP(hipStreamSynchronize(s));

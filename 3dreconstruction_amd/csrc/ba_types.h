@@ -11,7 +11,7 @@
 //   RCS      : Sband[ncam][D+1][6][6] (block (i,i-d)), Sarrow[nintr][ncam][4][6],
 //              Scorner[nintr][nintr][4][4], rhs[nF], bF[nF], cnF[nF]
 //   chunk slab: tiles[n_chunk][80][80] (-Z Z^T, row 79 = -Z w)
-//   image slab: Uimg[n_img][10][10], Ub[n_img][10], Ucn[n_img][10]
+//   image slab: Uimg[n_img][FW][FW], Ub[n_img][FW], Ucn[n_img][FW] (FW = 6 + intrinsics width)
 #pragma once
 #include <cstdint>
 

@@ -74,8 +74,22 @@ void project(int model, const double* intr, const double* extr, const double* X,
         uv[1] = intr[0] * d * yp;
         return;
     }
+    if (model == SFM_CAM_RADIAL3) {   // OpenMVG Pinhole_Intrinsic_Radial_K3 (f, ppx, ppy, k1, k2, k3)
+        const double x = P[0] / P[2], y = P[1] / P[2];
+        const double r2 = x * x + y * y;
+        const double c = 1.0 + intr[3] * r2 + intr[4] * r2 * r2 + intr[5] * r2 * r2 * r2;
+        uv[0] = intr[1] + intr[0] * (x * c);
+        uv[1] = intr[2] + intr[0] * (y * c);
+        return;
+    }
     uv[0] = intr[0] * (P[0] / P[2]) + intr[2];
     uv[1] = intr[1] * (P[1] / P[2]) + intr[3];
+}
+
+// doubles per intrinsics block (as sfm_ba_intr_width; this file also builds
+// into the oracle library, which has no planner)
+int synth_intr_width(int model) {
+    return model == SFM_CAM_RADIAL3 ? 6 : (model == SFM_CAM_PINHOLE || model == SFM_CAM_SNAVELY) ? 4 : 0;
 }
 
 enum : uint64_t { kStreamCam = 1, kStreamPt = 2, kStreamIntr = 3, kStreamLm = 4,
@@ -88,23 +102,28 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
                             double* extr, double* intr, double* X, double* gt_extr,
                             double* gt_intr, double* gt_X, int64_t* n_obs_out) {
     if (!cfg || cfg->n_cam < 1 || cfg->n_pt < 0 || cfg->k < 1 || cfg->k > cfg->n_cam ||
-        cfg->n_intr < 1 || cfg->n_intr > cfg->n_cam ||
-        (cfg->camera_model != SFM_CAM_PINHOLE && cfg->camera_model != SFM_CAM_SNAVELY))
+        cfg->n_intr < 1 || cfg->n_intr > cfg->n_cam || synth_intr_width(cfg->camera_model) == 0)
         return SFM_ERR_INVALID_ARG;
-    const int model = cfg->camera_model;
+    const int model = cfg->camera_model, iw = synth_intr_width(model);
     const int64_t n_obs = cfg->n_pt * cfg->k;
     if (n_obs_out) *n_obs_out = n_obs;
     if (!pt_offsets) return SFM_OK;  // size query
 
     const int nc = cfg->n_cam, k = cfg->k;
     const uint64_t seed = cfg->seed;
-    std::vector<double> ge(6 * (size_t)nc), gi(4 * (size_t)cfg->n_intr);
+    std::vector<double> ge(6 * (size_t)nc), gi((size_t)iw * cfg->n_intr);
     for (int q = 0; q < cfg->n_intr; ++q) {
         Rng r(entity_seed(seed, kStreamIntr, q));
         const double df = q == 0 ? 0.0 : 40.0 * (r.uni() - 0.5);
         if (model == SFM_CAM_SNAVELY) {   // BAL-like: f, l1, l2 (principal point at 0)
             gi[4 * q + 0] = 1000.0 + df; gi[4 * q + 1] = -0.08;
             gi[4 * q + 2] = 0.02;         gi[4 * q + 3] = 0.0;
+            continue;
+        }
+        if (model == SFM_CAM_RADIAL3) {
+            double* g = &gi[6 * (size_t)q];
+            g[0] = 2905.88 + df; g[1] = 1416.0; g[2] = 1064.0;
+            g[3] = -0.05;        g[4] = 0.01;   g[5] = -0.002;
             continue;
         }
         gi[4 * q + 0] = 2905.88 + df; gi[4 * q + 1] = 2905.88 + df;
@@ -162,7 +181,7 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
         for (int a = 0; a < k; ++a) {
             const int c = cams[a];
             double uv[2];
-            project(model, &gi[4 * (size_t)img_intr[c]], &ge[6 * (size_t)c], Xg, uv);
+            project(model, &gi[(size_t)iw * img_intr[c]], &ge[6 * (size_t)c], Xg, uv);
             uv[0] += cfg->noise_px * r.gauss();
             uv[1] += cfg->noise_px * r.gauss();
             if (r.uni() < cfg->outlier_frac) {
@@ -192,10 +211,14 @@ extern "C" int sfm_synth_ba(const sfm_synth_ba_config* cfg, int64_t* pt_offsets,
     }
     for (int q = 0; q < cfg->n_intr; ++q) {
         Rng r(entity_seed(seed ^ 0xA5A5ULL, kStreamIntr, q));
-        for (int a = 0; a < 4; ++a) {
-            const double g = gi[4 * (size_t)q + a];
-            if (gt_intr) gt_intr[4 * (size_t)q + a] = g;
-            if (model == SFM_CAM_SNAVELY)   // f by perturb_f, l1 / l2 by a proportional small amount
+        for (int a = 0; a < iw; ++a) {
+            const double g = gi[(size_t)iw * q + a];
+            if (gt_intr) gt_intr[(size_t)iw * q + a] = g;
+            if (model == SFM_CAM_RADIAL3)   // f by perturb_f, k1..k3 by a small relative amount
+                intr[6 * (size_t)q + a] = a == 0 ? g + cfg->perturb_f * r.gauss()
+                                        : a >= 3 ? g * (1.0 + 0.02 * r.gauss())
+                                                 : g;
+            else if (model == SFM_CAM_SNAVELY)   // f by perturb_f, l1 / l2 by a proportional small amount
                 intr[4 * (size_t)q + a] = a == 0 ? g + cfg->perturb_f * r.gauss()
                                         : a < 3  ? g + 2e-3 * cfg->perturb_f / 5.0 * r.gauss() / (a == 1 ? 1.0 : 4.0)
                                                  : g;

@@ -58,7 +58,7 @@ def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0, vis=0):
     sc = {
         "pt_offsets": np.zeros(n_pt + 1, np.int64), "obs_img": np.zeros(no, np.int32),
         "obs_uv": np.zeros(2 * no), "img_intr": np.zeros(n_cam, np.int32),
-        "extr": np.zeros(6 * n_cam), "intr": np.zeros(4), "X": np.zeros(3 * n_pt),
+        "extr": np.zeros(6 * n_cam), "intr": np.zeros(lib.sfm_ba_intr_width(model)), "X": np.zeros(3 * n_pt),
     }
     p = abi.ptr
     rc = lib.sfm_synth_ba(C.byref(cfg), p(sc["pt_offsets"], abi.i64p), p(sc["obs_img"], abi.i32p),
@@ -368,13 +368,17 @@ def synth_fpairs(n_pairs, n_match, outlier_frac=0.3, seed=0xF3, w=1920, h=1080, 
     return xs, [(w, h, w, h)] * n_pairs
 
 
-def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2):
+def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2, model=0):
     """SURVEY §8(d)'s dense-S stress case: random-k visibility (vis_mode 1),
     so every camera pair can share points, the reduced camera system is dense
     (nF = 6 (n_cam - 1) + 4) and the general-point path plus the blocked dense
-    Cholesky (ba_bcr.hip dense_*) carry the solve.  C4's sizes."""
+    Cholesky (ba_bcr.hip dense_*) carry the solve.  C4's sizes.
+    model = SFM_CAM_RADIAL3: C4's banded geometry under OpenMVG's
+    PINHOLE_CAMERA_RADIAL3 residual, which the planner
+    always sends through the general-point path and the dense RCS."""
     t0 = time.time()
-    sc = c4_scene(n_cam, n_pt, k=k, seed=0x5F3D0014, vis=1)
+    r3 = model == abi.SFM_CAM_RADIAL3
+    sc = c4_scene(n_cam, n_pt, k=k, seed=0x5F3D0004 if r3 else 0x5F3D0014, vis=0 if r3 else 1, model=model)
     plan = api.BAPlan(ctx, sc["problem"], sc["extr"], sc["intr"], sc["X"])
     t_plan = time.time() - t0
     info = plan.info()
@@ -389,14 +393,19 @@ def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2):
     dt = time.perf_counter() - t1
     plan.close()
     nF = info.rcs_dim
-    out = {"metric": "BA LM-iters/sec, dense reduced camera system (random-k visibility)",
+    out = {"metric": "BA LM-iters/sec, PINHOLE_CAMERA_RADIAL3 residual model" if r3 else
+                     "BA LM-iters/sec, dense reduced camera system (random-k visibility)",
            "value": iters / dt, "unit": "LM-iters/s", "ms_per_iteration": dt / max(iters, 1) * 1e3,
            "lm_iterations_per_solve": summ.iterations, "rmse_initial": summ.rmse_initial,
            "rmse_final": summ.rmse_final, "rcs_dim": nF, "dense": True,
            "rcs_factor_flops_per_iteration": nF ** 3 / 3.0, "host_plan_seconds": t_plan,
            "config": {"workload": f"{n_cam} cams / {n_pt} pts / {sc['n_obs']} obs, random k={k} visibility "
                                   "(SURVEY §8(d) dense-S stress variant of C4), HuberLoss(4)"}}
-    log(f"BA dense-S: {iters} LM iterations in {dt:.3f}s -> {iters / dt:.1f} it/s, rcs {nF}, plan {t_plan:.1f}s, "
+    if r3:
+        out["config"] = {"workload": f"C4 geometry ({n_cam} cams / {n_pt} pts / {sc['n_obs']} obs, banded k={k}), "
+                                     "OpenMVG Pinhole_Intrinsic_Radial_K3 residual {f, ppx, ppy, k1, k2, k3} "
+                                     "(one shared block, ADJUST_ALL), HuberLoss(4); general-point path + dense RCS"}
+    log(f"BA {'radial3' if r3 else 'dense-S'}: {iters} LM iterations in {dt:.3f}s -> {iters / dt:.1f} it/s, rcs {nF}, plan {t_plan:.1f}s, "
         f"rmse {summ.rmse_initial:.4f}->{summ.rmse_final:.4f}")
     return out
 
@@ -459,6 +468,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--no-snavely", action="store_true")
+    ap.add_argument("--no-radial3", action="store_true")
     ap.add_argument("--no-loop", action="store_true")
     ap.add_argument("--loop-images", type=int, default=300)
     ap.add_argument("--no-filter", action="store_true")
@@ -729,6 +739,9 @@ def main():
     dense_s = None
     if world == 1 and rank == 0 and not args.no_dense and args.fake_world <= 1:
         dense_s = bench_dense_s(ctx)
+    radial3 = None
+    if world == 1 and rank == 0 and not args.no_radial3 and args.fake_world <= 1:
+        radial3 = bench_dense_s(ctx, model=abi.SFM_CAM_RADIAL3)
 
     # ---------------- geometric filter ----------------
     filt = None
@@ -802,6 +815,7 @@ def main():
             "loop": loop,
             "filter": filt,
             "ba_dense_s": dense_s,
+            "ba_radial3": radial3,
         }
         print(json.dumps(out))
     plan.close()

@@ -87,7 +87,8 @@ int sfm_ctx_synchronize(sfm_ctx* ctx);
 /* Residual (BundleAdjuster.h:40-65): P = R(w) X + t (ceres::AngleAxisRotate- */
 /* Point), u = fx P0/P2 + cx, v = fy P1/P2 + cy, r = (u - obs.x, v - obs.y).   */
 /* Parameter blocks: extr[6*n_img] = {w0,w1,w2,t0,t1,t2} per image,          */
-/* intr[4*n_intr] = {fx,fy,cx,cy}, X[3*n_pt].  Loss HuberLoss(huber_a).       */
+/* intr[4*n_intr] = {fx,fy,cx,cy} (camera_model selects others), X[3*n_pt].   */
+/* Loss HuberLoss(huber_a).                                                  */
 /* ------------------------------------------------------------------------ */
 typedef struct sfm_ba_problem {
     int32_t n_img;           /* posed images (extrinsic blocks)                */
@@ -106,16 +107,28 @@ typedef struct sfm_ba_problem {
     double huber_a;          /* HuberLoss scale a (reference: 4.0); <=0: none  */
 } sfm_ba_problem;
 
-/* Residual models (sfm_ba_problem.camera_model).  Every model keeps the
- * 4-double intrinsics block layout of intr[]:
+/* Residual models (sfm_ba_problem.camera_model).  The intrinsics blocks of
+ * intr[] are 4 doubles wide, except RADIAL3's 6 (sfm_ba_intr_width()):
  *   SFM_CAM_PINHOLE  BundleAdjuster.h:33-69 ReprojectCost, {fx, fy, cx, cy}:
  *                    r = (fx P0/P2 + cx - u, fy P1/P2 + cy - v)
  *   SFM_CAM_SNAVELY  src/adjuster/SnavelyReprojectionError.h:16-54 (BAL /
  *                    Bundler), {f, l1, l2, -}: p = (-P0/P2, -P1/P2),
  *                    r = f (1 + |p|^2 (l1 + l2 |p|^2)) p - (u, v); the 4th
- *                    double is not a parameter (never read, never moved). */
+ *                    double is not a parameter (never read, never moved).
+ *   SFM_CAM_RADIAL3  OpenMVG Pinhole_Intrinsic_Radial_K3 with ADJUST_ALL, as
+ *                    reconstruction() selects it (sparseBuilder.cpp:1292-1299;
+ *                    ResidualErrorFunctor_Pinhole_Intrinsic_Radial_K3),
+ *                    {f, ppx, ppy, k1, k2, k3}: x = P0/P2, y = P1/P2,
+ *                    c = 1 + k1 r2 + k2 r2^2 + k3 r2^3 (r2 = x^2 + y^2),
+ *                    r = (ppx + f x c - u, ppy + f y c - v).  Solved through
+ *                    the general-point path and the dense reduced camera
+ *                    system. */
 #define SFM_CAM_PINHOLE 0
 #define SFM_CAM_SNAVELY 1
+#define SFM_CAM_RADIAL3 2
+/* [cpu] doubles per intrinsics block of a model (4, or 6 for RADIAL3);
+ * 0 for an unknown model. */
+int sfm_ba_intr_width(int32_t camera_model);
 
 typedef struct sfm_ba_options {  /* ceres::Solver::Options semantics      */
     int32_t max_num_iterations;            /* 50   */
@@ -201,7 +214,7 @@ typedef struct sfm_ba_plan_info {
     int32_t n_chunks;                       /* Schur work chunks              */
     int32_t band_blocks;                    /* block half-bandwidth D of S    */
     int32_t n_cam_active, n_intr_active;    /* RCS blocks                     */
-    int64_t rcs_dim;                        /* 6*n_cam_active+4*n_intr_active */
+    int64_t rcs_dim;                        /* 6*n_cam_active+w*n_intr_active */
     double  last_kernel_ms[8];              /* per-phase device time of the
                                                last iteration (HIP events)   */
     int64_t schur_flops_per_iter;           /* algorithmic flops, Schur kernel*/
@@ -243,7 +256,10 @@ typedef struct sfm_synth_ba_config {
     double perturb_rot, perturb_t, perturb_X, perturb_f; /* .01,.05,.05,5      */
     int32_t const_img;                    /* gauge (1)                          */
     int32_t camera_model;                 /* SFM_CAM_*; SNAVELY: f 1000,
-                                             l1 -0.08, l2 0.02 (+ perturbation) */
+                                             l1 -0.08, l2 0.02 (+ perturbation);
+                                             RADIAL3: pinhole f / principal point,
+                                             k1 -0.05, k2 0.01, k3 -0.002
+                                             (intr / gt_intr 6 doubles a block) */
 } sfm_synth_ba_config;
 int sfm_synth_ba(const sfm_synth_ba_config* cfg,
                  int64_t* pt_offsets, int32_t* obs_img, double* obs_uv,

@@ -45,8 +45,13 @@ namespace {
 
 constexpr double kEps = std::numeric_limits<double>::epsilon();
 
+// Jacobian row layout: intrinsics (up to 6; the model's width iw, zeros past
+// it) | extr 6 (w 3, t 3) | X 3.
+constexpr int kJR = 15, kJE = 6, kJX = 12;
+inline int intr_width(int model) { return model == SFM_CAM_RADIAL3 ? 6 : 4; }
+
 // ---------------------------------------------------------------------------
-// Analytic residual + Jacobian (row-major 2x13: intr 4 | extr 6 | X 3).
+// Analytic residual + Jacobian (row-major 2 x kJR).
 // dP/dw for the Rodrigues branch: -R [X]x (w w' + (R' - I)[w]x) / |w|^2
 // (Gallego & Yezzi 2015); small-angle branch of AngleAxisRotatePoint:
 // P = X + w x X, dP/dw = -[X]x, dP/dX = I + [w]x.
@@ -105,8 +110,35 @@ bool residual_jacobian(int model, const double* in, const double* e, const doubl
         }
     }
     P[0] += e[3]; P[1] += e[4]; P[2] += e[5];
-    double A[2][3], Ji[2][4];
-    if (model == SFM_CAM_SNAVELY) {
+    double A[2][3], Ji[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};
+    if (model == SFM_CAM_RADIAL3) {
+        // OpenMVG ResidualErrorFunctor_Pinhole_Intrinsic_Radial_K3 (PINHOLE_CAMERA_RADIAL3,
+        // sparseBuilder.cpp:1292-1299): x_u = P/P2, r_coeff = 1 + k1 r2 + k2 r4 + k3 r6,
+        // r = (ppx + f x_u r_coeff, ppy + f y_u r_coeff) - obs; in = (f, ppx, ppy, k1, k2, k3)
+        const double xu = P[0] / P[2], yu = P[1] / P[2];
+        const double r2 = xu * xu + yu * yu, r4 = r2 * r2, r6 = r4 * r2;
+        const double rc = 1.0 + in[3] * r2 + in[4] * r4 + in[5] * r6;
+        r[0] = in[1] + in[0] * (xu * rc) - uv[0];
+        r[1] = in[2] + in[0] * (yu * rc) - uv[1];
+        if (J) {
+            // d(rc)/d(xu, yu) = D (xu, yu), D = 2 (k1 + 2 k2 r2 + 3 k3 r4)
+            const double iz = 1.0 / P[2], D = 2.0 * (in[3] + 2.0 * in[4] * r2 + 3.0 * in[5] * r4);
+            const double B[2][2] = {{in[0] * (rc + D * xu * xu), in[0] * D * xu * yu},
+                                    {in[0] * D * xu * yu, in[0] * (rc + D * yu * yu)}};
+            const double pu[2] = {xu, yu};
+            for (int row = 0; row < 2; ++row) {
+                A[row][0] = iz * B[row][0];
+                A[row][1] = iz * B[row][1];
+                A[row][2] = -iz * (B[row][0] * xu + B[row][1] * yu);
+                Ji[row][0] = pu[row] * rc;
+                Ji[row][1] = row == 0 ? 1.0 : 0.0;
+                Ji[row][2] = row == 1 ? 1.0 : 0.0;
+                Ji[row][3] = in[0] * pu[row] * r2;
+                Ji[row][4] = in[0] * pu[row] * r4;
+                Ji[row][5] = in[0] * pu[row] * r6;
+            }
+        }
+    } else if (model == SFM_CAM_SNAVELY) {
         // SnavelyReprojectionError.h:31-47: p = -P/P2, d = 1 + r2 (l1 + l2 r2),
         // r = f d p - obs.  dr/dP = f [d I + 2 (l1 + 2 l2 r2) p p'] dp/dP,
         // dp/dP = -1/P2 [1 0 xp; 0 1 yp]
@@ -139,17 +171,18 @@ bool residual_jacobian(int model, const double* in, const double* e, const doubl
             const double A0[2][3] = {{in[0] * iz, 0.0, -in[0] * x * iz}, {0.0, in[1] * iz, -in[1] * y * iz}};
             const double J0[2][4] = {{x, 0.0, 1.0, 0.0}, {0.0, y, 0.0, 1.0}};
             std::memcpy(A, A0, sizeof A);
-            std::memcpy(Ji, J0, sizeof Ji);
+            for (int row = 0; row < 2; ++row)
+                for (int k = 0; k < 4; ++k) Ji[row][k] = J0[row][k];
         }
     }
     if (J) {
         for (int row = 0; row < 2; ++row) {
-            double* Jr = J + row * 13;
-            for (int k = 0; k < 4; ++k) Jr[k] = Ji[row][k];
+            double* Jr = J + row * kJR;
+            for (int k = 0; k < 6; ++k) Jr[k] = Ji[row][k];
             for (int j = 0; j < 3; ++j) {
                 double a = 0, b = 0;
                 for (int k = 0; k < 3; ++k) { a += A[row][k] * dPdw[k * 3 + j]; b += A[row][k] * dPdX[k * 3 + j]; }
-                Jr[4 + j] = a; Jr[7 + j] = A[row][j]; Jr[10 + j] = b;
+                Jr[kJE + j] = a; Jr[kJE + 3 + j] = A[row][j]; Jr[kJX + j] = b;
             }
         }
     }
@@ -157,25 +190,25 @@ bool residual_jacobian(int model, const double* in, const double* e, const doubl
 }
 
 // ---------------------------------------------------------------------------
-// Forward-mode dual numbers (ceres::Jet<double,13> semantics) for the
+// Forward-mode dual numbers (ceres::Jet<double,N> semantics) for the
 // autodiff cross-check.
 // ---------------------------------------------------------------------------
 struct Jet {
-    double a; double v[13];
+    double a; double v[kJR];
     Jet() : a(0) { std::memset(v, 0, sizeof v); }
     explicit Jet(double x) : a(x) { std::memset(v, 0, sizeof v); }
     Jet(double x, int k) : a(x) { std::memset(v, 0, sizeof v); v[k] = 1.0; }
 };
-inline Jet operator+(const Jet& f, const Jet& g) { Jet r(f.a + g.a); for (int k = 0; k < 13; ++k) r.v[k] = f.v[k] + g.v[k]; return r; }
-inline Jet operator-(const Jet& f, const Jet& g) { Jet r(f.a - g.a); for (int k = 0; k < 13; ++k) r.v[k] = f.v[k] - g.v[k]; return r; }
-inline Jet operator*(const Jet& f, const Jet& g) { Jet r(f.a * g.a); for (int k = 0; k < 13; ++k) r.v[k] = f.a * g.v[k] + f.v[k] * g.a; return r; }
+inline Jet operator+(const Jet& f, const Jet& g) { Jet r(f.a + g.a); for (int k = 0; k < kJR; ++k) r.v[k] = f.v[k] + g.v[k]; return r; }
+inline Jet operator-(const Jet& f, const Jet& g) { Jet r(f.a - g.a); for (int k = 0; k < kJR; ++k) r.v[k] = f.v[k] - g.v[k]; return r; }
+inline Jet operator*(const Jet& f, const Jet& g) { Jet r(f.a * g.a); for (int k = 0; k < kJR; ++k) r.v[k] = f.a * g.v[k] + f.v[k] * g.a; return r; }
 inline Jet operator/(const Jet& f, const Jet& g) {
     const double ia = 1.0 / g.a, abyb = f.a * ia;
-    Jet r(abyb); for (int k = 0; k < 13; ++k) r.v[k] = (f.v[k] - abyb * g.v[k]) * ia; return r;
+    Jet r(abyb); for (int k = 0; k < kJR; ++k) r.v[k] = (f.v[k] - abyb * g.v[k]) * ia; return r;
 }
-inline Jet jsqrt(const Jet& f) { const double t = std::sqrt(f.a), i2 = 1.0 / (2.0 * t); Jet r(t); for (int k = 0; k < 13; ++k) r.v[k] = f.v[k] * i2; return r; }
-inline Jet jcos(const Jet& f) { Jet r(std::cos(f.a)); const double s = -std::sin(f.a); for (int k = 0; k < 13; ++k) r.v[k] = s * f.v[k]; return r; }
-inline Jet jsin(const Jet& f) { Jet r(std::sin(f.a)); const double c = std::cos(f.a); for (int k = 0; k < 13; ++k) r.v[k] = c * f.v[k]; return r; }
+inline Jet jsqrt(const Jet& f) { const double t = std::sqrt(f.a), i2 = 1.0 / (2.0 * t); Jet r(t); for (int k = 0; k < kJR; ++k) r.v[k] = f.v[k] * i2; return r; }
+inline Jet jcos(const Jet& f) { Jet r(std::cos(f.a)); const double s = -std::sin(f.a); for (int k = 0; k < kJR; ++k) r.v[k] = s * f.v[k]; return r; }
+inline Jet jsin(const Jet& f) { Jet r(std::sin(f.a)); const double c = std::cos(f.a); for (int k = 0; k < kJR; ++k) r.v[k] = c * f.v[k]; return r; }
 
 void residual_jet(int model, const Jet* intr, const Jet* extr, const Jet* pt, const double* uv, Jet* res) {
     const Jet* w = extr;
@@ -192,6 +225,15 @@ void residual_jet(int model, const Jet* intr, const Jet* extr, const Jet* pt, co
         for (int a = 0; a < 3; ++a) P[a] = pt[a] + cr[a];
     }
     P[0] = P[0] + extr[3]; P[1] = P[1] + extr[4]; P[2] = P[2] + extr[5];
+    if (model == SFM_CAM_RADIAL3) {   // ResidualErrorFunctor_Pinhole_Intrinsic_Radial_K3, term by term
+        const Jet xu = P[0] / P[2], yu = P[1] / P[2];
+        const Jet r2 = xu * xu + yu * yu, r4 = r2 * r2, r6 = r4 * r2;
+        const Jet rc = Jet(1.0) + intr[3] * r2 + intr[4] * r4 + intr[5] * r6;
+        const Jet xd = xu * rc, yd = yu * rc;
+        res[0] = intr[1] + intr[0] * xd - Jet(uv[0]);
+        res[1] = intr[2] + intr[0] * yd - Jet(uv[1]);
+        return;
+    }
     if (model == SFM_CAM_SNAVELY) {   // SnavelyReprojectionError.h:31-47, term by term
         const Jet xp = Jet(0.0) - P[0] / P[2], yp = Jet(0.0) - P[1] / P[2];
         const Jet r2 = xp * xp + yp * yp;
@@ -344,6 +386,7 @@ struct Oracle {
 
     std::vector<int> cam_blk, intr_blk;
     int64_t ncam = 0, nintr = 0, nb = 0, na = 0, nF = 0, bw = 0;
+    int iw = 4;                        // intrinsics block width of the model
     std::vector<int64_t> pts;          // shard points (global ids)
     std::vector<int64_t> obs_ptr;      // per shard point: first obs slot in the shard obs arrays
     int64_t n_sobs = 0;
@@ -351,7 +394,7 @@ struct Oracle {
     std::vector<double> extr, intr;    // current full camera tables
     std::vector<double> xF, xE;        // active parameters (F: cams then intr; E: shard points)
     std::vector<double> scaleF, scaleE;
-    std::vector<double> f, J;          // per shard obs: corrected residual (2), Jacobian (26)
+    std::vector<double> f, J;          // per shard obs: corrected residual (2), Jacobian (2 x kJR)
     double x_cost = 0;
 
     Oracle(const sfm_ba_problem& p, const sfm_ba_options& o, orc_allreduce_fn a, void* u, int t)
@@ -362,16 +405,17 @@ struct Oracle {
     int64_t colF_cam(int img) const { return cam_blk[img] < 0 ? -1 : 6 * (int64_t)cam_blk[img]; }
     int64_t colF_intr(int img) const {
         const int q = intr_blk[P.img_intr[img]];
-        return q < 0 ? -1 : nb + 4 * (int64_t)q;
+        return q < 0 ? -1 : nb + iw * (int64_t)q;
     }
 
     void setup(const double* e, const double* in, const double* X, const int64_t* shard, int64_t nsh) {
+        iw = intr_width(P.camera_model);
         cam_blk.assign(P.n_img, -1); intr_blk.assign(P.n_intr, -1);
         std::vector<char> cam_used(P.n_img, 0), intr_used(P.n_intr, 0);
         for (int64_t o = 0; o < P.n_obs; ++o) { cam_used[P.obs_img[o]] = 1; intr_used[P.img_intr[P.obs_img[o]]] = 1; }
         for (int i = 0; i < P.n_img; ++i) if (cam_used[i] && i != P.const_img) cam_blk[i] = (int)ncam++;
         for (int q = 0; q < P.n_intr; ++q) if (intr_used[q]) intr_blk[q] = (int)nintr++;
-        nb = 6 * ncam; na = 4 * nintr; nF = nb + na;
+        nb = 6 * ncam; na = iw * nintr; nF = nb + na;
         int64_t D = 0;
         for (int64_t p = 0; p < P.n_pt; ++p) {
             int lo = INT32_MAX, hi = -1;
@@ -389,23 +433,23 @@ struct Oracle {
         for (size_t k = 0; k < pts.size(); ++k)
             obs_ptr[k + 1] = obs_ptr[k] + (P.pt_offsets[pts[k] + 1] - P.pt_offsets[pts[k]]);
         n_sobs = obs_ptr.back();
-        extr.assign(e, e + 6 * (size_t)P.n_img); intr.assign(in, in + 4 * (size_t)P.n_intr);
+        extr.assign(e, e + 6 * (size_t)P.n_img); intr.assign(in, in + iw * (size_t)P.n_intr);
         xF.assign(nF, 0.0);
         for (int i = 0; i < P.n_img; ++i) if (cam_blk[i] >= 0) for (int a = 0; a < 6; ++a) xF[6 * cam_blk[i] + a] = extr[6 * i + a];
         // SNAVELY: the 4th intrinsics double is not a parameter (held at 0, never written back)
         for (int q = 0; q < P.n_intr; ++q)
             if (intr_blk[q] >= 0)
-                for (int a = 0; a < 4; ++a)
-                    xF[nb + 4 * intr_blk[q] + a] = (P.camera_model == SFM_CAM_SNAVELY && a == 3) ? 0.0 : intr[4 * q + a];
+                for (int a = 0; a < iw; ++a)
+                    xF[nb + iw * intr_blk[q] + a] = (P.camera_model == SFM_CAM_SNAVELY && a == 3) ? 0.0 : intr[iw * q + a];
         xE.resize(3 * pts.size());
         for (size_t k = 0; k < pts.size(); ++k) for (int a = 0; a < 3; ++a) xE[3 * k + a] = X[3 * pts[k] + a];
-        f.assign(2 * n_sobs, 0.0); J.assign(26 * n_sobs, 0.0);
+        f.assign(2 * n_sobs, 0.0); J.assign(2 * kJR * n_sobs, 0.0);
         scaleF.assign(nF, 1.0); scaleE.assign(xE.size(), 1.0);
     }
 
     void load_cams(const std::vector<double>& xf) {
         for (int i = 0; i < P.n_img; ++i) if (cam_blk[i] >= 0) for (int a = 0; a < 6; ++a) extr[6 * i + a] = xf[6 * cam_blk[i] + a];
-        for (int q = 0; q < P.n_intr; ++q) if (intr_blk[q] >= 0) for (int a = 0; a < 4; ++a) intr[4 * q + a] = xf[nb + 4 * intr_blk[q] + a];
+        for (int q = 0; q < P.n_intr; ++q) if (intr_blk[q] >= 0) for (int a = 0; a < iw; ++a) intr[iw * q + a] = xf[nb + iw * intr_blk[q] + a];
     }
 
     // Evaluate cost (and optionally corrected f/J) at (xf, xe). Returns false
@@ -424,8 +468,8 @@ struct Oracle {
             const int64_t p = pts[k];
             for (int64_t o = P.pt_offsets[p], s = obs_ptr[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
                 const int img = P.obs_img[o];
-                double r[2], Jl[26];
-                const bool ok = residual_jacobian(P.camera_model, &intr[4 * (size_t)P.img_intr[img]], &extr[6 * (size_t)img],
+                double r[2], Jl[2 * kJR];
+                const bool ok = residual_jacobian(P.camera_model, &intr[iw * (size_t)P.img_intr[img]], &extr[6 * (size_t)img],
                                                   &xe[3 * k], &P.obs_uv[2 * o], r, jac ? Jl : nullptr);
                 if (!ok) { bad[tid] = 1; continue; }
                 const double sq = r[0] * r[0] + r[1] * r[1];
@@ -435,7 +479,7 @@ struct Oracle {
                 if (jac) {
                     const double sr = std::sqrt(rho[1]);
                     f[2 * s] = r[0] * sr; f[2 * s + 1] = r[1] * sr;
-                    for (int a = 0; a < 26; ++a) J[26 * s + a] = Jl[a] * sr;
+                    for (int a = 0; a < 2 * kJR; ++a) J[2 * kJR * s + a] = Jl[a] * sr;
                 }
             }
         }
@@ -456,10 +500,10 @@ struct Oracle {
                 const int img = P.obs_img[o];
                 const int64_t ci = colF_intr(img), cc = colF_cam(img);
                 for (int row = 0; row < 2; ++row) {
-                    const double* Jr = &J[26 * s + 13 * row];
-                    for (int a = 0; a < 4; ++a) { const double v = Jr[a] * (scaled ? scaleF[ci + a] : 1.0); cF[ci + a] += v * v; }
-                    if (cc >= 0) for (int a = 0; a < 6; ++a) { const double v = Jr[4 + a] * (scaled ? scaleF[cc + a] : 1.0); cF[cc + a] += v * v; }
-                    for (int a = 0; a < 3; ++a) { const double v = Jr[10 + a] * (scaled ? scaleE[3 * k + a] : 1.0); cE[3 * k + a] += v * v; }
+                    const double* Jr = &J[2 * kJR * s + kJR * row];
+                    for (int a = 0; a < iw; ++a) { const double v = Jr[a] * (scaled ? scaleF[ci + a] : 1.0); cF[ci + a] += v * v; }
+                    if (cc >= 0) for (int a = 0; a < 6; ++a) { const double v = Jr[kJE + a] * (scaled ? scaleF[cc + a] : 1.0); cF[cc + a] += v * v; }
+                    for (int a = 0; a < 3; ++a) { const double v = Jr[kJX + a] * (scaled ? scaleE[3 * k + a] : 1.0); cE[3 * k + a] += v * v; }
                 }
             }
         }
@@ -475,11 +519,11 @@ struct Oracle {
                 const int img = P.obs_img[o];
                 const int64_t ci = colF_intr(img), cc = colF_cam(img);
                 for (int row = 0; row < 2; ++row) {
-                    const double* Jr = &J[26 * s + 13 * row];
+                    const double* Jr = &J[2 * kJR * s + kJR * row];
                     const double fr = f[2 * s + row];
-                    for (int a = 0; a < 4; ++a) gF[ci + a] += Jr[a] * fr;
-                    if (cc >= 0) for (int a = 0; a < 6; ++a) gF[cc + a] += Jr[4 + a] * fr;
-                    for (int a = 0; a < 3; ++a) gE[3 * k + a] += Jr[10 + a] * fr;
+                    for (int a = 0; a < iw; ++a) gF[ci + a] += Jr[a] * fr;
+                    if (cc >= 0) for (int a = 0; a < 6; ++a) gF[cc + a] += Jr[kJE + a] * fr;
+                    for (int a = 0; a < 3; ++a) gE[3 * k + a] += Jr[kJX + a] * fr;
                 }
             }
         }
@@ -540,7 +584,7 @@ struct Oracle {
             std::vector<int> base(cols.size());
             for (size_t b = 0; b < cols.size(); ++b) {
                 base[b] = (int)gcol.size();
-                const int w = cols[b] >= nb ? 4 : 6;
+                const int w = cols[b] >= nb ? iw : 6;
                 for (int a = 0; a < w; ++a) gcol.push_back(cols[b] + a);
             }
             const int nl = (int)gcol.size();
@@ -551,12 +595,12 @@ struct Oracle {
                 const int64_t ci = colF_intr(img), cc = colF_cam(img);
                 // scaled row pieces
                 for (int row = 0; row < 2; ++row) {
-                    const double* Jr = &J[26 * s + 13 * row];
+                    const double* Jr = &J[2 * kJR * s + kJR * row];
                     const double fr = f[2 * s + row];
-                    double jx[3], jf[10]; int lf[10]; int nf = 0;
-                    for (int a = 0; a < 3; ++a) jx[a] = Jr[10 + a] * scaleE[3 * k + a];
-                    { const int b = c_of[2 * (o - o0)]; for (int a = 0; a < 4; ++a) { jf[nf] = Jr[a] * scaleF[ci + a]; lf[nf++] = base[b] + a; } }
-                    if (cc >= 0) { const int b = c_of[2 * (o - o0) + 1]; for (int a = 0; a < 6; ++a) { jf[nf] = Jr[4 + a] * scaleF[cc + a]; lf[nf++] = base[b] + a; } }
+                    double jx[3], jf[12]; int lf[12]; int nf = 0;
+                    for (int a = 0; a < 3; ++a) jx[a] = Jr[kJX + a] * scaleE[3 * k + a];
+                    { const int b = c_of[2 * (o - o0)]; for (int a = 0; a < iw; ++a) { jf[nf] = Jr[a] * scaleF[ci + a]; lf[nf++] = base[b] + a; } }
+                    if (cc >= 0) { const int b = c_of[2 * (o - o0) + 1]; for (int a = 0; a < 6; ++a) { jf[nf] = Jr[kJE + a] * scaleF[cc + a]; lf[nf++] = base[b] + a; } }
                     for (int a = 0; a < 3; ++a) { bE[a] += jx[a] * fr; for (int c = 0; c < 3; ++c) V[3 * a + c] += jx[a] * jx[c]; }
                     for (int u = 0; u < nf; ++u) {
                         bF[lf[u]] += jf[u] * fr;
@@ -616,12 +660,12 @@ struct Oracle {
                 const int img = P.obs_img[o];
                 const int64_t ci = colF_intr(img), cc = colF_cam(img);
                 for (int row = 0; row < 2; ++row) {
-                    const double* Jr = &J[26 * s + 13 * row];
+                    const double* Jr = &J[2 * kJR * s + kJR * row];
                     double jx[3];
-                    for (int a = 0; a < 3; ++a) jx[a] = Jr[10 + a] * scaleE[3 * k + a];
+                    for (int a = 0; a < 3; ++a) jx[a] = Jr[kJX + a] * scaleE[3 * k + a];
                     double q = 0;  // (J_F y_F) for this row
-                    for (int a = 0; a < 4; ++a) q += Jr[a] * scaleF[ci + a] * yF[ci + a];
-                    if (cc >= 0) for (int a = 0; a < 6; ++a) q += Jr[4 + a] * scaleF[cc + a] * yF[cc + a];
+                    for (int a = 0; a < iw; ++a) q += Jr[a] * scaleF[ci + a] * yF[ci + a];
+                    if (cc >= 0) for (int a = 0; a < 6; ++a) q += Jr[kJE + a] * scaleF[cc + a] * yF[cc + a];
                     const double fr = f[2 * s + row];
                     for (int a = 0; a < 3; ++a) {
                         b[a] += jx[a] * fr - jx[a] * q;
@@ -646,11 +690,11 @@ struct Oracle {
                 const int img = P.obs_img[o];
                 const int64_t ci = colF_intr(img), cc = colF_cam(img);
                 for (int row = 0; row < 2; ++row) {
-                    const double* Jr = &J[26 * s + 13 * row];
+                    const double* Jr = &J[2 * kJR * s + kJR * row];
                     double m = 0;
-                    for (int a = 0; a < 4; ++a) m += Jr[a] * scaleF[ci + a] * sF[ci + a];
-                    if (cc >= 0) for (int a = 0; a < 6; ++a) m += Jr[4 + a] * scaleF[cc + a] * sF[cc + a];
-                    for (int a = 0; a < 3; ++a) m += Jr[10 + a] * scaleE[3 * k + a] * sE[3 * k + a];
+                    for (int a = 0; a < iw; ++a) m += Jr[a] * scaleF[ci + a] * sF[ci + a];
+                    if (cc >= 0) for (int a = 0; a < 6; ++a) m += Jr[kJE + a] * scaleF[cc + a] * sF[cc + a];
+                    for (int a = 0; a < 3; ++a) m += Jr[kJX + a] * scaleE[3 * k + a] * sE[3 * k + a];
                     acc += m * (f[2 * s + row] + m / 2.0);
                 }
             }
@@ -669,18 +713,30 @@ extern "C" int orc_ba_jacobian(int32_t mode, const double* intr, const double* e
 
 extern "C" int orc_ba_jacobian_model(int32_t model, int32_t mode, const double* intr, const double* extr,
                                      const double* X, const double* uv, double* r, double* J) {
-    if (model != SFM_CAM_PINHOLE && model != SFM_CAM_SNAVELY) return SFM_ERR_INVALID_ARG;
-    if (mode == 0) return residual_jacobian(model, intr, extr, X, uv, r, J) ? SFM_OK : SFM_ERR_NOT_FINITE;
-    Jet in[4], ex[6], pt[3], res[2];
-    for (int a = 0; a < 4; ++a) in[a] = Jet(intr[a], a);
-    for (int a = 0; a < 6; ++a) ex[a] = Jet(extr[a], 4 + a);
-    for (int a = 0; a < 3; ++a) pt[a] = Jet(X[a], 10 + a);
-    residual_jet(model, in, ex, pt, uv, res);
-    for (int row = 0; row < 2; ++row) {
-        r[row] = res[row].a;
-        for (int k = 0; k < 13; ++k) J[13 * row + k] = res[row].v[k];
+    if (model != SFM_CAM_PINHOLE && model != SFM_CAM_SNAVELY && model != SFM_CAM_RADIAL3) return SFM_ERR_INVALID_ARG;
+    // public layout: 2 x (iw + 6 + 3), intrinsics | extr | X
+    const int iw = intr_width(model), w = iw + 9;
+    double Jf[2 * kJR];
+    bool ok;
+    if (mode == 0) {
+        ok = residual_jacobian(model, intr, extr, X, uv, r, Jf);
+    } else {
+        Jet in[6], ex[6], pt[3], res[2];
+        for (int a = 0; a < iw; ++a) in[a] = Jet(intr[a], a);
+        for (int a = 0; a < 6; ++a) ex[a] = Jet(extr[a], kJE + a);
+        for (int a = 0; a < 3; ++a) pt[a] = Jet(X[a], kJX + a);
+        residual_jet(model, in, ex, pt, uv, res);
+        for (int row = 0; row < 2; ++row) {
+            r[row] = res[row].a;
+            for (int k = 0; k < kJR; ++k) Jf[kJR * row + k] = res[row].v[k];
+        }
+        ok = std::isfinite(r[0]) && std::isfinite(r[1]);
     }
-    return std::isfinite(r[0]) && std::isfinite(r[1]) ? SFM_OK : SFM_ERR_NOT_FINITE;
+    for (int row = 0; row < 2; ++row) {
+        for (int k = 0; k < iw; ++k) J[w * row + k] = Jf[kJR * row + k];
+        for (int k = 0; k < 9; ++k) J[w * row + iw + k] = Jf[kJR * row + kJE + k];
+    }
+    return ok ? SFM_OK : SFM_ERR_NOT_FINITE;
 }
 
 extern "C" int orc_ba_cost(const sfm_ba_problem* P, const double* extr, const double* intr,
@@ -691,7 +747,7 @@ extern "C" int orc_ba_cost(const sfm_ba_problem* P, const double* extr, const do
         for (int64_t o = P->pt_offsets[p]; o < P->pt_offsets[p + 1]; ++o) {
             const int img = P->obs_img[o];
             double r[2];
-            residual_jacobian(P->camera_model, &intr[4 * (size_t)P->img_intr[img]], &extr[6 * (size_t)img], &X[3 * p],
+            residual_jacobian(P->camera_model, &intr[intr_width(P->camera_model) * (size_t)P->img_intr[img]], &extr[6 * (size_t)img], &X[3 * p],
                               &P->obs_uv[2 * o], r, nullptr);
             double rho[2];
             huber(P->huber_a, r[0] * r[0] + r[1] * r[1], rho);
@@ -708,7 +764,8 @@ extern "C" int orc_ba_solve(const sfm_ba_problem* P, double* extr, double* intr,
                             int64_t n_shard_pts, orc_allreduce_fn allreduce, void* user,
                             int32_t n_threads) {
     if (!P || !extr || !intr || !X || !sum || P->n_img < 0 || P->n_pt < 0) return SFM_ERR_INVALID_ARG;
-    if (P->camera_model != SFM_CAM_PINHOLE && P->camera_model != SFM_CAM_SNAVELY) return SFM_ERR_INVALID_ARG;
+    if (P->camera_model != SFM_CAM_PINHOLE && P->camera_model != SFM_CAM_SNAVELY && P->camera_model != SFM_CAM_RADIAL3)
+        return SFM_ERR_INVALID_ARG;
     sfm_ba_options O;
     if (opts) {
         O = *opts;
@@ -741,8 +798,8 @@ extern "C" int orc_ba_solve(const sfm_ba_problem* P, double* extr, double* intr,
             for (int i = 0; i < P->n_img; ++i) if (S.cam_blk[i] >= 0) for (int a = 0; a < 6; ++a) extr[6 * i + a] = S.xF[6 * S.cam_blk[i] + a];
             for (int q = 0; q < P->n_intr; ++q)
                 if (S.intr_blk[q] >= 0)
-                    for (int a = 0; a < (P->camera_model == SFM_CAM_SNAVELY ? 3 : 4); ++a)
-                        intr[4 * q + a] = S.xF[S.nb + 4 * S.intr_blk[q] + a];
+                    for (int a = 0; a < (P->camera_model == SFM_CAM_SNAVELY ? 3 : S.iw); ++a)
+                        intr[S.iw * q + a] = S.xF[S.nb + S.iw * S.intr_blk[q] + a];
             for (size_t k = 0; k < S.pts.size(); ++k) for (int a = 0; a < 3; ++a) X[3 * S.pts[k] + a] = S.xE[3 * k + a];
         }
         return term == SFM_TERM_FAILURE ? SFM_ERR_SOLVER : SFM_OK;

@@ -14,7 +14,8 @@
  *     Ceres 2.2 TrustRegionMinimizer / LevenbergMarquardtStrategy /
  *     SchurEliminator control flow (documented in oracle/ba_oracle.cpp),
  *     and src/adjuster/SnavelyReprojectionError.h:16-54 (BAL residual model,
- *     SURVEY.md §8(f) row 4) as an alternative residual;
+ *     SURVEY.md §8(f) row 4) and OpenMVG's PINHOLE_CAMERA_RADIAL3 residual
+ *     (sparseBuilder.cpp:1292-1299) as alternative residuals;
  *   - OpenMVG Matcher_Regions(BRUTE_FORCE_L2) ratio matching as selected by
  *     src/sparseBuilder/sparseBuilder.cpp:919-921 with fDistRatio 0.8 (:812);
  *   - OpenMVG Cascade_Hashing_Matcher_Regions(0.8), the "AUTO" default of
@@ -61,7 +62,8 @@ int orc_ba_jacobian(int32_t mode, const double* intr, const double* extr, const 
                     const double* uv, double* r, double* J);
 
 /* Same for a residual model SFM_CAM_* (SNAVELY: SnavelyReprojectionError.h,
- * intrinsics {f, l1, l2, -}, J column 3 is zero). */
+ * intrinsics {f, l1, l2, -}, J column 3 is zero; RADIAL3: OpenMVG
+ * Pinhole_Intrinsic_Radial_K3, {f, ppx, ppy, k1, k2, k3}, J row-major 2x15). */
 int orc_ba_jacobian_model(int32_t model, int32_t mode, const double* intr, const double* extr,
                           const double* X, const double* uv, double* r, double* J);
 

@@ -99,10 +99,11 @@ class Scene:
         self.obs_uv = np.zeros(2 * no, np.float64)
         self.img_intr = np.zeros(n_cam, np.int32)
         self.extr = np.zeros(6 * n_cam)
-        self.intr = np.zeros(4 * n_intr)
+        iw = 6 if model == abi.SFM_CAM_RADIAL3 else 4   # doubles per intrinsics block
+        self.intr = np.zeros(iw * n_intr)
         self.X = np.zeros(3 * n_pt)
         self.gt_extr = np.zeros(6 * n_cam)
-        self.gt_intr = np.zeros(4 * n_intr)
+        self.gt_intr = np.zeros(iw * n_intr)
         self.gt_X = np.zeros(3 * n_pt)
         p = abi.ptr
         rc = lib.sfm_synth_ba(C.byref(cfg), p(self.pt_offsets, abi.i64p), p(self.obs_img, abi.i32p),

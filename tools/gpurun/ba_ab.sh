@@ -6,7 +6,7 @@ TAG=${1:-ab}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--no-match --no-snavely --no-loop --no-pmc --no-filter --no-dense --no-cpu-baseline"
+ARGS="--no-match --no-snavely --no-loop --no-pmc --no-filter --no-dense --no-radial3 --no-cpu-baseline"
 timeout -k 10 300 python -u bench.py --steps 20 $ARGS > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
 grep "^\[bench\] BA" "$OUT/bench.err"
 cd /tmp

@@ -1,0 +1,12 @@
+# RADIAL3 + BA GPU parity tests, then a BA-only bench line (regression check).
+set -e
+cd "$GRAFT_REPO_ROOT"
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3}
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+    tests/test_radial3.py tests/test_snavely.py tests/test_ba_gpu.py > "$OUT/tests.log" 2>&1 \
+    || { tail -40 "$OUT/tests.log"; exit 1; }
+tail -3 "$OUT/tests.log"
+timeout -k 10 300 python -u bench.py --no-match --no-snavely --no-loop --no-pmc --no-filter --no-cpu-baseline --no-dense --no-radial3 \
+    > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
+grep "^\[bench\]" "$OUT/bench.err" | tail -8

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_ba_gpu.py -x -q -k memory_cache --timeout 200 --timeout-method thread > "$OUT/cache_test.log" 2>&1 || { tail -30 "$OUT/cache_test.log"; exit 1; }
 tail -2 "$OUT/cache_test.log"
-ARGS="--no-match --no-snavely --no-loop --no-pmc --no-filter --no-dense --no-cpu-baseline"
+ARGS="--no-match --no-snavely --no-loop --no-pmc --no-filter --no-dense --no-radial3 --no-cpu-baseline"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof8" -o s8 -- \
     python3 "$GRAFT_REPO_ROOT/bench.py" --fake-world 8 --steps 5 $ARGS > "$OUT/fake8.json" 2> "$OUT/fake8.err" || { tail -20 "$OUT/fake8.err"; exit 1; }
