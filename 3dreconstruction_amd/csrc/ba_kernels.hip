@@ -593,6 +593,12 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 #ifndef SFM_SCHUR4_SO
 #define SFM_SCHUR4_SO 48
 #endif
+#ifndef SFM_SCHUR5_SP   // the same for the 80-row variant (SO >= the planner's kSubObs)
+#define SFM_SCHUR5_SP kSubPts
+#endif
+#ifndef SFM_SCHUR5_SO
+#define SFM_SCHUR5_SO kSubObs
+#endif
 
 // NT = 5: rows 0..75 F blocks, row 79 = w, so -Z w comes out of the MFMA.
 // NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
@@ -620,15 +626,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
     // 14-double observation rows spread ds_write_b128 lane groups.
     constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT, kPS = kPR + 4;
     __shared__ double panel[kPK][kPS];          // [k][row]
-    __shared__ double wcol[kPK];                // NT = 4: w = L^-1 g_E per panel column
+    __shared__ double wcol[NT == 4 ? kPK : 1];  // NT = 4: w = L^-1 g_E per panel column
     // per-observation rows use odd strides (in doubles): a wave's ds_*_b64 at
     // lane-strided rows then hits 32 distinct bank pairs (even strides of 4,
     // 6, 10 doubles were 2- to 4-way bank conflicts, SQ_LDS_BANK_CONFLICT)
     constexpr int kOb = CM == SFM_CAM_SNAVELY ? 7 : 5;
     __shared__ double ob[SO][kOb];              // J_intr nonzeros (scaled) | pad
-    __shared__ double vs[SO][9];                // per observation: Jx'Jx (6) | Jx'f (3)
+    // per observation: Jx'Jx (6) | Jx'f (3) until the per-point sums, then
+    // M = Jx L^-T (6) from phase B on (obm: the same rows; 3.5 KB less LDS per
+    // wave, which is what the chip's co-resident wave count divides)
+    __shared__ double vs[SO][9];
     __shared__ double vsum[SP][10];             // per point: V (6) | g_E (3)
-    __shared__ double obm[SO][7];               // M = Jx L^-T | pad
+    double (*const obm)[9] = vs;
     __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
     // chunk-level staging: every camera / intrinsics block the chunk touches
     __shared__ CamPreL scp[kCamSlots];
@@ -705,7 +714,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
         for (int e = lane; e < kPK * kPS / 2; e += 64)
             reinterpret_cast<double2*>(&panel[0][0])[e] = double2{0.0, 0.0};
-        if (NT == 4 && lane < kPK) wcol[lane] = 0.0;   // columns past 3 * npts stay zero
+        if constexpr (NT == 4)
+            if (lane < kPK) wcol[lane] = 0.0;   // columns past 3 * npts stay zero
         SFM_STAMP(0)
         // ---- A: observations -> scaled, corrected Jacobians -----------------
         Lin L;
@@ -827,7 +837,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
                 const double w3[3] = {i00 * b[0], i10 * b[0] + i11 * b[1], i20 * b[0] + i21 * b[1] + i22 * b[2]};
 #pragma unroll
                 for (int a = 0; a < 3; ++a) {
-                    if (NT == 5) panel[3 * pl + a][kTileWRow % kPR] = w3[a];
+                    if constexpr (NT == 5) panel[3 * pl + a][kTileWRow % kPR] = w3[a];
                     else wcol[3 * pl + a] = w3[a];
                 }
             }
@@ -941,7 +951,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
             for (int q = 0; q < kNTiles; ++q)
                 acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ks][kTi[q]], op[ks][kTj[q]], acc[q], 0, 0, 0);
-        if (NT == 4) {
+        if constexpr (NT == 4) {
 #pragma unroll
             for (int k = 0; k < kPK; ++k) wacc += panel[k][lane] * wcol[k];
         }
@@ -2081,11 +2091,11 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
                                                dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
     } else {
         if (scale_e)
-            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, kSubPts, kSubObs, true>), dim3(P.n_chunk),
-                                               dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO, true>),
+                                               dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
         else
-            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5>), dim3(P.n_chunk), dim3(64), 0, s, P, cp,
-                                               intr, X, radius, stamps));
+            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO>), dim3(P.n_chunk),
+                                               dim3(64), 0, s, P, cp, intr, X, radius, stamps));
     }
     SFM_HIP(hipGetLastError());
 }

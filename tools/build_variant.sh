@@ -1,15 +1,12 @@
 #!/bin/bash
-# A/B builds of libsfmcore.so: tools/build_variant.sh NAME SOURCE "EXTRA HIPCC FLAGS"
-# Rebuilds one csrc/ source with extra flags and links it with the regular
-# objects into build/var_NAME/libsfmcore.so (load with SFMCORE_LIB=...).
+# Build a variant of libsfmcore.so with extra compile flags on one source:
+#   tools/build_variant.sh OUT.so SOURCE.hip [flags...]
+# (the other objects come from build/, made by `make`)
 set -e
-cd "$(dirname "$0")/.."
-make -s 3dreconstruction_amd/lib/libsfmcore.so
-NAME=$1; SRC=$2; FLAGS=$3
-D=build/var_$NAME
-mkdir -p $D
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -I/opt/rocm/include $FLAGS \
-    -c 3dreconstruction_amd/csrc/$SRC -o $D/$SRC.o
-OBJS=$(ls build/*.hip.o build/*.cpp.o | grep -v "/$SRC.o$")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libsfmcore.so $OBJS $D/$SRC.o -ldl
-echo $D/libsfmcore.so
+out=$1; src=$2; shift 2
+base=$(basename "$src")
+mkdir -p build_var
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -Wall -Wno-unused-result \
+    -I/opt/rocm/include "$@" -c "$src" -o "build_var/$base.o"
+objs=$(ls build/*.o | grep -v "/$base.o$")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" $objs "build_var/$base.o" -ldl
