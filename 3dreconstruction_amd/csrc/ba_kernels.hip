@@ -1776,45 +1776,51 @@ __global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
 }
 
 // Long product-term lists, pass 1: one workgroup per kReduceSeg-term segment,
-// one term per thread (all <= 36 elements of the block in registers), the
-// partial blocks combined by xor-butterflies and wave order (fixed).
+// each wave a quarter of it with one lane per element of the target block
+// (the loop preduce_kernel runs: the lanes of a term read its two Z rows
+// together, 4 terms' loads in flight), the wave partials added in wave order
+// (fixed, so deterministic).
 __global__ __launch_bounds__(256) void preduce_seg_kernel(DevProblem P) {
     const int sg = blockIdx.x;
     const int j = P.plseg[2 * sg], k0 = P.plseg[2 * sg + 1];
     const ReduceTarget T = P.targets[P.plong_targets[j]];
     const int E = T.rows * T.cols;
     const bool vec = T.cols == 1;
-    double s[36];
+    const int wave = threadIdx.x >> 6, e = threadIdx.x & 63;
+    constexpr int kQ = kReduceSeg / 4;
+    const int q0 = k0 + wave * kQ, q1 = min(min(k0 + kReduceSeg, (int)T.p_end), q0 + kQ);
+    double s = 0.0;
+    if (e < E) {
+        const int r = e / T.cols, cc = vec ? 0 : e % T.cols;
+        const double* Z = P.Z;
+        int q = q0;
+        for (; q + 4 <= q1; q += 4) {
+            double a[4][3], bb[4][3];
 #pragma unroll
-    for (int e = 0; e < 36; ++e) s[e] = 0.0;
-    const int k = k0 + (int)threadIdx.x;
-    if (k < T.p_end && k - k0 < kReduceSeg) {
-        const PTerm pt = P.pterms[k];
-        double a[18], b[18];
+            for (int t = 0; t < 4; ++t) {
+                const PTerm pt = P.pterms[q + t];
 #pragma unroll
-        for (int e = 0; e < 18; ++e) {
-            a[e] = e < 3 * T.rows ? P.Z[pt.za + e] : 0.0;
-            b[e] = e < (vec ? 3 : 3 * T.cols) ? P.Z[pt.zb + e] : 0.0;
-        }
-#pragma unroll
-        for (int e = 0; e < 36; ++e) {
-            if (e < E) {
-                const int r = e / T.cols, cc = vec ? 0 : e % T.cols;
-                s[e] = a[3 * r] * b[3 * cc] + a[3 * r + 1] * b[3 * cc + 1] + a[3 * r + 2] * b[3 * cc + 2];
+                for (int k = 0; k < 3; ++k) {
+                    a[t][k] = Z[pt.za + 3 * r + k];
+                    bb[t][k] = Z[pt.zb + 3 * cc + k];
+                }
             }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) s += a[t][0] * bb[t][0] + a[t][1] * bb[t][1] + a[t][2] * bb[t][2];
+        }
+        for (; q < q1; ++q) {
+            const PTerm pt = P.pterms[q];
+            const double* za = Z + pt.za + 3 * r;
+            const double* zb = Z + pt.zb + 3 * cc;
+            s += za[0] * zb[0] + za[1] * zb[1] + za[2] * zb[2];
         }
     }
-    wave_sum(s);
-    __shared__ double part[4][36];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
-#pragma unroll
-        for (int e = 0; e < 36; ++e) part[wave][e] = s[e];
-    }
+    __shared__ double part[4][64];
+    part[wave][e] = s;
     __syncthreads();
     if ((int)threadIdx.x < E) {
-        const int e = threadIdx.x;
-        P.plpart[(size_t)sg * 36 + e] = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
+        const int t = threadIdx.x;
+        P.plpart[(size_t)sg * 36 + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
     }
 }
 

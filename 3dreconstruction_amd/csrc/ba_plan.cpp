@@ -37,6 +37,15 @@ void parallel_ranges(int64_t n, F&& fn) {
     for (auto& x : th) x.join();
 }
 
+// fn(g) for g in [0, nseg) on nseg host threads (each g writes its own outputs)
+template <class F>
+void parallel_segments(int nseg, F&& fn) {
+    std::vector<std::thread> th;
+    for (int g = 1; g < nseg; ++g) th.emplace_back([&, g] { fn(g); });
+    if (nseg > 0) fn(0);
+    for (auto& x : th) x.join();
+}
+
 // block half-bandwidth of the points' camera spans under the order cam_blk
 int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk) {
     int32_t Dt[16] = {0};
@@ -650,6 +659,10 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         pl.n_z = pl.gz_off[pl.n_gpt];
     }
     tm.mark("general");
+    // the observation arrays are final from here on: the caller may start
+    // their upload while the reduce plan is built
+    if (pl.on_shard_ready) pl.on_shard_ready(pl);
+    tm.mark("shard_ready");
     pl.schur_flops = flops;
     pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +
                      (int64_t)pl.chunks.size() * kTileR * kTileR * 8;
@@ -713,19 +726,35 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         q.kind = kSrcUcn;
         cterms.push_back({t.first, q});
     }
-    // chunk tiles
-    for (int32_t c = 0; c < (int32_t)pl.chunks.size(); ++c) {
-        const ChunkDesc& cd = pl.chunks[c];
-        for (int a = 0; a < cd.n_slots; ++a) {
-            const int32_t fa = fb_of_col(cd.slot_col[a]);
-            // rhs contribution (-Z w) from tile row 79
-            vterms.push_back({fa, ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}});
-            for (int b = 0; b < cd.n_slots; ++b) {
-                const int32_t fb = fb_of_col(cd.slot_col[b]);
-                if (fa < fb) continue;
-                mterms.push_back({(int64_t)fa * nFB + fb,
-                                  ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f}});
+    // chunk tiles: fixed chunk ranges on host threads, appended in chunk order
+    {
+        const int32_t nch = (int32_t)pl.chunks.size();
+        const int nseg = nch >= 1024 ? 16 : 1;
+        std::vector<std::vector<std::pair<int64_t, ReduceTerm>>> sm(nseg), sv(nseg);
+        parallel_segments(nseg, [&](int g) {
+            const int32_t c0 = (int32_t)((int64_t)nch * g / nseg), c1 = (int32_t)((int64_t)nch * (g + 1) / nseg);
+            for (int32_t c = c0; c < c1; ++c) {
+                const ChunkDesc& cd = pl.chunks[c];
+                for (int a = 0; a < cd.n_slots; ++a) {
+                    const int32_t fa = fb_of_col(cd.slot_col[a]);
+                    // rhs contribution (-Z w) from tile row 79
+                    sv[g].push_back({fa, ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}});
+                    for (int b = 0; b < cd.n_slots; ++b) {
+                        const int32_t fb = fb_of_col(cd.slot_col[b]);
+                        if (fa < fb) continue;
+                        sm[g].push_back({(int64_t)fa * nFB + fb,
+                                         ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f}});
+                    }
+                }
             }
+        });
+        size_t nm = mterms.size(), nv = vterms.size();
+        for (int g = 0; g < nseg; ++g) { nm += sm[g].size(); nv += sv[g].size(); }
+        mterms.reserve(nm);
+        vterms.reserve(nv);
+        for (int g = 0; g < nseg; ++g) {
+            mterms.insert(mterms.end(), sm[g].begin(), sm[g].end());
+            vterms.insert(vterms.end(), sv[g].begin(), sv[g].end());
         }
     }
     // general points
@@ -739,20 +768,33 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 mprod.push_back({(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}});
         }
     }
-    // stable by key: a counting sort over the block-pair keys (< nFB^2) when
-    // they fit a count array, else std::stable_sort (the same order)
+    // stable by key (the order std::stable_sort gives): a counting pass over
+    // 4096 buckets of contiguous key ranges (the key's high bits), then a
+    // stable sort inside every bucket on the host threads
     auto sort_terms = [&](auto& v) {
         using E = typename std::decay_t<decltype(v)>::value_type;
-        const int64_t kmax = (int64_t)nFB * nFB + 1;
-        if (kmax > ((int64_t)1 << 25) || v.size() < 4096) {
-            std::stable_sort(v.begin(), v.end(), [](const E& x, const E& y) { return x.first < y.first; });
+        auto less = [](const E& x, const E& y) { return x.first < y.first; };
+        if (v.size() < 4096) {
+            std::stable_sort(v.begin(), v.end(), less);
             return;
         }
-        std::vector<int32_t> cnt((size_t)kmax + 1, 0);
-        for (const E& e : v) cnt[(size_t)e.first + 1]++;
-        for (int64_t k = 0; k < kmax; ++k) cnt[(size_t)k + 1] += cnt[(size_t)k];
+        int64_t kmax = 0;
+        for (const E& e : v) kmax = std::max(kmax, e.first);
+        int sh = 0;
+        while ((kmax >> sh) >= 4096) ++sh;
+        const int nbk = (int)(kmax >> sh) + 1;
+        std::vector<int64_t> cnt(nbk + 1, 0);
+        for (const E& e : v) cnt[(e.first >> sh) + 1]++;
+        for (int b = 0; b < nbk; ++b) cnt[b + 1] += cnt[b];
         std::vector<E> out(v.size());
-        for (const E& e : v) out[(size_t)cnt[(size_t)e.first]++] = e;
+        {
+            std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+            for (const E& e : v) out[pos[e.first >> sh]++] = e;
+        }
+        parallel_segments(16, [&](int g) {
+            for (int b = (int)((int64_t)nbk * g / 16); b < (int)((int64_t)nbk * (g + 1) / 16); ++b)
+                std::stable_sort(out.begin() + cnt[b], out.begin() + cnt[b + 1], less);
+        });
         v.swap(out);
     };
     tm.mark("terms");

@@ -1,6 +1,7 @@
 // Host-side planning of a BA problem for the gfx950 kernels.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "../../include/sfmcore.h"
@@ -58,6 +59,9 @@ struct BAHostPlan {
     std::vector<PTerm> pterms;
     int64_t n_sband = 0, n_sarrow = 0, n_scorner = 0;
     int64_t schur_flops = 0;    // algorithmic flops of one Schur pass
+    // called by build_plan once pt_off / obs_img / obs_slot / obs_uv are final
+    // (their upload then overlaps the rest of the planning)
+    std::function<void(BAHostPlan&)> on_shard_ready;
     int64_t schur_bytes = 0;    // algorithmic HBM bytes of one Schur pass
 };
 

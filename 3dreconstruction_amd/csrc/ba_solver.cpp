@@ -92,12 +92,15 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     hipStream_t s = ctx->stream;
     BAHostPlan& h = pl->hp;
     PhaseTimer tm("create_plan");
+    h.on_shard_ready = [&](BAHostPlan& hp) {
+        up(pl->pt_off, hp.pt_off, s);
+        up(pl->obs_img, hp.obs_img, s);
+        up(pl->obs_slot, hp.obs_slot, s);
+        up(pl->obs_uv, hp.obs_uv, s);
+    };
     build_plan(prob, ctx->rank, ctx->world, h);
+    h.on_shard_ready = nullptr;
     tm.mark("build_plan");
-    up(pl->pt_off, h.pt_off, s);
-    up(pl->obs_img, h.obs_img, s);
-    up(pl->obs_slot, h.obs_slot, s);
-    up(pl->obs_uv, h.obs_uv, s);
     up(pl->chunks, h.chunks, s);
     up(pl->img_obs_ptr, h.img_obs_ptr, s);
     pl->img_pt.alloc(std::max<int64_t>(h.n_sobs, 1));
