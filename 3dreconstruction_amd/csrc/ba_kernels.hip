@@ -1740,87 +1740,87 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
 // per general point) go through preduce_seg_kernel + preduce_long_kernel.
 constexpr int kLongPTerms = 64;
 
-__global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int e = threadIdx.x & 63;
-    if (t >= P.n_targets) return;
-    const ReduceTarget T = P.targets[t];
-    if (T.p_end == T.p_begin || T.p_end - T.p_begin > kLongPTerms || e >= T.rows * T.cols) return;
-    const int r = e / T.cols, cc = e % T.cols;
-    const bool vec = T.cols == 1;
+// sum over the product terms q = q0, q0 + G, q0 + 2G, ... < q1 of
+// Z_a[3r..3r+2] . Z_b[3cc..3cc+2], four terms' loads in flight
+__device__ __forceinline__ double pterm_sum(const DevProblem& P, int q0, int q1, int G, int r, int cc) {
     const double* Z = P.Z;
     double s = 0.0;
-    int q = T.p_begin;
-    for (; q + 4 <= T.p_end; q += 4) {   // 4 terms' loads in flight, sums in order
+    int q = q0;
+    for (; q + 3 * G < q1; q += 4 * G) {
         double a[4][3], bb[4][3];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const PTerm pt = P.pterms[q + j];
+        for (int t = 0; t < 4; ++t) {
+            const PTerm pt = P.pterms[q + t * G];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                a[j][k] = Z[pt.za + 3 * r + k];
-                bb[j][k] = Z[pt.zb + (vec ? 0 : 3 * cc) + k];
+                a[t][k] = Z[pt.za + 3 * r + k];
+                bb[t][k] = Z[pt.zb + 3 * cc + k];
             }
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s += a[j][0] * bb[j][0] + a[j][1] * bb[j][1] + a[j][2] * bb[j][2];
+        for (int t = 0; t < 4; ++t) s += a[t][0] * bb[t][0] + a[t][1] * bb[t][1] + a[t][2] * bb[t][2];
     }
-    for (; q < T.p_end; ++q) {
+    for (; q < q1; q += G) {
         const PTerm pt = P.pterms[q];
         const double* za = Z + pt.za + 3 * r;
-        const double* zb = Z + pt.zb + (vec ? 0 : 3 * cc);
+        const double* zb = Z + pt.zb + 3 * cc;
         s += za[0] * zb[0] + za[1] * zb[1] + za[2] * zb[2];
     }
-    double* dst = target_base(P, T.dst_kind) + T.dst + (vec ? r : (int64_t)r * T.ld + cc);
-    *dst -= s;
+    return s;
+}
+
+// One wave per target: its E = rows x cols elements are computed by
+// G = 64 / E lane groups, group g summing terms g, g + G, ... (a 6-vector
+// target keeps 60 lanes busy, a 6x6 block 36); the group partials are then
+// added in group order (fixed, so deterministic).
+__global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + wave;
+    __shared__ double part[4][64];
+    ReduceTarget T{};
+    bool act = t < P.n_targets;
+    if (act) {
+        T = P.targets[t];
+        act = T.p_end > T.p_begin && T.p_end - T.p_begin <= kLongPTerms;
+    }
+    if (!act) return;   // whole waves only: the exchange below is wave-local
+    const int E = T.rows * T.cols, G = 64 / E, g = lane / E, e = lane - g * E;
+    const bool vec = T.cols == 1;
+    double s = 0.0;
+    if (g < G) s = pterm_sum(P, T.p_begin + g, T.p_end, G, e / T.cols, vec ? 0 : e % T.cols);
+    part[wave][lane] = s;
+    wsync();
+    if (lane < E) {
+        double tot = 0.0;
+        for (int k = 0; k < G; ++k) tot += part[wave][k * E + lane];
+        const int r = lane / T.cols, cc = lane % T.cols;
+        target_base(P, T.dst_kind)[T.dst + (vec ? r : (int64_t)r * T.ld + cc)] -= tot;
+    }
 }
 
 // Long product-term lists, pass 1: one workgroup per kReduceSeg-term segment,
-// each wave a quarter of it with one lane per element of the target block
-// (the loop preduce_kernel runs: the lanes of a term read its two Z rows
-// together, 4 terms' loads in flight), the wave partials added in wave order
-// (fixed, so deterministic).
+// each wave a quarter of it, laid out as in preduce_kernel (G lane groups of
+// E elements); the partials added in (wave, group) order, fixed.
 __global__ __launch_bounds__(256) void preduce_seg_kernel(DevProblem P) {
     const int sg = blockIdx.x;
     const int j = P.plseg[2 * sg], k0 = P.plseg[2 * sg + 1];
     const ReduceTarget T = P.targets[P.plong_targets[j]];
-    const int E = T.rows * T.cols;
+    const int E = T.rows * T.cols, G = 64 / E;
     const bool vec = T.cols == 1;
-    const int wave = threadIdx.x >> 6, e = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane / E, e = lane - g * E;
     constexpr int kQ = kReduceSeg / 4;
     const int q0 = k0 + wave * kQ, q1 = min(min(k0 + kReduceSeg, (int)T.p_end), q0 + kQ);
     double s = 0.0;
-    if (e < E) {
-        const int r = e / T.cols, cc = vec ? 0 : e % T.cols;
-        const double* Z = P.Z;
-        int q = q0;
-        for (; q + 4 <= q1; q += 4) {
-            double a[4][3], bb[4][3];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const PTerm pt = P.pterms[q + t];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    a[t][k] = Z[pt.za + 3 * r + k];
-                    bb[t][k] = Z[pt.zb + 3 * cc + k];
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) s += a[t][0] * bb[t][0] + a[t][1] * bb[t][1] + a[t][2] * bb[t][2];
-        }
-        for (; q < q1; ++q) {
-            const PTerm pt = P.pterms[q];
-            const double* za = Z + pt.za + 3 * r;
-            const double* zb = Z + pt.zb + 3 * cc;
-            s += za[0] * zb[0] + za[1] * zb[1] + za[2] * zb[2];
-        }
-    }
+    if (g < G) s = pterm_sum(P, q0 + g, q1, G, e / T.cols, vec ? 0 : e % T.cols);
     __shared__ double part[4][64];
-    part[wave][e] = s;
+    part[wave][lane] = s;
     __syncthreads();
     if ((int)threadIdx.x < E) {
         const int t = threadIdx.x;
-        P.plpart[(size_t)sg * 36 + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+        double tot = 0.0;
+        for (int w = 0; w < 4; ++w)
+            for (int k = 0; k < G; ++k) tot += part[w][k * E + t];
+        P.plpart[(size_t)sg * 36 + t] = tot;
     }
 }
 
