@@ -2,9 +2,11 @@
 last timed solve's dispatches in order with their durations and the idle gap
 before each, plus totals (kernel time vs wall)."""
 import csv
+import gzip
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+f = sys.argv[1]
+rows = list(csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ks = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
 # the timed solves: schur launches mark iterations; take the span from the
@@ -13,9 +15,10 @@ starts = [i for i, k in enumerate(ks) if "gram_rescale" in k[0]]
 if len(starts) < 2:
     print("no solves found")
     sys.exit(0)
-a, b = starts[-2], starts[-1]
+# the timed solves run back to back: the shortest span between two starts
+a, b = min(zip(starts, starts[1:]), key=lambda ab: ks[ab[1]][1] - ks[ab[0]][1])
 seg = ks[a:b]
-short = lambda n: n.split("(")[0].replace("sfm::(anonymous namespace)::", "").replace("void ", "")[:48]
+short = lambda n: n.replace("sfm::(anonymous namespace)::", "").replace("void ", "").split("(")[0][:48]
 tot_k = sum(e - s for _, s, e in seg)
 wall = seg[-1][2] - seg[0][1]
 print(f"one solve: {len(seg)} dispatches, kernel {tot_k / 1e3:.1f} us, wall {wall / 1e3:.1f} us, "
