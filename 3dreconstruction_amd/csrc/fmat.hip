@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kFT) void fmatrix_ac_kernel(FArgs a) {
     __shared__ int s_redk[kFT / 64];
     __shared__ int s_nm, s_m, s_cnt, s_ac, s_upd, s_copy, s_stop;
     __shared__ uint32_t s_sample[kSample];
-    __shared__ int64_t s_nIter, s_nIterReserve, s_vsize, s_ninl, s_iter;
+    __shared__ int64_t s_nIter, s_nIterReserve, s_vsize, s_ninl;
     __shared__ double s_minNFA, s_errorMax;
 
     // ---- prologue: log10 table, logcombi tables, vec_index --------------------

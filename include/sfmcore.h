@@ -537,7 +537,9 @@ typedef struct sfm_fmatrix_result {
  * (width_I, height_I, width_J, height_J).  inliers[off[q] + t],
  * t < results[q].n_inliers: the kept correspondences (indices into the pair's
  * list) in OpenMVG's vec_inliers order (ascending residual).  opts NULL =
- * {4.0, 2048}.  A pair with more than 16384 correspondences returns
+ * {4.0, 2048}.  Pairs of any size (sort buffers move from LDS to global
+ * memory above 8192 correspondences); a pair whose RANSAC would draw more than
+ * 2^18 random numbers (2048 iterations draw about 15,000) returns
  * SFM_ERR_UNSUPPORTED. */
 int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off, const double* xy,
                    const int32_t* wh, const sfm_fmatrix_opts* opts,
