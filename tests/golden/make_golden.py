@@ -102,6 +102,7 @@ def write_ba_pin(name, model):
 def write_ba_pins():
     n = write_ba_pin("ba_c1_oracle.json", 0)
     write_ba_pin("ba_c1_snavely_oracle.json", 1)   # SnavelyReprojectionError.h model
+    write_ba_pin("ba_c1_radial3_oracle.json", 2)   # OpenMVG PINHOLE_CAMERA_RADIAL3
     return n
 
 

@@ -159,3 +159,20 @@ def test_radial3_gpu_shapes(ctx, args):
 def test_radial3_gpu_c2(ctx):
     sc = H.Scene(200, 50_000, 10, model=R3, seed=0x5F3D0002)
     _compare(ctx, sc)
+
+
+def test_radial3_regression_pin_c1():
+    # the oracle's C1 trajectory under RADIAL3 (tests/golden/make_golden.py
+    # --ba-only regenerates it; the pinhole and Snavely pins came out
+    # byte-identical after the 6-wide intrinsics generalisation of the oracle)
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ba_c1_radial3_oracle.json")))
+    sc = H.Scene(g["scene"]["n_cam"], g["scene"]["n_pt"], g["scene"]["k"], seed=g["scene"]["seed"], model=R3)
+    rc, s, tr, _ = H.oracle_solve(sc, threads=1)
+    assert rc == g["rc"] and s.iterations == g["iterations"]
+    assert s.successful_steps == g["successful_steps"]
+    assert abs(s.final_cost / g["final_cost"] - 1) < 1e-9
+    for t, gt in zip(tr, g["trace"]):
+        assert [t.iteration, t.step_is_valid, t.step_is_successful] == gt[:3]
+        assert abs(t.cost / gt[3] - 1) < 1e-9

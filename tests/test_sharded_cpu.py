@@ -52,7 +52,8 @@ def _worker(rank, world, port, out_path, scene_args):
 
 
 @pytest.mark.parametrize("scene_args", [dict(n_cam=16, n_pt=1200, k=4, seed=101),
-                                        dict(n_cam=20, n_pt=1500, k=5, vis_mode=1, seed=5)])
+                                        dict(n_cam=20, n_pt=1500, k=5, vis_mode=1, seed=5),
+                                        dict(n_cam=20, n_pt=2000, k=5, n_intr=2, seed=9, model=2)])
 def test_two_rank_sharded_solve_matches_single(tmp_path, scene_args):
     import _helpers as H
     out = str(tmp_path / "r.npz")
