@@ -700,6 +700,24 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     auto size_of_fb = [&](int32_t b) { return b < pl.ncam ? 6 : pl.iw; };
     std::vector<std::pair<int64_t, ReduceTerm>> mterms, vterms;
     std::vector<std::pair<int64_t, PTerm>> mprod, vprod;
+    {
+        // exact capacities: one growth-free allocation per list (the lists
+        // are fresh memory, so every reallocation is page faults again)
+        size_t nm = 3 * (size_t)kGramSeg * P.n_img, nv = 2 * (size_t)kGramSeg * P.n_img, npm = 0, npv = 0;
+        for (const ChunkDesc& cd : pl.chunks) {
+            nm += (size_t)cd.n_slots * (cd.n_slots + 1) / 2;
+            nv += (size_t)cd.n_slots;
+        }
+        for (int64_t g = 0; g < pl.n_gpt; ++g) {
+            const size_t b = (size_t)(pl.gblk_off[g + 1] - pl.gblk_off[g]);
+            npm += b * (b + 1) / 2;
+            npv += b;
+        }
+        mterms.reserve(nm);
+        vterms.reserve(nv);
+        mprod.reserve(npm);
+        vprod.reserve(npv);
+    }
     // image Gram blocks (kGramSeg partial slices per image)
     auto add_u = [&](std::vector<std::pair<int64_t, ReduceTerm>>& out, int64_t key, int32_t kind, int img,
                      int16_t ro, int16_t co) {
@@ -719,6 +737,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             add_u(vterms, fq, kSrcUb, img, 6, 0);
         }
     }
+    tm.mark("terms_images");
     // cnF: per block, image slices only (never a tile term)
     std::vector<std::pair<int64_t, ReduceTerm>> cterms;
     for (const auto& t : vterms) {
@@ -726,10 +745,11 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         q.kind = kSrcUcn;
         cterms.push_back({t.first, q});
     }
+    tm.mark("terms_cnf");
     // chunk tiles: fixed chunk ranges on host threads, appended in chunk order
     {
         const int32_t nch = (int32_t)pl.chunks.size();
-        const int nseg = nch >= 1024 ? 16 : 1;
+        const int nseg = nch >= 2048 ? 16 : 1;
         std::vector<std::vector<std::pair<int64_t, ReduceTerm>>> sm(nseg), sv(nseg);
         parallel_segments(nseg, [&](int g) {
             const int32_t c0 = (int32_t)((int64_t)nch * g / nseg), c1 = (int32_t)((int64_t)nch * (g + 1) / nseg);
@@ -757,6 +777,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             vterms.insert(vterms.end(), sv[g].begin(), sv[g].end());
         }
     }
+    tm.mark("terms_tiles");
     // general points
     for (int64_t g = 0; g < pl.n_gpt; ++g) {
         const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
@@ -768,34 +789,34 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 mprod.push_back({(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}});
         }
     }
-    // stable by key (the order std::stable_sort gives): a counting pass over
-    // 4096 buckets of contiguous key ranges (the key's high bits), then a
-    // stable sort inside every bucket on the host threads
+    // stable by key (the order std::stable_sort gives): LSD radix passes of
+    // 11-bit digits over the key (one pass for small problems, two at C4)
     auto sort_terms = [&](auto& v) {
         using E = typename std::decay_t<decltype(v)>::value_type;
         auto less = [](const E& x, const E& y) { return x.first < y.first; };
-        if (v.size() < 4096) {
+        int64_t kmax = 0;
+        for (const E& e : v) kmax = std::max(kmax, e.first);
+        int bits = 0;
+        while (bits < 63 && (kmax >> bits) != 0) ++bits;
+        if (v.size() < 2048 || bits > 44) {
             std::stable_sort(v.begin(), v.end(), less);
             return;
         }
-        int64_t kmax = 0;
-        for (const E& e : v) kmax = std::max(kmax, e.first);
-        int sh = 0;
-        while ((kmax >> sh) >= 4096) ++sh;
-        const int nbk = (int)(kmax >> sh) + 1;
-        std::vector<int64_t> cnt(nbk + 1, 0);
-        for (const E& e : v) cnt[(e.first >> sh) + 1]++;
-        for (int b = 0; b < nbk; ++b) cnt[b + 1] += cnt[b];
-        std::vector<E> out(v.size());
-        {
-            std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
-            for (const E& e : v) out[pos[e.first >> sh]++] = e;
+        constexpr int kD = 11;
+        const int passes = std::max(1, (bits + kD - 1) / kD);
+        std::vector<E> tmp(v.size());
+        E* src = v.data();
+        E* dst = tmp.data();
+        const size_t n = v.size();
+        for (int p = 0; p < passes; ++p) {
+            const int sh = p * kD;
+            std::vector<int64_t> cnt((1 << kD) + 1, 0);
+            for (size_t k = 0; k < n; ++k) cnt[((src[k].first >> sh) & ((1 << kD) - 1)) + 1]++;
+            for (int d = 0; d < (1 << kD); ++d) cnt[d + 1] += cnt[d];
+            for (size_t k = 0; k < n; ++k) dst[cnt[(src[k].first >> sh) & ((1 << kD) - 1)]++] = src[k];
+            std::swap(src, dst);
         }
-        parallel_segments(16, [&](int g) {
-            for (int b = (int)((int64_t)nbk * g / 16); b < (int)((int64_t)nbk * (g + 1) / 16); ++b)
-                std::stable_sort(out.begin() + cnt[b], out.begin() + cnt[b + 1], less);
-        });
-        v.swap(out);
+        if (src != v.data()) v.swap(tmp);
     };
     tm.mark("terms");
     sort_terms(mterms);
@@ -812,6 +833,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         pl.n_scorner = (int64_t)pl.nintr * pl.nintr * 16;
     }
     size_t im = 0, ipm = 0, iv = 0, ipv = 0, ic = 0;
+    // every term lands in one target (the corner's transposed copies aside)
+    pl.terms.reserve(mterms.size() + 2 * vterms.size() + cterms.size());
+    pl.pterms.reserve(mprod.size() + vprod.size());
     auto emit = [&](int64_t key, int32_t kind, int64_t dst, int rows, int cols, int ld,
                     std::vector<std::pair<int64_t, ReduceTerm>>& st, size_t& is,
                     std::vector<std::pair<int64_t, PTerm>>* pt, size_t* ip) {

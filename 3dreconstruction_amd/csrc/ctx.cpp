@@ -1,5 +1,6 @@
 // Context management, error reporting and the run-time RCCL binding.
 #include <dlfcn.h>
+#include <malloc.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -272,6 +273,26 @@ extern "C" int sfm_comm_unique_id(uint8_t* out128) {
     });
 }
 
+namespace {
+// Unmapping a large host allocation makes the GPU driver invalidate the
+// process's device-visible mappings, and the next GPU operation of the process
+// waits for it: 12-27 ms after a bundle adjustment freed its ~100 MB of
+// planner arrays, which the C5 loop paid before every image's match
+// (tools/match_latency.py).  glibc serves allocations above its mmap
+// threshold (128 KB, adaptive) with mmap / munmap; raising the threshold and
+// the trim threshold keeps freed blocks in the heap for reuse instead.
+// Once per process; SFM_KEEP_MALLOC=1 leaves the host application's malloc
+// settings alone.
+void tune_host_malloc() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (std::getenv("SFM_KEEP_MALLOC")) return;
+        mallopt(M_MMAP_THRESHOLD, 1 << 30);
+        mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    });
+}
+}  // namespace
+
 extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
     return guarded([&] {
         SFM_REQUIRE(opts && out, SFM_ERR_INVALID_ARG, "null argument");
@@ -289,6 +310,7 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         SFM_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, SFM_ERR_DEVICE,
                     "device %d is %s; this build targets gfx950 (MI355X) only", opts->device,
                     prop.gcnArchName);
+        tune_host_malloc();
         auto* c = new sfm_ctx;
         c->device = opts->device;
         c->rank = opts->rank;

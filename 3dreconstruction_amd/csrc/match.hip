@@ -341,7 +341,9 @@ struct sfm_match_plan {
 
 namespace {
 
-void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* off, int32_t n_img) {
+// srcs (optional): image i's rows start at srcs[i] instead of desc + 128 off[i]
+void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* off, int32_t n_img,
+                       const uint8_t* const* srcs = nullptr) {
     hipStream_t s = p->ctx->stream;
     p->n_img = n_img;
     p->row0.resize(n_img);
@@ -363,11 +365,15 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
         SFM_HIP(hipStreamSynchronize(s));
         tm.mark("presync");
     }
-    std::vector<uint8_t> staging((size_t)rows * 128, 128);  // pad rows -> a' = 0
-    std::vector<int64_t> rstart(rows, 0);
-    std::vector<int32_t> rvalid(rows, 0);
+    // page-locked staging from the context's host cache (a pageable source
+    // made each upload of a 300-image loop's collection cost milliseconds)
+    HostVec<uint8_t> staging((size_t)rows * 128, 128);  // pad rows -> a' = 0
+    HostVec<int64_t> rstart(rows, 0);
+    HostVec<int32_t> rvalid(rows, 0);
     for (int i = 0; i < n_img; ++i) {
-        std::memcpy(&staging[(size_t)p->row0[i] * 128], desc + off[i] * 128, (size_t)p->nrows[i] * 128);
+        if (p->nrows[i])
+            std::memcpy(&staging[(size_t)p->row0[i] * 128], srcs ? srcs[i] : desc + off[i] * 128,
+                        (size_t)p->nrows[i] * 128);
         const int64_t padded = (p->nrows[i] + kRowPad - 1) / kRowPad * kRowPad;
         for (int64_t r = 0; r < padded; ++r) {
             rstart[p->row0[i] + r] = p->row0[i];
@@ -724,14 +730,12 @@ extern "C" int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a, cons
                     SFM_ERR_INVALID_ARG, "bad arguments");
         CtxScope scope_(ctx);
         PhaseTimer tm("sfm_match_dense");
-        std::vector<uint8_t> desc((size_t)(n_a + n_b) * 128);
-        if (n_a) std::memcpy(desc.data(), a, (size_t)n_a * 128);
-        if (n_b) std::memcpy(desc.data() + (size_t)n_a * 128, b, (size_t)n_b * 128);
         const int64_t off[3] = {0, n_a, (int64_t)n_a + n_b};
+        const uint8_t* srcs[2] = {a, b};
         sfm_match_plan plan;
         plan.ctx = ctx;
         tm.mark("stage");
-        upload_collection(&plan, desc.data(), off, 2);
+        upload_collection(&plan, nullptr, off, 2, srcs);
         tm.mark("upload");
         const int32_t pair[2] = {0, 1};
         run_pairs(&plan, pair, 1, o, false);

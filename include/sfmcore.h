@@ -77,6 +77,11 @@ typedef struct sfm_ctx_opts {
 
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
 int sfm_comm_unique_id(uint8_t* out128);
+/* The first context of a process raises glibc's mmap and trim thresholds
+ * (mallopt, 1 GB): unmapping large host buffers stalls the process's next GPU
+ * operation for 10-30 ms while the driver invalidates its mappings, which an
+ * incremental loop (BA, then matching, per image) would pay every step.  Set
+ * SFM_KEEP_MALLOC=1 to keep the host application's malloc settings. */
 int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out);
 int sfm_ctx_destroy(sfm_ctx* ctx);
 int sfm_ctx_synchronize(sfm_ctx* ctx);
