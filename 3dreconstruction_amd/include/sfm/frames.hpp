@@ -6,6 +6,7 @@
 #pragma once
 #include <algorithm>
 #include <cstddef>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -60,18 +61,18 @@ class GlobalFrame {
    public:
     // world points in index order (the reference iterates its unordered_map,
     // GlobalFrame.h:16-20; index order is the deterministic choice)
-    GlobalFrame(const WorldStructure::Ptr& world, Image::Ptr image) : image_(std::move(image)) {
-        std::vector<std::pair<WorldPoint::Idx, WorldPoint::Ptr>> pts(world->world_points_.begin(),
-                                                                     world->world_points_.end());
-        std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
-        for (auto& p : pts) world_points_.push_back(p.second);
-    }
+    // (the world outlives the frame: it keeps the world's index-ordered list)
+    GlobalFrame(const WorldStructure::Ptr& world, Image::Ptr image)
+        : image_(std::move(image)), world_points_(&world->pointsByIdx()) {}
     // query = every world point's last_descriptor_, train = the image (:22-43)
     template <class M> std::size_t matchFeature(M& matcher) {
         matches_.clear();
-        std::vector<uint8_t> q;
-        q.reserve(world_points_.size() * 128);
-        for (auto& p : world_points_) q.insert(q.end(), p->last_descriptor_.begin(), p->last_descriptor_.end());
+        std::vector<uint8_t> q(world_points_->size() * 128);
+        uint8_t* dst = q.data();
+        for (const auto& p : *world_points_) {
+            std::memcpy(dst, p->last_descriptor_.data(), std::min<std::size_t>(128, p->last_descriptor_.size()));
+            dst += 128;
+        }
         std::vector<std::vector<DMatch>> v;
         matcher.knnMatch(q, image_->descriptors, v, 1);
         for (auto& row : v)
@@ -95,13 +96,13 @@ class GlobalFrame {
         matches_ = filterMatches();
         return matches_.size();
     }
-    const std::vector<WorldPoint::Ptr>& get_world_points() const { return world_points_; }
+    const std::vector<WorldPoint::Ptr>& get_world_points() const { return *world_points_; }
     const std::vector<DMatch>& getMatches() const { return matches_; }
 
    private:
     std::vector<DMatch> matches_;
     Image::Ptr image_;
-    std::vector<WorldPoint::Ptr> world_points_;
+    const std::vector<WorldPoint::Ptr>* world_points_;
     std::size_t raw_ = 0;
 };
 

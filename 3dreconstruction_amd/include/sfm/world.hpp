@@ -141,18 +141,23 @@ class WorldStructure {
         p->world_pos_ = pos;
         p->last_descriptor_ = std::move(descriptor);
         world_points_[p->idx_] = p;
+        by_idx_.push_back(p);
         return p->idx_;
     }
     void addLocalFrame(std::shared_ptr<LocalFrame> f) { local_frames_.push_back(std::move(f)); }
     const std::vector<std::shared_ptr<LocalFrame>>& getLocalFrames() const { return local_frames_; }
     WorldPoint::Ptr getPointFromIdx(WorldPoint::Idx i) const { return world_points_.at(i); }
     const std::unordered_map<WorldPoint::Idx, WorldPoint::Ptr>& points() const { return world_points_; }
+    // the same points in index order (points are only ever added, with
+    // increasing indices): what GlobalFrame iterates, without a sort per image
+    const std::vector<WorldPoint::Ptr>& pointsByIdx() const { return by_idx_; }
 
    private:
     WorldPoint::Idx cur_idx_ = 0;
     std::vector<std::shared_ptr<LocalFrame>> local_frames_;
     std::unordered_map<Image::Idx, Image::Ptr> images_;
     std::unordered_map<WorldPoint::Idx, WorldPoint::Ptr> world_points_;
+    std::vector<WorldPoint::Ptr> by_idx_;
     template <class> friend class BasicBundleAdjuster;
     friend class GlobalFrame;
 };
