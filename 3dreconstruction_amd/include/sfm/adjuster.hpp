@@ -73,8 +73,9 @@ class BasicBundleAdjuster {
    private:
     // loadDataFromWorld (:82-98) + problem assembly (:100-123)
     void load(const WorldStructure::Ptr& world) {
+        for (const auto& im : images_) img_slot_[im->getIdx()] = -1;   // (normally cleared already)
         images_.clear(); cams_.clear(); extr_.clear(); intr_.clear();
-        img_index_.clear(); cam_index_.clear(); img_cam_.clear();
+        cam_index_.clear(); img_cam_.clear();
         auto add_cam = [&](const Camera::Ptr& c, bool zero) {
             auto it = cam_index_.find(c.get());
             if (it != cam_index_.end()) return it->second;
@@ -85,11 +86,14 @@ class BasicBundleAdjuster {
             intr_.insert(intr_.end(), v.begin(), v.end());
             return k;
         };
+        // image -> problem index by the image's own index (a vector, not a hash
+        // lookup per observation)
         auto add_img = [&](const Image::Ptr& im, bool zero_pose) {
-            auto it = img_index_.find(im.get());
-            if (it != img_index_.end()) return it->second;
+            const std::size_t id = im->getIdx();
+            if (id >= img_slot_.size()) img_slot_.resize(id + 1, -1);
+            if (img_slot_[id] >= 0) return img_slot_[id];
             const int k = (int)images_.size();
-            img_index_[im.get()] = k;
+            img_slot_[id] = k;
             images_.push_back(im);
             const auto p = zero_pose ? std::array<double, 6>{} : im->pose();
             extr_.insert(extr_.end(), p.begin(), p.end());
@@ -101,11 +105,13 @@ class BasicBundleAdjuster {
             img_cam_[k] = add_cam(f->getImage2()->getCamera(), false);
         }
         const_img_ = world->local_frames_.empty() ? -1 : 0;
-        std::vector<std::pair<WorldPoint::Idx, WorldPoint::Ptr>> pts(world->world_points_.begin(),
-                                                                     world->world_points_.end());
-        std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
+        // points in index order (the reference iterates its unordered_map)
+        const std::vector<WorldPoint::Ptr>& pts = world->pointsByIdx();
         points_.clear(); X_.clear(); off_.assign(1, 0); obs_img_.clear(); uv_.clear();
-        for (auto& [idx, p] : pts) {
+        points_.reserve(pts.size());
+        X_.reserve(3 * pts.size());
+        off_.reserve(pts.size() + 1);
+        for (const auto& p : pts) {
             points_.push_back(p);
             X_.insert(X_.end(), p->world_pos_.begin(), p->world_pos_.end());
             for (auto& [im, uv] : p->observed_frames_) {
@@ -164,6 +170,7 @@ class BasicBundleAdjuster {
             cams_[k]->setIntrinsic({intr_[4 * k], intr_[4 * k + 1], intr_[4 * k + 2], intr_[4 * k + 3]});
     }
     void clear() {  // :158-164
+        for (const auto& im : images_) img_slot_[im->getIdx()] = -1;
         images_.clear(); cams_.clear(); points_.clear();
     }
 
@@ -172,7 +179,7 @@ class BasicBundleAdjuster {
     std::vector<Image::Ptr> images_;
     std::vector<Camera::Ptr> cams_;
     std::vector<WorldPoint::Ptr> points_;
-    std::unordered_map<const Image*, int> img_index_;
+    std::vector<int> img_slot_;   // Image::getIdx() -> problem image index or -1
     std::unordered_map<const Camera*, int> cam_index_;
     std::vector<int32_t> img_cam_, obs_img_;
     std::vector<double> extr_, intr_, X_, uv_;
