@@ -390,6 +390,9 @@ __device__ __forceinline__ void reduce_scatter64(double (&v)[64], int lane) {
 #ifndef SFM_GRAM_WPE
 #define SFM_GRAM_WPE 2
 #endif
+#ifndef SFM_GRAM_DEEP   // point gathers two iterations ahead instead of one
+#define SFM_GRAM_DEEP 1
+#endif
 // PASS: which 64 slots this launch sums (RADIAL3's 91 sums take two passes,
 // each re-linearising the image's observations; the other models one).
 template <int CM, int PASS>
@@ -431,6 +434,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
 #pragma unroll
         for (int a = 0; a < 3; ++a) x[a] = p >= 0 ? X[3 * (size_t)p + a] : 0.0;
     };
+#if SFM_GRAM_DEEP
+    // three stages: the point gather (random rows of X) two iterations ahead
+    int p_c, p_n, p_nn;
+    double2 uv_c, uv_n, uv_nn;
+    double x_c[3], x_n[3];
+    fetch_ids(o0 + 64 * wave, p_c, uv_c);
+    fetch_ids(o0 + 64 * wave + 256, p_n, uv_n);
+    fetch_ids(o0 + 64 * wave + 512, p_nn, uv_nn);
+    fetch_x(p_c, x_c);
+    fetch_x(p_n, x_n);
+    for (int base = o0 + 64 * wave; base < o1; base += 256) {
+        const int p_cur = p_c;
+        const double2 uv = uv_c;
+        const double Xp[3] = {x_c[0], x_c[1], x_c[2]};
+        p_c = p_n; uv_c = uv_n;
+        x_c[0] = x_n[0]; x_c[1] = x_n[1]; x_c[2] = x_n[2];
+        p_n = p_nn; uv_n = uv_nn;
+        fetch_x(p_n, x_n);
+        fetch_ids(base + 768, p_nn, uv_nn);
+#else
     int p_c, p_n;
     double2 uv_c, uv_n;
     double x_c[3];
@@ -445,6 +468,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         p_c = p_n; uv_c = uv_n;
         fetch_x(p_c, x_c);
         fetch_ids(base + 512, p_n, uv_n);
+#endif
         // re-read the staged camera from LDS each step instead of keeping its
         // 28 doubles live across the loop (register budget of 2 waves/SIMD)
         asm volatile("" ::: "memory");
