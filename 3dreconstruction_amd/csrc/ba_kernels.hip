@@ -2,22 +2,26 @@
 //
 // Reference: src/adjuster/BundleAdjuster.h — ReprojectCost :33-69 (pinhole,
 // ceres::AngleAxisRotatePoint), HuberLoss(4) :109, ceres::Solve with
-// SPARSE_SCHUR (point blocks eliminated) :125-126, 167-174.
+// SPARSE_SCHUR (point blocks eliminated) :125-126, 167-174; residual models
+// SnavelyReprojectionError.h:16-54 and OpenMVG PINHOLE_CAMERA_RADIAL3
+// (sparseBuilder.cpp:1292-1299) through the CM template parameter.
 //
-// One LM iteration on device (DESIGN.md §BA):
+// One LM iteration on device (DESIGN.md §5):
 //   campre      per-camera rotation terms (sin/cos once per camera, not per obs)
-//   image_gram  per image (WG): U = J_F' J_F over its observations (10x10:
-//               pose 6 | intrinsics 4), b = J_F' f, cost 1/2 sum rho   [after
-//               an accepted step only]
-//   schur       per chunk (WG): observations -> corrected, Jacobi-scaled
-//               Jacobians (VALU) -> per point V + D^2, Cholesky L, w = L^-1 g
-//               -> Z = W L^-T written into an LDS panel [48 x 80] -> the 80x80
-//               chunk tile -Z Z' (and -Z w in row 79) on the fp64 MFMA
-//               (v_mfma_f64_16x16x4_f64), lower tiles only
-//   reduce      static gather plan: tiles + image blocks -> banded RCS
-//   solve       one workgroup: block-banded Cholesky with the intrinsics arrow
-//               over an LDS sliding window, forward/back substitution
-//   fvec/step   candidate cameras; per point back-substitution y_E =
+//   image_gram  per image (WGs): U = J_F' J_F over its observations (pose 6 |
+//               intrinsics 4 or 6), b = J_F' f, cost 1/2 sum rho   [after an
+//               accepted step only]
+//   schur       chunk points, per chunk (one wave): observations -> corrected,
+//               Jacobi-scaled Jacobians (VALU) -> per point V + D^2, Cholesky
+//               L, w = L^-1 g -> Z = W L^-T into an LDS panel -> the chunk tile
+//               -Z Z' (and -Z w) on the fp64 MFMA (v_mfma_f64_16x16x4_f64),
+//               lower 16x16 tiles only
+//   zpoint      general points, per point (one wave): the same elimination,
+//               Z rows to a global buffer (product terms, preduce_*)
+//   reduce      static gather plan: tiles + image blocks (+ products) -> RCS
+//   solve       band + arrow: block cyclic reduction (ba_bcr.hip; solve_kernel
+//               is the one-workgroup fallback); dense: blocked Cholesky
+//   cand/step   candidate cameras; per point back-substitution y_E =
 //               L^-T (w - Z' y_F), model cost change, candidate cost
 //   finalize    fixed-order reduction of per-block partials (deterministic)
 #include <hip/hip_runtime.h>
