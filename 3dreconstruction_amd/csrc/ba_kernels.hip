@@ -1052,35 +1052,55 @@ __device__ __forceinline__ bool skip_kind(int kind, int vectors_only) {
     return vectors_only && kind != kDstBF && kind != kDstCnF;
 }
 
+// wave-local LDS exchange: every lane's writes visible to the wave
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ void reduce_kernel(DevProblem P, int vectors_only) {
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wave = threadIdx.x >> 6;
+    const int t = blockIdx.x * 4 + wave;
     const int e = threadIdx.x & 63;
+    __shared__ double part[4][64];
     if (t >= P.n_targets) return;
     const ReduceTarget T = P.targets[t];
     if (skip_kind(T.dst_kind, vectors_only) || T.c_end - T.c_begin > kLongTerms) return;
-    if (e >= T.rows * T.cols) return;
-    const int r = e / T.cols, cc = e % T.cols;
+    // G = 64 / E lane groups of the target's E elements: group g sums terms
+    // g, g + G, ... (a 6-vector target keeps 60 lanes busy instead of 6), the
+    // group partials are then added in group order (fixed, so deterministic)
+    const int E = T.rows * T.cols, G = 64 / E, g = e / E, el = e - g * E;
+    if (g >= G) return;
+    const int r = el / T.cols, cc = el % T.cols;
     const bool vec = T.cols == 1;
-    // batches of 16 (then 4) independent loads, summed in term order
-    // (deterministic); a target is a chain of dependent global round trips
-    // (term descriptor, then data), so the batch width sets its latency
+    // batches of 16 (then 4) independent loads; a target is a chain of
+    // dependent global round trips (term descriptor, then data), so the batch
+    // width sets its latency
     double s = 0.0;
-    int k = T.c_begin;
-    for (; k + 16 <= T.c_end; k += 16) {
+    int k = T.c_begin + g;
+    for (; k + 15 * G < T.c_end; k += 16 * G) {
         double v[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = term_value(P, P.terms[k + j], r, cc);
+        for (int j = 0; j < 16; ++j) v[j] = term_value(P, P.terms[k + j * G], r, cc);
 #pragma unroll
         for (int j = 0; j < 16; ++j) s += v[j];
     }
-    for (; k + 4 <= T.c_end; k += 4) {
+    for (; k + 3 * G < T.c_end; k += 4 * G) {
         double v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = term_value(P, P.terms[k + j], r, cc);
+        for (int j = 0; j < 4; ++j) v[j] = term_value(P, P.terms[k + j * G], r, cc);
 #pragma unroll
         for (int j = 0; j < 4; ++j) s += v[j];
     }
-    for (; k < T.c_end; ++k) s += term_value(P, P.terms[k], r, cc);
+    for (; k < T.c_end; k += G) s += term_value(P, P.terms[k], r, cc);
+    if (G > 1) {
+        part[wave][e] = s;
+        wsync();
+        if (g != 0) return;
+        s = 0.0;
+        for (int q = 0; q < G; ++q) s += part[wave][q * E + el];
+    }
     double* dst;
     dst = target_base(P, T.dst_kind);
     dst[T.dst + (vec ? r : r * T.ld + cc)] = s;
@@ -1584,11 +1604,6 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
 // general point's observations by image), an intrinsics block one masked
 // wave sum per 64-observation round, rounds in order.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 constexpr int kZStage = 19;   // doubles per staged observation row (18 used, odd stride)
 
