@@ -1113,29 +1113,36 @@ __global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int vecto
     const int sg = blockIdx.x;
     const int j = P.lseg[2 * sg], k0 = P.lseg[2 * sg + 1];
     const ReduceTarget T = P.targets[P.long_targets[j]];
-    if (skip_kind(T.dst_kind, vectors_only)) return;
-    const int E = T.rows * T.cols;
-    double s[36];
+    if (skip_kind(T.dst_kind, vectors_only)) return;   // (uniform over the workgroup)
+    // each wave a quarter of the segment, in G = 64 / E lane groups of the
+    // target's E elements (as reduce_kernel); partials added in (wave, group)
+    // order, fixed
+    const int E = T.rows * T.cols, G = 64 / E;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane / E, el = lane - g * E;
+    constexpr int kQ = kReduceSeg / 4;
+    const int q0 = k0 + wave * kQ, q1 = min(min(k0 + kReduceSeg, (int)T.c_end), q0 + kQ);
+    double s = 0.0;
+    if (g < G) {
+        const int r = el / T.cols, cc = el % T.cols;
+        int k = q0 + g;
+        for (; k + 3 * G < q1; k += 4 * G) {
+            double v[4];
 #pragma unroll
-    for (int e = 0; e < 36; ++e) s[e] = 0.0;
-    const int k = k0 + (int)threadIdx.x;
-    if (k < T.c_end && k - k0 < kReduceSeg) {
-        const FlatTerm q = P.terms[k];
+            for (int t = 0; t < 4; ++t) v[t] = term_value(P, P.terms[k + t * G], r, cc);
 #pragma unroll
-        for (int e = 0; e < 36; ++e)
-            if (e < E) s[e] = term_value(P, q, e / T.cols, e % T.cols);
+            for (int t = 0; t < 4; ++t) s += v[t];
+        }
+        for (; k < q1; k += G) s += term_value(P, P.terms[k], r, cc);
     }
-    wave_sum(s);
-    __shared__ double part[4][36];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
-#pragma unroll
-        for (int e = 0; e < 36; ++e) part[wave][e] = s[e];
-    }
+    __shared__ double part[4][64];
+    part[wave][lane] = s;
     __syncthreads();
     if ((int)threadIdx.x < E) {
-        const int e = threadIdx.x;
-        P.lpart[(size_t)sg * 36 + e] = ((part[0][e] + part[1][e]) + part[2][e]) + part[3][e];
+        const int t = threadIdx.x;
+        double tot = 0.0;
+        for (int w = 0; w < 4; ++w)
+            for (int q = 0; q < G; ++q) tot += part[w][q * E + t];
+        P.lpart[(size_t)sg * 36 + t] = tot;
     }
 }
 
