@@ -805,12 +805,17 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
 //             L_kk and X_kk = L_kk^-1, MFMA) and forms L_ik = A_ik X_kk';
 //             the k-th one stores L_kk, X_kk and y_k = X_kk b_k
 //   update k  A_ij -= L_ik L_jk' for k < j <= i (one workgroup per tile, MFMA),
-//             b_i -= L_ik y_k (forward substitution, fused)
+//             b_i -= L_ik y_k (forward substitution, fused); columns go in
+//             groups of SFM_DENSE_W so the trailing tiles are read and written
+//             once per group (the update is HBM bound on those tiles)
 //   back      x_k = X_kk' y_k, then y_i -= L_ki' x_k for i < k (one launch per k)
 // ===========================================================================
 namespace {
 
 constexpr int kDM = 64;   // tile
+#ifndef SFM_DENSE_W   // block columns per trailing update
+#define SFM_DENSE_W 4
+#endif
 
 __global__ __launch_bounds__(256) void dense_pack_kernel(DenseArgs d, DevProblem P, double radius) {
     const int64_t np = d.np;
@@ -878,45 +883,70 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
     }
 }
 
-// trailing update of column k: tiles (i, j), k < j <= i, plus rhs tiles
-__global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k, int n_tiles) {
+// trailing update from block columns k0 .. k0 + kw - 1: tiles (i, j) with
+// j0 <= j <= i (nw > 0: j < j0 + nw only) get A_ij -= sum_kk L_i,kk L_j,kk', the
+// accumulator staying in registers across the kw columns (one read and one
+// write of A_ij per launch instead of per column; the fp64 MFMA chain is the
+// same, so the result is bit-identical); then rhs tiles i > rc get
+// b_i -= L_i,rc y_rc (forward substitution, fused).
+__global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, int kw, int j0, int n_tiles,
+                                                          int nw, int rc) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* Li = sm;
     double* Lj = sm + M * LD;
     const int64_t np = d.np;
-    const int m = d.nt - k - 1;
     const int t = blockIdx.x;
-    if (t >= n_tiles) {   // rhs tile i: b_i -= L_ik y_k
-        const int i = k + 1 + (t - n_tiles);
+    if (t >= n_tiles) {   // rhs tile i: b_i -= L_i,rc y_rc
+        const int i = rc + 1 + (t - n_tiles);
         if (threadIdx.x < M) {
             const int r = threadIdx.x;
-            const double* L = d.A + ((int64_t)i * kDM + r) * np + (int64_t)k * kDM;
-            const double* yk = d.y + (int64_t)k * kDM;
+            const double* L = d.A + ((int64_t)i * kDM + r) * np + (int64_t)rc * kDM;
+            const double* yk = d.y + (int64_t)rc * kDM;
             double s = 0.0;
             for (int c = 0; c < M; ++c) s += L[c] * yk[c];
             d.b[(int64_t)i * kDM + r] -= s;
         }
         return;
     }
-    // t -> (i, j) over the lower triangle of the m x m trailing tile grid
-    int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while ((a + 1) * (a + 2) / 2 <= t) ++a;
-    while (a * (a + 1) / 2 > t) --a;
-    const int i = k + 1 + a, j = k + 1 + (t - a * (a + 1) / 2);
-    (void)m;
-    load_tile<64>(Li, LD, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
-    if (i != j) load_tile<64>(Lj, LD, d.A + (int64_t)j * kDM * np + (int64_t)k * kDM, (int)np);
-    __syncthreads();
-    const double* Lb = i != j ? Lj : Li;
+    int i, j;
+    if (nw > 0) {   // the nw block columns from j0, rectangle of rows j0 .. nt - 1
+        const int rows = d.nt - j0;
+        i = j0 + t % rows;
+        j = j0 + t / rows;
+        if (i < j) return;   // above the diagonal: whole workgroup
+    } else {   // t -> (i, j) over the lower triangle of the trailing tile grid
+        int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while ((a + 1) * (a + 2) / 2 <= t) ++a;
+        while (a * (a + 1) / 2 > t) --a;
+        i = j0 + a;
+        j = j0 + (t - a * (a + 1) / 2);
+    }
     double* C = d.A + (int64_t)i * kDM * np + (int64_t)j * kDM;
     const int wave = threadIdx.x >> 6;
+    const double* Lb = i != j ? Lj : Li;
+    v4d acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
-        if (i == j && tj > ti) continue;   // the diagonal tile's lower half (and its diagonal sub-tiles)
-        v4d acc = tile_ld(C, (int)np, 16 * ti, 16 * tj);
-        acc = tile_mm<false, true, true>(acc, Li, LD, 16 * ti, Lb, LD, 16 * tj, 0, M);
-        tile_st(C, (int)np, 16 * ti, 16 * tj, acc);
+        acc[q] = (i == j && tj > ti) ? zero4() : tile_ld(C, (int)np, 16 * ti, 16 * tj);
+    }
+    for (int kk = k0; kk < k0 + kw; ++kk) {
+        if (kk > k0) __syncthreads();   // the previous column's tiles are consumed
+        load_tile<64>(Li, LD, d.A + (int64_t)i * kDM * np + (int64_t)kk * kDM, (int)np);
+        if (i != j) load_tile<64>(Lj, LD, d.A + (int64_t)j * kDM * np + (int64_t)kk * kDM, (int)np);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
+            if (i == j && tj > ti) continue;   // the diagonal tile's lower half (and its diagonal sub-tiles)
+            acc[q] = tile_mm<false, true, true>(acc[q], Li, LD, 16 * ti, Lb, LD, 16 * tj, 0, M);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
+        if (i == j && tj > ti) continue;
+        tile_st(C, (int)np, 16 * ti, 16 * tj, acc[q]);
     }
 }
 
@@ -997,13 +1027,29 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
                                     (int)lds_u));
         attr = true;
     }
-    for (int k = 0; k < d.nt; ++k) {
-        hipLaunchKernelGGL(dense_panel_kernel, dim3(d.nt - k), dim3(NT), lds_p, s, d, k);
-        SFM_HIP(hipGetLastError());
-        const int m = d.nt - k - 1;
-        if (m > 0) {
-            const int n_tiles = m * (m + 1) / 2;
-            hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m), dim3(NT), lds_u, s, d, k, n_tiles);
+    // block columns in groups of W = SFM_DENSE_W: panel c, then the group's
+    // later columns updated from column c alone (rhs of column c fused), ...;
+    // after the group's last panel every later tile is updated from all W
+    // columns in one pass, read and written once
+    constexpr int W = SFM_DENSE_W;
+    for (int k = 0; k < d.nt; k += W) {
+        const int w = std::min(W, d.nt - k);
+        for (int c = k; c < k + w; ++c) {
+            hipLaunchKernelGGL(dense_panel_kernel, dim3(d.nt - c), dim3(NT), lds_p, s, d, c);
+            SFM_HIP(hipGetLastError());
+            const int m = d.nt - c - 1;   // rows below column c
+            if (c + 1 < k + w) {
+                const int nw = k + w - c - 1, n_tiles = nw * m;
+                hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m), dim3(NT), lds_u, s, d, c, 1, c + 1,
+                                   n_tiles, nw, c);
+                SFM_HIP(hipGetLastError());
+            }
+        }
+        const int m2 = d.nt - k - w;   // trailing block columns
+        if (m2 > 0) {
+            const int n_tiles = m2 * (m2 + 1) / 2;
+            hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m2), dim3(NT), lds_u, s, d, k, w, k + w, n_tiles, 0,
+                               k + w - 1);
             SFM_HIP(hipGetLastError());
         }
     }
