@@ -14,8 +14,9 @@
 //     each wave keeps its 64 queries' B fragments in VGPRs and streams the
 //     database in 32-row MFMA tiles; the C tile has the database row on the
 //     registers and the query on the lane, so the top-2 update is lane-local:
-//     key = ((|d'|^2 << 8) | row&255) - 512 * dot, b2 = med3(b1,b2,key),
-//     b1 = min(b1,key) (3 VALU ops per distance), merged with the running
+//     key = ((|d'|^2 << 8) | row&255) - 512 * dot, two keys x, y per update:
+//     b2 = min(med3(b1,x,y), b2), b1 = min3(b1,x,y) (2.5 VALU ops per
+//     distance including the key), merged with the running
 //     (value, index) state every 256 rows; lowest index wins ties.
 //   * the ratio test d1 < fl32(ratio^2) * d2 and the result write are fused
 //     into the epilogue; nothing but (idx, d1) per query leaves the chip.
@@ -120,6 +121,9 @@ struct MatchArgs {
     int32_t* out_d;            // [n_pairs][out_stride]
 };
 
+// kRatio = false (MUTUAL's two nearest-neighbour passes): only the nearest
+// key is tracked (min3 over two keys, 1.5 VALU per distance).
+template <bool kRatio>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES_PER_EU, MATCH_WAVES_PER_EU))) void match_top2_kernel(MatchArgs a) {
     // XCD-aware bijective remap of the flat workgroup id (guide §5 T1):
     // blocks b and b+8 share an XCD, so give each XCD a contiguous range of
@@ -206,20 +210,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
                 acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[1][s4], acc1, 0, 0, 0);
             // epilogue for both column tiles, interleaved for ILP:
             // key = nt - 512*dot (v_mad_i32_i24; |dot| < 2^21 fits 24 bits; the
-            // multiplier is a kernel argument so it is not strength-reduced),
-            // b2 = med3(b1, b2, key), b1 = min(b1, key): 3 VALU per distance.
+            // multiplier is a kernel argument so it is not strength-reduced).
+            // Two keys x, y of one query per update; the two smallest of the
+            // multiset {b1 <= b2, x, y} are
+            //   b1' = min3(b1, x, y),  b2' = min(med3(b1, x, y), b2)
+            // (b1 smallest: med3 = min(x, y); b1 in the middle: med3 = b1 <= b2;
+            // b1 largest: med3 = max(x, y) <= b1 <= b2), so 3 VALU per 2
+            // distances instead of med3 + min per distance.
             // The accumulators are consumed by compiler-generated code only: an
             // inline asm reading MFMA results gets no hazard padding.
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int k0 = __mul24(acc0[j], a.kmul) + nt4[j >> 2][j & 3];
-                const int k1 = __mul24(acc1[j], a.kmul) + nt4[j >> 2][j & 3];
-                asm("v_med3_i32 %1, %0, %1, %4\n\t"
-                    "v_med3_i32 %3, %2, %3, %5\n\t"
-                    "v_min_i32 %0, %0, %4\n\t"
-                    "v_min_i32 %2, %2, %5"
-                    : "+v"(b1[0]), "+v"(b2[0]), "+v"(b1[1]), "+v"(b2[1])
-                    : "v"(k0), "v"(k1));
+            for (int j = 0; j < 16; j += 2) {
+                const int x0 = __mul24(acc0[j], a.kmul) + nt4[j >> 2][j & 3];
+                const int x1 = __mul24(acc1[j], a.kmul) + nt4[j >> 2][j & 3];
+                const int y0 = __mul24(acc0[j + 1], a.kmul) + nt4[j >> 2][(j & 3) + 1];
+                const int y1 = __mul24(acc1[j + 1], a.kmul) + nt4[j >> 2][(j & 3) + 1];
+                if (!kRatio) {
+                    asm("v_min3_i32 %0, %0, %2, %3\n\t"
+                        "v_min3_i32 %1, %1, %4, %5"
+                        : "+v"(b1[0]), "+v"(b1[1])
+                        : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+                    continue;
+                }
+                int t0, t1;
+                asm("v_med3_i32 %4, %0, %6, %7\n\t"
+                    "v_med3_i32 %5, %2, %8, %9\n\t"
+                    "v_min3_i32 %0, %0, %6, %7\n\t"
+                    "v_min3_i32 %2, %2, %8, %9\n\t"
+                    "v_min_i32 %1, %4, %1\n\t"
+                    "v_min_i32 %3, %5, %3"
+                    : "+v"(b1[0]), "+v"(b2[0]), "+v"(b1[1]), "+v"(b2[1]), "=&v"(t0), "=&v"(t1)
+                    : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
             }
         }
         if (((sup + kStage) & 255) == 0) {   // keys carry row & 255: merge every 256 rows
@@ -238,7 +259,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
         if (h == 0 && q < n_q) {
             const int nq = a.nrm[a.img_row0[q_img] + q];
             int idx = g[t].g1i, d1 = nq + g[t].g1v;
-            if (a.ratio_test) {
+            if (kRatio) {
                 const bool keep = n_db >= 2 && (float)d1 < a.r2 * (float)(nq + g[t].g2v);
                 if (!keep) idx = -1;
             }
@@ -445,7 +466,10 @@ void run_top2(sfm_match_plan* p, const int32_t* pairs_d, int64_t n_pairs, int sw
         a.out_stride = stride;
         a.out_idx = out_idx + b0 * stride;
         a.out_d = out_d + b0 * stride;
-        hipLaunchKernelGGL(match_top2_kernel, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+        if (ratio_test)
+            hipLaunchKernelGGL(match_top2_kernel<true>, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(match_top2_kernel<false>, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
         SFM_HIP(hipGetLastError());
         ++p->launches;
     }
