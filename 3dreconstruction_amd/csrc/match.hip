@@ -15,7 +15,7 @@
 //     database in 32-row MFMA tiles; the C tile has the database row on the
 //     registers and the query on the lane, so the top-2 update is lane-local:
 //     key = ((|d'|^2 << 8) | row&255) - 512 * dot, two keys x, y per update:
-//     b2 = min(med3(b1,x,y), b2), b1 = min3(b1,x,y) (2.5 VALU ops per
+//     b2 = min(med3(b1,x,y), b2), b1 = min3(b1,x,y) (2.25 VALU ops per
 //     distance including the key), merged with the running
 //     (value, index) state every 256 rows; lowest index wins ties.
 //   * the ratio test d1 < fl32(ratio^2) * d2 and the result write are fused
@@ -216,31 +216,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
             //   b1' = min3(b1, x, y),  b2' = min(med3(b1, x, y), b2)
             // (b1 smallest: med3 = min(x, y); b1 in the middle: med3 = b1 <= b2;
             // b1 largest: med3 = max(x, y) <= b1 <= b2), so 3 VALU per 2
-            // distances instead of med3 + min per distance.
+            // distances instead of med3 + min per distance.  Two consecutive
+            // pairs share one b2 update, b2 = min3(b2, t_a, t_b) (the same
+            // value as two min steps): 5 VALU per 4 distances.
             // The accumulators are consumed by compiler-generated code only: an
             // inline asm reading MFMA results gets no hazard padding.
 #pragma unroll
-            for (int j = 0; j < 16; j += 2) {
-                const int x0 = __mul24(acc0[j], a.kmul) + nt4[j >> 2][j & 3];
-                const int x1 = __mul24(acc1[j], a.kmul) + nt4[j >> 2][j & 3];
-                const int y0 = __mul24(acc0[j + 1], a.kmul) + nt4[j >> 2][(j & 3) + 1];
-                const int y1 = __mul24(acc1[j + 1], a.kmul) + nt4[j >> 2][(j & 3) + 1];
+            for (int j = 0; j < 16; j += 4) {
+                const int x0 = __mul24(acc0[j], a.kmul) + nt4[j >> 2][0];
+                const int x1 = __mul24(acc1[j], a.kmul) + nt4[j >> 2][0];
+                const int y0 = __mul24(acc0[j + 1], a.kmul) + nt4[j >> 2][1];
+                const int y1 = __mul24(acc1[j + 1], a.kmul) + nt4[j >> 2][1];
+                const int z0 = __mul24(acc0[j + 2], a.kmul) + nt4[j >> 2][2];
+                const int z1 = __mul24(acc1[j + 2], a.kmul) + nt4[j >> 2][2];
+                const int w0 = __mul24(acc0[j + 3], a.kmul) + nt4[j >> 2][3];
+                const int w1 = __mul24(acc1[j + 3], a.kmul) + nt4[j >> 2][3];
                 if (!kRatio) {
                     asm("v_min3_i32 %0, %0, %2, %3\n\t"
-                        "v_min3_i32 %1, %1, %4, %5"
+                        "v_min3_i32 %1, %1, %4, %5\n\t"
+                        "v_min3_i32 %0, %0, %6, %7\n\t"
+                        "v_min3_i32 %1, %1, %8, %9"
                         : "+v"(b1[0]), "+v"(b1[1])
-                        : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+                        : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
                     continue;
                 }
-                int t0, t1;
-                asm("v_med3_i32 %4, %0, %6, %7\n\t"
-                    "v_med3_i32 %5, %2, %8, %9\n\t"
-                    "v_min3_i32 %0, %0, %6, %7\n\t"
-                    "v_min3_i32 %2, %2, %8, %9\n\t"
-                    "v_min_i32 %1, %4, %1\n\t"
-                    "v_min_i32 %3, %5, %3"
-                    : "+v"(b1[0]), "+v"(b2[0]), "+v"(b1[1]), "+v"(b2[1]), "=&v"(t0), "=&v"(t1)
-                    : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+                int ta0, ta1, tb0, tb1;
+                asm("v_med3_i32 %4, %0, %8, %9\n\t"
+                    "v_med3_i32 %5, %2, %10, %11\n\t"
+                    "v_min3_i32 %0, %0, %8, %9\n\t"
+                    "v_min3_i32 %2, %2, %10, %11\n\t"
+                    "v_med3_i32 %6, %0, %12, %13\n\t"
+                    "v_med3_i32 %7, %2, %14, %15\n\t"
+                    "v_min3_i32 %0, %0, %12, %13\n\t"
+                    "v_min3_i32 %2, %2, %14, %15\n\t"
+                    "v_min3_i32 %1, %1, %4, %6\n\t"
+                    "v_min3_i32 %3, %3, %5, %7"
+                    : "+v"(b1[0]), "+v"(b2[0]), "+v"(b1[1]), "+v"(b2[1]),
+                      "=&v"(ta0), "=&v"(ta1), "=&v"(tb0), "=&v"(tb1)
+                    : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
             }
         }
         if (((sup + kStage) & 255) == 0) {   // keys carry row & 255: merge every 256 rows
