@@ -10,8 +10,8 @@
 //     a' = a - 128 (translation keeps |a-b|^2) with |a'|^2 per row, so the
 //     distance matrix is an exact integer contraction on the i8 MFMA
 //     (v_mfma_i32_32x32x32_i8, int32 accumulate): |a'|^2+|b'|^2-2a'.b'.
-//   * one workgroup = 4 waves = 256 queries of image J against all of image I;
-//     each wave keeps its 64 queries' B fragments in VGPRs and streams the
+//   * one workgroup = 4 waves = 4 x 32 MATCH_CT queries of image J against all of image I;
+//     each wave keeps its 32 MATCH_CT queries' B fragments in VGPRs and streams the
 //     database in 32-row MFMA tiles; the C tile has the database row on the
 //     registers and the query on the lane, so the top-2 update is lane-local:
 //     key = ((|d'|^2 << 8) | row&255) - 512 * dot, two keys x, y per update:
@@ -39,14 +39,19 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kQB = 256;   // queries per workgroup (4 waves x 64)
-constexpr int kRowPad = 256;  // rows of every image padded to this multiple
+#ifndef MATCH_CT
+#define MATCH_CT 4                 // 32-query column tiles per wave (even; 4: 200 VGPRs, 2 waves/SIMD)
+#endif
+constexpr int kCT = MATCH_CT;
+constexpr int kQW = 32 * kCT;      // queries per wave
+constexpr int kQB = 4 * kQW;       // queries per workgroup (4 waves)
+constexpr int kRowPad = kQB > 256 ? kQB : 256;  // rows of every image padded to this multiple
 constexpr int kStage = 128;   // database rows per LDS stage (kRowPad multiple of it)
 #ifndef MATCH_TILE_UNROLL
 #define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
 #endif
 #ifndef MATCH_WAVES_PER_EU
-#define MATCH_WAVES_PER_EU 4           // waves per SIMD the register budget targets
+#define MATCH_WAVES_PER_EU 2           // waves per SIMD the register budget targets
 #endif
 
 // u8 -> int8 (a ^ 0x80 == a - 128), per-row |a'|^2 and the packed key base.
@@ -142,22 +147,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane >> 5, c = lane & 31;
-    const int64_t q_row0 = a.img_row0[q_img] + qblk * kQB + wave * 64;
+    const int64_t q_row0 = a.img_row0[q_img] + qblk * kQB + wave * kQW;
     const int64_t db_row0 = a.img_row0[db_img];
 
     // B fragments: 2 column tiles x 4 k-steps, lane holds bytes [64h+16s, +16)
     // of query row c (k assignment shared with A; MFMA pairs equal slots).
-    v4i bq[2][4];
+    v4i bq[kCT][4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < kCT; ++t) {
         const v4i* src = reinterpret_cast<const v4i*>(a.desc + (q_row0 + 32 * t + c) * 128 + 64 * h);
 #pragma unroll
         for (int s = 0; s < 4; ++s) bq[t][s] = src[s];
     }
 
-    Top2 g[2];
+    Top2 g[kCT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) { g[t].g1v = INT_MAX; g[t].g1i = -1; g[t].g2v = INT_MAX; }
+    for (int t = 0; t < kCT; ++t) { g[t].g1v = INT_MAX; g[t].g1i = -1; g[t].g2v = INT_MAX; }
 
     // Database rows are staged once per workgroup through LDS (double-buffered
     // kStage-row stages filled by global_load_lds, 16 B per lane), instead of
@@ -183,7 +188,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     };
 
     const int n_db_pad = (n_db + kRowPad - 1) / kRowPad * kRowPad;
-    int b1[2] = {INT_MAX, INT_MAX}, b2[2] = {INT_MAX, INT_MAX};
+    int b1[kCT], b2[kCT];
+#pragma unroll
+    for (int t = 0; t < kCT; ++t) b1[t] = b2[t] = INT_MAX;
     if (n_db_pad > 0) issue(0, 0);
     for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
         __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
@@ -201,13 +208,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
             v4i nt4[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) nt4[q] = *reinterpret_cast<const v4i*>(N + tile + 4 * h + 8 * q);
-            v16i acc0 = {}, acc1 = {};
+            v16i acc[kCT];
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4)
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[0][s4], acc0, 0, 0, 0);
+            for (int t = 0; t < kCT; ++t) {
+                acc[t] = v16i{};
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4)
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[1][s4], acc1, 0, 0, 0);
+                for (int s4 = 0; s4 < 4; ++s4)
+                    acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[t][s4], acc[t], 0, 0, 0);
+            }
             // epilogue for both column tiles, interleaved for ILP:
             // key = nt - 512*dot (v_mad_i32_i24; |dot| < 2^21 fits 24 bits; the
             // multiplier is a kernel argument so it is not strength-reduced).
@@ -222,21 +230,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
             // The accumulators are consumed by compiler-generated code only: an
             // inline asm reading MFMA results gets no hazard padding.
 #pragma unroll
+            for (int tp = 0; tp < kCT; tp += 2)
+#pragma unroll
             for (int j = 0; j < 16; j += 4) {
-                const int x0 = __mul24(acc0[j], a.kmul) + nt4[j >> 2][0];
-                const int x1 = __mul24(acc1[j], a.kmul) + nt4[j >> 2][0];
-                const int y0 = __mul24(acc0[j + 1], a.kmul) + nt4[j >> 2][1];
-                const int y1 = __mul24(acc1[j + 1], a.kmul) + nt4[j >> 2][1];
-                const int z0 = __mul24(acc0[j + 2], a.kmul) + nt4[j >> 2][2];
-                const int z1 = __mul24(acc1[j + 2], a.kmul) + nt4[j >> 2][2];
-                const int w0 = __mul24(acc0[j + 3], a.kmul) + nt4[j >> 2][3];
-                const int w1 = __mul24(acc1[j + 3], a.kmul) + nt4[j >> 2][3];
+                const int x0 = __mul24(acc[tp][j], a.kmul) + nt4[j >> 2][0];
+                const int x1 = __mul24(acc[tp + 1][j], a.kmul) + nt4[j >> 2][0];
+                const int y0 = __mul24(acc[tp][j + 1], a.kmul) + nt4[j >> 2][1];
+                const int y1 = __mul24(acc[tp + 1][j + 1], a.kmul) + nt4[j >> 2][1];
+                const int z0 = __mul24(acc[tp][j + 2], a.kmul) + nt4[j >> 2][2];
+                const int z1 = __mul24(acc[tp + 1][j + 2], a.kmul) + nt4[j >> 2][2];
+                const int w0 = __mul24(acc[tp][j + 3], a.kmul) + nt4[j >> 2][3];
+                const int w1 = __mul24(acc[tp + 1][j + 3], a.kmul) + nt4[j >> 2][3];
                 if (!kRatio) {
                     asm("v_min3_i32 %0, %0, %2, %3\n\t"
                         "v_min3_i32 %1, %1, %4, %5\n\t"
                         "v_min3_i32 %0, %0, %6, %7\n\t"
                         "v_min3_i32 %1, %1, %8, %9"
-                        : "+v"(b1[0]), "+v"(b1[1])
+                        : "+v"(b1[tp]), "+v"(b1[tp + 1])
                         : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
                     continue;
                 }
@@ -251,14 +261,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
                     "v_min3_i32 %2, %2, %14, %15\n\t"
                     "v_min3_i32 %1, %1, %4, %6\n\t"
                     "v_min3_i32 %3, %3, %5, %7"
-                    : "+v"(b1[0]), "+v"(b2[0]), "+v"(b1[1]), "+v"(b2[1]),
+                    : "+v"(b1[tp]), "+v"(b2[tp]), "+v"(b1[tp + 1]), "+v"(b2[tp + 1]),
                       "=&v"(ta0), "=&v"(ta1), "=&v"(tb0), "=&v"(tb1)
                     : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
             }
         }
         if (((sup + kStage) & 255) == 0) {   // keys carry row & 255: merge every 256 rows
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < kCT; ++t) {
                 merge_tile(g[t], b1[t], b2[t], sup + kStage - 256);
                 b1[t] = INT_MAX; b2[t] = INT_MAX;
             }
@@ -266,9 +276,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     }
 
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < kCT; ++t) {
         merge_lanes(g[t]);
-        const int q = qblk * kQB + wave * 64 + 32 * t + c;
+        const int q = qblk * kQB + wave * kQW + 32 * t + c;
         if (h == 0 && q < n_q) {
             const int nq = a.nrm[a.img_row0[q_img] + q];
             int idx = g[t].g1i, d1 = nq + g[t].g1v;
