@@ -46,7 +46,11 @@ constexpr int kCT = MATCH_CT;
 constexpr int kQW = 32 * kCT;      // queries per wave
 constexpr int kQB = 4 * kQW;       // queries per workgroup (4 waves)
 constexpr int kRowPad = kQB > 256 ? kQB : 256;  // rows of every image padded to this multiple
-constexpr int kStage = 128;   // database rows per LDS stage (kRowPad multiple of it)
+#ifndef MATCH_STAGE
+#define MATCH_STAGE 128            // database rows per LDS stage (A/B knob)
+#endif
+constexpr int kStage = MATCH_STAGE;   // database rows per LDS stage (kRowPad multiple of it)
+static_assert(kStage == 128 || kStage == 256, "merge windows are 256 rows");
 #ifndef MATCH_TILE_UNROLL
 #define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
 #endif
