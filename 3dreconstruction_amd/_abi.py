@@ -28,6 +28,8 @@ SFM_CAM_PINHOLE = 0
 SFM_CAM_SNAVELY = 1
 SFM_CAM_RADIAL3 = 2
 
+SFM_CTX_TUNE_HOST_MALLOC = 1
+
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1
 SFM_MATCH_CASCADE = 2
@@ -43,7 +45,7 @@ f64p = C.POINTER(C.c_double)
 
 class CtxOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
-                ("reserved", C.c_int32), ("comm_id", u8p),
+                ("flags", C.c_int32), ("comm_id", u8p),
                 ("allreduce", C.c_void_p), ("allreduce_user", C.c_void_p)]
 
 

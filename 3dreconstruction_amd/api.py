@@ -31,10 +31,10 @@ class Context:
     array in place across ranks (op 0 sum, 1 max); replaces RCCL, e.g. with a
     torch.distributed gloo group."""
 
-    def __init__(self, device=0, rank=0, world_size=1, comm_id=None, allreduce=None):
+    def __init__(self, device=0, rank=0, world_size=1, comm_id=None, allreduce=None, flags=0):
         self.lib = abi.load()
         o = abi.CtxOpts()
-        o.device, o.rank, o.world_size = device, rank, world_size
+        o.device, o.rank, o.world_size, o.flags = device, rank, world_size, flags
         self._id = None
         self._hook = None
         if comm_id is not None:

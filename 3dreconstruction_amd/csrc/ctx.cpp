@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -192,8 +193,10 @@ bool cached_free(void* p) {
     if (it == c.live.end()) return false;
     const Block b = it->second;
     c.live.erase(it);
-    // reuse only under the stream the block was last used on
-    const hipStream_t key = tl_stream ? tl_stream : b.key;
+    // reuse only under the stream the block was allocated and used on: a block
+    // freed while another context is bound may still have work queued on its
+    // own stream, which the other stream's order does not cover
+    const hipStream_t key = b.key;
     if (key && c.streams.count(key) && c.cached + b.bytes <= MemCache::kCap) {
         c.free[{key, b.kind, b.bytes}].push_back(p);
         c.cached += b.bytes;
@@ -279,16 +282,17 @@ namespace {
 // waits for it: 12-27 ms after a bundle adjustment freed its ~100 MB of
 // planner arrays, which the C5 loop paid before every image's match
 // (tools/match_latency.py).  glibc serves allocations above its mmap
-// threshold (128 KB, adaptive) with mmap / munmap; raising the threshold and
-// the trim threshold keeps freed blocks in the heap for reuse instead.
-// Once per process; SFM_KEEP_MALLOC=1 leaves the host application's malloc
-// settings alone.
+// threshold with mmap / munmap; the threshold at its maximum (32 MiB on
+// 64-bit: glibc rejects anything above HEAP_MAX_SIZE / 2) and a large trim
+// threshold keep freed blocks in the heap for reuse instead.  Opt-in
+// (SFM_CTX_TUNE_HOST_MALLOC or SFM_TUNE_MALLOC=1), once per process: a
+// long-running host application keeps its own malloc settings by default.
 void tune_host_malloc() {
     static std::once_flag once;
     std::call_once(once, [] {
-        if (std::getenv("SFM_KEEP_MALLOC")) return;
-        mallopt(M_MMAP_THRESHOLD, 1 << 30);
-        mallopt(M_TRIM_THRESHOLD, 1 << 30);
+        const int a = mallopt(M_MMAP_THRESHOLD, 32 << 20);
+        const int b = mallopt(M_TRIM_THRESHOLD, 1 << 30);
+        if (!a || !b) std::fprintf(stderr, "[sfmcore] mallopt rejected (mmap threshold %d, trim threshold %d)\n", a, b);
     });
 }
 }  // namespace
@@ -310,7 +314,7 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         SFM_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, SFM_ERR_DEVICE,
                     "device %d is %s; this build targets gfx950 (MI355X) only", opts->device,
                     prop.gcnArchName);
-        tune_host_malloc();
+        if ((opts->flags & SFM_CTX_TUNE_HOST_MALLOC) || std::getenv("SFM_TUNE_MALLOC")) tune_host_malloc();
         auto* c = new sfm_ctx;
         c->device = opts->device;
         c->rank = opts->rank;

@@ -288,9 +288,9 @@ struct FArgs {
     float* logc;              // [2 (n + n_pairs)] logc_n | logc_k per pair (scratch)
     uint32_t* vidx;           // [n] vec_index per pair (scratch)
     uint32_t* binl;           // [n] best inliers so far (result)
-    unsigned long long* gkey; // [n_pairs][slots] sort keys when they exceed LDS
+    unsigned long long* gkey; // sort keys of the pairs whose sort exceeds LDS, packed
     uint32_t* gval;
-    int64_t gslots;           // slots per pair in gkey / gval (0: LDS only)
+    const int64_t* goff;      // [n_pairs] slot offset of the pair in gkey / gval, -1: LDS
     double* Fout;             // [n_pairs][9] best model, normalised
     double* stat;             // [n_pairs][4] minNFA, errorMax (normalised), n_inliers, iterations
     int32_t* fail;            // set when a pair exhausts the random stream
@@ -324,9 +324,10 @@ __global__ __launch_bounds__(kFT) void fmatrix_ac_kernel(FArgs a) {
     float* logc_k = logc_n + (n + 1);            // [n + 1]
     uint32_t* vidx = a.vidx + o0;
     uint32_t* binl = a.binl + o0;
-    const bool lds_sort = a.gslots == 0;
-    unsigned long long* keys = lds_sort ? reinterpret_cast<unsigned long long*>(smem) : a.gkey + (size_t)q * a.gslots;
-    uint32_t* vals = lds_sort ? reinterpret_cast<uint32_t*>(smem + 8 * (size_t)a.lds_slots) : a.gval + (size_t)q * a.gslots;
+    const int64_t go = a.goff[q];
+    const bool lds_sort = go < 0;
+    unsigned long long* keys = lds_sort ? reinterpret_cast<unsigned long long*>(smem) : a.gkey + go;
+    uint32_t* vals = lds_sort ? reinterpret_cast<uint32_t*>(smem + 8 * (size_t)a.lds_slots) : a.gval + go;
 
     __shared__ double s_models[kMaxModels][9], s_bestF[9];
     __shared__ double s_red[kFT / 64];
@@ -601,7 +602,7 @@ extern "C" int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off,
             cst[4 * q + 3] = 0.0;
         }
         tm.mark("normalise");
-        DBuf<int64_t> d_off;
+        DBuf<int64_t> d_off, d_goff;
         DBuf<double> d_xn, d_cst, d_ltab, d_F, d_stat;
         DBuf<float> d_logc;
         DBuf<uint32_t> d_rng, d_vidx, d_binl, d_gval;
@@ -624,22 +625,33 @@ extern "C" int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off,
         d_stat.alloc(4 * (size_t)n_pairs);
         d_fail.alloc(1);
         d_fail.zero(s);
-        int64_t slots = 1;
-        while (slots < max_n) slots <<= 1;
+        // sort buffers per pair: next_pow2(n) slots, in LDS up to kMaxLdsSort;
+        // only the pairs above that get global (L2) buffers, packed by prefix
+        // sum, so one large pair does not move every pair to global memory
+        std::vector<int64_t> goff((size_t)n_pairs, -1);
+        int64_t lds_slots = 1, g_slots = 0;
+        for (int64_t q = 0; q < n_pairs; ++q) {
+            int64_t sl = 1;
+            while (sl < off[q + 1] - off[q]) sl <<= 1;
+            if (sl <= kMaxLdsSort) {
+                lds_slots = std::max(lds_slots, sl);
+            } else {
+                goff[q] = g_slots;
+                g_slots += sl;
+            }
+        }
         FArgs a{};
         a.off = d_off.p; a.xn = d_xn.p; a.cst = d_cst.p; a.rng = d_rng.p; a.rng_n = (int64_t)rw.size();
         a.ltab = d_ltab.p; a.logc = d_logc.p; a.vidx = d_vidx.p; a.binl = d_binl.p;
         a.Fout = d_F.p; a.stat = d_stat.p; a.fail = d_fail.p; a.max_iter = max_iter;
-        size_t lds = 0;
-        if (slots <= kMaxLdsSort) {
-            a.gslots = 0;
-            a.lds_slots = (int32_t)slots;
-            lds = 12 * (size_t)slots;
-        } else {   // large pairs: sort buffers in global memory (L2)
-            a.gslots = slots;
-            a.lds_slots = 0;
-            d_gkey.alloc((size_t)slots * n_pairs);
-            d_gval.alloc((size_t)slots * n_pairs);
+        d_goff.alloc(goff.size());
+        d_goff.upload(goff.data(), goff.size(), s);
+        a.goff = d_goff.p;
+        a.lds_slots = (int32_t)lds_slots;
+        const size_t lds = 12 * (size_t)lds_slots;
+        if (g_slots) {   // large pairs: sort buffers in global memory (L2)
+            d_gkey.alloc((size_t)g_slots);
+            d_gval.alloc((size_t)g_slots);
             a.gkey = d_gkey.p;
             a.gval = d_gval.p;
         }

@@ -43,6 +43,7 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 #define MATCH_CT 4                 // 32-query column tiles per wave (even; 4: 200 VGPRs, 2 waves/SIMD)
 #endif
 constexpr int kCT = MATCH_CT;
+static_assert(kCT % 2 == 0 && kCT >= 2, "MATCH_CT must be even: the epilogue walks column tiles in pairs");
 constexpr int kQW = 32 * kCT;      // queries per wave
 constexpr int kQB = 4 * kQW;       // queries per workgroup (4 waves)
 constexpr int kRowPad = kQB > 256 ? kQB : 256;  // rows of every image padded to this multiple

@@ -135,14 +135,17 @@ extern "C" int sfm_seq_bundle_adjust(sfm_seq* s, sfm_ba_summary* summary) {
 }
 
 extern "C" int sfm_seq_last_step(sfm_seq* s, sfm_seq_step* step) {
-    if (!s || !step) return SFM_ERR_INVALID_ARG;
-    *step = s->act->lastStep();
-    return SFM_OK;
+    return sfm::guarded([&] {
+        SFM_REQUIRE(s && step, SFM_ERR_INVALID_ARG, "null argument");
+        *step = s->act->lastStep();
+        return SFM_OK;
+    });
 }
 
 extern "C" int sfm_seq_matches(sfm_seq* s, int32_t which, int32_t* query, int32_t* train, float* dist,
                                int64_t cap, int64_t* n) {
-    if (!s || !n || (which != 0 && which != 1)) return SFM_ERR_INVALID_ARG;
+  return sfm::guarded([&] {
+    SFM_REQUIRE(s && n && (which == 0 || which == 1), SFM_ERR_INVALID_ARG, "bad argument");
     const auto& v = which == 0 ? s->act->lastLocalMatches() : s->act->lastGlobalMatches();
     *n = (int64_t)v.size();
     if (!query && !train && !dist) return SFM_OK;
@@ -153,11 +156,13 @@ extern "C" int sfm_seq_matches(sfm_seq* s, int32_t which, int32_t* query, int32_
         if (dist) dist[k] = v[k].distance;
     }
     return SFM_OK;
+  });
 }
 
 extern "C" int sfm_seq_world(sfm_seq* s, double* X, int64_t* n_obs, int64_t cap_pts, int64_t* n_pts,
                              double* poses, int32_t cap_img, int32_t* n_img, double* intr4) {
-    if (!s) return SFM_ERR_INVALID_ARG;
+  return sfm::guarded([&] {
+    SFM_REQUIRE(s, SFM_ERR_INVALID_ARG, "null sequence");
     auto w = s->act->getWorld();
     std::vector<std::pair<sfm::WorldPoint::Idx, sfm::WorldPoint::Ptr>> pts(w->points().begin(), w->points().end());
     std::sort(pts.begin(), pts.end(), [](auto& a, auto& b) { return a.first < b.first; });
@@ -176,11 +181,14 @@ extern "C" int sfm_seq_world(sfm_seq* s, double* X, int64_t* n_obs, int64_t cap_
         for (int a = 0; a < 4; ++a) intr4[a] = v[a];
     }
     return SFM_OK;
+  });
 }
 
 extern "C" int sfm_seq_observations(sfm_seq* s, int32_t* img, double* uv, int64_t cap, int64_t* n) {
-    if (!s || !n) return SFM_ERR_INVALID_ARG;
-    return seq_observations(*s->act, img, uv, cap, n);
+    return sfm::guarded([&] {
+        SFM_REQUIRE(s && n, SFM_ERR_INVALID_ARG, "null argument");
+        return seq_observations(*s->act, img, uv, cap, n);
+    });
 }
 
 extern "C" int sfm_seq_destroy(sfm_seq* s) {

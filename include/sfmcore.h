@@ -62,7 +62,7 @@ typedef struct sfm_ctx_opts {
     int32_t device;          /* HIP device ordinal (local to the process)      */
     int32_t rank;            /* 0 .. world_size-1                              */
     int32_t world_size;      /* 1 = single GPU; >1 = landmark-sharded BA       */
-    int32_t reserved;
+    int32_t flags;           /* SFM_CTX_* bits (0 = defaults)                  */
     const uint8_t* comm_id;  /* 128-byte RCCL unique id from rank 0's
                                 sfm_comm_unique_id(); NULL when world_size==1
                                 or when `allreduce` is given (at world_size 1
@@ -75,13 +75,18 @@ typedef struct sfm_ctx_opts {
     void* allreduce_user;
 } sfm_ctx_opts;
 
+/* sfm_ctx_opts.flags.  SFM_CTX_TUNE_HOST_MALLOC (opt-in; the environment
+ * variable SFM_TUNE_MALLOC=1 has the same effect): keep freed host memory in
+ * the process heap (glibc M_MMAP_THRESHOLD at its 32 MiB maximum, and
+ * M_TRIM_THRESHOLD).  Unmapping a large host buffer stalls the process's next
+ * GPU operation for 10-30 ms while the driver invalidates its mappings, which
+ * an incremental loop (BA, then matching, per image) pays every step; the
+ * price is that the heap does not shrink, so a long-running host application
+ * leaves it off (the default: its malloc settings are not touched). */
+#define SFM_CTX_TUNE_HOST_MALLOC 1
+
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
 int sfm_comm_unique_id(uint8_t* out128);
-/* The first context of a process raises glibc's mmap and trim thresholds
- * (mallopt, 1 GB): unmapping large host buffers stalls the process's next GPU
- * operation for 10-30 ms while the driver invalidates its mappings, which an
- * incremental loop (BA, then matching, per image) would pay every step.  Set
- * SFM_KEEP_MALLOC=1 to keep the host application's malloc settings. */
 int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out);
 int sfm_ctx_destroy(sfm_ctx* ctx);
 int sfm_ctx_synchronize(sfm_ctx* ctx);

@@ -265,6 +265,17 @@ def test_gpu_fmatrix_options_and_global_sort(ctx):
         _same(g, w)
 
 
+@pytest.mark.gpu
+def test_gpu_fmatrix_mixed_global_and_lds_sort(ctx):
+    # two pairs above the LDS sort capacity (different global buffer sizes,
+    # packed by prefix sum) between small pairs that keep the LDS sort
+    xs, whs = _batch([(300, 0.3), (17000, 0.2), (40, 0.1), (9000, 0.3), (700, 0.5), (0, 0), (2000, 0.2)],
+                     seed0=700)
+    o = api.fmatrix_opts(precision=4.0, max_iterations=200)
+    for g, w in zip(api.fmatrix_ac(ctx, xs, whs, o), oracle_fmatrix_ac(xs, whs, o)):
+        _same(g, w)
+
+
 def _stage(d, n_views=4, n_pts=400, seed=21):
     """sfm_data.json + <stem>.feat of n_views 640x480 views of one scene and a
     matches.putative.bin of every pair: true correspondences plus 25 % wrong
