@@ -55,6 +55,14 @@ static_assert(kStage == 128 || kStage == 256, "merge windows are 256 rows");
 #ifndef MATCH_TILE_UNROLL
 #define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
 #endif
+#ifndef MATCH_PIPE
+// software-pipelined tile loop (two accumulator sets; A/B knob).  Measured on
+// C3 (tools/gpurun/match_ab.sh, profiles/r03/a_match_pipe): 2 column tiles at
+// 2 waves/SIMD 472 k pairs/s, 4 column tiles at 1 wave/SIMD 366 k, against
+// 504 k for the plain loop -- two co-resident waves already overlap one
+// wave's epilogue with the other's MFMAs, so it is off.
+#define MATCH_PIPE 0
+#endif
 #ifndef MATCH_WAVES_PER_EU
 #define MATCH_WAVES_PER_EU 2           // waves per SIMD the register budget targets
 #endif
@@ -196,7 +204,123 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     int b1[kCT], b2[kCT];
 #pragma unroll
     for (int t = 0; t < kCT; ++t) b1[t] = b2[t] = INT_MAX;
+
+    // one 32-row database tile: A fragments (XOR-swizzled LDS image) and the
+    // packed key bases of this lane's 16 rows (rows (j&3) + 8(j>>2) + 4h)
+    auto load_frag = [&](const int8_t* A, const int32_t* N, int tile, v4i (&af)[4], v4i (&nt4)[4]) {
+        const int r = tile + c;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+            af[s4] = *reinterpret_cast<const v4i*>(A + r * 128 + (((4 * h + s4) ^ (r & 7)) << 4));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nt4[q] = *reinterpret_cast<const v4i*>(N + tile + 4 * h + 8 * q);
+    };
+    auto mfma_tile = [&](const v4i (&af)[4], v16i (&acc)[kCT]) {
+#pragma unroll
+        for (int t = 0; t < kCT; ++t) {
+            acc[t] = v16i{};
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[t][s4], acc[t], 0, 0, 0);
+        }
+    };
+    // epilogue of one tile for every column tile, pairs interleaved for ILP:
+    // key = nt - 512*dot (v_mad_i32_i24; |dot| < 2^21 fits 24 bits; the
+    // multiplier is a kernel argument so it is not strength-reduced).
+    // Two keys x, y of one query per update; the two smallest of the
+    // multiset {b1 <= b2, x, y} are
+    //   b1' = min3(b1, x, y),  b2' = min(med3(b1, x, y), b2)
+    // (b1 smallest: med3 = min(x, y); b1 in the middle: med3 = b1 <= b2;
+    // b1 largest: med3 = max(x, y) <= b1 <= b2), so 3 VALU per 2
+    // distances instead of med3 + min per distance.  Two consecutive
+    // pairs share one b2 update, b2 = min3(b2, t_a, t_b) (the same
+    // value as two min steps): 5 VALU per 4 distances.
+    // The accumulators are consumed by compiler-generated code only: an
+    // inline asm reading MFMA results gets no hazard padding.
+    auto epilogue = [&](const v16i (&acc)[kCT], const v4i (&nt4)[4]) {
+#pragma unroll
+        for (int tp = 0; tp < kCT; tp += 2)
+#pragma unroll
+        for (int j = 0; j < 16; j += 4) {
+            const int x0 = __mul24(acc[tp][j], a.kmul) + nt4[j >> 2][0];
+            const int x1 = __mul24(acc[tp + 1][j], a.kmul) + nt4[j >> 2][0];
+            const int y0 = __mul24(acc[tp][j + 1], a.kmul) + nt4[j >> 2][1];
+            const int y1 = __mul24(acc[tp + 1][j + 1], a.kmul) + nt4[j >> 2][1];
+            const int z0 = __mul24(acc[tp][j + 2], a.kmul) + nt4[j >> 2][2];
+            const int z1 = __mul24(acc[tp + 1][j + 2], a.kmul) + nt4[j >> 2][2];
+            const int w0 = __mul24(acc[tp][j + 3], a.kmul) + nt4[j >> 2][3];
+            const int w1 = __mul24(acc[tp + 1][j + 3], a.kmul) + nt4[j >> 2][3];
+            if (!kRatio) {
+                asm("v_min3_i32 %0, %0, %2, %3\n\t"
+                    "v_min3_i32 %1, %1, %4, %5\n\t"
+                    "v_min3_i32 %0, %0, %6, %7\n\t"
+                    "v_min3_i32 %1, %1, %8, %9"
+                    : "+v"(b1[tp]), "+v"(b1[tp + 1])
+                    : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
+                continue;
+            }
+            int ta0, ta1, tb0, tb1;
+            asm("v_med3_i32 %4, %0, %8, %9\n\t"
+                "v_med3_i32 %5, %2, %10, %11\n\t"
+                "v_min3_i32 %0, %0, %8, %9\n\t"
+                "v_min3_i32 %2, %2, %10, %11\n\t"
+                "v_med3_i32 %6, %0, %12, %13\n\t"
+                "v_med3_i32 %7, %2, %14, %15\n\t"
+                "v_min3_i32 %0, %0, %12, %13\n\t"
+                "v_min3_i32 %2, %2, %14, %15\n\t"
+                "v_min3_i32 %1, %1, %4, %6\n\t"
+                "v_min3_i32 %3, %3, %5, %7"
+                : "+v"(b1[tp]), "+v"(b2[tp]), "+v"(b1[tp + 1]), "+v"(b2[tp + 1]),
+                  "=&v"(ta0), "=&v"(ta1), "=&v"(tb0), "=&v"(tb1)
+                : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
+        }
+    };
+    // keys carry row & 255: the tile keys are merged into the running state
+    // every 256 rows
+    auto merge_window = [&](int base) {
+#pragma unroll
+        for (int t = 0; t < kCT; ++t) {
+            merge_tile(g[t], b1[t], b2[t], base);
+            b1[t] = INT_MAX; b2[t] = INT_MAX;
+        }
+    };
+
     if (n_db_pad > 0) issue(0, 0);
+#if MATCH_PIPE
+    // Software pipeline over the tiles: tile t's MFMAs are issued before the
+    // top-2 epilogue of tile t-1 (two accumulator sets, A for the even tiles of
+    // a stage, B for the odd ones), so the i8 MFMAs of one tile run under the
+    // VALU epilogue of the previous one inside each wave.  The epilogue of a
+    // stage's last tile runs at the head of the next stage, after its barrier.
+    static_assert(kStage % 64 == 0, "tiles go in A/B pairs");
+    v16i accA[kCT], accB[kCT];
+    v4i ntA[4], ntB[4];
+    bool pendB = false;              // accB holds a tile whose epilogue is pending
+    int merge_base = -1;             // a window merge pending after that epilogue
+    for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
+        __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
+        if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
+        const int8_t* A = sA[st & 1];
+        const int32_t* N = sN[st & 1];
+        for (int tile = 0; tile < kStage; tile += 64) {
+            v4i afA[4], afB[4];
+            load_frag(A, N, tile, afA, ntA);
+            mfma_tile(afA, accA);
+            if (pendB) epilogue(accB, ntB);
+            if (merge_base >= 0) {
+                merge_window(merge_base);
+                merge_base = -1;
+            }
+            load_frag(A, N, tile + 32, afB, ntB);
+            mfma_tile(afB, accB);
+            epilogue(accA, ntA);
+            pendB = true;
+        }
+        if (((sup + kStage) & 255) == 0) merge_base = sup + kStage - 256;
+    }
+    if (pendB) epilogue(accB, ntB);
+    if (merge_base >= 0) merge_window(merge_base);
+#else
     for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
         __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
         if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
@@ -204,81 +328,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
         const int32_t* N = sN[st & 1];
 #pragma unroll MATCH_TILE_UNROLL
         for (int tile = 0; tile < kStage; tile += 32) {
-            const int r = tile + c;
-            v4i af[4];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4)
-                af[s4] = *reinterpret_cast<const v4i*>(A + r * 128 + (((4 * h + s4) ^ (r & 7)) << 4));
-            // packed key bases of this lane's 16 rows: rows (j&3) + 8(j>>2) + 4h
-            v4i nt4[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) nt4[q] = *reinterpret_cast<const v4i*>(N + tile + 4 * h + 8 * q);
+            v4i af[4], nt4[4];
+            load_frag(A, N, tile, af, nt4);
             v16i acc[kCT];
-#pragma unroll
-            for (int t = 0; t < kCT; ++t) {
-                acc[t] = v16i{};
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4)
-                    acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[s4], bq[t][s4], acc[t], 0, 0, 0);
-            }
-            // epilogue for both column tiles, interleaved for ILP:
-            // key = nt - 512*dot (v_mad_i32_i24; |dot| < 2^21 fits 24 bits; the
-            // multiplier is a kernel argument so it is not strength-reduced).
-            // Two keys x, y of one query per update; the two smallest of the
-            // multiset {b1 <= b2, x, y} are
-            //   b1' = min3(b1, x, y),  b2' = min(med3(b1, x, y), b2)
-            // (b1 smallest: med3 = min(x, y); b1 in the middle: med3 = b1 <= b2;
-            // b1 largest: med3 = max(x, y) <= b1 <= b2), so 3 VALU per 2
-            // distances instead of med3 + min per distance.  Two consecutive
-            // pairs share one b2 update, b2 = min3(b2, t_a, t_b) (the same
-            // value as two min steps): 5 VALU per 4 distances.
-            // The accumulators are consumed by compiler-generated code only: an
-            // inline asm reading MFMA results gets no hazard padding.
-#pragma unroll
-            for (int tp = 0; tp < kCT; tp += 2)
-#pragma unroll
-            for (int j = 0; j < 16; j += 4) {
-                const int x0 = __mul24(acc[tp][j], a.kmul) + nt4[j >> 2][0];
-                const int x1 = __mul24(acc[tp + 1][j], a.kmul) + nt4[j >> 2][0];
-                const int y0 = __mul24(acc[tp][j + 1], a.kmul) + nt4[j >> 2][1];
-                const int y1 = __mul24(acc[tp + 1][j + 1], a.kmul) + nt4[j >> 2][1];
-                const int z0 = __mul24(acc[tp][j + 2], a.kmul) + nt4[j >> 2][2];
-                const int z1 = __mul24(acc[tp + 1][j + 2], a.kmul) + nt4[j >> 2][2];
-                const int w0 = __mul24(acc[tp][j + 3], a.kmul) + nt4[j >> 2][3];
-                const int w1 = __mul24(acc[tp + 1][j + 3], a.kmul) + nt4[j >> 2][3];
-                if (!kRatio) {
-                    asm("v_min3_i32 %0, %0, %2, %3\n\t"
-                        "v_min3_i32 %1, %1, %4, %5\n\t"
-                        "v_min3_i32 %0, %0, %6, %7\n\t"
-                        "v_min3_i32 %1, %1, %8, %9"
-                        : "+v"(b1[tp]), "+v"(b1[tp + 1])
-                        : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
-                    continue;
-                }
-                int ta0, ta1, tb0, tb1;
-                asm("v_med3_i32 %4, %0, %8, %9\n\t"
-                    "v_med3_i32 %5, %2, %10, %11\n\t"
-                    "v_min3_i32 %0, %0, %8, %9\n\t"
-                    "v_min3_i32 %2, %2, %10, %11\n\t"
-                    "v_med3_i32 %6, %0, %12, %13\n\t"
-                    "v_med3_i32 %7, %2, %14, %15\n\t"
-                    "v_min3_i32 %0, %0, %12, %13\n\t"
-                    "v_min3_i32 %2, %2, %14, %15\n\t"
-                    "v_min3_i32 %1, %1, %4, %6\n\t"
-                    "v_min3_i32 %3, %3, %5, %7"
-                    : "+v"(b1[tp]), "+v"(b2[tp]), "+v"(b1[tp + 1]), "+v"(b2[tp + 1]),
-                      "=&v"(ta0), "=&v"(ta1), "=&v"(tb0), "=&v"(tb1)
-                    : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
-            }
+            mfma_tile(af, acc);
+            epilogue(acc, nt4);
         }
-        if (((sup + kStage) & 255) == 0) {   // keys carry row & 255: merge every 256 rows
-#pragma unroll
-            for (int t = 0; t < kCT; ++t) {
-                merge_tile(g[t], b1[t], b2[t], sup + kStage - 256);
-                b1[t] = INT_MAX; b2[t] = INT_MAX;
-            }
-        }
+        if (((sup + kStage) & 255) == 0) merge_window(sup + kStage - 256);
     }
+#endif
 
 #pragma unroll
     for (int t = 0; t < kCT; ++t) {

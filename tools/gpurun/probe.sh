@@ -25,4 +25,4 @@ grep "^\[bench\] BA" "$OUT/fake8.err"
 SFM_BENCH_SAME_DEVICE=1 timeout -k 10 400 python -u bench.py --gpus 2 --steps 3 --allow-host-allreduce $ARGS \
     > "$OUT/n2.json" 2> "$OUT/n2.err" || { tail -30 "$OUT/n2.err"; exit 1; }
 grep "^\[bench\] BA" "$OUT/n2.err" | head -2
-python3 -c "import json; d=json.load(open('$OUT/n2.json')); print('N=2', d['n_gpus'], d['value'], d['config']['transport'], d['rmse_final'])"
+python3 -c "import json; d=[json.loads(l) for l in open('$OUT/n2.json') if l.startswith('{')][-1]; print('N=2', d['n_gpus'], d['value'], d['config']['transport'], d['rmse_final'])"
