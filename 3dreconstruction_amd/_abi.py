@@ -223,8 +223,13 @@ SIGNATURES = [
                                f64p, f64p, f64p, f64p, f64p, i64p]),
     ("sfm_match_dense", C.c_int, [C.c_void_p, u8p, C.c_int32, u8p, C.c_int32,
                                   C.POINTER(MatchOptions), i32p, i32p]),
+    ("sfm_match_dense_f32", C.c_int, [C.c_void_p, f32p, C.c_int32, f32p, C.c_int32,
+                                      C.POINTER(MatchOptions), i32p, f32p]),
     ("sfm_match_plan_create", C.c_int, [C.c_void_p, u8p, i64p, C.c_int32,
                                         C.POINTER(C.c_void_p)]),
+    ("sfm_match_plan_create_f32", C.c_int, [C.c_void_p, f32p, i64p, C.c_int32,
+                                            C.POINTER(C.c_void_p)]),
+    ("sfm_match_plan_fetch_f32", C.c_int, [C.c_void_p, i64p, u32p, u32p, f32p]),
     ("sfm_match_plan_run", C.c_int, [C.c_void_p, i32p, C.c_int64, C.POINTER(MatchOptions),
                                      i64p]),
     ("sfm_match_plan_fetch", C.c_int, [C.c_void_p, i64p, u32p, u32p, i32p]),

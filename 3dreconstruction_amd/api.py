@@ -100,18 +100,41 @@ def match_dense(ctx, a, b, mode=abi.SFM_MATCH_RATIO, ratio=0.8):
     return idx[:n_out], d2[:n_out]
 
 
+def match_dense_f32(ctx, a, b, mode=abi.SFM_MATCH_RATIO, ratio=0.8):
+    """sfm_match_dense_f32: float descriptors (cv::Mat CV_32F); returns
+    (idx, squared distance as float32, -1 where unmatched)."""
+    a = np.ascontiguousarray(a, np.float32).reshape(-1, 128)
+    b = np.ascontiguousarray(b, np.float32).reshape(-1, 128)
+    n_out = len(a) if mode == abi.SFM_MATCH_MUTUAL else len(b)
+    idx = np.zeros(max(n_out, 1), np.int32)
+    d2 = np.zeros(max(n_out, 1), np.float32)
+    o = abi.MatchOptions(mode, ratio)
+    _check(ctx.lib.sfm_match_dense_f32(ctx.h, abi.ptr(a, abi.f32p), len(a), abi.ptr(b, abi.f32p), len(b),
+                                       C.byref(o), abi.ptr(idx, abi.i32p), abi.ptr(d2, abi.f32p)),
+           "sfm_match_dense_f32")
+    return idx[:n_out], d2[:n_out]
+
+
 class MatchPlan:
-    """Resident descriptor collection for all-pairs matching."""
+    """Resident descriptor collection for all-pairs matching (uint8, or float32
+    through sfm_match_plan_create_f32: fetch() then returns float distances)."""
 
     def __init__(self, ctx, desc, offsets):
         self.ctx = ctx
-        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 128)
+        self.f32 = np.asarray(desc).dtype == np.float32
         offsets = np.ascontiguousarray(offsets, np.int64)
         self.n_img = len(offsets) - 1
         h = C.c_void_p()
-        _check(ctx.lib.sfm_match_plan_create(ctx.h, abi.ptr(desc, abi.u8p),
-                                             abi.ptr(offsets, abi.i64p), self.n_img, C.byref(h)),
-               "sfm_match_plan_create")
+        if self.f32:
+            desc = np.ascontiguousarray(desc, np.float32).reshape(-1, 128)
+            _check(ctx.lib.sfm_match_plan_create_f32(ctx.h, abi.ptr(desc, abi.f32p),
+                                                     abi.ptr(offsets, abi.i64p), self.n_img, C.byref(h)),
+                   "sfm_match_plan_create_f32")
+        else:
+            desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 128)
+            _check(ctx.lib.sfm_match_plan_create(ctx.h, abi.ptr(desc, abi.u8p),
+                                                 abi.ptr(offsets, abi.i64p), self.n_img, C.byref(h)),
+                   "sfm_match_plan_create")
         self.h = h
         self.n_pairs = 0
         ctx._adopt(self)
@@ -128,16 +151,22 @@ class MatchPlan:
 
     def fetch(self):
         counts = np.zeros(max(self.n_pairs, 1), np.int64)
-        _check(self.ctx.lib.sfm_match_plan_fetch(self.h, abi.ptr(counts, abi.i64p), None, None,
-                                                 None), "sfm_match_plan_fetch")
+        fetch = self.ctx.lib.sfm_match_plan_fetch_f32 if self.f32 else self.ctx.lib.sfm_match_plan_fetch
+        _check(fetch(self.h, abi.ptr(counts, abi.i64p), None, None, None), "sfm_match_plan_fetch")
         counts = counts[:self.n_pairs]
         tot = int(counts.sum())
         i = np.zeros(max(tot, 1), np.uint32)
         j = np.zeros(max(tot, 1), np.uint32)
-        d = np.zeros(max(tot, 1), np.int32)
-        _check(self.ctx.lib.sfm_match_plan_fetch(self.h, abi.ptr(counts, abi.i64p),
-                                                 abi.ptr(i, abi.u32p), abi.ptr(j, abi.u32p),
-                                                 abi.ptr(d, abi.i32p)), "sfm_match_plan_fetch")
+        if self.f32:
+            d = np.zeros(max(tot, 1), np.float32)
+            _check(self.ctx.lib.sfm_match_plan_fetch_f32(self.h, abi.ptr(counts, abi.i64p),
+                                                         abi.ptr(i, abi.u32p), abi.ptr(j, abi.u32p),
+                                                         abi.ptr(d, abi.f32p)), "sfm_match_plan_fetch_f32")
+        else:
+            d = np.zeros(max(tot, 1), np.int32)
+            _check(self.ctx.lib.sfm_match_plan_fetch(self.h, abi.ptr(counts, abi.i64p),
+                                                     abi.ptr(i, abi.u32p), abi.ptr(j, abi.u32p),
+                                                     abi.ptr(d, abi.i32p)), "sfm_match_plan_fetch")
         return counts, i[:tot], j[:tot], d[:tot]
 
     def cascade_index(self, pairs):

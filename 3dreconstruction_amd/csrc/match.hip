@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "cascade.h"
@@ -370,6 +371,90 @@ __global__ void mutual_kernel(int32_t* __restrict__ idx_q, int32_t* __restrict__
     if (t < 0 || idx_t[o + t] != q) { idx_q[o + q] = -1; d_q[o + q] = -1; }
 }
 
+// ---- float descriptors that are not integers in [0, 255] -------------------
+// (cv::Mat CV_32F behind LocalFrame/GlobalFrame::matchFeature, LocalFrame.h:38,
+// Image.h:39-41).  OpenCV's SIFT stores saturate_cast<uchar> values in its
+// float descriptors, so those take the exact u8 path above; anything else
+// lands here: one query per thread, d = sum_k (q_k - a_k)^2 as an fmaf chain
+// in k order (the oracle's restatement, bit for bit), database rows staged in
+// LDS and read as broadcasts, first minimum (lowest index) wins as in top2().
+struct MatchF32Args {
+    const float* desc;         // padded rows x 128 (f32)
+    const int64_t* img_row0;
+    const int32_t* img_n;
+    const int32_t* pairs;
+    int32_t n_pairs;
+    int32_t qblocks;           // 256-query blocks per pair
+    int32_t swap;
+    float r2;
+    int64_t out_stride;
+    int32_t* out_idx;
+    int32_t* out_d;            // float bits of the squared distance
+};
+
+constexpr int kF32Rows = 64;   // database rows per LDS stage
+
+template <bool kRatio>
+__global__ __launch_bounds__(256) void match_f32_kernel(MatchF32Args a) {
+    const int pair = blockIdx.x / a.qblocks, qblk = blockIdx.x - pair * a.qblocks;
+    if (pair >= a.n_pairs) return;
+    const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
+    const int db_img = a.swap ? J : I, q_img = a.swap ? I : J;
+    const int n_db = a.img_n[db_img], n_q = a.img_n[q_img];
+    if (qblk * 256 >= n_q) return;
+    const int q = qblk * 256 + (int)threadIdx.x;
+    const bool has_q = q < n_q;
+    float qv[128];
+    {
+        const float4* src = reinterpret_cast<const float4*>(a.desc + (a.img_row0[q_img] + (has_q ? q : 0)) * 128);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const float4 v = src[k];
+            qv[4 * k] = v.x; qv[4 * k + 1] = v.y; qv[4 * k + 2] = v.z; qv[4 * k + 3] = v.w;
+        }
+    }
+    __shared__ __attribute__((aligned(16))) float sA[kF32Rows * 128];
+    const float* db = a.desc + a.img_row0[db_img] * 128;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int i1 = -1;
+    for (int base = 0; base < n_db; base += kF32Rows) {
+        const int nr = min(kF32Rows, n_db - base);
+        __syncthreads();   // the previous stage is consumed
+        for (int e = threadIdx.x; e < kF32Rows * 32; e += 256)
+            reinterpret_cast<float4*>(sA)[e] =
+                e < nr * 32 ? reinterpret_cast<const float4*>(db + (int64_t)base * 128)[e] : float4{0.f, 0.f, 0.f, 0.f};
+        __syncthreads();
+        for (int r = 0; r < nr; ++r) {
+            const float4* row = reinterpret_cast<const float4*>(sA + r * 128);
+            float d = 0.f;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                const float4 v = row[k];
+                const float t0 = qv[4 * k] - v.x, t1 = qv[4 * k + 1] - v.y;
+                const float t2 = qv[4 * k + 2] - v.z, t3 = qv[4 * k + 3] - v.w;
+                d = __builtin_fmaf(t0, t0, d);
+                d = __builtin_fmaf(t1, t1, d);
+                d = __builtin_fmaf(t2, t2, d);
+                d = __builtin_fmaf(t3, t3, d);
+            }
+            if (d < b1) {
+                if (kRatio) b2 = b1;
+                b1 = d;
+                i1 = base + r;
+            } else if (kRatio && d < b2) {
+                b2 = d;
+            }
+        }
+    }
+    if (!has_q) return;
+    int idx = i1;
+    float d1 = b1;
+    if (kRatio && !(n_db >= 2 && b1 < a.r2 * b2)) idx = -1;
+    if (idx < 0) d1 = -1.f;
+    a.out_idx[(int64_t)pair * a.out_stride + q] = idx;
+    a.out_d[(int64_t)pair * a.out_stride + q] = __float_as_int(d1);
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
@@ -423,6 +508,8 @@ struct sfm_match_plan {
     int32_t max_n = 0;
     int64_t rows = 0;            // padded rows in total
     DBuf<uint8_t> desc;
+    DBuf<float> descf;           // f32 collection that is not integer-valued (match_f32_kernel)
+    bool f32 = false;
     DBuf<int32_t> nrm, ntr, img_n;
     DBuf<int64_t> img_row0;
     // last run
@@ -513,6 +600,63 @@ void upload_collection(sfm_match_plan* p, const uint8_t* desc, const int64_t* of
     tm.mark("sync");
 }
 
+// float descriptors: integers in [0, 255] (what cv::SIFT stores) are
+// converted exactly and take the u8 path; anything else is kept as f32
+bool f32_is_u8(const float* d, int64_t n) {
+    for (int64_t k = 0; k < n; ++k) {
+        const float v = d[k];
+        if (!(v >= 0.f && v <= 255.f) || v != (float)(int)v) return false;
+    }
+    return true;
+}
+
+void upload_collection_f32(sfm_match_plan* p, const float* desc, const int64_t* off, int32_t n_img,
+                           const float* const* srcs = nullptr) {
+    bool u8 = true;
+    for (int i = 0; i < n_img && u8; ++i)
+        u8 = f32_is_u8(srcs ? srcs[i] : desc + off[i] * 128, (off[i + 1] - off[i]) * 128);
+    if (u8) {
+        std::vector<uint8_t> b((size_t)std::max<int64_t>(off[n_img] - off[0], 0) * 128);
+        for (int i = 0; i < n_img; ++i) {
+            const float* src = srcs ? srcs[i] : desc + off[i] * 128;
+            uint8_t* dst = b.data() + (off[i] - off[0]) * 128;
+            for (int64_t k = 0; k < (off[i + 1] - off[i]) * 128; ++k) dst[k] = (uint8_t)src[k];
+        }
+        std::vector<int64_t> o(off, off + n_img + 1);
+        for (auto& v : o) v -= off[0];
+        upload_collection(p, b.data(), o.data(), n_img);
+        return;
+    }
+    hipStream_t s = p->ctx->stream;
+    p->f32 = true;
+    p->n_img = n_img;
+    p->row0.resize(n_img);
+    p->nrows.resize(n_img);
+    int64_t rows = 0;
+    for (int i = 0; i < n_img; ++i) {
+        const int64_t n = off[i + 1] - off[i];
+        SFM_REQUIRE(n >= 0 && n < (1 << 24), SFM_ERR_INVALID_ARG, "image %d has %lld rows", i, (long long)n);
+        p->row0[i] = rows;
+        p->nrows[i] = (int32_t)n;
+        p->max_n = std::max<int32_t>(p->max_n, (int32_t)n);
+        rows += (n + kRowPad - 1) / kRowPad * kRowPad;
+    }
+    rows += kRowPad;
+    p->rows = rows;
+    HostVec<float> staging((size_t)rows * 128, 0.f);
+    for (int i = 0; i < n_img; ++i)
+        if (p->nrows[i])
+            std::memcpy(&staging[(size_t)p->row0[i] * 128], srcs ? srcs[i] : desc + off[i] * 128,
+                        (size_t)p->nrows[i] * 128 * sizeof(float));
+    p->descf.alloc(staging.size());
+    p->descf.upload(staging.data(), staging.size(), s);
+    p->img_n.alloc(n_img);
+    p->img_n.upload(p->nrows.data(), n_img, s);
+    p->img_row0.alloc(n_img);
+    p->img_row0.upload(p->row0.data(), n_img, s);
+    SFM_HIP(hipStreamSynchronize(s));  // staging dies here
+}
+
 CascTables casc_tables(sfm_match_plan* p) {
     CascTables t;
     t.desc = reinterpret_cast<const int8_t*>(p->desc.p);
@@ -531,6 +675,32 @@ CascTables casc_tables(sfm_match_plan* p) {
 void run_top2(sfm_match_plan* p, const int32_t* pairs_d, int64_t n_pairs, int swap, int ratio_test,
               float r2, int32_t* out_idx, int32_t* out_d, int64_t stride) {
     hipStream_t s = p->ctx->stream;
+    if (p->f32) {
+        const int qblocks = std::max(1, (p->max_n + 255) / 256);
+        const int64_t batch = std::max<int64_t>(1, ((int64_t)1 << 22) / qblocks);
+        for (int64_t b0 = 0; b0 < n_pairs; b0 += batch) {
+            const int64_t nb = std::min(batch, n_pairs - b0);
+            MatchF32Args a;
+            a.desc = p->descf.p;
+            a.img_row0 = p->img_row0.p;
+            a.img_n = p->img_n.p;
+            a.pairs = pairs_d + 2 * b0;
+            a.n_pairs = (int32_t)nb;
+            a.qblocks = qblocks;
+            a.swap = swap;
+            a.r2 = r2;
+            a.out_stride = stride;
+            a.out_idx = out_idx + b0 * stride;
+            a.out_d = out_d + b0 * stride;
+            if (ratio_test)
+                hipLaunchKernelGGL(match_f32_kernel<true>, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL(match_f32_kernel<false>, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+            SFM_HIP(hipGetLastError());
+            ++p->launches;
+        }
+        return;
+    }
     const int qblocks = std::max(1, (p->max_n + kQB - 1) / kQB);
     const int64_t max_wg = 1 << 22;
     const int64_t batch = std::max<int64_t>(1, max_wg / qblocks);
@@ -642,6 +812,8 @@ void run_pairs(sfm_match_plan* p, const int32_t* pairs, int64_t n_pairs, const s
         SFM_REQUIRE(pairs[2 * q] >= 0 && pairs[2 * q] < p->n_img && pairs[2 * q + 1] >= 0 &&
                         pairs[2 * q + 1] < p->n_img,
                     SFM_ERR_INVALID_ARG, "pair %lld out of range", (long long)q);
+    SFM_REQUIRE(!(p->f32 && o->mode == SFM_MATCH_CASCADE), SFM_ERR_UNSUPPORTED,
+                "cascade hashing needs integer descriptors in [0, 255] (this f32 collection is not)");
     if (o->mode == SFM_MATCH_CASCADE) casc_prepare(p, pairs, n_pairs, false);
     p->mode = o->mode;
     p->n_pairs = n_pairs;
@@ -737,6 +909,8 @@ extern "C" int sfm_match_plan_cascade_index(sfm_match_plan* p, const int32_t* pa
         for (int64_t q = 0; q < 2 * n_pairs; ++q)
             SFM_REQUIRE(pairs[q] >= 0 && pairs[q] < p->n_img, SFM_ERR_INVALID_ARG,
                         "pair %lld out of range", (long long)(q / 2));
+        SFM_REQUIRE(!p->f32, SFM_ERR_UNSUPPORTED,
+                    "cascade hashing needs integer descriptors in [0, 255] (this f32 collection is not)");
         CtxScope scope_(p->ctx);
         casc_prepare(p, pairs, n_pairs, true);
         return SFM_OK;
@@ -765,43 +939,90 @@ extern "C" int sfm_match_plan_digest(sfm_match_plan* p, uint64_t* digest) {
     });
 }
 
+namespace {
+// D = int32_t: exact integer squared distances (u8 collections); D = float:
+// float squared distances (any collection; integers convert exactly)
+template <class D>
+void fetch_results(sfm_match_plan* p, int64_t* counts, uint32_t* i, uint32_t* j, D* d2) {
+    const size_t n = (size_t)(p->n_pairs * p->stride);
+    std::vector<int32_t> hi(n), hd(n);
+    if (n) {
+        SFM_HIP(hipMemcpyAsync(hi.data(), p->out_idx.p, n * 4, hipMemcpyDeviceToHost, p->ctx->stream));
+        SFM_HIP(hipMemcpyAsync(hd.data(), p->out_d.p, n * 4, hipMemcpyDeviceToHost, p->ctx->stream));
+    }
+    SFM_HIP(hipStreamSynchronize(p->ctx->stream));
+    int64_t off = 0;
+    std::vector<std::pair<uint64_t, int32_t>> v;
+    for (int64_t q = 0; q < p->n_pairs; ++q) {
+        const int I = p->pairs_h[2 * q], J = p->pairs_h[2 * q + 1];
+        const bool qJ = p->mode != SFM_MATCH_MUTUAL;
+        const int n_out = qJ ? p->nrows[J] : p->nrows[I];
+        v.clear();
+        for (int t = 0; t < n_out; ++t) {
+            const int m = hi[(size_t)q * p->stride + t];
+            if (m < 0) continue;
+            const uint32_t ii = qJ ? (uint32_t)m : (uint32_t)t;
+            const uint32_t jj = qJ ? (uint32_t)t : (uint32_t)m;
+            v.emplace_back(((uint64_t)ii << 32) | jj, hd[(size_t)q * p->stride + t]);
+        }
+        std::sort(v.begin(), v.end());  // IndMatch::getDeduplicated order
+        counts[q] = (int64_t)v.size();
+        if (i) {
+            for (const auto& m : v) {
+                i[off] = (uint32_t)(m.first >> 32);
+                j[off] = (uint32_t)(m.first & 0xffffffffu);
+                if constexpr (std::is_same<D, float>::value) {
+                    float f;
+                    if (p->f32) std::memcpy(&f, &m.second, 4);
+                    else f = (float)m.second;
+                    d2[off] = f;
+                } else {
+                    d2[off] = m.second;
+                }
+                ++off;
+            }
+        }
+    }
+}
+}  // namespace
+
 extern "C" int sfm_match_plan_fetch(sfm_match_plan* p, int64_t* counts, uint32_t* i, uint32_t* j,
                                     int32_t* d2) {
     return guarded([&] {
         SFM_REQUIRE(p && counts, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_REQUIRE(!p->f32, SFM_ERR_INVALID_ARG,
+                    "float distances: this collection is not integer-valued (sfm_match_plan_fetch_f32)");
         CtxScope scope_(p->ctx);
-        const size_t n = (size_t)(p->n_pairs * p->stride);
-        std::vector<int32_t> hi(n), hd(n);
-        if (n) {
-            SFM_HIP(hipMemcpyAsync(hi.data(), p->out_idx.p, n * 4, hipMemcpyDeviceToHost, p->ctx->stream));
-            SFM_HIP(hipMemcpyAsync(hd.data(), p->out_d.p, n * 4, hipMemcpyDeviceToHost, p->ctx->stream));
+        fetch_results(p, counts, i, j, d2);
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_fetch_f32(sfm_match_plan* p, int64_t* counts, uint32_t* i, uint32_t* j,
+                                        float* d2) {
+    return guarded([&] {
+        SFM_REQUIRE(p && counts, SFM_ERR_INVALID_ARG, "null argument");
+        CtxScope scope_(p->ctx);
+        fetch_results(p, counts, i, j, d2);
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_plan_create_f32(sfm_ctx* ctx, const float* desc, const int64_t* offsets,
+                                         int32_t n_img, sfm_match_plan** out) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && out && offsets && n_img >= 0, SFM_ERR_INVALID_ARG, "null argument");
+        SFM_REQUIRE(desc || offsets[n_img] == offsets[0], SFM_ERR_INVALID_ARG, "null descriptors");
+        CtxScope scope_(ctx);
+        auto* p = new sfm_match_plan;
+        p->ctx = ctx;
+        try {
+            upload_collection_f32(p, desc, offsets, n_img);
+        } catch (...) {
+            delete p;
+            throw;
         }
-        SFM_HIP(hipStreamSynchronize(p->ctx->stream));
-        int64_t off = 0;
-        std::vector<std::pair<uint64_t, int32_t>> v;
-        for (int64_t q = 0; q < p->n_pairs; ++q) {
-            const int I = p->pairs_h[2 * q], J = p->pairs_h[2 * q + 1];
-            const bool qJ = p->mode != SFM_MATCH_MUTUAL;
-            const int n_out = qJ ? p->nrows[J] : p->nrows[I];
-            v.clear();
-            for (int t = 0; t < n_out; ++t) {
-                const int m = hi[(size_t)q * p->stride + t];
-                if (m < 0) continue;
-                const uint32_t ii = qJ ? (uint32_t)m : (uint32_t)t;
-                const uint32_t jj = qJ ? (uint32_t)t : (uint32_t)m;
-                v.emplace_back(((uint64_t)ii << 32) | jj, hd[(size_t)q * p->stride + t]);
-            }
-            std::sort(v.begin(), v.end());  // IndMatch::getDeduplicated order
-            counts[q] = (int64_t)v.size();
-            if (i) {
-                for (const auto& m : v) {
-                    i[off] = (uint32_t)(m.first >> 32);
-                    j[off] = (uint32_t)(m.first & 0xffffffffu);
-                    d2[off] = m.second;
-                    ++off;
-                }
-            }
-        }
+        *out = p;
         return SFM_OK;
     });
 }
@@ -857,6 +1078,36 @@ extern "C" int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a, cons
         }
         SFM_HIP(hipStreamSynchronize(ctx->stream));
         tm.mark("sync+download");
+        return SFM_OK;
+    });
+}
+
+extern "C" int sfm_match_dense_f32(sfm_ctx* ctx, const float* a, int32_t n_a, const float* b, int32_t n_b,
+                                   const sfm_match_options* o, int32_t* match_idx, float* match_d2) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && o && match_idx && match_d2 && n_a >= 0 && n_b >= 0 && (a || n_a == 0) &&
+                        (b || n_b == 0),
+                    SFM_ERR_INVALID_ARG, "bad arguments");
+        CtxScope scope_(ctx);
+        const int64_t off[3] = {0, n_a, (int64_t)n_a + n_b};
+        const float* srcs[2] = {a, b};
+        sfm_match_plan plan;
+        plan.ctx = ctx;
+        upload_collection_f32(&plan, nullptr, off, 2, srcs);
+        const int32_t pair[2] = {0, 1};
+        run_pairs(&plan, pair, 1, o, false);
+        const int32_t n_out = o->mode != SFM_MATCH_MUTUAL ? n_b : n_a;
+        std::vector<int32_t> d(std::max(n_out, 1));
+        if (n_out) {
+            SFM_HIP(hipMemcpyAsync(match_idx, plan.out_idx.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
+            SFM_HIP(hipMemcpyAsync(d.data(), plan.out_d.p, (size_t)n_out * 4, hipMemcpyDeviceToHost, ctx->stream));
+        }
+        SFM_HIP(hipStreamSynchronize(ctx->stream));
+        for (int32_t q = 0; q < n_out; ++q) {
+            if (match_idx[q] < 0) { match_d2[q] = -1.f; continue; }
+            if (plan.f32) std::memcpy(&match_d2[q], &d[q], 4);
+            else match_d2[q] = (float)d[q];
+        }
         return SFM_OK;
     });
 }

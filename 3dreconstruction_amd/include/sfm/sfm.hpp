@@ -78,6 +78,22 @@ class Matcher {
         for (int q = 0; q < nq; ++q)
             if (idx[q] >= 0) out[q].push_back(DMatch{q, idx[q], 0, std::sqrt((float)d2[q])});
     }
+    // the same over float rows, the cv::Mat CV_32F cv::SIFT produces
+    // (LocalFrame.h:38, Image.h:39-41): integer-valued rows take the exact u8
+    // path, others the f32 one (sfm_match_dense_f32)
+    void knnMatch(const std::vector<float>& query, const std::vector<float>& train,
+                  std::vector<std::vector<DMatch>>& out, int k = 1) const {
+        if (k != 1) throw std::invalid_argument("crossCheck matcher supports k = 1 only");
+        const int nq = (int)(query.size() / 128), nt = (int)(train.size() / 128);
+        std::vector<int32_t> idx(std::max(nq, 1));
+        std::vector<float> d2(std::max(nq, 1));
+        sfm_match_options o{SFM_MATCH_MUTUAL, 0.8f};
+        check(sfm_match_dense_f32(ctx_->get(), query.data(), nq, train.data(), nt, &o, idx.data(), d2.data()),
+              "sfm_match_dense_f32");
+        out.assign(nq, {});
+        for (int q = 0; q < nq; ++q)
+            if (idx[q] >= 0) out[q].push_back(DMatch{q, idx[q], 0, std::sqrt(d2[q])});
+    }
     Context& context() const { return *ctx_; }
 
    private:

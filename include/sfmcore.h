@@ -310,12 +310,33 @@ int sfm_match_dense(sfm_ctx* ctx, const uint8_t* a, int32_t n_a,
                     const sfm_match_options* opts,
                     int32_t* match_idx, int32_t* match_d2);
 
+/* The same with float descriptors: the cv::Mat CV_32F rows cv::SIFT gives
+ * LocalFrame/GlobalFrame::matchFeature (src/frame/LocalFrame.h:38,
+ * GlobalFrame.h:28-34, src/component/Image.h:39-41).  OpenCV's SIFT stores
+ * saturate_cast<uchar> values in them, so rows whose every value is an
+ * integer in [0, 255] are converted exactly and matched on the u8 path
+ * (distances exact integers, < 2^24, hence exact floats).  Any other input is
+ * matched in f32: d = sum_k (a_k - b_k)^2 accumulated as an fmaf chain in k
+ * order (first minimum wins), bit for bit the oracle's restatement; OpenCV's
+ * own SIMD summation order is not pinned for such input.  match_d2 is the
+ * squared distance (DMatch.distance = sqrtf of it), -1 where unmatched. */
+int sfm_match_dense_f32(sfm_ctx* ctx, const float* a, int32_t n_a,
+                        const float* b, int32_t n_b,
+                        const sfm_match_options* opts,
+                        int32_t* match_idx, float* match_d2);
+
 /* All-pairs matching over a resident descriptor collection. */
 typedef struct sfm_match_plan sfm_match_plan;
 /* desc: concatenated [sum n_img][128] uint8; desc_offsets[n_img+1]. */
 int sfm_match_plan_create(sfm_ctx* ctx, const uint8_t* desc,
                           const int64_t* desc_offsets, int32_t n_img,
                           sfm_match_plan** out);
+/* Float collection (the rules of sfm_match_dense_f32; SFM_MATCH_CASCADE
+ * needs integer-valued descriptors and returns SFM_ERR_UNSUPPORTED
+ * otherwise). */
+int sfm_match_plan_create_f32(sfm_ctx* ctx, const float* desc,
+                              const int64_t* desc_offsets, int32_t n_img,
+                              sfm_match_plan** out);
 /* pairs[2*n_pairs] = (I, J).  Results stay on the device. */
 int sfm_match_plan_run(sfm_match_plan* plan, const int32_t* pairs,
                        int64_t n_pairs, const sfm_match_options* opts,
@@ -332,6 +353,10 @@ int sfm_match_plan_cascade_index(sfm_match_plan* plan, const int32_t* pairs,
  * keypoint-coordinate decorator is applied by sfm_sparse_match only). */
 int sfm_match_plan_fetch(sfm_match_plan* plan, int64_t* counts,
                          uint32_t* i, uint32_t* j, int32_t* d2);
+/* The same with float squared distances (any collection; a non-integer f32
+ * collection has only this one). */
+int sfm_match_plan_fetch_f32(sfm_match_plan* plan, int64_t* counts,
+                             uint32_t* i, uint32_t* j, float* d2);
 /* Order-independent digest of the last run's results (checksum of per-pair
  * checksums) computed on the device. */
 int sfm_match_plan_digest(sfm_match_plan* plan, uint64_t* digest);

@@ -16,6 +16,7 @@
 //   minimum (lowest index) wins.  Integer d ordering equals OpenCV's
 //   fl32(sqrt(d)) ordering for d < 2^22, which covers 512-normalised SIFT.
 #include <algorithm>
+#include <cmath>
 #include <climits>
 #include <cstdint>
 #include <cstring>
@@ -96,6 +97,69 @@ extern "C" int orc_match_dense_mt(const uint8_t* a, int32_t n_a, const uint8_t* 
                                  match_d2);
     }
     return SFM_ERR_INVALID_ARG;
+}
+
+// Float descriptors (cv::Mat CV_32F, LocalFrame.h:38): d = sum_k (a_k - b_k)^2
+// as an fmaf chain in k order, top-2 / first minimum as for u8.  For integer
+// values in [0, 255] every order gives the same exact integer (< 2^24), which
+// is OpenCV's result; for other values this order is the restatement's own
+// (OpenCV's SIMD summation order is not pinned here).
+namespace {
+inline float l2sq_f32(const float* a, const float* b) {
+    float s = 0.f;
+    for (int k = 0; k < 128; ++k) {
+        const float t = a[k] - b[k];
+        s = std::fmaf(t, t, s);
+    }
+    return s;
+}
+void top2_f32(const float* db, int32_t n_db, const float* q, int32_t n_q, int32_t* best_idx, float* best_d,
+              float* second_d, int n_threads) {
+#pragma omp parallel for schedule(static, 64) num_threads(n_threads > 0 ? n_threads : 1) if (n_threads > 1)
+    for (int32_t t = 0; t < n_q; ++t) {
+        float b1 = INFINITY, b2 = INFINITY;
+        int32_t i1 = -1;
+        const float* qt = q + (int64_t)t * 128;
+        for (int32_t s = 0; s < n_db; ++s) {
+            const float d = l2sq_f32(qt, db + (int64_t)s * 128);
+            if (d < b1) { b2 = b1; b1 = d; i1 = s; }
+            else if (d < b2) { b2 = d; }
+        }
+        best_idx[t] = i1; best_d[t] = b1;
+        if (second_d) second_d[t] = b2;
+    }
+}
+}  // namespace
+
+extern "C" int orc_match_dense_f32(const float* a, int32_t n_a, const float* b, int32_t n_b, int32_t mode,
+                                   float ratio, int32_t n_threads, int32_t* match_idx, float* match_d2) {
+    if (n_a < 0 || n_b < 0) return SFM_ERR_INVALID_ARG;
+    if (mode == SFM_MATCH_RATIO) {
+        std::vector<int32_t> bi(n_b);
+        std::vector<float> bd(n_b), sd(n_b);
+        top2_f32(a, n_a, b, n_b, bi.data(), bd.data(), sd.data(), n_threads);
+        const float r2 = ratio * ratio;
+        for (int32_t t = 0; t < n_b; ++t) {
+            const bool keep = n_a >= 2 && bd[t] < r2 * sd[t];
+            match_idx[t] = keep ? bi[t] : -1;
+            match_d2[t] = keep ? bd[t] : -1.f;
+        }
+        return SFM_OK;
+    }
+    if (mode == SFM_MATCH_MUTUAL) {
+        std::vector<int32_t> nq(n_a), nt(n_b);
+        std::vector<float> dq(n_a), dt(n_b);
+        top2_f32(b, n_b, a, n_a, nq.data(), dq.data(), nullptr, n_threads);
+        top2_f32(a, n_a, b, n_b, nt.data(), dt.data(), nullptr, n_threads);
+        for (int32_t q = 0; q < n_a; ++q) {
+            const int32_t t = nq[q];
+            const bool keep = t >= 0 && nt[t] == q;
+            match_idx[q] = keep ? t : -1;
+            match_d2[q] = keep ? dq[q] : -1.f;
+        }
+        return SFM_OK;
+    }
+    return SFM_ERR_UNSUPPORTED;
 }
 
 extern "C" int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,

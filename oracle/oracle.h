@@ -95,6 +95,9 @@ int orc_seq_destroy(orc_seq* s);
 int orc_seq_set_state(orc_seq* s, const double* X, int64_t n_pts, const double* poses, int32_t n_img,
                       const double* intr4);
 
+/* Float descriptors (sfm_match_dense_f32's restatement): RATIO / MUTUAL. */
+int orc_match_dense_f32(const float* a, int32_t n_a, const float* b, int32_t n_b, int32_t mode,
+                        float ratio, int32_t n_threads, int32_t* match_idx, float* match_d2);
 /* All-pairs, compacted (counts per pair; matches sorted by (i,j)).
  * Two calls: counts only when i/j/d2 are NULL. */
 int orc_match_pairs(const uint8_t* desc, const int64_t* offsets, int32_t n_img,

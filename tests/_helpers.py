@@ -169,6 +169,23 @@ def oracle_match_dense(a, b, mode, ratio=0.8):
     return idx, d2
 
 
+def oracle_match_dense_f32(a, b, mode, ratio=0.8, threads=8):
+    """The f32 restatement (fmaf chain in k order): (idx, float32 d2)."""
+    lib = oracle()
+    f = lib.orc_match_dense_f32
+    f.restype = C.c_int
+    f.argtypes = [abi.f32p, C.c_int32, abi.f32p, C.c_int32, C.c_int32, C.c_float, C.c_int32, abi.i32p, abi.f32p]
+    a = np.ascontiguousarray(a, np.float32).reshape(-1, 128)
+    b = np.ascontiguousarray(b, np.float32).reshape(-1, 128)
+    n_out = len(a) if mode == abi.SFM_MATCH_MUTUAL else len(b)
+    idx = np.zeros(max(n_out, 1), np.int32)
+    d2 = np.zeros(max(n_out, 1), np.float32)
+    rc = f(abi.ptr(a, abi.f32p), len(a), abi.ptr(b, abi.f32p), len(b), mode, ratio, threads,
+           abi.ptr(idx, abi.i32p), abi.ptr(d2, abi.f32p))
+    assert rc == 0
+    return idx[:n_out], d2[:n_out]
+
+
 def oracle_match_pairs(desc, offsets, pairs, mode, ratio=0.8, threads=8):
     """Compacted all-pairs oracle matches: (counts, i, j, d2)."""
     lib = oracle()

@@ -102,3 +102,70 @@ def test_all_pairs_plan(ctx, mode):
     assert total == n
     assert plan.digest() == api.match_digest(oc, oi, oj, od)
     plan.close()
+
+
+# ---- float descriptors (cv::Mat CV_32F behind LocalFrame/GlobalFrame) ------
+
+def _rootsift_f32(rng, n):
+    """Non-integer float descriptors (L1-normalised, square-rooted, x512)."""
+    v = rng.gamma(0.6, 1.0, size=(n, 128)).astype(np.float64)
+    v /= v.sum(1, keepdims=True) + 1e-12
+    return (512.0 * np.sqrt(v)).astype(np.float32)
+
+
+@pytest.mark.parametrize("mode", [abi.SFM_MATCH_RATIO, abi.SFM_MATCH_MUTUAL])
+def test_dense_f32_integer_valued_is_the_u8_path(ctx, mode):
+    # cv::SIFT stores saturate_cast<uchar> values in its float rows: converted
+    # exactly, same indices as the u8 matcher, distances exact integers
+    d = H.synth_descriptors(2, 1500)
+    a, b = d[:1500], d[1500:][:1100]
+    gi, gd = api.match_dense_f32(ctx, a.astype(np.float32), b.astype(np.float32), mode)
+    ui, ud = api.match_dense(ctx, a, b, mode)
+    oi, od = H.oracle_match_dense_f32(a.astype(np.float32), b.astype(np.float32), mode)
+    np.testing.assert_array_equal(gi, ui)
+    np.testing.assert_array_equal(gd, np.where(ui >= 0, ud, -1).astype(np.float32))
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+@pytest.mark.parametrize("mode", [abi.SFM_MATCH_RATIO, abi.SFM_MATCH_MUTUAL])
+@pytest.mark.parametrize("na,nb", [(0, 5), (5, 0), (1, 7), (2, 2), (300, 37), (777, 1029)])
+def test_dense_f32_non_integer_bit_exact(ctx, mode, na, nb):
+    rng = np.random.default_rng(na * 31 + nb)
+    a, b = _rootsift_f32(rng, na), _rootsift_f32(rng, nb)
+    if na > 4 and nb > 4:
+        b[:4] = a[:4] + np.float32(0.25)       # near-duplicates: real matches
+        a[na // 2] = a[0]                      # an exact tie for query 0 in RATIO
+    gi, gd = api.match_dense_f32(ctx, a, b, mode)
+    oi, od = H.oracle_match_dense_f32(a, b, mode)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd.view(np.uint32), od.view(np.uint32))
+
+
+def test_plan_f32_collection(ctx):
+    rng = np.random.default_rng(77)
+    sizes = [300, 0, 129, 513, 1]
+    desc = _rootsift_f32(rng, sum(sizes))
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    pairs = api.exhaustive_pairs(len(sizes))
+    plan = api.MatchPlan(ctx, desc, off)
+    for mode in (abi.SFM_MATCH_RATIO, abi.SFM_MATCH_MUTUAL):
+        plan.run(pairs, mode)
+        counts, i, j, d = plan.fetch()
+        assert d.dtype == np.float32
+        k = 0
+        for p, (I, J) in enumerate(pairs):
+            dI, dJ = desc[off[I]:off[I + 1]], desc[off[J]:off[J + 1]]
+            oi, od = H.oracle_match_dense_f32(dI, dJ, mode)
+            q = np.nonzero(oi >= 0)[0]
+            if mode == abi.SFM_MATCH_RATIO:
+                want = sorted(zip(oi[q].tolist(), q.tolist(), od[q].view(np.uint32).tolist()))
+            else:
+                want = sorted(zip(q.tolist(), oi[q].tolist(), od[q].view(np.uint32).tolist()))
+            got = list(zip(i[k:k + counts[p]].tolist(), j[k:k + counts[p]].tolist(),
+                           d[k:k + counts[p]].view(np.uint32).tolist()))
+            assert got == want, (p, I, J)
+            k += counts[p]
+    with pytest.raises(RuntimeError):
+        plan.run(pairs, abi.SFM_MATCH_CASCADE)     # hashing needs integer descriptors
+    plan.close()

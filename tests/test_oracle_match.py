@@ -10,6 +10,8 @@ import pytest
 import _helpers as H
 from golden.make_golden import numpy_match
 
+abi = H.abi
+
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
@@ -64,3 +66,32 @@ def test_ratio_uses_float32_square_of_0p8():
     q = np.zeros((1, 128), np.uint8)
     oi, od = H.oracle_match_dense(db, q, 0)
     assert oi[0] == 0 and od[0] == 64
+
+
+def test_oracle_f32_integer_valued_equals_u8():
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, size=(200, 128), dtype=np.uint8)
+    b = rng.integers(0, 256, size=(150, 128), dtype=np.uint8)
+    b[:20] = a[:20]
+    for mode in (abi.SFM_MATCH_RATIO, abi.SFM_MATCH_MUTUAL):
+        ui, ud = H.oracle_match_dense(a, b, mode)
+        fi, fd = H.oracle_match_dense_f32(a.astype(np.float32), b.astype(np.float32), mode)
+        np.testing.assert_array_equal(ui, fi)
+        np.testing.assert_array_equal(np.where(ui >= 0, ud, -1).astype(np.float32), fd)
+
+
+def test_oracle_f32_non_integer_against_float64():
+    # away from near-ties the f32 restatement picks the float64 nearest neighbour
+    rng = np.random.default_rng(4)
+    a = rng.random((300, 128), dtype=np.float32) * 100
+    b = rng.random((120, 128), dtype=np.float32) * 100
+    fi, fd = H.oracle_match_dense_f32(a, b, abi.SFM_MATCH_MUTUAL)
+    D = ((a[:, None, :].astype(np.float64) - b[None, :, :]) ** 2).sum(-1)
+    nn = D.argmin(1)
+    srt = np.sort(D, 1)
+    clear = srt[:, 1] - srt[:, 0] > 1e-3 * srt[:, 0]
+    mutual = D.argmin(0)[nn] == np.arange(len(a))
+    want = np.where(mutual, nn, -1)
+    np.testing.assert_array_equal(fi[clear], want[clear])
+    ok = fi >= 0
+    np.testing.assert_allclose(fd[ok], D[np.arange(len(a))[ok], fi[ok]], rtol=1e-5)
