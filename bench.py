@@ -302,17 +302,22 @@ def pmc_measure(args, kernel_regex="schur_kernel"):
     return out
 
 
-def bench_loop(ctx, n_img, cpu=True, cpu_images=16):
+def bench_loop(ctx, n_img, cpu=True, cpu_images=16, fixed_writeback=False, imgs=None):
     """C5: SequentialActuator over the synthetic closed orbit (src/main.cpp:99-108):
     init + BA, then addSingleImage + BA per image, a fresh BundleAdjuster per
     call.  Images are generated before the timed region (they stand for what
-    detectAndCompute leaves behind); the timed region is the whole loop."""
+    detectAndCompute leaves behind); the timed region is the whole loop.
+    fixed_writeback: the write-back without the Image::setIntrinsic quirk, so
+    the world keeps growing to the end of the orbit."""
     seq = api.OrbitSequence(n_img=n_img)
-    t0 = time.time()
-    imgs = [seq.image(k) for k in range(n_img)]
-    log(f"loop: {n_img} images generated in {time.time() - t0:.1f}s "
-        f"({np.mean([len(i['kp']) for i in imgs]):.0f} keypoints each)")
-    lp = api.SeqLoop(ctx)
+    if imgs is None:
+        t0 = time.time()
+        imgs = [seq.image(k) for k in range(n_img)]
+        log(f"loop: {n_img} images generated in {time.time() - t0:.1f}s "
+            f"({np.mean([len(i['kp']) for i in imgs]):.0f} keypoints each)")
+    so = api.seq_default_options()
+    so.fixed_writeback = 1 if fixed_writeback else 0
+    lp = api.SeqLoop(ctx, so)
     steps = []
     t0 = time.perf_counter()
     lp.init(imgs[0], imgs[1])
@@ -329,7 +334,8 @@ def bench_loop(ctx, n_img, cpu=True, cpu_images=16):
              for f in ("local_match", "global_match", "geometry", "ba")}
     iters = sum(s.ba.iterations for s in steps)
     last = steps[-1]
-    out = {"metric": "C5 incremental loop images/sec", "value": n_img / dt, "unit": "images/s",
+    out = {"metric": "C5 incremental loop images/sec" + (", fixed write-back" if fixed_writeback else ""),
+           "value": n_img / dt, "unit": "images/s",
            "seconds": dt, "stage_seconds": stage,
            "ba_calls": len(steps), "ba_lm_iterations": iters,
            "ba_lm_iters_per_sec_in_loop": iters / max(stage["ba"], 1e-12),
@@ -350,9 +356,12 @@ def bench_loop(ctx, n_img, cpu=True, cpu_images=16):
                                   f"({seq.cfg.n_landmarks} landmarks, tracks ~{seq.cfg.track_mean:g} images, "
                                   f"{seq.cfg.n_clutter} clutter keypoints/image), LocalFrame + GlobalFrame "
                                   "mutual matching and a fresh BundleAdjuster per image, "
-                                  "Image::setIntrinsic quirk on (reference write-back)",
+                                  + ("fixed write-back (Image::setIntrinsic quirk off)" if fixed_writeback else
+                                     "Image::setIntrinsic quirk on (reference write-back)"),
                        "host_malloc": "SFM_CTX_TUNE_HOST_MALLOC (opt-in, bench process only)"}}
-    log(f"loop: {n_img} images in {dt:.2f}s ({n_img / dt:.1f} images/s), stages "
+    out["images"] = imgs
+    log(f"loop{' (fixed write-back)' if fixed_writeback else ''}: {n_img} images in {dt:.2f}s "
+        f"({n_img / dt:.1f} images/s), kept {out['kept_images']}, stages "
         + ", ".join(f"{k} {v:.2f}s" for k, v in stage.items())
         + f"; {iters} LM iterations; world {last.world_points} pts / {last.world_observations} obs")
     if cpu:
@@ -784,9 +793,11 @@ def main():
             f"{len(pairs) / cdt:.0f} pairs/s, match kernels {ckms:.1f} ms")
 
     # ---------------- incremental loop (C5) ----------------
-    loop = None
+    loop = loop_fixed = None
     if world == 1 and rank == 0 and not args.no_loop and args.fake_world <= 1:
         loop = bench_loop(ctx, args.loop_images, cpu=not args.no_cpu_baseline)
+        loop_fixed = bench_loop(ctx, args.loop_images, cpu=False, fixed_writeback=True, imgs=loop.pop("images"))
+        loop_fixed.pop("images", None)
 
     # ---------------- dense-S stress case ----------------
     dense_s = None
@@ -866,6 +877,7 @@ def main():
             "ba_snavely": snav,
             "ba_pcie_inclusive": pcie,
             "loop": loop,
+            "loop_fixed_writeback": loop_fixed,
             "filter": filt,
             "ba_dense_s": dense_s,
             "ba_radial3": radial3,

@@ -355,3 +355,40 @@ def test_memory_cache_across_contexts_and_shapes(ctx):
             c2.close()
             c2 = api.Context(0)
     c2.close()
+
+
+def test_consecutive_invalid_steps_fail_like_oracle(ctx):
+    # A point at P = (0, 0, 1e-160) in the frame of a camera at the identity
+    # pose: its residual is finite, but without Jacobi scaling J'J overflows,
+    # so every step from iteration 1 on is non-finite (ba_solver.cpp:501-526:
+    # step_is_valid = 0, radius / decrease_factor, decrease_factor x 2) until
+    # max_num_consecutive_invalid_steps (Ceres default 5) ends the solve with
+    # FAILURE, and the world is not written back (BundleAdjuster.h:128-131).
+    sc = H.Scene(10, 300, 4, seed=21)
+    c = int(sc.obs_img[sc.pt_offsets[0]])
+    assert c != sc.const_img
+    sc.extr[6 * c:6 * c + 6] = 0.0
+    sc.X[0:3] = [0.0, 0.0, 1e-160]
+    o = abi.default_options()
+    o.jacobi_scaling = 0
+    orc_rc, os_, otr, _ = H.oracle_solve(sc, o)
+    assert orc_rc == abi.SFM_ERR_SOLVER and os_.termination == abi.SFM_TERM_FAILURE
+    assert [t.step_is_valid for t in otr] == [1, 0, 0, 0, 0]
+    plan = api.BAPlan(ctx, sc.problem(), *sc.params())
+    rc, gs = plan.run(o)
+    gtr = plan.trace()
+    plan.close()
+    assert rc == orc_rc and gs.termination == os_.termination and not gs.usable
+    assert gs.iterations == os_.iterations
+    assert len(gtr) == len(otr)
+    for g, t in zip(gtr, otr):
+        assert (g.iteration, g.step_is_valid, g.step_is_successful) == \
+               (t.iteration, t.step_is_valid, t.step_is_successful)
+        assert g.trust_region_radius == t.trust_region_radius
+        assert abs(g.cost / t.cost - 1) < 1e-12
+    e, i, x = sc.params()
+    e0, x0 = e.copy(), x.copy()
+    rc2, gs2 = api.ba_solve(ctx, sc.problem(), e, i, x, o)
+    assert rc2 == orc_rc and not gs2.usable
+    np.testing.assert_array_equal(e, e0)
+    np.testing.assert_array_equal(x, x0)

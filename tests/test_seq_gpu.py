@@ -106,3 +106,50 @@ def test_c5_loop_fixed_writeback_and_drop(ctx):
     gl, ol, steps = _run_both(ctx, seq, 12, o, H.corrupted_sequence(seq, 12, 6))
     assert [s.kept for s in steps] == [1] * 5 + [0] + [1] * 5
     assert steps[6].local_kept > 100     # image 7 matched against image 5
+
+
+def _full_loop(ctx, imgs, opts):
+    lp = api.SeqLoop(ctx, opts)
+    lp.init(imgs[0], imgs[1])
+    lp.bundle_adjust()
+    steps = [lp.step()]
+    for k in range(2, len(imgs)):
+        lp.add(imgs[k])
+        lp.bundle_adjust()
+        steps.append(lp.step())
+    lp.close()
+    return steps
+
+
+def _step_key(s):
+    return (s.kept, s.world_points, s.world_observations, s.ba_rc, s.ba.iterations, s.ba.successful_steps,
+            np.float64(s.ba.initial_cost).view(np.uint64), np.float64(s.ba.final_cost).view(np.uint64))
+
+
+@pytest.mark.parametrize("fixed", [0, 1])
+def test_c5_full_300_image_loop_properties(ctx, fixed):
+    # The whole C5 run (300 images) in both write-back modes, twice: bit-identical
+    # step by step (kept decisions, world growth, every BA call's iterations and
+    # cost bits), and every usable BA call lowers the reference's "RMSE".  With
+    # the Image::setIntrinsic quirk (Image.h:131-141) the world stops growing
+    # once PnP fails on the rewritten camera; with the fixed write-back it grows
+    # to the end of the orbit.
+    seq = api.OrbitSequence()
+    imgs = [seq.image(k) for k in range(seq.n_img)]
+    o = api.seq_default_options()
+    o.fixed_writeback = fixed
+    a = _full_loop(ctx, imgs, o)
+    b = _full_loop(ctx, imgs, o)
+    assert [_step_key(s) for s in a] == [_step_key(s) for s in b]
+    kept = 1 + sum(s.kept for s in a)
+    usable = [s.ba for s in a if s.ba.usable]
+    assert len(usable) >= len(a) - 2
+    assert all(s.rmse_final <= s.rmse_initial for s in usable)
+    growth = max(k for k, s in enumerate(a) if s.world_points > (a[k - 1].world_points if k else 0))
+    print(f"fixed_writeback={fixed}: kept {kept}/{seq.n_img}, last growth at step {growth}, "
+          f"world {a[-1].world_points} pts, final rmse {a[-1].ba.rmse_initial:.3f} -> {a[-1].ba.rmse_final:.3f}")
+    if fixed:
+        assert kept >= 290 and growth >= 280
+        assert a[-1].ba.rmse_final < 2.0
+    else:
+        assert kept >= 120 and growth >= 100
