@@ -209,6 +209,7 @@ SIGNATURES = [
     ("sfm_ba_default_options", None, [C.POINTER(BAOptions)]),
     ("sfm_ba_solve", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,
                                C.POINTER(BAOptions), C.POINTER(BASummary)]),
+    ("sfm_ba_cache_clear", C.c_int, [C.c_void_p]),
     ("sfm_ba_plan_create", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,
                                      C.POINTER(C.c_void_p)]),
     ("sfm_ba_plan_run", C.c_int, [C.c_void_p, C.POINTER(BAOptions), C.POINTER(BASummary)]),

@@ -70,4 +70,53 @@ void ba_image_order(const int32_t* obs_img, const double* obs_uv, const int32_t*
     // the temporaries go back to the context's cache, stream-ordered
 }
 
+namespace {
+
+// shard observation s of shard point k: source observation pt_offsets[pt_src[k]] + (s - pt_off[k])
+__global__ void obs_source_kernel(const int32_t* __restrict__ pt_src, const int64_t* __restrict__ pt_offsets,
+                                  const int32_t* __restrict__ pt_off, int32_t n_spt, int32_t* __restrict__ obs_src) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_spt) return;
+    const int64_t o0 = pt_offsets[pt_src[k]];
+    for (int32_t s = pt_off[k]; s < pt_off[k + 1]; ++s) obs_src[s] = (int32_t)(o0 + (s - pt_off[k]));
+}
+
+__global__ void gather_uv_kernel(const int32_t* __restrict__ obs_src, const double2* __restrict__ src, int32_t n,
+                                 double2* __restrict__ dst) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) dst[s] = src[obs_src[s]];
+}
+
+__global__ void gather_points_kernel(const int32_t* __restrict__ pt_src, const double* __restrict__ src, int32_t n,
+                                     double* __restrict__ dst) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 3 * n) return;
+    const int k = e / 3;
+    dst[e] = src[3 * (int64_t)pt_src[k] + (e - 3 * k)];
+}
+
+}  // namespace
+
+void ba_obs_source(const int32_t* pt_src, const int64_t* pt_offsets, const int32_t* pt_off, int32_t n_spt,
+                   int32_t* obs_src, hipStream_t s) {
+    if (n_spt <= 0) return;
+    hipLaunchKernelGGL(obs_source_kernel, dim3((unsigned)((n_spt + 255) / 256)), dim3(256), 0, s, pt_src, pt_offsets,
+                       pt_off, n_spt, obs_src);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_gather_uv(const int32_t* obs_src, const double* src_uv, int32_t n_sobs, double* dst_uv, hipStream_t s) {
+    if (n_sobs <= 0) return;
+    hipLaunchKernelGGL(gather_uv_kernel, dim3((unsigned)((n_sobs + 255) / 256)), dim3(256), 0, s, obs_src,
+                       reinterpret_cast<const double2*>(src_uv), n_sobs, reinterpret_cast<double2*>(dst_uv));
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_gather_points(const int32_t* pt_src, const double* src_X, int32_t n_spt, double* dst_X, hipStream_t s) {
+    if (n_spt <= 0) return;
+    hipLaunchKernelGGL(gather_points_kernel, dim3((unsigned)((3 * (int64_t)n_spt + 255) / 256)), dim3(256), 0, s,
+                       pt_src, src_X, n_spt, dst_X);
+    SFM_HIP(hipGetLastError());
+}
+
 }  // namespace sfm

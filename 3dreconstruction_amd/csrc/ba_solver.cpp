@@ -24,6 +24,9 @@
 #include <cstring>
 #include <limits>
 #include <vector>
+#include <unordered_map>
+#include <thread>
+#include <mutex>
 
 #include "ba_bcr.h"
 #include "ba_kernels.h"
@@ -61,6 +64,11 @@ struct sfm_ba_plan {
     DBuf<unsigned long long> stamps;   // SFM_SCHUR_STAMPS=1 diagnostic
     DBuf<unsigned long long> bcr_stamps;   // SFM_BCR_STAMPS=1 diagnostic
     DBuf<double> scal_g;                   // [world][kScMaxEnd] gathered partial scalars
+    // plan-cache refresh (sfm_ba_solve): shard -> problem point / observation
+    // maps (built on the first refresh) and staging for the new values
+    DBuf<int32_t> pt_src, obs_src;
+    DBuf<int64_t> src_off;
+    DBuf<double> raw_uv, raw_X;
     std::vector<double> scal_gh;
     BcrArgs bcr;
     bool use_bcr = false;
@@ -337,6 +345,45 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     h.obs_slot = HostVec<int32_t>();
     h.obs_uv = HostVec<double>();
     tm.mark("sync");
+}
+
+// New values for a plan whose problem structure is unchanged (the plan
+// cache of sfm_ba_solve): measurements, points, poses and intrinsics are
+// uploaded as the caller holds them and gathered into the plan's shard order
+// on the device; the image-ordered copy is rebuilt.  Everything structural
+// (order, chunks, reduce plan, RCS layout) is kept.
+void refresh_values(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr, const double* intr,
+                    const double* X) {
+    sfm_ctx* ctx = pl->ctx;
+    hipStream_t s = ctx->stream;
+    BAHostPlan& h = pl->hp;
+    PhaseTimer tm("refresh_values");
+    if (!pl->obs_src.p && h.n_sobs > 0) {
+        std::vector<int32_t> ps(h.n_spt);
+        for (int64_t k = 0; k < h.n_spt; ++k) ps[k] = (int32_t)h.spt_global[k];
+        up(pl->pt_src, ps, s);
+        pl->src_off.alloc(prob.n_pt + 1);
+        pl->src_off.upload(prob.pt_offsets, prob.n_pt + 1, s);
+        pl->obs_src.alloc(h.n_sobs);
+        ba_obs_source(pl->pt_src.p, pl->src_off.p, pl->pt_off.p, (int32_t)h.n_spt, pl->obs_src.p, s);
+        tm.mark("maps");
+    }
+    if (h.n_sobs > 0) {
+        if (pl->raw_uv.n < 2 * (size_t)prob.n_obs) pl->raw_uv.alloc(2 * (size_t)prob.n_obs);
+        SFM_HIP(hipMemcpyAsync(pl->raw_uv.p, prob.obs_uv, 2 * (size_t)prob.n_obs * 8, hipMemcpyHostToDevice, s));
+        ba_gather_uv(pl->obs_src.p, pl->raw_uv.p, (int32_t)h.n_sobs, pl->obs_uv.p, s);
+        ba_image_order(pl->obs_img.p, pl->obs_uv.p, pl->pt_off.p, (int32_t)h.n_sobs, (int32_t)h.n_spt, prob.n_img,
+                       pl->img_pt.p, pl->img_uv.p, s);
+    }
+    if (h.n_spt > 0) {
+        if (pl->raw_X.n < 3 * (size_t)prob.n_pt) pl->raw_X.alloc(3 * (size_t)prob.n_pt);
+        SFM_HIP(hipMemcpyAsync(pl->raw_X.p, X, 3 * (size_t)prob.n_pt * 8, hipMemcpyHostToDevice, s));
+        ba_gather_points(pl->pt_src.p, pl->raw_X.p, (int32_t)h.n_spt, pl->X0.p, s);
+    }
+    SFM_HIP(hipMemcpyAsync(pl->extr0.p, extr, 6 * (size_t)prob.n_img * 8, hipMemcpyHostToDevice, s));
+    SFM_HIP(hipMemcpyAsync(pl->intr0.p, intr, (size_t)h.iw * prob.n_intr * 8, hipMemcpyHostToDevice, s));
+    pl->P.huber_a = prob.huber_a;
+    tm.mark("upload+gather");
 }
 
 // Wait for finalize_kernel's publish of the iteration scalars (sequence word
@@ -709,13 +756,140 @@ extern "C" int sfm_ba_plan_get_trace(sfm_ba_plan* pl, sfm_ba_iter* out, int32_t 
     });
 }
 
+namespace {
+
+// ---- plan cache of sfm_ba_solve -------------------------------------------
+// The reference builds a fresh problem per BundleAdjuster call
+// (SequentialActuator.h:226-229); when the problem's structure (points,
+// observation images, intrinsics assignment, gauge, model) equals the last
+// one solved on this context -- a world that did not grow since the last
+// call, or a caller re-solving the same problem -- the plan is reused and
+// only the values are refreshed.  Keyed by an exact comparison, never a hash.
+// SFM_BA_NO_PLAN_CACHE=1 disables it; sfm_ba_cache_clear releases it.
+struct PlanKey {
+    int32_t n_img = -1, n_intr = 0, const_img = 0, model = 0;
+    int64_t n_pt = 0, n_obs = 0;
+    std::vector<int64_t> pt_offsets;
+    std::vector<int32_t> obs_img, img_intr;
+
+    template <class T>
+    static bool same(const T* a, const T* b, int64_t n) {
+        if (n <= 0) return true;
+        const int64_t kPar = 1 << 20;
+        if (n < kPar) return std::memcmp(a, b, (size_t)n * sizeof(T)) == 0;
+        const int nt = 8;
+        std::atomic<bool> ok{true};
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+                if (std::memcmp(a + lo, b + lo, (size_t)(hi - lo) * sizeof(T)) != 0) ok = false;
+            });
+        for (auto& x : th) x.join();
+        return ok;
+    }
+    bool matches(const sfm_ba_problem& P) const {
+        return n_img == P.n_img && n_intr == P.n_intr && const_img == P.const_img && model == P.camera_model &&
+               n_pt == P.n_pt && n_obs == P.n_obs && same(pt_offsets.data(), P.pt_offsets, P.n_pt + 1) &&
+               same(img_intr.data(), P.img_intr, P.n_img) && same(obs_img.data(), P.obs_img, P.n_obs);
+    }
+    void assign(const sfm_ba_problem& P) {
+        n_img = P.n_img; n_intr = P.n_intr; const_img = P.const_img; model = P.camera_model;
+        n_pt = P.n_pt; n_obs = P.n_obs;
+        pt_offsets.assign(P.pt_offsets, P.pt_offsets + P.n_pt + 1);
+        obs_img.assign(P.obs_img, P.obs_img + P.n_obs);
+        img_intr.assign(P.img_intr, P.img_intr + P.n_img);
+    }
+};
+
+struct CacheEntry {
+    sfm_ba_plan* plan = nullptr;
+    PlanKey key;
+};
+
+std::mutex g_cache_mu;
+std::unordered_map<const sfm_ctx*, CacheEntry>& plan_cache() {
+    static auto* m = new std::unordered_map<const sfm_ctx*, CacheEntry>;
+    return *m;
+}
+
+bool cache_enabled() {
+    static const bool on = std::getenv("SFM_BA_NO_PLAN_CACHE") == nullptr;
+    return on;
+}
+
+// take the context's cached plan out of the cache (nullptr if none)
+sfm_ba_plan* cache_take(const sfm_ctx* ctx, PlanKey* key) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    auto it = plan_cache().find(ctx);
+    if (it == plan_cache().end()) return nullptr;
+    sfm_ba_plan* pl = it->second.plan;
+    *key = std::move(it->second.key);
+    plan_cache().erase(it);
+    return pl;
+}
+
+void cache_put(const sfm_ctx* ctx, sfm_ba_plan* pl, PlanKey&& key) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    CacheEntry& e = plan_cache()[ctx];
+    e.plan = pl;
+    e.key = std::move(key);
+}
+
+}  // namespace
+
+void sfm::ba_cache_release(sfm_ctx* ctx) {
+    PlanKey k;
+    if (sfm_ba_plan* pl = cache_take(ctx, &k)) sfm_ba_plan_destroy(pl);
+}
+
+extern "C" int sfm_ba_cache_clear(sfm_ctx* ctx) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx, SFM_ERR_INVALID_ARG, "null ctx");
+        ba_cache_release(ctx);
+        return SFM_OK;
+    });
+}
+
 extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* extr, double* intr,
                             double* X, const sfm_ba_options* opts, sfm_ba_summary* sum) {
-    sfm_ba_plan* pl = nullptr;
+    if (!ctx || !prob || !extr || !intr || (!X && prob->n_pt > 0)) {
+        set_error("null argument");
+        return SFM_ERR_INVALID_ARG;
+    }
     sfm::PhaseTimer tm("sfm_ba_solve");
-    int rc = sfm_ba_plan_create(ctx, prob, extr, intr, X, &pl);
-    tm.mark("create");
-    if (rc != SFM_OK) return rc;
+    sfm_ba_plan* pl = nullptr;
+    PlanKey key;
+    bool hit = false;
+    if (cache_enabled()) {
+        pl = cache_take(ctx, &key);
+        if (pl) {
+            hit = key.matches(*prob);
+            if (!hit) {
+                sfm_ba_plan_destroy(pl);
+                pl = nullptr;
+            }
+        }
+        tm.mark("cache_lookup");
+    }
+    int rc = SFM_OK;
+    if (hit) {
+        rc = guarded([&] {
+            CtxScope scope_(ctx);
+            refresh_values(pl, *prob, extr, intr, X);
+            return SFM_OK;
+        });
+        tm.mark("refresh");
+        if (rc != SFM_OK) {
+            sfm_ba_plan_destroy(pl);
+            return rc;
+        }
+    } else {
+        rc = sfm_ba_plan_create(ctx, prob, extr, intr, X, &pl);
+        tm.mark("create");
+        if (rc != SFM_OK) return rc;
+        if (cache_enabled()) key.assign(*prob);
+    }
     rc = sfm_ba_plan_run(pl, opts, sum);
     tm.mark("run");
     if (sum && sum->usable) {  // BundleAdjuster::updateWorld only on success (:179-184)
@@ -723,7 +897,10 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* ex
         if (rc == SFM_OK) rc = rc2;
     }
     tm.mark("download");
-    sfm_ba_plan_destroy(pl);
-    tm.mark("destroy");
+    // a device or communication error leaves the plan suspect: not kept
+    const bool keep = cache_enabled() && rc != SFM_ERR_DEVICE && rc != SFM_ERR_COMM;
+    if (keep) cache_put(ctx, pl, std::move(key));
+    else sfm_ba_plan_destroy(pl);
+    tm.mark(keep ? "cached" : "destroy");
     return rc;
 }

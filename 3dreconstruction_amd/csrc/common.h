@@ -211,6 +211,8 @@ struct sfm_ctx {
 };
 
 namespace sfm {
+// releases the context's cached BA plan (ba_solver.cpp; sfm_ctx_destroy)
+void ba_cache_release(sfm_ctx* ctx);
 // the context's two timing events (created once, destroyed with the context)
 inline hipEvent_t* ctx_events(sfm_ctx* ctx) {
     if (!ctx->ev[0]) {

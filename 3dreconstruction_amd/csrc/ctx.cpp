@@ -349,6 +349,7 @@ extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
     return guarded([&] {
         if (!ctx) return SFM_OK;
         (void)hipSetDevice(ctx->device);
+        ba_cache_release(ctx);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         rccl_comm_destroy(ctx->comm);
         if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);

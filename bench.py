@@ -653,15 +653,22 @@ def main():
     # plan, solve, download) -- reported beside the bench value, never as it
     pcie = None
     if world == 1:
-        e_h, i_h, x_h = sc["extr"].copy(), sc["intr"].copy(), sc["X"].copy()
-        t1 = time.perf_counter()
-        rc_h, s_h = api.ba_solve(ctx, sc["problem"], e_h, i_h, x_h)
-        dt_h = time.perf_counter() - t1
-        pcie = {"value": s_h.iterations / dt_h, "unit": "LM-iters/s", "seconds": dt_h,
-                "iterations": s_h.iterations,
-                "what": "one sfm_ba_solve from host buffers: upload + plan + LM solve + download"}
-        log(f"BA from host buffers: {dt_h * 1e3:.1f} ms for {s_h.iterations} iterations")
-        del e_h, i_h, x_h
+        def host_solve():
+            e_h, i_h, x_h = sc["extr"].copy(), sc["intr"].copy(), sc["X"].copy()
+            t1 = time.perf_counter()
+            rc_h, s_h = api.ba_solve(ctx, sc["problem"], e_h, i_h, x_h)
+            return s_h, time.perf_counter() - t1
+        s_c, dt_c = host_solve()     # plan built from the host buffers (kept in the context)
+        s_w, dt_w = host_solve()     # same structure again: plan reused, values re-uploaded
+        pcie = {"value": s_w.iterations / dt_w, "unit": "LM-iters/s", "seconds": dt_w,
+                "iterations": s_w.iterations,
+                "what": "sfm_ba_solve from host buffers with the context's cached plan (same problem "
+                        "structure as the previous call): value upload + device gather + LM solve + download",
+                "cold": {"value": s_c.iterations / dt_c, "seconds": dt_c,
+                         "what": "first sfm_ba_solve: upload + symbolic plan + LM solve + download"}}
+        log(f"BA from host buffers: cold {dt_c * 1e3:.1f} ms, plan reused {dt_w * 1e3:.1f} ms "
+            f"for {s_w.iterations} iterations")
+        abi.load().sfm_ba_cache_clear(ctx.h)
 
     # ---------------- BA, BAL residual model ----------------
     snav = None

@@ -205,6 +205,14 @@ void sfm_ba_default_options(sfm_ba_options* opts);
 int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob,
                  double* extr, double* intr, double* X,
                  const sfm_ba_options* opts, sfm_ba_summary* summary);
+/* sfm_ba_solve keeps its last plan in the context: a later call whose problem
+ * has the same structure (n_*, pt_offsets, obs_img, img_intr, const_img,
+ * camera_model -- compared exactly) reuses it and only uploads the new values
+ * (a world that did not grow since the previous BundleAdjuster call,
+ * SequentialActuator.h:226-229).  This releases that plan (its device
+ * memory); sfm_ctx_destroy does too.  SFM_BA_NO_PLAN_CACHE=1 turns the cache
+ * off. */
+int sfm_ba_cache_clear(sfm_ctx* ctx);
 
 /* Resident variant (used by the benchmark): the plan uploads the problem and
  * the initial parameters once; every sfm_ba_plan_run restarts from those

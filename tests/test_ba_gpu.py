@@ -392,3 +392,50 @@ def test_consecutive_invalid_steps_fail_like_oracle(ctx):
     assert rc2 == orc_rc and not gs2.usable
     np.testing.assert_array_equal(e, e0)
     np.testing.assert_array_equal(x, x0)
+
+
+def _solve_keep(ctx, sc, e, i, x, opts=None):
+    rc, s = api.ba_solve(ctx, sc.problem(), e, i, x, opts)
+    return rc, s, (e, i, x)
+
+
+def test_plan_cache_reuse_is_bit_identical(ctx):
+    # sfm_ba_solve keeps its plan in the context; a problem of the same
+    # structure reuses it with only the values refreshed.  Every reuse must
+    # equal a solve from a fresh plan bit for bit: the same values twice, new
+    # measurements and points on the same structure, then a changed structure.
+    lib = abi.load()
+    sc = H.Scene(30, 4000, 6, seed=404)
+    lib.sfm_ba_cache_clear(ctx.h)
+    cold = _solve_keep(ctx, sc, *sc.params())            # plan built, kept
+    warm = _solve_keep(ctx, sc, *sc.params())            # same problem: reused
+    for a, b in ((cold, warm),):
+        assert a[0] == b[0] == 0
+        assert (a[1].iterations, a[1].final_cost, a[1].initial_cost) == (b[1].iterations, b[1].final_cost,
+                                                                         b[1].initial_cost)
+        for u, v in zip(a[2], b[2]):
+            np.testing.assert_array_equal(u, v)
+    # new values, same structure: reused vs a fresh plan (cache cleared)
+    rng = np.random.default_rng(1)
+    sc.obs_uv += rng.normal(0, 0.3, sc.obs_uv.shape)
+    sc.X += rng.normal(0, 0.01, sc.X.shape)
+    sc.extr[12:18] += 1e-3
+    reused = _solve_keep(ctx, sc, *sc.params())
+    lib.sfm_ba_cache_clear(ctx.h)
+    fresh = _solve_keep(ctx, sc, *sc.params())
+    assert reused[0] == fresh[0] == 0
+    assert (reused[1].iterations, reused[1].final_cost) == (fresh[1].iterations, fresh[1].final_cost)
+    for u, v in zip(reused[2], fresh[2]):
+        np.testing.assert_array_equal(u, v)
+    # and it is still the oracle's solve
+    _, os_, _, _ = H.oracle_solve(sc, threads=8)
+    assert reused[1].iterations == os_.iterations
+    assert abs(reused[1].rmse_final / os_.rmse_final - 1) < RTOL_COST
+    # a structure change (one observation moved to another image) is not reused
+    o = int(sc.pt_offsets[7])
+    sc.obs_img[o] = (sc.obs_img[o] + 3) % sc.n_cam
+    changed = _solve_keep(ctx, sc, *sc.params())
+    _, os2, _, _ = H.oracle_solve(sc, threads=8)
+    assert changed[0] == 0 and changed[1].iterations == os2.iterations
+    assert abs(changed[1].rmse_final / os2.rmse_final - 1) < RTOL_COST
+    lib.sfm_ba_cache_clear(ctx.h)
