@@ -29,6 +29,7 @@ SFM_CAM_SNAVELY = 1
 SFM_CAM_RADIAL3 = 2
 
 SFM_CTX_TUNE_HOST_MALLOC = 1
+SFM_CTX_DIAG_NO_EXCHANGE = 2
 
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1

@@ -121,6 +121,9 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
              hipStream_t s);
 // seq: written to scal_host[kScCount] after the scalars when scal_host is set
 void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq = 0);
+// world > 1 (RCCL): combine the all-gathered scalars in rank order and publish them
+void ba_publish_gathered(const double* gathered, int world, double* scal, double* scal_host, hipStream_t s,
+                         unsigned long long seq);
 size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
 size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);

@@ -2048,6 +2048,30 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
     }
 }
 
+// world > 1 over RCCL: the all-gathered per-rank scalars [world][kScMaxEnd]
+// combined in rank order (sums, maxima; the replicated slots are this rank's)
+// and published to host-mapped memory like finalize_kernel does at one rank,
+// so the host polls a sequence word instead of copying and synchronising
+__global__ void publish_gathered_kernel(const double* __restrict__ g, int world, double* __restrict__ scal,
+                                        double* __restrict__ host, unsigned long long seq) {
+    const int k = threadIdx.x;
+    if (k < kScCount) {
+        double v = k < kScMaxEnd ? g[k] : scal[k];
+        if (k < kScMaxEnd)
+            for (int r = 1; r < world; ++r) {
+                const double w = g[(size_t)r * kScMaxEnd + k];
+                v = k < kScSumEnd ? v + w : fmax(v, w);
+            }
+        scal[k] = v;
+        host[k] = v;
+        __threadfence_system();
+    }
+    __syncthreads();
+    if (k == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(host + kScCount), seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2235,6 +2259,12 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
 
 void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq) {
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinThreads), 0, s, P, ba_step_blocks(P), seq);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_publish_gathered(const double* gathered, int world, double* scal, double* scal_host, hipStream_t s,
+                         unsigned long long seq) {
+    hipLaunchKernelGGL(publish_gathered_kernel, dim3(1), dim3(64), 0, s, gathered, world, scal, scal_host, seq);
     SFM_HIP(hipGetLastError());
 }
 

@@ -726,6 +726,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     for (int img = 0; img < P.n_img; ++img) {
         const int cb = pl.cam_blk[img], q = pl.intr_blk[P.img_intr[img]];
         if (pl.img_obs_ptr[img + 1] == pl.img_obs_ptr[img] && cb < 0 && q < 0) continue;
+        // a landmark shard: an image none of this rank's observations sees
+        // contributes nothing here (its blocks come from the other ranks)
+        if (world > 1 && pl.img_obs_ptr[img + 1] == pl.img_obs_ptr[img]) continue;
         const int32_t fq = q >= 0 ? pl.ncam + q : -1;
         if (cb >= 0) {
             add_u(mterms, (int64_t)cb * nFB + cb, kSrcU, img, 0, 0);
@@ -925,6 +928,17 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstBF, col_of_fb(fb), size_of_fb(fb), 1, 1, bterms, ib, nullptr, nullptr);
     }
     for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstCnF, col_of_fb(fb), size_of_fb(fb), 1, 1, cterms, ic, nullptr, nullptr);
+    if (world > 1) {
+        // a shard writes only the blocks its points touch (about 1/world of the
+        // band); the solver clears the reduced camera system before each
+        // reduce instead of gathering zeros into the rest
+        size_t w = 0;
+        for (size_t t = 0; t < pl.targets.size(); ++t) {
+            const ReduceTarget& T = pl.targets[t];
+            if (T.c_begin != T.c_end || T.p_begin != T.p_end) pl.targets[w++] = T;
+        }
+        pl.targets.resize(w);
+    }
     tm.mark("targets");
 }
 

@@ -69,7 +69,6 @@ struct sfm_ba_plan {
     DBuf<int32_t> pt_src, obs_src;
     DBuf<int64_t> src_off;
     DBuf<double> raw_uv, raw_X;
-    std::vector<double> scal_gh;
     BcrArgs bcr;
     bool use_bcr = false;
     int64_t rcs_n = 0;
@@ -219,7 +218,6 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->scal.zero(s);
     if (ctx->comm) {
         pl->scal_g.alloc((size_t)ctx->world * kScMaxEnd);
-        pl->scal_gh.assign(pl->scal_g.n, 0.0);
     }
     pl->scal_h = static_cast<double*>(pinned_alloc((kScCount + 1) * sizeof(double)));
     std::memset(pl->scal_h, 0, (kScCount + 1) * sizeof(double));
@@ -445,6 +443,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     ba_fill(pl->scaleE.p, (int64_t)nx, 1.0, s);
     if (O.jacobi_scaling) {
         relinearize();                 // unscaled column norms of the F blocks
+        if (ctx->world > 1) SFM_HIP(hipMemsetAsync(pl->rcs.p, 0, (size_t)pl->rcs_n * sizeof(double), s));
         ba_reduce(P, true, s);
         allreduce_rcs();
         ba_fscale(P, s);
@@ -456,7 +455,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
 
     // one rank: the scalars come back through host-mapped memory (wait_scalars);
     // several: the device all-gather / host all-reduce below
-    P.scal_host = ctx->world == 1 ? pl->scal_dev : nullptr;
+    // (with an RCCL communicator, even a 1-rank one, the scalars go through
+    // the all-gather and publish_gathered_kernel instead)
+    P.scal_host = (!ctx->comm && (ctx->world == 1 || ctx->no_exchange)) ? pl->scal_dev : nullptr;
     double radius = O.initial_trust_region_radius, decrease_factor = 2.0;
     int consecutive_invalid = 0;
     double x_cost = 0.0, x_norm = 0.0;
@@ -490,10 +491,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(ev[0], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
         if (timed) SFM_HIP(hipEventRecord(ev[1], s));
-        // dense S across ranks: each rank writes only the blocks its own
-        // points touch, so the summed S of the last iteration is cleared first
-        if (P.dense && ctx->world > 1)
-            SFM_HIP(hipMemsetAsync(P.Sdense, 0, (size_t)h.n_sdense * sizeof(double), s));
+        // across ranks each shard writes only the blocks its own points touch,
+        // so the summed system of the last iteration is cleared first
+        if (ctx->world > 1) SFM_HIP(hipMemsetAsync(pl->rcs.p, 0, (size_t)pl->rcs_n * sizeof(double), s));
         ba_reduce(P, false, s);
         allreduce_rcs();
         if (P.dense) dense_solve(pl->dense, P, radius, s);
@@ -506,21 +506,13 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (P.scal_host) {
             wait_scalars(pl->scal_h, seq, s);
         } else if (ctx->comm && !ctx->host_allreduce) {
-            // one RCCL collective: gather every rank's partial scalars, then sum
-            // (rank order) / max them on the host
+            // one RCCL collective: gather every rank's partial scalars; a
+            // one-wave kernel sums (rank order) / maxes them and publishes to
+            // host-mapped memory, polled as at one rank (no copy, no sync)
             SFM_REQUIRE(rccl_allgather_f64(ctx->comm, P.scal, pl->scal_g.p, kScMaxEnd, s) == 0, SFM_ERR_COMM,
                         "RCCL all-gather failed");
-            SFM_HIP(hipMemcpyAsync(pl->scal_h, P.scal, kScCount * 8, hipMemcpyDeviceToHost, s));
-            SFM_HIP(hipMemcpyAsync(pl->scal_gh.data(), pl->scal_g.p, pl->scal_g.n * 8, hipMemcpyDeviceToHost, s));
-            SFM_HIP(hipStreamSynchronize(s));
-            for (int k = kScSumBegin; k < kScMaxEnd; ++k) {
-                double v = pl->scal_gh[k];
-                for (int r = 1; r < ctx->world; ++r) {
-                    const double w = pl->scal_gh[(size_t)r * kScMaxEnd + k];
-                    v = k < kScSumEnd ? v + w : std::max(v, w);
-                }
-                pl->scal_h[k] = v;
-            }
+            ba_publish_gathered(pl->scal_g.p, ctx->world, P.scal, pl->scal_dev, s, seq);
+            wait_scalars(pl->scal_h, seq, s);
         } else {
             if (ctx->world > 1) {
                 ctx_allreduce(ctx, P.scal + kScSumBegin, kScSumEnd - kScSumBegin, 0, s);

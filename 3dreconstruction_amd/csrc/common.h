@@ -207,6 +207,7 @@ struct sfm_ctx {
     double* host_buf = nullptr;                  // pinned staging for host_allreduce
     size_t host_cap = 0;
     int cu_count = 0;
+    bool no_exchange = false;                    // SFM_CTX_DIAG_NO_EXCHANGE (per-rank timing only)
     hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
 };
 

@@ -244,7 +244,7 @@ extern "C" const char* sfm_version(void) { return "sfmcore 0.1.0 (gfx950)"; }
 extern "C" const char* sfm_last_error(void) { return g_err.c_str(); }
 
 void sfm::ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStream_t s) {
-    if (n == 0 || (ctx->world <= 1 && !ctx->comm)) return;   // a 1-rank RCCL comm still runs
+    if (n == 0 || (ctx->world <= 1 && !ctx->comm) || ctx->no_exchange) return;   // a 1-rank RCCL comm still runs
     if (!ctx->host_allreduce) {
         SFM_REQUIRE(rccl_allreduce_f64(ctx->comm, dev_buf, n, op_max, s) == 0, SFM_ERR_COMM,
                     "RCCL all-reduce failed");
@@ -327,7 +327,11 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
             std::lock_guard<std::mutex> lk(mc.mu);
             mc.streams.insert(c->stream);
         }
-        if (c->world > 1 && opts->allreduce && !opts->comm_id) {
+        if (opts->flags & SFM_CTX_DIAG_NO_EXCHANGE) {
+            SFM_REQUIRE(!opts->comm_id && !opts->allreduce, SFM_ERR_INVALID_ARG,
+                        "SFM_CTX_DIAG_NO_EXCHANGE excludes a communicator or an all-reduce hook");
+            c->no_exchange = true;
+        } else if (c->world > 1 && opts->allreduce && !opts->comm_id) {
             c->host_allreduce = opts->allreduce;
             c->host_allreduce_user = opts->allreduce_user;
         } else if (c->world > 1 || opts->comm_id) {   // comm_id at world_size 1: a 1-rank RCCL comm

@@ -606,8 +606,8 @@ def main():
             log("falling back to the host-staged gloo all-reduce")
     elif args.fake_world > 1:
         ctx = api.Context(device=local_rank, rank=0, world_size=args.fake_world,
-                          allreduce=lambda a, op: None)
-        transport = f"none (diagnostic: shard 0 of {args.fake_world}, no-op all-reduce)"
+                          flags=abi.SFM_CTX_DIAG_NO_EXCHANGE)
+        transport = f"none (diagnostic: shard 0 of {args.fake_world}, exchanges skipped on the device)"
     else:
         # opt-in host malloc setting for this short-lived process
         ctx = api.Context(device=local_rank, flags=abi.SFM_CTX_TUNE_HOST_MALLOC)

@@ -84,6 +84,11 @@ typedef struct sfm_ctx_opts {
  * price is that the heap does not shrink, so a long-running host application
  * leaves it off (the default: its malloc settings are not touched). */
 #define SFM_CTX_TUNE_HOST_MALLOC 1
+/* Diagnostic only: world_size > 1 with every exchange a no-op (no RCCL, no
+ * hook).  The context plans and runs rank `rank`'s landmark shard alone, so
+ * its kernels and wall time are what that rank spends in an N-GPU run minus
+ * the collectives; the solve is not the global one (bench.py --fake-world). */
+#define SFM_CTX_DIAG_NO_EXCHANGE 2
 
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
 int sfm_comm_unique_id(uint8_t* out128);
