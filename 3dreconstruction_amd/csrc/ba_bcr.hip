@@ -344,16 +344,16 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
         A[e] = a;
         Cm[e] = cc;
     }
-    // R: column 0 = rhs, columns 1 + 4k + a = arrow (intr k, row a) transposed
+    // R: column 0 = rhs, columns 1 + iw k + a = arrow (intr k, row a) transposed
     for (int e = 4 * rg * b.nrhs + threadIdx.x; e < 4 * (rg + 1) * b.nrhs; e += NT) {
         const int r = e / b.nrhs, c = e % b.nrhs;
         double v = 0.0;
         if (r < nreal) {
             const int ci = c0 + r / 6;
             if (c == 0) v = P.rhs[6LL * ci + r % 6];
-            else if (c - 1 < 4 * P.nintr) {
-                const int k = (c - 1) / 4, a = (c - 1) % 4;
-                v = P.Sarrow[((size_t)k * P.ncam + ci) * 24 + a * 6 + r % 6];
+            else if (c - 1 < P.iw * P.nintr) {
+                const int k = (c - 1) / P.iw, a = (c - 1) % P.iw;
+                v = P.Sarrow[((size_t)k * P.ncam + ci) * 6 * P.iw + a * 6 + r % 6];
             }
         }
         R[e] = v;
@@ -654,7 +654,7 @@ __global__ __launch_bounds__(64) void bcr_corner_part_kernel(BcrArgs b, int na4)
 
 // Pass 2: partials added in super-block order, then the small dense solve.
 __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
-    const int na4 = 4 * P.nintr;
+    const int na4 = P.iw * P.nintr, iw = P.iw;   // bordered columns (<= 16)
     __shared__ double Mc[16 * 16 + 16];
     // partials of super-blocks [g N/8, (g+1) N/8) per lane, the 8 lanes of an
     // element then combined by a fixed xor butterfly (deterministic)
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
             const int a = k / na4, c = k % na4;
             const double red = sum_parts(a * 16 + c, g);
             if (g == 0) {
-                double m = P.Scorner[(((size_t)(a / 4) * P.nintr + c / 4) * 16) + (a % 4) * 4 + c % 4];
+                double m = P.Scorner[(((size_t)(a / iw) * P.nintr + c / iw) * iw * iw) + (a % iw) * iw + c % iw];
                 if (a == c) {
                     const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
                     m += lm * lm;
@@ -727,18 +727,20 @@ __global__ void bcr_final_kernel(BcrArgs b, DevProblem P) {
     const int ci = (int)(e / 6), I = ci / b.K, row = (ci - I * b.K) * 6 + (int)(e % 6);
     const double* Y = b.Y + ((size_t)I * M + row) * b.nrhs;
     double v = Y[0];
-    for (int a = 0; a < 4 * P.nintr; ++a) v -= Y[1 + a] * P.yF[P.nb + a];
+    for (int a = 0; a < P.iw * P.nintr; ++a) v -= Y[1 + a] * P.yF[P.nb + a];
     P.yF[e] = v;
 }
 
 }  // namespace
 
-bool bcr_supported(const DevProblem& P) { return P.D <= kBcrK && P.ncam > 0 && 1 + 4 * P.nintr <= 32; }
+// the bordered arrow: iw * nintr <= 16 columns (one MFMA column tile beside
+// the rhs; bcr_corner_part_kernel's 16 lanes, bcr_corner_kernel's 16 x 16)
+bool bcr_supported(const DevProblem& P) { return P.D <= kBcrK && P.ncam > 0 && P.iw * P.nintr <= 16; }
 
 void bcr_setup(BcrArgs& b, const DevProblem& P) {
     b.K = kBcrK;
     b.N = (P.ncam + b.K - 1) / b.K;
-    b.nrhs = ((1 + 4 * P.nintr) + 15) / 16 * 16;   // MFMA column tiles
+    b.nrhs = ((1 + P.iw * P.nintr) + 15) / 16 * 16;   // MFMA column tiles
 }
 
 size_t bcr_doubles(const BcrArgs& b) {
@@ -786,7 +788,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, stride);
         SFM_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(bcr_corner_part_kernel, dim3(b.N), dim3(64), 0, s, b, 4 * P.nintr);
+    hipLaunchKernelGGL(bcr_corner_part_kernel, dim3(b.N), dim3(64), 0, s, b, P.iw * P.nintr);
     SFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(bcr_corner_kernel, dim3(1), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());

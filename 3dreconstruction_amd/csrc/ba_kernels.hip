@@ -639,7 +639,9 @@ template <int CM, int NT, int SP = kSubPts, int SO = kSubObs, bool SE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WPE, SFM_SCHUR_WPE))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
-    static_assert(kIW<CM> == 4, "chunk tiles hold 4-wide intrinsics blocks");
+    constexpr int IW = kIW<CM>;   // tile rows (and F columns) of an intrinsics block
+    // intrinsics parameters with a Jacobian column: SNAVELY's 4th double is not one
+    constexpr int NK = CM == SFM_CAM_SNAVELY ? 3 : IW;
     unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
     if (stamps) tprev = stamp();
 #define SFM_STAMP(k)                                      \
@@ -658,7 +660,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
     // per-observation rows use odd strides (in doubles): a wave's ds_*_b64 at
     // lane-strided rows then hits 32 distinct bank pairs (even strides of 4,
     // 6, 10 doubles were 2- to 4-way bank conflicts, SQ_LDS_BANK_CONFLICT)
-    constexpr int kOb = CM == SFM_CAM_SNAVELY ? 7 : 5;
+    // pinhole: the 4 nonzeros of J_intr; SNAVELY / RADIAL3: both rows of every
+    // parameter column (2 NK values)
+    constexpr int kOb = CM == SFM_CAM_PINHOLE ? 5 : 2 * NK + 1;
     __shared__ double ob[SO][kOb];              // J_intr nonzeros (scaled) | pad
     // per observation: Jx'Jx (6) | Jx'f (3) until the per-point sums, then
     // M = Jx L^-T (6) from phase B on (obm: the same rows; 3.5 KB less LDS per
@@ -670,7 +674,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
     // chunk-level staging: every camera / intrinsics block the chunk touches
     __shared__ CamPreL scp[kCamSlots];
     __shared__ double csc[kCamSlots][6];        // camera column scales (0: constant image)
-    __shared__ double isc[kIntrSlots][8];       // intrinsics | their column scales
+    __shared__ double isc[kIntrSlots][2 * IW];  // intrinsics | their column scales
     __shared__ int crow[kCamSlots], irow[kIntrSlots];
     __shared__ int cpoff[kChunkPts + 1];        // chunk point offsets, relative to obs_begin
     const int c = blockIdx.x, lane = threadIdx.x;
@@ -686,10 +690,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
             csc[t][e - 6 * t] = col >= 0 ? P.scaleF[col + e - 6 * t] : 0.0;
         }
         if (lane < cd.n_cams) crow[lane] = cd.cam_row[lane];
-        if (lane < 4 * cd.n_intr) {
-            const int t = lane >> 2, k = lane & 3;
-            isc[t][k] = intr[4 * cd.intr_id[t] + k];
-            isc[t][4 + k] = P.scaleF[cd.intr_col[t] + k];
+        if (lane < IW * cd.n_intr) {
+            const int t = lane / IW, k = lane - IW * t;
+            isc[t][k] = intr[IW * cd.intr_id[t] + k];
+            isc[t][IW + k] = P.scaleF[cd.intr_col[t] + k];
         }
         if (lane < cd.n_intr) irow[lane] = cd.intr_row[lane];
     }
@@ -746,7 +750,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
             if (lane < kPK) wcol[lane] = 0.0;   // columns past 3 * npts stay zero
         SFM_STAMP(0)
         // ---- A: observations -> scaled, corrected Jacobians -----------------
-        Lin L;
+        LinT<CM> L;
         const int cs = slot & 255, is = (slot >> 8) & 255;
         if (lane < nobs) linearize<CM, true, true, true>(scp[cs].cp, &isc[is][0], Xp, u0, u1, P.huber_a, L);
         if constexpr (SE) {
@@ -798,12 +802,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
             for (int e = 0; e < 9; ++e) vs[lane][e] = cv[e];
             // J_intr rows are [x s, 0, s, 0] and [0, y s, 0, s]: keep the 4 nonzeros
-            if constexpr (CM == SFM_CAM_SNAVELY) {
-                // both rows of columns 0..2 (f, l1, l2); column 3 is not a parameter
+            if constexpr (CM != SFM_CAM_PINHOLE) {
+                // both rows of the parameter columns (SNAVELY f, l1, l2: column 3
+                // is not a parameter; RADIAL3 f, ppx, ppy, k1, k2, k3)
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    ob[lane][2 * k] = L.Ji[0][k] * isc[is][4 + k];
-                    ob[lane][2 * k + 1] = L.Ji[1][k] * isc[is][4 + k];
+                for (int k = 0; k < NK; ++k) {
+                    ob[lane][2 * k] = L.Ji[0][k] * isc[is][IW + k];
+                    ob[lane][2 * k + 1] = L.Ji[1][k] * isc[is][IW + k];
                 }
             } else {
                 ob[lane][0] = L.Ji[0][0] * isc[is][4];
@@ -893,11 +898,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
         SFM_STAMP(2)
         // ---- C2: intrinsics rows, ordered per point ---------------------------
         // (register sums per run of observations sharing an intrinsics block)
-        if constexpr (CM == SFM_CAM_SNAVELY) {
-            // one lane per (point, axis, intrinsics column k < 3):
+        if constexpr (CM != SFM_CAM_PINHOLE) {
+            // one lane per (point, axis, intrinsics column k < NK):
             // z_k = sum_q Ji[q][0][k] M[q][0][a] + Ji[q][1][k] M[q][1][a]
-            for (int e = lane; e < 9 * npts; e += 64) {
-                const int pt = e / 9, rem = e - 9 * pt, a = rem / 3, k = rem - 3 * a;
+            for (int e = lane; e < 3 * NK * npts; e += 64) {
+                const int pt = e / (3 * NK), rem = e - 3 * NK * pt, a = rem / NK, k = rem - NK * a;
                 const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
                 int row = orow[q0];
                 double z = 0.0;
@@ -1460,10 +1465,10 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                                                          const double* __restrict__ intr_c,
                                                          const double* __restrict__ X,
                                                          double* __restrict__ Xc, double radius) {
-    static_assert(kIW<CM> == 4, "chunk points carry 4-wide intrinsics blocks");
+    constexpr int IW = kIW<CM>;
     __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
     __shared__ double csy[kCamSlots][6];        // camera scaleF * yF (0 for a constant image)
-    __shared__ double isy[kIntrSlots][12];      // intrinsics | candidate | scaleF * yF
+    __shared__ double isy[kIntrSlots][3 * IW];  // intrinsics | candidate | scaleF * yF
     const int c = blockIdx.x, tid = threadIdx.x;
     const double inv_radius = 1.0 / radius;   // as schur_kernel
     const ChunkDesc& cd = P.chunks[c];
@@ -1478,11 +1483,11 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             const int t = e / 6, k = e - 6 * t, col = cd.cam_col[t];
             csy[t][k] = col >= 0 ? P.scaleF[col + k] * P.yF[col + k] : 0.0;
         }
-        if (tid < 4 * cd.n_intr) {
-            const int t = tid >> 2, k = tid & 3, col = cd.intr_col[t];
-            isy[t][k] = intr[4 * cd.intr_id[t] + k];
-            isy[t][4 + k] = intr_c[4 * cd.intr_id[t] + k];
-            isy[t][8 + k] = P.scaleF[col + k] * P.yF[col + k];
+        if (tid < IW * cd.n_intr) {
+            const int t = tid / IW, k = tid - IW * t, col = cd.intr_col[t];
+            isy[t][k] = intr[IW * cd.intr_id[t] + k];
+            isy[t][IW + k] = intr_c[IW * cd.intr_id[t] + k];
+            isy[t][2 * IW + k] = P.scaleF[col + k] * P.yF[col + k];
         }
     }
     __syncthreads();
@@ -1510,7 +1515,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                 nslot = P.obs_slot[o + 1];
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
             }
-            Lin L;
+            LinT<CM> L;
             linearize<CM, true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
             const bool cam = crow_valid(cd, cs);
 #pragma unroll
@@ -1520,7 +1525,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
 #pragma unroll
                     for (int a = 0; a < 6; ++a) q += L.Jc[r][a] * csy[cs][a];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) q += L.Ji[r][a] * isy[is][8 + a];
+                for (int a = 0; a < IW; ++a) q += L.Ji[r][a] * isy[is][2 * IW + a];
                 const double j0 = L.Jx[r][0] * sE[0], j1 = L.Jx[r][1] * sE[1], j2 = L.Jx[r][2] * sE[2];
                 const double fr = L.f[r];
                 V[0] += j0 * j0; V[1] += j1 * j0; V[2] += j1 * j1;
@@ -1574,8 +1579,8 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
                 nslot = P.obs_slot[o + 1];
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
             }
-            Lin C;
-            linearize<CM, false, false, false>(scc[cs], &isy[is][4], xc, uv.x, uv.y, P.huber_a, C);
+            LinT<CM> C;
+            linearize<CM, false, false, false>(scc[cs], &isy[is][IW], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;
             if (!C.ok) cbad = 1.0;
         }
@@ -2084,8 +2089,7 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
 }
 
 // the residual model is a template parameter of every kernel that linearises
-// (chunk kernels: the 4-wide intrinsics models only; the planner sends
-// RADIAL3 points through the general path)
+// (chunk tiles carry the model's intrinsics width: 4, RADIAL3 6)
 #define SFM_BY_MODEL(P, CALL)                                  \
     do {                                                       \
         if ((P).cam_model == SFM_CAM_SNAVELY) {                \
@@ -2164,17 +2168,17 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
     // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
     if (P.tile_nt == 4) {
         if (scale_e)
-            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO, true>),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO, true>),
                                                dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
         else
-            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>),
                                                dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
     } else {
         if (scale_e)
-            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO, true>),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO, true>),
                                                dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
         else
-            SFM_BY_MODEL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO>), dim3(P.n_chunk),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO>), dim3(P.n_chunk),
                                                dim3(64), 0, s, P, cp, intr, X, radius, stamps));
     }
     SFM_HIP(hipGetLastError());
@@ -2245,7 +2249,7 @@ int ba_step_blocks(const DevProblem& P) { return P.n_chunk + (P.n_gpt + kGStepTh
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
     if (P.n_chunk > 0) {
-        SFM_BY_MODEL(P, hipLaunchKernelGGL(step_kernel<CM>, dim3(P.n_chunk), dim3(kChunkPts), 0, s, P, cp, intr,
+        SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(step_kernel<CM>, dim3(P.n_chunk), dim3(kChunkPts), 0, s, P, cp, intr,
                                            cp_cand, intr_cand, X, X_cand, radius));
         SFM_HIP(hipGetLastError());
     }

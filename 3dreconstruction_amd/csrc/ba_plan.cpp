@@ -274,7 +274,7 @@ namespace {
 // intrinsics and repeated (point, image) observations).
 bool chunkable(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t p) {
     const int64_t o0 = P.pt_offsets[p], o1 = P.pt_offsets[p + 1];
-    if (o1 - o0 > kSubObs || pl.iw != 4) return false;   // chunk tiles: 4-wide intrinsics blocks
+    if (o1 - o0 > kSubObs) return false;
     int nc = 0, ni = 0;
     int32_t intrs[kIntrSlots];
     for (int64_t o = o0; o < o1; ++o) {
@@ -290,7 +290,7 @@ bool chunkable(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t p) {
             intrs[ni++] = q;
         }
     }
-    return o1 - o0 <= kCamSlots && 6 * nc + 4 * ni <= kTileRowsUsed;
+    return o1 - o0 <= kCamSlots && 6 * nc + pl.iw * ni <= kTileRowsUsed;
 }
 
 }  // namespace
@@ -336,7 +336,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
     // and a few intrinsics blocks, else dense (blocked Cholesky, ba_dense.hip)
     // (the band solver's arrow holds 4-wide intrinsics blocks: RADIAL3 is dense)
-    pl.dense = !(pl.D <= kBandMaxD && 1 + 4 * pl.nintr <= 32) || pl.iw != 4 || std::getenv("SFM_BA_DENSE") != nullptr;
+    // (the BCR arrow carries iw * nintr <= 16 bordered columns: one MFMA column
+    // tile besides the rhs, and a corner system of at most 16 x 16)
+    pl.dense = !(pl.D <= kBandMaxD && pl.iw * pl.nintr <= 16) || std::getenv("SFM_BA_DENSE") != nullptr;
     if (pl.dense) {
         SFM_REQUIRE(pl.nF <= 40000, SFM_ERR_UNSUPPORTED, "dense reduced camera system of %lld columns",
                     (long long)pl.nF);
@@ -458,11 +460,11 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 const int q = P.img_intr[img];
                 if (!pi.has(q)) pi.push_back(q);
             }
-            const int own = 6 * (int)pc.size() + 4 * (int)pi.size();
+            const int own = 6 * (int)pc.size() + pl.iw * (int)pi.size();
             SFM_REQUIRE(own <= cap, SFM_ERR_INVALID_ARG, "internal: chunk point over %d rows", cap);
             int add = 0, add_slots = 0, add_d = 0, add_i = 0;
             for (int img : pc) if (cam_slot[img] < 0) { add += 6; ++add_slots; }
-            for (int q : pi) if (intr_idx[q] < 0) { add += 4; ++add_slots; ++add_i; }
+            for (int q : pi) if (intr_idx[q] < 0) { add += pl.iw; ++add_slots; ++add_i; }
             for (int img : pd) if (dcam_idx[img] < 0) ++add_d;
             const bool full = k > cd.pt_begin &&
                               (rows + add > cap || k - cd.pt_begin >= chunk_pts ||
@@ -485,9 +487,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                     intrs.push_back(q);
                     intr_idx[q] = t;
                     cd.slot_intr[s] = q; cd.slot_row[s] = rows;
-                    cd.slot_col[s] = (int32_t)(pl.nb + 4 * pl.intr_blk[q]);
+                    cd.slot_col[s] = (int32_t)(pl.nb + (int64_t)pl.iw * pl.intr_blk[q]);
                     cd.intr_id[t] = q; cd.intr_row[t] = rows; cd.intr_col[t] = cd.slot_col[s];
-                    rows += 4;
+                    rows += pl.iw;
                 }
             for (int img : pd)
                 if (dcam_idx[img] < 0) {
@@ -553,7 +555,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                     const int q = P.img_intr[pl.obs_img[s]];
                     if (std::find(pi, pi + ni, q) == pi + ni) pi[ni++] = q;
                 }
-                lo_own = std::max(lo_own, 6 * nc + 4 * ni);
+                lo_own = std::max(lo_own, 6 * nc + pl.iw * ni);
             }
             mo[t] = lo_own;
             mb[t] = lo_obs;
@@ -832,8 +834,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     const int Dp = pl.D + 1;
     if (!pl.dense) {
         pl.n_sband = (int64_t)pl.ncam * Dp * 36;
-        pl.n_sarrow = (int64_t)pl.nintr * pl.ncam * 24;
-        pl.n_scorner = (int64_t)pl.nintr * pl.nintr * 16;
+        pl.n_sarrow = (int64_t)pl.nintr * pl.ncam * 6 * pl.iw;
+        pl.n_scorner = (int64_t)pl.nintr * pl.nintr * pl.iw * pl.iw;
     }
     size_t im = 0, ipm = 0, iv = 0, ipv = 0, ic = 0;
     // every term lands in one target (the corner's transposed copies aside)
@@ -865,11 +867,11 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 tl.push_back({(int64_t)i * nFB + (i - d), {kDstBand, ((int64_t)i * Dp + d) * 36}});
         for (int k = 0; k < pl.nintr; ++k)
             for (int i = 0; i < pl.ncam; ++i)
-                tl.push_back({(int64_t)(pl.ncam + k) * nFB + i, {kDstArrow, ((int64_t)k * pl.ncam + i) * 24}});
+                tl.push_back({(int64_t)(pl.ncam + k) * nFB + i, {kDstArrow, ((int64_t)k * pl.ncam + i) * 6 * pl.iw}});
         for (int k = 0; k < pl.nintr; ++k)
             for (int l = 0; l < pl.nintr; ++l)
                 tl.push_back({(int64_t)(pl.ncam + std::max(k, l)) * nFB + pl.ncam + std::min(k, l),
-                              {kDstCorner, ((int64_t)k * pl.nintr + l) * 16}});
+                              {kDstCorner, ((int64_t)k * pl.nintr + l) * pl.iw * pl.iw}});
         std::stable_sort(tl.begin(), tl.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
         // the corner is stored whole: block (k, l) with k < l is the transpose
         // of (l, k) and is gathered separately with swapped source offsets
@@ -878,20 +880,20 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             const int32_t kind = tl[x].second.first;
             const int64_t dst = tl[x].second.second;
             if (kind == kDstCorner) {
-                const int k = (int)(dst / 16) / pl.nintr, l = (int)(dst / 16) % pl.nintr;
+                const int k = (int)(dst / (pl.iw * pl.iw)) / pl.nintr, l = (int)(dst / (pl.iw * pl.iw)) % pl.nintr;
                 if (k < l) {
                     // transpose of the (l, k) block: same terms, row/column swapped
                     const size_t t0 = pl.terms.size(), p0 = pl.pterms.size();
                     size_t js = 0, jp = 0;
-                    emit(key, kind, dst, 4, 4, 4, mterms, js, &mprod, &jp);
+                    emit(key, kind, dst, pl.iw, pl.iw, pl.iw, mterms, js, &mprod, &jp);
                     for (size_t q = t0; q < pl.terms.size(); ++q) std::swap(pl.terms[q].roff, pl.terms[q].coff);
                     for (size_t q = p0; q < pl.pterms.size(); ++q) std::swap(pl.pterms[q].za, pl.pterms[q].zb);
                     continue;
                 }
-                emit(key, kind, dst, 4, 4, 4, mterms, im, &mprod, &ipm);
+                emit(key, kind, dst, pl.iw, pl.iw, pl.iw, mterms, im, &mprod, &ipm);
                 continue;
             }
-            const int rows = kind == kDstBand ? 6 : 4;
+            const int rows = kind == kDstBand ? 6 : pl.iw;
             emit(key, kind, dst, rows, 6, 6, mterms, im, &mprod, &ipm);
         }
     } else {

@@ -319,7 +319,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->part_f.alloc(3 * (size_t)P.n_fblk);
     P.part_f = pl->part_f.p;
     P.scal = pl->scal.p;
-    pl->use_bcr = !h.dense && bcr_supported(P) && std::getenv("SFM_BA_BAND_SOLVER") == nullptr;
+    // (SFM_BA_BAND_SOLVER: the sequential band solver, 4-wide intrinsics arrows only)
+    pl->use_bcr = !h.dense && bcr_supported(P) && (std::getenv("SFM_BA_BAND_SOLVER") == nullptr || P.iw != 4);
+    SFM_REQUIRE(h.dense || pl->use_bcr || P.iw == 4, SFM_ERR_UNSUPPORTED, "band solver: 4-wide intrinsics only");
     if (h.dense) {
         dense_setup(pl->dense, P);
         pl->dense_buf.alloc(dense_doubles(pl->dense));

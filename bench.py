@@ -543,7 +543,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("SFM_BENCH_LAUNCH_CHECK"):   # CPU test of the self-launch: no GPU work
-        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus}), flush=True)
+        # one write of the whole line (< PIPE_BUF): the ranks share the pipe
+        os.write(1, (json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "gpus": args.gpus})
+                     + "\n").encode())
         return
     if os.environ.get("SFM_BENCH_SAME_DEVICE"):   # rehearsal of N>1 on a one-GPU box
         local_rank = 0

@@ -9,8 +9,11 @@ its published form (parity unpinned beyond the restatement): the oracle's
 analytic Jacobian is checked against dual numbers run through a term-by-term
 restatement of the functor (the Ceres AutoDiff path) and against finite
 differences; noise-free scenes recover the ground truth.
-GPU: the HIP path (general points + dense reduced camera system) against the
-oracle with the same bars as the pinhole model.
+GPU: the HIP path against the oracle with the same bars as the pinhole model:
+banded sequences on the Schur chunk tiles (6-row intrinsics slots, 80-row
+tiles) and block cyclic reduction with a 6-column-per-block arrow; random
+visibility, long tracks or many intrinsics blocks on the general-point path and
+the dense reduced camera system.
 """
 import importlib
 
@@ -94,14 +97,28 @@ def test_radial3_noise_free_recovers_ground_truth():
     np.testing.assert_allclose(i[[0, 3, 4]], sc.gt_intr[[0, 3, 4]], rtol=1e-5, atol=1e-7)
 
 
-def test_radial3_planner_shape():
-    # every point goes through the general path, the RCS is dense, 6 columns
-    # per intrinsics block
-    sc = H.Scene(24, 3000, 6, model=R3, n_intr=2, seed=5)
+def _shape(sc):
     shp = abi.BAPlanShape()
     assert abi.load().sfm_ba_describe(H.C.byref(sc.problem()), 0, 1, H.C.byref(shp)) == 0
-    assert shp.n_chunks == 0 and shp.n_chunk_pts == 0 and shp.n_general_pts == sc.n_pt
-    assert shp.dense == 1 and shp.rcs_dim == 6 * (sc.n_cam - 1) + 6 * 2
+    return shp
+
+
+def test_radial3_planner_shape():
+    # a banded sequence: every point on the chunk tiles (6 rows per camera,
+    # 6 per intrinsics block: 80-row tiles), the band + arrow RCS, 6 columns
+    # per intrinsics block
+    sc = H.Scene(24, 3000, 6, model=R3, n_intr=2, seed=5)
+    shp = _shape(sc)
+    assert shp.n_chunks > 0 and shp.n_chunk_pts == sc.n_pt and shp.n_general_pts == 0
+    assert shp.dense == 0 and shp.rcs_dim == 6 * (sc.n_cam - 1) + 6 * 2
+    # the arrow holds at most 16 bordered columns: three 6-wide blocks are dense
+    sc3 = H.Scene(24, 3000, 6, model=R3, n_intr=3, seed=5)
+    shp3 = _shape(sc3)
+    assert shp3.dense == 1 and shp3.n_chunk_pts == sc3.n_pt
+    # random visibility: general points and a dense RCS, as for pinhole
+    scr = H.Scene(30, 1200, 6, vis_mode=1, model=R3, seed=3)
+    shpr = _shape(scr)
+    assert shpr.dense == 1 and shpr.n_general_pts > 0
 
 
 # ---------------------------------------------------------------------------
@@ -158,7 +175,27 @@ def test_radial3_gpu_shapes(ctx, args):
 @pytest.mark.gpu
 def test_radial3_gpu_c2(ctx):
     sc = H.Scene(200, 50_000, 10, model=R3, seed=0x5F3D0002)
+    assert _shape(sc).dense == 0 and _shape(sc).n_chunk_pts == sc.n_pt   # chunk tiles + BCR
     _compare(ctx, sc)
+
+
+@pytest.mark.gpu
+def test_radial3_band_equals_dense_solver(ctx, monkeypatch):
+    # the chunk + BCR path and the general + dense path solve the same system
+    sc = H.Scene(40, 5000, 8, model=R3, n_intr=2, seed=41)
+    res = []
+    for dense in (False, True):
+        if dense:
+            monkeypatch.setenv("SFM_BA_DENSE", "1")
+        plan = api.BAPlan(ctx, sc.problem(), *sc.params())
+        _, s = plan.run()
+        res.append((s, plan.trace()))
+        plan.close()
+    (s0, t0), (s1, t1) = res
+    assert s0.iterations == s1.iterations
+    assert abs(s0.final_cost / s1.final_cost - 1) < 1e-9
+    for a, b in zip(t0, t1):
+        assert a.step_is_successful == b.step_is_successful
 
 
 def test_radial3_regression_pin_c1():
