@@ -240,15 +240,26 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
 //   D(k+1) wave 0: A_{k+1,k+1} -= L_{k+1,k} L_{k+1,k}', then diag16(k+1);
 //          waves 1..3 meanwhile: the other trailing tiles of step k and the
 //          partial inverse rows T_{k+1,j} = sum_{m=j..k} L_{k+1,m} X_mj
-template <int NW = NT / 64>
+// pre0 / preN: work that must precede the factorisation but only the first
+// diagonal tile has to wait for: wave 0 runs pre0 (the update of A_00) and
+// goes straight on to diag16(0); the other waves run preN (the remaining
+// update tiles and anything else due before the first barrier) meanwhile.
+struct NoPre {
+    __device__ void operator()() const {}
+};
+template <int NW = NT / 64, class Pre0 = NoPre, class PreN = NoPre>
 __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
-                           unsigned long long* st = nullptr) {
+                           unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN()) {
     const int wave = threadIdx.x >> 6;
     unsigned long long t0 = 0, td = 0, ta = 0;
     if (st) t0 = stamp();
     if (wave == 0) {
+        pre0();
+        wave_sync();
         diag16(A, X, bad, col);
         if (st) td += stamp() - t0;
+    } else {
+        preN();
     }
     __syncthreads();
     for (int k = 0;; ++k) {
@@ -434,9 +445,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     constexpr int L16 = 17;
     double* A = sm;                 // [64][LD]
     double* X = A + M * LD;         // [64][LD]
-    double* Wa = X + M * LD;        // [64][64] Wr_{i-sp}
-    double* Wb = Wa + M * M;        // [64][64] Wl_{i+sp}
-    double* Cc = Wb + M * M;        // [64][17] column tile w of C_i
+    double* Wa_l = X + M * LD;      // [64][64] Wr_{i-sp}
+    double* Wb_l = Wa_l + M * M;    // [64][64] Wl_{i+sp}
+    double* Cc = Wb_l + M * M;      // [64][17] column tile w of C_i
     double* Cr = Cc + M * L16;      // [16][LD] row tile w of C_r
     double* Rc = Cr + 16 * LD;      // [64][17] column tile w of R_i
     double* bad = Rc + M * L16;
@@ -449,55 +460,67 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     load_rows<NTL>(Cc, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
     if (hr) load_tile<64, 16, NTL>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
     if (hz) load_rows<NTL>(Rc, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
+    if (sp > 0) {   // the neighbours' full W blocks (the A update's operands)
+        load_tile<64, 64, NTL>(Wa_l, M, b.Wr + (size_t)(i - sp) * M * M, M);
+        if (i + sp < b.N) load_tile<64, 64, NTL>(Wb_l, M, b.Wl + (size_t)(i + sp) * M * M, M);
+    }
+    __syncthreads();
+    if (st) {
+        t1 = stamp();
+        if (threadIdx.x == 0) atomicAdd(st + 5, t1 - t0);   // loads
+    }
     if (sp > 0) {
-        // neighbours eliminated at stride sp: i-sp (always there) and i+sp
+        // neighbours eliminated at stride sp: i-sp (always there) and i+sp.
+        // A_i -= Wa' Wa + Wb' Wb (lower tiles), R_i[:, w] -= Wa' z_{i-sp}[:, w] +
+        // Wb' z_{i+sp}[:, w], C_i[:, w] = -Wa' Wl_{i-sp}[:, w] and C_r's row tile
+        // w = -(Wr_{i+sp}[:, w])' Wl_{i+sp}.  Only tile A_00 is on the path to the
+        // first diagonal factor: wave 0 updates it and factors it while waves
+        // 1..7 do the other 9 tiles and the R / C products (their skinny
+        // operands read straight from global memory: X's LDS is being written).
         const int il = i - sp, ir = i + sp;
         const bool hir = ir < b.N;
-        // column tile w of z_{i-sp}, z_{i+sp}, Wl_{i-sp} and of Wr_{i+sp}, staged in
-        // X's space (free until the factorisation)
-        double* Z1 = X;
-        double* Z2 = Z1 + M * 16;
-        double* WL = Z2 + M * 16;
-        double* WR = WL + M * 16;
-        load_tile<64, 64, NTL>(Wa, M, b.Wr + (size_t)il * M * M, M);
-        load_tile<16, M, NTL>(WL, 16, b.Wl + (size_t)il * M * M + 16 * w, M);
-        if (hz) load_tile<16, M, NTL>(Z1, 16, b.Z + (size_t)il * M * b.nrhs + 16 * w, b.nrhs);
-        if (hir) {
-            load_tile<64, 64, NTL>(Wb, M, b.Wl + (size_t)ir * M * M, M);
-            if (hz) load_tile<16, M, NTL>(Z2, 16, b.Z + (size_t)ir * M * b.nrhs + 16 * w, b.nrhs);
-            if (hr) load_tile<16, M, NTL>(WR, 16, b.Wr + (size_t)ir * M * M + 16 * w, M);
-        }
-        __syncthreads();
-        if (st && threadIdx.x == 0) atomicAdd(st + 5, stamp() - t0);   // loads
-        // A_i -= Wa' Wa + Wb' Wb on the 10 lower tiles (the factorisation reads
-        // nothing above the diagonal): wave v takes tiles v, v+4, v+8
-        for (int q = wave; q < 10; q += NWL) {
+        const double* Z1 = b.Z + (size_t)il * M * b.nrhs + 16 * w;
+        const double* Z2 = b.Z + (size_t)ir * M * b.nrhs + 16 * w;
+        const double* WL = b.Wl + (size_t)il * M * M + 16 * w;
+        const double* WR = b.Wr + (size_t)ir * M * M + 16 * w;
+        double* Wal = Wa_l;
+        double* Wbl = Wb_l;
+        auto a_tile = [&](int q) {
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wa, M, 16 * ti, Wa, M, 16 * tj, 0, M);
-            if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * ti, Wb, M, 16 * tj, 0, M);
+            acc = tile_mm<true, false, true>(acc, Wal, M, 16 * ti, Wal, M, 16 * tj, 0, M);
+            if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * ti, Wbl, M, 16 * tj, 0, M);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
-        }
-        const int v = wave & 3;   // row tile; waves 0..3: R_i and C_i, waves 4..7: C_r
-        if (wave < 4) {
-            // R_i[:, w] -= Wa' z_{i-sp}[:, w] + Wb' z_{i+sp}[:, w]
-            if (hz) {
-                v4d acc = tile_ld(Rc, L16, 16 * v, 0);
-                acc = tile_mm<true, false, true>(acc, Wa, M, 16 * v, Z1, 16, 0, 0, M);
-                if (hir) acc = tile_mm<true, false, true>(acc, Wb, M, 16 * v, Z2, 16, 0, 0, M);
-                tile_st(Rc, L16, 16 * v, 0, acc);
+        };
+        auto pre0 = [&] { a_tile(0); };
+        auto preN = [&] {
+            // 21 items over waves 1..7: A tiles 1..9, R row tiles, C_i row
+            // tiles, C_r column tiles
+            for (int t = wave - 1; t < 21; t += NWL - 1) {
+                if (t < 9) {
+                    a_tile(t + 1);
+                } else if (t < 13) {
+                    const int v = t - 9;
+                    if (hz) {
+                        v4d acc = tile_ld(Rc, L16, 16 * v, 0);
+                        acc = tile_mm<true, false, true>(acc, Wal, M, 16 * v, Z1, b.nrhs, 0, 0, M);
+                        if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * v, Z2, b.nrhs, 0, 0, M);
+                        tile_st(Rc, L16, 16 * v, 0, acc);
+                    }
+                } else if (t < 17) {
+                    const int v = t - 13;   // block (i, i-2sp) = (i, i-s)
+                    tile_st(Cc, L16, 16 * v, 0, tile_mm<true, false, true>(zero4(), Wal, M, 16 * v, WL, M, 0, 0, M));
+                } else if (hr && hir) {
+                    const int v = t - 17;   // block (r, r-s) = (r, i)
+                    tile_st(Cr, LD, 0, 16 * v, tile_mm<true, false, true>(zero4(), WR, M, 0, Wbl, M, 16 * v, 0, M));
+                }
             }
-            // C_i[:, w] = -Wa' Wl_{i-sp}[:, w]   (block (i, i-2sp) = (i, i-s))
-            tile_st(Cc, L16, 16 * v, 0, tile_mm<true, false, true>(zero4(), Wa, M, 16 * v, WL, 16, 0, 0, M));
-        } else if (hr && hir) {
-            // C_r[w rows, :] = -(Wr_{i+sp}[:, w])' Wl_{i+sp}   (block (r, r-s) = (r, i))
-            tile_st(Cr, LD, 0, 16 * v, tile_mm<true, false, true>(zero4(), WR, 16, 0, Wb, M, 16 * v, 0, M));
-        }
+        };
+        chol_inv64<NWL>(A, X, bad, col, st, pre0, preN);
+    } else {
+        chol_inv64<NWL>(A, X, bad, col, st);
     }
-    __syncthreads();
-    if (st) t1 = stamp();
-    chol_inv64<NWL>(A, X, bad, col, st);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     {   // X for the back substitution: each of the block's 4 workgroups stores 16 rows
         double* Xg = b.L + (size_t)i * M * M + 16 * w * M;
@@ -562,25 +585,34 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
     for (int e = threadIdx.x; e < M * LD; e += NTL) X[e] = 0.0;
     __syncthreads();
     if (upd) {
-        // 8 waves: the 10 lower A tiles, and the R rows on waves 4..7
-        for (int q = wave; q < 10; q += NWL) {
+        // A_0 -= Wb' Wb (lower tiles) and R_0 -= Wb' z_sp: wave 0 updates A_00 and
+        // goes on to its diagonal factor, waves 1..7 do the other 9 tiles and
+        // the R row tiles meanwhile (as bcr_level_kernel)
+        auto a_tile = [&](int q) {
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
             acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, M);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
-        }
-        if (wave >= 4) {
-            const int v = wave - 4;
-            for (int tj = 0; tj < b.nrhs / 16; ++tj) {
-                v4d acc = tile_ld(R, ldr, 16 * v, 16 * tj);
-                acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, M);
-                tile_st(R, ldr, 16 * v, 16 * tj, acc);
+        };
+        const int nrt = b.nrhs / 16;
+        auto pre0 = [&] { a_tile(0); };
+        auto preN = [&] {
+            for (int t = wave - 1; t < 9 + 4 * nrt; t += NWL - 1) {
+                if (t < 9) {
+                    a_tile(t + 1);
+                } else {
+                    const int v = (t - 9) / nrt, tj = (t - 9) % nrt;
+                    v4d acc = tile_ld(R, ldr, 16 * v, 16 * tj);
+                    acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, M);
+                    tile_st(R, ldr, 16 * v, 16 * tj, acc);
+                }
             }
-        }
-        __syncthreads();
+        };
+        chol_inv64<NWL>(A, X, bad, sc, nullptr, pre0, preN);
+    } else {
+        chol_inv64<NWL>(A, X, bad, sc);
     }
-    chol_inv64<NWL>(A, X, bad, sc);
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     if (wave < 4)
         for (int tj = 0; tj < b.nrhs / 16; ++tj)
