@@ -244,12 +244,18 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
 // diagonal tile has to wait for: wave 0 runs pre0 (the update of A_00) and
 // goes straight on to diag16(0); the other waves run preN (the remaining
 // update tiles and anything else due before the first barrier) meanwhile.
+// bg(k): background work of the helper waves in the window of diag16(k+1)
+// (k = 0..2), after their trailing tiles (they idle there otherwise).
 struct NoPre {
     __device__ void operator()() const {}
 };
-template <int NW = NT / 64, class Pre0 = NoPre, class PreN = NoPre>
+struct NoBg {
+    __device__ void operator()(int) const {}
+};
+template <int NW = NT / 64, class Pre0 = NoPre, class PreN = NoPre, class Bg = NoBg>
 __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
-                           unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN()) {
+                           unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN(),
+                           Bg bg = Bg()) {
     const int wave = threadIdx.x >> 6;
     unsigned long long t0 = 0, td = 0, ta = 0;
     if (st) t0 = stamp();
@@ -304,6 +310,7 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
                 if (t++ % (NW - 1) == wave - 1)   // X is lower triangular: m runs j..n-1
                     tile_st(X, LD, 16 * n, 16 * j,
                             tile_mm<false, false, false>(zero4(), A, LD, 16 * n, X, LD, 16 * j, 16 * j, 16 * n));
+            bg(k);
         }
         __syncthreads();
     }
@@ -494,30 +501,33 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         };
         auto pre0 = [&] { a_tile(0); };
+        // A tiles 1..9 over waves 1..7 before the first barrier (P(0) and D(1)
+        // read them)
         auto preN = [&] {
-            // 21 items over waves 1..7: A tiles 1..9, R row tiles, C_i row
-            // tiles, C_r column tiles
-            for (int t = wave - 1; t < 21; t += NWL - 1) {
-                if (t < 9) {
-                    a_tile(t + 1);
-                } else if (t < 13) {
-                    const int v = t - 9;
-                    if (hz) {
-                        v4d acc = tile_ld(Rc, L16, 16 * v, 0);
-                        acc = tile_mm<true, false, true>(acc, Wal, M, 16 * v, Z1, b.nrhs, 0, 0, M);
-                        if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * v, Z2, b.nrhs, 0, 0, M);
-                        tile_st(Rc, L16, 16 * v, 0, acc);
-                    }
-                } else if (t < 17) {
-                    const int v = t - 13;   // block (i, i-2sp) = (i, i-s)
-                    tile_st(Cc, L16, 16 * v, 0, tile_mm<true, false, true>(zero4(), Wal, M, 16 * v, WL, M, 0, 0, M));
-                } else if (hr && hir) {
-                    const int v = t - 17;   // block (r, r-s) = (r, i)
-                    tile_st(Cr, LD, 0, 16 * v, tile_mm<true, false, true>(zero4(), WR, M, 0, Wbl, M, 16 * v, 0, M));
+            for (int q = wave; q < 10; q += NWL - 1) a_tile(q);
+        };
+        // the R / C products are read only after the factorisation: one per
+        // helper wave in each of the windows of diag16(1..3), where those
+        // waves idle after their few trailing tiles (12 items, 21 slots)
+        auto bg = [&](int k) {
+            const int t = 7 * k + wave - 1;   // 0..20
+            if (t < 4) {
+                const int v = t;
+                if (hz) {
+                    v4d acc = tile_ld(Rc, L16, 16 * v, 0);
+                    acc = tile_mm<true, false, true>(acc, Wal, M, 16 * v, Z1, b.nrhs, 0, 0, M);
+                    if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * v, Z2, b.nrhs, 0, 0, M);
+                    tile_st(Rc, L16, 16 * v, 0, acc);
                 }
+            } else if (t < 8) {
+                const int v = t - 4;    // block (i, i-2sp) = (i, i-s)
+                tile_st(Cc, L16, 16 * v, 0, tile_mm<true, false, true>(zero4(), Wal, M, 16 * v, WL, M, 0, 0, M));
+            } else if (t < 12 && hr && hir) {
+                const int v = t - 8;    // block (r, r-s) = (r, i)
+                tile_st(Cr, LD, 0, 16 * v, tile_mm<true, false, true>(zero4(), WR, M, 0, Wbl, M, 16 * v, 0, M));
             }
         };
-        chol_inv64<NWL>(A, X, bad, col, st, pre0, preN);
+        chol_inv64<NWL>(A, X, bad, col, st, pre0, preN, bg);
     } else {
         chol_inv64<NWL>(A, X, bad, col, st);
     }
