@@ -212,6 +212,9 @@ __device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], in
 
 __device__ void diag16(double* A, double* X, double* bad, double* col) {
     (void)col;
+    // the critical path of the factorisation: ahead of the co-resident helper
+    // waves (trailing tiles, background products) in VALU issue arbitration
+    __builtin_amdgcn_s_setprio(2);
     const int lane = threadIdx.x & 63, i = lane;
     const bool act = lane < 16;
     double a[16], x[16];
@@ -228,6 +231,7 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
 #pragma unroll
         for (int m = 0; m < 16; ++m) X[m * LD + i] = x[m];
     }
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
