@@ -15,6 +15,7 @@ struct BcrArgs {
     int nrhs = 0;   // 1 + 4*nintr, padded to a multiple of 8
     double *A = nullptr, *C = nullptr, *L = nullptr, *Wl = nullptr, *Wr = nullptr;
     double *R = nullptr, *R0 = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
+    unsigned* yflag = nullptr;   // [N] back substitution: y_i published for epoch (bcr_back_all_kernel)
     unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums
 };
 
@@ -33,6 +34,7 @@ bool bcr_supported(const DevProblem& P);
 void bcr_setup(BcrArgs& b, const DevProblem& P);
 size_t bcr_doubles(const BcrArgs& b);
 void bcr_bind(BcrArgs& b, double* base);
-void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s);
+// epoch: a value the y flags do not hold yet (the plan counts its solves from 1)
+void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch);
 
 }  // namespace sfm

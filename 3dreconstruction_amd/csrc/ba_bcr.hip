@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <utility>
 
 #include "ba_bcr.h"
@@ -675,6 +676,85 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, int s) {
                 tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
 }
 
+// ---- all back-substitution levels in one launch (dataflow) ---------------------
+// Workgroup k takes the k-th odd block in top-down level order.  It stages
+// its own X, Wl, Wr (written by the forward levels, earlier launches) while
+// the blocks it depends on -- i - s and i + s, both odd at a coarser level or
+// block 0 (bcr_top_kernel, an earlier launch) -- finish, then waits for their
+// published y, computes y_i and publishes it: one agent-scope release and a
+// flag word per block, one agent-scope acquire per consumer
+// (cdna_hip_programming.md Guideline 16).  Every workgroup must be resident
+// (one per CU: N - 1 <= the CU count, checked by the caller) and every spin
+// is bounded (a timeout fails the solve, which the LM loop treats as an
+// invalid step).
+__device__ __forceinline__ void bcr_wait_y(const unsigned* flag, unsigned epoch, double* fail) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) {   // ~ seconds: a lost producer, never a normal wait
+                fail[0] = 1.0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void bcr_back_all_kernel(BcrArgs b, int s_top, unsigned epoch) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    int k = blockIdx.x, s = s_top / 2, i = -1;
+    for (; s >= 1; s >>= 1) {
+        const int n_odd = (b.N - s + 2 * s - 1) / (2 * s);
+        if (k < n_odd) {
+            i = s + 2 * s * k;
+            break;
+        }
+        k -= n_odd;
+    }
+    if (i < 0 || i >= b.N) return;
+    const int ldr = b.nrhs + 1;
+    double* X = sm;
+    double* Wl = X + M * LD;
+    double* Wr = Wl + M * LD;
+    double* Yl = Wr + M * LD;
+    double* Yr = Yl + M * ldr;
+    double* T = Yr + M * ldr;
+    const int l = i - s, r = i + s, wave = threadIdx.x >> 6;
+    const bool hr = r < b.N;
+    load_rows(X, LD, b.L + (size_t)i * M * M, M, M);
+    load_rows(Wl, LD, b.Wl + (size_t)i * M * M, M, M);
+    if (hr) load_rows(Wr, LD, b.Wr + (size_t)i * M * M, M, M);
+    if (l > 0) bcr_wait_y(b.yflag + l, epoch, b.fail);
+    if (hr) bcr_wait_y(b.yflag + r, epoch, b.fail);
+    load_rows(Yl, ldr, b.Y + (size_t)l * M * b.nrhs, b.nrhs, b.nrhs);
+    if (hr) load_rows(Yr, ldr, b.Y + (size_t)r * M * b.nrhs, b.nrhs, b.nrhs);
+    __syncthreads();
+    const double* Z = b.Z + (size_t)i * M * b.nrhs;
+    for (int tj = 0; tj < b.nrhs / 16; ++tj) {
+        v4d acc = tile_ld(Z, b.nrhs, 16 * wave, 16 * tj);
+        acc = tile_mm<false, false, true>(acc, Wl, LD, 16 * wave, Yl, ldr, 16 * tj, 0, M);
+        if (hr) acc = tile_mm<false, false, true>(acc, Wr, LD, 16 * wave, Yr, ldr, 16 * tj, 0, M);
+        tile_st(T, ldr, 16 * wave, 16 * tj, acc);
+    }
+    __syncthreads();
+    double* Y = b.Y + (size_t)i * M * b.nrhs;
+    for (int tj = 0; tj < b.nrhs / 16; ++tj)
+        tile_st(Y, b.nrhs, 16 * wave, 16 * tj,
+                tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
+    // publish y_i: every storing wave drains, the workgroup meets, one lane
+    // releases at agent scope and stores the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(b.yflag + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---- bordered arrow: corner system and final y_F --------------------------------
 // M_c = S_corner + D^2 - sum_I B_I' Yb_I ; v = rhs_c - sum_I B_I' y0_I
 // Pass 1: one wave per super-block, its 64 rows as 16 MFMA k-steps.
@@ -791,7 +871,8 @@ void bcr_setup(BcrArgs& b, const DevProblem& P) {
 
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
-    return 5 * mm + 4 * mr + 512 * (size_t)b.N + 8;  // A C L(=X) Wl Wr | R R0 Z Y | part | fail
+    // A C L(=X) Wl Wr | R R0 Z Y | part | fail | y flags (one word per block)
+    return 5 * mm + 4 * mr + 512 * (size_t)b.N + 8 + ((size_t)b.N + 1) / 2 + 2;
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
@@ -799,9 +880,10 @@ void bcr_bind(BcrArgs& b, double* base) {
     b.A = base; b.C = b.A + mm; b.L = b.C + mm; b.Wl = b.L + mm; b.Wr = b.Wl + mm;
     b.R = b.Wr + mm; b.R0 = b.R + mr; b.Z = b.R0 + mr; b.Y = b.Z + mr;
     b.part = b.Y + mr; b.fail = b.part + 512 * (size_t)b.N;
+    b.yflag = reinterpret_cast<unsigned*>(b.fail + 8);   // zeroed by the caller once
 }
 
-void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s) {
+void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
     hipLaunchKernelGGL(bcr_pack_kernel, dim3(16 * b.N), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());
     const size_t ldr = b.nrhs + 1;
@@ -816,6 +898,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_level_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
+        SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_all_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         attr = true;
     }
     int s_top = 1;
@@ -828,11 +911,23 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     }
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NTL), lds_t, s, b, s_top / 2);
     SFM_HIP(hipGetLastError());
-    for (int stride = s_top / 2; stride >= 1; stride /= 2) {
-        if (stride >= b.N) continue;
-        const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-        hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, stride);
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        SFM_HIP(hipGetDevice(&dev));
+        SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (b.N - 1 <= n_cu && b.N > 1 && !std::getenv("SFM_BCR_BACK_LEVELS")) {
+        // one workgroup per odd block, all resident (one per CU at this LDS size)
+        hipLaunchKernelGGL(bcr_back_all_kernel, dim3(b.N - 1), dim3(NT), lds_b, s, b, s_top, epoch);
         SFM_HIP(hipGetLastError());
+    } else {
+        for (int stride = s_top / 2; stride >= 1; stride /= 2) {
+            if (stride >= b.N) continue;
+            const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
+            hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, stride);
+            SFM_HIP(hipGetLastError());
+        }
     }
     hipLaunchKernelGGL(bcr_corner_part_kernel, dim3(b.N), dim3(64), 0, s, b, P.iw * P.nintr);
     SFM_HIP(hipGetLastError());

@@ -70,6 +70,7 @@ struct sfm_ba_plan {
     DBuf<int64_t> src_off;
     DBuf<double> raw_uv, raw_X;
     BcrArgs bcr;
+    unsigned bcr_epoch = 0;   // RCS solves so far (the back-substitution flags' epoch)
     bool use_bcr = false;
     int64_t rcs_n = 0;
     double* scal_h = nullptr;  // pinned, host-mapped: [kScCount] + finalize sequence word
@@ -331,6 +332,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         bcr_setup(pl->bcr, P);
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
         bcr_bind(pl->bcr, pl->bcr_buf.p);
+        SFM_HIP(hipMemsetAsync(pl->bcr.yflag, 0, sizeof(unsigned) * (size_t)pl->bcr.N, s));
         if (std::getenv("SFM_BCR_STAMPS")) {
             pl->bcr_stamps.alloc(7);
             pl->bcr_stamps.zero(s);
@@ -499,7 +501,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         ba_reduce(P, false, s);
         allreduce_rcs();
         if (P.dense) dense_solve(pl->dense, P, radius, s);
-        else if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s);
+        else if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s, ++pl->bcr_epoch);
         else ba_solve(P, radius, s);
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
