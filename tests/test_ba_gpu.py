@@ -238,7 +238,9 @@ def _shard_worker(rank, world, port, out_path, scene_args):
                                         # general points + dense RCS all-reduced
                                         dict(n_cam=30, n_pt=3000, k=6, vis_mode=1, seed=3),
                                         # RADIAL3: 6-wide intrinsics blocks in the exchange
-                                        dict(n_cam=20, n_pt=2000, k=5, n_intr=2, seed=9, model=2)])
+                                        dict(n_cam=20, n_pt=2000, k=5, n_intr=2, seed=9, model=2),
+                                        # C2 (BASELINE configs[1]: 200 cams / 50k pts / 500k obs)
+                                        dict(n_cam=200, n_pt=50000, k=10, seed=0x5F3D0002)])
 def test_sharded_two_ranks_one_gpu(ctx, tmp_path, scene_args):
     import torch.multiprocessing as mp
     out = str(tmp_path / "r.npz")
