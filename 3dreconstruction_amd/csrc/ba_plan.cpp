@@ -10,7 +10,11 @@
 #include "ba_plan.h"
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
+#include <condition_variable>
+#include <exception>
+#include <mutex>
 #include <cstdlib>
 #include <numeric>
 #include <thread>
@@ -21,48 +25,181 @@ namespace sfm {
 
 namespace {
 
+// Host worker pool for the planner: up to 15 threads started once and parked
+// on a condition variable, so a parallel phase costs a wake-up (tens of us)
+// instead of 15 thread creations.  One caller at a time uses the pool; a
+// concurrent caller (another context planning at the same moment) runs its
+// tasks on fresh threads instead.
+class PlanPool {
+   public:
+    static PlanPool& get() {
+        static PlanPool p;
+        return p;
+    }
+    static int width() {
+        // SFM_PLAN_THREADS: override (1 = serial planning, for profiling)
+        static const int w = [] {
+            int64_t n = std::min<int64_t>(16, std::thread::hardware_concurrency());
+            if (const char* e = std::getenv("SFM_PLAN_THREADS")) n = std::min<int64_t>(16, std::atoi(e));
+            return (int)std::max<int64_t>(1, n);
+        }();
+        return w;
+    }
+    // fn(t) for t in [0, n): tasks spread over the workers and the caller; an
+    // exception of any task is rethrown here once every task has finished
+    void run(int n, const std::function<void(int)>& fn) {
+        if (n <= 1) {
+            if (n == 1) fn(0);
+            return;
+        }
+        std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
+        if (!busy.owns_lock() || workers_.empty()) {
+            std::exception_ptr err;
+            std::mutex em;
+            auto call = [&](int t) {
+                try { fn(t); } catch (...) { std::lock_guard<std::mutex> g(em); if (!err) err = std::current_exception(); }
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < n; ++t) th.emplace_back(call, t);
+            call(0);
+            for (auto& x : th) x.join();
+            if (err) std::rethrow_exception(err);
+            return;
+        }
+        uint32_t g;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            g = ++gen_;
+            job_ = &fn;
+            n_tasks_ = n;
+            left_ = n;
+            err_ = nullptr;
+            next_.store((uint64_t)g << 32);
+        }
+        cv_.notify_all();
+        work(g, &fn, n);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return left_ == 0; });
+        job_ = nullptr;
+        if (err_) std::rethrow_exception(err_);
+    }
+
+   private:
+    PlanPool() {
+        for (int t = 1; t < width(); ++t) workers_.emplace_back([this] { loop(); });
+    }
+    ~PlanPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& x : workers_) x.join();
+    }
+    // Tasks are claimed from one word holding (generation << 32 | next task):
+    // a worker that wakes late for a finished run can never claim (or count)
+    // a task of the next one.
+    void work(uint32_t g, const std::function<void(int)>* job, int n) {
+        int done = 0;
+        for (;;) {
+            uint64_t v = next_.load();
+            int t = -1;
+            while ((uint32_t)(v >> 32) == g && (int)(v & 0xffffffffu) < n) {
+                if (next_.compare_exchange_weak(v, v + 1)) {
+                    t = (int)(v & 0xffffffffu);
+                    break;
+                }
+            }
+            if (t < 0) break;
+            try {
+                (*job)(t);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(m_);
+                if (!err_) err_ = std::current_exception();
+            }
+            ++done;
+        }
+        if (done) {
+            std::lock_guard<std::mutex> lk(m_);
+            left_ -= done;
+            if (left_ == 0) done_.notify_all();
+        }
+    }
+    void loop() {
+        uint32_t seen = 0;
+        for (;;) {
+            uint32_t g;
+            const std::function<void(int)>* job;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = g = gen_;
+                job = job_;
+                n = n_tasks_;
+            }
+            work(g, job, n);
+        }
+    }
+    std::mutex use_, m_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)>* job_ = nullptr;
+    std::atomic<uint64_t> next_{0};
+    std::exception_ptr err_;
+    int n_tasks_ = 0, left_ = 0;
+    uint32_t gen_ = 0;
+    bool stop_ = false;
+};
+
 // Split [0, n) into contiguous ranges over up to 16 host threads (results are
 // independent of the split: every range writes its own outputs).
 template <class F>
 void parallel_ranges(int64_t n, F&& fn) {
-    const int64_t hw = std::max<int64_t>(1, std::min<int64_t>(16, std::thread::hardware_concurrency()));
-    const int64_t nt = n < 65536 ? 1 : hw;
+    const int64_t nt = n < 4096 ? 1 : std::min<int64_t>(PlanPool::width(), n / 2048);
     if (nt <= 1) {
         fn(0, n, 0);
         return;
     }
-    std::vector<std::thread> th;
-    for (int64_t t = 1; t < nt; ++t) th.emplace_back([&, t] { fn(n * t / nt, n * (t + 1) / nt, (int)t); });
-    fn(0, n / nt, 0);
-    for (auto& x : th) x.join();
+    PlanPool::get().run((int)nt, [&](int t) { fn(n * t / nt, n * (t + 1) / nt, t); });
 }
 
-// fn(g) for g in [0, nseg) on nseg host threads (each g writes its own outputs)
+// fn(g) for g in [0, nseg) on the host threads (each g writes its own outputs)
 template <class F>
 void parallel_segments(int nseg, F&& fn) {
-    std::vector<std::thread> th;
-    for (int g = 1; g < nseg; ++g) th.emplace_back([&, g] { fn(g); });
-    if (nseg > 0) fn(0);
-    for (auto& x : th) x.join();
+    PlanPool::get().run(nseg, [&](int g) { fn(g); });
 }
 
-// block half-bandwidth of the points' camera spans under the order cam_blk
-int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk) {
-    int32_t Dt[16] = {0};
+// block half-bandwidth of the points' camera spans under the order cam_blk;
+// *lb_out (optional): a bound no camera order can beat, the largest number of
+// distinct active cameras one point sees, minus one
+int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int32_t* lb_out = nullptr) {
+    int32_t Dt[16] = {0}, Lt[16] = {0};
     parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int t) {
-        int32_t D = 0;
+        int32_t D = 0, L = 0;
+        std::vector<int32_t> cs;
         for (int64_t p = p0; p < p1; ++p) {
-            int lo = INT_MAX, hi = -1;
+            int lo = INT_MAX, hi = -1, n = 0;
             for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
                 const int b = cam_blk[P.obs_img[o]];
-                if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); }
+                if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); ++n; }
             }
             if (hi >= 0) D = std::max(D, hi - lo);
+            if (lb_out && n - 1 > L) {   // only a track longer than the bound so far is counted exactly
+                cs.clear();
+                for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o)
+                    if (cam_blk[P.obs_img[o]] >= 0) cs.push_back(cam_blk[P.obs_img[o]]);
+                std::sort(cs.begin(), cs.end());
+                L = std::max(L, (int32_t)(std::unique(cs.begin(), cs.end()) - cs.begin()) - 1);
+            }
         }
         Dt[t] = D;
+        Lt[t] = L;
     });
-    int32_t D = 0;
-    for (int32_t d : Dt) D = std::max(D, d);
+    int32_t D = 0, L = 0;
+    for (int t = 0; t < 16; ++t) { D = std::max(D, Dt[t]); L = std::max(L, Lt[t]); }
+    if (lb_out) *lb_out = L;
     return D;
 }
 
@@ -173,11 +310,15 @@ std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, i
     for (int i = 0; i < P.n_img; ++i)
         if (used[i] && i != P.const_img) cam_blk[i] = ncam++;
     tm.mark("used");
-    int32_t D = half_bandwidth(P, cam_blk);
+    int32_t lb = 0;
+    int32_t D = half_bandwidth(P, cam_blk, &lb);
     // reorder only when the image order does not give a band the BCR solver
-    // takes, and the co-visibility graph is small enough to build quickly
+    // takes, no order can (a point seeing more than kBandMaxD + 1 cameras
+    // keeps the RCS dense under any order), and the co-visibility graph is
+    // small enough to build quickly
     tm.mark("bandwidth");
-    if (D > kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20 && !std::getenv("SFM_BA_NO_RCM")) {
+    if (D > kBandMaxD && lb <= kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20 &&
+        !std::getenv("SFM_BA_NO_RCM")) {
         const std::vector<int32_t> pos = rcm_order(P, cam_blk, ncam);
         tm.mark("rcm");
         std::vector<int32_t> alt(cam_blk);
@@ -510,12 +651,12 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         if (k_end > k_begin) close(k_end);
         return flops;
     };
-    // Large shards are chunked in 16 fixed point ranges on host threads (a
-    // chunk never spans two ranges: at most 15 extra chunks out of thousands;
-    // the split depends on the shard only, never on the host)
+    // Shards are chunked in up to 16 fixed point ranges of >= 4096 points on
+    // host threads (a chunk never spans two ranges: at most 15 extra chunks
+    // out of thousands; the split depends on the shard only, never on the host)
     auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, HostVec<int32_t>& slot_out) -> int64_t {
         slot_out.resize(pl.pt_off[ncp]);   // every entry written by its range
-        const int nseg = ncp >= 65536 ? 16 : 1;
+        const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(16, ncp / 4096));
         std::vector<std::vector<ChunkDesc>> seg_chunks(nseg);
         std::vector<int64_t> seg_flops(nseg, 0);
         std::vector<int> seg_rc(nseg, SFM_OK);
@@ -526,10 +667,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 return SFM_OK;
             });
         };
-        std::vector<std::thread> th;
-        for (int g = 1; g < nseg; ++g) th.emplace_back(run, g);
-        run(0);
-        for (auto& t : th) t.join();
+        parallel_segments(nseg, run);
         int64_t flops = 0;
         chunks_out.clear();
         for (int g = 0; g < nseg; ++g) {
@@ -754,7 +892,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // chunk tiles: fixed chunk ranges on host threads, appended in chunk order
     {
         const int32_t nch = (int32_t)pl.chunks.size();
-        const int nseg = nch >= 2048 ? 16 : 1;
+        const int nseg = nch >= 128 ? 16 : 1;   // the output is the same for any split
         std::vector<std::vector<std::pair<int64_t, ReduceTerm>>> sm(nseg), sv(nseg);
         parallel_segments(nseg, [&](int g) {
             const int32_t c0 = (int32_t)((int64_t)nch * g / nseg), c1 = (int32_t)((int64_t)nch * (g + 1) / nseg);
@@ -824,11 +962,15 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         if (src != v.data()) v.swap(tmp);
     };
     tm.mark("terms");
-    sort_terms(mterms);
-    sort_terms(vterms);
-    sort_terms(cterms);
-    sort_terms(mprod);
-    sort_terms(vprod);
+    parallel_segments(5, [&](int g) {   // five independent lists
+        switch (g) {
+            case 0: sort_terms(mprod); break;
+            case 1: sort_terms(mterms); break;
+            case 2: sort_terms(vterms); break;
+            case 3: sort_terms(cterms); break;
+            default: sort_terms(vprod); break;
+        }
+    });
 
     tm.mark("term_sort");
     const int Dp = pl.D + 1;

@@ -4,6 +4,8 @@
 // (sfm_ba_solve), one fresh adjuster per bundleAdjustment() call as
 // src/actuator/SequentialActuator.h:226-229 makes it.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -29,10 +31,31 @@ struct CtxMatcher {
     }
 };
 
+// SFM_SEQ_DUMP=<dir> (diagnostic): every 100th solve's problem is written to
+// <dir>/ba_<call>.bin (int64 n_img n_intr n_pt n_obs const_img, then
+// pt_offsets, obs_img, obs_uv, img_intr) for replaying the planner offline
+void dump_problem(const sfm_ba_problem& pr) {
+    static const char* dir = std::getenv("SFM_SEQ_DUMP");
+    static int call = 0;
+    if (!dir || call++ % 100 != 99) return;
+    char path[512];
+    std::snprintf(path, sizeof path, "%s/ba_%03d.bin", dir, call - 1);
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return;
+    const int64_t h[5] = {pr.n_img, pr.n_intr, pr.n_pt, pr.n_obs, pr.const_img};
+    std::fwrite(h, sizeof h, 1, f);
+    std::fwrite(pr.pt_offsets, sizeof(int64_t), (size_t)pr.n_pt + 1, f);
+    std::fwrite(pr.obs_img, sizeof(int32_t), (size_t)pr.n_obs, f);
+    std::fwrite(pr.obs_uv, sizeof(double), 2 * (size_t)pr.n_obs, f);
+    std::fwrite(pr.img_intr, sizeof(int32_t), (size_t)pr.n_img, f);
+    std::fclose(f);
+}
+
 struct CtxSolver {
     sfm_ctx* ctx;
     int solve(const sfm_ba_problem& pr, double* extr, double* intr, double* X, const sfm_ba_options& o,
               sfm_ba_summary& s) const {
+        dump_problem(pr);
         return sfm_ba_solve(ctx, &pr, extr, intr, X, &o, &s);
     }
     const char* last_error() const { return sfm_last_error(); }
@@ -124,7 +147,9 @@ extern "C" int sfm_seq_add_image(sfm_seq* s, const sfm_seq_image* im, int32_t* k
 extern "C" int sfm_seq_bundle_adjust(sfm_seq* s, sfm_ba_summary* summary) {
     return sfm::guarded([&] {
         SFM_REQUIRE(s && s->initialised, SFM_ERR_INVALID_ARG, "sfm_seq_bundle_adjust: call sfm_seq_init first");
+        sfm::PhaseTimer tm("sfm_seq_bundle_adjust");
         s->act->bundleAdjustment();
+        tm.mark("total");
         const auto& st = s->act->lastStep();
         if (summary) *summary = st.ba;
         // "solution not usable" is the reference's printed-and-continue outcome

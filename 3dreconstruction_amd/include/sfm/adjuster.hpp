@@ -12,7 +12,9 @@
 #pragma once
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -58,9 +60,21 @@ class BasicBundleAdjuster {
     explicit BasicBundleAdjuster(Solver solver, Options opt = Options()) : solver_(std::move(solver)), opt_(opt) {}
 
     void operator()(WorldStructure::Ptr& world) {  // :176-186
+        // SFM_TIMING=1 (diagnostic): the adjuster's own phases on stderr
+        static const bool timing = std::getenv("SFM_TIMING") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         load(world);
-        if (solve()) update();
+        const auto t1 = std::chrono::steady_clock::now();
+        const bool ok = solve();
+        const auto t2 = std::chrono::steady_clock::now();
+        if (ok) update();
+        const auto t3 = std::chrono::steady_clock::now();
         clear();
+        if (timing) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::fprintf(stderr, "[timing] adjuster: load %.2f ms, solve %.2f ms, update %.2f ms, clear %.2f ms\n",
+                         ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, std::chrono::steady_clock::now()));
+        }
     }
     const sfm_ba_summary& summary() const { return summary_; }
     int lastError() const { return last_rc_; }   // SFM_OK or the last solve code
@@ -106,12 +120,28 @@ class BasicBundleAdjuster {
         }
         const_img_ = world->local_frames_.empty() ? -1 : 0;
         // points in index order (the reference iterates its unordered_map)
+        // The walk over the world is a pointer chase (every point and its
+        // observation list are separate heap blocks): both are prefetched a
+        // few points ahead, and the adjuster keeps plain pointers (the world
+        // owns the points for the whole call), so no reference counts move.
         const std::vector<WorldPoint::Ptr>& pts = world->pointsByIdx();
+        const std::size_t np = pts.size();
         points_.clear(); X_.clear(); off_.assign(1, 0); obs_img_.clear(); uv_.clear();
-        points_.reserve(pts.size());
-        X_.reserve(3 * pts.size());
-        off_.reserve(pts.size() + 1);
-        for (const auto& p : pts) {
+        points_.reserve(np);
+        X_.reserve(3 * np);
+        off_.reserve(np + 1);
+        obs_img_.reserve(8 * np);
+        uv_.reserve(16 * np);
+        constexpr std::size_t kAhead = 8;
+        for (std::size_t k = 0; k < np; ++k) {
+            if (k + 2 * kAhead < np) __builtin_prefetch(pts[k + 2 * kAhead].get());
+            if (k + kAhead < np) {
+                const auto& of = pts[k + kAhead]->observed_frames_;
+                __builtin_prefetch(of.data());
+                __builtin_prefetch(reinterpret_cast<const char*>(of.data()) + 64);
+                __builtin_prefetch(reinterpret_cast<const char*>(of.data()) + 128);
+            }
+            WorldPoint* p = pts[k].get();
             points_.push_back(p);
             X_.insert(X_.end(), p->world_pos_.begin(), p->world_pos_.end());
             for (auto& [im, uv] : p->observed_frames_) {
@@ -160,7 +190,10 @@ class BasicBundleAdjuster {
         return true;
     }
     void update() {  // updateWorld (:143-156)
-        for (std::size_t k = 0; k < points_.size(); ++k) points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
+        for (std::size_t k = 0; k < points_.size(); ++k) {
+            if (k + 8 < points_.size()) __builtin_prefetch(points_[k + 8], 1);
+            points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
+        }
         for (std::size_t k = 0; k < images_.size(); ++k) {
             std::array<double, 6> p;
             for (int a = 0; a < 6; ++a) p[a] = extr_[6 * k + a];
@@ -178,7 +211,7 @@ class BasicBundleAdjuster {
     Options opt_;
     std::vector<Image::Ptr> images_;
     std::vector<Camera::Ptr> cams_;
-    std::vector<WorldPoint::Ptr> points_;
+    std::vector<WorldPoint*> points_;   // owned by the world during the call
     std::vector<int> img_slot_;   // Image::getIdx() -> problem image index or -1
     std::unordered_map<const Camera*, int> cam_index_;
     std::vector<int32_t> img_cam_, obs_img_;

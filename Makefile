@@ -10,7 +10,7 @@ SRCS := $(wildcard $(CSRC)/*.cpp $(CSRC)/*.hip)
 OBJS := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) include/sfmcore.h $(wildcard $(PKG)/include/sfm/*.hpp)
 
-all: $(LIB) oracle/liboracle.so tests/cpp/facade_test
+all: $(LIB) oracle/liboracle.so tests/cpp/facade_test tests/cpp/plan_pool_test
 
 build/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
@@ -39,3 +39,8 @@ clean:
 tests/cpp/facade_test: tests/cpp/facade_test.cpp 3dreconstruction_amd/include/sfm/sfm.hpp 3dreconstruction_amd/include/sfm/world.hpp $(LIB) oracle/liboracle.so
 	g++ -O2 -std=c++17 -Wall -o $@ $< -I/opt/rocm/include -L3dreconstruction_amd/lib -Loracle -lsfmcore -loracle \
 	    -Wl,-rpath,'$$ORIGIN/../../3dreconstruction_amd/lib' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# planner worker-pool stress test (host only, no GPU)
+tests/cpp/plan_pool_test: tests/cpp/plan_pool_test.cpp $(CSRC)/ba_plan.cpp $(HDRS)
+	g++ -O2 -std=c++17 -w -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $@ $< -L/opt/rocm/lib -lamdhip64 -lpthread \
+	    -Wl,-rpath,/opt/rocm/lib
