@@ -24,11 +24,13 @@ struct DenseArgs {
     int nt = 0;          // tiles per side
     int64_t np = 0;      // padded order nt * 64
     double *A = nullptr, *X = nullptr, *b = nullptr, *y = nullptr, *x = nullptr, *fail = nullptr;
+    unsigned* xflag = nullptr;   // [nt] back substitution: x_k published for epoch (dense_back_all_kernel)
 };
 void dense_setup(DenseArgs& d, const DevProblem& P);
 size_t dense_doubles(const DenseArgs& d);
 void dense_bind(DenseArgs& d, double* base);
-void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s);
+// epoch: a value the x flags do not hold yet (the plan counts its solves from 1)
+void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch);
 
 bool bcr_supported(const DevProblem& P);
 void bcr_setup(BcrArgs& b, const DevProblem& P);

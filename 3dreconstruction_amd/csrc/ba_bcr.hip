@@ -1137,6 +1137,82 @@ __global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem 
     if (threadIdx.x < M) d.y[(int64_t)i * kDM + c] -= ((part[0][c] + part[1][c]) + part[2][c]) + part[3][c];
 }
 
+// back substitution, every block column in one launch (dataflow): workgroup
+// w takes block k = nt - 1 - w, accumulates y_k - sum_{j>k} L_jk' x_j as the
+// x_j are published (j descending, the L_jk loads issued before each wait),
+// then x_k = X_kk' (...) and publishes x_k.  The hand-off follows the
+// write-through form of cdna_hip_programming.md Guideline 16 (MI355X_MICROARCH
+// § visibility, first table row): x is stored with agent-scope (sc1) stores,
+// every storing wave drains, the workgroup meets, one lane stores the flag;
+// the consumer polls the flag with an sc1 load and reads x only with sc1
+// loads after a workgroup barrier, one workgroup per CU (the dynamic LDS
+// below is sized for that).  Every workgroup must be resident (nt <= the CU
+// count, checked by the caller) and every spin is bounded (a timeout marks the
+// solve failed, which the LM loop treats as an invalid step).
+__device__ __forceinline__ void dense_wait_x(const unsigned* flag, unsigned epoch, double* fail) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) {
+                __hip_atomic_store(fail, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProblem P, unsigned epoch) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Xs = sm;                 // [64][M + 1]
+    double* v = Xs + M * (M + 1);    // [64]
+    double (*part)[M] = reinterpret_cast<double (*)[M]>(v + M);   // [4][64]
+    const int k = d.nt - 1 - (int)blockIdx.x;
+    const int64_t np = d.np;
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    {   // X_kk (an earlier launch wrote it: plain loads)
+        const double* X = d.X + (int64_t)k * kDM * kDM;
+        double xv[M / 4];
+#pragma unroll
+        for (int q = 0; q < M / 4; ++q) xv[q] = X[(4 * q + g) * M + c];
+#pragma unroll
+        for (int q = 0; q < M / 4; ++q) Xs[(4 * q + g) * (M + 1) + c] = xv[q];
+    }
+    // thread (g, c): column c of L_jk', rows 4q + g
+    double acc = 0.0;
+    for (int j = d.nt - 1; j > k; --j) {
+        const double* L = d.A + (int64_t)j * kDM * np + (int64_t)k * kDM + c;
+        double lv[M / 4];
+#pragma unroll
+        for (int q = 0; q < M / 4; ++q) lv[q] = L[(int64_t)(4 * q + g) * np];
+        dense_wait_x(d.xflag + j, epoch, d.fail);
+        const double* xj = d.x + (int64_t)j * kDM;
+#pragma unroll
+        for (int q = 0; q < M / 4; ++q)
+            acc = fma(lv[q], __hip_atomic_load(xj + 4 * q + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), acc);
+    }
+    part[g][c] = acc;
+    __syncthreads();
+    if (threadIdx.x < M)
+        v[c] = d.y[(int64_t)k * kDM + c] - (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+    __syncthreads();
+    if (threadIdx.x < M) {   // x_k = X_kk' v: X lower, so rows m >= c
+        double x = 0.0;
+        for (int m = c; m < M; ++m) x = fma(Xs[m * (M + 1) + c], v[m], x);
+        __hip_atomic_store(d.x + (int64_t)k * kDM + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t e = (int64_t)k * kDM + c;
+        if (e < P.nF) P.yF[e] = x;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(d.xflag + k, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // block 0 finishes last (it waits for every other x): the solve's verdict
+        if (k == 0) P.scal[kScSolveFail] = __hip_atomic_load(d.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace
 
 void dense_setup(DenseArgs& d, const DevProblem& P) {
@@ -1145,7 +1221,8 @@ void dense_setup(DenseArgs& d, const DevProblem& P) {
 }
 
 size_t dense_doubles(const DenseArgs& d) {
-    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8;
+    // A | X | b y x | fail (8) | x flags (one word per block column)
+    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8 + ((size_t)d.nt + 1) / 2 + 2;
 }
 
 void dense_bind(DenseArgs& d, double* base) {
@@ -1155,9 +1232,10 @@ void dense_bind(DenseArgs& d, double* base) {
     d.y = d.b + d.np;
     d.x = d.y + d.np;
     d.fail = d.x + d.np;
+    d.xflag = reinterpret_cast<unsigned*>(d.fail + 8);   // zeroed by the caller once
 }
 
-void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s) {
+void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
     const int64_t n2 = d.np * d.np;
     hipLaunchKernelGGL(dense_pack_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d, P, radius);
     SFM_HIP(hipGetLastError());
@@ -1195,6 +1273,26 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
                                k + w - 1);
             SFM_HIP(hipGetLastError());
         }
+    }
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        SFM_HIP(hipGetDevice(&dev));
+        SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    if (d.nt <= n_cu && !std::getenv("SFM_DENSE_BACK_LAUNCHES")) {
+        // one workgroup per block column, all resident: more than half a CU's
+        // LDS each, so one per CU
+        constexpr size_t lds_all = 81 * 1024;
+        static bool attr_b = false;
+        if (!attr_b) {
+            SFM_HIP(hipFuncSetAttribute((const void*)dense_back_all_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_all));
+            attr_b = true;
+        }
+        hipLaunchKernelGGL(dense_back_all_kernel, dim3(d.nt), dim3(NT), lds_all, s, d, P, epoch);
+        SFM_HIP(hipGetLastError());
+        return;
     }
     for (int k = d.nt - 1; k >= 0; --k) {
         hipLaunchKernelGGL(dense_back_kernel, dim3(k > 0 ? k : 1), dim3(NT), 0, s, d, P, k);

@@ -762,9 +762,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     pl.gblk_col.clear();
     pl.gblk_z.clear();
     {
-        std::vector<int32_t> cols;
-        for (int64_t g = 0; g < pl.n_gpt; ++g) {
-            const int64_t k = pl.n_cpt + g;
+        // two passes on the host threads: block counts and Z sizes per point,
+        // then (after the prefix sums) every point writes its own blocks
+        auto point_cols = [&](int64_t k, std::vector<int32_t>& cols) {
             cols.clear();
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
                 const int img = pl.obs_img[s];
@@ -773,29 +773,59 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             }
             std::sort(cols.begin(), cols.end());
             cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
-            SFM_REQUIRE(cols.size() < 0xffff, SFM_ERR_UNSUPPORTED, "point with %zu parameter blocks", cols.size());
+        };
+        auto zrows = [&](const std::vector<int32_t>& cols) {
             int32_t z = 0;
-            for (int32_t c : cols) {
-                pl.gblk_col.push_back(c);
-                pl.gblk_z.push_back(z);
-                z += 3 * (c < pl.nb ? 6 : pl.iw);
+            for (int32_t c : cols) z += 3 * (c < pl.nb ? 6 : pl.iw);
+            return z;
+        };
+        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+            std::vector<int32_t> cols;
+            for (int64_t g = g0; g < g1; ++g) {
+                const int64_t k = pl.n_cpt + g;
+                point_cols(k, cols);
+                SFM_REQUIRE(cols.size() < 0xffff, SFM_ERR_UNSUPPORTED, "point with %zu parameter blocks", cols.size());
+                const int32_t z = zrows(cols);
+                SFM_REQUIRE(z + 3 <= kZMaxDoubles, SFM_ERR_UNSUPPORTED,
+                            "point %lld observed by %zu parameter blocks (more than the %d rows one wavefront eliminates)",
+                            (long long)pl.spt_global[k], cols.size(), kZMaxDoubles / 3);
+                pl.gblk_off[g + 1] = (int32_t)cols.size();
+                pl.gz_off[g + 1] = z + 3;   // + w = L^-1 g_E
             }
-            pl.gblk_off[g + 1] = (int32_t)pl.gblk_col.size();
-            pl.gz_off[g + 1] = pl.gz_off[g] + z + 3;   // + w = L^-1 g_E
-            pl.gz_max = std::max<int64_t>(pl.gz_max, z + 3);
-            SFM_REQUIRE(z + 3 <= kZMaxDoubles, SFM_ERR_UNSUPPORTED,
-                        "point %lld observed by %zu parameter blocks (more than the %d rows one wavefront eliminates)",
-                        (long long)pl.spt_global[k], cols.size(), kZMaxDoubles / 3);
-            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
-                const int img = pl.obs_img[s];
-                const int32_t cb = pl.img_colc[img] >= 0
-                                       ? (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_colc[img]) - cols.begin())
-                                       : 0xffff;
-                const int32_t ib = (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_coli[img]) - cols.begin());
-                pl.obs_slot[s] = cb | (ib << 16);
-            }
-            flops += point_flops(z / 3, pl.pt_off[k + 1] - pl.pt_off[k]);
+        });
+        for (int64_t g = 0; g < pl.n_gpt; ++g) {
+            pl.gz_max = std::max<int64_t>(pl.gz_max, pl.gz_off[g + 1]);
+            pl.gblk_off[g + 1] += pl.gblk_off[g];
+            pl.gz_off[g + 1] += pl.gz_off[g];
         }
+        pl.gblk_col.resize(pl.gblk_off[pl.n_gpt]);
+        pl.gblk_z.resize(pl.gblk_off[pl.n_gpt]);
+        int64_t gfl[16] = {0};
+        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int t) {
+            std::vector<int32_t> cols;
+            int64_t fl = 0;
+            for (int64_t g = g0; g < g1; ++g) {
+                const int64_t k = pl.n_cpt + g;
+                point_cols(k, cols);
+                int32_t z = 0, q = pl.gblk_off[g];
+                for (int32_t c : cols) {
+                    pl.gblk_col[q] = c;
+                    pl.gblk_z[q++] = z;
+                    z += 3 * (c < pl.nb ? 6 : pl.iw);
+                }
+                for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                    const int img = pl.obs_img[s];
+                    const int32_t cb = pl.img_colc[img] >= 0
+                                           ? (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_colc[img]) - cols.begin())
+                                           : 0xffff;
+                    const int32_t ib = (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_coli[img]) - cols.begin());
+                    pl.obs_slot[s] = cb | (ib << 16);
+                }
+                fl += point_flops(z / 3, pl.pt_off[k + 1] - pl.pt_off[k]);
+            }
+            gfl[t] = fl;
+        });
+        for (int64_t f : gfl) flops += f;
         pl.n_z = pl.gz_off[pl.n_gpt];
     }
     tm.mark("general");
@@ -921,19 +951,36 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
     }
     tm.mark("terms_tiles");
-    // general points
-    for (int64_t g = 0; g < pl.n_gpt; ++g) {
-        const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
-        const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
-        for (int32_t a = k0; a < k1; ++a) {
-            const int32_t fa = fb_of_col(pl.gblk_col[a]);
-            vprod.push_back({fa, PTerm{zb + pl.gblk_z[a], wz}});
-            for (int32_t b = k0; b <= a; ++b)
-                mprod.push_back({(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}});
+    // general points: point g's product terms go to fixed offsets (the
+    // triangle of its blocks), written on the host threads
+    {
+        std::vector<int64_t> mo(pl.n_gpt + 1, 0);
+        for (int64_t g = 0; g < pl.n_gpt; ++g) {
+            const int64_t b = pl.gblk_off[g + 1] - pl.gblk_off[g];
+            mo[g + 1] = mo[g] + b * (b + 1) / 2;
         }
+        mprod.resize(mo[pl.n_gpt]);
+        vprod.resize(pl.gblk_off[pl.n_gpt]);
+        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+            for (int64_t g = g0; g < g1; ++g) {
+                const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
+                const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
+                int64_t m = mo[g];
+                for (int32_t a = k0; a < k1; ++a) {
+                    const int32_t fa = fb_of_col(pl.gblk_col[a]);
+                    vprod[a] = {fa, PTerm{zb + pl.gblk_z[a], wz}};
+                    for (int32_t b = k0; b <= a; ++b)
+                        mprod[m++] = {(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]),
+                                      PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}};
+                }
+            }
+        });
     }
     // stable by key (the order std::stable_sort gives): LSD radix passes of
-    // 11-bit digits over the key (one pass for small problems, two at C4)
+    // 11-bit digits over the key (one pass for small problems, two at C4).
+    // Written for nr ranges (each histograms its digits, the (digit, range)
+    // prefix keeps every range's entries of one digit in range order, then
+    // every range scatters its own), run as one range here
     auto sort_terms = [&](auto& v) {
         using E = typename std::decay_t<decltype(v)>::value_type;
         auto less = [](const E& x, const E& y) { return x.first < y.first; };
@@ -945,24 +992,42 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             std::stable_sort(v.begin(), v.end(), less);
             return;
         }
-        constexpr int kD = 11;
+        constexpr int kD = 11, kB = 1 << kD;
         const int passes = std::max(1, (bits + kD - 1) / kD);
         std::vector<E> tmp(v.size());
         E* src = v.data();
         E* dst = tmp.data();
-        const size_t n = v.size();
+        const int64_t n = (int64_t)v.size();
+        const int nr = 1;   // (a split over host threads: see the call site)
+        std::vector<int64_t> cnt((size_t)nr * kB);
         for (int p = 0; p < passes; ++p) {
             const int sh = p * kD;
-            std::vector<int64_t> cnt((1 << kD) + 1, 0);
-            for (size_t k = 0; k < n; ++k) cnt[((src[k].first >> sh) & ((1 << kD) - 1)) + 1]++;
-            for (int d = 0; d < (1 << kD); ++d) cnt[d + 1] += cnt[d];
-            for (size_t k = 0; k < n; ++k) dst[cnt[(src[k].first >> sh) & ((1 << kD) - 1)]++] = src[k];
+            auto digit = [&](const E& e) { return (int)((e.first >> sh) & (kB - 1)); };
+            parallel_segments(nr, [&](int r) {
+                int64_t* c = cnt.data() + (size_t)r * kB;
+                std::fill(c, c + kB, 0);
+                for (int64_t k = n * r / nr; k < n * (r + 1) / nr; ++k) c[digit(src[k])]++;
+            });
+            int64_t acc = 0;
+            for (int d = 0; d < kB; ++d)
+                for (int r = 0; r < nr; ++r) {
+                    const int64_t c = cnt[(size_t)r * kB + d];
+                    cnt[(size_t)r * kB + d] = acc;
+                    acc += c;
+                }
+            parallel_segments(nr, [&](int r) {
+                int64_t* c = cnt.data() + (size_t)r * kB;
+                for (int64_t k = n * r / nr; k < n * (r + 1) / nr; ++k) dst[c[digit(src[k])]++] = src[k];
+            });
             std::swap(src, dst);
         }
         if (src != v.data()) v.swap(tmp);
     };
     tm.mark("terms");
-    parallel_segments(5, [&](int g) {   // five independent lists
+    // the five lists concurrently, each sorted by one thread (on the GPU
+    // box's 16 host CPUs this measured faster than one list after another
+    // with the radix passes themselves split over the threads)
+    parallel_segments(5, [&](int g) {
         switch (g) {
             case 0: sort_terms(mprod); break;
             case 1: sort_terms(mterms); break;
@@ -1039,26 +1104,50 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             emit(key, kind, dst, rows, 6, 6, mterms, im, &mprod, &ipm);
         }
     } else {
-        // dense: every block that receives a term (the rest stays zero)
-        // keys of both (sorted) term lists, merged without duplicates
-        std::vector<int64_t> keys;
-        {
-            size_t a = 0, b = 0;
-            int64_t last = -1;
-            while (a < mterms.size() || b < mprod.size()) {
-                const int64_t ka = a < mterms.size() ? mterms[a].first : INT64_MAX;
-                const int64_t kb = b < mprod.size() ? mprod[b].first : INT64_MAX;
-                const int64_t k = std::min(ka, kb);
-                if (k != last) keys.push_back(last = k);
-                if (ka == k) ++a;
-                else ++b;
-            }
-        }
-        for (int64_t key : keys) {
+        // dense: every block that receives a term (the rest stays zero), in
+        // key order.  Every key of the sorted lists is a target, so the
+        // target term lists are the sorted lists themselves: copied whole on
+        // the host threads, each target pointing at its key's run.
+        auto runs = [&](const auto& v, std::vector<std::pair<int64_t, int64_t>>& out) {   // (key, first index)
+            const int64_t n = (int64_t)v.size();
+            const int nr = n < 65536 ? 1 : PlanPool::width();
+            std::vector<std::vector<std::pair<int64_t, int64_t>>> part(nr);
+            parallel_segments(nr, [&](int r) {
+                for (int64_t k = n * r / nr; k < n * (r + 1) / nr; ++k)
+                    if (k == 0 || v[k].first != v[k - 1].first) part[r].push_back({v[k].first, k});
+            });
+            out.clear();
+            for (auto& q : part) out.insert(out.end(), q.begin(), q.end());
+            out.push_back({INT64_MAX, n});
+        };
+        std::vector<std::pair<int64_t, int64_t>> ra, rb;
+        runs(mterms, ra);
+        runs(mprod, rb);
+        const int32_t t0 = (int32_t)pl.terms.size(), q0 = (int32_t)pl.pterms.size();
+        pl.terms.resize(t0 + mterms.size());
+        pl.pterms.resize(q0 + mprod.size());
+        parallel_ranges((int64_t)mterms.size(), [&](int64_t a, int64_t b, int) {
+            for (int64_t k = a; k < b; ++k) pl.terms[t0 + k] = mterms[k].second;
+        });
+        parallel_ranges((int64_t)mprod.size(), [&](int64_t a, int64_t b, int) {
+            for (int64_t k = a; k < b; ++k) pl.pterms[q0 + k] = mprod[k].second;
+        });
+        size_t ia = 0, ib = 0;
+        while (ra[ia].first != INT64_MAX || rb[ib].first != INT64_MAX) {
+            const int64_t key = std::min(ra[ia].first, rb[ib].first);
             const int32_t a = (int32_t)(key / nFB), b = (int32_t)(key % nFB);
-            emit(key, kDstDense, col_of_fb(a) * pl.nF + col_of_fb(b), size_of_fb(a), size_of_fb(b), (int32_t)pl.nF,
-                 mterms, im, &mprod, &ipm);
+            ReduceTarget t{};
+            t.dst = col_of_fb(a) * pl.nF + col_of_fb(b);
+            t.dst_kind = kDstDense;
+            t.rows = size_of_fb(a); t.cols = size_of_fb(b); t.ld = (int32_t)pl.nF;
+            t.c_begin = t.c_end = t0 + (int32_t)ra[ia].second;
+            if (ra[ia].first == key) t.c_end = t0 + (int32_t)ra[++ia].second;
+            t.p_begin = t.p_end = q0 + (int32_t)rb[ib].second;
+            if (rb[ib].first == key) t.p_end = q0 + (int32_t)rb[++ib].second;
+            pl.targets.push_back(t);
         }
+        im = mterms.size();
+        ipm = mprod.size();
     }
     // vectors: rhs = bF - Z w, bF, cnF, per F block in order
     for (int32_t fb = 0; fb < nFB; ++fb)

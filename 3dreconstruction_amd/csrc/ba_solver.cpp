@@ -70,7 +70,7 @@ struct sfm_ba_plan {
     DBuf<int64_t> src_off;
     DBuf<double> raw_uv, raw_X;
     BcrArgs bcr;
-    unsigned bcr_epoch = 0;   // RCS solves so far (the back-substitution flags' epoch)
+    unsigned bcr_epoch = 0;   // RCS solves so far (the back-substitution flags' epoch, BCR or dense)
     bool use_bcr = false;
     int64_t rcs_n = 0;
     double* scal_h = nullptr;  // pinned, host-mapped: [kScCount] + finalize sequence word
@@ -327,6 +327,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         dense_setup(pl->dense, P);
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
+        SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * (size_t)pl->dense.nt, s));
     }
     if (pl->use_bcr) {
         bcr_setup(pl->bcr, P);
@@ -500,7 +501,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (ctx->world > 1) SFM_HIP(hipMemsetAsync(pl->rcs.p, 0, (size_t)pl->rcs_n * sizeof(double), s));
         ba_reduce(P, false, s);
         allreduce_rcs();
-        if (P.dense) dense_solve(pl->dense, P, radius, s);
+        if (P.dense) dense_solve(pl->dense, P, radius, s, ++pl->bcr_epoch);
         else if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s, ++pl->bcr_epoch);
         else ba_solve(P, radius, s);
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -119,42 +120,79 @@ class BasicBundleAdjuster {
             img_cam_[k] = add_cam(f->getImage2()->getCamera(), false);
         }
         const_img_ = world->local_frames_.empty() ? -1 : 0;
-        // points in index order (the reference iterates its unordered_map)
+        // points in index order (the reference iterates its unordered_map).
         // The walk over the world is a pointer chase (every point and its
-        // observation list are separate heap blocks): both are prefetched a
-        // few points ahead, and the adjuster keeps plain pointers (the world
-        // owns the points for the whole call), so no reference counts move.
+        // observation list are separate heap blocks), so it runs on host
+        // threads over point ranges, each prefetching a few points ahead:
+        //   pass 1: observations per point, and the images each range meets
+        //           first, in order (merged in range order, that is the
+        //           problem's image order of a serial walk: first appearance);
+        //   pass 2: every range writes its points' X, image indices and uv.
+        // The adjuster keeps plain pointers (the world owns the points for the
+        // whole call), so no reference counts move.
         const std::vector<WorldPoint::Ptr>& pts = world->pointsByIdx();
         const std::size_t np = pts.size();
-        points_.clear(); X_.clear(); off_.assign(1, 0); obs_img_.clear(); uv_.clear();
-        points_.reserve(np);
-        X_.reserve(3 * np);
-        off_.reserve(np + 1);
-        obs_img_.reserve(8 * np);
-        uv_.reserve(16 * np);
+        const int nr = (int)std::max<std::size_t>(
+            1, std::min<std::size_t>({16, std::max(1u, std::thread::hardware_concurrency()), np / 4096}));
+        std::vector<std::vector<const Image::Ptr*>> first(nr);   // into the world's lists
+        points_.resize(np);
+        X_.resize(3 * np);
+        off_.assign(np + 1, 0);
+        auto ranges = [&](auto&& fn) {
+            std::vector<std::thread> th;
+            for (int r = 1; r < nr; ++r) th.emplace_back([&, r] { fn(r, np * r / nr, np * (r + 1) / nr); });
+            fn(0, 0, np / nr);
+            for (auto& t : th) t.join();
+        };
         constexpr std::size_t kAhead = 8;
-        for (std::size_t k = 0; k < np; ++k) {
-            if (k + 2 * kAhead < np) __builtin_prefetch(pts[k + 2 * kAhead].get());
-            if (k + kAhead < np) {
+        auto prefetch = [&](std::size_t k, std::size_t k1) {
+            if (k + 2 * kAhead < k1) __builtin_prefetch(pts[k + 2 * kAhead].get());
+            if (k + kAhead < k1) {
                 const auto& of = pts[k + kAhead]->observed_frames_;
                 __builtin_prefetch(of.data());
                 __builtin_prefetch(reinterpret_cast<const char*>(of.data()) + 64);
                 __builtin_prefetch(reinterpret_cast<const char*>(of.data()) + 128);
             }
-            WorldPoint* p = pts[k].get();
-            points_.push_back(p);
-            X_.insert(X_.end(), p->world_pos_.begin(), p->world_pos_.end());
-            for (auto& [im, uv] : p->observed_frames_) {
-                // image_extrinsic_[image] / camera_intrinsics_[camera] are
-                // operator[]: unseen blocks are inserted as zeros (:118-119)
-                const int k = add_img(im, true);
-                if (img_cam_[k] < 0) img_cam_[k] = add_cam(im->getCamera(), true);
-                obs_img_.push_back(k);
-                uv_.push_back(uv.x);
-                uv_.push_back(uv.y);
+        };
+        ranges([&](int r, std::size_t k0, std::size_t k1) {
+            std::vector<char> seen;
+            for (std::size_t k = k0; k < k1; ++k) {
+                prefetch(k, k1);
+                WorldPoint* p = pts[k].get();
+                points_[k] = p;
+                off_[k + 1] = (int64_t)p->observed_frames_.size();
+                for (auto& ob : p->observed_frames_) {
+                    const std::size_t id = ob.first->getIdx();
+                    if (id >= seen.size()) seen.resize(id + 1, 0);
+                    if (!seen[id]) { seen[id] = 1; first[r].push_back(&ob.first); }
+                }
             }
-            off_.push_back((int64_t)obs_img_.size());
-        }
+        });
+        for (std::size_t k = 0; k < np; ++k) off_[k + 1] += off_[k];
+        // image_extrinsic_[image] / camera_intrinsics_[camera] are operator[]:
+        // unseen blocks are inserted as zeros (:118-119)
+        for (const auto& f : first)
+            for (const Image::Ptr* im : f) {
+                const int k = add_img(*im, true);
+                if (img_cam_[k] < 0) img_cam_[k] = add_cam((*im)->getCamera(), true);
+            }
+        const int64_t nobs = off_[np];
+        obs_img_.resize(nobs);
+        uv_.resize(2 * nobs);
+        ranges([&](int, std::size_t k0, std::size_t k1) {
+            for (std::size_t k = k0; k < k1; ++k) {
+                prefetch(k, k1);
+                const WorldPoint* p = points_[k];
+                for (int a = 0; a < 3; ++a) X_[3 * k + a] = p->world_pos_[a];
+                int64_t o = off_[k];
+                for (auto& ob : p->observed_frames_) {
+                    obs_img_[o] = img_slot_[ob.first->getIdx()];
+                    uv_[2 * o] = ob.second.x;
+                    uv_[2 * o + 1] = ob.second.y;
+                    ++o;
+                }
+            }
+        });
     }
     bool solve() {
         sfm_ba_problem pr{};
@@ -190,10 +228,19 @@ class BasicBundleAdjuster {
         return true;
     }
     void update() {  // updateWorld (:143-156)
-        for (std::size_t k = 0; k < points_.size(); ++k) {
-            if (k + 8 < points_.size()) __builtin_prefetch(points_[k + 8], 1);
-            points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
-        }
+        const std::size_t np = points_.size();
+        const int nr = (int)std::max<std::size_t>(
+            1, std::min<std::size_t>({16, std::max(1u, std::thread::hardware_concurrency()), np / 4096}));
+        auto range = [&](std::size_t k0, std::size_t k1) {
+            for (std::size_t k = k0; k < k1; ++k) {
+                if (k + 8 < k1) __builtin_prefetch(points_[k + 8], 1);
+                points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
+            }
+        };
+        std::vector<std::thread> th;
+        for (int r = 1; r < nr; ++r) th.emplace_back(range, np * r / nr, np * (r + 1) / nr);
+        range(0, np / nr);
+        for (auto& t : th) t.join();
         for (std::size_t k = 0; k < images_.size(); ++k) {
             std::array<double, 6> p;
             for (int a = 0; a < 6; ++a) p[a] = extr_[6 * k + a];
