@@ -424,8 +424,8 @@ def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2, model=0):
     (nF = 6 (n_cam - 1) + 4) and the general-point path plus the blocked dense
     Cholesky (ba_bcr.hip dense_*) carry the solve.  C4's sizes.
     model = SFM_CAM_RADIAL3: C4's banded geometry under OpenMVG's
-    PINHOLE_CAMERA_RADIAL3 residual, which the planner
-    always sends through the general-point path and the dense RCS."""
+    PINHOLE_CAMERA_RADIAL3 residual: the chunk path with
+    6-row intrinsics slots and the BCR band solver, as pinhole."""
     t0 = time.time()
     r3 = model == abi.SFM_CAM_RADIAL3
     sc = c4_scene(n_cam, n_pt, k=k, seed=0x5F3D0004 if r3 else 0x5F3D0014, vis=0 if r3 else 1, model=model)
@@ -443,18 +443,19 @@ def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2, model=0):
     dt = time.perf_counter() - t1
     plan.close()
     nF = info.rcs_dim
+    dense = bool(api.ba_describe(sc["problem"]).dense)
     out = {"metric": "BA LM-iters/sec, PINHOLE_CAMERA_RADIAL3 residual model" if r3 else
                      "BA LM-iters/sec, dense reduced camera system (random-k visibility)",
            "value": iters / dt, "unit": "LM-iters/s", "ms_per_iteration": dt / max(iters, 1) * 1e3,
            "lm_iterations_per_solve": summ.iterations, "rmse_initial": summ.rmse_initial,
-           "rmse_final": summ.rmse_final, "rcs_dim": nF, "dense": True,
-           "rcs_factor_flops_per_iteration": nF ** 3 / 3.0, "host_plan_seconds": t_plan,
+           "rmse_final": summ.rmse_final, "rcs_dim": nF, "dense": dense,
+           "rcs_factor_flops_per_iteration": nF ** 3 / 3.0 if dense else None, "host_plan_seconds": t_plan,
            "config": {"workload": f"{n_cam} cams / {n_pt} pts / {sc['n_obs']} obs, random k={k} visibility "
                                   "(SURVEY §8(d) dense-S stress variant of C4), HuberLoss(4)"}}
     if r3:
         out["config"] = {"workload": f"C4 geometry ({n_cam} cams / {n_pt} pts / {sc['n_obs']} obs, banded k={k}), "
                                      "OpenMVG Pinhole_Intrinsic_Radial_K3 residual {f, ppx, ppy, k1, k2, k3} "
-                                     "(one shared block, ADJUST_ALL), HuberLoss(4); general-point path + dense RCS"}
+                                     "(one shared block, ADJUST_ALL), HuberLoss(4); chunk path + BCR band solver"}
     log(f"BA {'radial3' if r3 else 'dense-S'}: {iters} LM iterations in {dt:.3f}s -> {iters / dt:.1f} it/s, rcs {nF}, plan {t_plan:.1f}s, "
         f"rmse {summ.rmse_initial:.4f}->{summ.rmse_final:.4f}")
     return out
