@@ -1795,31 +1795,61 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
 // per general point) go through preduce_seg_kernel + preduce_long_kernel.
 constexpr int kLongPTerms = 64;
 
-// sum over the product terms q = q0, q0 + G, q0 + 2G, ... < q1 of
-// Z_a[3r..3r+2] . Z_b[3cc..3cc+2], four terms' loads in flight
-__device__ __forceinline__ double pterm_sum(const DevProblem& P, int q0, int q1, int G, int r, int cc) {
+// sum over the product terms q = qa + g, qa + g + G, ... < qb of
+// Z_a[3r..3r+2] . Z_b[3cc..3cc+2] (ascending, one term after another, as a
+// plain per-lane loop would).  The Z blocks are staged through LDS kPtB terms
+// at a time: the wave loads each term's two blocks once, coalesced (the rows
+// are contiguous 3-vectors), instead of every lane gathering its own six
+// doubles per term (36 lanes x 6 scattered 8-byte loads per term made the
+// reduce address-bound).  Rows are padded to 4 doubles in LDS (two 16-byte
+// reads per 3-vector).  ra / rb: rows of the a / b block (b = w: 1 row).
+#ifndef SFM_PTB   // terms per staged batch of the product-term reduce
+#define SFM_PTB 16
+#endif
+constexpr int kPtB = SFM_PTB;
+constexpr int kPtLds = kPtB * 12 * 4 + 2 * kPtB;   // doubles of LDS per wave (<= 6 + 6 rows per term, the terms)
+__device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb, int G, int g, int r, int cc,
+                                            int ra, int rb, double* lds) {
     const double* Z = P.Z;
+    const int lane = threadIdx.x & 63;
+    const int la = 3 * ra, L = la + 3 * rb;   // doubles per term
+    double* La = lds;                          // [kPtB][ra][4]
+    double* Lb = lds + kPtB * ra * 4;          // [kPtB][rb][4]
+    PTerm* Lt = reinterpret_cast<PTerm*>(lds + kPtB * 12 * 4);   // [kPtB] the batch's terms
+    const bool isa = lane < la;
+    const int oo = isa ? lane : lane - la, orow = oo / 3, ok = oo - 3 * orow;
+    double* dst = (isa ? La + orow * 4 : Lb + orow * 4) + ok;
+    const int dstep = 4 * (isa ? ra : rb);
     double s = 0.0;
-    int q = q0;
-    for (; q + 3 * G < q1; q += 4 * G) {
-        double a[4][3], bb[4][3];
+    for (int q0 = qa; q0 < qb; q0 += kPtB) {
+        const int nb = min(kPtB, qb - q0);
+        // stage: the batch's term offsets through LDS, then lane o < L loads
+        // element o of every term (its row and column fixed: no index
+        // division), all kPtB loads in flight before the first store
+        if (lane < nb) Lt[lane] = P.pterms[q0 + lane];
+        wsync();
+        double v[kPtB];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const PTerm pt = P.pterms[q + t * G];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                a[t][k] = Z[pt.za + 3 * r + k];
-                bb[t][k] = Z[pt.zb + 3 * cc + k];
-            }
+        for (int t = 0; t < kPtB; ++t) {
+            const int64_t off = isa ? Lt[t].za : Lt[t].zb;
+            v[t] = (lane < L && t < nb) ? Z[off + oo] : 0.0;
         }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) s += a[t][0] * bb[t][0] + a[t][1] * bb[t][1] + a[t][2] * bb[t][2];
-    }
-    for (; q < q1; q += G) {
-        const PTerm pt = P.pterms[q];
-        const double* za = Z + pt.za + 3 * r;
-        const double* zb = Z + pt.zb + 3 * cc;
-        s += za[0] * zb[0] + za[1] * zb[1] + za[2] * zb[2];
+        for (int t = 0; t < kPtB; ++t)
+            if (lane < L && t < nb) dst[t * dstep] = v[t];
+        wsync();
+        if (g >= 0) {
+            // this group's terms in the batch: j = g - (q0 - qa) mod G, + G, ...
+            int j = (g - (q0 - qa) % G + G) % G;
+            for (; j < nb; j += G) {
+                const double2 a01 = *reinterpret_cast<const double2*>(La + (j * ra + r) * 4);
+                const double a2 = La[(j * ra + r) * 4 + 2];
+                const double2 b01 = *reinterpret_cast<const double2*>(Lb + (j * rb + cc) * 4);
+                const double b2 = Lb[(j * rb + cc) * 4 + 2];
+                s += a01.x * b01.x + a01.y * b01.y + a2 * b2;
+            }
+        }
+        wsync();
     }
     return s;
 }
@@ -1839,10 +1869,11 @@ __global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
         act = T.p_end > T.p_begin && T.p_end - T.p_begin <= kLongPTerms;
     }
     if (!act) return;   // whole waves only: the exchange below is wave-local
+    __shared__ __attribute__((aligned(16))) double stage[4][kPtLds];
     const int E = T.rows * T.cols, G = 64 / E, g = lane / E, e = lane - g * E;
     const bool vec = T.cols == 1;
-    double s = 0.0;
-    if (g < G) s = pterm_sum(P, T.p_begin + g, T.p_end, G, e / T.cols, vec ? 0 : e % T.cols);
+    const double s = pterm_sum(P, T.p_begin, T.p_end, G, g < G ? g : -1, e / T.cols, vec ? 0 : e % T.cols,
+                               T.rows, vec ? 1 : T.cols, stage[wave]);
     part[wave][lane] = s;
     wsync();
     if (lane < E) {
@@ -1865,8 +1896,10 @@ __global__ __launch_bounds__(256) void preduce_seg_kernel(DevProblem P) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane / E, e = lane - g * E;
     constexpr int kQ = kReduceSeg / 4;
     const int q0 = k0 + wave * kQ, q1 = min(min(k0 + kReduceSeg, (int)T.p_end), q0 + kQ);
-    double s = 0.0;
-    if (g < G) s = pterm_sum(P, q0 + g, q1, G, e / T.cols, vec ? 0 : e % T.cols);
+    __shared__ __attribute__((aligned(16))) double stage[4][kPtLds];
+    const double s = q0 < q1 ? pterm_sum(P, q0, q1, G, g < G ? g : -1, e / T.cols, vec ? 0 : e % T.cols, T.rows,
+                                         vec ? 1 : T.cols, stage[wave])
+                             : 0.0;
     __shared__ double part[4][64];
     part[wave][lane] = s;
     __syncthreads();

@@ -1,13 +1,10 @@
-# dense-S / RADIAL3 bench lines and the general-path kernel averages for
-# library variants: tools/gpurun/dense_ab.sh lib...
+# General-point / dense-RCS GPU tests, then the dense-S and RADIAL3 lines and
+# the dense-S kernel stats: tools/gpurun/dense_ab.sh <tag>
 set -e
 cd "$GRAFT_REPO_ROOT"
-export TMPDIR=/tmp
-ARGS="--no-match --no-snavely --no-loop --no-pmc --no-filter --no-cpu-baseline"
-OUT=$GRAFT_REPO_ROOT/gpurun_out/dab
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-da}
 mkdir -p "$OUT"
-for L in "$@"; do
-    if [ "$L" = base ]; then unset SFMCORE_LIB; else export SFMCORE_LIB=$GRAFT_REPO_ROOT/$L; fi
-    timeout -k 10 300 python -u bench.py $ARGS 2> "$OUT/$(basename $L).err" > /dev/null
-    echo "$L: $(grep -E '^\[bench\] BA (dense-S|radial3)' "$OUT/$(basename $L).err" | sed 's/, plan.*//' | tr '\n' ' ')"
-done
+timeout -k 10 900 python -u -m pytest tests/test_ba_general_gpu.py tests/test_radial3.py tests/test_snavely.py tests/test_ba_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
+tail -1 "$OUT/tests.log"
+timeout -k 10 300 python -u tools/dense_prof.py 2>&1 | grep "dense-S"
+bash tools/gpurun/dense_kstats.sh "${1:-da}"
