@@ -57,6 +57,11 @@ struct DevProblem {
     const int32_t* gblk_col;        // F column of each block
     const int32_t* gblk_z;          // block's offset within the point's Z
     const int64_t* gz_off;          // [n_gpt+1]
+    // general points split for the Z kernels: batches of consecutive short
+    // points (zbatch_kernel, one wave each) and the rest (zpoint_kernel)
+    int32_t n_zbatch, n_zlong;
+    const int32_t* zbatch;          // [n_zbatch][2] general point range [g0, g1)
+    const int32_t* zlong;           // [n_zlong] general point
     const PTerm* pterms;
     double* Z;                      // general points' eliminated rows, w after each point's blocks
     int32_t n_plong;                // targets with > preduce_long_threshold() product terms

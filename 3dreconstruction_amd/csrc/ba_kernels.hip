@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
     double* zc = zlds;                       // [64][kZStage] camera rows J_c' M of this round
     double* Zl = zlds + 64 * kZStage;        // the point's Z (blocks), accumulated
     __shared__ int cbl[64];
-    const int lane = threadIdx.x, g = blockIdx.x;
+    const int lane = threadIdx.x, g = P.zlong[blockIdx.x];
     const int k = P.n_cpt + g;
     const int o0 = P.pt_off[k], o1 = P.pt_off[k + 1];
     const int b0 = P.gblk_off[g];
@@ -1784,6 +1784,201 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
     if (lane < 3) {
         const double w3[3] = {i00 * b[0], i10 * b[0] + i11 * b[1], i20 * b[0] + i21 * b[1] + i22 * b[2]};
         Zg[zn + lane] = lane == 0 ? w3[0] : lane == 1 ? w3[1] : w3[2];
+    }
+}
+
+// Short general points (<= kZShortObs observations), a batch of consecutive
+// points per wave, one lane per observation (zpoint_kernel spent a wave on
+// each point, 10 of 64 lanes busy at random-k visibility, and linearised every
+// observation twice).  Each observation is linearised once; every per-point
+// sum (column norms, V | g_E, a camera block's run, an intrinsics block) is
+// taken by the first lane of its group over the group's LDS rows in
+// observation order, so the result is fixed.
+constexpr int kZRow = 19;   // LDS row stride (doubles) of a lane's staged values
+template <int CM, bool SE>
+__global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* __restrict__ cps,
+                                                    const double* __restrict__ intr, const double* __restrict__ X,
+                                                    double radius) {
+    constexpr int IW = kIW<CM>;
+    constexpr int NI = CM == SFM_CAM_SNAVELY ? 3 : IW;   // intrinsics parameters with a column
+    __shared__ double rc[64][kZRow];      // camera rows J_c' M (18); before that V | g_E (9), column norms (3)
+    __shared__ double ri[64][kZRow];      // intrinsics rows J_i' M (3 NI)
+    __shared__ double pv[kZBatchPts][12]; // per point: V (6) | g_E (3) | sE (3)
+    __shared__ int poff[kZBatchPts + 1], okey[64], oib[64];
+    const int lane = threadIdx.x;
+    const int g0 = P.zbatch[2 * blockIdx.x], g1 = P.zbatch[2 * blockIdx.x + 1], np = g1 - g0;
+    const int oA = P.pt_off[P.n_cpt + g0];
+    if (lane <= np) poff[lane] = P.pt_off[P.n_cpt + g0 + lane] - oA;
+    wsync();
+    const int nobs = poff[np];
+    const bool act = lane < nobs;
+    int pl = 0;   // this lane's point within the batch
+    for (int j = 1; j < np; ++j) pl += poff[j] <= lane ? 1 : 0;
+    const int g = g0 + pl, k = P.n_cpt + g, o = oA + lane;
+    const bool head = act && lane == poff[pl];   // the point's first observation
+    double Xp[3] = {0.0, 0.0, 0.0};
+    LinT<CM> L{};
+    int img = 0, cb = 0xffff, ib = 0;
+    if (act) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) Xp[a] = X[3 * (size_t)k + a];
+        img = P.obs_img[o];
+        const int slot = P.obs_slot[o];
+        cb = slot & 0xffff;
+        ib = slot >> 16;
+        const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+        linearize<CM, true, true, true>(cps[img], intr + IW * (size_t)P.img_intr[img], Xp, uv.x, uv.y, P.huber_a, L);
+    }
+    // per-point sums of n values staged in rc by every lane: the head lane adds
+    // its point's rows in order into pv[pl][at..at+n)
+    auto point_sum = [&](int n, int at) {
+        wsync();
+        if (head) {
+            for (int e = 0; e < n; ++e) {
+                double acc = rc[lane][e];
+                for (int q = lane + 1; q < poff[pl + 1]; ++q) acc += rc[q][e];
+                pv[pl][at + e] = acc;
+            }
+        }
+        wsync();
+    };
+    double sE[3];
+    if constexpr (SE) {
+        // the solve's first pass: Ceres' Jacobi point scales from the column
+        // norms of the unscaled point Jacobian
+        if (act)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) rc[lane][a] = L.Jx[0][a] * L.Jx[0][a] + L.Jx[1][a] * L.Jx[1][a];
+        point_sum(3, 9);
+        if (head)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double se = 1.0 / (1.0 + sqrt(pv[pl][9 + a]));
+                pv[pl][9 + a] = se;
+                P.scaleE[3 * (size_t)k + a] = se;
+            }
+        wsync();
+#pragma unroll
+        for (int a = 0; a < 3; ++a) sE[a] = pv[pl][9 + a];
+    } else {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) sE[a] = act ? P.scaleE[3 * (size_t)k + a] : 1.0;
+    }
+    // V = Jx' Jx, g_E = Jx' f per point (scaled)
+    double j[2][3];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) j[r][a] = L.Jx[r][a] * sE[a];
+    if (act) {
+        double v9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const double fr = L.f[r];
+            v9[0] += j[r][0] * j[r][0]; v9[1] += j[r][1] * j[r][0]; v9[2] += j[r][1] * j[r][1];
+            v9[3] += j[r][2] * j[r][0]; v9[4] += j[r][2] * j[r][1]; v9[5] += j[r][2] * j[r][2];
+            v9[6] += j[r][0] * fr; v9[7] += j[r][1] * fr; v9[8] += j[r][2] * fr;
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) rc[lane][e] = v9[e];
+    }
+    point_sum(9, 0);
+    double V[6], b[3];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) V[e] = pv[pl][e];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) b[e] = pv[pl][6 + e];
+    if (head) {   // gradient / norm bookkeeping at x
+        double xn2 = 0.0, gmx = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const double gg = b[a] * rcp_nr(sE[a]);
+            xn2 += Xp[a] * Xp[a];
+            gmx = fmax(gmx, fabs(Xp[a] - (Xp[a] - gg)));
+        }
+        P.part_s[2 * (size_t)(P.n_chunk + g)] = xn2;
+        P.part_s[2 * (size_t)(P.n_chunk + g) + 1] = gmx;
+    }
+    const double inv_radius = 1.0 / radius;
+    const int di[3] = {0, 2, 5};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
+        V[di[a]] += lm * lm;
+    }
+    const double i00 = rsqrt_nr(V[0]);
+    const double l10 = V[1] * i00, l20 = V[3] * i00;
+    const double i11 = rsqrt_nr(V[2] - l10 * l10);
+    const double l21 = (V[4] - l20 * l10) * i11;
+    const double i22 = rsqrt_nr(V[5] - l20 * l20 - l21 * l21);
+    const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    if (act) {
+        double M[2][3];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            M[r][0] = j[r][0] * i00;
+            M[r][1] = j[r][0] * i10 + j[r][1] * i11;
+            M[r][2] = j[r][0] * i20 + j[r][1] * i21 + j[r][2] * i22;
+        }
+        if (cb != 0xffff) {
+            const int colc = P.img_colc[img];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const double sc = P.scaleF[colc + r];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) rc[lane][3 * r + a] = (L.Jc[0][r] * sc) * M[0][a] + (L.Jc[1][r] * sc) * M[1][a];
+            }
+        }
+        const int coli = P.img_coli[img];
+#pragma unroll
+        for (int r = 0; r < NI; ++r) {
+            const double sc = P.scaleF[coli + r];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) ri[lane][3 * r + a] = (L.Ji[0][r] * sc) * M[0][a] + (L.Ji[1][r] * sc) * M[1][a];
+        }
+    }
+    okey[lane] = act ? (pl << 17 | cb) : -1;
+    oib[lane] = ib;
+    wsync();
+    if (act) {
+        double* Zp = P.Z + P.gz_off[g];
+        const int b0 = P.gblk_off[g], pend = poff[pl + 1];
+        // camera block: the first lane of a run of one (point, camera block)
+        // adds the run in order (the planner sorts a point's views by image)
+        if (cb != 0xffff && (lane == poff[pl] || okey[lane - 1] != okey[lane])) {
+            double acc[18];
+#pragma unroll
+            for (int e = 0; e < 18; ++e) acc[e] = rc[lane][e];
+            for (int q = lane + 1; q < pend && okey[q] == okey[lane]; ++q)
+#pragma unroll
+                for (int e = 0; e < 18; ++e) acc[e] += rc[q][e];
+            double* dst = Zp + P.gblk_z[b0 + cb];
+#pragma unroll
+            for (int e = 0; e < 18; ++e) dst[e] = acc[e];
+        }
+        // intrinsics block: the point's first lane with that block adds all of
+        // the point's lanes with it, in order
+        bool first = true;
+        for (int q = poff[pl]; q < lane; ++q) first = first && oib[q] != ib;
+        if (first) {
+            double acc[3 * NI];
+#pragma unroll
+            for (int e = 0; e < 3 * NI; ++e) acc[e] = ri[lane][e];
+            for (int q = lane + 1; q < pend; ++q)
+                if (oib[q] == ib)
+#pragma unroll
+                    for (int e = 0; e < 3 * NI; ++e) acc[e] += ri[q][e];
+            double* dst = Zp + P.gblk_z[b0 + ib];
+#pragma unroll
+            for (int e = 0; e < 3 * IW; ++e) dst[e] = e < 3 * NI ? acc[e < 3 * NI ? e : 0] : 0.0;   // SNAVELY: row 3 is 0
+        }
+        if (head) {   // w = L^-1 g_E after the point's blocks
+            const int zn = (int)(P.gz_off[g + 1] - P.gz_off[g]) - 3;
+            Zp[zn] = i00 * b[0];
+            Zp[zn + 1] = i10 * b[0] + i11 * b[1];
+            Zp[zn + 2] = i20 * b[0] + i21 * b[1] + i22 * b[2];
+        }
     }
 }
 
@@ -2178,21 +2373,30 @@ void ba_fscale(const DevProblem& P, hipStream_t s) {
 
 void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const double* X, double radius,
               hipStream_t s, unsigned long long* stamps, bool scale_e) {
-    if (P.n_gpt > 0) {
+    if (P.n_zbatch > 0) {
+        if (scale_e)
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((zbatch_kernel<CM, true>), dim3(P.n_zbatch), dim3(64), 0, s, P, cp,
+                                                   intr, X, radius));
+        else
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((zbatch_kernel<CM, false>), dim3(P.n_zbatch), dim3(64), 0, s, P,
+                                                   cp, intr, X, radius));
+        SFM_HIP(hipGetLastError());
+    }
+    if (P.n_zlong > 0) {
         const size_t lds = (64 * kZStage + (size_t)P.gz_max) * sizeof(double);
         if (scale_e)
             SFM_BY_MODEL_ALL(P, {
                 if (lds > 64 * 1024)
                     SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, true>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                hipLaunchKernelGGL((zpoint_kernel<CM, true>), dim3(P.n_gpt), dim3(64), lds, s, P, cp, intr, X, radius);
+                hipLaunchKernelGGL((zpoint_kernel<CM, true>), dim3(P.n_zlong), dim3(64), lds, s, P, cp, intr, X, radius);
             });
         else
             SFM_BY_MODEL_ALL(P, {
                 if (lds > 64 * 1024)
                     SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, false>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                hipLaunchKernelGGL((zpoint_kernel<CM, false>), dim3(P.n_gpt), dim3(64), lds, s, P, cp, intr, X, radius);
+                hipLaunchKernelGGL((zpoint_kernel<CM, false>), dim3(P.n_zlong), dim3(64), lds, s, P, cp, intr, X, radius);
             });
         SFM_HIP(hipGetLastError());
     }

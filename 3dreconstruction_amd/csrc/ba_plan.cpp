@@ -827,6 +827,28 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         });
         for (int64_t f : gfl) flops += f;
         pl.n_z = pl.gz_off[pl.n_gpt];
+        // Z kernel work: batches of consecutive short points, the rest alone
+        pl.zbatch.clear();
+        pl.zlong.clear();
+        int32_t g0 = -1, nobs = 0;
+        auto close = [&](int32_t g1) {
+            if (g0 >= 0) { pl.zbatch.push_back(g0); pl.zbatch.push_back(g1); }
+            g0 = -1;
+            nobs = 0;
+        };
+        for (int32_t g = 0; g < (int32_t)pl.n_gpt; ++g) {
+            const int64_t k = pl.n_cpt + g;
+            const int32_t n = pl.pt_off[k + 1] - pl.pt_off[k];
+            if (n > kZShortObs) {
+                close(g);
+                pl.zlong.push_back(g);
+                continue;
+            }
+            if (g0 >= 0 && (nobs + n > 64 || g - g0 >= kZBatchPts)) close(g);
+            if (g0 < 0) g0 = g;
+            nobs += n;
+        }
+        close((int32_t)pl.n_gpt);
     }
     tm.mark("general");
     // the observation arrays are final from here on: the caller may start

@@ -43,6 +43,12 @@ struct BAHostPlan {
     std::vector<int32_t> gblk_z;     // element offset of the block's Z rows within the point's Z
     std::vector<int64_t> gz_off;     // [n_gpt+1] Z buffer range of a point: blocks, then w (3)
     int64_t n_z = 0, gz_max = 0;     // Z doubles in all / of the largest point
+    // Z kernels: batches of consecutive general points of <= kZShortObs
+    // observations each, <= 64 observations and <= kZBatchPts points per batch
+    // (one wave, one lane per observation), and the longer points (one wave
+    // per point, rounds of 64)
+    std::vector<int32_t> zbatch;     // [n][2] general point range [g0, g1)
+    std::vector<int32_t> zlong;      // general point ids
     std::vector<int64_t> spt_global;  // shard point -> global point id
     // observation-sized arrays live in page-locked staging memory while a
     // context is bound (HostVec, common.h): uploaded, then released

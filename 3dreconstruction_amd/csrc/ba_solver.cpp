@@ -53,6 +53,7 @@ struct sfm_ba_plan {
     DBuf<int32_t> long_targets;
     DBuf<int32_t> gblk_off, gblk_col, gblk_z;   // general points
     DBuf<int64_t> gz_off;
+    DBuf<int32_t> zbatch, zlong;
     DBuf<PTerm> pterms;
     DBuf<double> Zbuf, dense_buf;
     DenseArgs dense;
@@ -131,6 +132,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->gblk_col, h.gblk_col, s);
     up(pl->gblk_z, h.gblk_z, s);
     up(pl->gz_off, h.gz_off, s);
+    up(pl->zbatch, h.zbatch, s);
+    up(pl->zlong, h.zlong, s);
     up(pl->pterms, h.pterms, s);
     pl->Zbuf.alloc(std::max<int64_t>(h.n_z, 1));
     std::vector<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
@@ -233,6 +236,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.dense = h.dense ? 1 : 0;
     P.gblk_off = pl->gblk_off.p; P.gblk_col = pl->gblk_col.p; P.gblk_z = pl->gblk_z.p;
     P.gz_off = pl->gz_off.p; P.pterms = pl->pterms.p; P.Z = pl->Zbuf.p;
+    P.zbatch = pl->zbatch.p; P.n_zbatch = (int32_t)(h.zbatch.size() / 2);
+    P.zlong = pl->zlong.p; P.n_zlong = (int32_t)h.zlong.size();
     P.tile_nt = h.tile_nt;
     P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D;
     P.nb = h.nb; P.nF = h.nF;

@@ -22,6 +22,8 @@ constexpr int kTileR = 16 * kTileN;       // 80 rows
 constexpr int kTileRowsUsed = 76;         // rows 0..75 for F blocks
 constexpr int kTileWRow = 79;             // row carrying w = L^-1 g_E
 constexpr int kSubPts = 6;                // points per wave batch (3 panel columns each)
+constexpr int kZShortObs = 32;            // general points the batched Z kernel takes (observations)
+constexpr int kZBatchPts = 16;            // points per batch of that kernel
 constexpr int kSubObs = 64;               // observations per wave batch (one per lane)
 constexpr int kChunkPts = 128;            // points per chunk (upper bound; step_kernel threads)
 constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass
