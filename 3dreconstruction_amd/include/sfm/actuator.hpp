@@ -403,9 +403,7 @@ class BasicSequentialActuator {
     }
     void end_step() {
         step_.world_points = (int64_t)world_->points().size();
-        int64_t nobs = 0;
-        for (auto& [i, p] : world_->points()) nobs += (int64_t)p->observed_frames_.size();
-        step_.world_observations = nobs;
+        step_.world_observations = world_->observationCount();
     }
     Image::Ptr make_image(const SeqImage& s) {
         auto im = std::make_shared<Image>(camera_);
@@ -463,16 +461,16 @@ class BasicSequentialActuator {
             auto it = im1->kpt_wpt_idx_map_.find((std::size_t)m.queryIdx);
             if (it != im1->kpt_wpt_idx_map_.end()) {   // a point seen before: extend its track
                 auto wp = world_->getPointFromIdx(it->second);
-                wp->last_descriptor_ = std::move(desc);
-                wp->observed_frames_.emplace_back(im2, im2->keypoints[m.trainIdx]);
+                world_->setLastDescriptor(it->second, std::move(desc));
+                world_->addObservation(wp, im2, im2->keypoints[m.trainIdx]);
                 im2->kpt_wpt_idx_map_[(std::size_t)m.trainIdx] = it->second;
                 ++step_.extended_obs;
                 continue;
             }
             const auto idx = world_->addPoint(pts[k], std::move(desc));
             auto wp = world_->getPointFromIdx(idx);
-            wp->observed_frames_.emplace_back(im1, im1->keypoints[m.queryIdx]);
-            wp->observed_frames_.emplace_back(im2, im2->keypoints[m.trainIdx]);
+            world_->addObservation(wp, im1, im1->keypoints[m.queryIdx]);
+            world_->addObservation(wp, im2, im2->keypoints[m.trainIdx]);
             im1->kpt_wpt_idx_map_[(std::size_t)m.queryIdx] = idx;
             im2->kpt_wpt_idx_map_[(std::size_t)m.trainIdx] = idx;
             ++step_.new_points;

@@ -63,18 +63,13 @@ class GlobalFrame {
     // GlobalFrame.h:16-20; index order is the deterministic choice)
     // (the world outlives the frame: it keeps the world's index-ordered list)
     GlobalFrame(const WorldStructure::Ptr& world, Image::Ptr image)
-        : image_(std::move(image)), world_points_(&world->pointsByIdx()) {}
-    // query = every world point's last_descriptor_, train = the image (:22-43)
+        : image_(std::move(image)), world_points_(&world->pointsByIdx()), world_desc_(&world->descriptorsByIdx()) {}
+    // query = every world point's last_descriptor_ (the world keeps them in
+    // one index-ordered array), train = the image (:22-43)
     template <class M> std::size_t matchFeature(M& matcher) {
         matches_.clear();
-        std::vector<uint8_t> q(world_points_->size() * 128);
-        uint8_t* dst = q.data();
-        for (const auto& p : *world_points_) {
-            std::memcpy(dst, p->last_descriptor_.data(), std::min<std::size_t>(128, p->last_descriptor_.size()));
-            dst += 128;
-        }
         std::vector<std::vector<DMatch>> v;
-        matcher.knnMatch(q, image_->descriptors, v, 1);
+        matcher.knnMatch(*world_desc_, image_->descriptors, v, 1);
         for (auto& row : v)
             if (!row.empty()) matches_.push_back(row[0]);
         raw_ = matches_.size();
@@ -103,6 +98,7 @@ class GlobalFrame {
     std::vector<DMatch> matches_;
     Image::Ptr image_;
     const std::vector<WorldPoint::Ptr>* world_points_;
+    const std::vector<uint8_t>* world_desc_;
     std::size_t raw_ = 0;
 };
 

@@ -7,6 +7,7 @@
 //   LocalFrame   src/frame/LocalFrame.h:19-83   (image pair + matches)
 // The fields BundleAdjuster and the matchers read/write keep their names.
 #pragma once
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstddef>
@@ -140,10 +141,25 @@ class WorldStructure {
         p->idx_ = cur_idx_++;
         p->world_pos_ = pos;
         p->last_descriptor_ = std::move(descriptor);
+        desc_.resize(desc_.size() + 128, 0);
+        std::copy_n(p->last_descriptor_.begin(), std::min<std::size_t>(128, p->last_descriptor_.size()),
+                    desc_.end() - 128);
         world_points_[p->idx_] = p;
         by_idx_.push_back(p);
         return p->idx_;
     }
+    // a point's latest descriptor (WorldPoint::last_descriptor_, kept in step
+    // with the index-ordered copy GlobalFrame matches against)
+    void setLastDescriptor(WorldPoint::Idx i, std::vector<uint8_t> descriptor) {
+        std::copy_n(descriptor.begin(), std::min<std::size_t>(128, descriptor.size()), desc_.begin() + 128 * i);
+        by_idx_[i]->last_descriptor_ = std::move(descriptor);
+    }
+    // a new observation of a point (its observed_frames_ list, and the count)
+    void addObservation(const WorldPoint::Ptr& p, std::shared_ptr<Image> im, Point2d uv) {
+        p->observed_frames_.emplace_back(std::move(im), uv);
+        ++n_obs_;
+    }
+    int64_t observationCount() const { return n_obs_; }
     void addLocalFrame(std::shared_ptr<LocalFrame> f) { local_frames_.push_back(std::move(f)); }
     const std::vector<std::shared_ptr<LocalFrame>>& getLocalFrames() const { return local_frames_; }
     WorldPoint::Ptr getPointFromIdx(WorldPoint::Idx i) const { return world_points_.at(i); }
@@ -151,6 +167,8 @@ class WorldStructure {
     // the same points in index order (points are only ever added, with
     // increasing indices): what GlobalFrame iterates, without a sort per image
     const std::vector<WorldPoint::Ptr>& pointsByIdx() const { return by_idx_; }
+    // every point's last descriptor, 128 bytes each, in index order
+    const std::vector<uint8_t>& descriptorsByIdx() const { return desc_; }
 
    private:
     WorldPoint::Idx cur_idx_ = 0;
@@ -158,6 +176,8 @@ class WorldStructure {
     std::unordered_map<Image::Idx, Image::Ptr> images_;
     std::unordered_map<WorldPoint::Idx, WorldPoint::Ptr> world_points_;
     std::vector<WorldPoint::Ptr> by_idx_;
+    std::vector<uint8_t> desc_;     // [points][128]
+    int64_t n_obs_ = 0;
     template <class> friend class BasicBundleAdjuster;
     friend class GlobalFrame;
 };
