@@ -25,6 +25,35 @@ namespace sfm {
 
 namespace {
 
+// (key, term) entries of the reduce plan's term lists: an aggregate (a
+// std::pair value-initialises), in vectors that default-initialise, so a
+// resize() before the entries are written costs no zero fill
+template <class T>
+struct KeyTerm {
+    int64_t first;
+    T second;
+};
+template <class T>
+struct DefInit : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefInit<U>;
+    };
+    DefInit() = default;
+    template <class U>
+    DefInit(const DefInit<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using KTVec = std::vector<KeyTerm<T>, DefInit<KeyTerm<T>>>;
+
 // Host worker pool for the planner: up to 15 threads started once and parked
 // on a condition variable, so a parallel phase costs a wake-up (tens of us)
 // instead of 15 thread creations.  One caller at a time uses the pool; a
@@ -742,8 +771,17 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             const int32_t s0 = pl.pt_off[k], n = pl.pt_off[k + 1] - s0;
             idx.resize(n);
             std::iota(idx.begin(), idx.end(), 0);
-            std::stable_sort(idx.begin(), idx.end(),
-                             [&](int32_t a, int32_t b) { return pl.obs_img[s0 + a] < pl.obs_img[s0 + b]; });
+            auto before = [&](int32_t a, int32_t b) { return pl.obs_img[s0 + a] < pl.obs_img[s0 + b]; };
+            if (n <= 64) {   // insertion sort: stable, no buffer (stable_sort allocated one per point)
+                for (int32_t q = 1; q < n; ++q) {
+                    const int32_t x = idx[q];
+                    int32_t r = q;
+                    for (; r > 0 && before(x, idx[r - 1]); --r) idx[r] = idx[r - 1];
+                    idx[r] = x;
+                }
+            } else {
+                std::stable_sort(idx.begin(), idx.end(), before);
+            }
             img.assign(pl.obs_img.begin() + s0, pl.obs_img.begin() + s0 + n);
             uv.assign(pl.obs_uv.begin() + 2 * s0, pl.obs_uv.begin() + 2 * (s0 + n));
             for (int32_t q = 0; q < n; ++q) {
@@ -890,8 +928,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     };
     auto col_of_fb = [&](int32_t b) -> int64_t { return b < pl.ncam ? 6LL * b : pl.nb + (int64_t)pl.iw * (b - pl.ncam); };
     auto size_of_fb = [&](int32_t b) { return b < pl.ncam ? 6 : pl.iw; };
-    std::vector<std::pair<int64_t, ReduceTerm>> mterms, vterms;
-    std::vector<std::pair<int64_t, PTerm>> mprod, vprod;
+    KTVec<ReduceTerm> mterms, vterms;
+    KTVec<PTerm> mprod, vprod;
     {
         // exact capacities: one growth-free allocation per list (the lists
         // are fresh memory, so every reallocation is page faults again)
@@ -911,7 +949,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         vprod.reserve(npv);
     }
     // image Gram blocks (kGramSeg partial slices per image)
-    auto add_u = [&](std::vector<std::pair<int64_t, ReduceTerm>>& out, int64_t key, int32_t kind, int img,
+    auto add_u = [&](KTVec<ReduceTerm>& out, int64_t key, int32_t kind, int img,
                      int16_t ro, int16_t co) {
         for (int g = 0; g < kGramSeg; ++g) out.push_back({key, ReduceTerm{kind, img * kGramSeg + g, ro, co, 1.f}});
     };
@@ -934,7 +972,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     }
     tm.mark("terms_images");
     // cnF: per block, image slices only (never a tile term)
-    std::vector<std::pair<int64_t, ReduceTerm>> cterms;
+    KTVec<ReduceTerm> cterms;
     for (const auto& t : vterms) {
         ReduceTerm q = t.second;
         q.kind = kSrcUcn;
@@ -945,7 +983,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     {
         const int32_t nch = (int32_t)pl.chunks.size();
         const int nseg = nch >= 128 ? 16 : 1;   // the output is the same for any split
-        std::vector<std::vector<std::pair<int64_t, ReduceTerm>>> sm(nseg), sv(nseg);
+        std::vector<KTVec<ReduceTerm>> sm(nseg), sv(nseg);
         parallel_segments(nseg, [&](int g) {
             const int32_t c0 = (int32_t)((int64_t)nch * g / nseg), c1 = (int32_t)((int64_t)nch * (g + 1) / nseg);
             for (int32_t c = c0; c < c1; ++c) {
@@ -1016,7 +1054,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         }
         constexpr int kD = 11, kB = 1 << kD;
         const int passes = std::max(1, (bits + kD - 1) / kD);
-        std::vector<E> tmp(v.size());
+        std::decay_t<decltype(v)> tmp(v.size());
         E* src = v.data();
         E* dst = tmp.data();
         const int64_t n = (int64_t)v.size();
@@ -1071,8 +1109,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     pl.terms.reserve(mterms.size() + 2 * vterms.size() + cterms.size());
     pl.pterms.reserve(mprod.size() + vprod.size());
     auto emit = [&](int64_t key, int32_t kind, int64_t dst, int rows, int cols, int ld,
-                    std::vector<std::pair<int64_t, ReduceTerm>>& st, size_t& is,
-                    std::vector<std::pair<int64_t, PTerm>>* pt, size_t* ip) {
+                    KTVec<ReduceTerm>& st, size_t& is,
+                    KTVec<PTerm>* pt, size_t* ip) {
         ReduceTarget t{};
         t.dst = dst; t.dst_kind = kind; t.rows = rows; t.cols = cols; t.ld = ld;
         while (is < st.size() && st[is].first < key) ++is;   // (keys with no target: none by construction)
@@ -1176,7 +1214,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         emit(fb, kDstRhs, col_of_fb(fb), size_of_fb(fb), 1, 1, vterms, iv, &vprod, &ipv);
     {
         // bF: the image slices of vterms only (no tile, no product term)
-        std::vector<std::pair<int64_t, ReduceTerm>> bterms;
+        KTVec<ReduceTerm> bterms;
         for (const auto& t : vterms)
             if (t.second.kind == kSrcUb) bterms.push_back(t);
         size_t ib = 0;

@@ -62,7 +62,7 @@ struct BAHostPlan {
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;
     std::vector<ReduceTerm> terms;
-    std::vector<PTerm> pterms;
+    HostVec<PTerm> pterms;           // uploaded as it is: page-locked staging
     int64_t n_sband = 0, n_sarrow = 0, n_scorner = 0;
     int64_t schur_flops = 0;    // algorithmic flops of one Schur pass
     // called by build_plan once pt_off / obs_img / obs_slot / obs_uv are final

@@ -136,7 +136,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(pl->zlong, h.zlong, s);
     up(pl->pterms, h.pterms, s);
     pl->Zbuf.alloc(std::max<int64_t>(h.n_z, 1));
-    std::vector<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
+    HostVec<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
     for (int64_t k = 0; k < h.n_spt; ++k)
         for (int a = 0; a < 3; ++a) xs[3 * k + a] = X[3 * h.spt_global[k] + a];
     up(pl->X0, xs, s);
@@ -159,8 +159,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
                  o_ucn = o_ub + fw * (size_t)prob.n_img * kGramSeg,
                  n_gram = o_ucn + fw * (size_t)prob.n_img * kGramSeg;
     pl->gram.alloc(n_gram);
+    // page-locked staging (DMA uploads); released after the synchronisation
+    // at the end, like the observation arrays
+    HostVec<FlatTerm> ft(std::max<size_t>(h.terms.size(), 1));
     {
-        std::vector<FlatTerm> ft(std::max<size_t>(h.terms.size(), 1));
         for (const ReduceTarget& T : h.targets) {
             const bool vec = T.cols == 1;
             for (int32_t k = T.c_begin; k < T.c_end; ++k) {
@@ -352,6 +354,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     h.obs_img = HostVec<int32_t>();
     h.obs_slot = HostVec<int32_t>();
     h.obs_uv = HostVec<double>();
+    h.pterms = HostVec<PTerm>();
     tm.mark("sync");
 }
 
