@@ -24,6 +24,7 @@
 
 #include "../../../include/sfmcore.h"
 #include "frames.hpp"
+#include "pool.hpp"
 #include "world.hpp"
 
 namespace sfm {
@@ -132,17 +133,13 @@ class BasicBundleAdjuster {
         // whole call), so no reference counts move.
         const std::vector<WorldPoint::Ptr>& pts = world->pointsByIdx();
         const std::size_t np = pts.size();
-        const int nr = (int)std::max<std::size_t>(
-            1, std::min<std::size_t>({16, std::max(1u, std::thread::hardware_concurrency()), np / 4096}));
+        const int nr = (int)std::max<std::size_t>(1, std::min<std::size_t>(PlanPool::width(), np / 4096));
         std::vector<std::vector<const Image::Ptr*>> first(nr);   // into the world's lists
         points_.resize(np);
         X_.resize(3 * np);
         off_.assign(np + 1, 0);
-        auto ranges = [&](auto&& fn) {
-            std::vector<std::thread> th;
-            for (int r = 1; r < nr; ++r) th.emplace_back([&, r] { fn(r, np * r / nr, np * (r + 1) / nr); });
-            fn(0, 0, np / nr);
-            for (auto& t : th) t.join();
+        auto ranges = [&](auto&& fn) {   // on the worker pool (pool.hpp)
+            pool_ranges((int64_t)np, nr, [&](int64_t k0, int64_t k1, int r) { fn(r, (std::size_t)k0, (std::size_t)k1); });
         };
         constexpr std::size_t kAhead = 8;
         auto prefetch = [&](std::size_t k, std::size_t k1) {
@@ -229,18 +226,13 @@ class BasicBundleAdjuster {
     }
     void update() {  // updateWorld (:143-156)
         const std::size_t np = points_.size();
-        const int nr = (int)std::max<std::size_t>(
-            1, std::min<std::size_t>({16, std::max(1u, std::thread::hardware_concurrency()), np / 4096}));
-        auto range = [&](std::size_t k0, std::size_t k1) {
-            for (std::size_t k = k0; k < k1; ++k) {
+        const int nr = (int)std::max<std::size_t>(1, std::min<std::size_t>(PlanPool::width(), np / 4096));
+        pool_ranges((int64_t)np, nr, [&](int64_t k0, int64_t k1, int) {
+            for (int64_t k = k0; k < k1; ++k) {
                 if (k + 8 < k1) __builtin_prefetch(points_[k + 8], 1);
                 points_[k]->setPos({X_[3 * k], X_[3 * k + 1], X_[3 * k + 2]});
             }
-        };
-        std::vector<std::thread> th;
-        for (int r = 1; r < nr; ++r) th.emplace_back(range, np * r / nr, np * (r + 1) / nr);
-        range(0, np / nr);
-        for (auto& t : th) t.join();
+        });
         for (std::size_t k = 0; k < images_.size(); ++k) {
             std::array<double, 6> p;
             for (int a = 0; a < 6; ++a) p[a] = extr_[6 * k + a];
