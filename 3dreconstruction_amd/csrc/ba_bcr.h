@@ -25,7 +25,10 @@ struct DenseArgs {
     int64_t np = 0;      // padded order nt * 64
     double *A = nullptr, *X = nullptr, *b = nullptr, *y = nullptr, *x = nullptr, *fail = nullptr;
     unsigned* xflag = nullptr;   // [nt] back substitution: x_k published for epoch (dense_back_all_kernel)
+    unsigned* fflag = nullptr;   // [2 nt^2 + nt] dataflow factorisation: L tiles, chain inputs, y (dense_flow_kernel)
 };
+// flag words of a DenseArgs (x flags + the factorisation's), zeroed once at bind
+size_t dense_flag_words(const DenseArgs& d);
 void dense_setup(DenseArgs& d, const DevProblem& P);
 size_t dense_doubles(const DenseArgs& d);
 void dense_bind(DenseArgs& d, double* base);

@@ -1213,6 +1213,254 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
     }
 }
 
+// ---- the whole factorisation + both substitutions in one dataflow launch ----
+// For small dense systems (the C5 loop's: nt <= 29 block columns) the panel /
+// update launch chain is latency bound (a 64-pivot factor per column plus two
+// launches).  Here workgroup 0 runs the diagonal chain -- for k: L_k,k-1 =
+// A~_k,k-1 X_k-1', A_kk -= L_k,k-1 L_k,k-1', factor + invert A_kk -- and every
+// other workgroup owns one task, left-looking:
+//   D(i)     A~_ii    = A_ii    - sum_{m < i-1} L_im L_im'       (for the chain)
+//   S(i)     A~_i,i-1 = A_i,i-1 - sum_{m < i-1} L_im L_i-1,m'    (for the chain)
+//   T(i, j)  L_ij = (A_ij - sum_{m < j} L_im L_jm') X_j'         (i >= j + 2)
+//   Y(j)     y_j = X_j (b_j - sum_{m < j} L_jm y_m)
+//   B(k)     x_k = X_k' (y_k - sum_{i > k} L_ik' x_i)
+// Each accumulates its terms as their inputs are published, in m order.
+// Hand-offs: payload stored write-through (agent-scope stores), every storing
+// wave drains, the workgroup meets, one lane stores the flag; consumers poll
+// relaxed, acquire once per run of ready inputs, then read plainly
+// (cdna_hip_programming.md Guideline 16).  Every workgroup is resident (at
+// most two per CU at this LDS size: checked by the caller) and has its own
+// task, so every wait ends; spins are bounded (a timeout fails the solve).
+constexpr int kDfLds = 2 * M * LD + 32;   // doubles: two tiles + small state
+
+__device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void tile_st_wt(double* C, int ldc, int r0, int c0, v4d v) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st_wt(C + (r0 + kk + 4 * r) * (int64_t)ldc + c0 + i, v[r]);
+}
+// publish: every storing wave drains, the workgroup meets, one lane flags
+__device__ __forceinline__ void df_publish(unsigned* flag, unsigned epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wait until fa[m * sa] (and fb[m * sb], if given) hold epoch for m = m0 and
+// return the end m' <= m1 of the run of ready m from m0 (one acquire for all);
+// every thread gets it (the workgroup meets)
+__device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const unsigned* fb, int sb, int m0, int m1,
+                                           unsigned epoch, double* fail, int* sh) {
+    if (threadIdx.x == 0) {
+        auto ready = [&](int m) {
+            return __hip_atomic_load(fa + (int64_t)m * sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+                   (!fb || __hip_atomic_load(fb + (int64_t)m * sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
+        };
+        unsigned spins = 0;
+        while (!ready(m0)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) {
+                __hip_atomic_store(fail, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        int m = m0 + 1;
+        while (m < m1 && ready(m)) ++m;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *sh = m;
+    }
+    __syncthreads();
+    return *sh;
+}
+
+// number of tasks (helper workgroups) for nt block columns
+__host__ __device__ __forceinline__ int df_tasks(int nt) {
+    int n = 0;
+    for (int j = 0; j < nt; ++j) n += j + 1 < nt ? nt - j + 1 : 1;
+    return n + nt;
+}
+
+__global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem P, unsigned epoch) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* T1 = sm;
+    double* T2 = sm + M * LD;
+    double* bad = T2 + M * LD;     // [2]
+    double* col = bad + 2;         // [16] (diag16)
+    int* sh = reinterpret_cast<int*>(col + 16);
+    const int nt = d.nt, wave = threadIdx.x >> 6;
+    const int64_t np = d.np;
+    unsigned* fL = d.fflag;                 // [nt][nt]: L_ij final (i > j), X_j final (i == j)
+    unsigned* fR = d.fflag + nt * nt;       // [nt][nt]: A~_ii (D), A~_i,i-1 (S) ready for the chain
+    unsigned* fy = d.fflag + 2 * nt * nt;   // [nt]
+    unsigned* fx = d.xflag;                 // [nt]
+    auto tA = [&](int i, int j) { return d.A + (int64_t)i * kDM * np + (int64_t)j * kDM; };
+    // ---------------- the diagonal chain ----------------
+    if (blockIdx.x == 0) {
+        for (int k = 0; k < nt; ++k) {
+            v4d acc[4];
+            if (k > 0) {
+                // L_k,k-1 = A~_k,k-1 X_k-1' (X_k-1 in T2 from the previous step)
+                df_wait_run(fR + k * nt + k - 1, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
+                load_tile<64>(T1, LD, tA(k, k - 1), (int)np);
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tile_st_wt(tA(k, k - 1), (int)np, 16 * wave, 16 * q, acc[q]);
+                df_publish(fL + k * nt + k - 1, epoch);   // (the workgroup met: T2 is free)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tile_st(T2, LD, 16 * wave, 16 * q, acc[q]);
+                df_wait_run(fR + k * nt + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
+                load_tile<64>(T1, LD, tA(k, k), (int)np);
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q > wave) continue;   // lower 16x16 tiles
+                    const v4d a = tile_ld(T1, LD, 16 * wave, 16 * q);
+                    acc[q] = tile_mm<false, true, true>(a, T2, LD, 16 * wave, T2, LD, 16 * q, 0, M);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q <= wave) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
+            } else {
+                load_tile<64>(T1, LD, tA(0, 0), (int)np);
+            }
+            for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
+            if (threadIdx.x == 0) bad[0] = 0.0;
+            __syncthreads();
+            chol_inv64(T1, T2, bad, col);
+            double* xd = d.X + (int64_t)k * kDM * kDM;
+            for (int e = threadIdx.x; e < M * M; e += NT) st_wt(xd + e, T2[(e / M) * LD + e % M]);
+            if (threadIdx.x == 0 && bad[0] != 0.0) st_wt(d.fail, 1.0);
+            df_publish(fL + k * nt + k, epoch);
+        }
+        return;
+    }
+    // ---------------- one task per helper workgroup ----------------
+    int t = blockIdx.x - 1, j = 0;
+    for (; j < nt; ++j) {   // column j's tasks: [D(j+1), S(j+1)] (j + 1 < nt), T(j+2.., j), Y(j)
+        const int c = j + 1 < nt ? nt - j + 1 : 1;
+        if (t < c) break;
+        t -= c;
+    }
+    if (j < nt) {
+        const bool two = j + 1 < nt;
+        const int kind = !two ? 3 : t == 0 ? 0 : t == 1 ? 1 : t < nt - j ? 2 : 3;   // D S T Y
+        if (kind <= 2) {
+            const int i = kind == 2 ? j + t : j + 1, jj = kind == 0 ? j + 1 : j;   // target tile (i, jj)
+            const int mend = j;   // D(j+1), S(j+1): m < j; T(i, j): m < j
+            const bool diag = kind == 0;
+            v4d acc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                acc[q] = (diag && q > wave) ? zero4() : tile_ld(tA(i, jj), (int)np, 16 * wave, 16 * q);
+            for (int m = 0; m < mend;) {
+                const int m1 = df_wait_run(fL + i * nt, 1, diag ? nullptr : fL + jj * nt, 1, m, mend, epoch, d.fail, sh);
+                for (; m < m1; ++m) {
+                    load_tile<64>(T1, LD, tA(i, m), (int)np);
+                    if (!diag) load_tile<64>(T2, LD, tA(jj, m), (int)np);
+                    __syncthreads();
+                    const double* Lb = diag ? T1 : T2;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (diag && q > wave) continue;
+                        acc[q] = tile_mm<false, true, true>(acc[q], T1, LD, 16 * wave, Lb, LD, 16 * q, 0, M);
+                    }
+                    __syncthreads();
+                }
+            }
+            if (kind < 2) {
+                if (mend > 0) {   // (nothing subtracted: the packed tile stands)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (!(diag && q > wave)) tile_st_wt(tA(i, jj), (int)np, 16 * wave, 16 * q, acc[q]);
+                }
+                df_publish(fR + i * nt + jj, epoch);
+                return;
+            }
+            // T: L_ij = A~_ij X_j'
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
+            df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j
+            load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tile_st_wt(tA(i, j), (int)np, 16 * wave, 16 * q, acc[q]);
+            df_publish(fL + i * nt + j, epoch);
+            return;
+        }
+        // Y(j): thread (g, r) sums columns 16 g .. 16 g + 15 of row r of every L_jm
+        const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
+        double s = 0.0;
+        for (int m = 0; m < j;) {
+            const int m1 = df_wait_run(fL + j * nt, 1, fy, 1, m, j, epoch, d.fail, sh);
+            for (; m < m1; ++m) {
+                const double* L = tA(j, m) + (int64_t)r * np + 16 * g;
+                const double* y = d.y + (int64_t)m * kDM + 16 * g;
+#pragma unroll
+                for (int c = 0; c < 16; ++c) s = fma(L[c], y[c], s);
+            }
+        }
+        double* part = T1;   // [4][64]
+        double* v = T1 + 4 * M;
+        part[g * M + r] = s;
+        df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j (the workgroup meets)
+        if (threadIdx.x < M)
+            v[r] = d.b[(int64_t)j * kDM + r] - (((part[r] + part[M + r]) + part[2 * M + r]) + part[3 * M + r]);
+        __syncthreads();
+        if (threadIdx.x < M) {   // y_j = X_j v (X lower: columns c <= r)
+            const double* X = d.X + (int64_t)j * kDM * kDM + (int64_t)r * M;
+            double yv = 0.0;
+            for (int c = 0; c <= r; ++c) yv = fma(X[c], v[c], yv);
+            st_wt(d.y + (int64_t)j * kDM + r, yv);
+        }
+        df_publish(fy + j, epoch);
+        return;
+    }
+    // B(k), k = nt - 1 - t: x_k = X_k' (y_k - sum_{i > k} L_ik' x_i)
+    const int k = nt - 1 - t;
+    if (k < 0) return;
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    double s = 0.0;
+    // inputs i = nt - 1 down to k + 1, i.e. m = nt - 1 - i = 0 .. nt - 2 - k
+    for (int m = 0; m < nt - 1 - k;) {
+        const int m1 = df_wait_run(fx + nt - 1, -1, fL + (int64_t)(nt - 1) * nt + k, -nt, m, nt - 1 - k, epoch,
+                                   d.fail, sh);
+        for (; m < m1; ++m) {
+            const int i = nt - 1 - m;
+            const double* L = tA(i, k) + c;
+            const double* x = d.x + (int64_t)i * kDM;
+#pragma unroll
+            for (int q = 0; q < M / 4; ++q) s = fma(L[(int64_t)(4 * q + g) * np], x[4 * q + g], s);
+        }
+    }
+    double* part = T1;
+    double* v = T1 + 4 * M;
+    part[g * M + c] = s;
+    df_wait_run(fy + k, 0, fL + k * nt + k, 0, 0, 1, epoch, d.fail, sh);   // y_k, X_k
+    if (threadIdx.x < M)
+        v[c] = d.y[(int64_t)k * kDM + c] - (((part[c] + part[M + c]) + part[2 * M + c]) + part[3 * M + c]);
+    __syncthreads();
+    if (threadIdx.x < M) {   // x_k = X_k' v: X lower, rows m >= c
+        const double* X = d.X + (int64_t)k * kDM * kDM;
+        double xv = 0.0;
+        for (int m = c; m < M; ++m) xv = fma(X[(int64_t)m * M + c], v[m], xv);
+        st_wt(d.x + (int64_t)k * kDM + c, xv);
+        const int64_t e = (int64_t)k * kDM + c;
+        if (e < P.nF) P.yF[e] = xv;
+    }
+    df_publish(fx + k, epoch);
+    if (k == 0 && threadIdx.x == 0)   // every other task feeds x_0: the verdict is final
+        P.scal[kScSolveFail] = __hip_atomic_load(d.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 void dense_setup(DenseArgs& d, const DevProblem& P) {
@@ -1220,9 +1468,11 @@ void dense_setup(DenseArgs& d, const DevProblem& P) {
     d.np = (int64_t)d.nt * kDM;
 }
 
+size_t dense_flag_words(const DenseArgs& d) { return (size_t)d.nt + 2 * (size_t)d.nt * d.nt + d.nt; }
+
 size_t dense_doubles(const DenseArgs& d) {
-    // A | X | b y x | fail (8) | x flags (one word per block column)
-    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8 + ((size_t)d.nt + 1) / 2 + 2;
+    // A | X | b y x | fail (8) | flags: x (nt), L tiles + chain inputs (2 nt^2), y (nt)
+    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8 + (dense_flag_words(d) + 1) / 2 + 2;
 }
 
 void dense_bind(DenseArgs& d, double* base) {
@@ -1233,6 +1483,7 @@ void dense_bind(DenseArgs& d, double* base) {
     d.x = d.y + d.np;
     d.fail = d.x + d.np;
     d.xflag = reinterpret_cast<unsigned*>(d.fail + 8);   // zeroed by the caller once
+    d.fflag = d.xflag + d.nt;
 }
 
 void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
@@ -1247,6 +1498,27 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         SFM_HIP(hipFuncSetAttribute((const void*)dense_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds_u));
         attr = true;
+    }
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        SFM_HIP(hipGetDevice(&dev));
+        SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    static const bool flow_off = std::getenv("SFM_DENSE_LAUNCHES") != nullptr;
+    if (!flow_off && 1 + df_tasks(d.nt) <= 2 * n_cu) {
+        // small system: factorisation and both substitutions in one dataflow
+        // launch, every workgroup resident (two per CU at this LDS size)
+        const size_t lds_f = kDfLds * sizeof(double);
+        static bool attr_f = false;
+        if (!attr_f) {
+            SFM_HIP(hipFuncSetAttribute((const void*)dense_flow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds_f));
+            attr_f = true;
+        }
+        hipLaunchKernelGGL(dense_flow_kernel, dim3(1 + df_tasks(d.nt)), dim3(NT), lds_f, s, d, P, epoch);
+        SFM_HIP(hipGetLastError());
+        return;
     }
     // block columns in groups of W = SFM_DENSE_W: panel c, then the group's
     // later columns updated from column c alone (rhs of column c fused), ...;
@@ -1273,12 +1545,6 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
                                k + w - 1);
             SFM_HIP(hipGetLastError());
         }
-    }
-    static int n_cu = 0;
-    if (!n_cu) {
-        int dev = 0;
-        SFM_HIP(hipGetDevice(&dev));
-        SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     }
     if (d.nt <= n_cu && !std::getenv("SFM_DENSE_BACK_LAUNCHES")) {
         // one workgroup per block column, all resident: more than half a CU's

@@ -334,7 +334,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         dense_setup(pl->dense, P);
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
-        SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * (size_t)pl->dense.nt, s));
+        SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * dense_flag_words(pl->dense), s));
     }
     if (pl->use_bcr) {
         bcr_setup(pl->bcr, P);
