@@ -218,9 +218,17 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
     __builtin_amdgcn_s_setprio(2);
     const int lane = threadIdx.x & 63, i = lane;
     const bool act = lane < 16;
+    // every caller's A and X are LDS tiles: address them as such (ds_* instead
+    // of flat accesses, which wait on both counters), and load every row
+    // unconditionally (lane i & 15), masking after, instead of 16 branches
+    typedef __attribute__((address_space(3))) double lds_f64;
+    lds_f64* const Al = (lds_f64*)A;
+    lds_f64* const Xl = (lds_f64*)X;
     double a[16], x[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? A[i * LD + j] : 0.0;
+    for (int j = 0; j < 16; ++j) a[j] = Al[(i & 15) * LD + j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? a[j] : 0.0;
     diag16_step<0>(a, x, i);
     double lii = 1.0;   // this lane's L_ii (a[i], extracted without dynamic indexing)
 #pragma unroll
@@ -228,9 +236,9 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
     if (__ballot(act && !(lii > 0.0)) != 0 && lane == 0) bad[0] = 1.0;
     if (act) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) A[i * LD + j] = j <= i ? a[j] : 0.0;
+        for (int j = 0; j < 16; ++j) Al[i * LD + j] = j <= i ? a[j] : 0.0;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) X[m * LD + i] = x[m];
+        for (int m = 0; m < 16; ++m) Xl[m * LD + i] = x[m];
     }
     __builtin_amdgcn_s_setprio(0);
 }
@@ -262,13 +270,18 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
                            unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN(),
                            Bg bg = Bg()) {
     const int wave = threadIdx.x >> 6;
-    unsigned long long t0 = 0, td = 0, ta = 0;
+    unsigned long long t0 = 0, td = 0, ta = 0, tq = 0, tb = 0;
     if (st) t0 = stamp();
     if (wave == 0) {
         pre0();
         wave_sync();
+        if (st) tb = stamp();
         diag16(A, X, bad, col);
-        if (st) td += stamp() - t0;
+        if (st) {
+            const unsigned long long te = stamp();
+            td += te - t0;
+            tq += te - tb;
+        }
     } else {
         preN();
     }
@@ -296,8 +309,13 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
             acc = tile_mm<false, true, true>(acc, A, LD, 16 * n, A, LD, 16 * n, 16 * k, 16 * k + 16);
             tile_st(A, LD, 16 * n, 16 * n, acc);
             wave_sync();
+            if (st) tb = stamp();
             diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
-            if (st) td += stamp() - ta;
+            if (st) {
+                const unsigned long long te = stamp();
+                td += te - ta;
+                tq += te - tb;
+            }
         } else {
             // items: trailing tiles (i, j), n <= j <= i < 4, (i, j) != (n, n);
             // then T_nj, j < n
@@ -322,6 +340,7 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
     if (st && threadIdx.x == 0) {
         atomicAdd(st + 0, td);
         atomicAdd(st + 1, stamp() - t0);
+        atomicAdd(st + 7, tq);
     }
 }
 
@@ -1228,9 +1247,10 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
 // Hand-offs: payload stored write-through (agent-scope stores), every storing
 // wave drains, the workgroup meets, one lane stores the flag; consumers poll
 // relaxed, acquire once per run of ready inputs, then read plainly
-// (cdna_hip_programming.md Guideline 16).  Every workgroup is resident (at
-// most two per CU at this LDS size: checked by the caller) and has its own
-// task, so every wait ends; spins are bounded (a timeout fails the solve).
+// (cdna_hip_programming.md Guideline 16).  Every workgroup is resident (one
+// per CU, at most n_cu: the caller) and the task workers take tasks round
+// robin in an order where every input comes from a lower task or the chain,
+// so every wait ends; spins are bounded (a timeout fails the solve).
 constexpr int kDfLds = 2 * M * LD + 32;   // doubles: two tiles + small state
 
 __device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
@@ -1340,125 +1360,135 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         }
         return;
     }
-    // ---------------- one task per helper workgroup ----------------
-    int t = blockIdx.x - 1, j = 0;
-    for (; j < nt; ++j) {   // column j's tasks: [D(j+1), S(j+1)] (j + 1 < nt), T(j+2.., j), Y(j)
-        const int c = j + 1 < nt ? nt - j + 1 : 1;
-        if (t < c) break;
-        t -= c;
-    }
-    if (j < nt) {
-        const bool two = j + 1 < nt;
-        const int kind = !two ? 3 : t == 0 ? 0 : t == 1 ? 1 : t < nt - j ? 2 : 3;   // D S T Y
-        if (kind <= 2) {
-            const int i = kind == 2 ? j + t : j + 1, jj = kind == 0 ? j + 1 : j;   // target tile (i, jj)
-            const int mend = j;   // D(j+1), S(j+1): m < j; T(i, j): m < j
-            const bool diag = kind == 0;
-            v4d acc[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                acc[q] = (diag && q > wave) ? zero4() : tile_ld(tA(i, jj), (int)np, 16 * wave, 16 * q);
-            for (int m = 0; m < mend;) {
-                const int m1 = df_wait_run(fL + i * nt, 1, diag ? nullptr : fL + jj * nt, 1, m, mend, epoch, d.fail, sh);
-                for (; m < m1; ++m) {
-                    load_tile<64>(T1, LD, tA(i, m), (int)np);
-                    if (!diag) load_tile<64>(T2, LD, tA(jj, m), (int)np);
-                    __syncthreads();
-                    const double* Lb = diag ? T1 : T2;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (diag && q > wave) continue;
-                        acc[q] = tile_mm<false, true, true>(acc[q], T1, LD, 16 * wave, Lb, LD, 16 * q, 0, M);
+    // ---------------- tasks: round robin over the helper workgroups ----------------
+    // (every task waits only on tasks of lower index and on the chain, so the
+    // lowest unfinished task can always run: its worker has finished the ones
+    // before it)
+    auto task = [&](int t) {
+        int j = 0;
+        for (; j < nt; ++j) {   // column j's tasks: [D(j+1), S(j+1)] (j + 1 < nt), T(j+2.., j), Y(j)
+            const int c = j + 1 < nt ? nt - j + 1 : 1;
+            if (t < c) break;
+            t -= c;
+        }
+        if (j < nt) {
+            const bool two = j + 1 < nt;
+            const int kind = !two ? 3 : t == 0 ? 0 : t == 1 ? 1 : t < nt - j ? 2 : 3;   // D S T Y
+            if (kind <= 2) {
+                const int i = kind == 2 ? j + t : j + 1, jj = kind == 0 ? j + 1 : j;   // target tile (i, jj)
+                const int mend = j;   // D(j+1), S(j+1): m < j; T(i, j): m < j
+                const bool diag = kind == 0;
+                v4d acc[4];
+    #pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[q] = (diag && q > wave) ? zero4() : tile_ld(tA(i, jj), (int)np, 16 * wave, 16 * q);
+                for (int m = 0; m < mend;) {
+                    const int m1 = df_wait_run(fL + i * nt, 1, diag ? nullptr : fL + jj * nt, 1, m, mend, epoch, d.fail, sh);
+                    for (; m < m1; ++m) {
+                        load_tile<64>(T1, LD, tA(i, m), (int)np);
+                        if (!diag) load_tile<64>(T2, LD, tA(jj, m), (int)np);
+                        __syncthreads();
+                        const double* Lb = diag ? T1 : T2;
+    #pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            if (diag && q > wave) continue;
+                            acc[q] = tile_mm<false, true, true>(acc[q], T1, LD, 16 * wave, Lb, LD, 16 * q, 0, M);
+                        }
+                        __syncthreads();
                     }
-                    __syncthreads();
                 }
-            }
-            if (kind < 2) {
-                if (mend > 0) {   // (nothing subtracted: the packed tile stands)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (!(diag && q > wave)) tile_st_wt(tA(i, jj), (int)np, 16 * wave, 16 * q, acc[q]);
+                if (kind < 2) {
+                    if (mend > 0) {   // (nothing subtracted: the packed tile stands)
+    #pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (!(diag && q > wave)) tile_st_wt(tA(i, jj), (int)np, 16 * wave, 16 * q, acc[q]);
+                    }
+                    df_publish(fR + i * nt + jj, epoch);
+                    return;
                 }
-                df_publish(fR + i * nt + jj, epoch);
+                // T: L_ij = A~_ij X_j'
+    #pragma unroll
+                for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
+                df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j
+                load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
+                __syncthreads();
+    #pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
+    #pragma unroll
+                for (int q = 0; q < 4; ++q) tile_st_wt(tA(i, j), (int)np, 16 * wave, 16 * q, acc[q]);
+                df_publish(fL + i * nt + j, epoch);
                 return;
             }
-            // T: L_ij = A~_ij X_j'
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
-            df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j
-            load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
+            // Y(j): thread (g, r) sums columns 16 g .. 16 g + 15 of row r of every L_jm
+            const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
+            double s = 0.0;
+            for (int m = 0; m < j;) {
+                const int m1 = df_wait_run(fL + j * nt, 1, fy, 1, m, j, epoch, d.fail, sh);
+                for (; m < m1; ++m) {
+                    const double* L = tA(j, m) + (int64_t)r * np + 16 * g;
+                    const double* y = d.y + (int64_t)m * kDM + 16 * g;
+    #pragma unroll
+                    for (int c = 0; c < 16; ++c) s = fma(L[c], y[c], s);
+                }
+            }
+            double* part = T1;   // [4][64]
+            double* v = T1 + 4 * M;
+            part[g * M + r] = s;
+            df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j (the workgroup meets)
+            if (threadIdx.x < M)
+                v[r] = d.b[(int64_t)j * kDM + r] - (((part[r] + part[M + r]) + part[2 * M + r]) + part[3 * M + r]);
             __syncthreads();
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tile_st_wt(tA(i, j), (int)np, 16 * wave, 16 * q, acc[q]);
-            df_publish(fL + i * nt + j, epoch);
+            if (threadIdx.x < M) {   // y_j = X_j v (X lower: columns c <= r)
+                const double* X = d.X + (int64_t)j * kDM * kDM + (int64_t)r * M;
+                double yv = 0.0;
+                for (int c = 0; c <= r; ++c) yv = fma(X[c], v[c], yv);
+                st_wt(d.y + (int64_t)j * kDM + r, yv);
+            }
+            df_publish(fy + j, epoch);
             return;
         }
-        // Y(j): thread (g, r) sums columns 16 g .. 16 g + 15 of row r of every L_jm
-        const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
+        // B(k), k = nt - 1 - t: x_k = X_k' (y_k - sum_{i > k} L_ik' x_i)
+        const int k = nt - 1 - t;
+        if (k < 0) return;
+        const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
         double s = 0.0;
-        for (int m = 0; m < j;) {
-            const int m1 = df_wait_run(fL + j * nt, 1, fy, 1, m, j, epoch, d.fail, sh);
+        // inputs i = nt - 1 down to k + 1, i.e. m = nt - 1 - i = 0 .. nt - 2 - k
+        for (int m = 0; m < nt - 1 - k;) {
+            const int m1 = df_wait_run(fx + nt - 1, -1, fL + (int64_t)(nt - 1) * nt + k, -nt, m, nt - 1 - k, epoch,
+                                       d.fail, sh);
             for (; m < m1; ++m) {
-                const double* L = tA(j, m) + (int64_t)r * np + 16 * g;
-                const double* y = d.y + (int64_t)m * kDM + 16 * g;
-#pragma unroll
-                for (int c = 0; c < 16; ++c) s = fma(L[c], y[c], s);
+                const int i = nt - 1 - m;
+                const double* L = tA(i, k) + c;
+                const double* x = d.x + (int64_t)i * kDM;
+    #pragma unroll
+                for (int q = 0; q < M / 4; ++q) s = fma(L[(int64_t)(4 * q + g) * np], x[4 * q + g], s);
             }
         }
-        double* part = T1;   // [4][64]
+        double* part = T1;
         double* v = T1 + 4 * M;
-        part[g * M + r] = s;
-        df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j (the workgroup meets)
+        part[g * M + c] = s;
+        df_wait_run(fy + k, 0, fL + k * nt + k, 0, 0, 1, epoch, d.fail, sh);   // y_k, X_k
         if (threadIdx.x < M)
-            v[r] = d.b[(int64_t)j * kDM + r] - (((part[r] + part[M + r]) + part[2 * M + r]) + part[3 * M + r]);
+            v[c] = d.y[(int64_t)k * kDM + c] - (((part[c] + part[M + c]) + part[2 * M + c]) + part[3 * M + c]);
         __syncthreads();
-        if (threadIdx.x < M) {   // y_j = X_j v (X lower: columns c <= r)
-            const double* X = d.X + (int64_t)j * kDM * kDM + (int64_t)r * M;
-            double yv = 0.0;
-            for (int c = 0; c <= r; ++c) yv = fma(X[c], v[c], yv);
-            st_wt(d.y + (int64_t)j * kDM + r, yv);
+        if (threadIdx.x < M) {   // x_k = X_k' v: X lower, rows m >= c
+            const double* X = d.X + (int64_t)k * kDM * kDM;
+            double xv = 0.0;
+            for (int m = c; m < M; ++m) xv = fma(X[(int64_t)m * M + c], v[m], xv);
+            st_wt(d.x + (int64_t)k * kDM + c, xv);
+            const int64_t e = (int64_t)k * kDM + c;
+            if (e < P.nF) P.yF[e] = xv;
         }
-        df_publish(fy + j, epoch);
-        return;
+        df_publish(fx + k, epoch);
+        if (k == 0 && threadIdx.x == 0)   // every other task feeds x_0: the verdict is final
+            P.scal[kScSolveFail] = __hip_atomic_load(d.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const int ntask = df_tasks(nt);
+    for (int t = blockIdx.x - 1; t < ntask; t += gridDim.x - 1) {
+        __syncthreads();   // the previous task is done with the LDS tiles
+        task(t);
     }
-    // B(k), k = nt - 1 - t: x_k = X_k' (y_k - sum_{i > k} L_ik' x_i)
-    const int k = nt - 1 - t;
-    if (k < 0) return;
-    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    double s = 0.0;
-    // inputs i = nt - 1 down to k + 1, i.e. m = nt - 1 - i = 0 .. nt - 2 - k
-    for (int m = 0; m < nt - 1 - k;) {
-        const int m1 = df_wait_run(fx + nt - 1, -1, fL + (int64_t)(nt - 1) * nt + k, -nt, m, nt - 1 - k, epoch,
-                                   d.fail, sh);
-        for (; m < m1; ++m) {
-            const int i = nt - 1 - m;
-            const double* L = tA(i, k) + c;
-            const double* x = d.x + (int64_t)i * kDM;
-#pragma unroll
-            for (int q = 0; q < M / 4; ++q) s = fma(L[(int64_t)(4 * q + g) * np], x[4 * q + g], s);
-        }
-    }
-    double* part = T1;
-    double* v = T1 + 4 * M;
-    part[g * M + c] = s;
-    df_wait_run(fy + k, 0, fL + k * nt + k, 0, 0, 1, epoch, d.fail, sh);   // y_k, X_k
-    if (threadIdx.x < M)
-        v[c] = d.y[(int64_t)k * kDM + c] - (((part[c] + part[M + c]) + part[2 * M + c]) + part[3 * M + c]);
-    __syncthreads();
-    if (threadIdx.x < M) {   // x_k = X_k' v: X lower, rows m >= c
-        const double* X = d.X + (int64_t)k * kDM * kDM;
-        double xv = 0.0;
-        for (int m = c; m < M; ++m) xv = fma(X[(int64_t)m * M + c], v[m], xv);
-        st_wt(d.x + (int64_t)k * kDM + c, xv);
-        const int64_t e = (int64_t)k * kDM + c;
-        if (e < P.nF) P.yF[e] = xv;
-    }
-    df_publish(fx + k, epoch);
-    if (k == 0 && threadIdx.x == 0)   // every other task feeds x_0: the verdict is final
-        P.scal[kScSolveFail] = __hip_atomic_load(d.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -1506,17 +1536,26 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     }
     static const bool flow_off = std::getenv("SFM_DENSE_LAUNCHES") != nullptr;
-    if (!flow_off && 1 + df_tasks(d.nt) <= 2 * n_cu) {
-        // small system: factorisation and both substitutions in one dataflow
-        // launch, every workgroup resident (two per CU at this LDS size)
-        const size_t lds_f = kDfLds * sizeof(double);
+    static const int flow_max_nt = [] {
+        const char* e = std::getenv("SFM_DENSE_FLOW_MAX_NT");
+        return e ? std::atoi(e) : 29;
+    }();
+    if (!flow_off && d.nt <= flow_max_nt) {
+        // factorisation and both substitutions in one dataflow launch: the
+        // chain workgroup and up to n_cu - 1 task workers, one workgroup per CU
+        // (the LDS request forces it): the chain's pivot wave must not share
+        // its SIMD with another workgroup's fp64 MFMAs, which stall its fp64
+        // VALU (15x in tools/probe/diag16_probe.hip), and every workgroup is
+        // resident, so every wait ends
+        const size_t lds_f = std::max<size_t>(kDfLds * sizeof(double), 81 * 1024);
         static bool attr_f = false;
         if (!attr_f) {
             SFM_HIP(hipFuncSetAttribute((const void*)dense_flow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)lds_f));
             attr_f = true;
         }
-        hipLaunchKernelGGL(dense_flow_kernel, dim3(1 + df_tasks(d.nt)), dim3(NT), lds_f, s, d, P, epoch);
+        const int workers = std::min(df_tasks(d.nt), n_cu - 1);
+        hipLaunchKernelGGL(dense_flow_kernel, dim3(1 + workers), dim3(NT), lds_f, s, d, P, epoch);
         SFM_HIP(hipGetLastError());
         return;
     }

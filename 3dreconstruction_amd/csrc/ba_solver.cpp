@@ -342,7 +342,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         bcr_bind(pl->bcr, pl->bcr_buf.p);
         SFM_HIP(hipMemsetAsync(pl->bcr.yflag, 0, sizeof(unsigned) * (size_t)pl->bcr.N, s));
         if (std::getenv("SFM_BCR_STAMPS")) {
-            pl->bcr_stamps.alloc(7);
+            pl->bcr_stamps.alloc(8);
             pl->bcr_stamps.zero(s);
             pl->bcr.stamps = pl->bcr_stamps.p;
         }
@@ -614,12 +614,12 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         term = finalize(cur, prev_gmax);
     }
     if (pl->bcr.stamps) {  // diagnostic: average cycles per odd block, all levels
-        unsigned long long st[7];
+        unsigned long long st[8];
         SFM_HIP(hipMemcpy(st, pl->bcr.stamps, sizeof st, hipMemcpyDeviceToHost));
         const double n = st[4] ? (double)st[4] : 1.0;
-        std::fprintf(stderr, "[bcr stamps] cycles/odd block: loads %.0f load+update %.0f chol %.0f (diag16 %.0f) "
-                     "to X copy %.0f total %.0f over %llu\n",
-                     st[5] / n, st[2] / n, st[1] / n, st[0] / n, st[6] / n, st[3] / n, st[4]);
+        std::fprintf(stderr, "[bcr stamps] cycles/odd block: loads %.0f load+update %.0f chol %.0f (diag16 %.0f, "
+                     "pivots alone %.0f) to X copy %.0f total %.0f over %llu\n",
+                     st[5] / n, st[2] / n, st[1] / n, st[0] / n, st[7] / n, st[6] / n, st[3] / n, st[4]);
     }
     if (pl->stamps.p) {  // diagnostic: average phase cycles per chunk (last Schur launch)
         std::vector<unsigned long long> st(pl->stamps.n);

@@ -14,3 +14,4 @@ for v in flow launches; do
 done
 unset SFM_DENSE_LAUNCHES
 timeout -k 10 300 python -u tools/dense_prof.py 2>&1 | grep "dense-S"
+SFM_DENSE_FLOW_MAX_NT=1000 timeout -k 10 300 python -u tools/dense_prof.py 2>&1 | grep "dense-S" | sed 's/^/flow all nt: /'
