@@ -128,6 +128,27 @@ __device__ __forceinline__ void load_tile(double* dst, int ld_dst, const double*
         }
     }
 }
+// two 64x64 global tiles -> LDS [64][LD], every load of both in flight before
+// the first LDS store (one memory latency instead of two)
+__device__ __forceinline__ void load_tiles2(double* d1, const double* __restrict__ s1, double* d2,
+                                            const double* __restrict__ s2, int ld_src) {
+    constexpr int n2 = M * M / 2, per = n2 / NT;
+    double2 v[2 * per];
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        const int e = threadIdx.x + q * NT, r = e / (M / 2), c = 2 * (e % (M / 2));
+        v[q] = *reinterpret_cast<const double2*>(s1 + r * ld_src + c);
+        v[per + q] = *reinterpret_cast<const double2*>(s2 + r * ld_src + c);
+    }
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+        const int e = threadIdx.x + q * NT, r = e / (M / 2), c = 2 * (e % (M / 2));
+        d1[r * LD + c] = v[q].x;
+        d1[r * LD + c + 1] = v[q].y;
+        d2[r * LD + c] = v[per + q].x;
+        d2[r * LD + c + 1] = v[per + q].y;
+    }
+}
 template <int TH = NT>
 __device__ __forceinline__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src, int nc) {
     if (nc == 64) load_tile<64, M, TH>(dst, ld_dst, src, ld_src);
@@ -211,7 +232,7 @@ __device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], in
     if constexpr (K < 15) diag16_step<K + 1>(a, x, i);
 }
 
-__device__ void diag16(double* A, double* X, double* bad, double* col) {
+__device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, double* col) {
     (void)col;
     // the critical path of the factorisation: ahead of the co-resident helper
     // waves (trailing tiles, background products) in VALU issue arbitration
@@ -243,6 +264,11 @@ __device__ void diag16(double* A, double* X, double* bad, double* col) {
     __builtin_amdgcn_s_setprio(0);
 }
 
+// called (BCR level / top kernels: inlined there it costs the helper waves'
+// registers, 47 spilled VGPRs) or inlined (the dense kernels: 6 % faster
+// factor, no spills)
+__device__ __noinline__ void diag16(double* A, double* X, double* bad, double* col) { diag16_body(A, X, bad, col); }
+
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
 // the caller).  All 256 threads; ends synchronised.
 //
@@ -265,7 +291,7 @@ struct NoPre {
 struct NoBg {
     __device__ void operator()(int) const {}
 };
-template <int NW = NT / 64, class Pre0 = NoPre, class PreN = NoPre, class Bg = NoBg>
+template <int NW = NT / 64, class Pre0 = NoPre, class PreN = NoPre, class Bg = NoBg, bool INL = false>
 __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
                            unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN(),
                            Bg bg = Bg()) {
@@ -276,7 +302,8 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
         pre0();
         wave_sync();
         if (st) tb = stamp();
-        diag16(A, X, bad, col);
+        if constexpr (INL) diag16_body(A, X, bad, col);
+        else diag16(A, X, bad, col);
         if (st) {
             const unsigned long long te = stamp();
             td += te - t0;
@@ -310,7 +337,8 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
             tile_st(A, LD, 16 * n, 16 * n, acc);
             wave_sync();
             if (st) tb = stamp();
-            diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+            if constexpr (INL) diag16_body(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+            else diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
             if (st) {
                 const unsigned long long te = stamp();
                 td += te - ta;
@@ -1015,7 +1043,7 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
     if (threadIdx.x == 0) flag[0] = 0.0;
     if (i > k) load_tile<64>(Aik, LD, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
     __syncthreads();
-    chol_inv64(Akk, Xkk, flag, flag + 1);
+    chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(Akk, Xkk, flag, flag + 1);
     const int wave = threadIdx.x >> 6;
     if (i == k) {
         double* dst = d.A + (int64_t)k * kDM * np + (int64_t)k * kDM;
@@ -1251,7 +1279,7 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
 // per CU, at most n_cu: the caller) and the task workers take tasks round
 // robin in an order where every input comes from a lower task or the chain,
 // so every wait ends; spins are bounded (a timeout fails the solve).
-constexpr int kDfLds = 2 * M * LD + 32;   // doubles: two tiles + small state
+constexpr int kDfLds = 3 * M * LD + 32;   // doubles: three tiles + small state
 
 __device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1306,7 +1334,8 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* T1 = sm;
     double* T2 = sm + M * LD;
-    double* bad = T2 + M * LD;     // [2]
+    double* T3 = T2 + M * LD;      // the chain's diagonal tile
+    double* bad = T3 + M * LD;     // [2]
     double* col = bad + 2;         // [16] (diag16)
     int* sh = reinterpret_cast<int*>(col + 16);
     const int nt = d.nt, wave = threadIdx.x >> 6;
@@ -1318,45 +1347,62 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
     auto tA = [&](int i, int j) { return d.A + (int64_t)i * kDM * np + (int64_t)j * kDM; };
     // ---------------- the diagonal chain ----------------
     if (blockIdx.x == 0) {
+        unsigned long long ts[7] = {0, 0, 0, 0, 0, 0, 0}, tp = 0;
+        const bool stm = d.stamps != nullptr;
+        auto mark = [&](int ph) {
+            if (stm) {
+                const unsigned long long tn = stamp();
+                ts[ph] += tn - tp;
+                tp = tn;
+            }
+        };
+        if (stm) tp = stamp();
         for (int k = 0; k < nt; ++k) {
-            v4d acc[4];
+            // T2 holds X_k-1; A~_k,k-1 goes to T1 and A~_kk to T3, loaded together
             if (k > 0) {
-                // L_k,k-1 = A~_k,k-1 X_k-1' (X_k-1 in T2 from the previous step)
-                df_wait_run(fR + k * nt + k - 1, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
-                load_tile<64>(T1, LD, tA(k, k - 1), (int)np);
+                df_wait_run(fR + k * nt + k - 1, 0, fR + k * nt + k, 0, 0, 1, epoch, d.fail, sh);   // S(k), D(k)
+                mark(0);
+                load_tiles2(T1, tA(k, k - 1), T3, tA(k, k), (int)np);
                 __syncthreads();
+                // L_k,k-1 = A~_k,k-1 X_k-1'
+                v4d acc[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) tile_st_wt(tA(k, k - 1), (int)np, 16 * wave, 16 * q, acc[q]);
-                df_publish(fL + k * nt + k - 1, epoch);   // (the workgroup met: T2 is free)
+                df_publish(fL + k * nt + k - 1, epoch);   // (the workgroup met: T1 and T2 are free)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) tile_st(T2, LD, 16 * wave, 16 * q, acc[q]);
-                df_wait_run(fR + k * nt + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
-                load_tile<64>(T1, LD, tA(k, k), (int)np);
+                for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
+                for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
+                mark(1);
                 __syncthreads();
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (q > wave) continue;   // lower 16x16 tiles
-                    const v4d a = tile_ld(T1, LD, 16 * wave, 16 * q);
-                    acc[q] = tile_mm<false, true, true>(a, T2, LD, 16 * wave, T2, LD, 16 * q, 0, M);
+                // A~_kk -= L L': the 10 lower 16x16 tiles round robin over the waves
+                for (int q = wave; q < 10; q += NT / 64) {
+                    const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
+                    const int tj = q - ti * (ti + 1) / 2;
+                    const v4d a = tile_ld(T3, LD, 16 * ti, 16 * tj);
+                    tile_st(T3, LD, 16 * ti, 16 * tj, tile_mm<false, true, true>(a, T1, LD, 16 * ti, T1, LD, 16 * tj, 0, M));
                 }
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (q <= wave) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
+                mark(2);
             } else {
-                load_tile<64>(T1, LD, tA(0, 0), (int)np);
+                load_tile<64>(T3, LD, tA(0, 0), (int)np);
+                for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
             }
-            for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
             if (threadIdx.x == 0) bad[0] = 0.0;
             __syncthreads();
-            chol_inv64(T1, T2, bad, col);
+            mark(3);
+            chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(T3, T2, bad, col, stm ? d.stamps + 8 : nullptr);
+            mark(4);
             double* xd = d.X + (int64_t)k * kDM * kDM;
             for (int e = threadIdx.x; e < M * M; e += NT) st_wt(xd + e, T2[(e / M) * LD + e % M]);
             if (threadIdx.x == 0 && bad[0] != 0.0) st_wt(d.fail, 1.0);
             df_publish(fL + k * nt + k, epoch);
+            mark(5);
+        }
+        if (stm && threadIdx.x == 0) {
+            for (int q = 0; q < 6; ++q) atomicAdd(d.stamps + q, ts[q]);
+            atomicAdd(d.stamps + 6, (unsigned long long)nt);
         }
         return;
     }

@@ -335,6 +335,11 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
         SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * dense_flag_words(pl->dense), s));
+        if (std::getenv("SFM_DENSE_STAMPS")) {
+            pl->bcr_stamps.alloc(16);
+            pl->bcr_stamps.zero(s);
+            pl->dense.stamps = pl->bcr_stamps.p;
+        }
     }
     if (pl->use_bcr) {
         bcr_setup(pl->bcr, P);
@@ -620,6 +625,14 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         std::fprintf(stderr, "[bcr stamps] cycles/odd block: loads %.0f load+update %.0f chol %.0f (diag16 %.0f, "
                      "pivots alone %.0f) to X copy %.0f total %.0f over %llu\n",
                      st[5] / n, st[2] / n, st[1] / n, st[0] / n, st[7] / n, st[6] / n, st[3] / n, st[4]);
+    }
+    if (pl->dense.stamps) {  // diagnostic: dataflow chain, average cycles per block column
+        unsigned long long st[16];
+        SFM_HIP(hipMemcpy(st, pl->dense.stamps, sizeof st, hipMemcpyDeviceToHost));
+        const double n = st[6] ? (double)st[6] : 1.0;
+        std::fprintf(stderr, "[dense stamps] cycles/column: wait S %.0f  L %.0f  wait D %.0f  update %.0f  "
+                     "factor %.0f (diag16 + updates %.0f, pivots %.0f)  X out %.0f  over %llu columns\n",
+                     st[0] / n, st[1] / n, st[2] / n, st[3] / n, st[4] / n, st[8] / n, st[15] / n, st[5] / n, st[6]);
     }
     if (pl->stamps.p) {  // diagnostic: average phase cycles per chunk (last Schur launch)
         std::vector<unsigned long long> st(pl->stamps.n);
