@@ -1295,6 +1295,14 @@ __device__ __forceinline__ void df_publish(unsigned* flag, unsigned epoch) {
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void df_publish2(unsigned* f1, unsigned* f2, unsigned epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(f1, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(f2, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 // wait until fa[m * sa] (and fb[m * sb], if given) hold epoch for m = m0 and
 // return the end m' <= m1 of the run of ready m from m0 (one acquire for all);
 // every thread gets it (the workgroup meets)
@@ -1356,6 +1364,12 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                 tp = tn;
             }
         };
+        // X_k (in T2) to global, write-through; the factor's verdict with it
+        auto x_out = [&](int k) {
+            double* xd = d.X + (int64_t)k * kDM * kDM;
+            for (int e = threadIdx.x; e < M * M; e += NT) st_wt(xd + e, T2[(e / M) * LD + e % M]);
+            if (threadIdx.x == 0 && bad[0] != 0.0) st_wt(d.fail, 1.0);
+        };
         if (stm) tp = stamp();
         for (int k = 0; k < nt; ++k) {
             // T2 holds X_k-1; A~_k,k-1 goes to T1 and A~_kk to T3, loaded together
@@ -1371,7 +1385,10 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                     acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) tile_st_wt(tA(k, k - 1), (int)np, 16 * wave, 16 * q, acc[q]);
-                df_publish(fL + k * nt + k - 1, epoch);   // (the workgroup met: T1 and T2 are free)
+                // X_k-1 goes out with L_k,k-1 (one drain and barrier for both;
+                // the next factor does not wait for it)
+                x_out(k - 1);
+                df_publish2(fL + k * nt + k - 1, fL + (k - 1) * nt + k - 1, epoch);   // (T1, T2 are free)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
                 for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
@@ -1394,12 +1411,10 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             mark(3);
             chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(T3, T2, bad, col, stm ? d.stamps + 8 : nullptr);
             mark(4);
-            double* xd = d.X + (int64_t)k * kDM * kDM;
-            for (int e = threadIdx.x; e < M * M; e += NT) st_wt(xd + e, T2[(e / M) * LD + e % M]);
-            if (threadIdx.x == 0 && bad[0] != 0.0) st_wt(d.fail, 1.0);
-            df_publish(fL + k * nt + k, epoch);
-            mark(5);
         }
+        x_out(nt - 1);
+        df_publish(fL + (nt - 1) * nt + nt - 1, epoch);
+        mark(5);
         if (stm && threadIdx.x == 0) {
             for (int q = 0; q < 6; ++q) atomicAdd(d.stamps + q, ts[q]);
             atomicAdd(d.stamps + 6, (unsigned long long)nt);
