@@ -22,6 +22,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 #include "ba_bcr.h"
@@ -128,6 +129,32 @@ __device__ __forceinline__ void load_tile(double* dst, int ld_dst, const double*
         }
     }
 }
+// a tile's global -> LDS copy split in two: fetch (every 16-byte load of the
+// thread issued) and put (LDS stores), so several tiles' loads can be in flight
+// together -- one memory latency for all of them instead of one per tile
+template <int NC, int R = M, int TH = NT>
+struct TileFetch {
+    static constexpr int n2 = R * NC / 2, per = (n2 + TH - 1) / TH;
+    double2 v[per];
+    __device__ __forceinline__ void fetch(const double* __restrict__ src, int ld_src) {
+#pragma unroll
+        for (int q = 0; q < per; ++q) {
+            const int e = threadIdx.x + q * TH;
+            if (e < n2) v[q] = *reinterpret_cast<const double2*>(src + (e / (NC / 2)) * ld_src + 2 * (e % (NC / 2)));
+        }
+    }
+    __device__ __forceinline__ void put(double* dst, int ld_dst) const {
+#pragma unroll
+        for (int q = 0; q < per; ++q) {
+            const int e = threadIdx.x + q * TH;
+            if (e < n2) {
+                double* d = dst + (e / (NC / 2)) * ld_dst + 2 * (e % (NC / 2));
+                d[0] = v[q].x;
+                d[1] = v[q].y;
+            }
+        }
+    }
+};
 // two 64x64 global tiles -> LDS [64][LD], every load of both in flight before
 // the first LDS store (one memory latency instead of two)
 __device__ __forceinline__ void load_tiles2(double* d1, const double* __restrict__ s1, double* d2,
@@ -447,15 +474,32 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
     // waves 0..3: A tile (w, v); waves 4..7: R and C tiles (w, v - 4)
     const int il = j - s, ir = j + s, wv = threadIdx.x >> 6, v = wv & 3;
     const bool hl = il >= 0, hr = ir < b.N, hc = hl && j - 2 * s >= 0;
-    if (hl) {
-        load_rows<TH>(Wa, LD, b.Wr + (size_t)il * M * M, M, M);
-        load_rows<TH>(Za, ldr, b.Z + (size_t)il * M * b.nrhs, b.nrhs, b.nrhs);
-    }
-    if (hr) {
-        load_rows<TH>(Wb, LD, b.Wl + (size_t)ir * M * M, M, M);
-        load_rows<TH>(Zb, ldr, b.Z + (size_t)ir * M * b.nrhs, b.nrhs, b.nrhs);
-    }
-    if (hc) load_rows<TH>(Wc, LD, b.Wl + (size_t)il * M * M, M, M);
+    // every tile's loads in flight together (nrhs is 16 or 32: bcr_supported)
+    auto loads = [&](auto ncz) {
+        constexpr int NCZ = decltype(ncz)::value;
+        TileFetch<64, M, TH> fwa, fwb, fwc;
+        TileFetch<NCZ, M, TH> fza, fzb;
+        if (hl) {
+            fwa.fetch(b.Wr + (size_t)il * M * M, M);
+            fza.fetch(b.Z + (size_t)il * M * b.nrhs, b.nrhs);
+        }
+        if (hr) {
+            fwb.fetch(b.Wl + (size_t)ir * M * M, M);
+            fzb.fetch(b.Z + (size_t)ir * M * b.nrhs, b.nrhs);
+        }
+        if (hc) fwc.fetch(b.Wl + (size_t)il * M * M, M);
+        if (hl) {
+            fwa.put(Wa, LD);
+            fza.put(Za, ldr);
+        }
+        if (hr) {
+            fwb.put(Wb, LD);
+            fzb.put(Zb, ldr);
+        }
+        if (hc) fwc.put(Wc, LD);
+    };
+    if (b.nrhs == 16) loads(std::integral_constant<int, 16>{});
+    else loads(std::integral_constant<int, 32>{});
     __syncthreads();
     double* Aj = b.A + (size_t)j * M * M;
     if (wv < 4) {
@@ -515,13 +559,23 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     unsigned long long t0 = 0, t1 = 0;
     if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
-    load_rows<NTL>(A, LD, b.A + (size_t)i * M * M, M, M);
-    load_rows<NTL>(Cc, L16, b.C + (size_t)i * M * M + 16 * w, M, 16);
-    if (hr) load_tile<64, 16, NTL>(Cr, LD, b.C + (size_t)r * M * M + 16 * w * M, M);
-    if (hz) load_rows<NTL>(Rc, L16, b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs, 16);
-    if (sp > 0) {   // the neighbours' full W blocks (the A update's operands)
-        load_tile<64, 64, NTL>(Wa_l, M, b.Wr + (size_t)(i - sp) * M * M, M);
-        if (i + sp < b.N) load_tile<64, 64, NTL>(Wb_l, M, b.Wl + (size_t)(i + sp) * M * M, M);
+    {   // every tile's loads in flight together, then the LDS stores
+        TileFetch<64, M, NTL> fa, fwa, fwb;
+        TileFetch<16, M, NTL> fcc, frc;
+        TileFetch<64, 16, NTL> fcr;
+        const bool hwa = sp > 0, hwb = sp > 0 && i + sp < b.N;   // the neighbours' W blocks (the A update's operands)
+        fa.fetch(b.A + (size_t)i * M * M, M);
+        fcc.fetch(b.C + (size_t)i * M * M + 16 * w, M);
+        if (hr) fcr.fetch(b.C + (size_t)r * M * M + 16 * w * M, M);
+        if (hz) frc.fetch(b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs);
+        if (hwa) fwa.fetch(b.Wr + (size_t)(i - sp) * M * M, M);
+        if (hwb) fwb.fetch(b.Wl + (size_t)(i + sp) * M * M, M);
+        fa.put(A, LD);
+        fcc.put(Cc, L16);
+        if (hr) fcr.put(Cr, LD);
+        if (hz) frc.put(Rc, L16);
+        if (hwa) fwa.put(Wa_l, M);
+        if (hwb) fwb.put(Wb_l, M);
     }
     __syncthreads();
     if (st) {
@@ -638,12 +692,25 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
     const int wave = threadIdx.x >> 6;
     const bool upd = sp > 0 && sp < b.N;
     if (threadIdx.x == 0) bad[0] = 0.0;
-    load_rows<NTL>(A, LD, b.A, M, M);
-    load_rows<NTL>(R, ldr, b.R, b.nrhs, b.nrhs);
-    if (upd) {
-        load_rows<NTL>(Wb, LD, b.Wl + (size_t)sp * M * M, M, M);
-        load_rows<NTL>(Zb, ldr, b.Z + (size_t)sp * M * b.nrhs, b.nrhs, b.nrhs);
-    }
+    auto loads = [&](auto ncz) {   // every tile's loads in flight together
+        constexpr int NCZ = decltype(ncz)::value;
+        TileFetch<64, M, NTL> fa, fwb;
+        TileFetch<NCZ, M, NTL> fr, fzb;
+        fa.fetch(b.A, M);
+        fr.fetch(b.R, b.nrhs);
+        if (upd) {
+            fwb.fetch(b.Wl + (size_t)sp * M * M, M);
+            fzb.fetch(b.Z + (size_t)sp * M * b.nrhs, b.nrhs);
+        }
+        fa.put(A, LD);
+        fr.put(R, ldr);
+        if (upd) {
+            fwb.put(Wb, LD);
+            fzb.put(Zb, ldr);
+        }
+    };
+    if (b.nrhs == 16) loads(std::integral_constant<int, 16>{});
+    else loads(std::integral_constant<int, 32>{});
     for (int e = threadIdx.x; e < M * LD; e += NTL) X[e] = 0.0;
     __syncthreads();
     if (upd) {
@@ -1446,8 +1513,8 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                 for (int m = 0; m < mend;) {
                     const int m1 = df_wait_run(fL + i * nt, 1, diag ? nullptr : fL + jj * nt, 1, m, mend, epoch, d.fail, sh);
                     for (; m < m1; ++m) {
-                        load_tile<64>(T1, LD, tA(i, m), (int)np);
-                        if (!diag) load_tile<64>(T2, LD, tA(jj, m), (int)np);
+                        if (diag) load_tile<64>(T1, LD, tA(i, m), (int)np);
+                        else load_tiles2(T1, tA(i, m), T2, tA(jj, m), (int)np);
                         __syncthreads();
                         const double* Lb = diag ? T1 : T2;
     #pragma unroll
