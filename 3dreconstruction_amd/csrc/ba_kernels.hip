@@ -615,12 +615,6 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 #ifndef SFM_SCHUR_WPE   // waves per SIMD the Schur kernel is compiled for
 #define SFM_SCHUR_WPE 2
 #endif
-#ifndef SFM_SCHUR4_SP   // points / observations per batch of the 64-row variant
-#define SFM_SCHUR4_SP 4
-#endif
-#ifndef SFM_SCHUR4_SO
-#define SFM_SCHUR4_SO 48
-#endif
 #ifndef SFM_SCHUR5_SP   // the same for the 80-row variant (SO >= the planner's kSubObs)
 #define SFM_SCHUR5_SP kSubPts
 #endif
@@ -2401,14 +2395,14 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
         SFM_HIP(hipGetLastError());
     }
     if (P.n_chunk <= 0) return;
-    // 64-row tiles: 4-point batches (12 panel columns, no k padding) keep LDS
-    // at 16 KB per wave, i.e. 8 waves per CU (6-point batches: 7, and 9% slower)
+    // 64-row tiles: batches of schur4_pts(CM) points (ba_types.h) at 8 waves
+    // per CU (6-point batches' LDS allows 7, and measured 9% slower)
     if (P.tile_nt == 4) {
         if (scale_e)
-            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO, true>),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, schur4_pts(CM), schur4_obs(CM), true>),
                                                dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
         else
-            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, SFM_SCHUR4_SP, SFM_SCHUR4_SO>),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, schur4_pts(CM), schur4_obs(CM)>),
                                                dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
     } else {
         if (scale_e)

@@ -606,8 +606,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     int64_t flops = 0;
     HostVec<int32_t> cslot;
     pl.tile_nt = 5;
-    // the 64-row kernel walks 48-observation batches (ba_kernels.hip)
-    if (max_own <= 64 && max_obs <= 48 && !std::getenv("SFM_BA_TILE80")) {
+    // the 64-row kernel walks batches of at most schur4_obs observations
+    if (max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !std::getenv("SFM_BA_TILE80")) {
         // both tile heights are planned (each over the host threads)
         std::vector<ChunkDesc> c4, c5;
         HostVec<int32_t> s4, s5;

@@ -25,6 +25,14 @@ constexpr int kSubPts = 6;                // points per wave batch (3 panel colu
 constexpr int kZShortObs = 32;            // general points the batched Z kernel takes (observations)
 constexpr int kZBatchPts = 16;            // points per batch of that kernel
 constexpr int kSubObs = 64;               // observations per wave batch (one per lane)
+// points / observations per batch of the 64-row Schur variant, by residual
+// model (SFM_CAM_*: 0 pinhole, 1 BAL, 2 RADIAL3), sized so its LDS stays
+// under 20 KB, i.e. 8 waves per CU (the register limit): pinhole 5 / 52
+// (20.2 KB), BAL 4 / 48 (17.8 KB; 5 points would pass 20 KB), RADIAL3 4 / 44
+// (19.4 KB; 48 observations: 20.1 KB, 7 waves).  A point above the
+// observation count goes to the 80-row variant.
+constexpr int schur4_pts(int cm) { return cm == 0 ? 5 : 4; }
+constexpr int schur4_obs(int cm) { return cm == 0 ? 52 : cm == 2 ? 44 : 48; }
 constexpr int kChunkPts = 128;            // points per chunk (upper bound; step_kernel threads)
 constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
