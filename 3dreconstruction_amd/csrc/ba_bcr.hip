@@ -1452,10 +1452,10 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                     acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) tile_st_wt(tA(k, k - 1), (int)np, 16 * wave, 16 * q, acc[q]);
-                // X_k-1 goes out with L_k,k-1 (one drain and barrier for both;
-                // the next factor does not wait for it)
+                // X_k-1 goes out with L_k,k-1; their drain and flags come after
+                // the diagonal update below, so the stores complete meanwhile
                 x_out(k - 1);
-                df_publish2(fL + k * nt + k - 1, fL + (k - 1) * nt + k - 1, epoch);   // (T1, T2 are free)
+                __syncthreads();   // T1 and T2 are read
 #pragma unroll
                 for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
                 for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
@@ -1468,6 +1468,7 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                     const v4d a = tile_ld(T3, LD, 16 * ti, 16 * tj);
                     tile_st(T3, LD, 16 * ti, 16 * tj, tile_mm<false, true, true>(a, T1, LD, 16 * ti, T1, LD, 16 * tj, 0, M));
                 }
+                df_publish2(fL + k * nt + k - 1, fL + (k - 1) * nt + k - 1, epoch);   // L_k,k-1 and X_k-1
                 mark(2);
             } else {
                 load_tile<64>(T3, LD, tA(0, 0), (int)np);
