@@ -68,6 +68,18 @@ __device__ __forceinline__ double clampd(double v, double lo, double hi) {
     return fmin(fmax(v, lo), hi);
 }
 
+// LM damping of a point-block diagonal entry: D^2 = clamp(diag) / radius.
+// Ceres forms D = sqrt(clamp(diag) / radius) and adds D * D (the oracle does
+// the same); the square of the rounded square root differs from its argument
+// by about an ulp, and dropping the sqrt takes three dependent sqrt sequences
+// off the point factorisation's critical path (Schur 0.347 -> 0.335 ms at
+// C4).  Every point kernel (Schur, step, general points) uses this formula,
+// so the elimination and the back substitution see the same V + D^2.  The
+// camera columns keep Ceres's form (formed once per RCS, not per point).
+__device__ __forceinline__ double point_d2(const DevProblem& P, double diag, double inv_radius) {
+    return clampd(diag, P.min_diag, P.max_diag) * inv_radius;
+}
+
 // ---------------------------------------------------------------------------
 // per-camera precompute
 // ---------------------------------------------------------------------------
@@ -146,8 +158,10 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
         P[2] = X[2] * cp.c + cr2 * cp.s + u[2] * tmp;
     }
     P[0] += cp.t[0]; P[1] += cp.t[1]; P[2] += cp.t[2];
-    // one reciprocal for the projection and its Jacobian (x = P0/P2 to 1 ulp)
-    const double iz = 1.0 / P[2];
+    // one reciprocal for the projection and its Jacobian (x = P0/P2 to about
+    // 1 ulp): v_rcp + two Newton steps, a shorter dependent chain than the
+    // IEEE division sequence (C4 +0.6 % LM iterations/s)
+    const double iz = rcp_nr(P[2]);
     double r0, r1;
     // unscaled dr/dP (2x3) and dr/d(intrinsics) (2 x kIW) of the model
     double A[2][3], Ji[2][kIW<CM>];
@@ -612,6 +626,9 @@ __device__ __forceinline__ bool crow_valid(const ChunkDesc& cd, int t) { return 
 __device__ constexpr int kTi[15] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4};
 __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4};
 
+#ifndef SFM_SCHUR_PRE_WAIT   // the first batch's loads waited before the batch loop
+#define SFM_SCHUR_PRE_WAIT 1
+#endif
 #ifndef SFM_SCHUR_WPE   // waves per SIMD the Schur kernel is compiled for
 #define SFM_SCHUR_WPE 2
 #endif
@@ -674,6 +691,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
     const int c = blockIdx.x, lane = threadIdx.x;
     const ChunkDesc& cd = P.chunks[c];
     const int pb = cd.pt_begin, np = cd.pt_end - pb, ob0 = cd.obs_begin;
+    // read once: a ChunkDesc load inside the batch loop would be waited on
+    // with the in-order counter, i.e. together with the next batch's prefetch
+    const bool one_intr = cd.n_intr == 1;
     const double inv_radius = 1.0 / radius;   // LM diagonal D^2 = clamp(diag) / radius (as step_kernel)
 
     for (int e = lane; e <= np; e += 64) cpoff[e] = P.pt_off[pb + e] - ob0;
@@ -727,6 +747,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
     };
     BatchIn nx;
     fetch(0, nx);
+#if SFM_SCHUR_PRE_WAIT
+    // The first batch's loads complete before the loop.  Without this the
+    // waitcnt pass merges the loop entry (loads pending in the registers the
+    // loop body reads) with the back edge and waits on the counter inside
+    // phase A of EVERY batch -- which, the counter being in order, also waits
+    // for the next batch's prefetch, so its HBM latency was never hidden.
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+#endif
     for (int p0 = 0; p0 < np;) {
         const int npts = nx.npts;   // batch [p0, p1)
         if (npts == 0) break;   // a point above SO observations: excluded by the planner
@@ -850,8 +878,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
             const int di[3] = {0, 2, 5};
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
-                const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
-                V[di[a]] += lm * lm;
+                V[di[a]] += point_d2(P, V[di[a]], inv_radius);
             }
             const double i00 = rsqrt_nr(V[0]);
             const double l10 = V[1] * i00, l20 = V[3] * i00;
@@ -892,7 +919,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
         SFM_STAMP(2)
         // ---- C2: intrinsics rows, ordered per point ---------------------------
         // (register sums per run of observations sharing an intrinsics block)
-        if constexpr (CM != SFM_CAM_PINHOLE) {
+        // One intrinsics block in the chunk (shared intrinsics, as C4 and the
+        // SequentialActuator's single camera): every observation has the same
+        // row, so the sums run without the run-boundary test (same fma order,
+        // same bits as the general loops below).
+        if (one_intr) {
+            constexpr int NZ = 3 * NK;   // (axis, column) sums per point
+            const int row = irow[0];
+            for (int e = lane; e < NZ * npts; e += 64) {
+                const int pt = e / NZ, rem = e - NZ * pt, a = rem / NK, k = rem - NK * a;
+                const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
+                double z = 0.0;
+                int q = q0;
+                if constexpr (CM == SFM_CAM_PINHOLE) {
+                    // z_k = sum_q Ji[q][k] M[q][k & 1][a]
+                    const int mo = 3 * (k & 1) + a;
+                    for (; q + 4 <= q1; q += 4) {
+                        double jv[4], mv[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) { jv[j] = ob[q + j][k]; mv[j] = obm[q + j][mo]; }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) z = fma(jv[j], mv[j], z);
+                    }
+                    for (; q < q1; ++q) z = fma(ob[q][k], obm[q][mo], z);
+                } else {
+                    for (; q + 2 <= q1; q += 2) {
+                        double jv[4], mv[4];
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            jv[2 * j] = ob[q + j][2 * k]; jv[2 * j + 1] = ob[q + j][2 * k + 1];
+                            mv[2 * j] = obm[q + j][a]; mv[2 * j + 1] = obm[q + j][3 + a];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) z = fma(jv[j], mv[j], z);
+                    }
+                    for (; q < q1; ++q) {
+                        z = fma(ob[q][2 * k], obm[q][a], z);
+                        z = fma(ob[q][2 * k + 1], obm[q][3 + a], z);
+                    }
+                }
+                panel[3 * pt + a][row + k] += z;
+            }
+        } else if constexpr (CM != SFM_CAM_PINHOLE) {
             // one lane per (point, axis, intrinsics column k < NK):
             // z_k = sum_q Ji[q][0][k] M[q][0][a] + Ji[q][1][k] M[q][1][a]
             for (int e = lane; e < 3 * NK * npts; e += 64) {
@@ -1462,6 +1530,10 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
     constexpr int IW = kIW<CM>;
     __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
     __shared__ double csy[kCamSlots][6];        // camera scaleF * yF (0 for a constant image)
+    // staged camera t has F columns: read from LDS in the observation loop (a
+    // ChunkDesc load there was waited on together with the next observation's
+    // prefetch, the vector memory counter being in order)
+    __shared__ int scam[kCamSlots];
     __shared__ double isy[kIntrSlots][3 * IW];  // intrinsics | candidate | scaleF * yF
     const int c = blockIdx.x, tid = threadIdx.x;
     const double inv_radius = 1.0 / radius;   // as schur_kernel
@@ -1477,6 +1549,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             const int t = e / 6, k = e - 6 * t, col = cd.cam_col[t];
             csy[t][k] = col >= 0 ? P.scaleF[col + k] * P.yF[col + k] : 0.0;
         }
+        if (tid < cd.n_cams) scam[tid] = crow_valid(cd, tid) ? 1 : 0;
         if (tid < IW * cd.n_intr) {
             const int t = tid / IW, k = tid - IW * t, col = cd.intr_col[t];
             isy[t][k] = intr[IW * cd.intr_id[t] + k];
@@ -1511,7 +1584,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             }
             LinT<CM> L;
             linearize<CM, true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
-            const bool cam = crow_valid(cd, cs);
+            const bool cam = scam[cs] != 0;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 double q = 0.0;  // (J_F y_F) for this row
@@ -1535,8 +1608,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
         const int di[3] = {0, 2, 5};
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
-            V[di[a]] += lm * lm;
+            V[di[a]] += point_d2(P, V[di[a]], inv_radius);
         }
         // y_E = (V + D^2)^-1 (g_E - W' y_F) via Cholesky
         const double l00 = sqrt(V[0]), l10 = V[1] / l00, l20 = V[3] / l00;
@@ -1684,8 +1756,7 @@ __global__ __launch_bounds__(64) void zpoint_kernel(DevProblem P, const CamPre* 
     const int di[3] = {0, 2, 5};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
-        V[di[a]] += lm * lm;
+        V[di[a]] += point_d2(P, V[di[a]], inv_radius);
     }
     const double i00 = rsqrt_nr(V[0]);
     const double l10 = V[1] * i00, l20 = V[3] * i00;
@@ -1897,8 +1968,7 @@ __global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* 
     const int di[3] = {0, 2, 5};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
-        V[di[a]] += lm * lm;
+        V[di[a]] += point_d2(P, V[di[a]], inv_radius);
     }
     const double i00 = rsqrt_nr(V[0]);
     const double l10 = V[1] * i00, l20 = V[3] * i00;
@@ -2163,8 +2233,7 @@ __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
         const int di[3] = {0, 2, 5};
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const double lm = sqrt(clampd(V[di[a]], P.min_diag, P.max_diag) * inv_radius);
-            V[di[a]] += lm * lm;
+            V[di[a]] += point_d2(P, V[di[a]], inv_radius);
         }
         const double l00 = sqrt(V[0]), l10 = V[1] / l00, l20 = V[3] / l00;
         const double l11 = sqrt(V[2] - l10 * l10), l21 = (V[4] - l20 * l10) / l11;
@@ -2227,21 +2296,31 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
                                                                unsigned long long seq) {
     double s[7] = {0, 0, 0, 0, 0, 0, 0};
     double m[5] = {0, 0, 0, 0, 0};
-#pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_fblk; i += kFinThreads) {
-        s[5] += P.part_f[3 * i]; s[6] += P.part_f[3 * i + 1]; m[4] = fmax(m[4], P.part_f[3 * i + 2]);
-    }
-#pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_img * kGramSeg; i += kFinThreads) {
-        s[0] += P.part_u[2 * i]; m[0] = fmax(m[0], P.part_u[2 * i + 1]);
-    }
-#pragma unroll 4
-    for (int i = threadIdx.x; i < P.n_chunk + P.n_gpt; i += kFinThreads) { s[1] += P.part_s[2 * i]; m[1] = fmax(m[1], P.part_s[2 * i + 1]); }
-#pragma unroll 4
-    for (int i = threadIdx.x; i < n_step_blocks; i += kFinThreads) {
-        s[2] += P.part_t[kPartT * i]; s[3] += P.part_t[kPartT * i + 1]; s[4] += P.part_t[kPartT * i + 2];
-        m[2] = fmax(m[2], P.part_t[kPartT * i + 4]);
-        m[3] = fmax(m[3], P.part_t[kPartT * i + 3]);
+    // the four lists in one loop, so every list's loads are in flight together
+    // (four separate loops were four serial memory latencies); each list is
+    // still summed by this thread in index order, as before
+    const int nf = P.n_fblk, nu = P.n_img * kGramSeg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
+    const int nmax = max(max(nf, nu), max(ns, nt));
+#pragma unroll 2
+    for (int i = threadIdx.x; i < nmax; i += kFinThreads) {
+        // loads from clamped indices (unconditional, so the compiler issues
+        // them all before the first use), accumulated only where in range
+        const bool bf = i < nf, bu = i < nu, bs = i < ns, bt = i < nt;
+        const int jf = bf ? i : 0, ju = bu ? i : 0, js = bs ? i : 0, jt = bt ? i : 0;
+        // (an empty list may have no buffer: its loads are skipped, uniformly)
+        double f0 = 0.0, f1 = 0.0, f2 = 0.0, u0 = 0.0, u1 = 0.0, s0 = 0.0, s1 = 0.0;
+        double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0, t4 = 0.0;
+        if (nf > 0) { f0 = P.part_f[3 * jf]; f1 = P.part_f[3 * jf + 1]; f2 = P.part_f[3 * jf + 2]; }
+        if (nu > 0) { u0 = P.part_u[2 * ju]; u1 = P.part_u[2 * ju + 1]; }
+        if (ns > 0) { s0 = P.part_s[2 * js]; s1 = P.part_s[2 * js + 1]; }
+        if (nt > 0) {
+            t0 = P.part_t[kPartT * jt]; t1 = P.part_t[kPartT * jt + 1]; t2 = P.part_t[kPartT * jt + 2];
+            t3 = P.part_t[kPartT * jt + 3]; t4 = P.part_t[kPartT * jt + 4];
+        }
+        if (bf) { s[5] += f0; s[6] += f1; m[4] = fmax(m[4], f2); }
+        if (bu) { s[0] += u0; m[0] = fmax(m[0], u1); }
+        if (bs) { s[1] += s0; m[1] = fmax(m[1], s1); }
+        if (bt) { s[2] += t0; s[3] += t1; s[4] += t2; m[2] = fmax(m[2], t4); m[3] = fmax(m[3], t3); }
     }
     wave_sum(s);
 #pragma unroll

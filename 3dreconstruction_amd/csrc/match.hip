@@ -56,6 +56,14 @@ static_assert(kStage == 128 || kStage == 256, "merge windows are 256 rows");
 #ifndef MATCH_TILE_UNROLL
 #define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
 #endif
+#ifndef MATCH_SPLIT
+// The two stage buffers as separate LDS objects, the stage loop unrolled by
+// two so every fragment read names one of them: the waitcnt pass can then
+// tell that the reads of stage st do not alias the LDS-DMA writes of stage
+// st+1 and stops waiting for those (vmcnt(0) at the tile loop's head, which
+// exposed every stage's load latency: the double buffer did not overlap).
+#define MATCH_SPLIT 1
+#endif
 #ifndef MATCH_PIPE
 // software-pipelined tile loop (two accumulator sets; A/B knob).  Measured on
 // C3 (tools/gpurun/match_ab.sh, profiles/r03/a_match_pipe): 2 column tiles at
@@ -184,22 +192,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     // bank conflicts of the 32-rows-one-chunk fragment reads are removed by
     // storing logical 16-byte chunk k of row r at slot k ^ (r & 7) (the XOR is
     // applied to the global SOURCE address, and again on the read).
+#if MATCH_SPLIT
+    __shared__ __attribute__((aligned(16))) int8_t sA0[kStage * 128], sA1[kStage * 128];
+    __shared__ __attribute__((aligned(16))) int32_t sN0[kStage], sN1[kStage];
+#else
     __shared__ __attribute__((aligned(16))) int8_t sA[2][kStage * 128];
     __shared__ __attribute__((aligned(16))) int32_t sN[2][kStage];
-    auto issue = [&](int buf, int row_base) {
+#endif
+    auto issue_to = [&](int8_t* dA, int32_t* dN, int row_base) {
 #pragma unroll
         for (int q = 0; q < kStage * 8 / 256; ++q) {
             const int L = q * 256 + wave * 64 + lane;          // 16-byte slot in the stage
             const int r = L >> 3, k = (L & 7) ^ (r & 7);
             const int8_t* src = a.desc + (db_row0 + row_base + r) * 128 + k * 16;
-            __builtin_amdgcn_global_load_lds(src, &sA[buf][(q * 256 + wave * 64) * 16], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src, dA + (q * 256 + wave * 64) * 16, 16, 0, 0);
         }
         if (wave == 0) {
 #pragma unroll
             for (int q = 0; q < kStage / 64; ++q)
-                __builtin_amdgcn_global_load_lds(a.ntr + db_row0 + row_base + q * 64 + lane, &sN[buf][q * 64], 4, 0, 0);
+                __builtin_amdgcn_global_load_lds(a.ntr + db_row0 + row_base + q * 64 + lane, dN + q * 64, 4, 0, 0);
         }
     };
+#if MATCH_SPLIT
+    auto issue = [&](int buf, int row_base) {
+        if (buf) issue_to(sA1, sN1, row_base);
+        else issue_to(sA0, sN0, row_base);
+    };
+#else
+    auto issue = [&](int buf, int row_base) { issue_to(sA[buf], sN[buf], row_base); };
+#endif
 
     const int n_db_pad = (n_db + kRowPad - 1) / kRowPad * kRowPad;
     int b1[kCT], b2[kCT];
@@ -321,6 +342,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     }
     if (pendB) epilogue(accB, ntB);
     if (merge_base >= 0) merge_window(merge_base);
+#elif MATCH_SPLIT
+    // one stage: its tiles from (A, N) while the next stage lands in (nA, nN)
+    auto stage = [&](const int8_t* A, const int32_t* N, int8_t* nA, int32_t* nN, int sup) {
+        __syncthreads();   // this stage has landed (vmcnt drained); the other buffer is free
+        if (sup + kStage < n_db_pad) issue_to(nA, nN, sup + kStage);
+#pragma unroll MATCH_TILE_UNROLL
+        for (int tile = 0; tile < kStage; tile += 32) {
+            v4i af[4], nt4[4];
+            load_frag(A, N, tile, af, nt4);
+            v16i acc[kCT];
+            mfma_tile(af, acc);
+            epilogue(acc, nt4);
+        }
+        if (((sup + kStage) & 255) == 0) merge_window(sup + kStage - 256);
+    };
+    for (int sup = 0; sup < n_db_pad; sup += 2 * kStage) {
+        stage(sA0, sN0, sA1, sN1, sup);
+        if (sup + kStage < n_db_pad) stage(sA1, sN1, sA0, sN0, sup + kStage);
+    }
 #else
     for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
         __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
