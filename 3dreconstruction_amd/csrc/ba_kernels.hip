@@ -452,6 +452,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
 #pragma unroll
         for (int a = 0; a < 3; ++a) x[a] = p >= 0 ? X[3 * (size_t)p + a] : 0.0;
     };
+    // one observation's contribution (lane's running sums, observation order)
+    auto process = [&](int p_cur, const double2& uv, const double (&Xp)[3]) {
+    // re-read the staged camera from LDS each step instead of keeping its
+    // 28 doubles live across the loop (register budget of 2 waves/SIMD)
+    asm volatile("" ::: "memory");
+    if (p_cur >= 0) {
+        LinT<CM> L;
+        linearize<CM, true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
+        if constexpr (kHasCost) g[kT::kCost - S0] += L.half_rho;
+        bad = fmax(bad, L.ok ? 0.0 : 1.0);
+        // unscaled rows; the per-image column scales are applied to the sums
+        auto r = [&](int q, int i) -> double {
+            return i < 6 ? L.Jc[q][i] : i < FW ? L.Ji[q][i - 6] : L.f[q];
+        };
+#pragma unroll
+        for (int s = 0; s < 64; ++s) {
+            if (S0 + s >= kT::kS.n) break;
+            const int i = kT::kS.i[S0 + s], j = kT::kS.j[S0 + s];
+            if (gram::in0<CM>(i) && gram::in0<CM>(j)) g[s] = fma(r(0, i), r(0, j), g[s]);
+            if (gram::in1<CM>(i) && gram::in1<CM>(j)) g[s] = fma(r(1, i), r(1, j), g[s]);
+        }
+    }
+    };
 #if SFM_GRAM_DEEP
     // three stages: the point gather (random rows of X) two iterations ahead
     int p_c, p_n, p_nn;
@@ -471,6 +494,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         p_n = p_nn; uv_n = uv_nn;
         fetch_x(p_n, x_n);
         fetch_ids(base + 768, p_nn, uv_nn);
+        process(p_cur, uv, Xp);
+    }
 #else
     int p_c, p_n;
     double2 uv_c, uv_n;
@@ -486,28 +511,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         p_c = p_n; uv_c = uv_n;
         fetch_x(p_c, x_c);
         fetch_ids(base + 512, p_n, uv_n);
-#endif
-        // re-read the staged camera from LDS each step instead of keeping its
-        // 28 doubles live across the loop (register budget of 2 waves/SIMD)
-        asm volatile("" ::: "memory");
-        if (p_cur >= 0) {
-            LinT<CM> L;
-            linearize<CM, true, true, false>(scp, sin_, Xp, uv.x, uv.y, P.huber_a, L);
-            if constexpr (kHasCost) g[kT::kCost - S0] += L.half_rho;
-            bad = fmax(bad, L.ok ? 0.0 : 1.0);
-            // unscaled rows; the per-image column scales are applied to the sums
-            auto r = [&](int q, int i) -> double {
-                return i < 6 ? L.Jc[q][i] : i < FW ? L.Ji[q][i - 6] : L.f[q];
-            };
-#pragma unroll
-            for (int s = 0; s < 64; ++s) {
-                if (S0 + s >= kT::kS.n) break;
-                const int i = kT::kS.i[S0 + s], j = kT::kS.j[S0 + s];
-                if (gram::in0<CM>(i) && gram::in0<CM>(j)) g[s] = fma(r(0, i), r(0, j), g[s]);
-                if (gram::in1<CM>(i) && gram::in1<CM>(j)) g[s] = fma(r(1, i), r(1, j), g[s]);
-            }
-        }
+        process(p_cur, uv, Xp);
     }
+#endif
     gram::reduce_scatter64(g, lane);
     bad = wave_max(bad);
     part[wave][lane] = g[0];
@@ -1120,10 +1126,12 @@ __device__ __forceinline__ bool skip_kind(int kind, int vectors_only) {
 }
 
 // wave-local LDS exchange: every lane's writes visible to the wave
+// (LDS-only fences: the exchange is through LDS, so the fences need not
+// order, or wait for, the wave's global accesses -- e.g. a prefetch in flight)
 __device__ __forceinline__ void wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 __global__ void reduce_kernel(DevProblem P, int vectors_only) {
@@ -2080,18 +2088,29 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
     double* dst = (isa ? La + orow * 4 : Lb + orow * 4) + ok;
     const int dstep = 4 * (isa ? ra : rb);
     double s = 0.0;
+    // the next batch's term offsets are loaded one batch ahead (with this
+    // batch's Z loads, so a batch waits for one memory latency, not two)
+    // (two scalars, not a PTerm: the struct was promoted to LDS, and its
+    // store there waited for the load it was meant to prefetch)
+    const longlong2* pt2 = reinterpret_cast<const longlong2*>(P.pterms);
+    longlong2 nxt = make_longlong2(0, 0);
+    if (lane < min(kPtB, qb - qa)) nxt = pt2[qa + lane];
     for (int q0 = qa; q0 < qb; q0 += kPtB) {
         const int nb = min(kPtB, qb - q0);
         // stage: the batch's term offsets through LDS, then lane o < L loads
         // element o of every term (its row and column fixed: no index
         // division), all kPtB loads in flight before the first store
-        if (lane < nb) Lt[lane] = P.pterms[q0 + lane];
+        if (lane < nb) Lt[lane] = PTerm{nxt.x, nxt.y};
+        if (lane < min(kPtB, qb - q0 - kPtB)) nxt = pt2[q0 + kPtB + lane];
         wsync();
         double v[kPtB];
 #pragma unroll
         for (int t = 0; t < kPtB; ++t) {
+            // unconditional load (clamped index; Z is not empty when there
+            // are terms): a conditional one left a 0.0 default whose
+            // register write waited for the previous batch's loads
             const int64_t off = isa ? Lt[t].za : Lt[t].zb;
-            v[t] = (lane < L && t < nb) ? Z[off + oo] : 0.0;
+            v[t] = Z[(lane < L && t < nb) ? off + oo : 0];
         }
 #pragma unroll
         for (int t = 0; t < kPtB; ++t)
