@@ -1528,8 +1528,16 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
 // and candidate cameras, intrinsics, column scales and y_F are staged in LDS
 // once, so the per-observation work gathers only the measurement.
 // ---------------------------------------------------------------------------
+#ifndef SFM_STEP_PREFETCH   // A/B knob: the next observation's (slot, uv) loaded one ahead
+#define SFM_STEP_PREFETCH 1
+#endif
+#ifdef SFM_STEP_WPE   // A/B knob: waves per SIMD the step kernel is compiled for
+#define SFM_STEP_ATTR __attribute__((amdgpu_waves_per_eu(SFM_STEP_WPE, SFM_STEP_WPE)))
+#else
+#define SFM_STEP_ATTR
+#endif
 template <int CM>
-__global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
+__global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const CamPre* __restrict__ cps_c,
                                                          const double* __restrict__ intr_c,
@@ -1538,10 +1546,6 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
     constexpr int IW = kIW<CM>;
     __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
     __shared__ double csy[kCamSlots][6];        // camera scaleF * yF (0 for a constant image)
-    // staged camera t has F columns: read from LDS in the observation loop (a
-    // ChunkDesc load there was waited on together with the next observation's
-    // prefetch, the vector memory counter being in order)
-    __shared__ int scam[kCamSlots];
     __shared__ double isy[kIntrSlots][3 * IW];  // intrinsics | candidate | scaleF * yF
     const int c = blockIdx.x, tid = threadIdx.x;
     const double inv_radius = 1.0 / radius;   // as schur_kernel
@@ -1557,7 +1561,7 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             const int t = e / 6, k = e - 6 * t, col = cd.cam_col[t];
             csy[t][k] = col >= 0 ? P.scaleF[col + k] * P.yF[col + k] : 0.0;
         }
-        if (tid < cd.n_cams) scam[tid] = crow_valid(cd, tid) ? 1 : 0;
+
         if (tid < IW * cd.n_intr) {
             const int t = tid / IW, k = tid - IW * t, col = cd.intr_col[t];
             isy[t][k] = intr[IW * cd.intr_id[t] + k];
@@ -1581,18 +1585,27 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
         double sqf = 0.0, sqq = 0.0;
         const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
         // the next observation's (slot, uv) is loaded while this one is linearised
+#if SFM_STEP_PREFETCH
         int nslot = o0 < o1 ? P.obs_slot[o0] : 0;
         double2 nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
+#endif
         for (int o = o0; o < o1; ++o) {
+#if SFM_STEP_PREFETCH
             const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = nuv;
             if (o + 1 < o1) {
                 nslot = P.obs_slot[o + 1];
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
             }
+#else
+            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+#endif
             LinT<CM> L;
             linearize<CM, true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
-            const bool cam = scam[cs] != 0;
+            // (a ChunkDesc read: an LDS copy of the flag measured 8 % slower,
+            // 94.8 -> 102.5 us at C4, profiles/r03/q_final/step_ab.txt)
+            const bool cam = crow_valid(cd, cs);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 double q = 0.0;  // (J_F y_F) for this row
@@ -1644,15 +1657,22 @@ __global__ __launch_bounds__(kChunkPts) void step_kernel(DevProblem P, const Cam
             acc[0] = -(sqf + ybf) + 0.5 * (sqq + 2.0 * ybq + yVy);
         }
         // candidate residuals at (x_c, candidate cameras / intrinsics)
+#if SFM_STEP_PREFETCH
         nslot = o0 < o1 ? P.obs_slot[o0] : 0;
         nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
+#endif
         for (int o = o0; o < o1; ++o) {
+#if SFM_STEP_PREFETCH
             const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = nuv;
             if (o + 1 < o1) {
                 nslot = P.obs_slot[o + 1];
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
             }
+#else
+            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
+            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
+#endif
             LinT<CM> C;
             linearize<CM, false, false, false>(scc[cs], &isy[is][IW], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;
