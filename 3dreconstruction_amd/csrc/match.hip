@@ -54,7 +54,7 @@ constexpr int kRowPad = kQB > 256 ? kQB : 256;  // rows of every image padded to
 constexpr int kStage = MATCH_STAGE;   // database rows per LDS stage (kRowPad multiple of it)
 static_assert(kStage == 128 || kStage == 256, "merge windows are 256 rows");
 #ifndef MATCH_TILE_UNROLL
-#define MATCH_TILE_UNROLL 2        // tile-loop unroll (2: +0.5 % ratio, +2.5 % mutual pairs/s, 218 VGPRs, no spills)
+#define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
 #endif
 #ifndef MATCH_SPLIT
 // The two stage buffers as separate LDS objects, the stage loop unrolled by
