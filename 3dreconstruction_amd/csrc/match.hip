@@ -99,6 +99,16 @@ __global__ void prep_kernel(uint8_t* __restrict__ d, int32_t* __restrict__ nrm,
     }
 }
 
+// lowered to v_min3_i32 / v_med3_i32 (SIISelLowering's min/max combines)
+__device__ __forceinline__ int min3i(int a, int b, int c) { return min(min(a, b), c); }
+__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+// the value unchanged, hidden from the optimiser (an empty asm: no
+// instruction is emitted, so there is nothing for the hazard recognizer)
+__device__ __forceinline__ int opaque(int v) {
+    asm("" : "+v"(v));
+    return v;
+}
+
 struct Top2 {
     int g1v, g1i, g2v;
 };
@@ -257,8 +267,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     // distances instead of med3 + min per distance.  Two consecutive
     // pairs share one b2 update, b2 = min3(b2, t_a, t_b) (the same
     // value as two min steps): 5 VALU per 4 distances.
-    // The accumulators are consumed by compiler-generated code only: an
-    // inline asm reading MFMA results gets no hazard padding.
+    // Plain C min / max: the compiler selects v_min3_i32 / v_med3_i32 for
+    // these shapes (checked in the ISA, tests/test_match_isa.py) and its
+    // hazard recognizer sees every instruction.
     auto epilogue = [&](const v16i (&acc)[kCT], const v4i (&nt4)[4]) {
 #pragma unroll
         for (int tp = 0; tp < kCT; tp += 2)
@@ -273,28 +284,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
             const int w0 = __mul24(acc[tp][j + 3], a.kmul) + nt4[j >> 2][3];
             const int w1 = __mul24(acc[tp + 1][j + 3], a.kmul) + nt4[j >> 2][3];
             if (!kRatio) {
-                asm("v_min3_i32 %0, %0, %2, %3\n\t"
-                    "v_min3_i32 %1, %1, %4, %5\n\t"
-                    "v_min3_i32 %0, %0, %6, %7\n\t"
-                    "v_min3_i32 %1, %1, %8, %9"
-                    : "+v"(b1[tp]), "+v"(b1[tp + 1])
-                    : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
+                b1[tp] = min3i(min3i(b1[tp], x0, y0), z0, w0);
+                b1[tp + 1] = min3i(min3i(b1[tp + 1], x1, y1), z1, w1);
                 continue;
             }
-            int ta0, ta1, tb0, tb1;
-            asm("v_med3_i32 %4, %0, %8, %9\n\t"
-                "v_med3_i32 %5, %2, %10, %11\n\t"
-                "v_min3_i32 %0, %0, %8, %9\n\t"
-                "v_min3_i32 %2, %2, %10, %11\n\t"
-                "v_med3_i32 %6, %0, %12, %13\n\t"
-                "v_med3_i32 %7, %2, %14, %15\n\t"
-                "v_min3_i32 %0, %0, %12, %13\n\t"
-                "v_min3_i32 %2, %2, %14, %15\n\t"
-                "v_min3_i32 %1, %1, %4, %6\n\t"
-                "v_min3_i32 %3, %3, %5, %7"
-                : "+v"(b1[tp]), "+v"(b2[tp]), "+v"(b1[tp + 1]), "+v"(b2[tp + 1]),
-                  "=&v"(ta0), "=&v"(ta1), "=&v"(tb0), "=&v"(tb1)
-                : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(z0), "v"(w0), "v"(z1), "v"(w1));
+            // b1' through opaque(): no min(b1, x) shared with med3, so the
+            // selector keeps v_min3 (a shared inner min is not one-use)
+            const int ta0 = med3i(b1[tp], x0, y0), ta1 = med3i(b1[tp + 1], x1, y1);
+            b1[tp] = min3i(b1[tp], opaque(x0), y0);
+            b1[tp + 1] = min3i(b1[tp + 1], opaque(x1), y1);
+            const int tb0 = med3i(b1[tp], z0, w0), tb1 = med3i(b1[tp + 1], z1, w1);
+            b1[tp] = min3i(b1[tp], opaque(z0), w0);
+            b1[tp + 1] = min3i(b1[tp + 1], opaque(z1), w1);
+            b2[tp] = min3i(b2[tp], ta0, tb0);
+            b2[tp + 1] = min3i(b2[tp + 1], ta1, tb1);
         }
     };
     // keys carry row & 255: the tile keys are merged into the running state
@@ -307,6 +310,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
         }
     };
 
+    // A stage is filled by all four waves' LDS DMA, and read by every wave:
+    // each wave drains its own DMA (vmcnt) BEFORE the barrier.  __syncthreads
+    // alone does not (gfx950's workgroup release fence does not wait for
+    // loads), and the waitcnt pass places its LDS-DMA wait next to the first
+    // aliasing ds_read, after the barrier, where it covers only the wave's
+    // own part -- in the round-3 ISA it omitted it altogether on the stage
+    // loop's back edge (the cause of the MUTUAL mismatch of the unrolled
+    // build).
+    auto stage_landed = [&] {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
     if (n_db_pad > 0) issue(0, 0);
 #if MATCH_PIPE
     // Software pipeline over the tiles: tile t's MFMAs are issued before the
@@ -320,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     bool pendB = false;              // accB holds a tile whose epilogue is pending
     int merge_base = -1;             // a window merge pending after that epilogue
     for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
-        __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
+        stage_landed();    // stage st has landed in every wave's part; buffer st+1 is free
         if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
         const int8_t* A = sA[st & 1];
         const int32_t* N = sN[st & 1];
@@ -345,7 +360,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
 #elif MATCH_SPLIT
     // one stage: its tiles from (A, N) while the next stage lands in (nA, nN)
     auto stage = [&](const int8_t* A, const int32_t* N, int8_t* nA, int32_t* nN, int sup) {
-        __syncthreads();   // this stage has landed (vmcnt drained); the other buffer is free
+        stage_landed();    // this stage has landed in every wave's part; the other buffer is free
         if (sup + kStage < n_db_pad) issue_to(nA, nN, sup + kStage);
 #pragma unroll MATCH_TILE_UNROLL
         for (int tile = 0; tile < kStage; tile += 32) {
@@ -363,7 +378,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     }
 #else
     for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
-        __syncthreads();   // stage st has landed (vmcnt drained); buffer st+1 is free
+        stage_landed();    // stage st has landed in every wave's part; buffer st+1 is free
         if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
         const int8_t* A = sA[st & 1];
         const int32_t* N = sN[st & 1];
