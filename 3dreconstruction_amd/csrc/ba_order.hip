@@ -72,13 +72,21 @@ void ba_image_order(const int32_t* obs_img, const double* obs_uv, const int32_t*
 
 namespace {
 
-// shard observation s of shard point k: source observation pt_offsets[pt_src[k]] + (s - pt_off[k])
+// shard observation s of shard point k: source observation pt_offsets[pt_src[k]] + (s - pt_off[k]) for
+// a point that kept the problem's order; a general point re-sorted by image (k >= n_cpt) maps through
+// gperm[s - pt_off[n_cpt]] (null: no point was re-sorted)
 __global__ void obs_source_kernel(const int32_t* __restrict__ pt_src, const int64_t* __restrict__ pt_offsets,
-                                  const int32_t* __restrict__ pt_off, int32_t n_spt, int32_t* __restrict__ obs_src) {
+                                  const int32_t* __restrict__ pt_off, int32_t n_spt, int32_t n_cpt,
+                                  const int32_t* __restrict__ gperm, int32_t* __restrict__ obs_src) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_spt) return;
     const int64_t o0 = pt_offsets[pt_src[k]];
-    for (int32_t s = pt_off[k]; s < pt_off[k + 1]; ++s) obs_src[s] = (int32_t)(o0 + (s - pt_off[k]));
+    if (gperm && k >= n_cpt) {
+        const int32_t g0 = pt_off[n_cpt];
+        for (int32_t s = pt_off[k]; s < pt_off[k + 1]; ++s) obs_src[s] = (int32_t)(o0 + gperm[s - g0]);
+    } else {
+        for (int32_t s = pt_off[k]; s < pt_off[k + 1]; ++s) obs_src[s] = (int32_t)(o0 + (s - pt_off[k]));
+    }
 }
 
 __global__ void gather_uv_kernel(const int32_t* __restrict__ obs_src, const double2* __restrict__ src, int32_t n,
@@ -98,10 +106,10 @@ __global__ void gather_points_kernel(const int32_t* __restrict__ pt_src, const d
 }  // namespace
 
 void ba_obs_source(const int32_t* pt_src, const int64_t* pt_offsets, const int32_t* pt_off, int32_t n_spt,
-                   int32_t* obs_src, hipStream_t s) {
+                   int32_t n_cpt, const int32_t* gperm, int32_t* obs_src, hipStream_t s) {
     if (n_spt <= 0) return;
     hipLaunchKernelGGL(obs_source_kernel, dim3((unsigned)((n_spt + 255) / 256)), dim3(256), 0, s, pt_src, pt_offsets,
-                       pt_off, n_spt, obs_src);
+                       pt_off, n_spt, n_cpt, gperm, obs_src);
     SFM_HIP(hipGetLastError());
 }
 

@@ -3,6 +3,7 @@
 // matcher (sfm_match_dense, MUTUAL = BFMatcher crossCheck) and GPU solver
 // (sfm_ba_solve), one fresh adjuster per bundleAdjustment() call as
 // src/actuator/SequentialActuator.h:226-229 makes it.
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -36,10 +37,12 @@ struct CtxMatcher {
 // pt_offsets, obs_img, obs_uv, img_intr) for replaying the planner offline
 void dump_problem(const sfm_ba_problem& pr) {
     static const char* dir = std::getenv("SFM_SEQ_DUMP");
-    static int call = 0;
-    if (!dir || call++ % 100 != 99) return;
+    static std::atomic<int> calls{0};   // sequences may solve on several threads
+    if (!dir) return;
+    const int call = calls.fetch_add(1);
+    if (call % 100 != 99) return;
     char path[512];
-    std::snprintf(path, sizeof path, "%s/ba_%03d.bin", dir, call - 1);
+    std::snprintf(path, sizeof path, "%s/ba_%03d.bin", dir, call);
     FILE* f = std::fopen(path, "wb");
     if (!f) return;
     const int64_t h[5] = {pr.n_img, pr.n_intr, pr.n_pt, pr.n_obs, pr.const_img};

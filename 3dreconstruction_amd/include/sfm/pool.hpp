@@ -36,9 +36,16 @@ class PlanPool {
     }
     // fn(t) for t in [0, n): tasks spread over the workers and the caller; an
     // exception of any task is rethrown here once every task has finished
+    // A nested call (a task of this pool calling run() again, on a worker or
+    // on the calling thread) runs its tasks serially on the thread that makes
+    // it: it never touches use_, which that thread may already hold.
     void run(int n, const std::function<void(int)>& fn) {
         if (n <= 1) {
             if (n == 1) fn(0);
+            return;
+        }
+        if (in_task()) {
+            for (int t = 0; t < n; ++t) fn(t);
             return;
         }
         std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
@@ -66,7 +73,10 @@ class PlanPool {
             next_.store((uint64_t)g << 32);
         }
         cv_.notify_all();
-        work(g, &fn, n);
+        {
+            TaskScope scope;
+            work(g, &fn, n);
+        }
         std::unique_lock<std::mutex> lk(m_);
         done_.wait(lk, [&] { return left_ == 0; });
         job_ = nullptr;
@@ -74,6 +84,16 @@ class PlanPool {
     }
 
    private:
+    // set while this thread runs tasks of the pool (workers: always)
+    static bool& in_task() {
+        static thread_local bool f = false;
+        return f;
+    }
+    struct TaskScope {
+        bool prev = in_task();
+        TaskScope() { in_task() = true; }
+        ~TaskScope() { in_task() = prev; }
+    };
     PlanPool() {
         for (int t = 1; t < width(); ++t) workers_.emplace_back([this] { loop(); });
     }
@@ -115,6 +135,7 @@ class PlanPool {
         }
     }
     void loop() {
+        in_task() = true;
         uint32_t seen = 0;
         for (;;) {
             uint32_t g;

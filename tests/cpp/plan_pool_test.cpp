@@ -46,6 +46,13 @@ int main(int argc, char** argv) {
     } catch (const std::runtime_error&) {
         caught = true;
     }
+    // a task that runs a phase of its own (on a worker or on the caller,
+    // which holds the pool): serial on its thread, every inner task once
+    std::vector<int> nested(8 * 9, 0);
+    PlanPool::get().run(8, [&](int g) {
+        PlanPool::get().run(9, [&](int h) { nested[g * 9 + h]++; });
+    });
+    for (int v : nested) bad += v != 1;
     std::printf("pool: %d phases, %ld bad, exception %s\n", iters, bad, caught ? "caught" : "lost");
     return bad == 0 && caught ? 0 : 1;
 }
