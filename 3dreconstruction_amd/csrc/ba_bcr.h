@@ -12,10 +12,13 @@ constexpr int kBcrK = 10;   // camera blocks per super-block (6*K <= 64)
 struct BcrArgs {
     int N = 0;      // super-blocks
     int K = 0;      // camera blocks per super-block
-    int nrhs = 0;   // 1 + 4*nintr, padded to a multiple of 8
+    int nrhs = 0;   // 1 + iw*nintr (rhs + arrow columns), padded to a multiple of 16
     double *A = nullptr, *C = nullptr, *L = nullptr, *Wl = nullptr, *Wr = nullptr;
-    double *R = nullptr, *R0 = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
-    unsigned* yflag = nullptr;   // [N] back substitution: y_i published for epoch (bcr_back_all_kernel)
+    // R: rhs + arrow columns as updated; Z: each block's forward solve X R;
+    // Y: the back substitution's y, as 128 tagged granules per block; part: corner partials;
+    // fail: [0] numerical, [1] wait timeout, [4] / [5] workgroup counters
+    double *R = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
+    unsigned* yflag = nullptr;   // [N] back substitution: y_i published for epoch (bcr_back_kernel<true>)
     unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums
 };
 
@@ -39,6 +42,8 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
 bool bcr_supported(const DevProblem& P);
 void bcr_setup(BcrArgs& b, const DevProblem& P);
 size_t bcr_doubles(const BcrArgs& b);
+// 8-byte words of the back substitution's tagged y granules at b.Y (zeroed once at bind)
+inline size_t bcr_y_granules(const BcrArgs& b) { return (size_t)b.N * 128; }
 void bcr_bind(BcrArgs& b, double* base);
 // epoch: a value the y flags do not hold yet (the plan counts its solves from 1)
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch);

@@ -35,7 +35,30 @@ constexpr int M = kBcrM;      // 64
 constexpr int LD = M + 1;     // LDS row stride (bank spread)
 constexpr int NT = 256;
 
+// The published solve verdict (kScSolveFail): 0 ok, 1 numerical failure (a
+// non-positive pivot: the LM loop's invalid step), kSolveWaitTimeout when a
+// dataflow wait timed out (fail[1]: a workgroup was not resident, e.g. another
+// context held the CUs; the host reports SFM_ERR_DEVICE instead of counting
+// an invalid step).
+__device__ __forceinline__ double solve_verdict(const double* fail) {
+    const double t = __hip_atomic_load(fail + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t != 0.0 ? kSolveWaitTimeout : __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
+
+// Global-address-space agent-scope accesses for words handed between
+// workgroups of one launch (sc1: written through / read past this CU's L1;
+// cdna_hip_programming.md Guideline 16)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) double gf64;
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gf64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __hip_atomic_load((gf64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
@@ -406,7 +429,6 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
     double* A = b.A + (size_t)I * M * M;
     double* Cm = b.C + (size_t)I * M * M;
     double* R = b.R + (size_t)I * M * b.nrhs;
-    double* R0 = b.R0 + (size_t)I * M * b.nrhs;
     const int c0 = I * b.K, nreal = min(b.K, P.ncam - c0) * 6;
     const int Dp = P.D + 1;
     {
@@ -454,9 +476,13 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
             }
         }
         R[e] = v;
-        R0[e] = v;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *b.fail = 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        b.fail[0] = 0.0;   // numerical failure
+        b.fail[1] = 0.0;   // dataflow wait timeout
+        reinterpret_cast<unsigned*>(b.fail + 4)[0] = 0u;   // bcr_corner_kernel's finished workgroups
+        reinterpret_cast<unsigned*>(b.fail + 5)[0] = 0u;   // bcr_back_kernel<true>'s
+    }
 }
 
 // ---- update of one 16-row tile w of an even block j after eliminating its odd
@@ -535,7 +561,11 @@ constexpr int NTL = 512, NWL = NTL / 64;   // level kernel: 8 waves
 
 __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_odd) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int item = blockIdx.x >> 2, w = blockIdx.x & 3, sp = s >> 1;
+    // XCD-aware: workgroup b runs on XCD b % 8, so the four workgroups (w) of
+    // one item are b = x + 8 (4 j + w): the same XCD, whose L2 then serves the
+    // block's A and neighbour W tiles once for all four
+    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+    const int item = xcd + 8 * (q >> 2), w = q & 3, sp = s >> 1;
     if (item >= n_odd) {
         const int j = 2 * s * (item - n_odd);
         if (sp > 0 && j < b.N) update_tile_rows<NTL>(b, sp, j, w, sm);
@@ -606,7 +636,27 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
             if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * ti, Wbl, M, 16 * tj, 0, M);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         };
-        auto pre0 = [&] { a_tile(0); };
+        // A_00's update, the only one before the first diagonal factor: its 8
+        // k-chunk products (4 per neighbour) on the 8 waves, one MFMA chunk
+        // each, staged in X rows 16..63 (free until P(1)); wave 0 subtracts
+        // them in a fixed order and goes on to diag16(0) (a 32-MFMA chain on
+        // wave 0 alone before)
+        {
+            double* scr = X + 16 * LD;
+            const int v = wave & 3;
+            v4d part = zero4();
+            if (wave < 4) part = tile_mm<true, false, false>(part, Wal, M, 0, Wal, M, 0, 16 * v, 16 * v + 16);
+            else if (hir) part = tile_mm<true, false, false>(part, Wbl, M, 0, Wbl, M, 0, 16 * v, 16 * v + 16);
+            tile_st(scr + 256 * wave, 16, 0, 0, part);
+        }
+        __syncthreads();
+        auto pre0 = [&] {
+            const double* scr = X + 16 * LD;
+            v4d acc = tile_ld(A, LD, 0, 0);
+#pragma unroll
+            for (int q = 0; q < NWL; ++q) acc -= tile_ld(scr + 256 * q, 16, 0, 0);
+            tile_st(A, LD, 0, 0, acc);
+        };
         // A tiles 1..9 over waves 1..7 before the first barrier (P(0) and D(1)
         // read them)
         auto preN = [&] {
@@ -725,7 +775,20 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         };
         const int nrt = b.nrhs / 16;
-        auto pre0 = [&] { a_tile(0); };
+        {   // A_00's update: its 4 k-chunk products on waves 0..3 (X rows 16..63 free until P(1))
+            double* scr = X + 16 * LD;
+            if (wave < 4)
+                tile_st(scr + 256 * wave, 16, 0, 0,
+                        tile_mm<true, false, false>(zero4(), Wb, LD, 0, Wb, LD, 0, 16 * wave, 16 * wave + 16));
+        }
+        __syncthreads();
+        auto pre0 = [&] {
+            const double* scr = X + 16 * LD;
+            v4d acc = tile_ld(A, LD, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc -= tile_ld(scr + 256 * q, 16, 0, 0);
+            tile_st(A, LD, 0, 0, acc);
+        };
         auto preN = [&] {
             for (int t = wave - 1; t < 9 + 4 * nrt; t += NWL - 1) {
                 if (t < 9) {
@@ -743,177 +806,99 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
         chol_inv64<NWL>(A, X, bad, sc);
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
-    if (wave < 4)
+    // the root's forward solve z_0 = X R_0, every column (the corner system
+    // reduces the arrow's, bcr_corner_kernel), and X_0 for the back substitution
+    if (wave < 4) {
         for (int tj = 0; tj < b.nrhs / 16; ++tj)
-            tile_st(T, ldr, 16 * wave, 16 * tj,
+            tile_st(b.Z, b.nrhs, 16 * wave, 16 * tj,
                     tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
-    __syncthreads();
-    if (wave < 4)
-        for (int tj = 0; tj < b.nrhs / 16; ++tj)   // X' is upper triangular
-            tile_st(b.Y, b.nrhs, 16 * wave, 16 * tj,
-                    tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
+    } else {
+        for (int e = threadIdx.x - 256; e < M * M; e += NTL - 256) b.L[e] = X[(e / M) * LD + e % M];
+    }
 }
 
-// ---- back substitution at level l: y_i = X_i' (z_i - Wl y_l - Wr y_r) ----------
-__global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, int s) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int ldr = b.nrhs + 1;
-    double* X = sm;
-    double* Wl = X + M * LD;
-    double* Wr = Wl + M * LD;
-    double* Yl = Wr + M * LD;
-    double* Yr = Yl + M * ldr;
-    double* T = Yr + M * ldr;
-    const int i = s + 2 * s * blockIdx.x;
-    if (i >= b.N) return;
-    const int l = i - s, r = i + s, wave = threadIdx.x >> 6;
-    const bool hr = r < b.N;
-    load_rows(X, LD, b.L + (size_t)i * M * M, M, M);
-    load_rows(Wl, LD, b.Wl + (size_t)i * M * M, M, M);
-    load_rows(Yl, ldr, b.Y + (size_t)l * M * b.nrhs, b.nrhs, b.nrhs);
-    if (hr) {
-        load_rows(Wr, LD, b.Wr + (size_t)i * M * M, M, M);
-        load_rows(Yr, ldr, b.Y + (size_t)r * M * b.nrhs, b.nrhs, b.nrhs);
-    }
-    __syncthreads();
-    const double* Z = b.Z + (size_t)i * M * b.nrhs;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj) {
-        v4d acc = tile_ld(Z, b.nrhs, 16 * wave, 16 * tj);
-        acc = tile_mm<false, false, true>(acc, Wl, LD, 16 * wave, Yl, ldr, 16 * tj, 0, M);
-        if (hr) acc = tile_mm<false, false, true>(acc, Wr, LD, 16 * wave, Yr, ldr, 16 * tj, 0, M);
-        tile_st(T, ldr, 16 * wave, 16 * tj, acc);
-    }
-    __syncthreads();
-    double* Y = b.Y + (size_t)i * M * b.nrhs;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj)
-        tile_st(Y, b.nrhs, 16 * wave, 16 * tj,
-                tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
-}
-
-// ---- all back-substitution levels in one launch (dataflow) ---------------------
-// Workgroup k takes the k-th odd block in top-down level order.  It stages
-// its own X, Wl, Wr (written by the forward levels, earlier launches) while
-// the blocks it depends on -- i - s and i + s, both odd at a coarser level or
-// block 0 (bcr_top_kernel, an earlier launch) -- finish, then waits for their
-// published y, computes y_i and publishes it: one agent-scope release and a
-// flag word per block, one agent-scope acquire per consumer
-// (cdna_hip_programming.md Guideline 16).  Every workgroup must be resident
-// (one per CU: N - 1 <= the CU count, checked by the caller) and every spin
-// is bounded (a timeout fails the solve, which the LM loop treats as an
-// invalid step).
-__device__ __forceinline__ void bcr_wait_y(const unsigned* flag, unsigned epoch, double* fail) {
-    if (threadIdx.x == 0) {
-        unsigned spins = 0;
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 22)) {   // ~ seconds: a lost producer, never a normal wait
-                fail[0] = 1.0;
-                break;
+// ---- bordered arrow, corner first ---------------------------------------------
+// The forward levels (and the top) leave every block's z_i = X_i R_i, all
+// columns: the rhs and the arrow's.  With B = L L' the band's CR
+// factorisation (blocks in elimination order), E' B^-1 E = sum_i z_i[:, E]'
+// z_i[:, E] and E' B^-1 r = sum_i z_i[:, E]' z_i[:, 0], so the corner system
+//   (S_c + D^2 - E' B^-1 E) x_c = rhs_c - E' B^-1 r
+// is formed before any back substitution, which then carries one column,
+//   z'_i = z_i[:, 0] - z_i[:, E] x_c   (the forward solve of r - E x_c),
+// instead of the 1 + na columns (padded to 16) a bordered back substitution
+// carries.  One workgroup per block: wave 0 forms Q_i = z_i' z_i on the MFMA
+// and stores its rows 1..na, columns 0..na; the last workgroup to finish (an
+// agent-scope counter, reset by bcr_pack) adds the partials in block order
+// and solves the corner.
+__global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
+    const int I = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int na = P.iw * P.nintr, iw = P.iw;   // bordered columns (<= 16)
+    constexpr int kQ = 17;                      // part row stride: columns 0..16
+    __shared__ double Mc[16 * 16 + 16];
+    __shared__ int last;
+    unsigned* counter = reinterpret_cast<unsigned*>(b.fail + 4);
+    if (wave == 0) {
+        const int i = lane & 15, kk = lane >> 4, ntc = b.nrhs / 16;
+        const double* Z = b.Z + (size_t)I * M * b.nrhs;
+        double z0[16], z1[16];   // z[4 ks + kk][i], z[4 ks + kk][16 + i]: every load issued first
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) z0[ks] = Z[(4 * ks + kk) * b.nrhs + i];
+        if (ntc > 1) {
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) z1[ks] = Z[(4 * ks + kk) * b.nrhs + 16 + i];
+        }
+        v4d q00 = zero4(), q10 = zero4(), q11 = zero4();
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) q00 = __builtin_amdgcn_mfma_f64_16x16x4f64(z0[ks], z0[ks], q00, 0, 0, 0);
+        if (ntc > 1) {
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                q10 = __builtin_amdgcn_mfma_f64_16x16x4f64(z1[ks], z0[ks], q10, 0, 0, 0);
+                q11 = __builtin_amdgcn_mfma_f64_16x16x4f64(z1[ks], z1[ks], q11, 0, 0, 0);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(NT) void bcr_back_all_kernel(BcrArgs b, int s_top, unsigned epoch) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    int k = blockIdx.x, s = s_top / 2, i = -1;
-    for (; s >= 1; s >>= 1) {
-        const int n_odd = (b.N - s + 2 * s - 1) / (2 * s);
-        if (k < n_odd) {
-            i = s + 2 * s * k;
-            break;
-        }
-        k -= n_odd;
-    }
-    if (i < 0 || i >= b.N) return;
-    const int ldr = b.nrhs + 1;
-    double* X = sm;
-    double* Wl = X + M * LD;
-    double* Wr = Wl + M * LD;
-    double* Yl = Wr + M * LD;
-    double* Yr = Yl + M * ldr;
-    double* T = Yr + M * ldr;
-    const int l = i - s, r = i + s, wave = threadIdx.x >> 6;
-    const bool hr = r < b.N;
-    load_rows(X, LD, b.L + (size_t)i * M * M, M, M);
-    load_rows(Wl, LD, b.Wl + (size_t)i * M * M, M, M);
-    if (hr) load_rows(Wr, LD, b.Wr + (size_t)i * M * M, M, M);
-    if (l > 0) bcr_wait_y(b.yflag + l, epoch, b.fail);
-    if (hr) bcr_wait_y(b.yflag + r, epoch, b.fail);
-    load_rows(Yl, ldr, b.Y + (size_t)l * M * b.nrhs, b.nrhs, b.nrhs);
-    if (hr) load_rows(Yr, ldr, b.Y + (size_t)r * M * b.nrhs, b.nrhs, b.nrhs);
-    __syncthreads();
-    const double* Z = b.Z + (size_t)i * M * b.nrhs;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj) {
-        v4d acc = tile_ld(Z, b.nrhs, 16 * wave, 16 * tj);
-        acc = tile_mm<false, false, true>(acc, Wl, LD, 16 * wave, Yl, ldr, 16 * tj, 0, M);
-        if (hr) acc = tile_mm<false, false, true>(acc, Wr, LD, 16 * wave, Yr, ldr, 16 * tj, 0, M);
-        tile_st(T, ldr, 16 * wave, 16 * tj, acc);
-    }
-    __syncthreads();
-    double* Y = b.Y + (size_t)i * M * b.nrhs;
-    for (int tj = 0; tj < b.nrhs / 16; ++tj)
-        tile_st(Y, b.nrhs, 16 * wave, 16 * tj,
-                tile_mm<true, false, false>(zero4(), X, LD, 16 * wave, T, ldr, 16 * tj, 16 * wave, M));
-    // publish y_i: every storing wave drains, the workgroup meets, one lane
-    // releases at agent scope and stores the flag
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(b.yflag + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// ---- bordered arrow: corner system and final y_F --------------------------------
-// M_c = S_corner + D^2 - sum_I B_I' Yb_I ; v = rhs_c - sum_I B_I' y0_I
-// Pass 1: one wave per super-block, its 64 rows as 16 MFMA k-steps.
-__global__ __launch_bounds__(64) void bcr_corner_part_kernel(BcrArgs b, int na4) {
-    const int I = blockIdx.x, lane = threadIdx.x, i = lane & 15, kk = lane >> 4;
-    v4d m1 = zero4(), m2 = zero4();
-    for (int k = I * M; k < I * M + M; k += 4) {
-        const double* R0 = b.R0 + (size_t)(k + kk) * b.nrhs;
-        const double* Y = b.Y + (size_t)(k + kk) * b.nrhs;
-        const double a = i < na4 ? R0[1 + i] : 0.0;
-        const double y1 = i < na4 ? Y[1 + i] : 0.0;
-        const double y0 = i == 0 ? Y[0] : 0.0;
-        m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y1, m1, 0, 0, 0);
-        m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y0, m2, 0, 0, 0);
-    }
-    double* out = b.part + (size_t)I * 512;
+        // element (row kk + 4r, column i) of each tile; keep rows 1..na, columns 0..na
+        double* out = b.part + (size_t)I * 512;
+        auto put = [&](const v4d& q, int r0, int c0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        out[(kk + 4 * r) * 16 + i] = m1[r];
-        out[256 + (kk + 4 * r) * 16 + i] = m2[r];
+            for (int r = 0; r < 4; ++r) {
+                const int ga = r0 + kk + 4 * r, gc = c0 + i;
+                if (ga >= 1 && ga <= na && gc <= na) st_sc1(out + (ga - 1) * kQ + gc, q[r]);
+            }
+        };
+        put(q00, 0, 0);
+        if (ntc > 1) {
+            put(q10, 16, 0);
+            put(q11, 16, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-}
-
-// Pass 2: partials added in super-block order, then the small dense solve.
-__global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
-    const int na4 = P.iw * P.nintr, iw = P.iw;   // bordered columns (<= 16)
-    __shared__ double Mc[16 * 16 + 16];
-    // partials of super-blocks [g N/8, (g+1) N/8) per lane, the 8 lanes of an
+    // the partials are stored write-through (sc1) and drained above: a
+    // relaxed ticket publishes them, and the last arriver reads them with sc1
+    // loads (no release or acquire fence: Guideline 16, counter form)
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    // partials of blocks [g N/8, (g+1) N/8) per lane, the 8 lanes of an
     // element then combined by a fixed xor butterfly (deterministic)
     auto sum_parts = [&](int off, int g) {
         const int I0 = b.N * g / 8, I1 = b.N * (g + 1) / 8;
         double t = 0.0;
 #pragma unroll 4
-        for (int I = I0; I < I1; ++I) t += b.part[(size_t)I * 512 + off];
+        for (int J = I0; J < I1; ++J) t += ld_sc1(b.part + (size_t)J * 512 + off);
 #pragma unroll
         for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o);
         return t;
     };
     const int el = threadIdx.x >> 3, g = threadIdx.x & 7;   // 32 elements x 8 lanes per pass
-    for (int base = 0; base < na4 * na4 + na4; base += NT / 8) {
+    for (int base = 0; base < na * na + na; base += NT / 8) {
         const int k = base + el;
-        if (k < na4 * na4) {
-            const int a = k / na4, c = k % na4;
-            const double red = sum_parts(a * 16 + c, g);
-            if (g == 0) {
+        if (k < na * na) {
+            const int a = k / na, c = k % na;   // lower triangle (a >= c), mirrored
+            const double red = sum_parts(a * kQ + (a >= c ? c : a) + 1, g);
+            if (g == 0 && a >= c) {
                 double m = P.Scorner[(((size_t)(a / iw) * P.nintr + c / iw) * iw * iw) + (a % iw) * iw + c % iw];
                 if (a == c) {
                     const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
@@ -921,37 +906,37 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
                 }
                 Mc[a * 16 + c] = m - red;
             }
-        } else if (k < na4 * na4 + na4) {
-            const int a = k - na4 * na4;
-            const double red = sum_parts(256 + a * 16, g);
+        } else if (k < na * na + na) {
+            const int a = k - na * na;
+            const double red = sum_parts(a * kQ, g);
             if (g == 0) Mc[256 + a] = P.rhs[P.nb + a] - red;
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        // dense Cholesky solve of the corner (<= 16 x 16)
+        // dense Cholesky solve of the corner (<= 16 x 16, lower triangle)
         bool ok = true;
-        for (int j = 0; j < na4; ++j) {
+        for (int j = 0; j < na; ++j) {
             double d = Mc[j * 16 + j];
             for (int k = 0; k < j; ++k) d -= Mc[j * 16 + k] * Mc[j * 16 + k];
             if (!(d > 0.0)) ok = false;
             d = sqrt(d);
             Mc[j * 16 + j] = d;
-            for (int i2 = j + 1; i2 < na4; ++i2) {
+            for (int i2 = j + 1; i2 < na; ++i2) {
                 double t = Mc[i2 * 16 + j];
                 for (int k = 0; k < j; ++k) t -= Mc[i2 * 16 + k] * Mc[j * 16 + k];
                 Mc[i2 * 16 + j] = t / d;
             }
         }
         double* v = Mc + 256;
-        for (int i2 = 0; i2 < na4; ++i2) {
+        for (int i2 = 0; i2 < na; ++i2) {
             double t = v[i2];
             for (int k = 0; k < i2; ++k) t -= Mc[i2 * 16 + k] * v[k];
             v[i2] = t / Mc[i2 * 16 + i2];
         }
-        for (int i2 = na4 - 1; i2 >= 0; --i2) {
+        for (int i2 = na - 1; i2 >= 0; --i2) {
             double t = v[i2];
-            for (int k = i2 + 1; k < na4; ++k) t -= Mc[k * 16 + i2] * v[k];
+            for (int k = i2 + 1; k < na; ++k) t -= Mc[k * 16 + i2] * v[k];
             v[i2] = t / Mc[i2 * 16 + i2];
             P.yF[P.nb + i2] = v[i2];
         }
@@ -959,17 +944,163 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
     }
 }
 
-// y_band = y0 - Yb x_c, written in F order; also the solve-failure flag
-__global__ void bcr_final_kernel(BcrArgs b, DevProblem P) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e == 0) P.scal[kScSolveFail] = b.fail[0];
-    if (e >= P.nb) return;
-    const int ci = (int)(e / 6), I = ci / b.K, row = (ci - I * b.K) * 6 + (int)(e % 6);
-    const double* Y = b.Y + ((size_t)I * M + row) * b.nrhs;
-    double v = Y[0];
-    for (int a = 0; a < P.iw * P.nintr; ++a) v -= Y[1 + a] * P.yF[P.nb + a];
-    P.yF[e] = v;
+// ---- back substitution, one column --------------------------------------------
+//   y_i = X_i' (z'_i - Wl_i y_{i-s} - Wr_i y_{i+s}),  z'_i = z_i[:, 0] - z_i[:, E] x_c
+// for block i eliminated at stride s (the root, block 0: no neighbours); its
+// real rows go to yF.  256 threads: thread (row, p) takes 32 of the row's 128
+// [Wl | Wr] coefficients, then 16 of the rows of X' (X staged in LDS);
+// four-lane sums in a fixed order.
+// FLOW: every block of every level in one launch, top-down (workgroup k waits
+// only for workgroups < k, so any residency makes progress).  y_i (64
+// doubles) is handed over as 128 tagged granules {epoch, 32 bits} stored
+// write-through (Guideline 16 R2: the data is the flag, no fence either
+// side): a consumer's wave 0 re-reads its neighbours' granules until every
+// tag holds this solve's epoch, after staging everything the forward pass
+// left.  The last workgroup to finish publishes the solve verdict.
+constexpr int kYG = 128;   // granules per block
+__device__ __forceinline__ void put_y(unsigned long long* g, int row, double v, unsigned epoch) {
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(v), tag = (unsigned long long)epoch << 32;
+    __hip_atomic_store((gu64*)(g + 2 * row), tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)(g + 2 * row + 1), tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// wave 0: granules of y_a (and y_b) into LDS dst_a / dst_b as doubles
+__device__ __forceinline__ void get_y(const unsigned long long* ga, const unsigned long long* gb, double* dst_a,
+                                      double* dst_b, unsigned epoch, double* fail) {
+    const int lane = threadIdx.x & 63;
+    unsigned va[2], vb[2];
+    for (unsigned spins = 0;;) {
+        bool ok = true;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const unsigned long long x = __hip_atomic_load((gu64*)(ga + lane + 64 * h), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            va[h] = (unsigned)x;
+            ok &= (unsigned)(x >> 32) == epoch;
+            if (gb) {
+                const unsigned long long y = __hip_atomic_load((gu64*)(gb + lane + 64 * h), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                vb[h] = (unsigned)y;
+                ok &= (unsigned)(y >> 32) == epoch;
+            }
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) {   // ~ seconds: a lost producer, never a normal wait
+            if (lane == 0) st_sc1(fail + 1, 1.0);   // a wait timeout, not a numerical failure
+            break;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        reinterpret_cast<unsigned*>(dst_a)[lane + 64 * h] = va[h];   // little endian: granule 2j = low word of y_j
+        if (gb) reinterpret_cast<unsigned*>(dst_b)[lane + 64 * h] = vb[h];
+    }
+}
+
+template <bool FLOW>
+__global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, int s_arg, unsigned epoch) {
+    __shared__ double Xs[M * LD];
+    __shared__ double u[M];
+    __shared__ double yl[M], yr[M];
+    int i = -1, s = 0;
+    if (FLOW) {   // workgroup k: the root, then the odd blocks of s_top / 2, ..., 1
+        int k = blockIdx.x;
+        if (k == 0) {
+            i = 0;
+        } else {
+            --k;
+            for (s = s_arg / 2; s >= 1; s >>= 1) {
+                const int n_odd = (b.N - s + 2 * s - 1) / (2 * s);
+                if (k < n_odd) {
+                    i = s + 2 * s * k;
+                    break;
+                }
+                k -= n_odd;
+            }
+        }
+    } else {      // one level: s_arg = 0 the root, else its odd blocks
+        s = s_arg;
+        i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
+    }
+    unsigned long long* Yg = reinterpret_cast<unsigned long long*>(b.Y);   // [N][kYG] granules
+    const int t = threadIdx.x, row = t >> 2, p = t & 3;
+    const bool valid = i >= 0 && i < b.N;
+    if (valid) {
+        const int l = i - s, r = i + s;
+        const bool hl = s > 0, hr = s > 0 && r < b.N;
+        const bool use = p < 2 ? hl : hr;
+        // everything of the forward pass first: this row's [Wl | Wr]
+        // coefficients, X into LDS, and z'_row
+        double w[32];
+        if (use) {
+            const double2* src = reinterpret_cast<const double2*>(
+                (p < 2 ? b.Wl : b.Wr) + (size_t)i * M * M + row * M + 32 * (p & 1));
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const double2 v = src[q];
+                w[2 * q] = v.x;
+                w[2 * q + 1] = v.y;
+            }
+        }
+        load_tile<64, M, NT>(Xs, LD, b.L + (size_t)i * M * M, M);
+        double zr = 0.0;
+        if (p == 0) {
+            const double* z = b.Z + ((size_t)i * M + row) * b.nrhs;
+            const double* xc = P.yF + P.nb;
+            zr = z[0];
+            for (int a = 0; a < P.iw * P.nintr; ++a) zr -= z[1 + a] * xc[a];
+        }
+        if (hl) {
+            if (t < 64) {
+                if (FLOW) get_y(Yg + (size_t)l * kYG, hr ? Yg + (size_t)r * kYG : nullptr, yl, yr, epoch, b.fail);
+                else {   // an earlier launch wrote them
+                    for (int e = t; e < 2 * kYG; e += 64) {
+                        const bool right = e >= kYG;
+                        if (right && !hr) break;
+                        reinterpret_cast<unsigned*>(right ? yr : yl)[e & (kYG - 1)] =
+                            (unsigned)Yg[(size_t)(right ? r : l) * kYG + (e & (kYG - 1))];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        double acc = 0.0;
+        if (use) {
+            const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
+#pragma unroll
+            for (int q = 0; q < 32; ++q) acc = fma(w[q], y[q], acc);
+        }
+        acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
+        acc += __shfl_xor(acc, 2);
+        if (p == 0) u[row] = zr - acc;
+        __syncthreads();
+        // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
+        // exact zeros above the diagonal; the tiles above are never written)
+        double a2 = 0.0;
+        if (p >= (row >> 4)) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) a2 = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], a2);
+        }
+        a2 += __shfl_xor(a2, 1);
+        a2 += __shfl_xor(a2, 2);
+        if (p == 0) {
+            put_y(Yg + (size_t)i * kYG, row, a2, epoch);
+            const int nreal = min(b.K, P.ncam - i * b.K) * 6;
+            if (row < nreal) P.yF[(size_t)i * b.K * 6 + row] = a2;
+        }
+    }
+    if (FLOW) {   // the last workgroup publishes the verdict (every timeout word drained before its ticket)
+        unsigned* counter = reinterpret_cast<unsigned*>(b.fail + 5);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0 &&
+            __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
+            P.scal[kScSolveFail] = solve_verdict(b.fail);
+    }
+}
+
+// the verdict after per-level back substitution launches
+__global__ void bcr_verdict_kernel(BcrArgs b, DevProblem P) { P.scal[kScSolveFail] = solve_verdict(b.fail); }
 
 }  // namespace
 
@@ -985,14 +1116,14 @@ void bcr_setup(BcrArgs& b, const DevProblem& P) {
 
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
-    // A C L(=X) Wl Wr | R R0 Z Y | part | fail | y flags (one word per block)
-    return 5 * mm + 4 * mr + 512 * (size_t)b.N + 8 + ((size_t)b.N + 1) / 2 + 2;
+    // A C L(=X) Wl Wr | R Z Y | part | fail (+ counters) | y flags (one word per block)
+    return 5 * mm + 3 * mr + 512 * (size_t)b.N + 8 + ((size_t)b.N + 1) / 2 + 2;
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
     b.A = base; b.C = b.A + mm; b.L = b.C + mm; b.Wl = b.L + mm; b.Wr = b.Wl + mm;
-    b.R = b.Wr + mm; b.R0 = b.R + mr; b.Z = b.R0 + mr; b.Y = b.Z + mr;
+    b.R = b.Wr + mm; b.Z = b.R + mr; b.Y = b.Z + mr;
     b.part = b.Y + mr; b.fail = b.part + 512 * (size_t)b.N;
     b.yflag = reinterpret_cast<unsigned*>(b.fail + 8);   // zeroed by the caller once
 }
@@ -1005,50 +1136,44 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);
     const size_t lds_l = std::max(lds_odd, lds_even);
     const size_t lds_t = (3 * M * LD + 3 * M * ldr + 34) * sizeof(double);
-    const size_t lds_b = (3 * M * LD + 3 * M * ldr) * sizeof(double);
     static bool attr = false;
     if (!attr) {   // sized for the largest nrhs (32)
         const int cap = 160 * 1024;
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_level_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_back_all_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
         attr = true;
     }
     int s_top = 1;
     for (int stride = 1; stride < b.N; stride *= 2) {
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
         const int n_even = stride > 1 ? (b.N + 2 * stride - 1) / (2 * stride) : 0;
-        hipLaunchKernelGGL(bcr_level_kernel, dim3(4 * (n_odd + n_even)), dim3(NTL), lds_l, s, b, stride, n_odd);
+        hipLaunchKernelGGL(bcr_level_kernel, dim3(32 * ((n_odd + n_even + 7) / 8)), dim3(NTL), lds_l, s, b, stride,
+                           n_odd);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
     hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NTL), lds_t, s, b, s_top / 2);
     SFM_HIP(hipGetLastError());
-    static int n_cu = 0;
-    if (!n_cu) {
-        int dev = 0;
-        SFM_HIP(hipGetDevice(&dev));
-        SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    if (b.N - 1 <= n_cu && b.N > 1 && !std::getenv("SFM_BCR_BACK_LEVELS")) {
-        // one workgroup per odd block, all resident (one per CU at this LDS size)
-        hipLaunchKernelGGL(bcr_back_all_kernel, dim3(b.N - 1), dim3(NT), lds_b, s, b, s_top, epoch);
+    // corner first (one column left for the back substitution), then every
+    // back-substitution level in one top-down dataflow launch
+    hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
+    SFM_HIP(hipGetLastError());
+    int n_back = 1;
+    for (int stride = s_top / 2; stride >= 1; stride /= 2) n_back += (b.N - stride + 2 * stride - 1) / (2 * stride);
+    if (!std::getenv("SFM_BCR_BACK_LEVELS")) {
+        hipLaunchKernelGGL(bcr_back_kernel<true>, dim3(n_back), dim3(NT), 0, s, b, P, s_top, epoch);
         SFM_HIP(hipGetLastError());
-    } else {
+    } else {   // diagnostic: one launch per level
+        hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(1), dim3(NT), 0, s, b, P, 0, epoch);
+        SFM_HIP(hipGetLastError());
         for (int stride = s_top / 2; stride >= 1; stride /= 2) {
-            if (stride >= b.N) continue;
             const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-            hipLaunchKernelGGL(bcr_back_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, stride);
+            hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(n_odd), dim3(NT), 0, s, b, P, stride, epoch);
             SFM_HIP(hipGetLastError());
         }
+        hipLaunchKernelGGL(bcr_verdict_kernel, dim3(1), dim3(1), 0, s, b, P);
+        SFM_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(bcr_corner_part_kernel, dim3(b.N), dim3(64), 0, s, b, P.iw * P.nintr);
-    SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(bcr_corner_kernel, dim3(1), dim3(NT), 0, s, b, P, radius);
-    SFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(bcr_final_kernel, dim3((unsigned)((P.nb + 255) / 256 + 1)), dim3(256), 0, s, b, P);
-    SFM_HIP(hipGetLastError());
 }
 
 
@@ -1092,7 +1217,7 @@ __global__ __launch_bounds__(256) void dense_pack_kernel(DenseArgs d, DevProblem
         d.A[e] = v;
     }
     if (e < np) d.b[e] = e < P.nF ? P.rhs[e] : 0.0;
-    if (e == 0) d.fail[0] = 0.0;
+    if (e == 0) { d.fail[0] = 0.0; d.fail[1] = 0.0; }
 }
 
 // column k: workgroup w handles row tile i = k + w
@@ -1235,7 +1360,7 @@ __global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem 
     __syncthreads();
     if (k == 0) {
         for (int64_t e = threadIdx.x; e < P.nF; e += NT) P.yF[e] = e < M ? xk[e] : d.x[e];
-        if (threadIdx.x == 0) P.scal[kScSolveFail] = d.fail[0];
+        if (threadIdx.x == 0) P.scal[kScSolveFail] = solve_verdict(d.fail);
         return;
     }
     const int i = blockIdx.x;   // < k
@@ -1269,7 +1394,7 @@ __device__ __forceinline__ void dense_wait_x(const unsigned* flag, unsigned epoc
         while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 22)) {
-                __hip_atomic_store(fail, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fail + 1, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // timeout
                 break;
             }
         }
@@ -1323,7 +1448,7 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
     if (threadIdx.x == 0) {
         __hip_atomic_store(d.xflag + k, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // block 0 finishes last (it waits for every other x): the solve's verdict
-        if (k == 0) P.scal[kScSolveFail] = __hip_atomic_load(d.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0) P.scal[kScSolveFail] = solve_verdict(d.fail);
     }
 }
 
@@ -1384,7 +1509,7 @@ __device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const uns
         while (!ready(m0)) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 22)) {
-                __hip_atomic_store(fail, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fail + 1, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // timeout
                 break;
             }
         }
@@ -1611,7 +1736,7 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         }
         df_publish(fx + k, epoch);
         if (k == 0 && threadIdx.x == 0)   // every other task feeds x_0: the verdict is final
-            P.scal[kScSolveFail] = __hip_atomic_load(d.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            P.scal[kScSolveFail] = solve_verdict(d.fail);
     };
     const int ntask = df_tasks(nt);
     for (int t = blockIdx.x - 1; t < ntask; t += gridDim.x - 1) {

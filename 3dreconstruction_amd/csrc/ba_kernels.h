@@ -16,11 +16,15 @@ enum : int {
     kScXnorm2F, kScStepnorm2F, kScGmaxF, kScSolveFail,                   // replicated
     kScCount
 };
+// kScSolveFail: 0 solved, 1 numerical failure (an invalid LM step),
+// kSolveWaitTimeout a dataflow solve's wait timed out (a device error)
+constexpr double kSolveWaitTimeout = 2.0;
 constexpr int kScSumBegin = 0, kScSumEnd = 5, kScMaxBegin = 5, kScMaxEnd = 9;
 constexpr int kPartT = 5;  // per step block: model acc, cand cost, step norm^2, step bad, cand bad
 
 struct DevProblem {
     int32_t n_img, n_intr, n_spt, n_sobs, n_chunk, ncam, nintr, D;
+    int32_t n_group;                // tile groups (one Schur workgroup and one tile each)
     int32_t n_cpt, n_gpt;           // chunk points [0, n_cpt), general points [n_cpt, n_spt)
     int32_t gz_max;                 // Z doubles of the largest general point
     int32_t dense;                  // RCS stored dense (Sdense) rather than band + arrow
@@ -35,6 +39,7 @@ struct DevProblem {
     const int32_t* obs_slot;
     const double* obs_uv;
     const ChunkDesc* chunks;
+    const int32_t* group_off;       // [n_group + 1] chunk range of a tile group
     const int32_t* img_obs_ptr;
     const int32_t* img_pt;          // image order (img_obs_ptr): point, measurement
     const double* img_uv;
@@ -73,7 +78,7 @@ struct DevProblem {
     // state
     double* scaleE;     // [3*n_spt]
     double* scaleF;     // [nF]
-    double* tiles;      // [n_chunk][80][80]
+    double* tiles;      // [n_group][80][80]
     double* U;          // [n_img * kGramSeg][FW * FW], FW = 6 + iw
     double* Ub;         // [n_img * kGramSeg][FW]
     double* Ucn;        // [n_img * kGramSeg][FW]

@@ -579,18 +579,22 @@ __global__ void fscale_kernel(DevProblem P) {
 }
 
 // ---------------------------------------------------------------------------
-// Schur chunk kernel: one wavefront per chunk
+// Schur chunk kernel: one workgroup per tile group, one wavefront per chunk
 //
-// The wave owns the chunk's whole 80x80 tile as 15 lower 16x16 fp64 MFMA
-// accumulators and walks the chunk in batches of <= kSubPts points /
-// <= kSubObs (= 64) observations:
+// A tile group's chunks (<= kGroupChunks) share one slot layout.  Each wave
+// owns its chunk's whole 80x80 tile as 15 lower 16x16 fp64 MFMA accumulators
+// and walks the chunk in batches of <= kSubPts points / <= kSubObs (= 64)
+// observations:
 //   A  lane = observation: linearise, Jacobi-scale, stage Jx | f | J_intr
 //   B  lane = point: V + D^2, Cholesky, L^-1, w = L^-1 g  (panel row 79)
 //   C  lane = observation: M = Jx L^-T, camera rows of Z = J_c' M
 //   C2 lane = (point, column): intrinsics rows of Z, ordered sum
 //   D  tile -= panel panel' : ceil(3 npts / 4) k-steps x 15 MFMAs
-// No block barriers: co-resident waves overlap each other's VALU and MFMA
-// phases.  Every sum has a fixed order, so results are bit-reproducible.
+// Inside the batch loop each wave syncs only itself (its LDS is its own), so
+// co-resident waves overlap each other's VALU and MFMA phases; at the end the
+// group's waves add their tiles in LDS in wave order and wave 0 writes the
+// group's one tile.  Every sum has a fixed order, so results are
+// bit-reproducible.
 // ---------------------------------------------------------------------------
 
 __device__ __forceinline__ unsigned long long stamp() {
@@ -599,7 +603,15 @@ __device__ __forceinline__ unsigned long long stamp() {
     return t;
 }
 
-// copy the chunk's staged cameras' CamPre into LDS (one wave)
+// wave-local LDS exchange: every lane's writes visible to the wave
+// (LDS-only fences: the exchange is through LDS, so the fences need not
+// order, or wait for, the wave's global accesses -- e.g. a prefetch in flight)
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
 // LDS copy of a CamPre padded to 240 B (60 dwords): lanes of a batch read up
 // to 10 different cameras' fields at once, and a 60-dword stride puts their
 // 16-byte reads on disjoint banks (224 B = 56 dwords collided: 56 * 8 = 0 mod 64)
@@ -607,15 +619,6 @@ struct alignas(16) CamPreL {
     CamPre cp;
     double pad[2];
 };
-__device__ __forceinline__ void stage_campre(const ChunkDesc& cd, const CamPre* __restrict__ cps, CamPreL* dst) {
-    constexpr int kCpW = sizeof(CamPre) / 8;
-    for (int e = threadIdx.x; e < cd.n_cams * kCpW; e += 64) {
-        const int t = e / kCpW;
-        reinterpret_cast<double*>(&dst[t].cp)[e - t * kCpW] =
-            reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
-    }
-}
-
 // next wave batch from p0: <= kSubPts points and <= kSubObs observations
 // (cpoff = chunk-relative point offsets in LDS); returns its point count
 template <int SP = kSubPts, int SO = kSubObs>
@@ -653,7 +656,7 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 // point_scale_kernel computes) from the unscaled Jx it linearises anyway,
 // writes them to scaleE and uses them, instead of a separate pass.
 template <int CM, int NT, int SP = kSubPts, int SO = kSubObs, bool SE = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WPE, SFM_SCHUR_WPE))) void schur_kernel(
+__global__ __launch_bounds__(64 * schur_group(NT)) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WPE, SFM_SCHUR_WPE))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
     constexpr int IW = kIW<CM>;   // tile rows (and F columns) of an intrinsics block
@@ -672,53 +675,80 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
     // that the intrinsics pass updates at one column on distinct banks, and
     // 14-double observation rows spread ds_write_b128 lane groups.
     constexpr int kPK = 4 * ((3 * SP + 3) / 4), kPR = 16 * NT, kPS = kPR + 4;
-    __shared__ double panel[kPK][kPS];          // [k][row]
-    __shared__ double wcol[NT == 4 ? kPK : 1];  // NT = 4: w = L^-1 g_E per panel column
     // per-observation rows use odd strides (in doubles): a wave's ds_*_b64 at
     // lane-strided rows then hits 32 distinct bank pairs (even strides of 4,
     // 6, 10 doubles were 2- to 4-way bank conflicts, SQ_LDS_BANK_CONFLICT)
     // pinhole: the 4 nonzeros of J_intr; SNAVELY / RADIAL3: both rows of every
     // parameter column (2 NK values)
     constexpr int kOb = CM == SFM_CAM_PINHOLE ? 5 : 2 * NK + 1;
-    __shared__ double ob[SO][kOb];              // J_intr nonzeros (scaled) | pad
-    // per observation: Jx'Jx (6) | Jx'f (3) until the per-point sums, then
-    // M = Jx L^-T (6) from phase B on (obm: the same rows; 3.5 KB less LDS per
-    // wave, which is what the chip's co-resident wave count divides)
-    __shared__ double vs[SO][9];
-    __shared__ double vsum[SP][10];             // per point: V (6) | g_E (3)
-    double (*const obm)[9] = vs;
-    __shared__ int orow[SO];                    // tile row of the obs' intrinsics block
-    // chunk-level staging: every camera / intrinsics block the chunk touches
+    constexpr int kNTiles = NT * (NT + 1) / 2;
+    constexpr int kComb = 5;                    // tiles per round of the group's tile sum
+    // each wave's own LDS; its space also carries the wave's tiles to wave 0
+    // at the end (kComb 16x16 tiles per round)
+    struct WaveLds {
+        double panel[kPK][kPS];                 // [k][row]
+        double wcol[NT == 4 ? kPK : 1];         // NT = 4: w = L^-1 g_E per panel column
+        double ob[SO][kOb];                     // J_intr nonzeros (scaled) | pad
+        // per observation: Jx'Jx (6) | Jx'f (3) until the per-point sums, then
+        // M = Jx L^-T (6) from phase B on (obm: the same rows)
+        double vs[SO][9];
+        double vsum[SP][10];                    // per point: V (6) | g_E (3)
+        int orow[SO];                           // tile row of the obs' intrinsics block
+        int cpoff[kChunkPts + 1];               // chunk point offsets, relative to obs_begin
+    };
+    union WaveU {
+        WaveLds w;
+        double comb[kComb * 256 + 64];          // kComb tiles + the NT = 4 -Zw column
+    };
+    static_assert(sizeof(WaveLds) >= sizeof(double) * (kComb * 256 + 64), "tile hand-over space");
+    constexpr int GW = schur_group(NT);         // waves (chunks) per group
+    __shared__ WaveU wl[GW];
+    // group-level staging: every camera / intrinsics block the group touches
     __shared__ CamPreL scp[kCamSlots];
     __shared__ double csc[kCamSlots][6];        // camera column scales (0: constant image)
     __shared__ double isc[kIntrSlots][2 * IW];  // intrinsics | their column scales
     __shared__ int crow[kCamSlots], irow[kIntrSlots];
-    __shared__ int cpoff[kChunkPts + 1];        // chunk point offsets, relative to obs_begin
-    const int c = blockIdx.x, lane = threadIdx.x;
+    // wave-uniform (scalar): the LDS bases and chunk fields below stay in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, grp = blockIdx.x;
+    const int c0 = P.group_off[grp], n_sub = P.group_off[grp + 1] - c0;
+    const int c = c0 + (wave < n_sub ? wave : 0);   // this wave's chunk (a wave past the group's chunks idles)
     const ChunkDesc& cd = P.chunks[c];
-    const int pb = cd.pt_begin, np = cd.pt_end - pb, ob0 = cd.obs_begin;
+    WaveLds& W = wl[wave].w;
+    double (&panel)[kPK][kPS] = W.panel;
+    double (&wcol)[NT == 4 ? kPK : 1] = W.wcol;
+    double (&ob)[SO][kOb] = W.ob;
+    double (&vs)[SO][9] = W.vs;
+    double (&vsum)[SP][10] = W.vsum;
+    double (*const obm)[9] = vs;
+    int (&orow)[SO] = W.orow;
+    int (&cpoff)[kChunkPts + 1] = W.cpoff;
+    const int pb = cd.pt_begin, np = wave < n_sub ? cd.pt_end - pb : 0, ob0 = cd.obs_begin;
     // read once: a ChunkDesc load inside the batch loop would be waited on
     // with the in-order counter, i.e. together with the next batch's prefetch
     const bool one_intr = cd.n_intr == 1;
     const double inv_radius = 1.0 / radius;   // LM diagonal D^2 = clamp(diag) / radius (as step_kernel)
 
     for (int e = lane; e <= np; e += 64) cpoff[e] = P.pt_off[pb + e] - ob0;
-    stage_campre(cd, cps, scp);
-    {
-        for (int e = lane; e < cd.n_cams * 6; e += 64) {
+    {   // the group's staging, by all its waves
+        constexpr int kCpW = sizeof(CamPre) / 8;
+        for (int e = threadIdx.x; e < cd.n_cams * kCpW; e += 64 * GW) {
+            const int t = e / kCpW;
+            reinterpret_cast<double*>(&scp[t].cp)[e - t * kCpW] =
+                reinterpret_cast<const double*>(&cps[cd.cam_img[t]])[e - t * kCpW];
+        }
+        for (int e = threadIdx.x; e < cd.n_cams * 6; e += 64 * GW) {
             const int t = e / 6, col = cd.cam_col[t];
             csc[t][e - 6 * t] = col >= 0 ? P.scaleF[col + e - 6 * t] : 0.0;
         }
-        if (lane < cd.n_cams) crow[lane] = cd.cam_row[lane];
-        if (lane < IW * cd.n_intr) {
-            const int t = lane / IW, k = lane - IW * t;
+        if (threadIdx.x < cd.n_cams) crow[threadIdx.x] = cd.cam_row[threadIdx.x];
+        if (threadIdx.x < IW * cd.n_intr) {
+            const int t = threadIdx.x / IW, k = threadIdx.x - IW * t;
             isc[t][k] = intr[IW * cd.intr_id[t] + k];
             isc[t][IW + k] = P.scaleF[cd.intr_col[t] + k];
         }
-        if (lane < cd.n_intr) irow[lane] = cd.intr_row[lane];
+        if (threadIdx.x < cd.n_intr) irow[threadIdx.x] = cd.intr_row[threadIdx.x];
     }
 
-    constexpr int kNTiles = NT * (NT + 1) / 2;
     v4d acc[kNTiles];
 #pragma unroll
     for (int q = 0; q < kNTiles; ++q) acc[q] = v4d{0.0, 0.0, 0.0, 0.0};
@@ -790,7 +820,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
                     for (int a = 0; a < 3; ++a) obm[lane][3 * r + a] = L.Jx[r][a];
             }
-            __syncthreads();
+            wsync();
             if (lane < 3 * npts) {
                 const int pt = lane / 3, a = lane - 3 * pt;
                 const int q0 = cpoff[p0 + pt] - o0, q1 = cpoff[p0 + pt + 1] - o0;
@@ -803,12 +833,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
                 vsum[pt][a] = se;   // vsum is rewritten after phase A
                 P.scaleE[3 * (size_t)(pb + p0 + pt) + a] = se;
             }
-            __syncthreads();
+            wsync();
             if (lane < nobs) {
 #pragma unroll
                 for (int a = 0; a < 3; ++a) sE[a] = vsum[pl][a];
             }
-            __syncthreads();   // vsum is reused by the per-point sums below
+            wsync();   // vsum is reused by the per-point sums below
         }
         if (lane < nobs) {
 #pragma unroll
@@ -846,7 +876,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
             }
             orow[lane] = irow[is];
         }
-        __syncthreads();
+        wsync();
         // per-point sums in observation order, one lane per (point, entry)
         if (lane < 9 * npts) {
             const int pt = lane / 9, e = lane - 9 * pt;
@@ -860,7 +890,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
             for (; q < q1; ++q) acc += vs[q][e];
             vsum[pt][e] = acc;
         }
-        __syncthreads();
+        wsync();
         SFM_STAMP(1)
         // ---- B: every observation lane takes its point's V + D^2 and g_E (the
         // per-point sums above: identical on all lanes of the point), factors
@@ -921,7 +951,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
                 for (int a = 0; a < 3; ++a) obm[lane][3 * r + a] = M[r][a];
         }
-        __syncthreads();
+        wsync();
         SFM_STAMP(2)
         // ---- C2: intrinsics rows, ordered per point ---------------------------
         // (register sums per run of observations sharing an intrinsics block)
@@ -1036,7 +1066,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
             panel[3 * pt + a][row + 0] += z0; panel[3 * pt + a][row + 1] += z1;
             panel[3 * pt + a][row + 2] += z2; panel[3 * pt + a][row + 3] += z3;
         }
-        __syncthreads();
+        wsync();
         SFM_STAMP(3)
         // ---- D: tile += panel panel' on the fp64 MFMA -------------------------
         // all operands first (padding columns are zero), then the MFMAs
@@ -1056,33 +1086,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WP
 #pragma unroll
             for (int k = 0; k < kPK; ++k) wacc += panel[k][lane] * wcol[k];
         }
-        __syncthreads();
+        wsync();
         SFM_STAMP(4)
         p0 = p1;
     }
-    // ---- write the negated tile: its lower 16x16 tiles only (the gather reads
-    // upper blocks at their symmetric partner, FlatTerm modes), row-contiguous
-    double* out = P.tiles + (size_t)c * kTileR * kTileR;
-    if (NT == 4) out[kTileWRow * kTileR + lane] = -wacc;
+    // ---- the group's tile: waves 1.. hand their accumulators to wave 0
+    // through their own LDS, kComb 16x16 tiles per round, added in wave order;
+    // wave 0 writes the negated tile, its lower 16x16 tiles only (the gather
+    // reads upper blocks at their symmetric partner, FlatTerm modes)
+    __syncthreads();   // every wave is past its batch loop: its LDS is free
+    double* out = P.tiles + (size_t)grp * kTileR * kTileR;
 #pragma unroll
-    for (int q = 0; q < kNTiles; ++q) {
-        const int ti = kTi[q], tj = kTj[q];
+    for (int q0 = 0; q0 < kNTiles; q0 += kComb) {
+        if (wave > 0 && wave < n_sub) {
+            double* cb = wl[wave].comb;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 16 * ti + (lane >> 4) + 4 * r, col = 16 * tj + (lane & 15);
-            out[row * kTileR + col] = -acc[q][r];
+            for (int q = q0; q < q0 + kComb && q < kNTiles; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cb[(q - q0) * 256 + r * 64 + lane] = acc[q][r];
+            if (NT == 4 && q0 == 0) cb[kComb * 256 + lane] = wacc;
         }
+        __syncthreads();
+        if (wave == 0) {
+            for (int w2 = 1; w2 < n_sub; ++w2) {
+                const double* cb = wl[w2].comb;
+#pragma unroll
+                for (int q = q0; q < q0 + kComb && q < kNTiles; ++q)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[q][r] += cb[(q - q0) * 256 + r * 64 + lane];
+                if (NT == 4 && q0 == 0) wacc += cb[kComb * 256 + lane];
+            }
+#pragma unroll
+            for (int q = q0; q < q0 + kComb && q < kNTiles; ++q) {
+                const int ti = kTi[q], tj = kTj[q];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * ti + (lane >> 4) + 4 * r, col = 16 * tj + (lane & 15);
+                    out[row * kTileR + col] = -acc[q][r];
+                }
+            }
+            if (NT == 4 && q0 == 0) out[kTileWRow * kTileR + lane] = -wacc;
+        }
+        if (q0 + kComb < kNTiles) __syncthreads();   // wave 0 has read this round
     }
-    // ---- point partials (fixed-order wave reduction) --------------------------
+    // ---- point partials of this wave's chunk (fixed-order wave reduction) ----
     double s1[1] = {xn2};
     wave_sum(s1);
     const double m1 = wave_max(gmx);
-    if (lane == 0) {
+    if (lane == 0 && wave < n_sub) {
         P.part_s[2 * (size_t)c] = s1[0];
         P.part_s[2 * (size_t)c + 1] = m1;
     }
     SFM_STAMP(5)
-    if (stamps && lane == 0)
+    if (stamps && lane == 0 && wave < n_sub)
         for (int k = 0; k < 6; ++k) stamps[6 * (size_t)c + k] = tacc[k];
 #undef SFM_STAMP
 }
@@ -1123,15 +1179,6 @@ constexpr int kLongTerms = 256;
 // vectors_only (iteration 0, before the Jacobi scales): bF and cnF only
 __device__ __forceinline__ bool skip_kind(int kind, int vectors_only) {
     return vectors_only && kind != kDstBF && kind != kDstCnF;
-}
-
-// wave-local LDS exchange: every lane's writes visible to the wave
-// (LDS-only fences: the exchange is through LDS, so the fences need not
-// order, or wait for, the wave's global accesses -- e.g. a prefetch in flight)
-__device__ __forceinline__ void wsync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 __global__ void reduce_kernel(DevProblem P, int vectors_only) {
@@ -2512,23 +2559,23 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
             });
         SFM_HIP(hipGetLastError());
     }
-    if (P.n_chunk <= 0) return;
+    if (P.n_group <= 0) return;
     // 64-row tiles: batches of schur4_pts(CM) points (ba_types.h) at 8 waves
     // per CU (6-point batches' LDS allows 7, and measured 9% slower)
     if (P.tile_nt == 4) {
         if (scale_e)
             SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, schur4_pts(CM), schur4_obs(CM), true>),
-                                               dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+                                               dim3(P.n_group), dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
         else
             SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 4, schur4_pts(CM), schur4_obs(CM)>),
-                                               dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+                                               dim3(P.n_group), dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
     } else {
         if (scale_e)
             SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO, true>),
-                                               dim3(P.n_chunk), dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+                                               dim3(P.n_group), dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
         else
-            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO>), dim3(P.n_chunk),
-                                               dim3(64), 0, s, P, cp, intr, X, radius, stamps));
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO>), dim3(P.n_group),
+                                               dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
     }
     SFM_HIP(hipGetLastError());
 }

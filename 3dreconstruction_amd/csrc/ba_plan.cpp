@@ -442,6 +442,11 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     constexpr int64_t kTargetChunks = 2048;
     int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
     if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));   // tuning override
+    // Chunks of one tile group share one slot layout and one tile: the Schur
+    // kernel runs a group as one workgroup, a wave per chunk, and adds the
+    // waves' tiles in LDS (wave order) before the one write -- a quarter of the
+    // tile traffic and of the reduce plan's tile terms of single-chunk tiles
+    int group_pts = kGroupChunks * chunk_pts;   // set per tile height (schur_group) before each chunking
     const int32_t ncp = (int32_t)pl.n_cpt;
     auto point_flops = [](int64_t rows, int64_t nobs) {
         // algorithmic flops: the symmetric Z Z' over the
@@ -473,13 +478,25 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             for (int q : intrs) intr_idx[q] = -1;
             cams.clear(); intrs.clear(); dcams.clear(); rows = 0;
         };
+        // a tile group: its points split evenly into <= kGroupChunks chunks of
+        // <= chunk_pts points, every chunk carrying the group's slot layout
         auto close = [&](int32_t p_end) {
             cd.pt_end = p_end;
             cd.obs_end = pl.pt_off[p_end];
             cd.n_slots = (int32_t)(cams.size() + intrs.size());
             cd.n_cams = (int32_t)dcams.size();
             cd.n_intr = (int32_t)intrs.size();
-            chunks_out.push_back(cd);
+            const int32_t p0 = cd.pt_begin, npg = p_end - p0;
+            const int n_sub = std::max(1, (npg + chunk_pts - 1) / chunk_pts);
+            for (int j = 0; j < n_sub; ++j) {
+                ChunkDesc sub = cd;
+                sub.pt_begin = p0 + (int32_t)((int64_t)npg * j / n_sub);
+                sub.pt_end = p0 + (int32_t)((int64_t)npg * (j + 1) / n_sub);
+                sub.obs_begin = pl.pt_off[sub.pt_begin];
+                sub.obs_end = pl.pt_off[sub.pt_end];
+                sub.sub = j;
+                chunks_out.push_back(sub);
+            }
         };
         // per-point image lists in fixed storage (<= kSubObs each): this loop
         // runs once per point, and heap vectors here dominated planning time
@@ -510,7 +527,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             for (int q : pi) if (intr_idx[q] < 0) { add += pl.iw; ++add_slots; ++add_i; }
             for (int img : pd) if (dcam_idx[img] < 0) ++add_d;
             const bool full = k > cd.pt_begin &&
-                              (rows + add > cap || k - cd.pt_begin >= chunk_pts ||
+                              (rows + add > cap || k - cd.pt_begin >= group_pts ||
                                (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots ||
                                (int)dcams.size() + add_d > kCamSlots ||
                                (int)intrs.size() + add_i > kIntrSlots);
@@ -557,6 +574,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // host threads (a chunk never spans two ranges: at most 15 extra chunks
     // out of thousands; the split depends on the shard only, never on the host)
     auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, HostVec<int32_t>& slot_out) -> int64_t {
+        int gw = schur_group(cap == 64 ? 4 : 5);
+        if (const char* e = std::getenv("SFM_BA_TILE_GROUP")) gw = std::max(1, std::min(gw, std::atoi(e)));   // diagnostic
+        group_pts = gw * chunk_pts;
         slot_out.resize(pl.pt_off[ncp]);   // every entry written by its range
         const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(16, ncp / 4096));
         std::vector<std::vector<ChunkDesc>> seg_chunks(nseg);
@@ -630,12 +650,20 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         pl.n_cpt = 0;
         flops = 0;
     }
+    pl.group_off.clear();
+    for (int32_t c = 0; c < (int32_t)pl.chunks.size(); ++c)
+        if (pl.chunks[c].sub == 0) pl.group_off.push_back(c);
+    pl.group_off.push_back((int32_t)pl.chunks.size());
     tm.mark("chunks");
     std::copy(cslot.begin(), cslot.end(), pl.obs_slot.begin());
     pl.n_gpt = pl.n_spt - pl.n_cpt;
     // a general point's observations in image order, so that repeated views
-    // of one image are adjacent (the Z kernel sums runs of one camera block)
-    parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+    // of one image are adjacent (the Z kernel sums runs of one camera block);
+    // the permutation is kept for the plan cache's value refresh
+    const int32_t gobs0 = pl.pt_off[pl.n_cpt];
+    pl.gobs_perm.assign(pl.n_sobs - gobs0, 0);
+    int permuted[16] = {0};
+    parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int t) {
         std::vector<int32_t> idx;
         std::vector<int32_t> img;
         std::vector<double> uv;
@@ -661,9 +689,12 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 pl.obs_img[s0 + q] = img[idx[q]];
                 pl.obs_uv[2 * (s0 + q)] = uv[2 * idx[q]];
                 pl.obs_uv[2 * (s0 + q) + 1] = uv[2 * idx[q] + 1];
+                pl.gobs_perm[s0 + q - gobs0] = idx[q];
+                permuted[t] |= idx[q] != q;
             }
         }
     });
+    if (std::none_of(permuted, permuted + 16, [](int v) { return v != 0; })) pl.gobs_perm.clear();
 
     // ---- general points: their F blocks and Z buffer layout --------------------
     // blocks in F-column order; obs_slot = local camera block (0xffff: constant
@@ -768,7 +799,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     tm.mark("shard_ready");
     pl.schur_flops = flops;
     pl.schur_bytes = pl.n_sobs * (16 + 4 + 4 + 4) + pl.n_spt * (24 + 24 + 4) +
-                     (int64_t)pl.chunks.size() * kTileR * kTileR * 8;
+                     (int64_t)pl.n_group() * kTileR * kTileR * 8;
 
     // ---- observations per image (the image-ordered copy itself is built on
     // the device from the uploaded shard arrays: ba_image_order) -------------
@@ -807,7 +838,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         // exact capacities: one growth-free allocation per list (the lists
         // are fresh memory, so every reallocation is page faults again)
         size_t nm = 3 * (size_t)kGramSeg * P.n_img, nv = 2 * (size_t)kGramSeg * P.n_img, npm = 0, npv = 0;
-        for (const ChunkDesc& cd : pl.chunks) {
+        for (int64_t g = 0; g < pl.n_group(); ++g) {
+            const ChunkDesc& cd = pl.chunks[pl.group_off[g]];
             nm += (size_t)cd.n_slots * (cd.n_slots + 1) / 2;
             nv += (size_t)cd.n_slots;
         }
@@ -854,13 +886,13 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     tm.mark("terms_cnf");
     // chunk tiles: fixed chunk ranges on host threads, appended in chunk order
     {
-        const int32_t nch = (int32_t)pl.chunks.size();
+        const int32_t nch = (int32_t)pl.n_group();   // one tile per group (its first chunk's layout)
         const int nseg = nch >= 128 ? 16 : 1;   // the output is the same for any split
         std::vector<KTVec<ReduceTerm>> sm(nseg), sv(nseg);
         parallel_segments(nseg, [&](int g) {
             const int32_t c0 = (int32_t)((int64_t)nch * g / nseg), c1 = (int32_t)((int64_t)nch * (g + 1) / nseg);
             for (int32_t c = c0; c < c1; ++c) {
-                const ChunkDesc& cd = pl.chunks[c];
+                const ChunkDesc& cd = pl.chunks[pl.group_off[c]];
                 for (int a = 0; a < cd.n_slots; ++a) {
                     const int32_t fa = fb_of_col(cd.slot_col[a]);
                     // rhs contribution (-Z w) from tile row 79

@@ -50,12 +50,22 @@ struct BAHostPlan {
     std::vector<int32_t> zbatch;     // [n][2] general point range [g0, g1)
     std::vector<int32_t> zlong;      // general point ids
     std::vector<int64_t> spt_global;  // shard point -> global point id
+    // a general point's observations are re-sorted by image (chunk points keep
+    // the problem's order): gobs_perm[s - pt_off[n_cpt]] = the problem-local
+    // index (within its point) of shard observation s; empty when every
+    // general point was already in image order.  The plan cache's value
+    // refresh maps new measurements through it (ba_obs_source).
+    std::vector<int32_t> gobs_perm;
     // observation-sized arrays live in page-locked staging memory while a
     // context is bound (HostVec, common.h): uploaded, then released
     HostVec<int32_t> pt_off;          // [n_spt+1]
     HostVec<int32_t> obs_img, obs_slot;
     HostVec<double> obs_uv;
     std::vector<ChunkDesc> chunks;
+    // tile groups: chunks [group_off[g], group_off[g+1]) share one slot
+    // layout and one tile (index g); <= kGroupChunks chunks each
+    std::vector<int32_t> group_off;
+    int64_t n_group() const { return group_off.empty() ? 0 : (int64_t)group_off.size() - 1; }
     int32_t tile_nt = 5;              // 16-row MFMA tiles per chunk side (4 or 5)
     std::vector<int32_t> img_obs_ptr;  // [n_img+1] shard observations per image (prefix)
 

@@ -44,6 +44,7 @@ struct sfm_ba_plan {
         img_coli, img_intr, intr_col, blk_img, blk_intr;
     DBuf<double> obs_uv;
     DBuf<ChunkDesc> chunks;
+    DBuf<int32_t> group_off;   // tile groups of chunks
     DBuf<ReduceTarget> targets;
     DBuf<FlatTerm> terms;
     DBuf<double> X0, Xa, Xb, extr0, intr0, ea, eb, ia, ib;
@@ -111,6 +112,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     h.on_shard_ready = nullptr;
     tm.mark("build_plan");
     up(pl->chunks, h.chunks, s);
+    up(pl->group_off, h.group_off, s);
     up(pl->img_obs_ptr, h.img_obs_ptr, s);
     pl->img_pt.alloc(std::max<int64_t>(h.n_sobs, 1));
     pl->img_uv.alloc(2 * std::max<int64_t>(h.n_sobs, 1));
@@ -153,7 +155,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->scaleF.alloc(nF);
     // per-chunk Schur tiles and per-image Gram slices share one buffer so the
     // reduction terms address every source with a single offset
-    const size_t n_tiles = std::max<size_t>(h.chunks.size(), 1) * kTileR * kTileR;
+    const size_t n_tiles = std::max<size_t>(h.n_group(), 1) * kTileR * kTileR;
     const size_t fw = 6 + (size_t)h.iw;   // F columns of an image block
     const size_t o_u = n_tiles, o_ub = o_u + fw * fw * (size_t)prob.n_img * kGramSeg,
                  o_ucn = o_ub + fw * (size_t)prob.n_img * kGramSeg,
@@ -233,6 +235,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.n_img = prob.n_img; P.n_intr = prob.n_intr;
     P.n_spt = (int32_t)h.n_spt; P.n_sobs = (int32_t)h.n_sobs;
     P.n_chunk = (int32_t)h.chunks.size();
+    P.n_group = (int32_t)h.n_group();
     P.n_cpt = (int32_t)h.n_cpt; P.n_gpt = (int32_t)h.n_gpt;
     P.gz_max = (int32_t)h.gz_max;
     P.dense = h.dense ? 1 : 0;
@@ -248,6 +251,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.iw = h.iw;
     P.pt_off = pl->pt_off.p; P.obs_img = pl->obs_img.p;
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
+    P.group_off = pl->group_off.p;
     P.img_obs_ptr = pl->img_obs_ptr.p;
     P.img_pt = pl->img_pt.p; P.img_uv = pl->img_uv.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
@@ -346,6 +350,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
         bcr_bind(pl->bcr, pl->bcr_buf.p);
         SFM_HIP(hipMemsetAsync(pl->bcr.yflag, 0, sizeof(unsigned) * (size_t)pl->bcr.N, s));
+        // the back substitution's tagged y granules (tags = solve epochs from 1)
+        SFM_HIP(hipMemsetAsync(pl->bcr.Y, 0, sizeof(double) * bcr_y_granules(pl->bcr), s));
         if (std::getenv("SFM_BCR_STAMPS")) {
             pl->bcr_stamps.alloc(8);
             pl->bcr_stamps.zero(s);
@@ -381,7 +387,10 @@ void refresh_values(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* e
         pl->src_off.alloc(prob.n_pt + 1);
         pl->src_off.upload(prob.pt_offsets, prob.n_pt + 1, s);
         pl->obs_src.alloc(h.n_sobs);
-        ba_obs_source(pl->pt_src.p, pl->src_off.p, pl->pt_off.p, (int32_t)h.n_spt, pl->obs_src.p, s);
+        DBuf<int32_t> gperm;   // back to the context's cache, stream-ordered
+        if (!h.gobs_perm.empty()) up(gperm, h.gobs_perm, s);
+        ba_obs_source(pl->pt_src.p, pl->src_off.p, pl->pt_off.p, (int32_t)h.n_spt, (int32_t)h.n_cpt,
+                      h.gobs_perm.empty() ? nullptr : gperm.p, pl->obs_src.p, s);
         tm.mark("maps");
     }
     if (h.n_sobs > 0) {
@@ -577,6 +586,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         cur.iteration = last_iter + 1;
         const double model_change = -sc[kScModelAcc];
         cur.model_cost_change = model_change;
+        SFM_REQUIRE(sc[kScSolveFail] != kSolveWaitTimeout, SFM_ERR_DEVICE,
+                    "RCS solve: a dataflow wait timed out (workgroups not co-resident; another context holding the CUs?)");
         const bool finite = sc[kScSolveFail] == 0.0 && sc[kScStepBad] == 0.0 && std::isfinite(model_change);
         cur.step_is_valid = finite && model_change > 0.0;
         if (!cur.step_is_valid) {

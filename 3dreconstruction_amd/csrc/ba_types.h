@@ -10,7 +10,7 @@
 //              CamPre[n_img] (per-camera rotation terms), scaleF[nF]
 //   RCS      : Sband[ncam][D+1][6][6] (block (i,i-d)), Sarrow[nintr][ncam][4][6],
 //              Scorner[nintr][nintr][4][4], rhs[nF], bF[nF], cnF[nF]
-//   chunk slab: tiles[n_chunk][80][80] (-Z Z^T, row 79 = -Z w)
+//   chunk slab: tiles[n_group][80][80] (-Z Z^T, row 79 = -Z w), one per tile group of <= 4 chunks
 //   image slab: Uimg[n_img][FW][FW], Ub[n_img][FW], Ucn[n_img][FW] (FW = 6 + intrinsics width)
 #pragma once
 #include <cstdint>
@@ -34,6 +34,15 @@ constexpr int kSubObs = 64;               // observations per wave batch (one pe
 constexpr int schur4_pts(int cm) { return cm == 0 ? 5 : 4; }
 constexpr int schur4_obs(int cm) { return cm == 0 ? 52 : cm == 2 ? 44 : 48; }
 constexpr int kChunkPts = 128;            // points per chunk (upper bound; step_kernel threads)
+constexpr int kGroupChunks = 4;           // chunks per tile group, at most (the Schur kernel's waves per workgroup)
+// chunks per tile group by tile height: 4 for 64-row tiles (four waves' LDS
+// is 60-68 KB: two workgroups, 8 waves per CU as one-wave chunks had), 1 for
+// 80-row tiles (their 26-30 KB per wave: two-wave groups would cost the
+// RADIAL3 variant a wave per CU)
+#ifndef SFM_SCHUR_GROUP   // A/B builds: chunks per group of 64-row tiles
+#define SFM_SCHUR_GROUP kGroupChunks
+#endif
+constexpr int schur_group(int tile_nt) { return tile_nt == 4 ? SFM_SCHUR_GROUP : 1; }
 constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
 constexpr int kCamSlots = 14;             // staged cameras per chunk (incl. constant images)
@@ -59,7 +68,8 @@ struct ChunkDesc {
     int32_t pt_begin, pt_end;      // shard point range
     int32_t obs_begin, obs_end;    // shard obs range
     int32_t n_slots;               // F slots (reduce plan)
-    int32_t n_cams, n_intr, pad;   // staged cameras / intrinsics
+    int32_t n_cams, n_intr;        // staged cameras / intrinsics
+    int32_t sub;                   // index within its tile group (the group's slot layout)
     int32_t cam_img[kCamSlots];    // image of a staged camera
     int32_t cam_row[kCamSlots];    // its first tile row, -1 for a constant image
     int32_t cam_col[kCamSlots];    // its first scaleF column, -1 for a constant image

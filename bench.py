@@ -811,6 +811,24 @@ def main():
         loop = bench_loop(ctx, args.loop_images, cpu=not args.no_cpu_baseline)
         loop_fixed = bench_loop(ctx, args.loop_images, cpu=False, fixed_writeback=True, imgs=loop.pop("images"))
         loop_fixed.pop("images", None)
+    elif world > 1 and not args.no_loop:
+        # C5 at N > 1: replicas only (DESIGN.md §7 -- the loop is host bound,
+        # one image after another).  Every rank runs its own sequence on a
+        # one-rank context of its GPU; the line is the aggregate images/s over
+        # the slowest rank's wall time (weak scaling).
+        lctx = api.Context(device=local_rank)
+        barrier()
+        r = bench_loop(lctx, args.loop_images, cpu=False, fixed_writeback=True)
+        r.pop("images", None)
+        lctx.synchronize()
+        lctx.close()
+        t_max = max_over_ranks(r["seconds"])
+        if rank == 0:
+            loop_fixed = dict(r, value=world * args.loop_images / t_max, seconds=t_max, replicas=world,
+                              scaling="weak (independent sequences, one per GPU; DESIGN.md §7)")
+            loop_fixed["metric"] += f", {world} replicas"
+            log(f"loop replicas: {world} x {args.loop_images} images, slowest rank {t_max:.2f}s "
+                f"-> {loop_fixed['value']:.1f} images/s aggregate")
 
     # ---------------- dense-S stress case ----------------
     dense_s = None

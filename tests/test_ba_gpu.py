@@ -242,10 +242,21 @@ def _shard_worker(rank, world, port, out_path, scene_args):
                                         # C2 (BASELINE configs[1]: 200 cams / 50k pts / 500k obs)
                                         dict(n_cam=200, n_pt=50000, k=10, seed=0x5F3D0002)])
 def test_sharded_two_ranks_one_gpu(ctx, tmp_path, scene_args):
+    _check_sharded(ctx, tmp_path, scene_args, 2)
+
+
+def test_sharded_eight_ranks_one_gpu(ctx, tmp_path):
+    # the north_star's 8-way landmark partition through the product (eight
+    # processes on one GPU, the RCS exchange over the host gloo hook): C4's
+    # banded shape at 1/10 size, decision for decision against one rank
+    _check_sharded(ctx, tmp_path, dict(n_cam=100, n_pt=50000, k=10, seed=0x5F3D0008), 8)
+
+
+def _check_sharded(ctx, tmp_path, scene_args, world):
     import torch.multiprocessing as mp
     out = str(tmp_path / "r.npz")
-    port = 31500 + (os.getpid() % 2000)
-    mp.spawn(_shard_worker, args=(2, port, out, scene_args), nprocs=2, join=True)
+    port = 31500 + (os.getpid() % 2000) + 7 * world
+    mp.spawn(_shard_worker, args=(world, port, out, scene_args), nprocs=world, join=True)
     r = np.load(out)
     sc = H.Scene(**scene_args)
     plan = api.BAPlan(ctx, sc.problem(), *sc.params())
@@ -440,4 +451,48 @@ def test_plan_cache_reuse_is_bit_identical(ctx):
     _, os2, _, _ = H.oracle_solve(sc, threads=8)
     assert changed[0] == 0 and changed[1].iterations == os2.iterations
     assert abs(changed[1].rmse_final / os2.rmse_final - 1) < RTOL_COST
+    lib.sfm_ba_cache_clear(ctx.h)
+
+
+def _shuffle_within_points(sc, seed):
+    # each point's observations in a random (non-image) order, measurements
+    # moved with their images: the same problem, a different layout
+    rng = np.random.default_rng(seed)
+    for p in range(sc.n_pt):
+        o0, o1 = int(sc.pt_offsets[p]), int(sc.pt_offsets[p + 1])
+        perm = o0 + rng.permutation(o1 - o0)
+        sc.obs_img[o0:o1] = sc.obs_img[perm].copy()
+        uv = sc.obs_uv.reshape(-1, 2)
+        uv[o0:o1] = uv[perm].copy()
+
+
+@pytest.mark.parametrize("shape", ["long_tracks", "random_visibility"])
+def test_plan_cache_reuse_general_points_bit_identical(ctx, shape):
+    # general points have their observations re-sorted by
+    # image in the plan, so the cache's value refresh must map each new
+    # measurement through that permutation.  Reuse vs a fresh plan, bit for
+    # bit, on general points whose observations are not in image order.
+    lib = abi.load()
+    if shape == "long_tracks":
+        sc = H.Scene(60, 1500, 30, seed=4041)          # 180 F rows per point: all general
+    else:
+        sc = H.Scene(50, 5000, 7, vis_mode=1, seed=4042)   # random visibility: chunks dropped
+    _shuffle_within_points(sc, 7)
+    lib.sfm_ba_cache_clear(ctx.h)
+    cold = _solve_keep(ctx, sc, *sc.params())
+    assert cold[0] == 0
+    rng = np.random.default_rng(2)
+    sc.obs_uv += rng.normal(0, 0.3, sc.obs_uv.shape)
+    sc.X += rng.normal(0, 0.01, sc.X.shape)
+    reused = _solve_keep(ctx, sc, *sc.params())
+    lib.sfm_ba_cache_clear(ctx.h)
+    fresh = _solve_keep(ctx, sc, *sc.params())
+    assert reused[0] == fresh[0] == 0
+    assert (reused[1].iterations, reused[1].initial_cost, reused[1].final_cost) == \
+        (fresh[1].iterations, fresh[1].initial_cost, fresh[1].final_cost)
+    for u, v in zip(reused[2], fresh[2]):
+        np.testing.assert_array_equal(u, v)
+    _, os_, _, _ = H.oracle_solve(sc, threads=8)
+    assert reused[1].iterations == os_.iterations
+    assert abs(reused[1].rmse_final / os_.rmse_final - 1) < RTOL_COST
     lib.sfm_ba_cache_clear(ctx.h)

@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the landmark-sharded BA algebra.
+"""CPU, world_size 2 and 8 (gloo): the landmark-sharded BA algebra.
 
 Each rank takes its point block from the product's sfm_ba_partition and runs
 the oracle on that shard with every cross-rank quantity (RCS S and rhs,
@@ -66,6 +66,26 @@ def test_two_rank_sharded_solve_matches_single(tmp_path, scene_args):
     assert abs(float(r["init"]) / s.initial_cost - 1) < 1e-12
     # decision for decision: the same iterations, the same accept/reject
     # sequence, per-iteration costs to 1e-9 and the final "RMSE" to 1e-6
+    assert int(r["it"]) == s.iterations and int(r["succ"]) == s.successful_steps
+    assert list(r["tr_succ"]) == [t.step_is_successful for t in tr]
+    np.testing.assert_allclose(r["tr_cost"], [t.cost for t in tr], rtol=1e-9)
+    assert abs(np.sqrt(float(r["cost"]) / s.final_cost) - 1) < 1e-6
+    np.testing.assert_allclose(r["x"], x, atol=5e-3 * (np.abs(x).max() + 1))
+
+
+def test_eight_rank_sharded_solve_matches_single(tmp_path):
+    # the north_star's rank count: C4's banded orbit shape (k = 10 views per
+    # point, one shared intrinsics block) cut into 8 landmark blocks
+    import _helpers as H
+    scene_args = dict(n_cam=80, n_pt=8000, k=10, seed=0x5F3D0008)
+    out = str(tmp_path / "r8.npz")
+    port = 27500 + (os.getpid() % 2000)
+    mp.spawn(_worker, args=(8, port, out, scene_args), nprocs=8, join=True)
+    r = np.load(out)
+    sc = H.Scene(**scene_args)
+    rc, s, tr, (e, i, x) = H.oracle_solve(sc, threads=8)
+    assert int(r["rc"]) == rc == 0
+    assert abs(float(r["init"]) / s.initial_cost - 1) < 1e-12
     assert int(r["it"]) == s.iterations and int(r["succ"]) == s.successful_steps
     assert list(r["tr_succ"]) == [t.step_is_successful for t in tr]
     np.testing.assert_allclose(r["tr_cost"], [t.cost for t in tr], rtol=1e-9)
