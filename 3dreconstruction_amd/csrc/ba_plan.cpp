@@ -26,35 +26,6 @@ namespace sfm {
 
 namespace {
 
-// (key, term) entries of the reduce plan's term lists: an aggregate (a
-// std::pair value-initialises), in vectors that default-initialise, so a
-// resize() before the entries are written costs no zero fill
-template <class T>
-struct KeyTerm {
-    int64_t first;
-    T second;
-};
-template <class T>
-struct DefInit : std::allocator<T> {
-    template <class U>
-    struct rebind {
-        using other = DefInit<U>;
-    };
-    DefInit() = default;
-    template <class U>
-    DefInit(const DefInit<U>&) noexcept {}
-    template <class U>
-    void construct(U* p) noexcept {
-        ::new (static_cast<void*>(p)) U;
-    }
-    template <class U, class... A>
-    void construct(U* p, A&&... a) {
-        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
-    }
-};
-template <class T>
-using KTVec = std::vector<KeyTerm<T>, DefInit<KeyTerm<T>>>;
-
 // Split [0, n) into contiguous ranges over up to 16 host threads (results are
 // independent of the split: every range writes its own outputs).
 template <class F>
@@ -455,6 +426,14 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         // factor, M = Jx L^-T, Z = J' M: 180 per observation + 30)
         return 3 * rows * (rows + 1) + 780 * nobs + 30;
     };
+    // A chunking is abandoned as soon as its chunk count (over all ranges)
+    // passes abort_at: from there on its outcome no longer matters (see the
+    // choice of the tile height below), e.g. under random visibility, where
+    // chunks are dropped whatever the count.  The ranges add their chunks to
+    // one shared counter as they close them.
+    std::atomic<int64_t> n_closed{0};
+    std::atomic<bool> abandoned{false};
+    int64_t abort_at = INT64_MAX;
     // greedy chunking of shard points [k_begin, k_end); slot_out is indexed by
     // shard observation (each range writes its own)
     auto make_chunks_range = [&](int cap, int32_t k_begin, int32_t k_end, std::vector<ChunkDesc>& chunks_out,
@@ -497,6 +476,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 sub.sub = j;
                 chunks_out.push_back(sub);
             }
+            if (n_closed.fetch_add(n_sub, std::memory_order_relaxed) + n_sub > abort_at)
+                abandoned.store(true, std::memory_order_relaxed);
         };
         // per-point image lists in fixed storage (<= kSubObs each): this loop
         // runs once per point, and heap vectors here dominated planning time
@@ -511,6 +492,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         };
         if (k_end > k_begin) reset(k_begin);
         for (int32_t k = k_begin; k < k_end; ++k) {
+            if (((k - k_begin) & 255) == 0 && abandoned.load(std::memory_order_relaxed)) return flops;
             const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
             Small pc, pi, pd;
             for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
@@ -573,7 +555,12 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // Shards are chunked in up to 16 fixed point ranges of >= 4096 points on
     // host threads (a chunk never spans two ranges: at most 15 extra chunks
     // out of thousands; the split depends on the shard only, never on the host)
-    auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, HostVec<int32_t>& slot_out) -> int64_t {
+    // returns false if the chunking was abandoned (more than `limit` chunks)
+    auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, HostVec<int32_t>& slot_out, int64_t limit,
+                           int64_t& flops) -> bool {
+        n_closed = 0;
+        abandoned = false;
+        abort_at = limit;
         int gw = schur_group(cap == 64 ? 4 : 5);
         if (const char* e = std::getenv("SFM_BA_TILE_GROUP")) gw = std::max(1, std::min(gw, std::atoi(e)));   // diagnostic
         group_pts = gw * chunk_pts;
@@ -590,14 +577,16 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             });
         };
         parallel_segments(nseg, run);
-        int64_t flops = 0;
+        flops = 0;
         chunks_out.clear();
-        for (int g = 0; g < nseg; ++g) {
+        for (int g = 0; g < nseg; ++g)
             if (seg_rc[g] != SFM_OK) throw SfmError{seg_rc[g]};
+        if (abandoned.load()) return false;
+        for (int g = 0; g < nseg; ++g) {
             chunks_out.insert(chunks_out.end(), seg_chunks[g].begin(), seg_chunks[g].end());
             flops += seg_flops[g];
         }
-        return flops;
+        return true;
     };
     tm.mark("shard_copy");
     int max_own = 0, max_obs = 0;
@@ -626,25 +615,34 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     int64_t flops = 0;
     HostVec<int32_t> cslot;
     pl.tile_nt = 5;
-    // the 64-row kernel walks batches of at most schur4_obs observations
-    if (max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !std::getenv("SFM_BA_TILE80")) {
-        // both tile heights are planned (each over the host threads)
-        std::vector<ChunkDesc> c4, c5;
-        HostVec<int32_t> s4, s5;
-        const int64_t f5 = make_chunks(kTileRowsUsed, c5, s5);
-        const int64_t f4 = make_chunks(64, c4, s4);
-        if (c4.size() * 4 <= c5.size() * 5) {
-            pl.tile_nt = 4; pl.chunks.swap(c4); cslot.swap(s4); flops = f4;
-        } else {
-            pl.chunks.swap(c5); cslot.swap(s5); flops = f5;
-        }
-    } else {
-        flops = make_chunks(kTileRowsUsed, pl.chunks, cslot);
-    }
     // Chunks pay off when camera windows are shared by many consecutive
     // points (sequences, orbits); under random visibility a chunk holds one
-    // or two points and its tile traffic exceeds the general path's
-    if (pl.n_cpt > 0 && (int64_t)pl.chunks.size() * 4 > pl.n_cpt) {
+    // or two points and its tile traffic exceeds the general path's: a
+    // chunking of more than n_cpt / 4 chunks is dropped
+    const int64_t keep_max = pl.n_cpt / 4;
+    bool kept = true;
+    // the 64-row kernel walks batches of at most schur4_obs observations
+    if (max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !std::getenv("SFM_BA_TILE80")) {
+        // both tile heights are planned (each over the host threads); the
+        // 64-row one is taken unless it needs 5/4 as many chunks.  80 rows
+        // over keep_max: dropped if taken, so 64 rows matter only within
+        // keep_max; else 64 rows matter only within 5/4 of the 80-row count
+        std::vector<ChunkDesc> c4, c5;
+        HostVec<int32_t> s4, s5;
+        int64_t f4 = 0, f5 = 0;
+        const bool ok5 = make_chunks(kTileRowsUsed, c5, s5, keep_max, f5);
+        const bool ok4 = make_chunks(64, c4, s4, ok5 ? (int64_t)c5.size() * 5 / 4 : keep_max, f4);
+        if (ok4) {
+            pl.tile_nt = 4; pl.chunks.swap(c4); cslot.swap(s4); flops = f4;
+        } else if (ok5) {
+            pl.chunks.swap(c5); cslot.swap(s5); flops = f5;
+        } else {
+            kept = false;
+        }
+    } else {
+        kept = make_chunks(kTileRowsUsed, pl.chunks, cslot, keep_max, flops);
+    }
+    if (!kept || (pl.n_cpt > 0 && (int64_t)pl.chunks.size() * 4 > pl.n_cpt)) {
         pl.chunks.clear();
         cslot.clear();
         pl.n_cpt = 0;
@@ -821,311 +819,394 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     tm.mark("image_csr");
     // ---- reduce plan -----------------------------------------------------------
     // Every matrix block (a, b), a >= b in F-block order (cameras, then
-    // intrinsics), collects sum terms (image Gram slices first, then chunk tile
-    // sub-blocks in chunk order) and product terms (general points in order);
-    // vectors (rhs, bF, cnF) likewise per block.  Terms are gathered as (key,
-    // term) pairs and stably sorted by key: a fixed order, so every sum is
-    // bit-reproducible.
-    const int32_t nFB = pl.nFB;
-    auto fb_of_col = [&](int64_t col) -> int32_t {
-        return col < pl.nb ? (int32_t)(col / 6) : (int32_t)(pl.ncam + (col - pl.nb) / pl.iw);
-    };
-    auto col_of_fb = [&](int32_t b) -> int64_t { return b < pl.ncam ? 6LL * b : pl.nb + (int64_t)pl.iw * (b - pl.ncam); };
-    auto size_of_fb = [&](int32_t b) { return b < pl.ncam ? 6 : pl.iw; };
-    KTVec<ReduceTerm> mterms, vterms;
-    KTVec<PTerm> mprod, vprod;
-    {
-        // exact capacities: one growth-free allocation per list (the lists
-        // are fresh memory, so every reallocation is page faults again)
-        size_t nm = 3 * (size_t)kGramSeg * P.n_img, nv = 2 * (size_t)kGramSeg * P.n_img, npm = 0, npv = 0;
-        for (int64_t g = 0; g < pl.n_group(); ++g) {
-            const ChunkDesc& cd = pl.chunks[pl.group_off[g]];
-            nm += (size_t)cd.n_slots * (cd.n_slots + 1) / 2;
-            nv += (size_t)cd.n_slots;
-        }
-        for (int64_t g = 0; g < pl.n_gpt; ++g) {
-            const size_t b = (size_t)(pl.gblk_off[g + 1] - pl.gblk_off[g]);
-            npm += b * (b + 1) / 2;
-            npv += b;
-        }
-        mterms.reserve(nm);
-        vterms.reserve(nv);
-        mprod.reserve(npm);
-        vprod.reserve(npv);
+    // intrinsics), is a target summing its terms in a fixed order: sum terms
+    // (image Gram slices in image order, then chunk tile sub-blocks in tile
+    // group order) and product terms (general points in order); vectors (rhs,
+    // bF, cnF) likewise per block -- so every sum is bit-reproducible.  Both
+    // lists are laid out target after target.  They are built by a counting
+    // scatter over F-block rows, without materialising or sorting (key, term)
+    // lists: per-row term counts first (one pass over the sources, O(blocks)),
+    // which fix every row's first position; then each host thread takes a
+    // range of rows, counts its targets' terms, and writes every term of its
+    // rows straight to its final place, visiting the sources in their order.
+    const int32_t nFB = pl.nFB, ncam = pl.ncam, nintr = pl.nintr, D = pl.D;
+    const int Dp = D + 1;
+    const bool band = !pl.dense;
+    if (band) {
+        pl.n_sband = (int64_t)ncam * Dp * 36;
+        pl.n_sarrow = (int64_t)nintr * ncam * 6 * pl.iw;
+        pl.n_scorner = (int64_t)nintr * nintr * pl.iw * pl.iw;
     }
-    // image Gram blocks (kGramSeg partial slices per image)
-    auto add_u = [&](KTVec<ReduceTerm>& out, int64_t key, int32_t kind, int img,
-                     int16_t ro, int16_t co) {
-        for (int g = 0; g < kGramSeg; ++g) out.push_back({key, ReduceTerm{kind, img * kGramSeg + g, ro, co, 1.f}});
+    auto fb_of_col = [&](int64_t col) -> int32_t {
+        return col < pl.nb ? (int32_t)(col / 6) : (int32_t)(ncam + (col - pl.nb) / pl.iw);
     };
+    auto col_of_fb = [&](int32_t b) -> int64_t { return b < ncam ? 6LL * b : pl.nb + (int64_t)pl.iw * (b - ncam); };
+    auto size_of_fb = [&](int32_t b) { return b < ncam ? 6 : pl.iw; };
+    // band: a corner block (k, l), k < l, is stored too, as the transpose of
+    // (l, k): terms of an off-diagonal corner key go to two targets
+    auto twice = [&](int32_t fa, int32_t fb) { return band && fb >= ncam && fb != fa; };
+    // a tile group's window can be wider than the band: its slot pairs
+    // further apart than D are structurally zero (no point sees both) and
+    // have no target
+    auto held = [&](int32_t fa, int32_t fb) { return !band || fa >= ncam || fa - fb <= D; };
+    // the images that contribute Gram slices: (image, camera block, F block of its intrinsics)
+    struct ImgSrc {
+        int32_t img, cb, fq;
+    };
+    std::vector<ImgSrc> isrc;
     for (int img = 0; img < P.n_img; ++img) {
         const int cb = pl.cam_blk[img], q = pl.intr_blk[P.img_intr[img]];
-        if (pl.img_obs_ptr[img + 1] == pl.img_obs_ptr[img] && cb < 0 && q < 0) continue;
+        const bool seen = pl.img_obs_ptr[img + 1] != pl.img_obs_ptr[img];
+        if (!seen && cb < 0 && q < 0) continue;
         // a landmark shard: an image none of this rank's observations sees
         // contributes nothing here (its blocks come from the other ranks)
-        if (world > 1 && pl.img_obs_ptr[img + 1] == pl.img_obs_ptr[img]) continue;
-        const int32_t fq = q >= 0 ? pl.ncam + q : -1;
-        if (cb >= 0) {
-            add_u(mterms, (int64_t)cb * nFB + cb, kSrcU, img, 0, 0);
-            if (fq >= 0) add_u(mterms, (int64_t)fq * nFB + cb, kSrcU, img, 6, 0);
-            add_u(vterms, cb, kSrcUb, img, 0, 0);
+        if (world > 1 && !seen) continue;
+        isrc.push_back({img, cb, q >= 0 ? ncam + q : -1});
+    }
+    const int32_t ngrp = (int32_t)pl.n_group();
+    auto grp = [&](int32_t c) -> const ChunkDesc& { return pl.chunks[pl.group_off[c]]; };
+    // F-block range of every tile group and general point (rows they write)
+    std::vector<int32_t> g_lo(ngrp), g_hi(ngrp), p_lo(pl.n_gpt), p_hi(pl.n_gpt);
+    // F block of every general-point block (pfb) and tile-group slot (gfb)
+    std::vector<int32_t> pfb(pl.gblk_col.size()), gfb((size_t)ngrp * kMaxSlots);
+    for (int32_t c = 0; c < ngrp; ++c) {
+        int32_t lo = INT32_MAX, hi = -1;
+        for (int a = 0; a < grp(c).n_slots; ++a) {
+            const int32_t f = fb_of_col(grp(c).slot_col[a]);
+            gfb[(size_t)c * kMaxSlots + a] = f;
+            lo = std::min(lo, f);
+            hi = std::max(hi, f);
         }
-        if (fq >= 0) {
-            add_u(mterms, (int64_t)fq * nFB + fq, kSrcU, img, 6, 6);
-            add_u(vterms, fq, kSrcUb, img, 6, 0);
+        g_lo[c] = lo;
+        g_hi[c] = hi;
+    }
+    parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+        for (int64_t g = g0; g < g1; ++g) {
+            const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
+            for (int32_t a = k0; a < k1; ++a) pfb[a] = fb_of_col(pl.gblk_col[a]);
+            p_lo[g] = k1 > k0 ? fb_of_col(pl.gblk_col[k0]) : INT32_MAX;   // columns ascend
+            p_hi[g] = k1 > k0 ? fb_of_col(pl.gblk_col[k1 - 1]) : -1;
+        }
+    });
+    tm.mark("terms_sources");
+
+    // ---- per-row counts: matrix sum / product terms, rhs sum / product
+    // terms, image slices (bF and cnF) ------------------------------------------
+    enum { kMc, kMp, kVc, kVp, kVb, kNC };
+    std::vector<int64_t> rc((size_t)kNC * (nFB + 1), 0);
+    auto RC = [&](int w, int32_t f) -> int64_t& { return rc[(size_t)w * (nFB + 1) + f]; };
+    for (const ImgSrc& s : isrc) {
+        if (s.cb >= 0) {
+            RC(kMc, s.cb) += kGramSeg;
+            if (s.fq >= 0) RC(kMc, s.fq) += kGramSeg;
+            RC(kVc, s.cb) += kGramSeg;
+            RC(kVb, s.cb) += kGramSeg;
+        }
+        if (s.fq >= 0) {
+            RC(kMc, s.fq) += kGramSeg;
+            RC(kVc, s.fq) += kGramSeg;
+            RC(kVb, s.fq) += kGramSeg;
         }
     }
-    tm.mark("terms_images");
-    // cnF: per block, image slices only (never a tile term)
-    KTVec<ReduceTerm> cterms;
-    for (const auto& t : vterms) {
-        ReduceTerm q = t.second;
-        q.kind = kSrcUcn;
-        cterms.push_back({t.first, q});
-    }
-    tm.mark("terms_cnf");
-    // chunk tiles: fixed chunk ranges on host threads, appended in chunk order
     {
-        const int32_t nch = (int32_t)pl.n_group();   // one tile per group (its first chunk's layout)
-        const int nseg = nch >= 128 ? 16 : 1;   // the output is the same for any split
-        std::vector<KTVec<ReduceTerm>> sm(nseg), sv(nseg);
-        parallel_segments(nseg, [&](int g) {
-            const int32_t c0 = (int32_t)((int64_t)nch * g / nseg), c1 = (int32_t)((int64_t)nch * (g + 1) / nseg);
-            for (int32_t c = c0; c < c1; ++c) {
-                const ChunkDesc& cd = pl.chunks[pl.group_off[c]];
+        // tile groups and general points, per host range into private rows
+        std::vector<std::vector<int64_t>> part(16);
+        auto acc_groups = [&](int64_t c0, int64_t c1, std::vector<int64_t>& r) {
+            for (int64_t c = c0; c < c1; ++c) {
+                const ChunkDesc& cd = grp((int32_t)c);
                 for (int a = 0; a < cd.n_slots; ++a) {
-                    const int32_t fa = fb_of_col(cd.slot_col[a]);
-                    // rhs contribution (-Z w) from tile row 79
-                    sv[g].push_back({fa, ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}});
+                    const int32_t fa = gfb[(size_t)c * kMaxSlots + a];
+                    r[(size_t)kVc * (nFB + 1) + fa] += 1;
                     for (int b = 0; b < cd.n_slots; ++b) {
-                        const int32_t fb = fb_of_col(cd.slot_col[b]);
-                        if (fa < fb) continue;
-                        sm[g].push_back({(int64_t)fa * nFB + fb,
-                                         ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f}});
+                        const int32_t fb = gfb[(size_t)c * kMaxSlots + b];
+                        if (fa >= fb && held(fa, fb)) r[(size_t)kMc * (nFB + 1) + fa] += twice(fa, fb) ? 2 : 1;
                     }
                 }
             }
-        });
-        size_t nm = mterms.size(), nv = vterms.size();
-        for (int g = 0; g < nseg; ++g) { nm += sm[g].size(); nv += sv[g].size(); }
-        mterms.reserve(nm);
-        vterms.reserve(nv);
-        for (int g = 0; g < nseg; ++g) {
-            mterms.insert(mterms.end(), sm[g].begin(), sm[g].end());
-            vterms.insert(vterms.end(), sv[g].begin(), sv[g].end());
-        }
-    }
-    tm.mark("terms_tiles");
-    // general points: point g's product terms go to fixed offsets (the
-    // triangle of its blocks), written on the host threads
-    {
-        std::vector<int64_t> mo(pl.n_gpt + 1, 0);
-        for (int64_t g = 0; g < pl.n_gpt; ++g) {
-            const int64_t b = pl.gblk_off[g + 1] - pl.gblk_off[g];
-            mo[g + 1] = mo[g] + b * (b + 1) / 2;
-        }
-        mprod.resize(mo[pl.n_gpt]);
-        vprod.resize(pl.gblk_off[pl.n_gpt]);
-        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+        };
+        auto acc_points = [&](int64_t g0, int64_t g1, std::vector<int64_t>& r) {
             for (int64_t g = g0; g < g1; ++g) {
                 const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
-                const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
-                int64_t m = mo[g];
+                int32_t first_i = k1;   // first intrinsics block (columns ascend)
                 for (int32_t a = k0; a < k1; ++a) {
-                    const int32_t fa = fb_of_col(pl.gblk_col[a]);
-                    vprod[a] = {fa, PTerm{zb + pl.gblk_z[a], wz}};
-                    for (int32_t b = k0; b <= a; ++b)
-                        mprod[m++] = {(int64_t)fa * nFB + fb_of_col(pl.gblk_col[b]),
-                                      PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]}};
+                    const int32_t fa = pfb[a];
+                    if (fa >= ncam && first_i == k1) first_i = a;
+                    r[(size_t)kVp * (nFB + 1) + fa] += 1;
+                    const int64_t pairs = a - k0 + 1, dbl = band && fa >= ncam ? a - first_i : 0;
+                    r[(size_t)kMp * (nFB + 1) + fa] += pairs + dbl;
                 }
             }
-        });
-    }
-    // stable by key (the order std::stable_sort gives): LSD radix passes of
-    // 11-bit digits over the key (one pass for small problems, two at C4).
-    // Written for nr ranges (each histograms its digits, the (digit, range)
-    // prefix keeps every range's entries of one digit in range order, then
-    // every range scatters its own), run as one range here
-    auto sort_terms = [&](auto& v) {
-        using E = typename std::decay_t<decltype(v)>::value_type;
-        auto less = [](const E& x, const E& y) { return x.first < y.first; };
-        int64_t kmax = 0;
-        for (const E& e : v) kmax = std::max(kmax, e.first);
-        int bits = 0;
-        while (bits < 63 && (kmax >> bits) != 0) ++bits;
-        if (v.size() < 2048 || bits > 44) {
-            std::stable_sort(v.begin(), v.end(), less);
-            return;
-        }
-        constexpr int kD = 11, kB = 1 << kD;
-        const int passes = std::max(1, (bits + kD - 1) / kD);
-        std::decay_t<decltype(v)> tmp(v.size());
-        E* src = v.data();
-        E* dst = tmp.data();
-        const int64_t n = (int64_t)v.size();
-        const int nr = 1;   // (a split over host threads: see the call site)
-        std::vector<int64_t> cnt((size_t)nr * kB);
-        for (int p = 0; p < passes; ++p) {
-            const int sh = p * kD;
-            auto digit = [&](const E& e) { return (int)((e.first >> sh) & (kB - 1)); };
-            parallel_segments(nr, [&](int r) {
-                int64_t* c = cnt.data() + (size_t)r * kB;
-                std::fill(c, c + kB, 0);
-                for (int64_t k = n * r / nr; k < n * (r + 1) / nr; ++k) c[digit(src[k])]++;
-            });
-            int64_t acc = 0;
-            for (int d = 0; d < kB; ++d)
-                for (int r = 0; r < nr; ++r) {
-                    const int64_t c = cnt[(size_t)r * kB + d];
-                    cnt[(size_t)r * kB + d] = acc;
-                    acc += c;
-                }
-            parallel_segments(nr, [&](int r) {
-                int64_t* c = cnt.data() + (size_t)r * kB;
-                for (int64_t k = n * r / nr; k < n * (r + 1) / nr; ++k) dst[c[digit(src[k])]++] = src[k];
-            });
-            std::swap(src, dst);
-        }
-        if (src != v.data()) v.swap(tmp);
-    };
-    tm.mark("terms");
-    // the five lists concurrently, each sorted by one thread (on the GPU
-    // box's 16 host CPUs this measured faster than one list after another
-    // with the radix passes themselves split over the threads)
-    parallel_segments(5, [&](int g) {
-        switch (g) {
-            case 0: sort_terms(mprod); break;
-            case 1: sort_terms(mterms); break;
-            case 2: sort_terms(vterms); break;
-            case 3: sort_terms(cterms); break;
-            default: sort_terms(vprod); break;
-        }
-    });
-
-    tm.mark("term_sort");
-    const int Dp = pl.D + 1;
-    if (!pl.dense) {
-        pl.n_sband = (int64_t)pl.ncam * Dp * 36;
-        pl.n_sarrow = (int64_t)pl.nintr * pl.ncam * 6 * pl.iw;
-        pl.n_scorner = (int64_t)pl.nintr * pl.nintr * pl.iw * pl.iw;
-    }
-    size_t im = 0, ipm = 0, iv = 0, ipv = 0, ic = 0;
-    // every term lands in one target (the corner's transposed copies aside)
-    pl.terms.reserve(mterms.size() + 2 * vterms.size() + cterms.size());
-    pl.pterms.reserve(mprod.size() + vprod.size());
-    auto emit = [&](int64_t key, int32_t kind, int64_t dst, int rows, int cols, int ld,
-                    KTVec<ReduceTerm>& st, size_t& is,
-                    KTVec<PTerm>* pt, size_t* ip) {
-        ReduceTarget t{};
-        t.dst = dst; t.dst_kind = kind; t.rows = rows; t.cols = cols; t.ld = ld;
-        while (is < st.size() && st[is].first < key) ++is;   // (keys with no target: none by construction)
-        t.c_begin = (int32_t)pl.terms.size();
-        for (; is < st.size() && st[is].first == key; ++is) pl.terms.push_back(st[is].second);
-        t.c_end = (int32_t)pl.terms.size();
-        t.p_begin = t.p_end = (int32_t)pl.pterms.size();
-        if (pt) {
-            while (*ip < pt->size() && (*pt)[*ip].first < key) ++*ip;
-            for (; *ip < pt->size() && (*pt)[*ip].first == key; ++*ip) pl.pterms.push_back((*pt)[*ip].second);
-            t.p_end = (int32_t)pl.pterms.size();
-        }
-        pl.targets.push_back(t);
-    };
-    if (!pl.dense) {
-        // every band block (i, i-d), d <= D, then the arrow and the corner, in
-        // key order within each family
-        std::vector<std::pair<int64_t, std::pair<int32_t, int64_t>>> tl;   // key -> (kind, dst)
-        for (int i = 0; i < pl.ncam; ++i)
-            for (int d = std::min(pl.D, i); d >= 0; --d)
-                tl.push_back({(int64_t)i * nFB + (i - d), {kDstBand, ((int64_t)i * Dp + d) * 36}});
-        for (int k = 0; k < pl.nintr; ++k)
-            for (int i = 0; i < pl.ncam; ++i)
-                tl.push_back({(int64_t)(pl.ncam + k) * nFB + i, {kDstArrow, ((int64_t)k * pl.ncam + i) * 6 * pl.iw}});
-        for (int k = 0; k < pl.nintr; ++k)
-            for (int l = 0; l < pl.nintr; ++l)
-                tl.push_back({(int64_t)(pl.ncam + std::max(k, l)) * nFB + pl.ncam + std::min(k, l),
-                              {kDstCorner, ((int64_t)k * pl.nintr + l) * pl.iw * pl.iw}});
-        std::stable_sort(tl.begin(), tl.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-        // the corner is stored whole: block (k, l) with k < l is the transpose
-        // of (l, k) and is gathered separately with swapped source offsets
-        for (size_t x = 0; x < tl.size(); ++x) {
-            const int64_t key = tl[x].first;
-            const int32_t kind = tl[x].second.first;
-            const int64_t dst = tl[x].second.second;
-            if (kind == kDstCorner) {
-                const int k = (int)(dst / (pl.iw * pl.iw)) / pl.nintr, l = (int)(dst / (pl.iw * pl.iw)) % pl.nintr;
-                if (k < l) {
-                    // transpose of the (l, k) block: same terms, row/column swapped
-                    const size_t t0 = pl.terms.size(), p0 = pl.pterms.size();
-                    size_t js = 0, jp = 0;
-                    emit(key, kind, dst, pl.iw, pl.iw, pl.iw, mterms, js, &mprod, &jp);
-                    for (size_t q = t0; q < pl.terms.size(); ++q) std::swap(pl.terms[q].roff, pl.terms[q].coff);
-                    for (size_t q = p0; q < pl.pterms.size(); ++q) std::swap(pl.pterms[q].za, pl.pterms[q].zb);
-                    continue;
-                }
-                emit(key, kind, dst, pl.iw, pl.iw, pl.iw, mterms, im, &mprod, &ipm);
-                continue;
-            }
-            const int rows = kind == kDstBand ? 6 : pl.iw;
-            emit(key, kind, dst, rows, 6, 6, mterms, im, &mprod, &ipm);
-        }
-    } else {
-        // dense: every block that receives a term (the rest stays zero), in
-        // key order.  Every key of the sorted lists is a target, so the
-        // target term lists are the sorted lists themselves: copied whole on
-        // the host threads, each target pointing at its key's run.
-        auto runs = [&](const auto& v, std::vector<std::pair<int64_t, int64_t>>& out) {   // (key, first index)
-            const int64_t n = (int64_t)v.size();
-            const int nr = n < 65536 ? 1 : PlanPool::width();
-            std::vector<std::vector<std::pair<int64_t, int64_t>>> part(nr);
-            parallel_segments(nr, [&](int r) {
-                for (int64_t k = n * r / nr; k < n * (r + 1) / nr; ++k)
-                    if (k == 0 || v[k].first != v[k - 1].first) part[r].push_back({v[k].first, k});
-            });
-            out.clear();
-            for (auto& q : part) out.insert(out.end(), q.begin(), q.end());
-            out.push_back({INT64_MAX, n});
         };
-        std::vector<std::pair<int64_t, int64_t>> ra, rb;
-        runs(mterms, ra);
-        runs(mprod, rb);
-        const int32_t t0 = (int32_t)pl.terms.size(), q0 = (int32_t)pl.pterms.size();
-        pl.terms.resize(t0 + mterms.size());
-        pl.pterms.resize(q0 + mprod.size());
-        parallel_ranges((int64_t)mterms.size(), [&](int64_t a, int64_t b, int) {
-            for (int64_t k = a; k < b; ++k) pl.terms[t0 + k] = mterms[k].second;
+        parallel_ranges(ngrp, [&](int64_t c0, int64_t c1, int t) {
+            part[t].assign((size_t)kNC * (nFB + 1), 0);
+            acc_groups(c0, c1, part[t]);
         });
-        parallel_ranges((int64_t)mprod.size(), [&](int64_t a, int64_t b, int) {
-            for (int64_t k = a; k < b; ++k) pl.pterms[q0 + k] = mprod[k].second;
-        });
-        size_t ia = 0, ib = 0;
-        while (ra[ia].first != INT64_MAX || rb[ib].first != INT64_MAX) {
-            const int64_t key = std::min(ra[ia].first, rb[ib].first);
-            const int32_t a = (int32_t)(key / nFB), b = (int32_t)(key % nFB);
-            ReduceTarget t{};
-            t.dst = col_of_fb(a) * pl.nF + col_of_fb(b);
-            t.dst_kind = kDstDense;
-            t.rows = size_of_fb(a); t.cols = size_of_fb(b); t.ld = (int32_t)pl.nF;
-            t.c_begin = t.c_end = t0 + (int32_t)ra[ia].second;
-            if (ra[ia].first == key) t.c_end = t0 + (int32_t)ra[++ia].second;
-            t.p_begin = t.p_end = q0 + (int32_t)rb[ib].second;
-            if (rb[ib].first == key) t.p_end = q0 + (int32_t)rb[++ib].second;
-            pl.targets.push_back(t);
+        for (auto& p : part) {
+            if (p.empty()) continue;
+            for (size_t k = 0; k < p.size(); ++k) rc[k] += p[k];
+            p.clear();
         }
-        im = mterms.size();
-        ipm = mprod.size();
+        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int t) {
+            part[t].assign((size_t)kNC * (nFB + 1), 0);
+            acc_points(g0, g1, part[t]);
+        });
+        for (auto& p : part)
+            for (size_t k = 0; k < p.size(); ++k) rc[k] += p[k];
+    }
+    // first position of every row in its list: matrix sum terms, then rhs,
+    // bF and cnF sum terms; matrix product terms, then rhs product terms
+    std::vector<int64_t> base((size_t)kNC * (nFB + 1) + 1, 0);
+    auto BS = [&](int w, int32_t f) -> int64_t& { return base[(size_t)w * (nFB + 1) + f]; };
+    int64_t n_mc = 0, n_mp = 0, n_vc = 0, n_vp = 0, n_vb = 0;
+    for (int32_t f = 0; f < nFB; ++f) {
+        BS(kMc, f) = n_mc; n_mc += RC(kMc, f);
+        BS(kMp, f) = n_mp; n_mp += RC(kMp, f);
+        BS(kVc, f) = n_vc; n_vc += RC(kVc, f);
+        BS(kVp, f) = n_vp; n_vp += RC(kVp, f);
+        BS(kVb, f) = n_vb; n_vb += RC(kVb, f);
+    }
+    BS(kMc, nFB) = n_mc; BS(kMp, nFB) = n_mp;
+    const int64_t n_terms = n_mc + n_vc + 2 * n_vb, n_pterms = n_mp + n_vp;
+    SFM_REQUIRE(n_terms < INT32_MAX && n_pterms < INT32_MAX, SFM_ERR_UNSUPPORTED,
+                "reduce plan of %lld sum / %lld product terms", (long long)n_terms, (long long)n_pterms);
+    pl.terms.resize(n_terms);
+    pl.pterms.resize(n_pterms);
+    tm.mark("terms_count");
+
+    // ---- targets and terms, by row ranges ----------------------------------
+    // matrix targets of row fa: band -- the band blocks (fa, fa-d), d from
+    // min(D, fa) down to 0; an intrinsics row ncam+m: the arrow (m, i) for
+    // every camera, then per corner column l <= m the transposed (l, m) (l <
+    // m) and (m, l) -- the order a stable sort of the targets by key gives.
+    // Dense: every block (fa, fb <= fa) that receives a term.
+    auto row_slots = [&](int32_t f) -> int64_t {
+        if (!band) return (int64_t)f + 1;
+        return f < ncam ? std::min(D, f) + 1 : ncam + 2 * (f - ncam) + 1;
+    };
+    // slot of (fa, fb) within row fa; *second: a transposed twin at slot - 1
+    auto slot_of = [&](int32_t fa, int32_t fb) -> int64_t {
+        if (!band) return fb;
+        if (fa < ncam) return fb - (fa - std::min(D, fa));
+        if (fb < ncam) return fb;
+        return ncam + 2 * (fb - ncam) + (fb != fa ? 1 : 0);   // the (fa, fb) target; its twin precedes it
+    };
+    auto make_target = [&](int32_t fa, int64_t s) {
+        ReduceTarget t{};
+        if (!band) {
+            const int32_t fb = (int32_t)s;
+            t.dst = col_of_fb(fa) * pl.nF + col_of_fb(fb);
+            t.dst_kind = kDstDense;
+            t.rows = size_of_fb(fa); t.cols = size_of_fb(fb); t.ld = (int32_t)pl.nF;
+        } else if (fa < ncam) {
+            const int d = std::min(D, fa) - (int)s;
+            t.dst = ((int64_t)fa * Dp + d) * 36;
+            t.dst_kind = kDstBand;
+            t.rows = 6; t.cols = 6; t.ld = 6;
+        } else if (s < ncam) {
+            t.dst = ((int64_t)(fa - ncam) * ncam + s) * 6 * pl.iw;
+            t.dst_kind = kDstArrow;
+            t.rows = pl.iw; t.cols = 6; t.ld = 6;
+        } else {
+            const int m = fa - ncam, u = (int)(s - ncam), lp = u / 2;
+            const bool trans = (u & 1) == 0 && lp < m;
+            const int k = trans ? lp : m, l = trans ? m : lp;
+            t.dst = ((int64_t)k * nintr + l) * pl.iw * pl.iw;
+            t.dst_kind = kDstCorner;
+            t.rows = pl.iw; t.cols = pl.iw; t.ld = pl.iw;
+        }
+        return t;
+    };
+    // row ranges of about equal work (terms, plus the row's targets)
+    std::vector<int32_t> cut{0};
+    {
+        int64_t tot = 0;
+        std::vector<int64_t> w(nFB);
+        for (int32_t f = 0; f < nFB; ++f) {
+            w[f] = RC(kMc, f) + RC(kMp, f) + RC(kVc, f) + RC(kVp, f) + 2 * RC(kVb, f) + row_slots(f);
+            tot += w[f];
+        }
+        const int nt = tot < 65536 ? 1 : std::min<int>(PlanPool::width(), std::max(1, nFB));
+        int64_t acc = 0;
+        for (int32_t f = 0; f < nFB; ++f) {
+            acc += w[f];
+            if ((int)cut.size() < nt && acc * nt >= (int64_t)cut.size() * tot && f + 1 < nFB) cut.push_back(f + 1);
+        }
+        cut.push_back(nFB);
+    }
+    const int nseg = (int)cut.size() - 1;
+    std::vector<std::vector<ReduceTarget>> seg_targets(nseg);
+    std::vector<int> seg_rc(nseg, SFM_OK);
+    parallel_segments(nseg, [&](int sg) {
+        seg_rc[sg] = guarded([&] {
+            const int32_t r0 = cut[sg], r1 = cut[sg + 1];
+            std::vector<int64_t> sbase(r1 - r0 + 1, 0);   // first slot of each row
+            for (int32_t f = r0; f < r1; ++f) sbase[f - r0 + 1] = sbase[f - r0] + row_slots(f);
+            const int64_t ns = sbase[r1 - r0];
+            // per slot: sum / product term counts, then write cursors
+            std::vector<int64_t> cs(ns, 0), ps(ns, 0);
+            auto S = [&](int32_t fa, int32_t fb) { return sbase[fa - r0] + slot_of(fa, fb); };
+            auto in = [&](int32_t f) { return f >= r0 && f < r1; };
+            // (1) counts
+            for (const ImgSrc& s : isrc) {
+                if (s.cb >= 0 && in(s.cb)) cs[S(s.cb, s.cb)] += kGramSeg;
+                if (s.fq >= 0 && in(s.fq)) {
+                    if (s.cb >= 0) cs[S(s.fq, s.cb)] += kGramSeg;
+                    cs[S(s.fq, s.fq)] += kGramSeg;
+                }
+            }
+            for (int32_t c = 0; c < ngrp; ++c) {
+                if (g_hi[c] < r0 || g_lo[c] >= r1) continue;
+                const ChunkDesc& cd = grp(c);
+                for (int a = 0; a < cd.n_slots; ++a) {
+                    const int32_t fa = gfb[(size_t)c * kMaxSlots + a];
+                    if (!in(fa)) continue;
+                    for (int b = 0; b < cd.n_slots; ++b) {
+                        const int32_t fb = gfb[(size_t)c * kMaxSlots + b];
+                        if (fa < fb || !held(fa, fb)) continue;
+                        const int64_t q = S(fa, fb);
+                        cs[q]++;
+                        if (twice(fa, fb)) cs[q - 1]++;
+                    }
+                }
+            }
+            for (int64_t g = 0; g < pl.n_gpt; ++g) {
+                if (p_hi[g] < r0 || p_lo[g] >= r1) continue;
+                const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
+                for (int32_t a = k0; a < k1; ++a) {
+                    const int32_t fa = pfb[a];
+                    if (fa < r0) continue;
+                    if (fa >= r1) break;
+                    for (int32_t b = k0; b <= a; ++b) {
+                        const int32_t fb = pfb[b];
+                        const int64_t q = S(fa, fb);
+                        ps[q]++;
+                        if (twice(fa, fb)) ps[q - 1]++;
+                    }
+                }
+            }
+            // (2) targets in slot order; the counts become write cursors
+            auto& tg = seg_targets[sg];
+            int64_t c_at = BS(kMc, r0), p_at = BS(kMp, r0);
+            for (int32_t f = r0; f < r1; ++f)
+                for (int64_t s = 0; s < row_slots(f); ++s) {
+                    const int64_t q = sbase[f - r0] + s;
+                    const int64_t nc = cs[q], np = ps[q];
+                    cs[q] = c_at;
+                    ps[q] = p_at;
+                    if (!band && nc == 0 && np == 0) continue;
+                    ReduceTarget t = make_target(f, s);
+                    t.c_begin = (int32_t)c_at; t.c_end = (int32_t)(c_at + nc);
+                    t.p_begin = (int32_t)p_at; t.p_end = (int32_t)(p_at + np);
+                    c_at += nc;
+                    p_at += np;
+                    tg.push_back(t);
+                }
+            // (3) the terms, sources in order
+            ReduceTerm* T = pl.terms.data();
+            PTerm* PT = pl.pterms.data();
+            auto put = [&](int64_t q, bool tw, ReduceTerm r) {
+                T[cs[q]++] = r;
+                if (tw) {
+                    std::swap(r.roff, r.coff);
+                    T[cs[q - 1]++] = r;
+                }
+            };
+            auto put_p = [&](int64_t q, bool tw, PTerm r) {
+                PT[ps[q]++] = r;
+                if (tw) {
+                    std::swap(r.za, r.zb);
+                    PT[ps[q - 1]++] = r;
+                }
+            };
+            // vector cursors of this range's rows: rhs sum / product, bF, cnF
+            std::vector<int64_t> vcur(4 * (size_t)(r1 - r0));
+            for (int32_t f = r0; f < r1; ++f) {
+                vcur[4 * (f - r0) + 0] = n_mc + BS(kVc, f);
+                vcur[4 * (f - r0) + 1] = n_mp + BS(kVp, f);
+                vcur[4 * (f - r0) + 2] = n_mc + n_vc + BS(kVb, f);
+                vcur[4 * (f - r0) + 3] = n_mc + n_vc + n_vb + BS(kVb, f);
+            }
+            auto put_v = [&](int32_t f, int16_t ro, int32_t idx) {
+                int64_t* v = &vcur[4 * (f - r0)];
+                T[v[0]++] = ReduceTerm{kSrcUb, idx, ro, 0, 1.f};
+                T[v[2]++] = ReduceTerm{kSrcUb, idx, ro, 0, 1.f};
+                T[v[3]++] = ReduceTerm{kSrcUcn, idx, ro, 0, 1.f};
+            };
+            for (const ImgSrc& s : isrc)
+                for (int g = 0; g < kGramSeg; ++g) {
+                    const int32_t idx = s.img * kGramSeg + g;
+                    if (s.cb >= 0 && in(s.cb)) {
+                        put(S(s.cb, s.cb), false, ReduceTerm{kSrcU, idx, 0, 0, 1.f});
+                        put_v(s.cb, 0, idx);
+                    }
+                    if (s.fq >= 0 && in(s.fq)) {
+                        if (s.cb >= 0) put(S(s.fq, s.cb), false, ReduceTerm{kSrcU, idx, 6, 0, 1.f});
+                        put(S(s.fq, s.fq), false, ReduceTerm{kSrcU, idx, 6, 6, 1.f});
+                        put_v(s.fq, 6, idx);
+                    }
+                }
+            for (int32_t c = 0; c < ngrp; ++c) {
+                if (g_hi[c] < r0 || g_lo[c] >= r1) continue;
+                const ChunkDesc& cd = grp(c);
+                for (int a = 0; a < cd.n_slots; ++a) {
+                    const int32_t fa = gfb[(size_t)c * kMaxSlots + a];
+                    if (!in(fa)) continue;
+                    // rhs contribution (-Z w) from tile row 79
+                    T[vcur[4 * (fa - r0)]++] = ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f};
+                    for (int b = 0; b < cd.n_slots; ++b) {
+                        const int32_t fb = gfb[(size_t)c * kMaxSlots + b];
+                        if (fa < fb || !held(fa, fb)) continue;
+                        put(S(fa, fb), twice(fa, fb),
+                            ReduceTerm{kSrcTile, c, (int16_t)cd.slot_row[a], (int16_t)cd.slot_row[b], 1.f});
+                    }
+                }
+            }
+            for (int64_t g = 0; g < pl.n_gpt; ++g) {
+                if (p_hi[g] < r0 || p_lo[g] >= r1) continue;
+                const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
+                const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
+                for (int32_t a = k0; a < k1; ++a) {
+                    const int32_t fa = pfb[a];
+                    if (fa < r0) continue;
+                    if (fa >= r1) break;
+                    PT[vcur[4 * (fa - r0) + 1]++] = PTerm{zb + pl.gblk_z[a], wz};
+                    for (int32_t b = k0; b <= a; ++b) {
+                        const int32_t fb = pfb[b];
+                        put_p(S(fa, fb), twice(fa, fb), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]});
+                    }
+                }
+            }
+            return SFM_OK;
+        });
+    });
+    for (int sg = 0; sg < nseg; ++sg)
+        if (seg_rc[sg] != SFM_OK) throw SfmError{seg_rc[sg]};
+    tm.mark("terms");
+    {
+        size_t nt = 3 * (size_t)nFB;
+        for (const auto& v : seg_targets) nt += v.size();
+        pl.targets.clear();
+        pl.targets.reserve(nt);
+        for (const auto& v : seg_targets) pl.targets.insert(pl.targets.end(), v.begin(), v.end());
     }
     // vectors: rhs = bF - Z w, bF, cnF, per F block in order
-    for (int32_t fb = 0; fb < nFB; ++fb)
-        emit(fb, kDstRhs, col_of_fb(fb), size_of_fb(fb), 1, 1, vterms, iv, &vprod, &ipv);
-    {
-        // bF: the image slices of vterms only (no tile, no product term)
-        KTVec<ReduceTerm> bterms;
-        for (const auto& t : vterms)
-            if (t.second.kind == kSrcUb) bterms.push_back(t);
-        size_t ib = 0;
-        for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstBF, col_of_fb(fb), size_of_fb(fb), 1, 1, bterms, ib, nullptr, nullptr);
-    }
-    for (int32_t fb = 0; fb < nFB; ++fb) emit(fb, kDstCnF, col_of_fb(fb), size_of_fb(fb), 1, 1, cterms, ic, nullptr, nullptr);
+    for (int pass = 0; pass < 3; ++pass)
+        for (int32_t fb = 0; fb < nFB; ++fb) {
+            ReduceTarget t{};
+            t.dst = col_of_fb(fb);
+            t.dst_kind = pass == 0 ? kDstRhs : pass == 1 ? kDstBF : kDstCnF;
+            t.rows = size_of_fb(fb); t.cols = 1; t.ld = 1;
+            const int64_t c0 = pass == 0 ? n_mc + BS(kVc, fb) : n_mc + n_vc + (pass - 1) * n_vb + BS(kVb, fb);
+            const int64_t nc = pass == 0 ? RC(kVc, fb) : RC(kVb, fb);
+            t.c_begin = (int32_t)c0; t.c_end = (int32_t)(c0 + nc);
+            if (pass == 0) {
+                t.p_begin = (int32_t)(n_mp + BS(kVp, fb));
+                t.p_end = (int32_t)(t.p_begin + RC(kVp, fb));
+            } else {
+                t.p_begin = t.p_end = (int32_t)n_pterms;
+            }
+            pl.targets.push_back(t);
+        }
     if (world > 1) {
         // a shard writes only the blocks its points touch (about 1/world of the
         // band); the solver clears the reduced camera system before each
@@ -1172,6 +1253,22 @@ extern "C" int sfm_ba_describe(const sfm_ba_problem* prob, int32_t rank, int32_t
                     "bad arguments");
         BAHostPlan h;
         build_plan(*prob, rank, world_size, h);
+        if (std::getenv("SFM_PLAN_DIGEST")) {
+            // diagnostic: FNV-1a of every plan array (planner refactors must
+            // keep it; the arrays' element types carry no padding)
+            auto fnv = [](const auto& v) {
+                uint64_t x = 1469598103934665603ull;
+                const auto* b = reinterpret_cast<const unsigned char*>(v.data());
+                for (size_t i = 0; i < v.size() * sizeof(v[0]); ++i) x = (x ^ b[i]) * 1099511628211ull;
+                return (unsigned long long)x;
+            };
+            std::fprintf(stderr,
+                         "[digest] targets %016llx terms %016llx pterms %016llx chunks %016llx obs %016llx %016llx "
+                         "%016llx gen %016llx %016llx %016llx %016llx %016llx %016llx order %016llx %016llx\n",
+                         fnv(h.targets), fnv(h.terms), fnv(h.pterms), fnv(h.chunks), fnv(h.obs_img), fnv(h.obs_slot),
+                         fnv(h.obs_uv), fnv(h.gblk_off), fnv(h.gblk_col), fnv(h.gblk_z), fnv(h.gz_off), fnv(h.zbatch),
+                         fnv(h.zlong), fnv(h.spt_global), fnv(h.img_obs_ptr));
+        }
         *out = sfm_ba_plan_shape{};
         out->n_chunks = (int32_t)h.chunks.size();
         out->band_blocks = h.D;
