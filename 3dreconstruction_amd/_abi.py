@@ -206,6 +206,7 @@ SIGNATURES = [
     ("sfm_comm_unique_id", C.c_int, [u8p]),
     ("sfm_ctx_create", C.c_int, [C.POINTER(CtxOpts), C.POINTER(C.c_void_p)]),
     ("sfm_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("sfm_ctx_last_kernel_ms", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     ("sfm_ctx_synchronize", C.c_int, [C.c_void_p]),
     ("sfm_ba_default_options", None, [C.POINTER(BAOptions)]),
     ("sfm_ba_solve", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,

@@ -90,9 +90,8 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 // op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.  The LDS
 // operands of the next 16-wide k chunk are read while the current chunk's four
 // MFMAs run, so a runtime-length product is not LDS-latency bound.
-template <bool TA, bool TB, bool NEG>
-__device__ __forceinline__ v4d tile_mm(v4d acc, const double* A, int lda, int ar, const double* B, int ldb,
-                                       int bc, int k0, int k1) {
+template <bool TA, bool TB, bool NEG, class PA = const double*, class PB = const double*>
+__device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int ldb, int bc, int k0, int k1) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
     double a[4], b[4];
     auto load = [&](int k, double (&av)[4], double (&bv)[4]) {
@@ -117,6 +116,29 @@ __device__ __forceinline__ v4d tile_mm(v4d acc, const double* A, int lda, int ar
     }
     return acc;
 }
+// Out-of-line tile products for the level kernel.  Its eight waves run
+// different code at the same time, and with every product inlined the kernel
+// was 61 KB of code: past the 64 KB instruction cache two CUs share, so the
+// pivot wave's diagonal factor waited on instruction fetches.  Operands are
+// typed by address space (LDS: ds_read; global: global_load), since a
+// generic pointer through a call would become flat accesses.
+typedef __attribute__((address_space(3))) const double lds_cd;
+typedef __attribute__((address_space(1))) const double glb_cd;
+template <bool TA, bool TB, bool NEG>
+__device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
+    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
+}
+template <bool TA, bool TB, bool NEG>
+__device__ __noinline__ v4d mm_lg(v4d acc, lds_cd* A, int lda, int ar, glb_cd* B, int ldb, int bc, int k0, int k1) {
+    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
+}
+template <bool TA, bool TB, bool NEG>
+__device__ __noinline__ v4d mm_gl(v4d acc, glb_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
+    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
+}
+__device__ __forceinline__ lds_cd* L3(const double* p) { return (lds_cd*)p; }
+__device__ __forceinline__ glb_cd* G1(const double* p) { return (glb_cd*)p; }
+
 __device__ __forceinline__ v4d tile_ld(const double* C, int ldc, int r0, int c0) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
     v4d v;
@@ -346,8 +368,21 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
                            unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN(),
                            Bg bg = Bg()) {
     const int wave = threadIdx.x >> 6;
-    unsigned long long t0 = 0, td = 0, ta = 0, tq = 0, tb = 0;
-    if (st) t0 = stamp();
+    unsigned long long t0 = 0, td = 0, ta = 0, tq = 0, tb = 0, tw = 0;
+    // diagnostic (st): per window k (diag16(k) and the helpers' work beside
+    // it) the pivot wave's and the slowest helper's cycles, LDS maxima in the
+    // (otherwise unused) diag16 column scratch
+    unsigned long long* wmax = reinterpret_cast<unsigned long long*>(col);
+    if (st) {
+        if (threadIdx.x < 8) wmax[threadIdx.x] = 0;
+        __syncthreads();
+        t0 = stamp();
+    }
+    auto wend = [&](int k) {   // this wave's window k is done
+        if (st && (threadIdx.x & 63) == 0)
+            atomicMax(wmax + (wave == 0 ? 4 : 0) + k, stamp() - tw);
+    };
+    tw = t0;
     if (wave == 0) {
         pre0();
         wave_sync();
@@ -362,6 +397,7 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
     } else {
         preN();
     }
+    wend(0);
     __syncthreads();
     for (int k = 0;; ++k) {
         // ---- P(k): 3 - k panels, then k inverse tiles ----------------------
@@ -380,6 +416,7 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
         if (k == 3) break;
         // ---- D(k+1) ---------------------------------------------------------
         const int n = k + 1;
+        if (st) tw = stamp();
         if (wave == 0) {
             if (st) ta = stamp();
             v4d acc = tile_ld(A, LD, 16 * n, 16 * n);
@@ -413,12 +450,14 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
                             tile_mm<false, false, false>(zero4(), A, LD, 16 * n, X, LD, 16 * j, 16 * j, 16 * n));
             bg(k);
         }
+        wend(n);
         __syncthreads();
     }
     if (st && threadIdx.x == 0) {
         atomicAdd(st + 0, td);
         atomicAdd(st + 1, stamp() - t0);
         atomicAdd(st + 7, tq);
+        for (int q = 0; q < 8; ++q) atomicAdd(st + 8 + q, wmax[q]);
     }
 }
 
@@ -530,21 +569,21 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
     double* Aj = b.A + (size_t)j * M * M;
     if (wv < 4) {
         v4d acc = tile_ld(Aj, M, 16 * w, 16 * v);
-        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * w, Wa, LD, 16 * v, 0, M);
-        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * w, Wb, LD, 16 * v, 0, M);
+        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Wa), LD, 16 * v, 0, M);
+        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Wb), LD, 16 * v, 0, M);
         tile_st(Aj, M, 16 * w, 16 * v, acc);
         return;
     }
     if (16 * v < b.nrhs) {
         double* Rj = b.R + (size_t)j * M * b.nrhs;
         v4d acc = tile_ld(Rj, b.nrhs, 16 * w, 16 * v);
-        if (hl) acc = tile_mm<true, false, true>(acc, Wa, LD, 16 * w, Za, ldr, 16 * v, 0, M);
-        if (hr) acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * w, Zb, ldr, 16 * v, 0, M);
+        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Za), ldr, 16 * v, 0, M);
+        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Zb), ldr, 16 * v, 0, M);
         tile_st(Rj, b.nrhs, 16 * w, 16 * v, acc);
     }
     if (hc)
         tile_st(b.C + (size_t)j * M * M, M, 16 * w, 16 * v,
-                tile_mm<true, false, true>(zero4(), Wa, LD, 16 * w, Wc, LD, 16 * v, 0, M));
+                mm_ll<true, false, true>(zero4(), L3(Wa), LD, 16 * w, L3(Wc), LD, 16 * v, 0, M));
 }
 
 // ---- one cyclic-reduction level at stride s, one launch --------------------------
@@ -584,7 +623,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     double* Cr = Cc + M * L16;      // [16][LD] row tile w of C_r
     double* Rc = Cr + 16 * LD;      // [64][17] column tile w of R_i
     double* bad = Rc + M * L16;
-    double* col = bad + 2;          // [16] diag16 column broadcast
+    double* col = bad + 2;          // [16] diag16 column scratch; stamp maxima (diagnostic)
     unsigned long long* st = (b.stamps && w == 0) ? b.stamps : nullptr;
     unsigned long long t0 = 0, t1 = 0;
     if (st) t0 = stamp();
@@ -612,80 +651,223 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         t1 = stamp();
         if (threadIdx.x == 0) atomicAdd(st + 5, t1 - t0);   // loads
     }
-    if (sp > 0) {
-        // neighbours eliminated at stride sp: i-sp (always there) and i+sp.
-        // A_i -= Wa' Wa + Wb' Wb (lower tiles), R_i[:, w] -= Wa' z_{i-sp}[:, w] +
-        // Wb' z_{i+sp}[:, w], C_i[:, w] = -Wa' Wl_{i-sp}[:, w] and C_r's row tile
-        // w = -(Wr_{i+sp}[:, w])' Wl_{i+sp}.  Only tile A_00 is on the path to the
-        // first diagonal factor: wave 0 updates it and factors it while waves
-        // 1..7 do the other 9 tiles and the R / C products (their skinny
-        // operands read straight from global memory: X's LDS is being written).
-        const int il = i - sp, ir = i + sp;
-        const bool hir = ir < b.N;
-        const double* Z1 = b.Z + (size_t)il * M * b.nrhs + 16 * w;
-        const double* Z2 = b.Z + (size_t)ir * M * b.nrhs + 16 * w;
-        const double* WL = b.Wl + (size_t)il * M * M + 16 * w;
-        const double* WR = b.Wr + (size_t)ir * M * M + 16 * w;
-        double* Wal = Wa_l;
-        double* Wbl = Wb_l;
-        auto a_tile = [&](int q) {
-            const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
-            const int tj = q - ti * (ti + 1) / 2;
-            v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wal, M, 16 * ti, Wal, M, 16 * tj, 0, M);
-            if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * ti, Wbl, M, 16 * tj, 0, M);
-            tile_st(A, LD, 16 * ti, 16 * tj, acc);
-        };
-        // A_00's update, the only one before the first diagonal factor: its 8
-        // k-chunk products (4 per neighbour) on the 8 waves, one MFMA chunk
-        // each, staged in X rows 16..63 (free until P(1)); wave 0 subtracts
-        // them in a fixed order and goes on to diag16(0) (a 32-MFMA chain on
-        // wave 0 alone before)
-        {
-            double* scr = X + 16 * LD;
-            const int v = wave & 3;
-            v4d part = zero4();
-            if (wave < 4) part = tile_mm<true, false, false>(part, Wal, M, 0, Wal, M, 0, 16 * v, 16 * v + 16);
-            else if (hir) part = tile_mm<true, false, false>(part, Wbl, M, 0, Wbl, M, 0, 16 * v, 16 * v + 16);
-            tile_st(scr + 256 * wave, 16, 0, 0, part);
+    {
+    // neighbours eliminated at stride sp: i-sp (always there) and i+sp.
+    // A_i -= Wa' Wa + Wb' Wb (lower tiles), R_i[:, w] -= Wa' z_{i-sp}[:, w] +
+    // Wb' z_{i+sp}[:, w], C_i[:, w] = -Wa' Wl_{i-sp}[:, w] and C_r's row tile
+    // w = -(Wr_{i+sp}[:, w])' Wl_{i+sp}; then the factorisation.
+    //
+    // Just-in-time schedule (round 4).  fp64 MFMAs on a SIMD stall the
+    // fp64 VALU of the pivot wave (wave 0) there, so wave 0's SIMD
+    // partner (wave 4) issues no MFMA while a diagonal factor runs, and
+    // the six helper waves (1-3, 5-7: SIMDs 1-3) do every tile product in
+    // the four factor windows W0..W3, each tile's A update folded into
+    // its trailing updates and done just before the panel or factor that
+    // reads it, the R / C products spread over the windows' slack:
+    //   S0  all waves: A_00's update as 8 one-chunk products
+    //   W0  wave 0: A_00, diag16(0) | helpers: A updates of tiles (1,0),
+    //       (2,0), (3,0), (1,1) as 8 half products (one per neighbour),
+    //       C_0
+    //   P0  L_i0 = (A_i0 - halves) X_00'
+    //   W1  wave 0: A_11 (- halves - L_10 L_10'), diag16(1) | helpers:
+    //       tiles (2,1), (3,1), (2,2) (A update + step 0), T_10, C_1..3
+    //   P1, W2: tiles (3,2), (3,3) (A update + steps 0, 1), T_20, T_21, Cr
+    //   P2, W3: T_30, T_31, T_32, R_0..2;  P3 with R_3 on wave 4
+    // upd: the neighbours eliminated at stride sp update A / R / C (every
+    // level but the first, whose blocks come straight from bcr_pack)
+    const bool upd = sp > 0;
+    const int il = i - sp, ir = i + sp;
+    const bool hir = upd && ir < b.N;
+    const double* Z1 = b.Z + (size_t)il * M * b.nrhs + 16 * w;
+    const double* Z2 = b.Z + (size_t)ir * M * b.nrhs + 16 * w;
+    const double* WL = b.Wl + (size_t)il * M * M + 16 * w;
+    const double* WR = b.Wr + (size_t)ir * M * M + 16 * w;
+    double* Wal = Wa_l;
+    double* Wbl = Wb_l;
+    // scratch tiles (LD layout): X's lower tiles until T_10 (window 1);
+    // the tiles above the block diagonal of X and A, which nothing reads
+    auto tile_at = [&](int sel, int r, int c) { return (sel ? X : A) + 16 * r * LD + 16 * c; };
+    constexpr int8_t kS0[8][2] = {{1, 0}, {2, 0}, {3, 0}, {2, 1}, {3, 1}, {3, 2}, {0, 1}, {0, 2}};   // in X
+    constexpr int8_t kHp[8][3] = {{0, 0, 1}, {0, 0, 2}, {0, 0, 3}, {0, 1, 2}, {0, 1, 3}, {0, 2, 3},
+                                  {1, 0, 3}, {1, 1, 2}};   // (X?, r, c)
+    auto hp = [&](int h) { return tile_at(kHp[h][0], kHp[h][1], kHp[h][2]); };
+    constexpr int8_t kHt[4][2] = {{1, 0}, {2, 0}, {3, 0}, {1, 1}};   // half products: tile h / 2, neighbour h & 1
+    auto half = [&](int h) {
+        if (!upd) return;
+        const int ti = kHt[h >> 1][0], tj = kHt[h >> 1][1];
+        double* W = (h & 1) ? Wbl : Wal;
+        if ((h & 1) && !hir) return;
+        tile_st(hp(h), LD, 0, 0, mm_ll<true, false, false>(zero4(), L3(W), M, 16 * ti, L3(W), M, 16 * tj, 0, M));
+    };
+    auto sub_halves = [&](v4d acc, int t) {   // acc - half a - half b of tile t (fixed order)
+        if (!upd) return acc;
+        acc -= tile_ld(hp(2 * t), LD, 0, 0);
+        if (hir) acc -= tile_ld(hp(2 * t + 1), LD, 0, 0);
+        return acc;
+    };
+    // tile (ti, tj): its A update, then the trailing updates of steps 0..nk-1
+    auto full = [&](int ti, int tj, int nk) {
+        v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
+        if (upd) acc = mm_ll<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, 0, M);
+        if (hir) acc = mm_ll<true, false, true>(acc, L3(Wbl), M, 16 * ti, L3(Wbl), M, 16 * tj, 0, M);
+        for (int k = 0; k < nk; ++k)
+            acc = mm_ll<false, true, true>(acc, L3(A), LD, 16 * ti, L3(A), LD, 16 * tj, 16 * k, 16 * k + 16);
+        tile_st(A, LD, 16 * ti, 16 * tj, acc);
+    };
+    // T_nj = sum_{m=j..n-1} L_nm X_mj into X tile (n, j)
+    auto tinv = [&](int n, int j) {
+        tile_st(X, LD, 16 * n, 16 * j, mm_ll<false, false, false>(zero4(), L3(A), LD, 16 * n, L3(X), LD, 16 * j, 16 * j, 16 * n));
+    };
+    auto bgR = [&](int v) {
+        if (!hz || !upd) return;
+        v4d acc = tile_ld(Rc, L16, 16 * v, 0);
+        acc = mm_lg<true, false, true>(acc, L3(Wal), M, 16 * v, G1(Z1), b.nrhs, 0, 0, M);
+        if (hir) acc = mm_lg<true, false, true>(acc, L3(Wbl), M, 16 * v, G1(Z2), b.nrhs, 0, 0, M);
+        tile_st(Rc, L16, 16 * v, 0, acc);
+    };
+    auto bgC = [&](int v) {   // block (i, i-2sp) = (i, i-s)
+        if (upd) tile_st(Cc, L16, 16 * v, 0, mm_lg<true, false, true>(zero4(), L3(Wal), M, 16 * v, G1(WL), M, 0, 0, M));
+    };
+    auto bgCr = [&](int v) {   // block (r, r-s) = (r, i)
+        if (hr && hir)
+            tile_st(Cr, LD, 0, 16 * v, mm_gl<true, false, true>(zero4(), G1(WR), M, 0, L3(Wbl), M, 16 * v, 0, M));
+    };
+    // P(k), k >= 1: panels L_ik = A_ik X_kk' (i > k) and X_kj = -X_kk T_kj (j < k), waves 0..2
+    auto pphase = [&](int k) {
+        if (wave >= 3) return;
+        if (wave < 3 - k) {
+            const int ii = k + 1 + wave;
+            tile_st(A, LD, 16 * ii, 16 * k,
+                    tile_mm<false, true, false>(zero4(), L3(A), LD, 16 * ii, L3(X), LD, 16 * k, 16 * k, 16 * k + 16));
+        } else {
+            const int j = wave - (3 - k);
+            tile_st(X, LD, 16 * k, 16 * j,
+                    tile_mm<false, false, true>(zero4(), L3(X), LD, 16 * k, L3(X), LD, 16 * j, 16 * k, 16 * k + 16));
         }
-        __syncthreads();
-        auto pre0 = [&] {
-            const double* scr = X + 16 * LD;
+    };
+    // diagnostic stamps (w == 0 workgroups, SFM_BCR_STAMPS): as chol_inv64
+    unsigned long long* wmax = reinterpret_cast<unsigned long long*>(col);
+    unsigned long long tf0 = 0, td = 0, tq = 0, tw = 0;
+    if (st) {
+        if (threadIdx.x < 8) wmax[threadIdx.x] = 0;
+        tf0 = stamp();
+    }
+    auto wend = [&](int k) {
+        if (st && (threadIdx.x & 63) == 0) atomicMax(wmax + (wave == 0 ? 4 : 0) + k, stamp() - tw);
+    };
+    // the pivot wave: A_nn's last update, then diag16(n)
+    auto dfac = [&](int n, v4d acc) {
+        unsigned long long ta = 0, tb = 0;
+        if (st) ta = stamp();
+        tile_st(A, LD, 16 * n, 16 * n, acc);
+        wave_sync();
+        if (st) tb = stamp();
+        diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+        if (st) {
+            const unsigned long long te = stamp();
+            td += te - ta;
+            tq += te - tb;
+        }
+    };
+    // ---- S0 -----------------------------------------------------------------
+    {
+        const int v = wave & 3;
+        v4d part = zero4();
+        if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, 16 * v + 16);
+        else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, 16 * v + 16);
+        if (upd) tile_st(tile_at(1, kS0[wave][0], kS0[wave][1]), LD, 0, 0, part);
+    }
+    __syncthreads();
+    // ---- W0 -----------------------------------------------------------------
+    if (st) tw = stamp();
+    switch (wave) {
+        case 0: {
             v4d acc = tile_ld(A, LD, 0, 0);
+            if (upd) {
 #pragma unroll
-            for (int q = 0; q < NWL; ++q) acc -= tile_ld(scr + 256 * q, 16, 0, 0);
-            tile_st(A, LD, 0, 0, acc);
-        };
-        // A tiles 1..9 over waves 1..7 before the first barrier (P(0) and D(1)
-        // read them)
-        auto preN = [&] {
-            for (int q = wave; q < 10; q += NWL - 1) a_tile(q);
-        };
-        // the R / C products are read only after the factorisation: one per
-        // helper wave in each of the windows of diag16(1..3), where those
-        // waves idle after their few trailing tiles (12 items, 21 slots)
-        auto bg = [&](int k) {
-            const int t = 7 * k + wave - 1;   // 0..20
-            if (t < 4) {
-                const int v = t;
-                if (hz) {
-                    v4d acc = tile_ld(Rc, L16, 16 * v, 0);
-                    acc = tile_mm<true, false, true>(acc, Wal, M, 16 * v, Z1, b.nrhs, 0, 0, M);
-                    if (hir) acc = tile_mm<true, false, true>(acc, Wbl, M, 16 * v, Z2, b.nrhs, 0, 0, M);
-                    tile_st(Rc, L16, 16 * v, 0, acc);
-                }
-            } else if (t < 8) {
-                const int v = t - 4;    // block (i, i-2sp) = (i, i-s)
-                tile_st(Cc, L16, 16 * v, 0, tile_mm<true, false, true>(zero4(), Wal, M, 16 * v, WL, M, 0, 0, M));
-            } else if (t < 12 && hr && hir) {
-                const int v = t - 8;    // block (r, r-s) = (r, i)
-                tile_st(Cr, LD, 0, 16 * v, tile_mm<true, false, true>(zero4(), WR, M, 0, Wbl, M, 16 * v, 0, M));
+                for (int q = 0; q < NWL; ++q) acc -= tile_ld(tile_at(1, kS0[q][0], kS0[q][1]), LD, 0, 0);
             }
-        };
-        chol_inv64<NWL>(A, X, bad, col, st, pre0, preN, bg);
-    } else {
-        chol_inv64<NWL>(A, X, bad, col, st);
+            dfac(0, acc);
+            break;
+        }
+        case 1: half(0); half(3); break;
+        case 2: half(1); half(4); break;
+        case 3: half(2); break;
+        case 5: half(6); break;
+        case 6: half(7); break;
+        case 7: half(5); bgC(0); break;
+        default: break;
+    }
+    wend(0);
+    __syncthreads();
+    // ---- P0 -----------------------------------------------------------------
+    if (wave < 3) {
+        const int ii = 1 + wave;
+        tile_st(A, LD, 16 * ii, 0, sub_halves(tile_ld(A, LD, 16 * ii, 0), wave));
+        wave_sync();
+        tile_st(A, LD, 16 * ii, 0, tile_mm<false, true, false>(zero4(), L3(A), LD, 16 * ii, L3(X), LD, 0, 0, 16));
+    }
+    __syncthreads();
+    // ---- W1 -----------------------------------------------------------------
+    if (st) tw = stamp();
+    switch (wave) {
+        case 0: {
+            v4d acc = sub_halves(tile_ld(A, LD, 16, 16), 3);
+            dfac(1, tile_mm<false, true, true>(acc, L3(A), LD, 16, L3(A), LD, 16, 0, 16));
+            break;
+        }
+        case 1: full(2, 1, 1); break;
+        case 2: full(3, 1, 1); break;
+        case 3: full(2, 2, 1); break;
+        case 5: tinv(1, 0); bgC(1); break;
+        case 6: bgC(2); break;
+        case 7: bgC(3); break;
+        default: break;
+    }
+    wend(1);
+    __syncthreads();
+    pphase(1);
+    __syncthreads();
+    // ---- W2 -----------------------------------------------------------------
+    if (st) tw = stamp();
+    switch (wave) {
+        case 0: dfac(2, tile_mm<false, true, true>(tile_ld(A, LD, 32, 32), L3(A), LD, 32, L3(A), LD, 32, 16, 32)); break;
+        case 1: full(3, 2, 2); break;
+        case 2: full(3, 3, 2); break;
+        case 3: tinv(2, 0); tinv(2, 1); break;
+        case 5: bgCr(0); break;
+        case 6: bgCr(1); break;
+        case 7: bgCr(2); bgCr(3); break;
+        default: break;
+    }
+    wend(2);
+    __syncthreads();
+    pphase(2);
+    __syncthreads();
+    // ---- W3 -----------------------------------------------------------------
+    if (st) tw = stamp();
+    switch (wave) {
+        case 0: dfac(3, tile_mm<false, true, true>(tile_ld(A, LD, 48, 48), L3(A), LD, 48, L3(A), LD, 48, 32, 48)); break;
+        case 1: tinv(3, 0); break;
+        case 2: tinv(3, 1); break;
+        case 3: tinv(3, 2); break;
+        case 5: bgR(0); break;
+        case 6: bgR(1); break;
+        case 7: bgR(2); break;
+        default: break;
+    }
+    wend(3);
+    __syncthreads();
+    // ---- P3 (+ R_3 on wave 4) ----------------------------------------------
+    pphase(3);
+    if (wave == 4) bgR(3);   // (no-op at the first level)
+    __syncthreads();
+    if (st && threadIdx.x == 0) {
+        atomicAdd(st + 0, td);
+        atomicAdd(st + 1, stamp() - tf0);
+        atomicAdd(st + 7, tq);
+        for (int q = 0; q < 8; ++q) atomicAdd(st + 8 + q, wmax[q]);
+    }
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     {   // X for the back substitution: each of the block's 4 workgroups stores 16 rows
@@ -707,13 +889,13 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         if (pr < 0) break;
         if (pr == 0)
             tile_st(b.Wl + (size_t)i * M * M, M, 16 * r, 16 * w,
-                    tile_mm<false, false, false>(zero4(), X, LD, 16 * r, Cc, L16, 0, 0, kend));
+                    tile_mm<false, false, false>(zero4(), L3(X), LD, 16 * r, L3(Cc), L16, 0, 0, kend));
         else if (pr == 1 && hr)   // op(B)[k][n] = C_r[16w + n][k]
             tile_st(b.Wr + (size_t)i * M * M, M, 16 * r, 16 * w,
-                    tile_mm<false, true, false>(zero4(), X, LD, 16 * r, Cr, LD, 0, 0, kend));
+                    tile_mm<false, true, false>(zero4(), L3(X), LD, 16 * r, L3(Cr), LD, 0, 0, kend));
         else if (pr == 2 && hz)
             tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * r, 16 * w,
-                    tile_mm<false, false, false>(zero4(), X, LD, 16 * r, Rc, L16, 0, 0, kend));
+                    tile_mm<false, false, false>(zero4(), L3(X), LD, 16 * r, L3(Rc), L16, 0, 0, kend));
     }
     if (st) {
         __syncthreads();

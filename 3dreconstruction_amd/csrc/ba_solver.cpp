@@ -353,7 +353,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         // the back substitution's tagged y granules (tags = solve epochs from 1)
         SFM_HIP(hipMemsetAsync(pl->bcr.Y, 0, sizeof(double) * bcr_y_granules(pl->bcr), s));
         if (std::getenv("SFM_BCR_STAMPS")) {
-            pl->bcr_stamps.alloc(8);
+            pl->bcr_stamps.alloc(16);
             pl->bcr_stamps.zero(s);
             pl->bcr.stamps = pl->bcr_stamps.p;
         }
@@ -507,13 +507,15 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
 
     double prev_gmax = 0.0;
     int step_no = 0;
+    // SFM_SCHUR_TIME_ALL (measurement): time every Schur launch after the first
+    const bool time_all = std::getenv("SFM_SCHUR_TIME_ALL") != nullptr;
     while (term < 0) {
         // ---- one step on the device ------------------------------------------
         // the Schur launch is timed with events on the second and third steps of each
         // solve only: an event pair costs ~12 us of stream serialisation
         // (the first pass, which also forms the point scales, is not timed)
         const bool first = step_no == 0;
-        const bool timed = step_no == 1 || step_no == 2;
+        const bool timed = time_all ? step_no >= 1 : (step_no == 1 || step_no == 2);
         ++step_no;
         if (timed) SFM_HIP(hipEventRecord(ev[0], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
@@ -630,12 +632,14 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         term = finalize(cur, prev_gmax);
     }
     if (pl->bcr.stamps) {  // diagnostic: average cycles per odd block, all levels
-        unsigned long long st[8];
+        unsigned long long st[16];
         SFM_HIP(hipMemcpy(st, pl->bcr.stamps, sizeof st, hipMemcpyDeviceToHost));
         const double n = st[4] ? (double)st[4] : 1.0;
         std::fprintf(stderr, "[bcr stamps] cycles/odd block: loads %.0f load+update %.0f chol %.0f (diag16 %.0f, "
-                     "pivots alone %.0f) to X copy %.0f total %.0f over %llu\n",
-                     st[5] / n, st[2] / n, st[1] / n, st[0] / n, st[7] / n, st[6] / n, st[3] / n, st[4]);
+                     "pivots alone %.0f) to X copy %.0f total %.0f over %llu; windows 0..3 pivot wave %.0f %.0f %.0f "
+                     "%.0f, slowest helper %.0f %.0f %.0f %.0f\n",
+                     st[5] / n, st[2] / n, st[1] / n, st[0] / n, st[7] / n, st[6] / n, st[3] / n, st[4],
+                     st[12] / n, st[13] / n, st[14] / n, st[15] / n, st[8] / n, st[9] / n, st[10] / n, st[11] / n);
     }
     if (pl->dense.stamps) {  // diagnostic: dataflow chain, average cycles per block column
         unsigned long long st[16];

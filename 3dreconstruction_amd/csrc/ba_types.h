@@ -39,8 +39,13 @@ constexpr int kGroupChunks = 4;           // chunks per tile group, at most (the
 // is 60-68 KB: two workgroups, 8 waves per CU as one-wave chunks had), 1 for
 // 80-row tiles (their 26-30 KB per wave: two-wave groups would cost the
 // RADIAL3 variant a wave per CU)
+// Default 1 (round 4): four-chunk groups cut the tile writes four-fold and
+// the reduce kernels from 39 to 27 us per iteration at C4, but the Schur
+// launch went 0.339 -> 0.368 ms (a group's waves finish together and hold
+// its LDS until the slowest is done): C4 1041 vs 1048 LM-iters/s on one box
+// (profiles/r04/c_jit/ab.txt).  -DSFM_SCHUR_GROUP=4 builds the grouped form.
 #ifndef SFM_SCHUR_GROUP   // A/B builds: chunks per group of 64-row tiles
-#define SFM_SCHUR_GROUP kGroupChunks
+#define SFM_SCHUR_GROUP 1
 #endif
 constexpr int schur_group(int tile_nt) { return tile_nt == 4 ? SFM_SCHUR_GROUP : 1; }
 constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass

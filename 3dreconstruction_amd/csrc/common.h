@@ -209,6 +209,7 @@ struct sfm_ctx {
     int cu_count = 0;
     bool no_exchange = false;                    // SFM_CTX_DIAG_NO_EXCHANGE (per-rank timing only)
     hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
+    double last_kernel_ms = 0.0;                 // sfm_fmatrix_ac's kernel (sfm_ctx_last_kernel_ms)
 };
 
 namespace sfm {

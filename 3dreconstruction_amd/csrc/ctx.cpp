@@ -349,6 +349,14 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
     });
 }
 
+extern "C" int sfm_ctx_last_kernel_ms(sfm_ctx* ctx, double* ms) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx && ms, SFM_ERR_INVALID_ARG, "sfm_ctx_last_kernel_ms: bad arguments");
+        *ms = ctx->last_kernel_ms;
+        return SFM_OK;
+    });
+}
+
 extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
     return guarded([&] {
         if (!ctx) return SFM_OK;

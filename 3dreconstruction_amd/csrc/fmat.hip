@@ -662,9 +662,17 @@ extern "C" int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off,
             attr = true;
         }
         SFM_REQUIRE(n_pairs < ((int64_t)1 << 31), SFM_ERR_UNSUPPORTED, "sfm_fmatrix_ac: too many pairs");
+        // the kernel alone (sfm_ctx_last_kernel_ms): the uploads are drained
+        // first, or the start event can be stamped while a DMA of the stream
+        // is still running (measured: 48 ms by events against rocprofv3's 29)
+        SFM_HIP(hipStreamSynchronize(s));
+        tm.mark("upload");
+        hipEvent_t* ev = ctx_events(ctx);
+        SFM_HIP(hipEventRecord(ev[0], s));
         hipLaunchKernelGGL(fmatrix_ac_kernel, dim3((unsigned)n_pairs), dim3(kFT), lds, s, a);
         SFM_HIP(hipGetLastError());
-        tm.mark("upload+launch");
+        SFM_HIP(hipEventRecord(ev[1], s));
+        tm.mark("launch");
         std::vector<double> F(9 * (size_t)n_pairs), stat(4 * (size_t)n_pairs);
         std::vector<uint32_t> binl((size_t)std::max<int64_t>(n, 1));
         int32_t fail = 0;
@@ -673,6 +681,11 @@ extern "C" int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off,
         if (n) SFM_HIP(hipMemcpyAsync(binl.data(), d_binl.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
         SFM_HIP(hipMemcpyAsync(&fail, d_fail.p, 4, hipMemcpyDeviceToHost, s));
         SFM_HIP(hipStreamSynchronize(s));
+        {
+            float ms = 0.f;
+            SFM_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+            ctx->last_kernel_ms = ms;
+        }
         tm.mark("kernel+download");
         SFM_REQUIRE(!fail, SFM_ERR_UNSUPPORTED, "sfm_fmatrix_ac: a pair drew more than %lld random numbers",
                     (long long)kRngWords);

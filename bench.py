@@ -253,9 +253,24 @@ def pmc_child(args):
     ctx.close()
 
 
-def pmc_measure(args, kernel_regex="schur_kernel"):
-    """HBM bytes and MFMA-busy cycles per launch of the Schur kernel, measured
-    now by rocprofv3 --pmc passes over a child run of the same C4 plan.
+def pmc_child_match(args):
+    """--pmc-child-match: the C3 collection matched once (ratio mode, every
+    pair in one launch, as the bench's timed run), nothing else."""
+    ctx = api.Context(0)
+    nf, nkp = args.match_frames, 4096
+    desc = api.synth_descriptors(nf, nkp)
+    off = np.arange(nf + 1, dtype=np.int64) * nkp
+    mplan = api.MatchPlan(ctx, desc, off)
+    mplan.run(api.exhaustive_pairs(nf), count=False)
+    ctx.synchronize()
+    mplan.close()
+    ctx.close()
+
+
+def pmc_measure(args, kernel_regex="schur_kernel", child="--pmc-child"):
+    """HBM bytes and MFMA-busy cycles per launch of the Schur kernel (or the
+    matcher: child --pmc-child-match), measured now by rocprofv3 --pmc passes
+    over a child run of the same configuration.
     Returns None when rocprofv3 is unavailable or a pass fails."""
     import csv
     import glob
@@ -272,8 +287,8 @@ def pmc_measure(args, kernel_regex="schur_kernel"):
         for k, counters in enumerate(PMC_PASSES):
             d = os.path.join(tmp, f"pass{k}")
             cmd = [prof, "--pmc", *counters, "--kernel-include-regex", kernel_regex, "--output-format", "csv",
-                   "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--pmc-child",
-                   "--n-cam", str(args.n_cam), "--n-pt", str(args.n_pt)]
+                   "-d", d, "-o", "p", "--", sys.executable, os.path.abspath(__file__), child,
+                   "--n-cam", str(args.n_cam), "--n-pt", str(args.n_pt), "--match-frames", str(args.match_frames)]
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
             except subprocess.TimeoutExpired:
@@ -470,11 +485,16 @@ def bench_filter(ctx, n_pairs, n_match, cpu=True, cpu_pairs=32):
     t0 = time.perf_counter()
     res = api.fmatrix_ac(ctx, xs, whs)
     dt = time.perf_counter() - t0
+    kms = C.c_double(0.0)
+    abi.load().sfm_ctx_last_kernel_ms(ctx.h, C.byref(kms))
     iters = sum(r["iterations"] for r in res)
     kept = sum(r["n_inliers"] > 0 for r in res)
     out = {"metric": "geometric filter pairs/sec (F-matrix AC-RANSAC, 2048 iterations)", "value": n_pairs / dt,
            "unit": "pairs/s", "seconds": dt, "pairs": n_pairs, "matches_per_pair": n_match,
            "ransac_iterations_per_sec": iters / dt, "pairs_kept": kept,
+           # the timed call includes the host normalisation, the uploads and
+           # the result download; the kernel alone (HIP events):
+           "kernel_ms": kms.value, "kernel_pairs_per_sec": n_pairs / (kms.value * 1e-3) if kms.value > 0 else None,
            "inliers": int(sum(r["n_inliers"] for r in res)),
            "workload": f"{n_pairs} pairs x {n_match} putative matches (30% clutter), 1920x1080 views, "
                        "GeometricFilter_FMatrix_AC(4.0, 2048) semantics (sparseBuilder.cpp:1179-1186); "
@@ -538,9 +558,13 @@ def main():
     ap.add_argument("--allow-host-allreduce", action="store_true")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child-match", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         pmc_child(args)
+        return
+    if args.pmc_child_match:
+        pmc_child_match(args)
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -649,6 +673,20 @@ def main():
     dt = max_over_ranks(time.perf_counter() - t0)
     value = iters / dt
     obs_per_sec = iters * sc["n_obs"] / dt
+    schur_sampled_ms = schur_ms / max(schur_n, 1)
+    # the roofline's launch time: every Schur launch but each solve's first
+    # (which also forms the point scales), over separate solves after the timed
+    # region (the timed solves carry events on two launches each: an event
+    # pair serialises the stream for ~12 us)
+    os.environ["SFM_SCHUR_TIME_ALL"] = "1"
+    schur_ms, schur_n = 0.0, 0
+    for _ in range(max(3, min(args.steps, 10))):
+        plan.run()
+        inf = plan.info()
+        schur_ms += inf.schur_ms_total
+        schur_n += inf.schur_launches
+    ctx.synchronize()
+    del os.environ["SFM_SCHUR_TIME_ALL"]
     schur_avg_ms = schur_ms / max(schur_n, 1)
     flops = info.schur_flops_per_iter
     achieved = flops / (schur_avg_ms * 1e-3) / 1e12 if schur_n else 0.0
@@ -865,9 +903,26 @@ def main():
         t1 = time.time()
         pmc = pmc_measure(args)
         log(f"pmc passes: {time.time() - t1:.1f}s -> {pmc}")
+        if match is not None:
+            t1 = time.time()
+            pm = pmc_measure(args, kernel_regex="match_top2", child="--pmc-child-match")
+            log(f"pmc passes (matcher): {time.time() - t1:.1f}s -> {pm}")
+            if pm is not None:
+                mr = match["roofline"]
+                mr["traffic"] = pm["traffic"]
+                mr["traffic_source"] = (f"rocprofv3 --pmc in this run: FETCH_SIZE x2 (gfx950) + WRITE_SIZE of the "
+                                        f"C3 launch ({pm['launches']} launch(es))")
+                # the distinct bytes a C3 launch must read at least once: every
+                # image's int8 rows and key bases (each image is reused by ~499 pairs)
+                mr["algorithmic_bytes_per_launch"] = args.match_frames * 4096 * (128 + 4 + 4)
+                if "SQ_VALU_MFMA_BUSY_CYCLES" in pm and mr.get("per_launch_ms"):
+                    mr["mfma_busy"] = pm["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * mr["per_launch_ms"] * 1e-3 * 2.4e9)
     roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TF,
             "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TF,
             "traffic": None, "kernel": "schur_kernel", "per_launch_ms": schur_avg_ms,
+            "per_launch_ms_basis": f"HIP events on all {schur_n} non-first Schur launches of "
+                                   f"{max(3, min(args.steps, 10))} solves after the timed region",
+            "per_launch_ms_sampled": schur_sampled_ms,
             "algorithmic_flops_per_launch": flops,
             "flops_formula": "sum over points of 3 r (r+1) + 780 k + 30 (r = F rows of the point, "
                              "k = its observations; DESIGN.md §5)"}

@@ -593,6 +593,11 @@ int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off, const doub
                    const int32_t* wh, const sfm_fmatrix_opts* opts,
                    sfm_fmatrix_result* results, int32_t* inliers);
 
+/* Device time (HIP events on the context's stream) of the kernel of the
+ * context's last sfm_fmatrix_ac call, without its host normalisation,
+ * uploads and downloads (measurement; no reference counterpart). */
+int sfm_ctx_last_kernel_ms(sfm_ctx* ctx, double* ms);
+
 /* sparseBuilder::filter(), file-staged: sfm_data.json (view sizes) +
  * <stem>.feat + matches.putative.bin -> sfm_fmatrix_ac ->
  * matches.f.bin (kept pairs, each pair's IndMatches in vec_inliers order).

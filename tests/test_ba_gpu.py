@@ -454,6 +454,47 @@ def test_plan_cache_reuse_is_bit_identical(ctx):
     lib.sfm_ba_cache_clear(ctx.h)
 
 
+@pytest.mark.parametrize("vis_mode", [0, 1])
+def test_grown_structure_after_cached_plan_bit_identical(ctx, vis_mode):
+    # the loop's calls see a world grown by one image.  A
+    # solve of the grown problem on a context whose cache holds the previous
+    # call's plan (the structure changed: the plan is rebuilt over recycled
+    # device / staging memory, flags and epochs included) must equal a solve
+    # on a fresh context bit for bit -- band (vis 0) and dense with general
+    # points (vis 1) -- and stay the oracle's solve.
+    lib = abi.load()
+    seed = 5150 + vis_mode
+
+    def scene():
+        s = H.Scene(40, 4000, 6, vis_mode=vis_mode, seed=seed)
+        s._seed = seed
+        return s
+    sc = scene()
+    cut = sc.n_cam - 1
+    obs_img = sc.obs_img.copy()
+    before = _subset(scene(), lambda p, ids: (lambda k: k if len(k) >= 2 else [])(
+        [o for o in ids if obs_img[o] < cut]))
+    after = scene()
+    lib.sfm_ba_cache_clear(ctx.h)
+    rc0, s0, _ = _solve_keep(ctx, before, *before.params())
+    assert rc0 == 0
+    grown = _solve_keep(ctx, after, *after.params())     # cache holds `before`'s plan
+    c2 = api.Context(0)
+    try:
+        fresh = _solve_keep(c2, after, *after.params())
+    finally:
+        c2.close()
+    assert grown[0] == fresh[0] == 0
+    assert (grown[1].iterations, grown[1].initial_cost, grown[1].final_cost) == \
+        (fresh[1].iterations, fresh[1].initial_cost, fresh[1].final_cost)
+    for u, v in zip(grown[2], fresh[2]):
+        np.testing.assert_array_equal(u, v)
+    _, os_, _, _ = H.oracle_solve(after, threads=8)
+    assert grown[1].iterations == os_.iterations
+    assert abs(grown[1].rmse_final / os_.rmse_final - 1) < RTOL_COST
+    lib.sfm_ba_cache_clear(ctx.h)
+
+
 def _shuffle_within_points(sc, seed):
     # each point's observations in a random (non-image) order, measurements
     # moved with their images: the same problem, a different layout
