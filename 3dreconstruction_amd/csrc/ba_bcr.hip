@@ -1420,13 +1420,14 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
     chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(Akk, Xkk, flag, flag + 1);
     const int wave = threadIdx.x >> 6;
     if (i == k) {
-        double* dst = d.A + (int64_t)k * kDM * np + (int64_t)k * kDM;
+        // X_kk only.  L_kk itself is never read again (the updates and both
+        // substitutions use X_kk and the off-diagonal L tiles), and writing it
+        // over A_kk raced with this launch's other workgroups, which read A_kk
+        // as they start: a workgroup dispatched late -- e.g. behind another
+        // stream's kernel holding the CUs -- factored L_kk instead of A_kk.
+        // That was the round-3 look-ahead's wrong solves.
         double* xd = d.X + (int64_t)k * kDM * kDM;
-        for (int e = threadIdx.x; e < M * M; e += NT) {
-            const int r = e / M, c = e % M;
-            dst[(int64_t)r * np + c] = Akk[r * LD + c];
-            xd[e] = Xkk[r * LD + c];
-        }
+        for (int e = threadIdx.x; e < M * M; e += NT) xd[e] = Xkk[(e / M) * LD + e % M];
         // y_k = X_kk b_k (b_k final: every earlier column's update is done)
         if (threadIdx.x < M) {
             const int r = threadIdx.x;

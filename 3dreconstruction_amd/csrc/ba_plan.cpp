@@ -386,7 +386,6 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     tm.mark("pt_off");
     pl.obs_img.resize(pl.n_sobs);
     pl.obs_uv.resize(2 * pl.n_sobs);
-    pl.obs_slot.assign(pl.n_sobs, 0);
     parallel_ranges(pl.n_spt, [&](int64_t k0, int64_t k1, int) {
         for (int64_t k = k0; k < k1; ++k) {
             const int64_t p = pl.spt_global[k];
@@ -653,7 +652,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         if (pl.chunks[c].sub == 0) pl.group_off.push_back(c);
     pl.group_off.push_back((int32_t)pl.chunks.size());
     tm.mark("chunks");
-    std::copy(cslot.begin(), cslot.end(), pl.obs_slot.begin());
+    // the chunk points' slots are final; the general points' are written below
+    cslot.resize(pl.n_sobs);
+    pl.obs_slot.swap(cslot);
     pl.n_gpt = pl.n_spt - pl.n_cpt;
     // a general point's observations in image order, so that repeated views
     // of one image are adjacent (the Z kernel sums runs of one camera block);
@@ -842,6 +843,49 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     };
     auto col_of_fb = [&](int32_t b) -> int64_t { return b < ncam ? 6LL * b : pl.nb + (int64_t)pl.iw * (b - ncam); };
     auto size_of_fb = [&](int32_t b) { return b < ncam ? 6 : pl.iw; };
+    // Terms are stored resolved against the solver's one source buffer
+    // [chunk tiles | U | Ub | Ucn] (ba_solver.cpp create_plan: the same layout)
+    const int64_t fw = 6 + pl.iw;
+    const int64_t o_u = std::max<int64_t>(pl.n_group(), 1) * kTileR * kTileR, o_ub = o_u + fw * fw * P.n_img * kGramSeg,
+                  o_ucn = o_ub + fw * P.n_img * kGramSeg;
+    auto flat = [&](const ReduceTerm& q, bool vec) {
+        FlatTerm f{};
+        f.sign = q.sign;
+        f.mode = kFlatRows;
+        switch (q.kind) {
+            case kSrcTile: {
+                // slot blocks occupy disjoint tile rows, so a block of two
+                // slots is wholly below or wholly above the diagonal
+                const int64_t base = (int64_t)q.index * kTileR * kTileR;
+                if (vec || q.roff > q.coff) {
+                    f.off = base + q.roff * kTileR + q.coff;
+                    f.rs = vec ? 1 : kTileR;
+                } else if (q.roff < q.coff) {
+                    f.off = base + q.coff * kTileR + q.roff;
+                    f.rs = 1;
+                    f.mode = kFlatTrans;
+                } else {   // rs = the origin's offset within the tile
+                    f.off = base + q.roff * kTileR + q.coff;
+                    f.rs = (int16_t)(q.roff * kTileR + q.coff);
+                    f.mode = kFlatSym;
+                }
+                break;
+            }
+            case kSrcU:
+                f.off = o_u + q.index * fw * fw + q.roff * fw + q.coff;
+                f.rs = (int16_t)fw;
+                break;
+            case kSrcUb:
+                f.off = o_ub + q.index * fw + q.roff;
+                f.rs = 1;
+                break;
+            default:
+                f.off = o_ucn + q.index * fw + q.roff;
+                f.rs = 1;
+                break;
+        }
+        return f;
+    };
     // band: a corner block (k, l), k < l, is stored too, as the transpose of
     // (l, k): terms of an off-diagonal corner key go to two targets
     auto twice = [&](int32_t fa, int32_t fb) { return band && fb >= ncam && fb != fa; };
@@ -1102,13 +1146,13 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                     tg.push_back(t);
                 }
             // (3) the terms, sources in order
-            ReduceTerm* T = pl.terms.data();
+            FlatTerm* T = pl.terms.data();
             PTerm* PT = pl.pterms.data();
             auto put = [&](int64_t q, bool tw, ReduceTerm r) {
-                T[cs[q]++] = r;
+                T[cs[q]++] = flat(r, false);
                 if (tw) {
                     std::swap(r.roff, r.coff);
-                    T[cs[q - 1]++] = r;
+                    T[cs[q - 1]++] = flat(r, false);
                 }
             };
             auto put_p = [&](int64_t q, bool tw, PTerm r) {
@@ -1128,9 +1172,9 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             }
             auto put_v = [&](int32_t f, int16_t ro, int32_t idx) {
                 int64_t* v = &vcur[4 * (f - r0)];
-                T[v[0]++] = ReduceTerm{kSrcUb, idx, ro, 0, 1.f};
-                T[v[2]++] = ReduceTerm{kSrcUb, idx, ro, 0, 1.f};
-                T[v[3]++] = ReduceTerm{kSrcUcn, idx, ro, 0, 1.f};
+                T[v[0]++] = flat(ReduceTerm{kSrcUb, idx, ro, 0, 1.f}, true);
+                T[v[2]++] = flat(ReduceTerm{kSrcUb, idx, ro, 0, 1.f}, true);
+                T[v[3]++] = flat(ReduceTerm{kSrcUcn, idx, ro, 0, 1.f}, true);
             };
             for (const ImgSrc& s : isrc)
                 for (int g = 0; g < kGramSeg; ++g) {
@@ -1152,7 +1196,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                     const int32_t fa = gfb[(size_t)c * kMaxSlots + a];
                     if (!in(fa)) continue;
                     // rhs contribution (-Z w) from tile row 79
-                    T[vcur[4 * (fa - r0)]++] = ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f};
+                    T[vcur[4 * (fa - r0)]++] = flat(ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}, true);
                     for (int b = 0; b < cd.n_slots; ++b) {
                         const int32_t fb = gfb[(size_t)c * kMaxSlots + b];
                         if (fa < fb || !held(fa, fb)) continue;

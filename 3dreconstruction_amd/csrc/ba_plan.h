@@ -71,7 +71,7 @@ struct BAHostPlan {
 
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;
-    HostVec<ReduceTerm> terms;       // (default-initialised: every entry is written)
+    HostVec<FlatTerm> terms;         // resolved against the solver's source buffer (default-initialised)
     HostVec<PTerm> pterms;           // uploaded as it is: page-locked staging
     int64_t n_sband = 0, n_sarrow = 0, n_scorner = 0;
     int64_t schur_flops = 0;    // algorithmic flops of one Schur pass

@@ -161,53 +161,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
                  o_ucn = o_ub + fw * (size_t)prob.n_img * kGramSeg,
                  n_gram = o_ucn + fw * (size_t)prob.n_img * kGramSeg;
     pl->gram.alloc(n_gram);
-    // page-locked staging (DMA uploads); released after the synchronisation
-    // at the end, like the observation arrays
-    HostVec<FlatTerm> ft(std::max<size_t>(h.terms.size(), 1));
-    {
-        for (const ReduceTarget& T : h.targets) {
-            const bool vec = T.cols == 1;
-            for (int32_t k = T.c_begin; k < T.c_end; ++k) {
-                const ReduceTerm& q = h.terms[k];
-                FlatTerm& f = ft[k];
-                f.sign = q.sign;
-                f.mode = kFlatRows;
-                switch (q.kind) {
-                    case kSrcTile: {
-                        // slot blocks occupy disjoint tile rows, so a block of two
-                        // slots is wholly below or wholly above the diagonal
-                        const int64_t base = (int64_t)q.index * kTileR * kTileR;
-                        if (vec || q.roff > q.coff) {
-                            f.off = base + q.roff * kTileR + q.coff;
-                            f.rs = vec ? 1 : kTileR;
-                        } else if (q.roff < q.coff) {
-                            f.off = base + q.coff * kTileR + q.roff;
-                            f.rs = 1;
-                            f.mode = kFlatTrans;
-                        } else {   // rs = the origin's offset within the tile
-                            f.off = base + q.roff * kTileR + q.coff;
-                            f.rs = (int16_t)(q.roff * kTileR + q.coff);
-                            f.mode = kFlatSym;
-                        }
-                        break;
-                    }
-                    case kSrcU:
-                        f.off = (int64_t)o_u + (int64_t)(q.index * fw * fw + q.roff * fw + q.coff);
-                        f.rs = (int16_t)fw;
-                        break;
-                    case kSrcUb:
-                        f.off = (int64_t)o_ub + (int64_t)(q.index * fw + q.roff);
-                        f.rs = 1;
-                        break;
-                    default:
-                        f.off = (int64_t)o_ucn + (int64_t)(q.index * fw + q.roff);
-                        f.rs = 1;
-                        break;
-                }
-            }
-        }
-        up(pl->terms, ft, s);
-    }
+    // the terms arrive resolved against this buffer (build_plan, same layout)
+    up(pl->terms, h.terms, s);
     // RCS: band + arrow + corner, or dense; the parts of a dense S no target
     // writes stay zero from here on
     pl->rcs_n = h.n_sband + h.n_sarrow + h.n_scorner + h.n_sdense + 3 * h.nF + 1;
@@ -366,6 +321,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     h.obs_slot = HostVec<int32_t>();
     h.obs_uv = HostVec<double>();
     h.pterms = HostVec<PTerm>();
+    h.terms = HostVec<FlatTerm>();
     tm.mark("sync");
 }
 
