@@ -73,11 +73,11 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0, vis=0):
+def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0, vis=0, n_intr=1):
     lib = abi.load()
     cfg = abi.SynthBAConfig()
     cfg.camera_model = model
-    cfg.n_cam, cfg.k, cfg.vis_mode, cfg.n_intr = n_cam, k, vis, 1
+    cfg.n_cam, cfg.k, cfg.vis_mode, cfg.n_intr = n_cam, k, vis, n_intr
     cfg.n_pt, cfg.seed = n_pt, seed
     cfg.noise_px, cfg.outlier_frac = 0.5, 0.01
     cfg.perturb_rot, cfg.perturb_t, cfg.perturb_X, cfg.perturb_f = 0.01, 0.05, 0.05, 5.0
@@ -89,7 +89,7 @@ def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0, vis=0):
     sc = {
         "pt_offsets": np.zeros(n_pt + 1, np.int64), "obs_img": np.zeros(no, np.int32),
         "obs_uv": np.zeros(2 * no), "img_intr": np.zeros(n_cam, np.int32),
-        "extr": np.zeros(6 * n_cam), "intr": np.zeros(lib.sfm_ba_intr_width(model)), "X": np.zeros(3 * n_pt),
+        "extr": np.zeros(6 * n_cam), "intr": np.zeros(lib.sfm_ba_intr_width(model) * n_intr), "X": np.zeros(3 * n_pt),
     }
     p = abi.ptr
     rc = lib.sfm_synth_ba(C.byref(cfg), p(sc["pt_offsets"], abi.i64p), p(sc["obs_img"], abi.i32p),
@@ -98,7 +98,7 @@ def c4_scene(n_cam=1000, n_pt=500_000, k=10, seed=0x5F3D0004, model=0, vis=0):
                           None, None, None, C.byref(n_obs))
     assert rc == 0
     pr = abi.BAProblem()
-    pr.n_img, pr.n_intr, pr.n_pt, pr.n_obs = n_cam, 1, n_pt, no
+    pr.n_img, pr.n_intr, pr.n_pt, pr.n_obs = n_cam, n_intr, n_pt, no
     pr.pt_offsets = p(sc["pt_offsets"], abi.i64p)
     pr.obs_img = p(sc["obs_img"], abi.i32p)
     pr.obs_uv = p(sc["obs_uv"], abi.f64p)
@@ -431,6 +431,42 @@ def synth_fpairs(n_pairs, n_match, outlier_frac=0.3, seed=0xF3, w=1920, h=1080, 
         u2[out] = np.stack([rng.uniform(0, w, out.sum()), rng.uniform(0, h, out.sum())], 1)
         xs.append(np.concatenate([u1, u2], 1))
     return xs, [(w, h, w, h)] * n_pairs
+
+
+def bench_radial3_percam(ctx, n_cam=200, n_pt=50_000, k=10, steps=2):
+    """reconstruction()'s one intrinsics group per camera
+    (sparseBuilder.cpp:1292-1299) under OpenMVG's PINHOLE_CAMERA_RADIAL3: the
+    arrow is as wide as the band (6 n_cam intrinsics columns), so the RCS is
+    dense, and a point's 2 x 6k F rows exceed a chunk tile, so every point
+    takes the general path.  C2-sized (the per-camera arrow multiplies the
+    RCS by 2 and the product terms by ~4 against pinhole)."""
+    t0 = time.time()
+    sc = c4_scene(n_cam, n_pt, k=k, seed=0x5F3D0024, vis=0, model=abi.SFM_CAM_RADIAL3, n_intr=n_cam)
+    plan = api.BAPlan(ctx, sc["problem"], sc["extr"], sc["intr"], sc["X"])
+    t_plan = time.time() - t0
+    info = plan.info()
+    plan.run()   # warm-up
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    iters = 0
+    for _ in range(steps):
+        rc, summ = plan.run()
+        iters += summ.iterations
+    ctx.synchronize()
+    dt = time.perf_counter() - t1
+    plan.close()
+    shape = api.ba_describe(sc["problem"])
+    out = {"metric": "BA LM-iters/sec, RADIAL3 with one intrinsics block per camera", "value": iters / dt,
+           "unit": "LM-iters/s", "ms_per_iteration": dt / max(iters, 1) * 1e3,
+           "lm_iterations_per_solve": summ.iterations, "rmse_initial": summ.rmse_initial,
+           "rmse_final": summ.rmse_final, "rcs_dim": info.rcs_dim, "dense": bool(shape.dense),
+           "general_points": shape.n_general_pts, "product_terms": shape.n_pterms, "host_plan_seconds": t_plan,
+           "config": {"workload": f"{n_cam} cams / {n_pt} pts / {sc['n_obs']} obs, banded k={k}, "
+                                  "Pinhole_Intrinsic_Radial_K3 per camera (reconstruction()'s grouping), HuberLoss(4)"}}
+    log(f"BA radial3 per-camera: {iters} LM iterations in {dt:.3f}s -> {iters / dt:.1f} it/s, rcs {info.rcs_dim}, "
+        f"dense {bool(shape.dense)}, {shape.n_general_pts} general points, plan {t_plan:.1f}s, "
+        f"rmse {summ.rmse_initial:.4f}->{summ.rmse_final:.4f}")
+    return out
 
 
 def bench_dense_s(ctx, n_cam=1000, n_pt=500_000, k=10, steps=2, model=0):
@@ -872,9 +908,10 @@ def main():
     dense_s = None
     if world == 1 and rank == 0 and not args.no_dense and args.fake_world <= 1:
         dense_s = bench_dense_s(ctx)
-    radial3 = None
+    radial3 = radial3_percam = None
     if world == 1 and rank == 0 and not args.no_radial3 and args.fake_world <= 1:
         radial3 = bench_dense_s(ctx, model=abi.SFM_CAM_RADIAL3)
+        radial3_percam = bench_radial3_percam(ctx)
 
     # ---------------- geometric filter ----------------
     filt = None
@@ -967,6 +1004,7 @@ def main():
             "filter": filt,
             "ba_dense_s": dense_s,
             "ba_radial3": radial3,
+            "ba_radial3_percam": radial3_percam,
         }
         print(json.dumps(out))
     plan.close()
