@@ -563,6 +563,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         int gw = schur_group(cap == 64 ? 4 : 5);
         if (const char* e = std::getenv("SFM_BA_TILE_GROUP")) gw = std::max(1, std::min(gw, std::atoi(e)));   // diagnostic
         group_pts = gw * chunk_pts;
+        slot_out.reserve(pl.n_sobs);        // (grown to every observation once kept, in place)
         slot_out.resize(pl.pt_off[ncp]);   // every entry written by its range
         const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(16, ncp / 4096));
         std::vector<std::vector<ChunkDesc>> seg_chunks(nseg);

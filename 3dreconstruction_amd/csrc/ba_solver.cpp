@@ -96,6 +96,33 @@ void up(DBuf<T>& d, const V& h, hipStream_t s) {
     d.upload(h.data(), h.size(), s);
 }
 
+// Page-locked staging for the plan's pageable host vectors: each is copied
+// into it and uploaded from there, so every upload is an asynchronous DMA
+// (a hipMemcpyAsync from pageable memory stages synchronously, per call).
+// Blocks stay put until the staging is destroyed, after the stream's sync.
+struct Staging {
+    std::vector<HostVec<char>> blocks;
+    size_t used = 0;
+    template <class T>
+    const T* put(const T* p, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (blocks.empty() || used + bytes > blocks.back().size()) {
+            blocks.emplace_back();
+            blocks.back().resize(std::max<size_t>(bytes, (size_t)1 << 20));
+            used = 0;
+        }
+        char* d = blocks.back().data() + used;
+        std::memcpy(d, p, bytes);
+        used += (bytes + 255) & ~(size_t)255;
+        return reinterpret_cast<const T*>(d);
+    }
+};
+template <class T, class A>
+void up(Staging& st, DBuf<T>& d, const std::vector<T, A>& h, hipStream_t s) {
+    d.alloc(std::max<size_t>(h.size(), 1));
+    if (!h.empty()) d.upload(st.put(h.data(), h.size()), h.size(), s);
+}
+
 void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr, const double* intr,
                  const double* X) {
     sfm_ctx* ctx = pl->ctx;
@@ -111,31 +138,32 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     build_plan(prob, ctx->rank, ctx->world, h);
     h.on_shard_ready = nullptr;
     tm.mark("build_plan");
-    up(pl->chunks, h.chunks, s);
-    up(pl->group_off, h.group_off, s);
-    up(pl->img_obs_ptr, h.img_obs_ptr, s);
+    Staging st;
+    up(st, pl->chunks, h.chunks, s);
+    up(st, pl->group_off, h.group_off, s);
+    up(st, pl->img_obs_ptr, h.img_obs_ptr, s);
     pl->img_pt.alloc(std::max<int64_t>(h.n_sobs, 1));
     pl->img_uv.alloc(2 * std::max<int64_t>(h.n_sobs, 1));
     ba_image_order(pl->obs_img.p, pl->obs_uv.p, pl->pt_off.p, (int32_t)h.n_sobs, (int32_t)h.n_spt, prob.n_img,
                    pl->img_pt.p, pl->img_uv.p, s);
-    up(pl->img_colc, h.img_colc, s);
-    up(pl->img_coli, h.img_coli, s);
+    up(st, pl->img_colc, h.img_colc, s);
+    up(st, pl->img_coli, h.img_coli, s);
     {
         std::vector<int32_t> ic(std::max(prob.n_intr, 1), -1);
         for (int q = 0; q < prob.n_intr; ++q)
             if (h.intr_blk[q] >= 0) ic[q] = (int32_t)(h.nb + (int64_t)h.iw * h.intr_blk[q]);
-        up(pl->intr_col, ic, s);
+        up(st, pl->intr_col, ic, s);
     }
-    up(pl->img_intr, h.img_intr, s);
-    up(pl->blk_img, h.blk_img, s);
-    up(pl->blk_intr, h.blk_intr, s);
-    up(pl->targets, h.targets, s);
-    up(pl->gblk_off, h.gblk_off, s);
-    up(pl->gblk_col, h.gblk_col, s);
-    up(pl->gblk_z, h.gblk_z, s);
-    up(pl->gz_off, h.gz_off, s);
-    up(pl->zbatch, h.zbatch, s);
-    up(pl->zlong, h.zlong, s);
+    up(st, pl->img_intr, h.img_intr, s);
+    up(st, pl->blk_img, h.blk_img, s);
+    up(st, pl->blk_intr, h.blk_intr, s);
+    up(st, pl->targets, h.targets, s);
+    up(st, pl->gblk_off, h.gblk_off, s);
+    up(st, pl->gblk_col, h.gblk_col, s);
+    up(st, pl->gblk_z, h.gblk_z, s);
+    up(st, pl->gz_off, h.gz_off, s);
+    up(st, pl->zbatch, h.zbatch, s);
+    up(st, pl->zlong, h.zlong, s);
     up(pl->pterms, h.pterms, s);
     pl->Zbuf.alloc(std::max<int64_t>(h.n_z, 1));
     HostVec<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
@@ -145,8 +173,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->Xa.alloc(xs.size());
     pl->Xb.alloc(xs.size());
     std::vector<double> e(extr, extr + 6 * (size_t)prob.n_img), in(intr, intr + (size_t)h.iw * prob.n_intr);
-    up(pl->extr0, e, s);
-    up(pl->intr0, in, s);
+    up(st, pl->extr0, e, s);
+    up(st, pl->intr0, in, s);
     pl->ea.alloc(e.size()); pl->eb.alloc(e.size());
     pl->ia.alloc(in.size()); pl->ib.alloc(in.size());
     pl->cpa.alloc(prob.n_img); pl->cpb.alloc(prob.n_img);
@@ -230,7 +258,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         std::vector<int32_t> all(lt);
         all.insert(all.end(), off.begin(), off.end());
         all.insert(all.end(), seg.begin(), seg.end());
-        up(pl->long_targets, all, s);
+        up(st, pl->long_targets, all, s);
         P.long_targets = pl->long_targets.p;
         P.lseg_off = P.long_targets + P.n_long;
         P.lseg = P.lseg_off + P.n_long + 1;
@@ -255,7 +283,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         std::vector<int32_t> all(lt);
         all.insert(all.end(), off.begin(), off.end());
         all.insert(all.end(), seg.begin(), seg.end());
-        up(pl->plong_targets, all, s);
+        up(st, pl->plong_targets, all, s);
         P.plong_targets = pl->plong_targets.p;
         P.plseg_off = P.plong_targets + P.n_plong;
         P.plseg = P.plseg_off + P.n_plong + 1;
