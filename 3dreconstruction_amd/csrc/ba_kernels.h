@@ -31,6 +31,8 @@ struct DevProblem {
     int32_t tile_nt;    // 16-row MFMA tiles per chunk side: 4 (64 F rows) or 5 (76 + w row)
     int32_t cam_model;  // SFM_CAM_* residual model
     int32_t iw;         // doubles per intrinsics block (4; RADIAL3 6)
+    int32_t chunk_pts_max;   // longest Schur chunk (points)
+    int32_t gram_seg;   // image Gram workgroups per image (1..kGramSeg; U / Ub / Ucn / part_u stride)
     int64_t nb, nF;
     double huber_a, min_diag, max_diag;
     // shard data

@@ -307,7 +307,7 @@ __device__ __forceinline__ double wave_max(double v) {
 
 // ---------------------------------------------------------------------------
 // per-image Gram blocks: U = J_F' J_F (10x10), b = J_F' f, cost
-// kGramSeg workgroups per image, one observation per lane per step.  Each lane
+// P.gram_seg (<= kGramSeg) workgroups per image, one observation per lane per step.  Each lane
 // keeps its own running sums of the 62 structurally nonzero entries of
 // [J_c | J_i | f]' [J_c | J_i | f] (J_i row 0 = [x s, 0, s, 0], row 1 =
 // [0, y s, 0, s]) plus the cost on the VALU -- 90 FMAs per observation, no
@@ -420,9 +420,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
     using kT = gram::SlotTable<CM>;
     constexpr int IW = kIW<CM>, FW = gram::FW<CM>, S0 = 64 * PASS;
     constexpr bool kHasCost = kT::kCost >= S0 && kT::kCost < S0 + 64;
-    const int img = blockIdx.x / kGramSeg, seg = blockIdx.x - kGramSeg * img;   // slice of the image
+    const int ns = P.gram_seg, img = blockIdx.x / ns, seg = blockIdx.x - ns * img;   // slice of the image
     const int a0 = P.img_obs_ptr[img], n = P.img_obs_ptr[img + 1] - a0;
-    const int o0 = a0 + (int)((int64_t)n * seg / kGramSeg), o1 = a0 + (int)((int64_t)n * (seg + 1) / kGramSeg);
+    const int o0 = a0 + (int)((int64_t)n * seg / ns), o1 = a0 + (int)((int64_t)n * (seg + 1) / ns);
     const int colc = P.img_colc[img], coli = P.img_coli[img];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __shared__ CamPre scp;
@@ -548,7 +548,7 @@ template <int CM>
 __global__ __launch_bounds__(128) void gram_rescale_kernel(DevProblem P) {
     using kT = gram::SlotTable<CM>;
     constexpr int FW = gram::FW<CM>;
-    const int b = blockIdx.x, img = b / kGramSeg;
+    const int b = blockIdx.x, img = b / P.gram_seg;
     const int colc = P.img_colc[img], coli = P.img_coli[img];
     __shared__ double ssc[FW];
     if (threadIdx.x < FW) {
@@ -1571,9 +1571,15 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
 
 // ---------------------------------------------------------------------------
 // per-point back substitution, model cost change, candidate cost
-// One workgroup per Schur chunk, one thread per point.  The chunk's current
-// and candidate cameras, intrinsics, column scales and y_F are staged in LDS
-// once, so the per-observation work gathers only the measurement.
+// One workgroup per Schur chunk, SPLIT threads per point (adjacent lanes, each
+// taking every SPLIT-th observation; their sums are combined with xor
+// shuffles, identical in every lane of the group), at most kStepThreads
+// threads.  A landmark shard at N = 8 has short chunks (~30 points, so that
+// the Schur pass keeps dividing by N): one thread per point would leave three
+// quarters of a 128-thread workgroup idle and each lane a chain of 20
+// linearisations.  The chunk's current and candidate cameras, intrinsics, column scales
+// and y_F are staged in LDS once, so the per-observation work gathers only the
+// measurement.
 // ---------------------------------------------------------------------------
 #ifndef SFM_STEP_PREFETCH   // A/B knob: the next observation's (slot, uv) loaded one ahead
 #define SFM_STEP_PREFETCH 1
@@ -1583,8 +1589,9 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
 #else
 #define SFM_STEP_ATTR
 #endif
-template <int CM>
-__global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
+constexpr int kStepThreads = 256;
+template <int CM, int SPLIT>
+__global__ __launch_bounds__(kStepThreads) SFM_STEP_ATTR void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const CamPre* __restrict__ cps_c,
                                                          const double* __restrict__ intr_c,
@@ -1617,7 +1624,7 @@ __global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProble
         }
     }
     __syncthreads();
-    const int p = cd.pt_begin + tid;
+    const int p = cd.pt_begin + tid / SPLIT, sub = tid % SPLIT;
     double acc[3] = {0.0, 0.0, 0.0};  // model acc, candidate cost, step norm^2
     double bad = 0.0, cbad = 0.0;     // non-finite step / non-finite candidate residual
     if (p < cd.pt_end) {
@@ -1630,19 +1637,19 @@ __global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProble
         //   -(sum q f + y_E . bf) + (sum q^2 + 2 y_E . bq + y_E' V y_E) / 2.
         double V[6] = {0, 0, 0, 0, 0, 0}, bf[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
         double sqf = 0.0, sqq = 0.0;
-        const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+        const int o0 = P.pt_off[p] + sub, o1 = P.pt_off[p + 1];
         // the next observation's (slot, uv) is loaded while this one is linearised
 #if SFM_STEP_PREFETCH
         int nslot = o0 < o1 ? P.obs_slot[o0] : 0;
         double2 nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
 #endif
-        for (int o = o0; o < o1; ++o) {
+        for (int o = o0; o < o1; o += SPLIT) {
 #if SFM_STEP_PREFETCH
             const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = nuv;
-            if (o + 1 < o1) {
-                nslot = P.obs_slot[o + 1];
-                nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
+            if (o + SPLIT < o1) {
+                nslot = P.obs_slot[o + SPLIT];
+                nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + SPLIT];
             }
 #else
             const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
@@ -1671,6 +1678,21 @@ __global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProble
                 sqq += q * q;
             }
         }
+        if constexpr (SPLIT > 1) {
+            // the group's partial sums (xor butterfly: the same value in every lane)
+#pragma unroll
+            for (int m = 1; m < SPLIT; m <<= 1) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) V[k] += __shfl_xor(V[k], m);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    bf[k] += __shfl_xor(bf[k], m);
+                    bq[k] += __shfl_xor(bq[k], m);
+                }
+                sqf += __shfl_xor(sqf, m);
+                sqq += __shfl_xor(sqq, m);
+            }
+        }
         const double V0[6] = {V[0], V[1], V[2], V[3], V[4], V[5]};
         const double b[3] = {bf[0] - bq[0], bf[1] - bq[1], bf[2] - bq[2]};
         const int di[3] = {0, 2, 5};
@@ -1691,7 +1713,7 @@ __global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProble
             xc[a] = Xp[a] + (-yE[a]) * sE[a];
             const double d = Xp[a] - xc[a];
             acc[2] += d * d;
-            Xc[3 * (size_t)p + a] = xc[a];
+            if (sub == 0) Xc[3 * (size_t)p + a] = xc[a];
             if (!isfinite(xc[a])) bad = 1.0;
         }
         {
@@ -1703,18 +1725,19 @@ __global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProble
             const double yVy = yE[0] * Vy0 + yE[1] * Vy1 + yE[2] * Vy2;
             acc[0] = -(sqf + ybf) + 0.5 * (sqq + 2.0 * ybq + yVy);
         }
+        if (sub != 0) acc[0] = acc[2] = 0.0;   // one lane of the group carries the point's terms
         // candidate residuals at (x_c, candidate cameras / intrinsics)
 #if SFM_STEP_PREFETCH
         nslot = o0 < o1 ? P.obs_slot[o0] : 0;
         nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
 #endif
-        for (int o = o0; o < o1; ++o) {
+        for (int o = o0; o < o1; o += SPLIT) {
 #if SFM_STEP_PREFETCH
             const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = nuv;
-            if (o + 1 < o1) {
-                nslot = P.obs_slot[o + 1];
-                nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + 1];
+            if (o + SPLIT < o1) {
+                nslot = P.obs_slot[o + SPLIT];
+                nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + SPLIT];
             }
 #else
             const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
@@ -1730,7 +1753,7 @@ __global__ __launch_bounds__(kChunkPts) SFM_STEP_ATTR void step_kernel(DevProble
     wave_sum(acc);
     bad = wave_max(bad);
     cbad = wave_max(cbad);
-    __shared__ double red[kChunkPts / 64][kPartT];
+    __shared__ double red[kStepThreads / 64][kPartT];
     const int wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
     if (lane == 0) {
         red[wave][0] = acc[0]; red[wave][1] = acc[1]; red[wave][2] = acc[2];
@@ -2385,7 +2408,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
     // the four lists in one loop, so every list's loads are in flight together
     // (four separate loops were four serial memory latencies); each list is
     // still summed by this thread in index order, as before
-    const int nf = P.n_fblk, nu = P.n_img * kGramSeg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
+    const int nf = P.n_fblk, nu = P.n_img * P.gram_seg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
     const int nmax = max(max(nf, nu), max(ns, nt));
 #pragma unroll 2
     for (int i = threadIdx.x; i < nmax; i += kFinThreads) {
@@ -2504,16 +2527,16 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                    hipStream_t s) {
     SFM_BY_MODEL_ALL(P, {
-        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp, intr, X);
+        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
         if constexpr (gram::SlotTable<CM>::kPasses > 1)
-            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_img * kGramSeg), dim3(256), 0, s, P, cp, intr, X);
+            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
     });
     SFM_HIP(hipGetLastError());
 }
 
 void ba_gram_rescale(const DevProblem& P, hipStream_t s) {
     if (P.n_img <= 0) return;
-    SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_img * kGramSeg), dim3(128), 0, s, P));
+    SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_img * P.gram_seg), dim3(128), 0, s, P));
     SFM_HIP(hipGetLastError());
 }
 
@@ -2640,13 +2663,38 @@ void ba_cand(const DevProblem& P, const double* extr, const double* intr, double
     SFM_HIP(hipGetLastError());
 }
 
+// threads per point in step_kernel: two (SFM_STEP_SPLIT overrides, A/B only).
+// profiles/r04/l_split: C4 1062-1067 / 1076-1078 LM-iters/s with 1 / 2, rank 0
+// of N = 8 2145-2148 / 2191-2198 / 2175-2177 / 2128 with 1 / 2 / 4 / 8 (the
+// step kernel 95 -> 85.5 us at C4: adjacent lanes read adjacent observations)
+static int step_split(const DevProblem& P) {
+    static const int forced = [] {
+        const char* e = std::getenv("SFM_STEP_SPLIT");
+        return e ? std::atoi(e) : 0;
+    }();
+    int sp = 2;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8) sp = forced;
+    while (sp > 1 && P.chunk_pts_max * sp > kStepThreads) sp /= 2;
+    return sp;
+}
+
 int ba_step_blocks(const DevProblem& P) { return P.n_chunk + (P.n_gpt + kGStepThreads - 1) / kGStepThreads; }
 
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
     if (P.n_chunk > 0) {
-        SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(step_kernel<CM>, dim3(P.n_chunk), dim3(kChunkPts), 0, s, P, cp, intr,
-                                           cp_cand, intr_cand, X, X_cand, radius));
+        const int split = step_split(P);
+        const int threads = std::min(kStepThreads, (P.chunk_pts_max * split + 63) / 64 * 64);
+        SFM_REQUIRE(P.chunk_pts_max * split <= threads, SFM_ERR_UNSUPPORTED, "step kernel: chunk exceeds the workgroup");
+        auto go = [&](auto tag) {
+            constexpr int SP = decltype(tag)::value;
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((step_kernel<CM, SP>), dim3(P.n_chunk), dim3(threads), 0, s, P,
+                                                   cp, intr, cp_cand, intr_cand, X, X_cand, radius));
+        };
+        if (split == 8) go(std::integral_constant<int, 8>{});
+        else if (split == 4) go(std::integral_constant<int, 4>{});
+        else if (split == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 1>{});
         SFM_HIP(hipGetLastError());
     }
     if (P.n_gpt > 0) {

@@ -817,6 +817,11 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 if (!cnt[t].empty()) tot += cnt[t][i];
             pl.img_obs_ptr[i + 1] = pl.img_obs_ptr[i] + tot;
         }
+        // image Gram workgroups per image (SFM_GRAM_SEG, A/B only): one per
+        // image at a C4 shard of N = 8 (~625 observations each) measured
+        // slower than three (33.0 vs 30.5 us, profiles/r04/k_shard)
+        if (const char* e = std::getenv("SFM_GRAM_SEG"))
+            pl.gram_seg = std::min(kGramSeg, std::max(1, std::atoi(e)));
     }
     tm.mark("image_csr");
     // ---- reduce plan -----------------------------------------------------------
@@ -940,17 +945,18 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     enum { kMc, kMp, kVc, kVp, kVb, kNC };
     std::vector<int64_t> rc((size_t)kNC * (nFB + 1), 0);
     auto RC = [&](int w, int32_t f) -> int64_t& { return rc[(size_t)w * (nFB + 1) + f]; };
+    const int32_t gseg = pl.gram_seg;
     for (const ImgSrc& s : isrc) {
         if (s.cb >= 0) {
-            RC(kMc, s.cb) += kGramSeg;
-            if (s.fq >= 0) RC(kMc, s.fq) += kGramSeg;
-            RC(kVc, s.cb) += kGramSeg;
-            RC(kVb, s.cb) += kGramSeg;
+            RC(kMc, s.cb) += gseg;
+            if (s.fq >= 0) RC(kMc, s.fq) += gseg;
+            RC(kVc, s.cb) += gseg;
+            RC(kVb, s.cb) += gseg;
         }
         if (s.fq >= 0) {
-            RC(kMc, s.fq) += kGramSeg;
-            RC(kVc, s.fq) += kGramSeg;
-            RC(kVb, s.fq) += kGramSeg;
+            RC(kMc, s.fq) += gseg;
+            RC(kVc, s.fq) += gseg;
+            RC(kVb, s.fq) += gseg;
         }
     }
     {
@@ -1093,10 +1099,10 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             auto in = [&](int32_t f) { return f >= r0 && f < r1; };
             // (1) counts
             for (const ImgSrc& s : isrc) {
-                if (s.cb >= 0 && in(s.cb)) cs[S(s.cb, s.cb)] += kGramSeg;
+                if (s.cb >= 0 && in(s.cb)) cs[S(s.cb, s.cb)] += gseg;
                 if (s.fq >= 0 && in(s.fq)) {
-                    if (s.cb >= 0) cs[S(s.fq, s.cb)] += kGramSeg;
-                    cs[S(s.fq, s.fq)] += kGramSeg;
+                    if (s.cb >= 0) cs[S(s.fq, s.cb)] += gseg;
+                    cs[S(s.fq, s.fq)] += gseg;
                 }
             }
             for (int32_t c = 0; c < ngrp; ++c) {
@@ -1178,8 +1184,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 T[v[3]++] = flat(ReduceTerm{kSrcUcn, idx, ro, 0, 1.f}, true);
             };
             for (const ImgSrc& s : isrc)
-                for (int g = 0; g < kGramSeg; ++g) {
-                    const int32_t idx = s.img * kGramSeg + g;
+                for (int g = 0; g < gseg; ++g) {
+                    const int32_t idx = s.img * gseg + g;
                     if (s.cb >= 0 && in(s.cb)) {
                         put(S(s.cb, s.cb), false, ReduceTerm{kSrcU, idx, 0, 0, 1.f});
                         put_v(s.cb, 0, idx);

@@ -218,6 +218,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.n_img = prob.n_img; P.n_intr = prob.n_intr;
     P.n_spt = (int32_t)h.n_spt; P.n_sobs = (int32_t)h.n_sobs;
     P.n_chunk = (int32_t)h.chunks.size();
+    P.gram_seg = h.gram_seg;
+    P.chunk_pts_max = 0;
+    for (const ChunkDesc& c : h.chunks) P.chunk_pts_max = std::max(P.chunk_pts_max, c.pt_end - c.pt_begin);
     P.n_group = (int32_t)h.n_group();
     P.n_cpt = (int32_t)h.n_cpt; P.n_gpt = (int32_t)h.n_gpt;
     P.gz_max = (int32_t)h.gz_max;
@@ -454,7 +457,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     ba_fill(pl->scaleE.p, (int64_t)nx, 1.0, s);
     if (O.jacobi_scaling) {
         relinearize();                 // unscaled column norms of the F blocks
-        if (ctx->world > 1) SFM_HIP(hipMemsetAsync(pl->rcs.p, 0, (size_t)pl->rcs_n * sizeof(double), s));
+        if (ctx->world > 1) ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // one launch (a memset is two blits)
         ba_reduce(P, true, s);
         allreduce_rcs();
         ba_fscale(P, s);
@@ -506,7 +509,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(ev[1], s));
         // across ranks each shard writes only the blocks its own points touch,
         // so the summed system of the last iteration is cleared first
-        if (ctx->world > 1) SFM_HIP(hipMemsetAsync(pl->rcs.p, 0, (size_t)pl->rcs_n * sizeof(double), s));
+        if (ctx->world > 1) ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // one launch (a memset is two blits)
         ba_reduce(P, false, s);
         allreduce_rcs();
         if (P.dense) dense_solve(pl->dense, P, radius, s, ++pl->bcr_epoch);
