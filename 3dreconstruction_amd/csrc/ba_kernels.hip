@@ -1181,51 +1181,67 @@ __device__ __forceinline__ bool skip_kind(int kind, int vectors_only) {
     return vectors_only && kind != kDstBF && kind != kDstCnF;
 }
 
-__global__ void reduce_kernel(DevProblem P, int vectors_only) {
-    const int wave = threadIdx.x >> 6;
-    const int t = blockIdx.x * 4 + wave;
-    const int e = threadIdx.x & 63;
+// P.red_waves (1, 2 or 4) waves per target: wave w of a target sums its
+// lane groups' terms w, w + W, ... (in units of G), and the partials are added
+// in (wave, group) order -- fixed, so deterministic.  More waves per target
+// shorten the chain of dependent term loads where targets collect many terms
+// (a landmark shard at N = 8 has ~30-point chunks, so ~170 tile terms per
+// band block against ~80 at N = 1).
+__global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_only) {
+    const int W = P.red_waves, wave = threadIdx.x >> 6, e = threadIdx.x & 63;
+    const int t = blockIdx.x * (4 / W) + wave / W, ws = wave - (wave / W) * W;
     __shared__ double part[4][64];
-    if (t >= P.n_targets) return;
-    const ReduceTarget T = P.targets[t];
-    if (skip_kind(T.dst_kind, vectors_only) || T.c_end - T.c_begin > kLongTerms) return;
+    bool live = t < P.n_targets;
+    ReduceTarget T{};
+    if (live) {
+        T = P.targets[t];
+        live = !skip_kind(T.dst_kind, vectors_only) && T.c_end - T.c_begin <= kLongTerms;
+    }
     // G = 64 / E lane groups of the target's E elements: group g sums terms
-    // g, g + G, ... (a 6-vector target keeps 60 lanes busy instead of 6), the
-    // group partials are then added in group order (fixed, so deterministic)
-    const int E = T.rows * T.cols, G = 64 / E, g = e / E, el = e - g * E;
-    if (g >= G) return;
-    const int r = el / T.cols, cc = el % T.cols;
-    const bool vec = T.cols == 1;
+    // g, g + G, ... (a 6-vector target keeps 60 lanes busy instead of 6)
+    const int E = live ? T.rows * T.cols : 64, G = 64 / E, g = e / E, el = e - g * E;
+    const int r = live ? el / T.cols : 0, cc = live ? el % T.cols : 0;
     // batches of 16 (then 4) independent loads; a target is a chain of
     // dependent global round trips (term descriptor, then data), so the batch
     // width sets its latency
     double s = 0.0;
-    int k = T.c_begin + g;
-    for (; k + 15 * G < T.c_end; k += 16 * G) {
-        double v[16];
+    if (live && g < G) {
+        const int GW = G * W;
+        int k = T.c_begin + ws * G + g;
+        for (; k + 15 * GW < T.c_end; k += 16 * GW) {
+            double v[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = term_value(P, P.terms[k + j * G], r, cc);
+            for (int j = 0; j < 16; ++j) v[j] = term_value(P, P.terms[k + j * GW], r, cc);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) s += v[j];
+            for (int j = 0; j < 16; ++j) s += v[j];
+        }
+        for (; k + 3 * GW < T.c_end; k += 4 * GW) {
+            double v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = term_value(P, P.terms[k + j * GW], r, cc);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s += v[j];
+        }
+        for (; k < T.c_end; k += GW) s += term_value(P, P.terms[k], r, cc);
     }
-    for (; k + 3 * G < T.c_end; k += 4 * G) {
-        double v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = term_value(P, P.terms[k + j * G], r, cc);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s += v[j];
-    }
-    for (; k < T.c_end; k += G) s += term_value(P, P.terms[k], r, cc);
-    if (G > 1) {
+    if (W > 1) {   // (uniform over the launch: every wave reaches the barrier)
+        part[wave][e] = s;
+        __syncthreads();
+        if (!live || ws != 0 || g != 0) return;
+        s = 0.0;
+        for (int w = 0; w < W; ++w)
+            for (int q = 0; q < G; ++q) s += part[wave + w][q * E + el];
+    } else if (G > 1) {
         part[wave][e] = s;
         wsync();
-        if (g != 0) return;
+        if (!live || g != 0) return;
         s = 0.0;
         for (int q = 0; q < G; ++q) s += part[wave][q * E + el];
+    } else if (!live || g != 0) {   // (G = 1: lanes past the E elements)
+        return;
     }
-    double* dst;
-    dst = target_base(P, T.dst_kind);
-    dst[T.dst + (vec ? r : r * T.ld + cc)] = s;
+    const bool vec = T.cols == 1;
+    target_base(P, T.dst_kind)[T.dst + (vec ? r : r * T.ld + cc)] = s;
 }
 
 // Long targets, pass 1: one workgroup per kReduceSeg-term segment, one term
@@ -2605,7 +2621,9 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
 
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     if (P.n_targets <= 0) return;
-    hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + 3) / 4), dim3(256), 0, s, P, vectors_only ? 1 : 0);
+    const int per_block = 4 / P.red_waves;
+    hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + per_block - 1) / per_block), dim3(256), 0, s, P,
+                       vectors_only ? 1 : 0);
     SFM_HIP(hipGetLastError());
     if (P.n_long > 0) {
         hipLaunchKernelGGL(reduce_seg_kernel, dim3(P.n_lseg), dim3(256), 0, s, P, vectors_only ? 1 : 0);

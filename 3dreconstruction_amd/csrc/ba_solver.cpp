@@ -244,6 +244,24 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.intr_col = pl->intr_col.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
     {
+        // reduce_kernel waves per target from the mean term count of the
+        // targets it sums: C4 24 at N = 1, 50 at N = 4, 92 at N = 8
+        // (profiles/r04/m_redw: N = 1 1072 / 1063 / 1046 LM-iters/s with 1 / 2
+        // / 4 waves, rank 0 of N = 8 2123-2132 / 2215-2226 / 2244-2245;
+        // SFM_REDUCE_WAVES overrides, A/B only)
+        int64_t nt = 0, nterm = 0;
+        for (const ReduceTarget& T : h.targets) {
+            const int32_t n = T.c_end - T.c_begin;
+            if (n <= reduce_long_threshold()) { ++nt; nterm += n; }
+        }
+        const int64_t mean = nt > 0 ? nterm / nt : 0;
+        P.red_waves = mean >= 80 ? 4 : mean >= 40 ? 2 : 1;
+        if (const char* e = std::getenv("SFM_REDUCE_WAVES")) {
+            const int w = std::atoi(e);
+            if (w == 1 || w == 2 || w == 4) P.red_waves = w;
+        }
+    }
+    {
         // long targets: [n_long targets | n_long+1 segment offsets | n_seg (long idx, term begin)]
         std::vector<int32_t> lt, off{0}, seg;
         for (size_t t = 0; t < h.targets.size(); ++t) {
