@@ -43,10 +43,20 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 #ifndef MATCH_CT
 #define MATCH_CT 4                 // 32-query column tiles per wave (even; 4: 200 VGPRs, 2 waves/SIMD)
 #endif
+#ifndef MATCH_PP
+// Ping-pong (A/B knob): 8 waves per workgroup, waves w and w + 4 share a SIMD
+// and run half a tile apart -- one group issues its MFMAs while the other
+// runs its top-2 epilogue, swapped at every workgroup barrier, so the
+// matrix core and the VALU of a SIMD work at the same time instead of both
+// co-resident waves alternating in phase.
+#define MATCH_PP 0
+#endif
+constexpr int kWaves = MATCH_PP ? 8 : 4;   // waves per workgroup
+constexpr int kThreads = 64 * kWaves;
 constexpr int kCT = MATCH_CT;
 static_assert(kCT % 2 == 0 && kCT >= 2, "MATCH_CT must be even: the epilogue walks column tiles in pairs");
 constexpr int kQW = 32 * kCT;      // queries per wave
-constexpr int kQB = 4 * kQW;       // queries per workgroup (4 waves)
+constexpr int kQB = kWaves * kQW;  // queries per workgroup
 constexpr int kRowPad = kQB > 256 ? kQB : 256;  // rows of every image padded to this multiple
 #ifndef MATCH_STAGE
 #define MATCH_STAGE 128            // database rows per LDS stage (A/B knob)
@@ -161,7 +171,7 @@ struct MatchArgs {
 // kRatio = false (MUTUAL's two nearest-neighbour passes): only the nearest
 // key is tracked (min3 over two keys, 1.5 VALU per distance).
 template <bool kRatio>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES_PER_EU, MATCH_WAVES_PER_EU))) void match_top2_kernel(MatchArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES_PER_EU, MATCH_WAVES_PER_EU))) void match_top2_kernel(MatchArgs a) {
     // XCD-aware bijective remap of the flat workgroup id (guide §5 T1):
     // blocks b and b+8 share an XCD, so give each XCD a contiguous range of
     // work items (pair-major, query block minor).
@@ -211,11 +221,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
 #endif
     auto issue_to = [&](int8_t* dA, int32_t* dN, int row_base) {
 #pragma unroll
-        for (int q = 0; q < kStage * 8 / 256; ++q) {
-            const int L = q * 256 + wave * 64 + lane;          // 16-byte slot in the stage
+        for (int q = 0; q < kStage * 8 / kThreads; ++q) {
+            const int L = q * kThreads + wave * 64 + lane;     // 16-byte slot in the stage
             const int r = L >> 3, k = (L & 7) ^ (r & 7);
             const int8_t* src = a.desc + (db_row0 + row_base + r) * 128 + k * 16;
-            __builtin_amdgcn_global_load_lds(src, dA + (q * 256 + wave * 64) * 16, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src, dA + (q * kThreads + wave * 64) * 16, 16, 0, 0);
         }
         if (wave == 0) {
 #pragma unroll
@@ -232,7 +242,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     auto issue = [&](int buf, int row_base) { issue_to(sA[buf], sN[buf], row_base); };
 #endif
 
-    const int n_db_pad = (n_db + kRowPad - 1) / kRowPad * kRowPad;
+    // (256-row merge windows; the image rows are padded to kRowPad >= 256)
+    const int n_db_pad = (n_db + 255) / 256 * 256;
     int b1[kCT], b2[kCT];
 #pragma unroll
     for (int t = 0; t < kCT; ++t) b1[t] = b2[t] = INT_MAX;
@@ -357,6 +368,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES
     }
     if (pendB) epilogue(accB, ntB);
     if (merge_base >= 0) merge_window(merge_base);
+#elif MATCH_PP
+    // Phases separated by workgroup barriers; per tile, phase a: group 0
+    // (waves 0-3) loads and issues the tile's MFMAs while group 1 (waves 4-7)
+    // runs the epilogue of its previous tile; phase b: the reverse.  Every
+    // wave reaches every barrier (the branches are wave-uniform and hold no
+    // barrier).  A stage's first phase waits for its LDS DMA (each wave drains
+    // its own part, then the barrier) and issues the next stage into the
+    // other buffer, which group 1 finished reading in the previous phase.
+    // waves w and w + 4 share a SIMD (HW_ID probe, profiles/r04/n_pp/simd_probe.txt)
+    const bool g1 = wave >= 4;
+    v4i af[4], nt4[4];
+    v16i acc[kCT];
+    bool pend = false;      // group 1: a tile's epilogue is pending
+    int pend_merge = -1;    // group 1: a window merge pending after it
+    auto g1_epilogue = [&] {
+        if (!pend) return;
+        epilogue(acc, nt4);
+        pend = false;
+        if (pend_merge >= 0) { merge_window(pend_merge); pend_merge = -1; }
+    };
+    auto stage = [&](const int8_t* A, const int32_t* N, int8_t* nA, int32_t* nN, int sup) {
+        stage_landed();
+        if (sup + kStage < n_db_pad) issue_to(nA, nN, sup + kStage);
+        // (the phase barriers inside a stage order no memory -- the stage has
+        // landed -- so they are bare s_barrier: __syncthreads' fence would
+        // drain the next stage's DMA at each of them)
+        for (int tile = 0; tile < kStage; tile += 32) {
+            if (tile) __builtin_amdgcn_s_barrier();
+            if (g1) {
+                g1_epilogue();
+            } else {
+                load_frag(A, N, tile, af, nt4);
+                mfma_tile(af, acc);
+            }
+            __builtin_amdgcn_s_barrier();
+            if (g1) {
+                load_frag(A, N, tile, af, nt4);
+                mfma_tile(af, acc);
+                pend = true;
+            } else {
+                epilogue(acc, nt4);
+            }
+        }
+        if (((sup + kStage) & 255) == 0) {
+            if (g1) pend_merge = sup + kStage - 256;
+            else merge_window(sup + kStage - 256);
+        }
+    };
+    for (int sup = 0; sup < n_db_pad; sup += 2 * kStage) {
+        stage(sA0, sN0, sA1, sN1, sup);
+        if (sup + kStage < n_db_pad) stage(sA1, sN1, sA0, sN0, sup + kStage);
+    }
+    if (g1) g1_epilogue();
 #elif MATCH_SPLIT
     // one stage: its tiles from (A, N) while the next stage lands in (nA, nN)
     auto stage = [&](const int8_t* A, const int32_t* N, int8_t* nA, int32_t* nN, int sup) {
@@ -778,9 +842,9 @@ void run_top2(sfm_match_plan* p, const int32_t* pairs_d, int64_t n_pairs, int sw
         a.out_idx = out_idx + b0 * stride;
         a.out_d = out_d + b0 * stride;
         if (ratio_test)
-            hipLaunchKernelGGL(match_top2_kernel<true>, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(match_top2_kernel<true>, dim3((unsigned)(nb * qblocks)), dim3(kThreads), 0, s, a);
         else
-            hipLaunchKernelGGL(match_top2_kernel<false>, dim3((unsigned)(nb * qblocks)), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(match_top2_kernel<false>, dim3((unsigned)(nb * qblocks)), dim3(kThreads), 0, s, a);
         SFM_HIP(hipGetLastError());
         ++p->launches;
     }
