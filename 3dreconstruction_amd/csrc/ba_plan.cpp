@@ -406,10 +406,15 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // 128 points per chunk: ~2x the co-resident waves of the chip at C4 size,
     // so the last round of chunks is short (256 measured 17% slower).
     // A shard too small to give every wave slot of the chip a 128-point chunk
-    // (a landmark shard at N = 4, 8) gets shorter chunks instead, down to 16
+    // (a landmark shard at N = 2, 4, 8) gets shorter chunks instead, down to 16
     // points: the Schur pass takes about one chunk's latency once the chunks
-    // fit in one round, so 2048 chunks (8 waves per CU) keep it dividing by N.
-    constexpr int64_t kTargetChunks = 2048;
+    // fit in one round of the chip's 2048 wave slots (256 CUs x 2 waves per
+    // SIMD x 4), and a chunk count just past a round costs a second one.  So
+    // the target is 1600 chunks, a margin for the camera-window cuts
+    // (profiles/r04/o_n8knobs/pts.txt, rank 0 of a C4 shard: N = 8 2147-2180
+    // LM-iters/s at 31 points (2107 chunks), 2272-2282 at 40; N = 4 1838-1870
+    // at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128).
+    constexpr int64_t kTargetChunks = 1600;
     int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
     if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));   // tuning override
     // Chunks of one tile group share one slot layout and one tile: the Schur
