@@ -2681,27 +2681,12 @@ void ba_cand(const DevProblem& P, const double* extr, const double* intr, double
     SFM_HIP(hipGetLastError());
 }
 
-// threads per point in step_kernel: two (SFM_STEP_SPLIT overrides, A/B only).
-// profiles/r04/l_split: C4 1062-1067 / 1076-1078 LM-iters/s with 1 / 2, rank 0
-// of N = 8 2145-2148 / 2191-2198 / 2175-2177 / 2128 with 1 / 2 / 4 / 8 (the
-// step kernel 95 -> 85.5 us at C4: adjacent lanes read adjacent observations)
-static int step_split(const DevProblem& P) {
-    static const int forced = [] {
-        const char* e = std::getenv("SFM_STEP_SPLIT");
-        return e ? std::atoi(e) : 0;
-    }();
-    int sp = 2;
-    if (forced == 1 || forced == 2 || forced == 4 || forced == 8) sp = forced;
-    while (sp > 1 && P.chunk_pts_max * sp > kStepThreads) sp /= 2;
-    return sp;
-}
-
 int ba_step_blocks(const DevProblem& P) { return P.n_chunk + (P.n_gpt + kGStepThreads - 1) / kGStepThreads; }
 
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
     if (P.n_chunk > 0) {
-        const int split = step_split(P);
+        const int split = P.step_split;
         const int threads = std::min(kStepThreads, (P.chunk_pts_max * split + 63) / 64 * 64);
         SFM_REQUIRE(P.chunk_pts_max * split <= threads, SFM_ERR_UNSUPPORTED, "step kernel: chunk exceeds the workgroup");
         auto go = [&](auto tag) {

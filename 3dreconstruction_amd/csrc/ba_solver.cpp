@@ -221,6 +221,20 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.gram_seg = h.gram_seg;
     P.chunk_pts_max = 0;
     for (const ChunkDesc& c : h.chunks) P.chunk_pts_max = std::max(P.chunk_pts_max, c.pt_end - c.pt_begin);
+    {
+        // step_kernel lanes per point: two (profiles/r04/l_split: C4 1062-1067
+        // / 1076-1078 LM-iters/s with 1 / 2, rank 0 of N = 8 2145-2148 / 2191-
+        // 2198 / 2175-2177 / 2128 with 1 / 2 / 4 / 8; adjacent lanes read
+        // adjacent observations).  SFM_STEP_SPLIT overrides (A/B, tests); the
+        // longest chunk must fit the kernel's 256 threads
+        int sp = 2;
+        if (const char* e = std::getenv("SFM_STEP_SPLIT")) {
+            const int f = std::atoi(e);
+            if (f == 1 || f == 2 || f == 4 || f == 8) sp = f;
+        }
+        while (sp > 1 && P.chunk_pts_max * sp > 256) sp /= 2;
+        P.step_split = sp;
+    }
     P.n_group = (int32_t)h.n_group();
     P.n_cpt = (int32_t)h.n_cpt; P.n_gpt = (int32_t)h.n_gpt;
     P.gz_max = (int32_t)h.gz_max;

@@ -537,3 +537,30 @@ def test_plan_cache_reuse_general_points_bit_identical(ctx, shape):
     assert reused[1].iterations == os_.iterations
     assert abs(reused[1].rmse_final / os_.rmse_final - 1) < RTOL_COST
     lib.sfm_ba_cache_clear(ctx.h)
+
+
+@pytest.mark.parametrize("vis_mode", [0, 1])
+def test_step_split_and_reduce_waves_agree(ctx, monkeypatch, vis_mode):
+    # Round 4's launch shapes: step_kernel with 1 / 2 / 4 / 8 lanes per point
+    # (SFM_STEP_SPLIT) and reduce_kernel with 1 / 2 / 4 waves per target
+    # (SFM_REDUCE_WAVES) change only the order of the sums, so every shape
+    # takes the oracle's accept / reject sequence and agrees with the others
+    # to rounding (the plan, which carries both, is rebuilt for each).
+    lib = abi.load()
+    sc = H.Scene(60, 12000, 8, vis_mode=vis_mode, seed=4242 + vis_mode)
+    _, os_, otr, _ = H.oracle_solve(sc, threads=8)
+    base = None
+    for split, waves in [(1, 1), (2, 1), (4, 2), (8, 4), (2, 4)]:
+        monkeypatch.setenv("SFM_STEP_SPLIT", str(split))
+        monkeypatch.setenv("SFM_REDUCE_WAVES", str(waves))
+        lib.sfm_ba_cache_clear(ctx.h)
+        e, i, x = sc.params()
+        rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
+        assert rc == 0, api.abi.load().sfm_last_error()
+        assert (gs.iterations, gs.successful_steps) == (os_.iterations, os_.successful_steps), (split, waves)
+        assert abs(gs.final_cost / os_.final_cost - 1) < RTOL_COST
+        if base is None:
+            base = gs
+        else:
+            assert abs(gs.final_cost / base.final_cost - 1) < 1e-10, (split, waves)
+    lib.sfm_ba_cache_clear(ctx.h)
