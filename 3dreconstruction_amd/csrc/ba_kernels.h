@@ -61,6 +61,7 @@ struct DevProblem {
     const int32_t* lseg_off;        // [n_long+1] segment ranges per long target
     const int32_t* lseg;            // [n_lseg][2] (long index, first term)
     double* lpart;                  // [n_lseg][36] segment partial sums
+    unsigned* lcount;               // [n_long] segments done this launch (the last one combines; reset by it)
     // general points (ba_plan.h): blocks, Z layout, product terms
     const int32_t* gblk_off;        // [n_gpt+1]
     const int32_t* gblk_col;        // F column of each block

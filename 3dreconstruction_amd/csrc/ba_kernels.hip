@@ -288,6 +288,18 @@ __device__ __forceinline__ void linearize(const CamPre& cp, const double* in, co
     }
 }
 
+// Global-address-space agent-scope accesses for values handed between
+// workgroups of one launch (sc1: written through / read past this CU's L1;
+// cdna_hip_programming.md Guideline 16, counter form)
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+typedef __attribute__((address_space(1))) double gf64_t;
+__device__ __forceinline__ void st_wt64(double* p, double v) {
+    __hip_atomic_store((gf64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt64(const double* p) {
+    return __hip_atomic_load((gf64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------
 // block reduction helpers (256 threads, fixed order => deterministic)
 // ---------------------------------------------------------------------------
@@ -1187,7 +1199,18 @@ __device__ __forceinline__ bool skip_kind(int kind, int vectors_only) {
 // shorten the chain of dependent term loads where targets collect many terms
 // (a landmark shard at N = 8 has ~30-point chunks, so ~170 tile terms per
 // band block against ~80 at N = 1).
-__global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_only) {
+template <bool FUSED>
+__device__ void reduce_segment(const DevProblem& P, int vectors_only, int sg);
+
+// n_short_blocks: the short targets' workgroups; FUSED: every workgroup past
+// them is one segment of a long target (reduce_segment<true>), so the whole
+// reduce is one launch instead of three
+template <bool FUSED>
+__global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_only, int n_short_blocks) {
+    if (FUSED && (int)blockIdx.x >= n_short_blocks) {
+        reduce_segment<true>(P, vectors_only, blockIdx.x - n_short_blocks);
+        return;
+    }
     const int W = P.red_waves, wave = threadIdx.x >> 6, e = threadIdx.x & 63;
     const int t = blockIdx.x * (4 / W) + wave / W, ws = wave - (wave / W) * W;
     __shared__ double part[4][64];
@@ -1247,8 +1270,11 @@ __global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_o
 // Long targets, pass 1: one workgroup per kReduceSeg-term segment, one term
 // per thread (every element of the block, <= 36, in registers); the 256
 // partial blocks are combined by xor-butterflies and wave order (fixed).
-__global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int vectors_only) {
-    const int sg = blockIdx.x;
+// (one workgroup: segment sg of its long target, partial into lpart[sg];
+// FUSED: stored write-through, and the target's last segment to finish adds
+// the partials in segment order -- the same sum as reduce_long_kernel)
+template <bool FUSED>
+__device__ __forceinline__ void reduce_segment(const DevProblem& P, int vectors_only, int sg) {
     const int j = P.lseg[2 * sg], k0 = P.lseg[2 * sg + 1];
     const ReduceTarget T = P.targets[P.long_targets[j]];
     if (skip_kind(T.dst_kind, vectors_only)) return;   // (uniform over the workgroup)
@@ -1273,6 +1299,7 @@ __global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int vecto
         for (; k < q1; k += G) s += term_value(P, P.terms[k], r, cc);
     }
     __shared__ double part[4][64];
+    __shared__ int last;
     part[wave][lane] = s;
     __syncthreads();
     if ((int)threadIdx.x < E) {
@@ -1280,8 +1307,34 @@ __global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int vecto
         double tot = 0.0;
         for (int w = 0; w < 4; ++w)
             for (int q = 0; q < G; ++q) tot += part[w][q * E + t];
-        P.lpart[(size_t)sg * 36 + t] = tot;
+        if (FUSED) st_wt64(P.lpart + (size_t)sg * 36 + t, tot);
+        else P.lpart[(size_t)sg * 36 + t] = tot;
     }
+    if (!FUSED) return;
+    // the partial is drained before the ticket; the last arriver reads every
+    // partial of the target write-through (no fences: the counter form)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int s0 = P.lseg_off[j], s1 = P.lseg_off[j + 1];
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add((gu32_t*)(P.lcount + j), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(s1 - s0 - 1);
+    __syncthreads();
+    if (!last) return;
+    if ((int)threadIdx.x < E) {
+        const int e = threadIdx.x;
+        double t = 0.0;
+#pragma unroll 8
+        for (int q = s0; q < s1; ++q) t += ld_wt64(P.lpart + (size_t)q * 36 + e);
+        const int r = e / T.cols, cc = e % T.cols;
+        target_base(P, T.dst_kind)[T.dst + (T.cols == 1 ? r : r * T.ld + cc)] = t;
+    }
+    if (threadIdx.x == 0)   // ready for the next launch (stream order)
+        __hip_atomic_store((gu32_t*)(P.lcount + j), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void reduce_seg_kernel(DevProblem P, int vectors_only) {
+    reduce_segment<false>(P, vectors_only, blockIdx.x);
 }
 
 // pass 2: segment partials added in segment order
@@ -2621,11 +2674,16 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
 
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     if (P.n_targets <= 0) return;
-    const int per_block = 4 / P.red_waves;
-    hipLaunchKernelGGL(reduce_kernel, dim3((P.n_targets + per_block - 1) / per_block), dim3(256), 0, s, P,
-                       vectors_only ? 1 : 0);
-    SFM_HIP(hipGetLastError());
-    if (P.n_long > 0) {
+    const int per_block = 4 / P.red_waves, nb = (P.n_targets + per_block - 1) / per_block;
+    const bool split = std::getenv("SFM_REDUCE_SPLIT") != nullptr;   // A/B and tests: three launches
+    if (P.n_long > 0 && !split) {
+        hipLaunchKernelGGL(reduce_kernel<true>, dim3(nb + P.n_lseg), dim3(256), 0, s, P, vectors_only ? 1 : 0, nb);
+        SFM_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(reduce_kernel<false>, dim3(nb), dim3(256), 0, s, P, vectors_only ? 1 : 0, nb);
+        SFM_HIP(hipGetLastError());
+    }
+    if (P.n_long > 0 && split) {
         hipLaunchKernelGGL(reduce_seg_kernel, dim3(P.n_lseg), dim3(256), 0, s, P, vectors_only ? 1 : 0);
         SFM_HIP(hipGetLastError());
         hipLaunchKernelGGL(reduce_long_kernel, dim3(P.n_long), dim3(64), 0, s, P, vectors_only ? 1 : 0);

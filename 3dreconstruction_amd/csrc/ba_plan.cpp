@@ -47,8 +47,15 @@ void parallel_segments(int nseg, F&& fn) {
 // block half-bandwidth of the points' camera spans under the order cam_blk;
 // *lb_out (optional): a bound no camera order can beat, the largest number of
 // distinct active cameras one point sees, minus one
-int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int32_t* lb_out = nullptr) {
+// (spans, optional: every point's [first, last + 1) active block, (ncam, 0)
+// without one -- partition_points' sort keys, computed in the same pass)
+int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int32_t* lb_out = nullptr,
+                       PointSpans* spans = nullptr, int32_t ncam = 0) {
     int32_t Dt[16] = {0}, Lt[16] = {0};
+    if (spans) {
+        spans->lo.resize(P.n_pt);
+        spans->hi.resize(P.n_pt);
+    }
     parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int t) {
         int32_t D = 0, L = 0;
         std::vector<int32_t> cs;
@@ -59,6 +66,10 @@ int32_t half_bandwidth(const sfm_ba_problem& P, const std::vector<int32_t>& cam_
                 if (b >= 0) { lo = std::min(lo, b); hi = std::max(hi, b); ++n; }
             }
             if (hi >= 0) D = std::max(D, hi - lo);
+            if (spans) {
+                spans->lo[p] = hi >= 0 ? lo : ncam;
+                spans->hi[p] = hi + 1;
+            }
             if (lb_out && n - 1 > L) {   // only a track longer than the bound so far is counted exactly
                 cs.clear();
                 for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o)
@@ -174,7 +185,8 @@ std::vector<int32_t> rcm_order(const sfm_ba_problem& P, const std::vector<int32_
 
 }  // namespace
 
-std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, int32_t* D_out) {
+std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, int32_t* D_out, PointSpans* spans,
+                                   std::vector<char>* used_out) {
     PhaseTimer tm("camera_blocks");
     std::vector<int32_t> cam_blk(P.n_img, -1);
     std::vector<char> used;
@@ -184,7 +196,7 @@ std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, i
         if (used[i] && i != P.const_img) cam_blk[i] = ncam++;
     tm.mark("used");
     int32_t lb = 0;
-    int32_t D = half_bandwidth(P, cam_blk, &lb);
+    int32_t D = half_bandwidth(P, cam_blk, &lb, spans, ncam);
     // reorder only when the image order does not give a band the BCR solver
     // takes, no order can (a point seeing more than kBandMaxD + 1 cameras
     // keeps the RCS dense under any order), and the co-visibility graph is
@@ -197,26 +209,32 @@ std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, i
         std::vector<int32_t> alt(cam_blk);
         for (auto& b : alt)
             if (b >= 0) b = pos[b];
-        const int32_t D2 = half_bandwidth(P, alt);
-        if (D2 < D) { cam_blk.swap(alt); D = D2; }
+        PointSpans alt_spans;
+        const int32_t D2 = half_bandwidth(P, alt, nullptr, spans ? &alt_spans : nullptr, ncam);
+        if (D2 < D) {
+            cam_blk.swap(alt);
+            D = D2;
+            if (spans) *spans = std::move(alt_spans);
+        }
         tm.mark("bandwidth2");
     }
     if (ncam_out) *ncam_out = ncam;
     if (D_out) *D_out = D;
+    if (used_out) used_out->swap(used);
     return cam_blk;
 }
 
 namespace {
 
-void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
-    pl.cam_blk = camera_blocks(P, &pl.ncam, &pl.D);
+void active_sets(const sfm_ba_problem& P, BAHostPlan& pl, PointSpans* spans) {
+    std::vector<char> im;   // observed images
+    pl.cam_blk = camera_blocks(P, &pl.ncam, &pl.D, spans, &im);
     pl.blk_img.assign(pl.ncam, -1);
     for (int i = 0; i < P.n_img; ++i)
         if (pl.cam_blk[i] >= 0) pl.blk_img[pl.cam_blk[i]] = i;
     pl.intr_blk.assign(P.n_intr, -1);
     // intrinsics blocks of observed images
-    std::vector<char> iu(P.n_intr, 0), im;
-    mark_used(P.obs_img, P.n_obs, P.n_img, im);
+    std::vector<char> iu(P.n_intr, 0);
     for (int i = 0; i < P.n_img; ++i)
         if (im[i]) iu[P.img_intr[i]] = 1;
     for (int q = 0; q < P.n_intr; ++q)
@@ -239,33 +257,68 @@ void active_sets(const sfm_ba_problem& P, BAHostPlan& pl) {
 }  // namespace
 
 void partition_points(const sfm_ba_problem& P, const std::vector<int32_t>& cam_blk, int world,
-                      std::vector<int64_t>& order, std::vector<int64_t>& bounds) {
+                      std::vector<int64_t>& order, std::vector<int64_t>& bounds, const PointSpans* spans) {
     // stable order by (first, last) active camera block: two stable counting
     // passes (last, then first) over ncam + 1 buckets (no active camera sorts
     // last), the order std::stable_sort on the pair gives
     int32_t ncam = 0;
     for (int32_t b : cam_blk) ncam = std::max(ncam, b + 1);
-    std::vector<int32_t> lo(P.n_pt), hi(P.n_pt);
-    parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int) {
-        for (int64_t p = p0; p < p1; ++p) {
-            int l = ncam, h = 0;
-            for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
-                const int b = cam_blk[P.obs_img[o]];
-                if (b >= 0) { l = std::min(l, b); h = std::max(h, b + 1); }
+    PointSpans own;
+    if (!spans) {   // (camera_blocks' pass gives them to build_plan)
+        own.lo.resize(P.n_pt);
+        own.hi.resize(P.n_pt);
+        parallel_ranges(P.n_pt, [&](int64_t p0, int64_t p1, int) {
+            for (int64_t p = p0; p < p1; ++p) {
+                int l = ncam, h = 0;
+                for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+                    const int b = cam_blk[P.obs_img[o]];
+                    if (b >= 0) { l = std::min(l, b); h = std::max(h, b + 1); }
+                }
+                own.lo[p] = l;
+                own.hi[p] = h;
             }
-            lo[p] = l;
-            hi[p] = h;
-        }
-    });
-    std::vector<int64_t> tmp(P.n_pt), cnt(ncam + 2);
+        });
+        spans = &own;
+    }
+    const std::vector<int32_t>& lo = spans->lo;
+    const std::vector<int32_t>& hi = spans->hi;
+    // each pass a stable counting sort over host ranges: per-range bucket
+    // counts, offsets in (bucket, range) order, every range scattering its
+    // own items in order -- the serial pass's output
+    constexpr int kMaxR = 16;
+    const int64_t nr = P.n_pt < 16384 ? 1 : std::min<int64_t>(kMaxR, std::min<int64_t>(PlanPool::width(), P.n_pt / 8192));
+    std::vector<int64_t> tmp(P.n_pt), cnt((size_t)nr * (ncam + 2));
     auto pass = [&](const std::vector<int32_t>& key, const int64_t* in, int64_t* out) {
+        auto range = [&](int r, int64_t& k0, int64_t& k1) { k0 = P.n_pt * r / nr; k1 = P.n_pt * (r + 1) / nr; };
         std::fill(cnt.begin(), cnt.end(), 0);
-        for (int64_t k = 0; k < P.n_pt; ++k) cnt[key[in ? in[k] : k] + 1]++;
-        for (int32_t b = 0; b <= ncam; ++b) cnt[b + 1] += cnt[b];
-        for (int64_t k = 0; k < P.n_pt; ++k) {
-            const int64_t p = in ? in[k] : k;
-            out[cnt[key[p]]++] = p;
-        }
+        auto count = [&](int r) {
+            int64_t k0, k1;
+            range(r, k0, k1);
+            int64_t* c = &cnt[(size_t)r * (ncam + 2)];
+            for (int64_t k = k0; k < k1; ++k) c[key[in ? in[k] : k] + 1]++;
+        };
+        auto scatter = [&](int r) {
+            int64_t k0, k1;
+            range(r, k0, k1);
+            int64_t* c = &cnt[(size_t)r * (ncam + 2)];
+            for (int64_t k = k0; k < k1; ++k) {
+                const int64_t p = in ? in[k] : k;
+                out[c[key[p]]++] = p;
+            }
+        };
+        if (nr > 1) PlanPool::get().run((int)nr, count);
+        else count(0);
+        // c[r][b] (after the scan) = first slot of bucket b's items from range r
+        int64_t acc = 0;
+        for (int32_t b = 0; b <= ncam; ++b)
+            for (int r = 0; r < nr; ++r) {
+                int64_t& c = cnt[(size_t)r * (ncam + 2) + b + 1];
+                const int64_t n = c;
+                cnt[(size_t)r * (ncam + 2) + b] = acc;   // slot b holds the start (b + 1 held the count)
+                acc += n;
+            }
+        if (nr > 1) PlanPool::get().run((int)nr, scatter);
+        else scatter(0);
     };
     order.resize(P.n_pt);
     pass(hi, nullptr, tmp.data());
@@ -344,7 +397,8 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     tm.mark("validate");
     pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
     pl.rank = rank; pl.world = world;
-    active_sets(P, pl);
+    PointSpans spans;   // every point's active camera span: the partition's sort keys
+    active_sets(P, pl, &spans);
     tm.mark("active");
     // RCS storage and solver, identical on every rank: the block-banded form
     // (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
@@ -359,7 +413,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         pl.n_sdense = pl.nF * pl.nF;
     }
 
-    partition_points(P, pl.cam_blk, world, pl.order, pl.bounds);
+    partition_points(P, pl.cam_blk, world, pl.order, pl.bounds, &spans);
     tm.mark("partition");
 
     // ---- shard arrays: chunkable points first, then general points ---------

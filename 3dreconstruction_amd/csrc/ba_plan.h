@@ -85,14 +85,23 @@ struct BAHostPlan {
 // Validates the problem and fills every field.  Throws SfmError.
 void build_plan(const sfm_ba_problem& prob, int rank, int world, BAHostPlan& plan);
 
-// Landmark-block partition (sfm_ba_partition).
+// Every point's active camera span [lo, hi) under a camera order ((ncam, 0):
+// no active camera): the partition's sort keys.
+struct PointSpans {
+    std::vector<int32_t> lo, hi;
+};
+
+// Landmark-block partition (sfm_ba_partition); spans: precomputed keys (optional).
 void partition_points(const sfm_ba_problem& prob, const std::vector<int32_t>& cam_blk, int world,
-                      std::vector<int64_t>& order, std::vector<int64_t>& bounds);
+                      std::vector<int64_t>& order, std::vector<int64_t>& bounds, const PointSpans* spans = nullptr);
 
 // Image -> active camera block (-1: constant or unobserved) in the RCS order:
 // image order, or reverse Cuthill-McKee over the camera co-visibility graph
 // when that gives a narrower band.  *D_out = the block half-bandwidth.
-std::vector<int32_t> camera_blocks(const sfm_ba_problem& prob, int32_t* ncam_out, int32_t* D_out);
+// spans / used_out (optional): every point's span under the returned order,
+// and the observed-image flags, from the same passes.
+std::vector<int32_t> camera_blocks(const sfm_ba_problem& prob, int32_t* ncam_out, int32_t* D_out,
+                                   PointSpans* spans = nullptr, std::vector<char>* used_out = nullptr);
 
 // Largest camera half-bandwidth the block-cyclic-reduction solver takes.
 constexpr int kBandMaxD = 10;

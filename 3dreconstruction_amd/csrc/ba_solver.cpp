@@ -59,6 +59,7 @@ struct sfm_ba_plan {
     DBuf<double> Zbuf, dense_buf;
     DenseArgs dense;
     DBuf<double> lpart;           // long-target segment partials [n_lseg][36]
+    DBuf<unsigned> lcount;        // per long target: segment tickets of the fused reduce
     DBuf<int32_t> plong_targets;  // long product-term targets, offsets, segments
     DBuf<double> plpart;          // their segment partials [n_plseg][36]
     DBuf<int32_t> img_pt;         // image-ordered observations (image Gram pass)
@@ -299,6 +300,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         P.lseg = P.lseg_off + P.n_long + 1;
         pl->lpart.alloc(36 * std::max<size_t>(P.n_lseg, 1));
         P.lpart = pl->lpart.p;
+        pl->lcount.alloc(std::max<size_t>(P.n_long, 1));
+        pl->lcount.zero(s);
+        P.lcount = pl->lcount.p;
     }
     {
         // the same for long product-term lists (general points)

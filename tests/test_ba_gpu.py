@@ -564,3 +564,30 @@ def test_step_split_and_reduce_waves_agree(ctx, monkeypatch, vis_mode):
         else:
             assert abs(gs.final_cost / base.final_cost - 1) < 1e-10, (split, waves)
     lib.sfm_ba_cache_clear(ctx.h)
+
+
+def test_fused_long_target_reduce_bit_identical(ctx, monkeypatch):
+    # The long reduce targets (the intrinsics corner and arrow collect one tile
+    # term per chunk) are summed by segment workgroups inside the reduce
+    # launch, the last segment to finish adding the partials in segment order
+    # (write-through partials, an agent-scope ticket).  That is the same
+    # arithmetic as the three-launch form (segments, then a combine launch;
+    # SFM_REDUCE_SPLIT), so the solves agree bit for bit.
+    lib = abi.load()
+    sc = H.Scene(200, 50000, 10, seed=909)
+    out = []
+    for split in (True, False):
+        if split:
+            monkeypatch.setenv("SFM_REDUCE_SPLIT", "1")
+        else:
+            monkeypatch.delenv("SFM_REDUCE_SPLIT", raising=False)
+        lib.sfm_ba_cache_clear(ctx.h)
+        e, i, x = sc.params()
+        rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
+        assert rc == 0, api.abi.load().sfm_last_error()
+        out.append((gs.iterations, gs.initial_cost, gs.final_cost, e, i, x))
+    a, b = out
+    assert a[:3] == b[:3]
+    for u, v in zip(a[3:], b[3:]):
+        np.testing.assert_array_equal(u, v)
+    lib.sfm_ba_cache_clear(ctx.h)
