@@ -910,8 +910,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
 // ---- top: super-block 0 alone; y_0 = X' X R_0 ----------------------------------
 // sp > 0: first block 0's update from its right neighbour sp, eliminated by
 // the last level (A_0 -= Wl_sp' Wl_sp, R_0 -= Wl_sp' z_sp; lower tiles only).
-__global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+__device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* sm) {
     const int ldr = b.nrhs + 1;
     double* A = sm;
     double* X = A + M * LD;
@@ -999,6 +998,11 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
     }
 }
 
+__global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    bcr_top_body(b, sp, sm);
+}
+
 // ---- bordered arrow, corner first ---------------------------------------------
 // The forward levels (and the top) leave every block's z_i = X_i R_i, all
 // columns: the rhs and the arrow's.  With B = L L' the band's CR
@@ -1012,8 +1016,11 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
 // and stores its rows 1..na, columns 0..na; the last workgroup to finish (an
 // agent-scope counter, reset by bcr_pack) adds the partials in block order
 // and solves the corner.
-__global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
-    const int I = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// (z_fresh: this workgroup wrote z_I itself just before -- the top, in the
+// fused launch -- so wave 0 reads it write-through, past this CU's L1)
+__device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProblem& P, double radius, int I,
+                                                bool z_fresh) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int na = P.iw * P.nintr, iw = P.iw;   // bordered columns (<= 16)
     constexpr int kQ = 17;                      // part row stride: columns 0..16
     __shared__ double Mc[16 * 16 + 16];
@@ -1023,11 +1030,20 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
         const int i = lane & 15, kk = lane >> 4, ntc = b.nrhs / 16;
         const double* Z = b.Z + (size_t)I * M * b.nrhs;
         double z0[16], z1[16];   // z[4 ks + kk][i], z[4 ks + kk][16 + i]: every load issued first
+        if (z_fresh) {
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) z0[ks] = Z[(4 * ks + kk) * b.nrhs + i];
-        if (ntc > 1) {
+            for (int ks = 0; ks < 16; ++ks) z0[ks] = ld_sc1(Z + (4 * ks + kk) * b.nrhs + i);
+            if (ntc > 1) {
 #pragma unroll
-            for (int ks = 0; ks < 16; ++ks) z1[ks] = Z[(4 * ks + kk) * b.nrhs + 16 + i];
+                for (int ks = 0; ks < 16; ++ks) z1[ks] = ld_sc1(Z + (4 * ks + kk) * b.nrhs + 16 + i);
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) z0[ks] = Z[(4 * ks + kk) * b.nrhs + i];
+            if (ntc > 1) {
+#pragma unroll
+                for (int ks = 0; ks < 16; ++ks) z1[ks] = Z[(4 * ks + kk) * b.nrhs + 16 + i];
+            }
         }
         v4d q00 = zero4(), q10 = zero4(), q11 = zero4();
 #pragma unroll
@@ -1075,7 +1091,7 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
         return t;
     };
     const int el = threadIdx.x >> 3, g = threadIdx.x & 7;   // 32 elements x 8 lanes per pass
-    for (int base = 0; base < na * na + na; base += NT / 8) {
+    for (int base = 0; base < na * na + na && (int)threadIdx.x < NT; base += NT / 8) {
         const int k = base + el;
         if (k < na * na) {
             const int a = k / na, c = k % na;   // lower triangle (a >= c), mirrored
@@ -1124,6 +1140,24 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
         }
         if (!ok) b.fail[0] = 1.0;
     }
+}
+
+__global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P, double radius) {
+    bcr_corner_body(b, P, radius, blockIdx.x, false);
+}
+
+// top + corner in one launch: workgroup 0 solves the top system (z_0, X_0)
+// and then adds its corner partial; the other workgroups add theirs at once
+// (their z_i are final since the levels); the last to arrive, normally the
+// top's, solves the corner.  No workgroup waits for another.
+__global__ __launch_bounds__(NTL) void bcr_top_corner_kernel(BcrArgs b, DevProblem P, double radius, int sp) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (blockIdx.x == 0) {
+        bcr_top_body(b, sp, sm);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // z_0 written (read back write-through)
+        __syncthreads();
+    }
+    bcr_corner_body(b, P, radius, blockIdx.x, blockIdx.x == 0);
 }
 
 // ---- back substitution, one column --------------------------------------------
@@ -1334,12 +1368,25 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
-    hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NTL), lds_t, s, b, s_top / 2);
-    SFM_HIP(hipGetLastError());
-    // corner first (one column left for the back substitution), then every
-    // back-substitution level in one top-down dataflow launch
-    hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
-    SFM_HIP(hipGetLastError());
+    // the top, then the corner (one column left for the back substitution) --
+    // one launch unless SFM_BCR_TOP_SPLIT (A/B) -- then every back-substitution
+    // level in one top-down dataflow launch
+    if (!std::getenv("SFM_BCR_TOP_SPLIT")) {
+        static bool attr_tc = false;
+        if (!attr_tc) {
+            // (160 KB less the corner's static LDS)
+            SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_corner_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024));
+            attr_tc = true;
+        }
+        hipLaunchKernelGGL(bcr_top_corner_kernel, dim3(b.N), dim3(NTL), lds_t, s, b, P, radius, s_top / 2);
+        SFM_HIP(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(bcr_top_kernel, dim3(1), dim3(NTL), lds_t, s, b, s_top / 2);
+        SFM_HIP(hipGetLastError());
+        hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
+        SFM_HIP(hipGetLastError());
+    }
     int n_back = 1;
     for (int stride = s_top / 2; stride >= 1; stride /= 2) n_back += (b.N - stride + 2 * stride - 1) / (2 * stride);
     if (!std::getenv("SFM_BCR_BACK_LEVELS")) {

@@ -566,28 +566,32 @@ def test_step_split_and_reduce_waves_agree(ctx, monkeypatch, vis_mode):
     lib.sfm_ba_cache_clear(ctx.h)
 
 
-def test_fused_long_target_reduce_bit_identical(ctx, monkeypatch):
-    # The long reduce targets (the intrinsics corner and arrow collect one tile
-    # term per chunk) are summed by segment workgroups inside the reduce
-    # launch, the last segment to finish adding the partials in segment order
-    # (write-through partials, an agent-scope ticket).  That is the same
-    # arithmetic as the three-launch form (segments, then a combine launch;
-    # SFM_REDUCE_SPLIT), so the solves agree bit for bit.
+def test_fused_launches_bit_identical(ctx, monkeypatch):
+    # Launch fusions with unchanged arithmetic: (1) the long reduce targets
+    # (the intrinsics corner and arrow collect one tile term per chunk) are
+    # summed by segment workgroups inside the reduce launch, the last segment
+    # to finish adding the partials in segment order (write-through partials,
+    # an agent-scope ticket) -- SFM_REDUCE_SPLIT restores the three launches;
+    # (2) the BCR top and corner run in one launch, the corner partials of
+    # blocks 1.. beside the top's solve -- SFM_BCR_TOP_SPLIT restores two.
+    # Every combination solves bit for bit alike.
     lib = abi.load()
     sc = H.Scene(200, 50000, 10, seed=909)
     out = []
-    for split in (True, False):
-        if split:
-            monkeypatch.setenv("SFM_REDUCE_SPLIT", "1")
-        else:
-            monkeypatch.delenv("SFM_REDUCE_SPLIT", raising=False)
+    for red_split, top_split in ((True, True), (False, True), (False, False)):
+        for var, on in (("SFM_REDUCE_SPLIT", red_split), ("SFM_BCR_TOP_SPLIT", top_split)):
+            if on:
+                monkeypatch.setenv(var, "1")
+            else:
+                monkeypatch.delenv(var, raising=False)
         lib.sfm_ba_cache_clear(ctx.h)
         e, i, x = sc.params()
         rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
         assert rc == 0, api.abi.load().sfm_last_error()
         out.append((gs.iterations, gs.initial_cost, gs.final_cost, e, i, x))
-    a, b = out
-    assert a[:3] == b[:3]
-    for u, v in zip(a[3:], b[3:]):
-        np.testing.assert_array_equal(u, v)
+    a = out[0]
+    for b in out[1:]:
+        assert a[:3] == b[:3]
+        for u, v in zip(a[3:], b[3:]):
+            np.testing.assert_array_equal(u, v)
     lib.sfm_ba_cache_clear(ctx.h)
