@@ -2479,7 +2479,9 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
     // still summed by this thread in index order, as before
     const int nf = P.n_fblk, nu = P.n_img * P.gram_seg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
     const int nmax = max(max(nf, nu), max(ns, nt));
-#pragma unroll 2
+    // (unrolled by four: C4's 3976 chunks are four rounds of the 1024 threads,
+    // so every load is in flight before the first add)
+#pragma unroll 4
     for (int i = threadIdx.x; i < nmax; i += kFinThreads) {
         // loads from clamped indices (unconditional, so the compiler issues
         // them all before the first use), accumulated only where in range
