@@ -33,6 +33,7 @@ struct DevProblem {
     int32_t iw;         // doubles per intrinsics block (4; RADIAL3 6)
     int32_t chunk_pts_max;   // longest Schur chunk (points)
     int32_t step_split;  // lanes per point in step_kernel (1, 2, 4, 8)
+    int32_t n_zero;     // world > 1: targets[n_targets, n_targets + n_zero) are cleared, not summed
     int32_t red_waves;  // waves per target in reduce_kernel (1, 2, 4)
     int32_t gram_seg;   // image Gram workgroups per image (1..kGramSeg; U / Ub / Ucn / part_u stride)
     int64_t nb, nF;

@@ -1205,8 +1205,26 @@ __device__ void reduce_segment(const DevProblem& P, int vectors_only, int sg);
 // n_short_blocks: the short targets' workgroups; FUSED: every workgroup past
 // them is one segment of a long target (reduce_segment<true>), so the whole
 // reduce is one launch instead of three
+// zero_first: the first workgroup of the zero list (world > 1: the blocks
+// other shards write, cleared before the all-reduce; 16 per workgroup, every
+// kind, also in the vectors-only pass)
 template <bool FUSED>
-__global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_only, int n_short_blocks) {
+__global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_only, int n_short_blocks,
+                                                     int zero_first) {
+    if ((int)blockIdx.x >= zero_first) {
+        const int wave = threadIdx.x >> 6, e = threadIdx.x & 63;
+        for (int q = 0; q < 4; ++q) {
+            const int z = ((int)blockIdx.x - zero_first) * 16 + wave * 4 + q;
+            if (z >= P.n_zero) break;
+            const ReduceTarget T = P.targets[P.n_targets + z];
+            const int E = T.rows * T.cols;
+            if (e < E) {
+                const int r = e / T.cols, cc = e % T.cols;
+                target_base(P, T.dst_kind)[T.dst + (T.cols == 1 ? r : r * T.ld + cc)] = 0.0;
+            }
+        }
+        return;
+    }
     if (FUSED && (int)blockIdx.x >= n_short_blocks) {
         reduce_segment<true>(P, vectors_only, blockIdx.x - n_short_blocks);
         return;
@@ -2675,14 +2693,16 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
 }
 
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
-    if (P.n_targets <= 0) return;
+    if (P.n_targets <= 0 && P.n_zero <= 0) return;
     const int per_block = 4 / P.red_waves, nb = (P.n_targets + per_block - 1) / per_block;
     const bool split = std::getenv("SFM_REDUCE_SPLIT") != nullptr;   // A/B and tests: three launches
+    const int nz = (P.n_zero + 15) / 16;   // zero-list workgroups, last in the grid
     if (P.n_long > 0 && !split) {
-        hipLaunchKernelGGL(reduce_kernel<true>, dim3(nb + P.n_lseg), dim3(256), 0, s, P, vectors_only ? 1 : 0, nb);
+        hipLaunchKernelGGL(reduce_kernel<true>, dim3(nb + P.n_lseg + nz), dim3(256), 0, s, P, vectors_only ? 1 : 0,
+                           nb, nb + P.n_lseg);
         SFM_HIP(hipGetLastError());
     } else {
-        hipLaunchKernelGGL(reduce_kernel<false>, dim3(nb), dim3(256), 0, s, P, vectors_only ? 1 : 0, nb);
+        hipLaunchKernelGGL(reduce_kernel<false>, dim3(nb + nz), dim3(256), 0, s, P, vectors_only ? 1 : 0, nb, nb);
         SFM_HIP(hipGetLastError());
     }
     if (P.n_long > 0 && split) {

@@ -1317,14 +1317,18 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
             }
             pl.targets.push_back(t);
         }
+    pl.zero_targets.clear();
     if (world > 1) {
-        // a shard writes only the blocks its points touch (about 1/world of the
-        // band); the solver clears the reduced camera system before each
-        // reduce instead of gathering zeros into the rest
+        // a shard gathers terms only into the blocks its points touch (about
+        // 1/world of the band); the others, which other shards write, go to a
+        // zero list that the reduce launch clears beside the real targets.
+        // (Dense plans list only this shard's blocks, so the solver clears
+        // their whole system before each reduce instead.)
         size_t w = 0;
         for (size_t t = 0; t < pl.targets.size(); ++t) {
             const ReduceTarget& T = pl.targets[t];
             if (T.c_begin != T.c_end || T.p_begin != T.p_end) pl.targets[w++] = T;
+            else pl.zero_targets.push_back(T);
         }
         pl.targets.resize(w);
     }

@@ -72,6 +72,7 @@ struct BAHostPlan {
 
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;
+    std::vector<ReduceTarget> zero_targets;   // world > 1: blocks other shards write (zeroed by the reduce)
     HostVec<FlatTerm> terms;         // resolved against the solver's source buffer (default-initialised)
     HostVec<PTerm> pterms;           // uploaded as it is: page-locked staging
     int64_t n_sband = 0, n_sarrow = 0, n_scorner = 0;

@@ -158,7 +158,13 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(st, pl->img_intr, h.img_intr, s);
     up(st, pl->blk_img, h.blk_img, s);
     up(st, pl->blk_intr, h.blk_intr, s);
-    up(st, pl->targets, h.targets, s);
+    if (h.zero_targets.empty()) {
+        up(st, pl->targets, h.targets, s);
+    } else {   // the zero list after the real targets, one buffer
+        std::vector<ReduceTarget> all(h.targets);
+        all.insert(all.end(), h.zero_targets.begin(), h.zero_targets.end());
+        up(st, pl->targets, all, s);
+    }
     up(st, pl->gblk_off, h.gblk_off, s);
     up(st, pl->gblk_col, h.gblk_col, s);
     up(st, pl->gblk_z, h.gblk_z, s);
@@ -258,6 +264,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.intr_col = pl->intr_col.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
+    P.n_zero = (int32_t)h.zero_targets.size();
     {
         // reduce_kernel waves per target from the mean term count of the
         // targets it sums: C4 24 at N = 1, 50 at N = 4, 92 at N = 8
@@ -493,7 +500,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     ba_fill(pl->scaleE.p, (int64_t)nx, 1.0, s);
     if (O.jacobi_scaling) {
         relinearize();                 // unscaled column norms of the F blocks
-        if (ctx->world > 1) ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // one launch (a memset is two blits)
+        if (ctx->world > 1 && (h.dense || std::getenv("SFM_RCS_FILL")))
+            ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // dense: its targets are this shard's blocks only
         ba_reduce(P, true, s);
         allreduce_rcs();
         ba_fscale(P, s);
@@ -545,7 +553,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(ev[1], s));
         // across ranks each shard writes only the blocks its own points touch,
         // so the summed system of the last iteration is cleared first
-        if (ctx->world > 1) ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // one launch (a memset is two blits)
+        if (ctx->world > 1 && (h.dense || std::getenv("SFM_RCS_FILL")))
+            ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // dense: its targets are this shard's blocks only
         ba_reduce(P, false, s);
         allreduce_rcs();
         if (P.dense) dense_solve(pl->dense, P, radius, s, ++pl->bcr_epoch);
