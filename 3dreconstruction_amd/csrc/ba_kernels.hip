@@ -432,7 +432,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
     using kT = gram::SlotTable<CM>;
     constexpr int IW = kIW<CM>, FW = gram::FW<CM>, S0 = 64 * PASS;
     constexpr bool kHasCost = kT::kCost >= S0 && kT::kCost < S0 + 64;
-    const int ns = P.gram_seg, img = blockIdx.x / ns, seg = blockIdx.x - ns * img;   // slice of the image
+    // workgroup -> (image with observations, slice); outputs at b = img * ns + seg
+    const int ns = P.gram_seg, gi = blockIdx.x / ns, seg = blockIdx.x - ns * gi, img = P.gram_img[gi];
+    const int b = img * ns + seg;
     const int a0 = P.img_obs_ptr[img], n = P.img_obs_ptr[img + 1] - a0;
     const int o0 = a0 + (int)((int64_t)n * seg / ns), o1 = a0 + (int)((int64_t)n * (seg + 1) / ns);
     const int colc = P.img_colc[img], coli = P.img_coli[img];
@@ -538,17 +540,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         const int i = threadIdx.x / FW, j = threadIdx.x % FW, s = kT::kS.id[i][j];
         if (s >= 0 ? mine(s) : PASS == 0) {
             const double u = s >= 0 ? ssc[i] * ssc[j] * tot(s) : 0.0;
-            P.U[(size_t)blockIdx.x * (FW * FW) + threadIdx.x] = u;
-            if (i == j) P.Ucn[(size_t)blockIdx.x * FW + i] = u;
+            P.U[(size_t)b * (FW * FW) + threadIdx.x] = u;
+            if (i == j) P.Ucn[(size_t)b * FW + i] = u;
         }
     }
     if (threadIdx.x >= 160 && threadIdx.x < 160 + FW) {
         const int i = threadIdx.x - 160, s = kT::kS.id[FW][i];
-        if (mine(s)) P.Ub[(size_t)blockIdx.x * FW + i] = ssc[i] * tot(s);
+        if (mine(s)) P.Ub[(size_t)b * FW + i] = ssc[i] * tot(s);
     }
     if (kHasCost && threadIdx.x == 192) {
-        P.part_u[2 * (size_t)blockIdx.x] = tot(kT::kCost);
-        P.part_u[2 * (size_t)blockIdx.x + 1] = fmax(fmax(badw[0], badw[1]), fmax(badw[2], badw[3]));
+        P.part_u[2 * (size_t)b] = tot(kT::kCost);
+        P.part_u[2 * (size_t)b + 1] = fmax(fmax(badw[0], badw[1]), fmax(badw[2], badw[3]));
     }
 }
 
@@ -560,7 +562,8 @@ template <int CM>
 __global__ __launch_bounds__(128) void gram_rescale_kernel(DevProblem P) {
     using kT = gram::SlotTable<CM>;
     constexpr int FW = gram::FW<CM>;
-    const int b = blockIdx.x, img = b / P.gram_seg;
+    const int gi = blockIdx.x / P.gram_seg, img = P.gram_img[gi];
+    const int b = img * P.gram_seg + (blockIdx.x - gi * P.gram_seg);
     const int colc = P.img_colc[img], coli = P.img_coli[img];
     __shared__ double ssc[FW];
     if (threadIdx.x < FW) {
@@ -2615,17 +2618,18 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
 
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
                    hipStream_t s) {
+    if (P.n_gram_img <= 0) return;
     SFM_BY_MODEL_ALL(P, {
-        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
+        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_gram_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
         if constexpr (gram::SlotTable<CM>::kPasses > 1)
-            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
+            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_gram_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
     });
     SFM_HIP(hipGetLastError());
 }
 
 void ba_gram_rescale(const DevProblem& P, hipStream_t s) {
-    if (P.n_img <= 0) return;
-    SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_img * P.gram_seg), dim3(128), 0, s, P));
+    if (P.n_gram_img <= 0) return;
+    SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL(gram_rescale_kernel<CM>, dim3(P.n_gram_img * P.gram_seg), dim3(128), 0, s, P));
     SFM_HIP(hipGetLastError());
 }
 

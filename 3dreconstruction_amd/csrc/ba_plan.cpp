@@ -876,9 +876,18 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
                 if (!cnt[t].empty()) tot += cnt[t][i];
             pl.img_obs_ptr[i + 1] = pl.img_obs_ptr[i] + tot;
         }
-        // image Gram workgroups per image (SFM_GRAM_SEG, A/B only): one per
-        // image at a C4 shard of N = 8 (~625 observations each) measured
-        // slower than three (33.0 vs 30.5 us, profiles/r04/k_shard)
+        // image Gram workgroups per image from the shard's observations per
+        // image (profiles/r04/cc_gseg: C4 at N = 1, ~5000 each: 1086-1088 /
+        // 1080-1083 / 1047-1052 LM-iters/s with 3 / 4 / 6; rank 0 of N = 8,
+        // ~625 each: 2438-2444 / 2398-2401 / 2344-2347 with 2 / 3 / 4, and one
+        // measured slower than three, profiles/r04/k_shard); SFM_GRAM_SEG
+        // overrides (A/B only)
+        pl.gram_img.clear();
+        for (int i = 0; i < P.n_img; ++i)
+            if (pl.img_obs_ptr[i + 1] != pl.img_obs_ptr[i]) pl.gram_img.push_back(i);
+        const int64_t seen = (int64_t)pl.gram_img.size();
+        const int64_t avg = seen > 0 ? pl.n_sobs / seen : 0;
+        pl.gram_seg = std::min<int32_t>(kGramSeg, avg >= 1600 ? 3 : avg >= 128 ? 2 : 1);
         if (const char* e = std::getenv("SFM_GRAM_SEG"))
             pl.gram_seg = std::min(kGramSeg, std::max(1, std::atoi(e)));
     }

@@ -38,7 +38,8 @@ struct BAHostPlan {
     // eliminated rows Z go to a buffer and reach the RCS as product terms.
     int64_t n_spt = 0, n_sobs = 0;
     int64_t n_cpt = 0, n_gpt = 0;
-    int32_t gram_seg = kGramSeg;     // image Gram workgroups per image (1..kGramSeg)
+    int32_t gram_seg = kGramSeg < 3 ? kGramSeg : 3;   // image Gram workgroups per image (1..kGramSeg)
+    std::vector<int32_t> gram_img;   // images with observations in this shard (the Gram pass's images)
     std::vector<int32_t> gblk_off;   // [n_gpt+1] block range of a general point
     std::vector<int32_t> gblk_col;   // F column of each of its blocks (6 rows: camera, 4: intrinsics)
     std::vector<int32_t> gblk_z;     // element offset of the block's Z rows within the point's Z

@@ -40,6 +40,7 @@ struct sfm_ba_plan {
     sfm_ctx* ctx = nullptr;
     BAHostPlan hp;
     DevProblem P{};
+    DBuf<int32_t> gram_img;
     DBuf<int32_t> pt_off, obs_img, obs_slot, img_obs_ptr, img_colc,
         img_coli, img_intr, intr_col, blk_img, blk_intr;
     DBuf<double> obs_uv;
@@ -143,6 +144,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(st, pl->chunks, h.chunks, s);
     up(st, pl->group_off, h.group_off, s);
     up(st, pl->img_obs_ptr, h.img_obs_ptr, s);
+    if (!h.gram_img.empty()) up(st, pl->gram_img, h.gram_img, s);
     pl->img_pt.alloc(std::max<int64_t>(h.n_sobs, 1));
     pl->img_uv.alloc(2 * std::max<int64_t>(h.n_sobs, 1));
     ba_image_order(pl->obs_img.p, pl->obs_uv.p, pl->pt_off.p, (int32_t)h.n_sobs, (int32_t)h.n_spt, prob.n_img,
@@ -196,6 +198,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
                  o_ucn = o_ub + fw * (size_t)prob.n_img * kGramSeg,
                  n_gram = o_ucn + fw * (size_t)prob.n_img * kGramSeg;
     pl->gram.alloc(n_gram);
+    // the image blocks of images without observations in this shard are never
+    // written (the Gram pass runs over the others) but may be reduce sources
+    // (one rank: every image's U terms): zero once, they stay zero
+    SFM_HIP(hipMemsetAsync(pl->gram.p + o_u, 0, (n_gram - o_u) * sizeof(double), s));
     // the terms arrive resolved against this buffer (build_plan, same layout)
     up(pl->terms, h.terms, s);
     // RCS: band + arrow + corner, or dense; the parts of a dense S no target
@@ -211,6 +217,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->zF.alloc(nF);
     pl->yF.alloc(nF);
     pl->part_u.alloc(2 * (size_t)prob.n_img * kGramSeg);
+    pl->part_u.zero(s);   // the slots of images without observations stay zero (no Gram workgroup)
     pl->part_s.alloc(2 * std::max<size_t>(h.chunks.size() + h.n_gpt, 1));
     pl->scal.alloc(kScCount);
     pl->scal.zero(s);
@@ -260,6 +267,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.obs_slot = pl->obs_slot.p; P.obs_uv = pl->obs_uv.p; P.chunks = pl->chunks.p;
     P.group_off = pl->group_off.p;
     P.img_obs_ptr = pl->img_obs_ptr.p;
+    P.gram_img = pl->gram_img.p; P.n_gram_img = (int32_t)h.gram_img.size();
     P.img_pt = pl->img_pt.p; P.img_uv = pl->img_uv.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.intr_col = pl->intr_col.p;

@@ -48,7 +48,10 @@ constexpr int kGroupChunks = 4;           // chunks per tile group, at most (the
 #define SFM_SCHUR_GROUP 1
 #endif
 constexpr int schur_group(int tile_nt) { return tile_nt == 4 ? SFM_SCHUR_GROUP : 1; }
-constexpr int kGramSeg = 3;               // workgroups per image in the image Gram pass
+#ifndef SFM_GRAM_SEG_MAX   // A/B builds: the most image Gram workgroups per image (buffer stride)
+#define SFM_GRAM_SEG_MAX 3
+#endif
+constexpr int kGramSeg = SFM_GRAM_SEG_MAX;   // workgroups per image in the image Gram pass (at most)
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
 constexpr int kCamSlots = 14;             // staged cameras per chunk (incl. constant images)
 constexpr int kIntrSlots = 4;             // staged intrinsics blocks per chunk

@@ -1,0 +1,17 @@
+# Round 4: the image Gram pass launched over the shard's images with
+# observations only; GPU tier, then Gram workgroups per image (SFM_GRAM_SEG).
+set -e
+cd "$GRAFT_REPO_ROOT"
+OUT=$GRAFT_REPO_ROOT/gpurun_out/ee_gimg
+mkdir -p "$OUT"
+bash tools/gpurun/tests.sh
+cp gpurun_out/gputests.log "$OUT/gputests.log"
+ARGS="--no-match --no-snavely --no-loop --no-pmc --no-filter --no-cpu-baseline --no-dense --no-radial3"
+for rep in 1 2; do
+for g in 3 4; do
+  SFM_GRAM_SEG=$g timeout -k 10 300 python -u bench.py --steps 20 $ARGS 2>&1 >/dev/null | grep "^\[bench\] BA:" | sed "s/^/gseg$g N1 /" | tee -a "$OUT/ab.txt"
+done
+for g in 2 3 4 6; do
+  SFM_GRAM_SEG=$g timeout -k 10 300 python -u bench.py --fake-world 8 --steps 20 $ARGS 2>&1 >/dev/null | grep "^\[bench\] BA:" | sed "s/^/gseg$g rank0-of-8 /" | tee -a "$OUT/ab.txt"
+done
+done
