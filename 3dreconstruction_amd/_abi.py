@@ -30,6 +30,8 @@ SFM_CAM_RADIAL3 = 2
 
 SFM_CTX_TUNE_HOST_MALLOC = 1
 SFM_CTX_DIAG_NO_EXCHANGE = 2
+SFM_CTX_DIAG_FAIL_SOLVE_WAIT = 4
+SFM_CTX_TIME_KERNELS = 8
 
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1

@@ -28,6 +28,18 @@
 #include "ba_bcr.h"
 #include "common.h"
 
+// Inter-workgroup hand-offs in this file use the counter form of
+// cdna_hip_programming.md Guideline 16: payloads stored and loaded with
+// agent-scope relaxed atomics (sc1: written through / read past the CU's L1),
+// drained with s_waitcnt vmcnt(0) (on gfx9 the vector memory counter also
+// counts stores), then a relaxed agent-scope ticket or flag -- no release or
+// acquire fence.  That is a property of the gfx950 ISA and its cache
+// policy, not of the HIP memory model, so the device code refuses to build
+// for any other target.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "counter-form hand-offs (sc1 payloads + vmcnt drain + relaxed ticket) are written for gfx950 only"
+#endif
+
 namespace sfm {
 namespace {
 
@@ -1352,12 +1364,10 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);
     const size_t lds_l = std::max(lds_odd, lds_even);
     const size_t lds_t = (3 * M * LD + 3 * M * ldr + 34) * sizeof(double);
-    static bool attr = false;
-    if (!attr) {   // sized for the largest nrhs (32)
-        const int cap = 160 * 1024;
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_level_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
-        SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cap));
-        attr = true;
+    {   // sized for the largest nrhs (32)
+        const size_t cap = 160 * 1024;
+        set_dyn_lds((const void*)bcr_level_kernel, cap);
+        set_dyn_lds((const void*)bcr_top_kernel, cap);
     }
     int s_top = 1;
     for (int stride = 1; stride < b.N; stride *= 2) {
@@ -1372,13 +1382,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     // one launch unless SFM_BCR_TOP_SPLIT (A/B) -- then every back-substitution
     // level in one top-down dataflow launch
     if (!std::getenv("SFM_BCR_TOP_SPLIT")) {
-        static bool attr_tc = false;
-        if (!attr_tc) {
-            // (160 KB less the corner's static LDS)
-            SFM_HIP(hipFuncSetAttribute((const void*)bcr_top_corner_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024));
-            attr_tc = true;
-        }
+        set_dyn_lds((const void*)bcr_top_corner_kernel, 156 * 1024);   // (160 KB less the corner's static LDS)
         hipLaunchKernelGGL(bcr_top_corner_kernel, dim3(b.N), dim3(NTL), lds_t, s, b, P, radius, s_top / 2);
         SFM_HIP(hipGetLastError());
     } else {
@@ -2005,20 +2009,9 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
     hipLaunchKernelGGL(dense_pack_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d, P, radius);
     SFM_HIP(hipGetLastError());
     const size_t lds_p = (3 * M * LD + 2) * sizeof(double), lds_u = 2 * M * LD * sizeof(double);
-    static bool attr = false;
-    if (!attr) {
-        SFM_HIP(hipFuncSetAttribute((const void*)dense_panel_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_p));
-        SFM_HIP(hipFuncSetAttribute((const void*)dense_update_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_u));
-        attr = true;
-    }
-    static int n_cu = 0;
-    if (!n_cu) {
-        int dev = 0;
-        SFM_HIP(hipGetDevice(&dev));
-        SFM_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    set_dyn_lds((const void*)dense_panel_kernel, lds_p);
+    set_dyn_lds((const void*)dense_update_kernel, lds_u);
+    const int n_cu = device_cu_count();
     static const bool flow_off = std::getenv("SFM_DENSE_LAUNCHES") != nullptr;
     static const int flow_max_nt = [] {
         const char* e = std::getenv("SFM_DENSE_FLOW_MAX_NT");
@@ -2032,12 +2025,7 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         // VALU (15x in tools/probe/diag16_probe.hip), and every workgroup is
         // resident, so every wait ends
         const size_t lds_f = std::max<size_t>(kDfLds * sizeof(double), 81 * 1024);
-        static bool attr_f = false;
-        if (!attr_f) {
-            SFM_HIP(hipFuncSetAttribute((const void*)dense_flow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_f));
-            attr_f = true;
-        }
+        set_dyn_lds((const void*)dense_flow_kernel, lds_f);
         const int workers = std::min(df_tasks(d.nt), n_cu - 1);
         hipLaunchKernelGGL(dense_flow_kernel, dim3(1 + workers), dim3(NT), lds_f, s, d, P, epoch);
         SFM_HIP(hipGetLastError());
@@ -2073,12 +2061,7 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         // one workgroup per block column, all resident: more than half a CU's
         // LDS each, so one per CU
         constexpr size_t lds_all = 81 * 1024;
-        static bool attr_b = false;
-        if (!attr_b) {
-            SFM_HIP(hipFuncSetAttribute((const void*)dense_back_all_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)lds_all));
-            attr_b = true;
-        }
+        set_dyn_lds((const void*)dense_back_all_kernel, lds_all);
         hipLaunchKernelGGL(dense_back_all_kernel, dim3(d.nt), dim3(NT), lds_all, s, d, P, epoch);
         SFM_HIP(hipGetLastError());
         return;

@@ -12,14 +12,19 @@ namespace sfm {
 // Scalar slots produced by ba_finalize (one double each).
 enum : int {
     kScCost = 0, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E,  // summed over ranks
-    kScBadX, kScGmaxE, kScCandBad, kScStepBad,                           // max over ranks
-    kScXnorm2F, kScStepnorm2F, kScGmaxF, kScSolveFail,                   // replicated
+    kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScSolveFail,             // max over ranks
+    kScXnorm2F, kScStepnorm2F, kScGmaxF,                                 // replicated
     kScCount
 };
 // kScSolveFail: 0 solved, 1 numerical failure (an invalid LM step),
-// kSolveWaitTimeout a dataflow solve's wait timed out (a device error)
+// kSolveWaitTimeout a dataflow solve's wait timed out (a device error).  Max
+// over ranks although every rank solves the same system: a numerical failure
+// is replicated, but a wait timeout depends on which workgroups were resident
+// on that rank's GPU, and every rank has to see it to leave the LM loop
+// together (a rank that stopped alone would leave the others waiting in the
+// next iteration's collective).
 constexpr double kSolveWaitTimeout = 2.0;
-constexpr int kScSumBegin = 0, kScSumEnd = 5, kScMaxBegin = 5, kScMaxEnd = 9;
+constexpr int kScSumBegin = 0, kScSumEnd = 5, kScMaxBegin = 5, kScMaxEnd = 10;
 constexpr int kPartT = 5;  // per step block: model acc, cand cost, step norm^2, step bad, cand bad
 
 struct DevProblem {

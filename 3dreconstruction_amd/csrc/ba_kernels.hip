@@ -34,6 +34,18 @@
 #include "ba_kernels.h"
 #include "common.h"
 
+// Inter-workgroup hand-offs in this file use the counter form of
+// cdna_hip_programming.md Guideline 16: payloads stored and loaded with
+// agent-scope relaxed atomics (sc1: written through / read past the CU's L1),
+// drained with s_waitcnt vmcnt(0) (on gfx9 the vector memory counter also
+// counts stores), then a relaxed agent-scope ticket or flag -- no release or
+// acquire fence.  That is a property of the gfx950 ISA and its cache
+// policy, not of the HIP memory model, so the device code refuses to build
+// for any other target.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "counter-form hand-offs (sc1 payloads + vmcnt drain + relaxed ticket) are written for gfx950 only"
+#endif
+
 namespace sfm {
 namespace {
 
@@ -2661,16 +2673,12 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
         const size_t lds = (64 * kZStage + (size_t)P.gz_max) * sizeof(double);
         if (scale_e)
             SFM_BY_MODEL_ALL(P, {
-                if (lds > 64 * 1024)
-                    SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, true>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                if (lds > 64 * 1024) set_dyn_lds((const void*)zpoint_kernel<CM, true>, lds);
                 hipLaunchKernelGGL((zpoint_kernel<CM, true>), dim3(P.n_zlong), dim3(64), lds, s, P, cp, intr, X, radius);
             });
         else
             SFM_BY_MODEL_ALL(P, {
-                if (lds > 64 * 1024)
-                    SFM_HIP(hipFuncSetAttribute((const void*)zpoint_kernel<CM, false>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                if (lds > 64 * 1024) set_dyn_lds((const void*)zpoint_kernel<CM, false>, lds);
                 hipLaunchKernelGGL((zpoint_kernel<CM, false>), dim3(P.n_zlong), dim3(64), lds, s, P, cp, intr, X, radius);
             });
         SFM_HIP(hipGetLastError());
@@ -2748,9 +2756,7 @@ void ba_solve(const DevProblem& P, double radius, hipStream_t s) {
     bool lds = false;
     const size_t bytes = solve_lds_bytes(P, &lds);
     SFM_REQUIRE(bytes <= 160 * 1024, SFM_ERR_UNSUPPORTED, "RCS band too wide (D=%d)", P.D);
-    if (bytes > 64 * 1024)
-        SFM_HIP(hipFuncSetAttribute((const void*)solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)bytes));
+    if (bytes > 64 * 1024) set_dyn_lds((const void*)solve_kernel, bytes);
     hipLaunchKernelGGL(solve_kernel, dim3(1), dim3(256), bytes, s, P, radius, lds ? 1 : 0);
     SFM_HIP(hipGetLastError());
 }

@@ -568,6 +568,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (P.dense) dense_solve(pl->dense, P, radius, s, ++pl->bcr_epoch);
         else if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s, ++pl->bcr_epoch);
         else ba_solve(P, radius, s);
+        if (ctx->fail_solve_wait) ba_fill(P.scal + kScSolveFail, 1, kSolveWaitTimeout, s);   // diagnostic
         ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         const unsigned long long seq = ++pl->fin_seq;

@@ -494,12 +494,7 @@ void casc_hash(const CascTables& t, const float* proj, const float* zm, const in
     SFM_REQUIRE(n <= 65535, SFM_ERR_UNSUPPORTED, "cascade hashing over %d images", n);
     {
         const size_t mlds = (size_t)kCascCode * kPtStride * sizeof(float);
-        static bool mattr = false;
-        if (!mattr) {
-            SFM_HIP(hipFuncSetAttribute((const void*)casc_hash_mfma_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)mlds));
-            mattr = true;
-        }
+        set_dyn_lds((const void*)casc_hash_mfma_kernel, mlds);
         // every workgroup stages the 106 KB projection image once: enough
         // workgroups to fill the chip (~1024), not one per 8 tiles
         const int tiles = (max_n + 15) / 16;
@@ -522,13 +517,7 @@ void casc_match(const CascMatchArgs& a, int max_n, hipStream_t s) {
     if (a.n_pairs == 0) return;
     const size_t lds = casc_lds_bytes(max_n);
     if (max_n <= kCascLdsMaxN) {
-        static bool attr = false;
-        if (!attr) {
-            SFM_HIP(hipFuncSetAttribute((const void*)casc_match_lds_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)casc_lds_bytes(kCascLdsMaxN)));
-            attr = true;
-        }
+        set_dyn_lds((const void*)casc_match_lds_kernel, casc_lds_bytes(kCascLdsMaxN));
         hipLaunchKernelGGL(casc_match_lds_kernel, dim3((unsigned)a.n_pairs), dim3(kCascLdsThreads),
                            lds, s, a);
     } else {

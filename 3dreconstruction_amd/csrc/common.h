@@ -73,6 +73,14 @@ void ctx_allreduce(sfm_ctx* ctx, double* dev_buf, size_t n, int op_max, hipStrea
 int rccl_comm_init(void** comm, int world, const uint8_t* id128, int rank);
 void rccl_comm_destroy(void* comm);
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for the current device,
+// once per (device, kernel) and raised only when a launch needs more:
+// attributes are per device, and contexts of one process may drive several
+// devices from several threads (ctx.cpp, under a mutex).
+void set_dyn_lds(const void* kernel, size_t bytes);
+// compute units of the current device (cached per device)
+int device_cu_count();
+
 // Device memory cache (ctx.cpp).  A block freed while a context is bound to
 // the calling thread (CtxScope) is kept for later allocations under the same
 // context stream instead of going back through hipFree, which synchronises
@@ -208,8 +216,10 @@ struct sfm_ctx {
     size_t host_cap = 0;
     int cu_count = 0;
     bool no_exchange = false;                    // SFM_CTX_DIAG_NO_EXCHANGE (per-rank timing only)
+    bool fail_solve_wait = false;                // SFM_CTX_DIAG_FAIL_SOLVE_WAIT (error-path tests)
+    bool time_kernels = false;                   // SFM_CTX_TIME_KERNELS (sfm_ctx_last_kernel_ms)
     hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
-    double last_kernel_ms = 0.0;                 // sfm_fmatrix_ac's kernel (sfm_ctx_last_kernel_ms)
+    double last_kernel_ms = -1.0;                // sfm_fmatrix_ac's kernel (sfm_ctx_last_kernel_ms)
 };
 
 namespace sfm {

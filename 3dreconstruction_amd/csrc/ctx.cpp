@@ -92,6 +92,29 @@ int rccl_allgather_f64(void* comm, const double* in, double* out, size_t n, hipS
     return SFM_OK;
 }
 
+void set_dyn_lds(const void* kernel, size_t bytes) {
+    int dev = 0;
+    SFM_HIP(hipGetDevice(&dev));
+    static std::mutex mu;
+    static auto* done = new std::map<std::pair<int, const void*>, size_t>;   // never destroyed
+    std::lock_guard<std::mutex> lk(mu);
+    size_t& have = (*done)[{dev, kernel}];
+    if (have >= bytes) return;
+    SFM_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    have = bytes;
+}
+
+int device_cu_count() {
+    int dev = 0;
+    SFM_HIP(hipGetDevice(&dev));
+    static std::mutex mu;
+    static auto* cus = new std::map<int, int>;
+    std::lock_guard<std::mutex> lk(mu);
+    int& n = (*cus)[dev];
+    if (!n) SFM_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    return n;
+}
+
 // ---- device memory cache ----------------------------------------------------
 namespace {
 
@@ -320,6 +343,8 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         c->rank = opts->rank;
         c->world = opts->world_size;
         c->cu_count = prop.multiProcessorCount;
+        c->fail_solve_wait = (opts->flags & SFM_CTX_DIAG_FAIL_SOLVE_WAIT) != 0;
+        c->time_kernels = (opts->flags & SFM_CTX_TIME_KERNELS) != 0;
         SFM_HIP(hipSetDevice(c->device));
         SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         {

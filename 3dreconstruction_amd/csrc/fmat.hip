@@ -655,23 +655,22 @@ extern "C" int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off,
             a.gkey = d_gkey.p;
             a.gval = d_gval.p;
         }
-        static bool attr = false;
-        if (!attr) {
-            SFM_HIP(hipFuncSetAttribute((const void*)fmatrix_ac_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        12 * kMaxLdsSort));
-            attr = true;
-        }
+        set_dyn_lds((const void*)fmatrix_ac_kernel, 12 * kMaxLdsSort);
         SFM_REQUIRE(n_pairs < ((int64_t)1 << 31), SFM_ERR_UNSUPPORTED, "sfm_fmatrix_ac: too many pairs");
-        // the kernel alone (sfm_ctx_last_kernel_ms): the uploads are drained
-        // first, or the start event can be stamped while a DMA of the stream
-        // is still running (measured: 48 ms by events against rocprofv3's 29)
-        SFM_HIP(hipStreamSynchronize(s));
+        // the kernel alone (sfm_ctx_last_kernel_ms, SFM_CTX_TIME_KERNELS only):
+        // the uploads are drained first, or the start event can be stamped
+        // while a DMA of the stream is still running (measured: 48 ms by
+        // events against rocprofv3's 29)
+        const bool timed = ctx->time_kernels;
+        hipEvent_t* ev = timed ? ctx_events(ctx) : nullptr;
+        if (timed) {
+            SFM_HIP(hipStreamSynchronize(s));
+            SFM_HIP(hipEventRecord(ev[0], s));
+        }
         tm.mark("upload");
-        hipEvent_t* ev = ctx_events(ctx);
-        SFM_HIP(hipEventRecord(ev[0], s));
         hipLaunchKernelGGL(fmatrix_ac_kernel, dim3((unsigned)n_pairs), dim3(kFT), lds, s, a);
         SFM_HIP(hipGetLastError());
-        SFM_HIP(hipEventRecord(ev[1], s));
+        if (timed) SFM_HIP(hipEventRecord(ev[1], s));
         tm.mark("launch");
         std::vector<double> F(9 * (size_t)n_pairs), stat(4 * (size_t)n_pairs);
         std::vector<uint32_t> binl((size_t)std::max<int64_t>(n, 1));
@@ -681,7 +680,8 @@ extern "C" int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off,
         if (n) SFM_HIP(hipMemcpyAsync(binl.data(), d_binl.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
         SFM_HIP(hipMemcpyAsync(&fail, d_fail.p, 4, hipMemcpyDeviceToHost, s));
         SFM_HIP(hipStreamSynchronize(s));
-        {
+        ctx->last_kernel_ms = -1.0;
+        if (timed) {
             float ms = 0.f;
             SFM_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
             ctx->last_kernel_ms = ms;

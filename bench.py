@@ -530,7 +530,8 @@ def bench_filter(ctx, n_pairs, n_match, cpu=True, cpu_pairs=32):
            "ransac_iterations_per_sec": iters / dt, "pairs_kept": kept,
            # the timed call includes the host normalisation, the uploads and
            # the result download; the kernel alone (HIP events):
-           "kernel_ms": kms.value, "kernel_pairs_per_sec": n_pairs / (kms.value * 1e-3) if kms.value > 0 else None,
+           "kernel_ms": kms.value if kms.value > 0 else None,
+           "kernel_pairs_per_sec": n_pairs / (kms.value * 1e-3) if kms.value > 0 else None,
            "inliers": int(sum(r["n_inliers"] for r in res)),
            "workload": f"{n_pairs} pairs x {n_match} putative matches (30% clutter), 1920x1080 views, "
                        "GeometricFilter_FMatrix_AC(4.0, 2048) semantics (sparseBuilder.cpp:1179-1186); "
@@ -561,6 +562,25 @@ def bench_filter(ctx, n_pairs, n_match, cpu=True, cpu_pairs=32):
             log(f"cpu baseline filter: {n} pairs in {cdt:.1f}s")
         except Exception as ex:
             log(f"cpu baseline filter unavailable: {ex}")
+    return out
+
+
+def loop_replica_line(r, seconds, images):
+    """The C5 line at N > 1: N independent replicas of the same sequence, one
+    per GPU (the loop does not shard).  `r` is rank 0's
+    bench_loop result, `seconds` every rank's loop wall time in rank order.
+    `value` is the aggregate images/s over the slowest replica (weak scaling:
+    N sequences, not one sequence N times faster); the metric name says so and
+    each replica's own rate is reported beside it, so the aggregate is not
+    read as a speedup of one reconstruction."""
+    world, t_max = len(seconds), max(seconds)
+    out = dict(r)
+    out.update(metric=f"C5 incremental loop images/sec, fixed write-back, aggregate of {world} independent "
+                      f"replicas (one sequence per GPU)",
+               value=world * images / t_max, seconds=t_max, replicas=world,
+               per_replica_images_per_sec=[images / t for t in seconds],
+               slowest_replica_images_per_sec=images / t_max,
+               scaling="weak (independent sequences, one per GPU; not a speedup of one sequence; DESIGN.md §7)")
     return out
 
 
@@ -636,6 +656,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def all_over_ranks(v):   # every rank's value, in rank order
+        if dist is None:
+            return [v]
+        got = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(got, torch.tensor([v], dtype=torch.float64))
+        return [float(t.item()) for t in got]
+
     comm_id = None
     transport = "none"
     if world > 1:
@@ -650,7 +677,8 @@ def main():
     ctx = None
     if comm_id is not None:
         try:
-            ctx = api.Context(device=local_rank, rank=rank, world_size=world, comm_id=comm_id)
+            ctx = api.Context(device=local_rank, rank=rank, world_size=world, comm_id=comm_id,
+                              flags=abi.SFM_CTX_TIME_KERNELS)
             transport = "rccl"
         except Exception as ex:
             log(f"RCCL communicator failed ({ex})")
@@ -667,16 +695,17 @@ def main():
             def host_allreduce(a, op):
                 dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM)
 
-            ctx = api.Context(device=local_rank, rank=rank, world_size=world, allreduce=host_allreduce)
+            ctx = api.Context(device=local_rank, rank=rank, world_size=world, allreduce=host_allreduce,
+                              flags=abi.SFM_CTX_TIME_KERNELS)
             transport = "gloo-host (RCCL unavailable)"
             log("falling back to the host-staged gloo all-reduce")
     elif args.fake_world > 1:
         ctx = api.Context(device=local_rank, rank=0, world_size=args.fake_world,
-                          flags=abi.SFM_CTX_DIAG_NO_EXCHANGE)
+                          flags=abi.SFM_CTX_DIAG_NO_EXCHANGE | abi.SFM_CTX_TIME_KERNELS)
         transport = f"none (diagnostic: shard 0 of {args.fake_world}, exchanges skipped on the device)"
     else:
         # opt-in host malloc setting for this short-lived process
-        ctx = api.Context(device=local_rank, flags=abi.SFM_CTX_TUNE_HOST_MALLOC)
+        ctx = api.Context(device=local_rank, flags=abi.SFM_CTX_TUNE_HOST_MALLOC | abi.SFM_CTX_TIME_KERNELS)
 
     # the committed PMC summary was measured on the default C4/C3 sizes at N=1
     pmc_ok = (world == 1 and args.n_pt == 500_000 and args.n_cam == 1000 and args.match_frames == 500)
@@ -888,20 +917,18 @@ def main():
     elif world > 1 and not args.no_loop:
         # C5 at N > 1: replicas only (DESIGN.md §7 -- the loop is host bound,
         # one image after another).  Every rank runs its own sequence on a
-        # one-rank context of its GPU; the line is the aggregate images/s over
-        # the slowest rank's wall time (weak scaling).
+        # one-rank context of its GPU; rank 0 reports the aggregate and every
+        # replica's own rate (loop_replica_line).
         lctx = api.Context(device=local_rank)
         barrier()
         r = bench_loop(lctx, args.loop_images, cpu=False, fixed_writeback=True)
         r.pop("images", None)
         lctx.synchronize()
         lctx.close()
-        t_max = max_over_ranks(r["seconds"])
+        secs = all_over_ranks(r["seconds"])
         if rank == 0:
-            loop_fixed = dict(r, value=world * args.loop_images / t_max, seconds=t_max, replicas=world,
-                              scaling="weak (independent sequences, one per GPU; DESIGN.md §7)")
-            loop_fixed["metric"] += f", {world} replicas"
-            log(f"loop replicas: {world} x {args.loop_images} images, slowest rank {t_max:.2f}s "
+            loop_fixed = loop_replica_line(r, secs, args.loop_images)
+            log(f"loop replicas: {world} x {args.loop_images} images, slowest rank {max(secs):.2f}s "
                 f"-> {loop_fixed['value']:.1f} images/s aggregate")
 
     # ---------------- dense-S stress case ----------------

@@ -89,6 +89,18 @@ typedef struct sfm_ctx_opts {
  * its kernels and wall time are what that rank spends in an N-GPU run minus
  * the collectives; the solve is not the global one (bench.py --fake-world). */
 #define SFM_CTX_DIAG_NO_EXCHANGE 2
+/* Diagnostic only (error-path tests): every reduced-camera-system solve of
+ * this context reports that one of its dataflow waits timed out, as when
+ * another context holds the CUs a persistent solve kernel needs.  The solve
+ * verdict is max-reduced over ranks with the other per-iteration maxima, so
+ * every rank of a sharded solve then returns SFM_ERR_DEVICE together instead
+ * of the others waiting in the next collective. */
+#define SFM_CTX_DIAG_FAIL_SOLVE_WAIT 4
+/* Measurement: sfm_fmatrix_ac brackets its kernel with HIP events (after
+ * draining its uploads) so that sfm_ctx_last_kernel_ms can report the kernel
+ * alone.  Off by default: the extra stream synchronisation and event pair are
+ * not part of the filter's production path. */
+#define SFM_CTX_TIME_KERNELS 8
 
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
 int sfm_comm_unique_id(uint8_t* out128);
@@ -595,7 +607,8 @@ int sfm_fmatrix_ac(sfm_ctx* ctx, int64_t n_pairs, const int64_t* off, const doub
 
 /* Device time (HIP events on the context's stream) of the kernel of the
  * context's last sfm_fmatrix_ac call, without its host normalisation,
- * uploads and downloads (measurement; no reference counterpart). */
+ * uploads and downloads (measurement; no reference counterpart).  Only a
+ * context created with SFM_CTX_TIME_KERNELS times it; -1 otherwise. */
 int sfm_ctx_last_kernel_ms(sfm_ctx* ctx, double* ms);
 
 /* sparseBuilder::filter(), file-staged: sfm_data.json (view sizes) +

@@ -276,6 +276,54 @@ def _check_sharded(ctx, tmp_path, scene_args, world):
     np.testing.assert_allclose(r["x"], x, atol=5e-3 * (np.abs(x).max() + 1))
 
 
+def _timeout_worker(rank, world, port, out_path, vis_mode):
+    import sys as _s
+    _s.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    _s.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import importlib as _il
+    import torch
+    import torch.distributed as dist
+    import _helpers as H2
+    api2 = _il.import_module("3dreconstruction_amd.api")
+    abi2 = _il.import_module("3dreconstruction_amd._abi")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allreduce(a, op):
+        dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.MAX if op == 1 else dist.ReduceOp.SUM)
+
+    # only the last rank's solves report a dataflow wait timeout
+    flags = abi2.SFM_CTX_DIAG_FAIL_SOLVE_WAIT if rank == world - 1 else 0
+    ctx2 = api2.Context(device=0, rank=rank, world_size=world, allreduce=allreduce, flags=flags)
+    sc = H2.Scene(n_cam=24, n_pt=3000, k=6, vis_mode=vis_mode, seed=17)
+    e, i, x = sc.params()
+    plan = api2.BAPlan(ctx2, sc.problem(), e, i, x)
+    rc, _ = plan.run(check=False)
+    plan.close()
+    rcs = torch.tensor([rc], dtype=torch.int64)
+    gathered = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(gathered, rcs)
+    if rank == 0:
+        np.save(out_path, np.array([int(g.item()) for g in gathered]))
+    dist.barrier()
+    ctx2.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("vis_mode", [0, 1])   # BCR band solver, dense RCS
+def test_solve_wait_timeout_reaches_every_rank(tmp_path, vis_mode):
+    """a dataflow-wait timeout is decided on one rank's GPU, so its
+    verdict is max-reduced with the per-iteration maxima: every rank returns
+    SFM_ERR_DEVICE in the same iteration (none is left waiting in the next
+    collective, which would hang this test until its timeout)."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "rc.npy")
+    port = 33500 + (os.getpid() % 2000) + vis_mode
+    mp.spawn(_timeout_worker, args=(2, port, out, vis_mode), nprocs=2, join=True)
+    assert list(np.load(out)) == [abi.SFM_ERR_DEVICE, abi.SFM_ERR_DEVICE]
+
+
 def test_rccl_single_rank_communicator(ctx):
     """The RCCL binding end to end on one GPU: a 1-rank communicator runs every
     per-iteration all-reduce (identities), so the solve must be bit-identical

@@ -338,3 +338,22 @@ def test_filter_stage_gpu(tmp_path, ctx):
         exp = np.stack([ii[off[q]:off[q + 1]][want[q]["inliers"]], jj[off[q]:off[q + 1]][want[q]["inliers"]]], 1)
         assert np.array_equal(got[pairs[q]], exp)
     assert st.n_pairs_out == len(kept) and st.n_matches_out == sum(want[q]["n_inliers"] for q in kept)
+
+
+@pytest.mark.gpu
+def test_gpu_fmatrix_kernel_timing_opt_in(ctx):
+    # the filter's production path takes no events and no extra stream sync:
+    # only a context created with SFM_CTX_TIME_KERNELS reports the kernel time
+    xs, whs = _batch([(300, 0.2), (800, 0.1)], seed0=900)
+    lib = abi.load()
+    ms = C.c_double(0.0)
+    got = api.fmatrix_ac(ctx, xs, whs)
+    assert lib.sfm_ctx_last_kernel_ms(ctx.h, C.byref(ms)) == 0 and ms.value == -1.0
+    tctx = api.Context(0, flags=abi.SFM_CTX_TIME_KERNELS)
+    try:
+        timed = api.fmatrix_ac(tctx, xs, whs)
+        assert lib.sfm_ctx_last_kernel_ms(tctx.h, C.byref(ms)) == 0 and ms.value > 0.0
+    finally:
+        tctx.close()
+    for g, t in zip(got, timed):
+        _same(g, t)
