@@ -32,6 +32,23 @@ SFM_CTX_TUNE_HOST_MALLOC = 1
 SFM_CTX_DIAG_NO_EXCHANGE = 2
 SFM_CTX_DIAG_FAIL_SOLVE_WAIT = 4
 SFM_CTX_TIME_KERNELS = 8
+SFM_CTX_BA_DENSE_RCS = 1 << 4
+SFM_CTX_BA_SEQ_BAND = 1 << 5
+SFM_CTX_BA_TILE80 = 1 << 6
+SFM_CTX_BA_SPLIT_REDUCE = 1 << 7
+SFM_CTX_BA_SPLIT_BCR = 1 << 8
+SFM_CTX_BA_DENSE_CHAIN = 1 << 9
+
+
+def SFM_CTX_BA_STEP_LANES(n):
+    return {1: 1, 2: 2, 4: 3, 8: 4}[n] << 12
+
+
+def SFM_CTX_BA_REDUCE_WAVES(n):
+    return {1: 1, 2: 2, 4: 3}[n] << 15
+
+
+SFM_RCS_BCR, SFM_RCS_DENSE, SFM_RCS_SEQ_BAND = 0, 1, 2
 
 SFM_MATCH_RATIO = 0
 SFM_MATCH_MUTUAL = 1
@@ -100,7 +117,8 @@ class BAPlanInfo(C.Structure):
                 ("band_blocks", C.c_int32), ("n_cam_active", C.c_int32),
                 ("n_intr_active", C.c_int32), ("rcs_dim", C.c_int64),
                 ("last_kernel_ms", C.c_double * 8), ("schur_flops_per_iter", C.c_int64),
-                ("schur_launches", C.c_int64), ("schur_ms_total", C.c_double)]
+                ("schur_launches", C.c_int64), ("schur_ms_total", C.c_double),
+                ("rcs_solver", C.c_int32), ("tile_rows", C.c_int32)]
 
 
 class BAPlanShape(C.Structure):

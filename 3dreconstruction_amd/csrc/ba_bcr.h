@@ -20,6 +20,7 @@ struct BcrArgs {
     double *R = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
     unsigned* yflag = nullptr;   // [N] back substitution: y_i published for epoch (bcr_back_kernel<true>)
     unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums
+    bool split = false;   // SFM_CTX_BA_SPLIT_BCR: top, corner and each back-substitution level as own launches
 };
 
 // Dense RCS solve (blocked Cholesky on 64x64 tiles, same file).
@@ -30,6 +31,7 @@ struct DenseArgs {
     unsigned* xflag = nullptr;   // [nt] back substitution: x_k published for epoch (dense_back_all_kernel)
     unsigned* fflag = nullptr;   // [2 nt^2 + nt] dataflow factorisation: L tiles, chain inputs, y (dense_flow_kernel)
     unsigned long long* stamps = nullptr;   // SFM_DENSE_STAMPS diagnostic: chain phase cycle sums [8]
+    bool chain = false;   // SFM_CTX_BA_DENSE_CHAIN: launch chains instead of the dataflow kernels
 };
 // flag words of a DenseArgs (x flags + the factorisation's), zeroed once at bind
 size_t dense_flag_words(const DenseArgs& d);

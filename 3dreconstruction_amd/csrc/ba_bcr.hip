@@ -1379,9 +1379,9 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         s_top = stride * 2;
     }
     // the top, then the corner (one column left for the back substitution) --
-    // one launch unless SFM_BCR_TOP_SPLIT (A/B) -- then every back-substitution
-    // level in one top-down dataflow launch
-    if (!std::getenv("SFM_BCR_TOP_SPLIT")) {
+    // one launch unless SFM_CTX_BA_SPLIT_BCR (A/B, tests) -- then every
+    // back-substitution level in one top-down dataflow launch
+    if (!b.split) {
         set_dyn_lds((const void*)bcr_top_corner_kernel, 156 * 1024);   // (160 KB less the corner's static LDS)
         hipLaunchKernelGGL(bcr_top_corner_kernel, dim3(b.N), dim3(NTL), lds_t, s, b, P, radius, s_top / 2);
         SFM_HIP(hipGetLastError());
@@ -1393,10 +1393,10 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     }
     int n_back = 1;
     for (int stride = s_top / 2; stride >= 1; stride /= 2) n_back += (b.N - stride + 2 * stride - 1) / (2 * stride);
-    if (!std::getenv("SFM_BCR_BACK_LEVELS")) {
+    if (!b.split) {
         hipLaunchKernelGGL(bcr_back_kernel<true>, dim3(n_back), dim3(NT), 0, s, b, P, s_top, epoch);
         SFM_HIP(hipGetLastError());
-    } else {   // diagnostic: one launch per level
+    } else {   // SFM_CTX_BA_SPLIT_BCR: one launch per level
         hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(1), dim3(NT), 0, s, b, P, 0, epoch);
         SFM_HIP(hipGetLastError());
         for (int stride = s_top / 2; stride >= 1; stride /= 2) {
@@ -1421,16 +1421,14 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
 //             the k-th one stores L_kk, X_kk and y_k = X_kk b_k
 //   update k  A_ij -= L_ik L_jk' for k < j <= i (one workgroup per tile, MFMA),
 //             b_i -= L_ik y_k (forward substitution, fused); columns go in
-//             groups of SFM_DENSE_W so the trailing tiles are read and written
+//             groups of kDenseW so the trailing tiles are read and written
 //             once per group (the update is HBM bound on those tiles)
 //   back      x_k = X_kk' y_k, then y_i -= L_ki' x_k for i < k (one launch per k)
 // ===========================================================================
 namespace {
 
 constexpr int kDM = 64;   // tile
-#ifndef SFM_DENSE_W   // block columns per trailing update
-#define SFM_DENSE_W 4
-#endif
+constexpr int kDenseW = 4;   // block columns per trailing update
 
 __global__ __launch_bounds__(256) void dense_pack_kernel(DenseArgs d, DevProblem P, double radius) {
     const int64_t np = d.np;
@@ -2012,12 +2010,12 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
     set_dyn_lds((const void*)dense_panel_kernel, lds_p);
     set_dyn_lds((const void*)dense_update_kernel, lds_u);
     const int n_cu = device_cu_count();
-    static const bool flow_off = std::getenv("SFM_DENSE_LAUNCHES") != nullptr;
-    static const int flow_max_nt = [] {
-        const char* e = std::getenv("SFM_DENSE_FLOW_MAX_NT");
-        return e ? std::atoi(e) : 29;
-    }();
-    if (!flow_off && d.nt <= flow_max_nt) {
+    // up to 29 block columns (the C5 loop's systems) the dataflow kernel; at
+    // dense-S's 94 it only equals the launch chain, which
+    // stays the form for wider systems (and every system under
+    // SFM_CTX_BA_DENSE_CHAIN)
+    constexpr int kFlowMaxNt = 29;
+    if (!d.chain && d.nt <= kFlowMaxNt) {
         // factorisation and both substitutions in one dataflow launch: the
         // chain workgroup and up to n_cu - 1 task workers, one workgroup per CU
         // (the LDS request forces it): the chain's pivot wave must not share
@@ -2031,11 +2029,11 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         SFM_HIP(hipGetLastError());
         return;
     }
-    // block columns in groups of W = SFM_DENSE_W: panel c, then the group's
+    // block columns in groups of W = kDenseW: panel c, then the group's
     // later columns updated from column c alone (rhs of column c fused), ...;
     // after the group's last panel every later tile is updated from all W
     // columns in one pass, read and written once
-    constexpr int W = SFM_DENSE_W;
+    constexpr int W = kDenseW;
     for (int k = 0; k < d.nt; k += W) {
         const int w = std::min(W, d.nt - k);
         for (int c = k; c < k + w; ++c) {
@@ -2057,7 +2055,7 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
             SFM_HIP(hipGetLastError());
         }
     }
-    if (d.nt <= n_cu && !std::getenv("SFM_DENSE_BACK_LAUNCHES")) {
+    if (d.nt <= n_cu && !d.chain) {
         // one workgroup per block column, all resident: more than half a CU's
         // LDS each, so one per CU
         constexpr size_t lds_all = 81 * 1024;

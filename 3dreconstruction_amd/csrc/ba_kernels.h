@@ -40,6 +40,7 @@ struct DevProblem {
     int32_t step_split;  // lanes per point in step_kernel (1, 2, 4, 8)
     int32_t n_zero;     // world > 1: targets[n_targets, n_targets + n_zero) are cleared, not summed
     int32_t red_waves;  // waves per target in reduce_kernel (1, 2, 4)
+    int32_t red_split;  // SFM_CTX_BA_SPLIT_REDUCE: long targets in their own two launches
     int32_t gram_seg;   // image Gram workgroups per image (1..kGramSeg; U / Ub / Ucn / part_u stride)
     int32_t n_gram_img;          // images with observations in this shard
     const int32_t* gram_img;     // [n_gram_img] their indices (the Gram pass's workgroups)

@@ -429,16 +429,10 @@ __device__ __forceinline__ void reduce_scatter64(double (&v)[64], int lane) {
 }
 }  // namespace gram
 
-#ifndef SFM_GRAM_WPE
-#define SFM_GRAM_WPE 2
-#endif
-#ifndef SFM_GRAM_DEEP   // point gathers two iterations ahead instead of one
-#define SFM_GRAM_DEEP 1
-#endif
 // PASS: which 64 slots this launch sums (RADIAL3's 91 sums take two passes,
 // each re-linearising the image's observations; the other models one).
 template <int CM, int PASS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WPE, SFM_GRAM_WPE))) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const double* __restrict__ X) {
     using kT = gram::SlotTable<CM>;
@@ -501,7 +495,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         }
     }
     };
-#if SFM_GRAM_DEEP
     // three stages: the point gather (random rows of X) two iterations ahead
     int p_c, p_n, p_nn;
     double2 uv_c, uv_n, uv_nn;
@@ -522,24 +515,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SFM_GRAM_WP
         fetch_ids(base + 768, p_nn, uv_nn);
         process(p_cur, uv, Xp);
     }
-#else
-    int p_c, p_n;
-    double2 uv_c, uv_n;
-    double x_c[3];
-    fetch_ids(o0 + 64 * wave, p_c, uv_c);
-    fetch_ids(o0 + 64 * wave + 256, p_n, uv_n);
-    fetch_x(p_c, x_c);
-    for (int base = o0 + 64 * wave; base < o1; base += 256) {
-        const int p_cur = p_c;
-        const double2 uv = uv_c;
-        const double Xp[3] = {x_c[0], x_c[1], x_c[2]};
-        // issue the next loads before this observation's arithmetic
-        p_c = p_n; uv_c = uv_n;
-        fetch_x(p_c, x_c);
-        fetch_ids(base + 512, p_n, uv_n);
-        process(p_cur, uv, Xp);
-    }
-#endif
     gram::reduce_scatter64(g, lane);
     bad = wave_max(bad);
     part[wave][lane] = g[0];
@@ -662,18 +637,6 @@ __device__ __forceinline__ bool crow_valid(const ChunkDesc& cd, int t) { return 
 __device__ constexpr int kTi[15] = {0, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 4};
 __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4};
 
-#ifndef SFM_SCHUR_PRE_WAIT   // the first batch's loads waited before the batch loop
-#define SFM_SCHUR_PRE_WAIT 1
-#endif
-#ifndef SFM_SCHUR_WPE   // waves per SIMD the Schur kernel is compiled for
-#define SFM_SCHUR_WPE 2
-#endif
-#ifndef SFM_SCHUR5_SP   // the same for the 80-row variant (SO >= the planner's kSubObs)
-#define SFM_SCHUR5_SP kSubPts
-#endif
-#ifndef SFM_SCHUR5_SO
-#define SFM_SCHUR5_SO kSubObs
-#endif
 
 // NT = 5: rows 0..75 F blocks, row 79 = w, so -Z w comes out of the MFMA.
 // NT = 4: rows 0..63 F blocks; -Z w (64 values) is a VALU dot product per lane.
@@ -683,7 +646,7 @@ __device__ constexpr int kTj[15] = {0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4}
 // point_scale_kernel computes) from the unscaled Jx it linearises anyway,
 // writes them to scaleE and uses them, instead of a separate pass.
 template <int CM, int NT, int SP = kSubPts, int SO = kSubObs, bool SE = false>
-__global__ __launch_bounds__(64 * schur_group(NT)) __attribute__((amdgpu_waves_per_eu(SFM_SCHUR_WPE, SFM_SCHUR_WPE))) void schur_kernel(
+__global__ __launch_bounds__(64 * schur_group(NT)) __attribute__((amdgpu_waves_per_eu(2, 2))) void schur_kernel(
     DevProblem P, const CamPre* __restrict__ cps, const double* __restrict__ intr,
     const double* __restrict__ X, double radius, unsigned long long* __restrict__ stamps) {
     constexpr int IW = kIW<CM>;   // tile rows (and F columns) of an intrinsics block
@@ -810,14 +773,12 @@ __global__ __launch_bounds__(64 * schur_group(NT)) __attribute__((amdgpu_waves_p
     };
     BatchIn nx;
     fetch(0, nx);
-#if SFM_SCHUR_PRE_WAIT
     // The first batch's loads complete before the loop.  Without this the
     // waitcnt pass merges the loop entry (loads pending in the registers the
     // loop body reads) with the back edge and waits on the counter inside
     // phase A of EVERY batch -- which, the counter being in order, also waits
     // for the next batch's prefetch, so its HBM latency was never hidden.
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-#endif
     for (int p0 = 0; p0 < np;) {
         const int npts = nx.npts;   // batch [p0, p1)
         if (npts == 0) break;   // a point above SO observations: excluded by the planner
@@ -1683,17 +1644,9 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
 // and y_F are staged in LDS once, so the per-observation work gathers only the
 // measurement.
 // ---------------------------------------------------------------------------
-#ifndef SFM_STEP_PREFETCH   // A/B knob: the next observation's (slot, uv) loaded one ahead
-#define SFM_STEP_PREFETCH 1
-#endif
-#ifdef SFM_STEP_WPE   // A/B knob: waves per SIMD the step kernel is compiled for
-#define SFM_STEP_ATTR __attribute__((amdgpu_waves_per_eu(SFM_STEP_WPE, SFM_STEP_WPE)))
-#else
-#define SFM_STEP_ATTR
-#endif
 constexpr int kStepThreads = 256;
 template <int CM, int SPLIT>
-__global__ __launch_bounds__(kStepThreads) SFM_STEP_ATTR void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
+__global__ __launch_bounds__(kStepThreads) void step_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
                                                          const CamPre* __restrict__ cps_c,
                                                          const double* __restrict__ intr_c,
@@ -1741,22 +1694,15 @@ __global__ __launch_bounds__(kStepThreads) SFM_STEP_ATTR void step_kernel(DevPro
         double sqf = 0.0, sqq = 0.0;
         const int o0 = P.pt_off[p] + sub, o1 = P.pt_off[p + 1];
         // the next observation's (slot, uv) is loaded while this one is linearised
-#if SFM_STEP_PREFETCH
         int nslot = o0 < o1 ? P.obs_slot[o0] : 0;
         double2 nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
-#endif
         for (int o = o0; o < o1; o += SPLIT) {
-#if SFM_STEP_PREFETCH
             const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = nuv;
             if (o + SPLIT < o1) {
                 nslot = P.obs_slot[o + SPLIT];
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + SPLIT];
             }
-#else
-            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
-            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-#endif
             LinT<CM> L;
             linearize<CM, true, true, true>(scp[cs], &isy[is][0], Xp, uv.x, uv.y, P.huber_a, L);
             // (a ChunkDesc read: an LDS copy of the flag measured 8 % slower,
@@ -1829,22 +1775,15 @@ __global__ __launch_bounds__(kStepThreads) SFM_STEP_ATTR void step_kernel(DevPro
         }
         if (sub != 0) acc[0] = acc[2] = 0.0;   // one lane of the group carries the point's terms
         // candidate residuals at (x_c, candidate cameras / intrinsics)
-#if SFM_STEP_PREFETCH
         nslot = o0 < o1 ? P.obs_slot[o0] : 0;
         nuv = o0 < o1 ? reinterpret_cast<const double2*>(P.obs_uv)[o0] : double2{0.0, 0.0};
-#endif
         for (int o = o0; o < o1; o += SPLIT) {
-#if SFM_STEP_PREFETCH
             const int slot = nslot, cs = slot & 255, is = (slot >> 8) & 255;
             const double2 uv = nuv;
             if (o + SPLIT < o1) {
                 nslot = P.obs_slot[o + SPLIT];
                 nuv = reinterpret_cast<const double2*>(P.obs_uv)[o + SPLIT];
             }
-#else
-            const int slot = P.obs_slot[o], cs = slot & 255, is = (slot >> 8) & 255;
-            const double2 uv = reinterpret_cast<const double2*>(P.obs_uv)[o];
-#endif
             LinT<CM> C;
             linearize<CM, false, false, false>(scc[cs], &isy[is][IW], xc, uv.x, uv.y, P.huber_a, C);
             acc[1] += C.half_rho;
@@ -2262,10 +2201,7 @@ constexpr int kLongPTerms = 64;
 // doubles per term (36 lanes x 6 scattered 8-byte loads per term made the
 // reduce address-bound).  Rows are padded to 4 doubles in LDS (two 16-byte
 // reads per 3-vector).  ra / rb: rows of the a / b block (b = w: 1 row).
-#ifndef SFM_PTB   // terms per staged batch of the product-term reduce
-#define SFM_PTB 16
-#endif
-constexpr int kPtB = SFM_PTB;
+constexpr int kPtB = 16;   // terms per staged batch of the product-term reduce
 constexpr int kPtLds = kPtB * 12 * 4 + 2 * kPtB;   // doubles of LDS per wave (<= 6 + 6 rows per term, the terms)
 __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb, int G, int g, int r, int cc,
                                             int ra, int rb, double* lds) {
@@ -2695,10 +2631,10 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
                                                dim3(P.n_group), dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
     } else {
         if (scale_e)
-            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO, true>),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, kSubPts, kSubObs, true>),
                                                dim3(P.n_group), dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
         else
-            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, SFM_SCHUR5_SP, SFM_SCHUR5_SO>), dim3(P.n_group),
+            SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((schur_kernel<CM, 5, kSubPts, kSubObs>), dim3(P.n_group),
                                                dim3(64 * schur_group(P.tile_nt)), 0, s, P, cp, intr, X, radius, stamps));
     }
     SFM_HIP(hipGetLastError());
@@ -2707,7 +2643,7 @@ void ba_schur(const DevProblem& P, const CamPre* cp, const double* intr, const d
 void ba_reduce(const DevProblem& P, bool vectors_only, hipStream_t s) {
     if (P.n_targets <= 0 && P.n_zero <= 0) return;
     const int per_block = 4 / P.red_waves, nb = (P.n_targets + per_block - 1) / per_block;
-    const bool split = std::getenv("SFM_REDUCE_SPLIT") != nullptr;   // A/B and tests: three launches
+    const bool split = P.red_split != 0;   // SFM_CTX_BA_SPLIT_REDUCE: three launches
     const int nz = (P.n_zero + 15) / 16;   // zero-list workgroups, last in the grid
     if (P.n_long > 0 && !split) {
         hipLaunchKernelGGL(reduce_kernel<true>, dim3(nb + P.n_lseg + nz), dim3(256), 0, s, P, vectors_only ? 1 : 0,

@@ -202,8 +202,7 @@ std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, i
     // keeps the RCS dense under any order), and the co-visibility graph is
     // small enough to build quickly
     tm.mark("bandwidth");
-    if (D > kBandMaxD && lb <= kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20 &&
-        !std::getenv("SFM_BA_NO_RCM")) {
+    if (D > kBandMaxD && lb <= kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20) {
         const std::vector<int32_t> pos = rcm_order(P, cam_blk, ncam);
         tm.mark("rcm");
         std::vector<int32_t> alt(cam_blk);
@@ -362,7 +361,7 @@ bool chunkable(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t p) {
 
 }  // namespace
 
-void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
+void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, const PlanOpts& opts) {
     SFM_REQUIRE(P.n_img >= 1 && P.n_intr >= 1 && P.n_pt >= 0 && P.n_obs >= 0 &&
                     P.pt_offsets && (P.n_obs == 0 || (P.obs_img && P.obs_uv)) && P.img_intr,
                 SFM_ERR_INVALID_ARG, "incomplete BA problem");
@@ -406,7 +405,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // (the band solver's arrow holds 4-wide intrinsics blocks: RADIAL3 is dense)
     // (the BCR arrow carries iw * nintr <= 16 bordered columns: one MFMA column
     // tile besides the rhs, and a corner system of at most 16 x 16)
-    pl.dense = !(pl.D <= kBandMaxD && pl.iw * pl.nintr <= 16) || std::getenv("SFM_BA_DENSE") != nullptr;
+    pl.dense = !(pl.D <= kBandMaxD && pl.iw * pl.nintr <= 16) || opts.force_dense;
     if (pl.dense) {
         SFM_REQUIRE(pl.nF <= 40000, SFM_ERR_UNSUPPORTED, "dense reduced camera system of %lld columns",
                     (long long)pl.nF);
@@ -470,7 +469,6 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     // at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128).
     constexpr int64_t kTargetChunks = 1600;
     int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
-    if (const char* e = std::getenv("SFM_BA_CHUNK_PTS")) chunk_pts = std::max(1, std::min(kChunkPts, std::atoi(e)));   // tuning override
     // Chunks of one tile group share one slot layout and one tile: the Schur
     // kernel runs a group as one workgroup, a wave per chunk, and adds the
     // waves' tiles in LDS (wave order) before the one write -- a quarter of the
@@ -619,8 +617,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         n_closed = 0;
         abandoned = false;
         abort_at = limit;
-        int gw = schur_group(cap == 64 ? 4 : 5);
-        if (const char* e = std::getenv("SFM_BA_TILE_GROUP")) gw = std::max(1, std::min(gw, std::atoi(e)));   // diagnostic
+        const int gw = schur_group(cap == 64 ? 4 : 5);
         group_pts = gw * chunk_pts;
         slot_out.reserve(pl.n_sobs);        // (grown to every observation once kept, in place)
         slot_out.resize(pl.pt_off[ncp]);   // every entry written by its range
@@ -681,7 +678,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
     const int64_t keep_max = pl.n_cpt / 4;
     bool kept = true;
     // the 64-row kernel walks batches of at most schur4_obs observations
-    if (max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !std::getenv("SFM_BA_TILE80")) {
+    if (max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !opts.tile80) {
         // both tile heights are planned (each over the host threads); the
         // 64-row one is taken unless it needs 5/4 as many chunks.  80 rows
         // over keep_max: dropped if taken, so 64 rows matter only within
@@ -888,8 +885,6 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl) {
         const int64_t seen = (int64_t)pl.gram_img.size();
         const int64_t avg = seen > 0 ? pl.n_sobs / seen : 0;
         pl.gram_seg = std::min<int32_t>(kGramSeg, avg >= 1600 ? 3 : avg >= 128 ? 2 : 1);
-        if (const char* e = std::getenv("SFM_GRAM_SEG"))
-            pl.gram_seg = std::min(kGramSeg, std::max(1, std::atoi(e)));
     }
     tm.mark("image_csr");
     // ---- reduce plan -----------------------------------------------------------

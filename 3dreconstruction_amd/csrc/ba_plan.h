@@ -84,8 +84,15 @@ struct BAHostPlan {
     int64_t schur_bytes = 0;    // algorithmic HBM bytes of one Schur pass
 };
 
+// Engine choices the planner takes from the context (SFM_CTX_BA_*): the
+// dense RCS for a narrow band, 80-row Schur tiles for every chunk.
+struct PlanOpts {
+    bool force_dense = false;
+    bool tile80 = false;
+};
+
 // Validates the problem and fills every field.  Throws SfmError.
-void build_plan(const sfm_ba_problem& prob, int rank, int world, BAHostPlan& plan);
+void build_plan(const sfm_ba_problem& prob, int rank, int world, BAHostPlan& plan, const PlanOpts& opts = {});
 
 // Every point's active camera span [lo, hi) under a camera order ((ncam, 0):
 // no active camera): the partition's sort keys.

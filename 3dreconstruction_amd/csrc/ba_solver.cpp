@@ -137,7 +137,10 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         up(pl->obs_slot, hp.obs_slot, s);
         up(pl->obs_uv, hp.obs_uv, s);
     };
-    build_plan(prob, ctx->rank, ctx->world, h);
+    PlanOpts po;
+    po.force_dense = (ctx->flags & SFM_CTX_BA_DENSE_RCS) != 0;
+    po.tile80 = (ctx->flags & SFM_CTX_BA_TILE80) != 0;
+    build_plan(prob, ctx->rank, ctx->world, h, po);
     h.on_shard_ready = nullptr;
     tm.mark("build_plan");
     Staging st;
@@ -239,13 +242,9 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         // step_kernel lanes per point: two (profiles/r04/l_split: C4 1062-1067
         // / 1076-1078 LM-iters/s with 1 / 2, rank 0 of N = 8 2145-2148 / 2191-
         // 2198 / 2175-2177 / 2128 with 1 / 2 / 4 / 8; adjacent lanes read
-        // adjacent observations).  SFM_STEP_SPLIT overrides (A/B, tests); the
-        // longest chunk must fit the kernel's 256 threads
-        int sp = 2;
-        if (const char* e = std::getenv("SFM_STEP_SPLIT")) {
-            const int f = std::atoi(e);
-            if (f == 1 || f == 2 || f == 4 || f == 8) sp = f;
-        }
+        // adjacent observations).  SFM_CTX_BA_STEP_LANES overrides (A/B,
+        // tests); the longest chunk must fit the kernel's 256 threads
+        int sp = ctx->step_lanes() ? ctx->step_lanes() : 2;
         while (sp > 1 && P.chunk_pts_max * sp > 256) sp /= 2;
         P.step_split = sp;
     }
@@ -278,18 +277,15 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         // targets it sums: C4 24 at N = 1, 50 at N = 4, 92 at N = 8
         // (profiles/r04/m_redw: N = 1 1072 / 1063 / 1046 LM-iters/s with 1 / 2
         // / 4 waves, rank 0 of N = 8 2123-2132 / 2215-2226 / 2244-2245;
-        // SFM_REDUCE_WAVES overrides, A/B only)
+        // SFM_CTX_BA_REDUCE_WAVES overrides: A/B, tests)
         int64_t nt = 0, nterm = 0;
         for (const ReduceTarget& T : h.targets) {
             const int32_t n = T.c_end - T.c_begin;
             if (n <= reduce_long_threshold()) { ++nt; nterm += n; }
         }
         const int64_t mean = nt > 0 ? nterm / nt : 0;
-        P.red_waves = mean >= 80 ? 4 : mean >= 40 ? 2 : 1;
-        if (const char* e = std::getenv("SFM_REDUCE_WAVES")) {
-            const int w = std::atoi(e);
-            if (w == 1 || w == 2 || w == 4) P.red_waves = w;
-        }
+        P.red_waves = ctx->reduce_waves() ? ctx->reduce_waves() : mean >= 80 ? 4 : mean >= 40 ? 2 : 1;
+        P.red_split = (ctx->flags & SFM_CTX_BA_SPLIT_REDUCE) ? 1 : 0;
     }
     {
         // long targets: [n_long targets | n_long+1 segment offsets | n_seg (long idx, term begin)]
@@ -368,11 +364,12 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->part_f.alloc(3 * (size_t)P.n_fblk);
     P.part_f = pl->part_f.p;
     P.scal = pl->scal.p;
-    // (SFM_BA_BAND_SOLVER: the sequential band solver, 4-wide intrinsics arrows only)
-    pl->use_bcr = !h.dense && bcr_supported(P) && (std::getenv("SFM_BA_BAND_SOLVER") == nullptr || P.iw != 4);
+    // (SFM_CTX_BA_SEQ_BAND: the sequential band solver, 4-wide intrinsics arrows only)
+    pl->use_bcr = !h.dense && bcr_supported(P) && (!(ctx->flags & SFM_CTX_BA_SEQ_BAND) || P.iw != 4);
     SFM_REQUIRE(h.dense || pl->use_bcr || P.iw == 4, SFM_ERR_UNSUPPORTED, "band solver: 4-wide intrinsics only");
     if (h.dense) {
         dense_setup(pl->dense, P);
+        pl->dense.chain = (ctx->flags & SFM_CTX_BA_DENSE_CHAIN) != 0;
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
         SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * dense_flag_words(pl->dense), s));
@@ -384,6 +381,7 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     }
     if (pl->use_bcr) {
         bcr_setup(pl->bcr, P);
+        pl->bcr.split = (ctx->flags & SFM_CTX_BA_SPLIT_BCR) != 0;
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
         bcr_bind(pl->bcr, pl->bcr_buf.p);
         SFM_HIP(hipMemsetAsync(pl->bcr.yflag, 0, sizeof(unsigned) * (size_t)pl->bcr.N, s));
@@ -508,7 +506,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     ba_fill(pl->scaleE.p, (int64_t)nx, 1.0, s);
     if (O.jacobi_scaling) {
         relinearize();                 // unscaled column norms of the F blocks
-        if (ctx->world > 1 && (h.dense || std::getenv("SFM_RCS_FILL")))
+        if (ctx->world > 1 && h.dense)
             ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // dense: its targets are this shard's blocks only
         ba_reduce(P, true, s);
         allreduce_rcs();
@@ -561,7 +559,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(ev[1], s));
         // across ranks each shard writes only the blocks its own points touch,
         // so the summed system of the last iteration is cleared first
-        if (ctx->world > 1 && (h.dense || std::getenv("SFM_RCS_FILL")))
+        if (ctx->world > 1 && h.dense)
             ba_fill(pl->rcs.p, (int64_t)pl->rcs_n, 0.0, s);   // dense: its targets are this shard's blocks only
         ba_reduce(P, false, s);
         allreduce_rcs();
@@ -816,6 +814,8 @@ extern "C" int sfm_ba_plan_get_info(sfm_ba_plan* pl, sfm_ba_plan_info* info) {
         info->schur_flops_per_iter = h.schur_flops;
         info->schur_launches = pl->schur_launches;
         info->schur_ms_total = pl->schur_ms_total;
+        info->rcs_solver = h.dense ? SFM_RCS_DENSE : pl->use_bcr ? SFM_RCS_BCR : SFM_RCS_SEQ_BAND;
+        info->tile_rows = 16 * h.tile_nt;
         return SFM_OK;
     });
 }

@@ -43,15 +43,10 @@ constexpr int kGroupChunks = 4;           // chunks per tile group, at most (the
 // the reduce kernels from 39 to 27 us per iteration at C4, but the Schur
 // launch went 0.339 -> 0.368 ms (a group's waves finish together and hold
 // its LDS until the slowest is done): C4 1041 vs 1048 LM-iters/s on one box
-// (profiles/r04/c_jit/ab.txt).  -DSFM_SCHUR_GROUP=4 builds the grouped form.
-#ifndef SFM_SCHUR_GROUP   // A/B builds: chunks per group of 64-row tiles
-#define SFM_SCHUR_GROUP 1
-#endif
-constexpr int schur_group(int tile_nt) { return tile_nt == 4 ? SFM_SCHUR_GROUP : 1; }
-#ifndef SFM_GRAM_SEG_MAX   // A/B builds: the most image Gram workgroups per image (buffer stride)
-#define SFM_GRAM_SEG_MAX 3
-#endif
-constexpr int kGramSeg = SFM_GRAM_SEG_MAX;   // workgroups per image in the image Gram pass (at most)
+// (profiles/r04/c_jit/ab.txt).  The group machinery stays (a group of one
+// chunk is the shipped form); the grouped form was an A/B build, not kept.
+constexpr int schur_group(int) { return 1; }
+constexpr int kGramSeg = 3;   // workgroups per image in the image Gram pass (at most)
 constexpr int kMaxSlots = 16;             // F slots (row-carrying cameras + intrinsics)
 constexpr int kCamSlots = 14;             // staged cameras per chunk (incl. constant images)
 constexpr int kIntrSlots = 4;             // staged intrinsics blocks per chunk

@@ -218,6 +218,17 @@ struct sfm_ctx {
     bool no_exchange = false;                    // SFM_CTX_DIAG_NO_EXCHANGE (per-rank timing only)
     bool fail_solve_wait = false;                // SFM_CTX_DIAG_FAIL_SOLVE_WAIT (error-path tests)
     bool time_kernels = false;                   // SFM_CTX_TIME_KERNELS (sfm_ctx_last_kernel_ms)
+    int32_t flags = 0;                           // sfm_ctx_opts.flags (the SFM_CTX_BA_* engine shape)
+    // engine shape decoded from the flags: lanes per point in the step pass,
+    // waves per reduce target (0: the plan chooses)
+    int step_lanes() const {
+        const int v = (flags >> 12) & 7;
+        return v ? 1 << (v - 1) : 0;
+    }
+    int reduce_waves() const {
+        const int v = (flags >> 15) & 7;
+        return v ? 1 << (v - 1) : 0;
+    }
     hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
     double last_kernel_ms = -1.0;                // sfm_fmatrix_ac's kernel (sfm_ctx_last_kernel_ms)
 };

@@ -308,7 +308,7 @@ namespace {
 // threshold with mmap / munmap; the threshold at its maximum (32 MiB on
 // 64-bit: glibc rejects anything above HEAP_MAX_SIZE / 2) and a large trim
 // threshold keep freed blocks in the heap for reuse instead.  Opt-in
-// (SFM_CTX_TUNE_HOST_MALLOC or SFM_TUNE_MALLOC=1), once per process: a
+// (SFM_CTX_TUNE_HOST_MALLOC), once per process: a
 // long-running host application keeps its own malloc settings by default.
 void tune_host_malloc() {
     static std::once_flag once;
@@ -326,6 +326,8 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         SFM_REQUIRE(opts->world_size >= 1 && opts->rank >= 0 && opts->rank < opts->world_size,
                     SFM_ERR_INVALID_ARG, "bad rank %d / world_size %d", opts->rank,
                     opts->world_size);
+        SFM_REQUIRE(((opts->flags >> 12) & 7) <= 4 && ((opts->flags >> 15) & 7) <= 3, SFM_ERR_INVALID_ARG,
+                    "bad SFM_CTX_BA_STEP_LANES / SFM_CTX_BA_REDUCE_WAVES field");
         int ndev = 0;
         hipError_t e = hipGetDeviceCount(&ndev);
         SFM_REQUIRE(e == hipSuccess && ndev > 0, SFM_ERR_DEVICE, "no HIP device available (%s)",
@@ -337,7 +339,7 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         SFM_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, SFM_ERR_DEVICE,
                     "device %d is %s; this build targets gfx950 (MI355X) only", opts->device,
                     prop.gcnArchName);
-        if ((opts->flags & SFM_CTX_TUNE_HOST_MALLOC) || std::getenv("SFM_TUNE_MALLOC")) tune_host_malloc();
+        if (opts->flags & SFM_CTX_TUNE_HOST_MALLOC) tune_host_malloc();
         auto* c = new sfm_ctx;
         c->device = opts->device;
         c->rank = opts->rank;
@@ -345,6 +347,7 @@ extern "C" int sfm_ctx_create(const sfm_ctx_opts* opts, sfm_ctx** out) {
         c->cu_count = prop.multiProcessorCount;
         c->fail_solve_wait = (opts->flags & SFM_CTX_DIAG_FAIL_SOLVE_WAIT) != 0;
         c->time_kernels = (opts->flags & SFM_CTX_TIME_KERNELS) != 0;
+        c->flags = opts->flags;
         SFM_HIP(hipSetDevice(c->device));
         SFM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         {

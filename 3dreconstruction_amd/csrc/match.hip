@@ -10,8 +10,8 @@
 //     a' = a - 128 (translation keeps |a-b|^2) with |a'|^2 per row, so the
 //     distance matrix is an exact integer contraction on the i8 MFMA
 //     (v_mfma_i32_32x32x32_i8, int32 accumulate): |a'|^2+|b'|^2-2a'.b'.
-//   * one workgroup = 4 waves = 4 x 32 MATCH_CT queries of image J against all of image I;
-//     each wave keeps its 32 MATCH_CT queries' B fragments in VGPRs and streams the
+//   * one workgroup = 4 waves of kCT x 32 queries of image J against all of image I;
+//     each wave keeps its kCT x 32 queries' B fragments in VGPRs and streams the
 //     database in 32-row MFMA tiles; the C tile has the database row on the
 //     registers and the query on the lane, so the top-2 update is lane-local:
 //     key = ((|d'|^2 << 8) | row&255) - 512 * dot, two keys x, y per update:
@@ -40,51 +40,23 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-#ifndef MATCH_CT
-#define MATCH_CT 4                 // 32-query column tiles per wave (even; 4: 200 VGPRs, 2 waves/SIMD)
-#endif
-#ifndef MATCH_PP
-// Ping-pong (A/B knob): 8 waves per workgroup, waves w and w + 4 share a SIMD
-// and run half a tile apart -- one group issues its MFMAs while the other
-// runs its top-2 epilogue, swapped at every workgroup barrier, so the
-// matrix core and the VALU of a SIMD work at the same time instead of both
-// co-resident waves alternating in phase.
-#define MATCH_PP 0
-#endif
-constexpr int kWaves = MATCH_PP ? 8 : 4;   // waves per workgroup
+constexpr int kWaves = 4;          // waves per workgroup
 constexpr int kThreads = 64 * kWaves;
-constexpr int kCT = MATCH_CT;
-static_assert(kCT % 2 == 0 && kCT >= 2, "MATCH_CT must be even: the epilogue walks column tiles in pairs");
+constexpr int kCT = 4;             // 32-query column tiles per wave (even; 4: 200 VGPRs, 2 waves/SIMD)
+static_assert(kCT % 2 == 0 && kCT >= 2, "the epilogue walks column tiles in pairs");
 constexpr int kQW = 32 * kCT;      // queries per wave
 constexpr int kQB = kWaves * kQW;  // queries per workgroup
 constexpr int kRowPad = kQB > 256 ? kQB : 256;  // rows of every image padded to this multiple
-#ifndef MATCH_STAGE
-#define MATCH_STAGE 128            // database rows per LDS stage (A/B knob)
-#endif
-constexpr int kStage = MATCH_STAGE;   // database rows per LDS stage (kRowPad multiple of it)
+constexpr int kStage = 128;        // database rows per LDS stage (kRowPad multiple of it)
 static_assert(kStage == 128 || kStage == 256, "merge windows are 256 rows");
 #ifndef MATCH_TILE_UNROLL
-#define MATCH_TILE_UNROLL 1        // tile-loop unroll (A/B builds only)
+#define MATCH_TILE_UNROLL 1        // tile-loop unroll (tests/test_match_isa.py builds 1 and 2)
 #endif
-#ifndef MATCH_SPLIT
-// The two stage buffers as separate LDS objects, the stage loop unrolled by
-// two so every fragment read names one of them: the waitcnt pass can then
-// tell that the reads of stage st do not alias the LDS-DMA writes of stage
-// st+1 and stops waiting for those (vmcnt(0) at the tile loop's head, which
-// exposed every stage's load latency: the double buffer did not overlap).
-#define MATCH_SPLIT 1
-#endif
-#ifndef MATCH_PIPE
-// software-pipelined tile loop (two accumulator sets; A/B knob).  Measured on
-// C3 (tools/gpurun/match_ab.sh, profiles/r03/a_match_pipe): 2 column tiles at
-// 2 waves/SIMD 472 k pairs/s, 4 column tiles at 1 wave/SIMD 366 k, against
-// 504 k for the plain loop -- two co-resident waves already overlap one
-// wave's epilogue with the other's MFMAs, so it is off.
-#define MATCH_PIPE 0
-#endif
-#ifndef MATCH_WAVES_PER_EU
-#define MATCH_WAVES_PER_EU 2           // waves per SIMD the register budget targets
-#endif
+// Measured and not kept (the code is in git history):
+// a software-pipelined tile loop (two accumulator sets), 8-wave ping-pong
+// workgroups (waves w and w + 4 half a tile apart), 256-row stages, one
+// [2][...] stage array (the waitcnt pass then waited for the next stage's
+// LDS DMA at every tile loop head).
 
 // u8 -> int8 (a ^ 0x80 == a - 128), per-row |a'|^2 and the packed key base.
 __global__ void prep_kernel(uint8_t* __restrict__ d, int32_t* __restrict__ nrm,
@@ -171,7 +143,7 @@ struct MatchArgs {
 // kRatio = false (MUTUAL's two nearest-neighbour passes): only the nearest
 // key is tracked (min3 over two keys, 1.5 VALU per distance).
 template <bool kRatio>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MATCH_WAVES_PER_EU, MATCH_WAVES_PER_EU))) void match_top2_kernel(MatchArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void match_top2_kernel(MatchArgs a) {
     // XCD-aware bijective remap of the flat workgroup id (guide §5 T1):
     // blocks b and b+8 share an XCD, so give each XCD a contiguous range of
     // work items (pair-major, query block minor).
@@ -212,13 +184,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MATCH_
     // bank conflicts of the 32-rows-one-chunk fragment reads are removed by
     // storing logical 16-byte chunk k of row r at slot k ^ (r & 7) (the XOR is
     // applied to the global SOURCE address, and again on the read).
-#if MATCH_SPLIT
+    // The two stage buffers are separate LDS objects and the stage loop is
+    // unrolled by two, so every fragment read names one of them: the waitcnt
+    // pass can then tell that the reads of one stage do not alias the LDS-DMA
+    // writes of the next and does not wait for those at the tile loop's head.
     __shared__ __attribute__((aligned(16))) int8_t sA0[kStage * 128], sA1[kStage * 128];
     __shared__ __attribute__((aligned(16))) int32_t sN0[kStage], sN1[kStage];
-#else
-    __shared__ __attribute__((aligned(16))) int8_t sA[2][kStage * 128];
-    __shared__ __attribute__((aligned(16))) int32_t sN[2][kStage];
-#endif
     auto issue_to = [&](int8_t* dA, int32_t* dN, int row_base) {
 #pragma unroll
         for (int q = 0; q < kStage * 8 / kThreads; ++q) {
@@ -233,15 +204,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MATCH_
                 __builtin_amdgcn_global_load_lds(a.ntr + db_row0 + row_base + q * 64 + lane, dN + q * 64, 4, 0, 0);
         }
     };
-#if MATCH_SPLIT
-    auto issue = [&](int buf, int row_base) {
-        if (buf) issue_to(sA1, sN1, row_base);
-        else issue_to(sA0, sN0, row_base);
-    };
-#else
-    auto issue = [&](int buf, int row_base) { issue_to(sA[buf], sN[buf], row_base); };
-#endif
-
     // (256-row merge windows; the image rows are padded to kRowPad >= 256)
     const int n_db_pad = (n_db + 255) / 256 * 256;
     int b1[kCT], b2[kCT];
@@ -333,95 +295,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MATCH_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     };
-    if (n_db_pad > 0) issue(0, 0);
-#if MATCH_PIPE
-    // Software pipeline over the tiles: tile t's MFMAs are issued before the
-    // top-2 epilogue of tile t-1 (two accumulator sets, A for the even tiles of
-    // a stage, B for the odd ones), so the i8 MFMAs of one tile run under the
-    // VALU epilogue of the previous one inside each wave.  The epilogue of a
-    // stage's last tile runs at the head of the next stage, after its barrier.
-    static_assert(kStage % 64 == 0, "tiles go in A/B pairs");
-    v16i accA[kCT], accB[kCT];
-    v4i ntA[4], ntB[4];
-    bool pendB = false;              // accB holds a tile whose epilogue is pending
-    int merge_base = -1;             // a window merge pending after that epilogue
-    for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
-        stage_landed();    // stage st has landed in every wave's part; buffer st+1 is free
-        if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
-        const int8_t* A = sA[st & 1];
-        const int32_t* N = sN[st & 1];
-        for (int tile = 0; tile < kStage; tile += 64) {
-            v4i afA[4], afB[4];
-            load_frag(A, N, tile, afA, ntA);
-            mfma_tile(afA, accA);
-            if (pendB) epilogue(accB, ntB);
-            if (merge_base >= 0) {
-                merge_window(merge_base);
-                merge_base = -1;
-            }
-            load_frag(A, N, tile + 32, afB, ntB);
-            mfma_tile(afB, accB);
-            epilogue(accA, ntA);
-            pendB = true;
-        }
-        if (((sup + kStage) & 255) == 0) merge_base = sup + kStage - 256;
-    }
-    if (pendB) epilogue(accB, ntB);
-    if (merge_base >= 0) merge_window(merge_base);
-#elif MATCH_PP
-    // Phases separated by workgroup barriers; per tile, phase a: group 0
-    // (waves 0-3) loads and issues the tile's MFMAs while group 1 (waves 4-7)
-    // runs the epilogue of its previous tile; phase b: the reverse.  Every
-    // wave reaches every barrier (the branches are wave-uniform and hold no
-    // barrier).  A stage's first phase waits for its LDS DMA (each wave drains
-    // its own part, then the barrier) and issues the next stage into the
-    // other buffer, which group 1 finished reading in the previous phase.
-    // waves w and w + 4 share a SIMD (HW_ID probe, profiles/r04/n_pp/simd_probe.txt)
-    const bool g1 = wave >= 4;
-    v4i af[4], nt4[4];
-    v16i acc[kCT];
-    bool pend = false;      // group 1: a tile's epilogue is pending
-    int pend_merge = -1;    // group 1: a window merge pending after it
-    auto g1_epilogue = [&] {
-        if (!pend) return;
-        epilogue(acc, nt4);
-        pend = false;
-        if (pend_merge >= 0) { merge_window(pend_merge); pend_merge = -1; }
-    };
-    auto stage = [&](const int8_t* A, const int32_t* N, int8_t* nA, int32_t* nN, int sup) {
-        stage_landed();
-        if (sup + kStage < n_db_pad) issue_to(nA, nN, sup + kStage);
-        // (the phase barriers inside a stage order no memory -- the stage has
-        // landed -- so they are bare s_barrier: __syncthreads' fence would
-        // drain the next stage's DMA at each of them)
-        for (int tile = 0; tile < kStage; tile += 32) {
-            if (tile) __builtin_amdgcn_s_barrier();
-            if (g1) {
-                g1_epilogue();
-            } else {
-                load_frag(A, N, tile, af, nt4);
-                mfma_tile(af, acc);
-            }
-            __builtin_amdgcn_s_barrier();
-            if (g1) {
-                load_frag(A, N, tile, af, nt4);
-                mfma_tile(af, acc);
-                pend = true;
-            } else {
-                epilogue(acc, nt4);
-            }
-        }
-        if (((sup + kStage) & 255) == 0) {
-            if (g1) pend_merge = sup + kStage - 256;
-            else merge_window(sup + kStage - 256);
-        }
-    };
-    for (int sup = 0; sup < n_db_pad; sup += 2 * kStage) {
-        stage(sA0, sN0, sA1, sN1, sup);
-        if (sup + kStage < n_db_pad) stage(sA1, sN1, sA0, sN0, sup + kStage);
-    }
-    if (g1) g1_epilogue();
-#elif MATCH_SPLIT
+    if (n_db_pad > 0) issue_to(sA0, sN0, 0);
     // one stage: its tiles from (A, N) while the next stage lands in (nA, nN)
     auto stage = [&](const int8_t* A, const int32_t* N, int8_t* nA, int32_t* nN, int sup) {
         stage_landed();    // this stage has landed in every wave's part; the other buffer is free
@@ -440,23 +314,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(MATCH_
         stage(sA0, sN0, sA1, sN1, sup);
         if (sup + kStage < n_db_pad) stage(sA1, sN1, sA0, sN0, sup + kStage);
     }
-#else
-    for (int sup = 0, st = 0; sup < n_db_pad; sup += kStage, ++st) {
-        stage_landed();    // stage st has landed in every wave's part; buffer st+1 is free
-        if (sup + kStage < n_db_pad) issue((st + 1) & 1, sup + kStage);
-        const int8_t* A = sA[st & 1];
-        const int32_t* N = sN[st & 1];
-#pragma unroll MATCH_TILE_UNROLL
-        for (int tile = 0; tile < kStage; tile += 32) {
-            v4i af[4], nt4[4];
-            load_frag(A, N, tile, af, nt4);
-            v16i acc[kCT];
-            mfma_tile(af, acc);
-            epilogue(acc, nt4);
-        }
-        if (((sup + kStage) & 255) == 0) merge_window(sup + kStage - 256);
-    }
-#endif
 
 #pragma unroll
     for (int t = 0; t < kCT; ++t) {

@@ -75,8 +75,7 @@ typedef struct sfm_ctx_opts {
     void* allreduce_user;
 } sfm_ctx_opts;
 
-/* sfm_ctx_opts.flags.  SFM_CTX_TUNE_HOST_MALLOC (opt-in; the environment
- * variable SFM_TUNE_MALLOC=1 has the same effect): keep freed host memory in
+/* sfm_ctx_opts.flags.  SFM_CTX_TUNE_HOST_MALLOC (opt-in): keep freed host memory in
  * the process heap (glibc M_MMAP_THRESHOLD at its 32 MiB maximum, and
  * M_TRIM_THRESHOLD).  Unmapping a large host buffer stalls the process's next
  * GPU operation for 10-30 ms while the driver invalidates its mappings, which
@@ -101,6 +100,33 @@ typedef struct sfm_ctx_opts {
  * alone.  Off by default: the extra stream synchronisation and event pair are
  * not part of the filter's production path. */
 #define SFM_CTX_TIME_KERNELS 8
+/* BA engine shape (A/B measurement and tests; 0 = the measured defaults).
+ * Every alternative is exact: the launch-shape bits and the per-point /
+ * per-target lane counts change only how the same sums are launched
+ * (bit-identical results, or sums in another fixed order), the solver bits
+ * pick the other direct solver of the same reduced camera system.  They are
+ * read when a plan is created (sfm_ba_plan_create, sfm_ba_solve); there are
+ * no environment switches for any of them.
+ *   SFM_CTX_BA_DENSE_RCS     blocked dense Cholesky even for a narrow band
+ *   SFM_CTX_BA_SEQ_BAND      the sequential block-band solver instead of
+ *                            cyclic reduction (4-wide intrinsics arrows)
+ *   SFM_CTX_BA_TILE80        80-row Schur tiles for every chunk
+ *   SFM_CTX_BA_SPLIT_REDUCE  the RCS reduction in three launches (short
+ *                            targets, long-target segments, their combine)
+ *   SFM_CTX_BA_SPLIT_BCR     cyclic reduction's top, corner and every
+ *                            back-substitution level as separate launches
+ *   SFM_CTX_BA_DENSE_CHAIN   the dense factorisation and back substitution
+ *                            as launch chains instead of dataflow kernels
+ *   SFM_CTX_BA_STEP_LANES(n) n = 1, 2, 4, 8 lanes per point in the step pass
+ *   SFM_CTX_BA_REDUCE_WAVES(n) n = 1, 2, 4 waves per reduce target */
+#define SFM_CTX_BA_DENSE_RCS      (1 << 4)
+#define SFM_CTX_BA_SEQ_BAND       (1 << 5)
+#define SFM_CTX_BA_TILE80         (1 << 6)
+#define SFM_CTX_BA_SPLIT_REDUCE   (1 << 7)
+#define SFM_CTX_BA_SPLIT_BCR      (1 << 8)
+#define SFM_CTX_BA_DENSE_CHAIN    (1 << 9)
+#define SFM_CTX_BA_STEP_LANES(n)  (((n) == 8 ? 4 : (n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 0) << 12)
+#define SFM_CTX_BA_REDUCE_WAVES(n) (((n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 0) << 15)
 
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
 int sfm_comm_unique_id(uint8_t* out128);
@@ -255,7 +281,13 @@ typedef struct sfm_ba_plan_info {
     int64_t schur_flops_per_iter;           /* algorithmic flops, Schur kernel*/
     int64_t schur_launches;                 /* Schur launches in last run     */
     double  schur_ms_total;                 /* summed Schur kernel time        */
+    int32_t rcs_solver;                     /* SFM_RCS_* the plan solves with  */
+    int32_t tile_rows;                      /* Schur chunk tile height (64/80) */
 } sfm_ba_plan_info;
+/* sfm_ba_plan_info.rcs_solver */
+#define SFM_RCS_BCR       0   /* block cyclic reduction of the band + arrow   */
+#define SFM_RCS_DENSE     1   /* blocked dense Cholesky                      */
+#define SFM_RCS_SEQ_BAND  2   /* sequential block-band Cholesky              */
 int sfm_ba_plan_get_info(sfm_ba_plan* plan, sfm_ba_plan_info* info);
 /* Iteration log of the last sfm_ba_plan_run (n <= cap entries written). */
 int sfm_ba_plan_get_trace(sfm_ba_plan* plan, sfm_ba_iter* out, int32_t cap, int32_t* n);

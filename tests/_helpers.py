@@ -265,3 +265,20 @@ def corrupted_sequence(seq, n, bad):
     imgs[bad] = {"kp": imgs[bad]["kp"], "prior": imgs[bad]["prior"],
                  "desc": np.resize(o["desc"], imgs[bad]["desc"].shape)}
     return imgs
+
+
+class engine_ctx:
+    """A context with SFM_CTX_BA_* engine-shape flags (include/sfmcore.h),
+    closed on exit: the alternative launch shapes and solvers are selected
+    per context, never through the environment."""
+
+    def __init__(self, flags=0, device=0):
+        self.flags, self.device = flags, device
+
+    def __enter__(self):
+        self.ctx = api.Context(self.device, flags=self.flags)
+        return self.ctx
+
+    def __exit__(self, *exc):
+        self.ctx.close()
+        return False

@@ -120,17 +120,17 @@ def test_mixed_chunks_and_long_tracks(ctx):
     _compare(ctx, sc)
 
 
-def test_dense_solver_matches_band_solver(ctx, monkeypatch):
+def test_dense_solver_matches_band_solver(ctx):
     sc = H.Scene(60, 6000, 8, n_intr=2, seed=31)
+    assert _shape(sc).dense == 0
     res = []
     for dense in (False, True):
-        if dense:
-            monkeypatch.setenv("SFM_BA_DENSE", "1")
-        assert _shape(sc).dense == (1 if dense else 0)
-        plan = api.BAPlan(ctx, sc.problem(), *sc.params())
-        _, s = plan.run()
-        res.append((s, plan.trace()))
-        plan.close()
+        with H.engine_ctx(abi.SFM_CTX_BA_DENSE_RCS if dense else 0) as c:
+            plan = api.BAPlan(c, sc.problem(), *sc.params())
+            assert plan.info().rcs_solver == (abi.SFM_RCS_DENSE if dense else abi.SFM_RCS_BCR)
+            _, s = plan.run()
+            res.append((s, plan.trace()))
+            plan.close()
     (s0, t0), (s1, t1) = res
     assert s0.iterations == s1.iterations
     assert [t.step_is_successful for t in t0] == [t.step_is_successful for t in t1]
@@ -168,3 +168,69 @@ def test_very_long_track(ctx):
     sh = _shape(sc)
     assert sh.n_general_pts == 12 and sh.dense == 1
     _compare(ctx, sc)
+
+
+@pytest.mark.parametrize("chain", [True, False])
+def test_dense_solve_under_contention(chain):
+    """the dense RCS solved while another context keeps the
+    CUs busy.  A second context on its own stream runs back-to-back matcher
+    launches (~14k workgroups of 256 threads each), so the solve's kernels are
+    dispatched into a chip that is already full and their workgroups start
+    late and out of step -- the condition under which dense_panel_kernel's
+    former store of L_kk over A_kk (round 4) corrupted the
+    panels of late workgroups, and under which the dataflow kernels
+    (dense_flow_kernel, dense_back_all_kernel) wait for workgroups that are
+    not resident yet.  chain: the launch chain (panel + trailing-update
+    launches); else the dataflow kernels.  Both must take the oracle's
+    decisions, with the matcher provably running during the solves."""
+    import threading
+    sc = H.Scene(100, 12000, 8, vis_mode=1, seed=2718)   # random visibility: dense RCS, 10 block columns
+    _, os_, otr, _ = H.oracle_solve(sc, threads=8)
+    desc = api.synth_descriptors(60, 4096)
+    off = np.arange(61, dtype=np.int64) * 4096
+    pairs = api.exhaustive_pairs(60)
+    stop, started = threading.Event(), threading.Event()
+    runs = {"n": 0, "during": 0, "err": None}
+    solving = threading.Event()
+
+    def matcher():
+        try:
+            c2 = api.Context(0)
+            mp = api.MatchPlan(c2, desc, off)
+            while not stop.is_set():
+                mp.run(pairs, count=True)   # returns after the launch completes
+                runs["n"] += 1
+                if solving.is_set():
+                    runs["during"] += 1
+                started.set()
+            mp.close()
+            c2.close()
+        except Exception as ex:  # reported by the main thread
+            runs["err"] = ex
+            started.set()
+
+    th = threading.Thread(target=matcher)
+    th.start()
+    try:
+        assert started.wait(120) and runs["err"] is None, runs["err"]
+        flags = abi.SFM_CTX_BA_DENSE_RCS | (abi.SFM_CTX_BA_DENSE_CHAIN if chain else 0)
+        with H.engine_ctx(flags) as c:
+            for rep in range(3):
+                plan = api.BAPlan(c, sc.problem(), *sc.params())
+                assert plan.info().rcs_solver == abi.SFM_RCS_DENSE
+                solving.set()
+                rc, gs = plan.run()
+                solving.clear()
+                tr = plan.trace()
+                plan.close()
+                assert rc == 0, abi.load().sfm_last_error()
+                assert (gs.iterations, gs.successful_steps) == (os_.iterations, os_.successful_steps), rep
+                assert [t.step_is_successful for t in tr] == [t.step_is_successful for t in otr]
+                for g, o in zip(tr, otr):
+                    assert abs(g.cost / o.cost - 1) < 1e-9
+                assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
+    finally:
+        stop.set()
+        th.join(300)
+    assert runs["err"] is None, runs["err"]
+    assert runs["during"] >= 1, runs   # the matcher ran while the solves did

@@ -74,13 +74,15 @@ def test_trace_matches(ctx):
 
 
 @pytest.mark.parametrize("tile80", [False, True])
-def test_chunk_tile_heights(ctx, monkeypatch, tile80):
+def test_chunk_tile_heights(ctx, tile80):
     # 64-row chunk tiles (4x4 MFMA tiles, -Zw on the VALU) are the default when
-    # every track fits 64 F rows; SFM_BA_TILE80 forces the 80-row form.
-    if tile80:
-        monkeypatch.setenv("SFM_BA_TILE80", "1")
+    # every track fits 64 F rows; SFM_CTX_BA_TILE80 forces the 80-row form.
     sc = H.Scene(24, 3000, 8, seed=17)
-    _compare(ctx, sc)
+    with H.engine_ctx(abi.SFM_CTX_BA_TILE80 if tile80 else 0) as c:
+        plan = api.BAPlan(c, sc.problem(), *sc.params())
+        assert plan.info().tile_rows == (80 if tile80 else 64)
+        plan.close()
+        _compare(c, sc)
 
 
 def test_noise_free_recovers_ground_truth(ctx):
@@ -165,16 +167,16 @@ def test_c2_banded_scale(ctx):
     assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
 
 
-def test_bcr_matches_sequential_band_solver(ctx, monkeypatch):
+def test_bcr_matches_sequential_band_solver(ctx):
     sc = H.Scene(95, 8000, 8, n_intr=2, seed=31)     # D = 7 -> BCR over 10 super-blocks
     res = []
     for band in (False, True):
-        if band:
-            monkeypatch.setenv("SFM_BA_BAND_SOLVER", "1")
-        plan = api.BAPlan(ctx, sc.problem(), *sc.params())
-        _, s = plan.run()
-        res.append((s, plan.trace()))
-        plan.close()
+        with H.engine_ctx(abi.SFM_CTX_BA_SEQ_BAND if band else 0) as c:
+            plan = api.BAPlan(c, sc.problem(), *sc.params())
+            assert plan.info().rcs_solver == (abi.SFM_RCS_SEQ_BAND if band else abi.SFM_RCS_BCR)
+            _, s = plan.run()
+            res.append((s, plan.trace()))
+            plan.close()
     (s0, t0), (s1, t1) = res
     assert s0.iterations == s1.iterations
     assert abs(s0.final_cost / s1.final_cost - 1) < 1e-9
@@ -588,22 +590,19 @@ def test_plan_cache_reuse_general_points_bit_identical(ctx, shape):
 
 
 @pytest.mark.parametrize("vis_mode", [0, 1])
-def test_step_split_and_reduce_waves_agree(ctx, monkeypatch, vis_mode):
+def test_step_split_and_reduce_waves_agree(vis_mode):
     # Round 4's launch shapes: step_kernel with 1 / 2 / 4 / 8 lanes per point
-    # (SFM_STEP_SPLIT) and reduce_kernel with 1 / 2 / 4 waves per target
-    # (SFM_REDUCE_WAVES) change only the order of the sums, so every shape
-    # takes the oracle's accept / reject sequence and agrees with the others
-    # to rounding (the plan, which carries both, is rebuilt for each).
-    lib = abi.load()
+    # (SFM_CTX_BA_STEP_LANES) and reduce_kernel with 1 / 2 / 4 waves per
+    # target (SFM_CTX_BA_REDUCE_WAVES) change only the order of the sums, so
+    # every shape takes the oracle's accept / reject sequence and agrees with
+    # the others to rounding.
     sc = H.Scene(60, 12000, 8, vis_mode=vis_mode, seed=4242 + vis_mode)
     _, os_, otr, _ = H.oracle_solve(sc, threads=8)
     base = None
     for split, waves in [(1, 1), (2, 1), (4, 2), (8, 4), (2, 4)]:
-        monkeypatch.setenv("SFM_STEP_SPLIT", str(split))
-        monkeypatch.setenv("SFM_REDUCE_WAVES", str(waves))
-        lib.sfm_ba_cache_clear(ctx.h)
         e, i, x = sc.params()
-        rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
+        with H.engine_ctx(abi.SFM_CTX_BA_STEP_LANES(split) | abi.SFM_CTX_BA_REDUCE_WAVES(waves)) as c:
+            rc, gs = api.ba_solve(c, sc.problem(), e, i, x)
         assert rc == 0, api.abi.load().sfm_last_error()
         assert (gs.iterations, gs.successful_steps) == (os_.iterations, os_.successful_steps), (split, waves)
         assert abs(gs.final_cost / os_.final_cost - 1) < RTOL_COST
@@ -611,30 +610,25 @@ def test_step_split_and_reduce_waves_agree(ctx, monkeypatch, vis_mode):
             base = gs
         else:
             assert abs(gs.final_cost / base.final_cost - 1) < 1e-10, (split, waves)
-    lib.sfm_ba_cache_clear(ctx.h)
 
 
-def test_fused_launches_bit_identical(ctx, monkeypatch):
+def test_fused_launches_bit_identical():
     # Launch fusions with unchanged arithmetic: (1) the long reduce targets
     # (the intrinsics corner and arrow collect one tile term per chunk) are
     # summed by segment workgroups inside the reduce launch, the last segment
     # to finish adding the partials in segment order (write-through partials,
-    # an agent-scope ticket) -- SFM_REDUCE_SPLIT restores the three launches;
-    # (2) the BCR top and corner run in one launch, the corner partials of
-    # blocks 1.. beside the top's solve -- SFM_BCR_TOP_SPLIT restores two.
-    # Every combination solves bit for bit alike.
-    lib = abi.load()
+    # an agent-scope ticket) -- SFM_CTX_BA_SPLIT_REDUCE restores the three
+    # launches; (2) the BCR top and corner run in one launch, the corner
+    # partials of blocks 1.. beside the top's solve, and every back-
+    # substitution level in one dataflow launch -- SFM_CTX_BA_SPLIT_BCR
+    # restores a launch each.  Every combination solves bit for bit alike.
     sc = H.Scene(200, 50000, 10, seed=909)
     out = []
     for red_split, top_split in ((True, True), (False, True), (False, False)):
-        for var, on in (("SFM_REDUCE_SPLIT", red_split), ("SFM_BCR_TOP_SPLIT", top_split)):
-            if on:
-                monkeypatch.setenv(var, "1")
-            else:
-                monkeypatch.delenv(var, raising=False)
-        lib.sfm_ba_cache_clear(ctx.h)
+        flags = (abi.SFM_CTX_BA_SPLIT_REDUCE if red_split else 0) | (abi.SFM_CTX_BA_SPLIT_BCR if top_split else 0)
         e, i, x = sc.params()
-        rc, gs = api.ba_solve(ctx, sc.problem(), e, i, x)
+        with H.engine_ctx(flags) as c:
+            rc, gs = api.ba_solve(c, sc.problem(), e, i, x)
         assert rc == 0, api.abi.load().sfm_last_error()
         out.append((gs.iterations, gs.initial_cost, gs.final_cost, e, i, x))
     a = out[0]

@@ -180,17 +180,16 @@ def test_radial3_gpu_c2(ctx):
 
 
 @pytest.mark.gpu
-def test_radial3_band_equals_dense_solver(ctx, monkeypatch):
+def test_radial3_band_equals_dense_solver(ctx):
     # the chunk + BCR path and the general + dense path solve the same system
     sc = H.Scene(40, 5000, 8, model=R3, n_intr=2, seed=41)
     res = []
     for dense in (False, True):
-        if dense:
-            monkeypatch.setenv("SFM_BA_DENSE", "1")
-        plan = api.BAPlan(ctx, sc.problem(), *sc.params())
-        _, s = plan.run()
-        res.append((s, plan.trace()))
-        plan.close()
+        with H.engine_ctx(H.abi.SFM_CTX_BA_DENSE_RCS if dense else 0) as c:
+            plan = api.BAPlan(c, sc.problem(), *sc.params())
+            _, s = plan.run()
+            res.append((s, plan.trace()))
+            plan.close()
     (s0, t0), (s1, t1) = res
     assert s0.iterations == s1.iterations
     assert abs(s0.final_cost / s1.final_cost - 1) < 1e-9
