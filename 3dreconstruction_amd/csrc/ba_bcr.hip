@@ -301,7 +301,7 @@ __device__ __forceinline__ void diag16_xrow(const double (&a)[16], const double 
 // below it, and only the never-read upper triangle above) and no per-pivot
 // definiteness test (a pivot d <= 0 or NaN leaves a non-positive or NaN L_KK,
 // checked once at the end).
-template <int K>
+template <int K, int NP>
 __device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], int i) {
     const double d = row_bcast(a[K], K);
     const double rinv = rsqrt_nr(d);
@@ -313,9 +313,16 @@ __device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], in
     double u0 = 0.0, u1 = 0.0;
     diag16_xrow<K>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
     x[K] = ((K == i ? 1.0 : 0.0) - (u0 + u1)) * rinv;
-    if constexpr (K < 15) diag16_step<K + 1>(a, x, i);
+    if constexpr (K + 1 < NP) diag16_step<K + 1, NP>(a, x, i);
 }
 
+// NP: pivots taken.  Rows NP..15 are a super-block's identity padding (the
+// 6K real rows of a block of K cameras end inside its last diagonal tile:
+// bcr_pack_kernel writes 1 on their diagonal and 0 elsewhere, and every
+// update leaves them so, since their rows and columns of each C, W and z are
+// zero): their L and X rows are the identity, so their pivots are skipped
+// (K = 9: 10 of the 64 pivots of a super-block).
+template <int NP = 16>
 __device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, double* col) {
     (void)col;
     // the critical path of the factorisation: ahead of the co-resident helper
@@ -334,7 +341,9 @@ __device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, d
     for (int j = 0; j < 16; ++j) a[j] = Al[(i & 15) * LD + j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? a[j] : 0.0;
-    diag16_step<0>(a, x, i);
+    diag16_step<0, NP>(a, x, i);
+#pragma unroll
+    for (int m = NP; m < 16; ++m) x[m] = m == i ? 1.0 : 0.0;   // identity padding (a keeps it)
     double lii = 1.0;   // this lane's L_ii (a[i], extracted without dynamic indexing)
 #pragma unroll
     for (int j = 0; j < 16; ++j) lii = j == i ? a[j] : lii;
@@ -351,7 +360,14 @@ __device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, d
 // called (BCR level / top kernels: inlined there it costs the helper waves'
 // registers, 47 spilled VGPRs) or inlined (the dense kernels: 6 % faster
 // factor, no spills)
-__device__ __noinline__ void diag16(double* A, double* X, double* bad, double* col) { diag16_body(A, X, bad, col); }
+template <int NP = 16>
+__device__ __noinline__ void diag16(double* A, double* X, double* bad, double* col) { diag16_body<NP>(A, X, bad, col); }
+// the last diagonal tile of a super-block: np3 = 6 K - 48 real pivots
+__device__ __forceinline__ void diag16_last(int np3, double* A, double* X, double* bad, double* col) {
+    if (np3 == 6) diag16<6>(A, X, bad, col);
+    else if (np3 == 12) diag16<12>(A, X, bad, col);
+    else diag16<16>(A, X, bad, col);
+}
 
 // Blocked Cholesky A = L L' of a 64x64 LDS tile and X = L^-1 (X zeroed by
 // the caller).  All 256 threads; ends synchronised.
@@ -375,10 +391,12 @@ struct NoPre {
 struct NoBg {
     __device__ void operator()(int) const {}
 };
+// np3: real pivots of the last diagonal tile (16: no padding; the BCR
+// super-blocks' 6 K - 48)
 template <int NW = NT / 64, class Pre0 = NoPre, class PreN = NoPre, class Bg = NoBg, bool INL = false>
 __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, double* col,
                            unsigned long long* st = nullptr, Pre0 pre0 = Pre0(), PreN preN = PreN(),
-                           Bg bg = Bg()) {
+                           Bg bg = Bg(), int np3 = 16) {
     const int wave = threadIdx.x >> 6;
     unsigned long long t0 = 0, td = 0, ta = 0, tq = 0, tb = 0, tw = 0;
     // diagnostic (st): per window k (diag16(k) and the helpers' work beside
@@ -437,6 +455,7 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
             wave_sync();
             if (st) tb = stamp();
             if constexpr (INL) diag16_body(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+            else if (n == 3) diag16_last(np3, A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
             else diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
             if (st) {
                 const unsigned long long te = stamp();
@@ -626,6 +645,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     if (i >= b.N) return;
     const int r = i + s, wave = threadIdx.x >> 6;
     const bool hr = r < b.N, hz = 16 * w < b.nrhs;
+    const int np3 = 6 * b.K - 48;   // real pivots of the last diagonal tile
     constexpr int L16 = 17;
     double* A = sm;                 // [64][LD]
     double* X = A + M * LD;         // [64][LD]
@@ -774,7 +794,8 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         tile_st(A, LD, 16 * n, 16 * n, acc);
         wave_sync();
         if (st) tb = stamp();
-        diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+        if (n == 3) diag16_last(np3, A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
+        else diag16(A + 16 * n * (LD + 1), X + 16 * n * (LD + 1), bad, col);
         if (st) {
             const unsigned long long te = stamp();
             td += te - ta;
@@ -994,9 +1015,9 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
                 }
             }
         };
-        chol_inv64<NWL>(A, X, bad, sc, nullptr, pre0, preN);
+        chol_inv64<NWL>(A, X, bad, sc, nullptr, pre0, preN, NoBg(), 6 * b.K - 48);
     } else {
-        chol_inv64<NWL>(A, X, bad, sc);
+        chol_inv64<NWL>(A, X, bad, sc, nullptr, NoPre(), NoPre(), NoBg(), 6 * b.K - 48);
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     // the root's forward solve z_0 = X R_0, every column (the corner system
@@ -1337,7 +1358,11 @@ __global__ void bcr_verdict_kernel(BcrArgs b, DevProblem P) { P.scal[kScSolveFai
 bool bcr_supported(const DevProblem& P) { return P.D <= kBcrK && P.ncam > 0 && P.iw * P.nintr <= 16; }
 
 void bcr_setup(BcrArgs& b, const DevProblem& P) {
-    b.K = kBcrK;
+    // K >= D keeps the super-blocks block-tridiagonal; K = 9 for a band of
+    // up to 9 camera blocks (C4: a point seen by 10 consecutive cameras):
+    // 54 real rows, so the last diagonal tile's factor takes 6 pivots instead
+    // of 12 real + 4 padding (diag16_last)
+    b.K = std::max(9, P.D);
     b.N = (P.ncam + b.K - 1) / b.K;
     b.nrhs = ((1 + P.iw * P.nintr) + 15) / 16 * 16;   // MFMA column tiles
 }

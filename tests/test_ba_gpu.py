@@ -636,4 +636,3 @@ def test_fused_launches_bit_identical():
         assert a[:3] == b[:3]
         for u, v in zip(a[3:], b[3:]):
             np.testing.assert_array_equal(u, v)
-    lib.sfm_ba_cache_clear(ctx.h)
