@@ -811,7 +811,72 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         if (upd) tile_st(tile_at(1, kS0[wave][0], kS0[wave][1]), LD, 0, 0, part);
     }
     __syncthreads();
+    // ---- forward substitution of this workgroup's column tile w -------------
+    // O_k = X_kk (B_k - sum_{m<k} L_km O_m), in place, for O = Wl[:, w]
+    // (B = C_i[:, w] in Cc), Wr[:, w] (B = C_r[w, :]' in Cr, transposed) and
+    // z[:, w] (B = R_i[:, w] in Rc): row tile k is formed as soon as the
+    // factor's diagonal tile k is done, on the helper waves inside the next
+    // window, instead of X C_i, X C_r', X R_i after the whole factorisation
+    // (round 5: that tail was ~10k of a level's ~47k cycles).  fs(k): B_k -=
+    // sum L_km O_m (L_km in A's lower tiles after P(m)); gs(k): O_k = X_kk B_k,
+    // kept in LDS for the later row tiles and stored to global.
+    double* const Wlg = b.Wl + (size_t)i * M * M;
+    double* const Wrg = b.Wr + (size_t)i * M * M;
+    double* const Zg = b.Z + (size_t)i * M * b.nrhs;
+    auto fs_l = [&](double* B, int k) {   // B = Cc or Rc ([64][L16])
+        v4d acc = tile_ld(B, L16, 16 * k, 0);
+        acc = mm_ll<false, false, true>(acc, L3(A), LD, 16 * k, L3(B), L16, 0, 0, 16 * k);
+        tile_st(B, L16, 16 * k, 0, acc);
+    };
+    auto gs_l = [&](double* B, int k, double* G, int ldg) {
+        const v4d o = mm_ll<false, false, false>(zero4(), L3(X), LD, 16 * k, L3(B), L16, 0, 16 * k, 16 * k + 16);
+        tile_st(B, L16, 16 * k, 0, o);
+        tile_st(G, ldg, 16 * k, 16 * w, o);
+    };
+    auto fs_r = [&](int k) {   // Cr(0, k) -= sum_m Cr(0, m) L_km'
+        v4d acc = tile_ld(Cr, LD, 0, 16 * k);
+        acc = mm_ll<false, true, true>(acc, L3(Cr), LD, 0, L3(A), LD, 16 * k, 0, 16 * k);
+        tile_st(Cr, LD, 0, 16 * k, acc);
+    };
+    auto gs_r = [&](int k) {   // Cr(0, k) = Cr(0, k) X_kk' = O_k'; Wr rows 16k.. (transposed store)
+        const v4d o = mm_ll<false, true, false>(zero4(), L3(Cr), LD, 0, L3(X), LD, 16 * k, 16 * k, 16 * k + 16);
+        tile_st(Cr, LD, 0, 16 * k, o);
+        const int lane = threadIdx.x & 63, li = lane & 15, kk = lane >> 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Wrg[(16 * k + li) * M + 16 * w + kk + 4 * q] = o[q];
+    };
+    // one output's row tiles k0 (gs) and k0 + 1 (fs), wave-ordered through LDS
+    auto fsub_l = [&](int k0) {
+        gs_l(Cc, k0, Wlg, M);
+        if (k0 < 3) {
+            wave_sync();
+            fs_l(Cc, k0 + 1);
+        }
+    };
+    auto fsub_z = [&](int k0) {
+        if (!hz) return;
+        gs_l(Rc, k0, Zg, b.nrhs);
+        if (k0 < 3) {
+            wave_sync();
+            fs_l(Rc, k0 + 1);
+        }
+    };
+    auto fsub_r = [&](int k0) {
+        if (!hr) return;
+        gs_r(k0);
+        if (k0 < 3) {
+            wave_sync();
+            fs_r(k0 + 1);
+        }
+    };
+    // this workgroup's row tile w of X for the back substitution (final after P(w))
+    auto store_x = [&](int nth, int t0) {
+        double* Xg = b.L + (size_t)i * M * M + 16 * w * M;
+        for (int e = t0; e < 16 * M; e += nth) Xg[e] = X[(16 * w + e / M) * LD + e % M];
+    };
     // ---- W0 -----------------------------------------------------------------
+    // (helpers: the A update halves, and every neighbour product of C_i, C_r
+    // and R_i that the forward substitution needs by window 1 or 2)
     if (st) tw = stamp();
     switch (wave) {
         case 0: {
@@ -823,12 +888,12 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
             dfac(0, acc);
             break;
         }
-        case 1: half(0); half(3); break;
-        case 2: half(1); half(4); break;
-        case 3: half(2); break;
-        case 5: half(6); break;
-        case 6: half(7); break;
-        case 7: half(5); bgC(0); break;
+        case 1: half(0); half(3); bgR(0); break;
+        case 2: half(1); half(4); bgR(1); break;
+        case 3: half(2); bgR(2); break;
+        case 5: half(6); bgCr(0); break;
+        case 6: half(7); bgCr(1); break;
+        case 7: half(5); bgC(0); bgC(1); break;
         default: break;
     }
     wend(0);
@@ -852,9 +917,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 1: full(2, 1, 1); break;
         case 2: full(3, 1, 1); break;
         case 3: full(2, 2, 1); break;
-        case 5: tinv(1, 0); bgC(1); break;
-        case 6: bgC(2); break;
-        case 7: bgC(3); break;
+        case 5: fsub_l(0); fsub_r(0); bgC(2); break;
+        case 6: fsub_z(0); bgR(3); break;
+        case 7: tinv(1, 0); bgC(3); bgCr(2); break;
         default: break;
     }
     wend(1);
@@ -867,10 +932,10 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 0: dfac(2, tile_mm<false, true, true>(tile_ld(A, LD, 32, 32), L3(A), LD, 32, L3(A), LD, 32, 16, 32)); break;
         case 1: full(3, 2, 2); break;
         case 2: full(3, 3, 2); break;
-        case 3: tinv(2, 0); tinv(2, 1); break;
-        case 5: bgCr(0); break;
-        case 6: bgCr(1); break;
-        case 7: bgCr(2); bgCr(3); break;
+        case 3: tinv(2, 0); tinv(2, 1); bgCr(3); break;
+        case 5: fsub_l(1); break;
+        case 6: fsub_z(1); break;
+        case 7: fsub_r(1); break;
         default: break;
     }
     wend(2);
@@ -884,51 +949,34 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 1: tinv(3, 0); break;
         case 2: tinv(3, 1); break;
         case 3: tinv(3, 2); break;
-        case 5: bgR(0); break;
-        case 6: bgR(1); break;
-        case 7: bgR(2); break;
+        case 4: if (w < 3) store_x(64, threadIdx.x & 63); break;   // no MFMA on the pivot wave's SIMD
+        case 5: fsub_l(2); break;
+        case 6: fsub_z(2); break;
+        case 7: fsub_r(2); break;
         default: break;
     }
     wend(3);
     __syncthreads();
-    // ---- P3 (+ R_3 on wave 4) ----------------------------------------------
+    // ---- P3: X's last row tile; the last row tile of every output -----------
     pphase(3);
-    if (wave == 4) bgR(3);   // (no-op at the first level)
-    __syncthreads();
+    if (wave == 5) fsub_l(3);
+    else if (wave == 6) fsub_z(3);
+    else if (wave == 7) fsub_r(3);
     if (st && threadIdx.x == 0) {
         atomicAdd(st + 0, td);
         atomicAdd(st + 1, stamp() - tf0);
         atomicAdd(st + 7, tq);
         for (int q = 0; q < 8; ++q) atomicAdd(st + 8 + q, wmax[q]);
     }
+    if (w == 3) {
+        __syncthreads();   // X_3j of P3
+        store_x(NTL, threadIdx.x);
+    }
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
-    {   // X for the back substitution: each of the block's 4 workgroups stores 16 rows
-        double* Xg = b.L + (size_t)i * M * M + 16 * w * M;
-        for (int e = threadIdx.x; e < 16 * M; e += NTL) Xg[e] = X[(16 * w + e / M) * LD + e % M];
-    }
     if (st) {
         __syncthreads();
         if (threadIdx.x == 0) atomicAdd(st + 6, stamp() - t0);   // through the X copy
-    }
-    // column tile w of Wl = X C_i, Wr = X C_r', z = X R_i: product p of row
-    // tile r costs r + 1 k-chunks (X is lower triangular); the 12 (p, r) items
-    // (30 chunks) are split at most 4 chunks per wave over the 8 waves
-    constexpr int8_t kItems[NWL][2][2] = {{{0, 3}, {-1, 0}}, {{1, 3}, {-1, 0}}, {{2, 3}, {-1, 0}},
-                                          {{0, 2}, {0, 0}},  {{1, 2}, {1, 0}},  {{2, 2}, {2, 0}},
-                                          {{0, 1}, {1, 1}},  {{2, 1}, {-1, 0}}};
-    for (int q = 0; q < 2; ++q) {
-        const int pr = kItems[wave][q][0], r = kItems[wave][q][1], kend = 16 * (r + 1);
-        if (pr < 0) break;
-        if (pr == 0)
-            tile_st(b.Wl + (size_t)i * M * M, M, 16 * r, 16 * w,
-                    tile_mm<false, false, false>(zero4(), L3(X), LD, 16 * r, L3(Cc), L16, 0, 0, kend));
-        else if (pr == 1 && hr)   // op(B)[k][n] = C_r[16w + n][k]
-            tile_st(b.Wr + (size_t)i * M * M, M, 16 * r, 16 * w,
-                    tile_mm<false, true, false>(zero4(), L3(X), LD, 16 * r, L3(Cr), LD, 0, 0, kend));
-        else if (pr == 2 && hz)
-            tile_st(b.Z + (size_t)i * M * b.nrhs, b.nrhs, 16 * r, 16 * w,
-                    tile_mm<false, false, false>(zero4(), L3(X), LD, 16 * r, L3(Rc), L16, 0, 0, kend));
     }
     if (st) {
         __syncthreads();
