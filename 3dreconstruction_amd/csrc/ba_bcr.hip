@@ -148,6 +148,49 @@ template <bool TA, bool TB, bool NEG>
 __device__ __noinline__ v4d mm_gl(v4d acc, glb_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
     return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
 }
+// A 64 x 16 column block of a global matrix held in registers, in the
+// operand order of tile_mm's k loop (v[4 c + j]: row 16 c + 4 j + kk, column
+// i).  The level kernel's neighbour products (C_i, C_r, R_i updates) fetch
+// their global operand this way at the start of a window, so the product
+// runs at LDS speed instead of waiting one L2 latency per 16-deep k chunk.
+struct GTile {
+    double v[16];
+    __device__ __forceinline__ void fetch(const double* p, int ld) {
+        const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * c + j] = p[(16 * c + 4 * j + kk) * ld + i];
+    }
+};
+// acc +/-= A[k][ar + m]' G[k][n], k = 0..63 (A in LDS, transposed)
+template <bool NEG, class PA>
+__device__ __forceinline__ v4d mm_tr(v4d acc, PA A, int lda, int ar, const GTile& g) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        double a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = A[(16 * c + 4 * j + kk) * lda + ar + i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], g.v[4 * c + j], acc, 0, 0, 0);
+    }
+    return acc;
+}
+// acc +/-= G[k][m]' B[k][bc + n], k = 0..63 (B in LDS)
+template <bool NEG, class PB>
+__device__ __forceinline__ v4d mm_rt(v4d acc, const GTile& g, PB B, int ldb, int bc) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        double bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j] = B[(16 * c + 4 * j + kk) * ldb + bc + i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -g.v[4 * c + j] : g.v[4 * c + j], bv[j], acc, 0, 0, 0);
+    }
+    return acc;
+}
 __device__ __forceinline__ lds_cd* L3(const double* p) { return (lds_cd*)p; }
 __device__ __forceinline__ glb_cd* G1(const double* p) { return (glb_cd*)p; }
 
@@ -750,19 +793,32 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     auto tinv = [&](int n, int j) {
         tile_st(X, LD, 16 * n, 16 * j, mm_ll<false, false, false>(zero4(), L3(A), LD, 16 * n, L3(X), LD, 16 * j, 16 * j, 16 * n));
     };
-    auto bgR = [&](int v) {
-        if (!hz || !upd) return;
+    // neighbour products; g*: the global operands, fetched into registers by
+    // the wave at the start of the window it runs them in (GTile)
+    const bool hzu = hz && upd;
+    auto bgR = [&](int v, const GTile& g1, const GTile& g2) {   // R_i[:, w] row tile v
+        if (!hzu) return;
         v4d acc = tile_ld(Rc, L16, 16 * v, 0);
-        acc = mm_lg<true, false, true>(acc, L3(Wal), M, 16 * v, G1(Z1), b.nrhs, 0, 0, M);
-        if (hir) acc = mm_lg<true, false, true>(acc, L3(Wbl), M, 16 * v, G1(Z2), b.nrhs, 0, 0, M);
+        acc = mm_tr<true>(acc, L3(Wal), M, 16 * v, g1);
+        if (hir) acc = mm_tr<true>(acc, L3(Wbl), M, 16 * v, g2);
         tile_st(Rc, L16, 16 * v, 0, acc);
     };
-    auto bgC = [&](int v) {   // block (i, i-2sp) = (i, i-s)
-        if (upd) tile_st(Cc, L16, 16 * v, 0, mm_lg<true, false, true>(zero4(), L3(Wal), M, 16 * v, G1(WL), M, 0, 0, M));
+    auto bgC = [&](int v, const GTile& gl) {   // block (i, i-2sp) = (i, i-s)
+        if (upd) tile_st(Cc, L16, 16 * v, 0, mm_tr<true>(zero4(), L3(Wal), M, 16 * v, gl));
     };
-    auto bgCr = [&](int v) {   // block (r, r-s) = (r, i)
-        if (hr && hir)
-            tile_st(Cr, LD, 0, 16 * v, mm_gl<true, false, true>(zero4(), G1(WR), M, 0, L3(Wbl), M, 16 * v, 0, M));
+    auto bgCr = [&](int v, const GTile& gr) {   // block (r, r-s) = (r, i)
+        if (hr && hir) tile_st(Cr, LD, 0, 16 * v, mm_rt<true>(zero4(), gr, L3(Wbl), M, 16 * v));
+    };
+    auto fetch_z = [&](GTile& g1, GTile& g2) {
+        if (!hzu) return;
+        g1.fetch(Z1, b.nrhs);
+        if (hir) g2.fetch(Z2, b.nrhs);
+    };
+    auto fetch_wl = [&](GTile& g) {
+        if (upd) g.fetch(WL, M);
+    };
+    auto fetch_wr = [&](GTile& g) {
+        if (hr && hir) g.fetch(WR, M);
     };
     // P(k), k >= 1: panels L_ik = A_ik X_kk' (i > k) and X_kj = -X_kk T_kj (j < k), waves 0..2
     auto pphase = [&](int k) {
@@ -888,12 +944,12 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
             dfac(0, acc);
             break;
         }
-        case 1: half(0); half(3); bgR(0); break;
-        case 2: half(1); half(4); bgR(1); break;
-        case 3: half(2); bgR(2); break;
-        case 5: half(6); bgCr(0); break;
-        case 6: half(7); bgCr(1); break;
-        case 7: half(5); bgC(0); bgC(1); break;
+        case 1: { GTile z1, z2; fetch_z(z1, z2); half(0); half(3); bgR(0, z1, z2); break; }
+        case 2: { GTile z1, z2; fetch_z(z1, z2); half(1); half(4); bgR(1, z1, z2); break; }
+        case 3: { GTile z1, z2; fetch_z(z1, z2); half(2); bgR(2, z1, z2); break; }
+        case 5: { GTile g; fetch_wr(g); half(6); bgCr(0, g); break; }
+        case 6: { GTile g; fetch_wr(g); half(7); bgCr(1, g); break; }
+        case 7: { GTile g; fetch_wl(g); half(5); bgC(0, g); bgC(1, g); break; }
         default: break;
     }
     wend(0);
@@ -917,9 +973,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 1: full(2, 1, 1); break;
         case 2: full(3, 1, 1); break;
         case 3: full(2, 2, 1); break;
-        case 5: fsub_l(0); fsub_r(0); bgC(2); break;
-        case 6: fsub_z(0); bgR(3); break;
-        case 7: tinv(1, 0); bgC(3); bgCr(2); break;
+        case 5: { GTile g; fetch_wl(g); fsub_l(0); fsub_r(0); bgC(2, g); break; }
+        case 6: { GTile z1, z2; fetch_z(z1, z2); fsub_z(0); bgR(3, z1, z2); break; }
+        case 7: { GTile gl, gr; fetch_wl(gl); fetch_wr(gr); tinv(1, 0); bgC(3, gl); bgCr(2, gr); break; }
         default: break;
     }
     wend(1);
@@ -932,7 +988,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 0: dfac(2, tile_mm<false, true, true>(tile_ld(A, LD, 32, 32), L3(A), LD, 32, L3(A), LD, 32, 16, 32)); break;
         case 1: full(3, 2, 2); break;
         case 2: full(3, 3, 2); break;
-        case 3: tinv(2, 0); tinv(2, 1); bgCr(3); break;
+        case 3: { GTile g; fetch_wr(g); tinv(2, 0); tinv(2, 1); bgCr(3, g); break; }
         case 5: fsub_l(1); break;
         case 6: fsub_z(1); break;
         case 7: fsub_r(1); break;

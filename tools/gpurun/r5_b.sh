@@ -24,3 +24,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 f=$(find "$OUT/p8" -name "*kernel_stats.csv" | head -1); cp "$f" "$OUT/kernel_stats_fake8.csv"
 rm -rf "$OUT/p1" "$OUT/p8"
 python3 "$GRAFT_REPO_ROOT/tools/kstat_brief.py" "$OUT/kernel_stats_c4.csv" "$OUT/kernel_stats_fake8.csv" | tee "$OUT/kstat_brief.txt"
+# the C5 loops with SFM_TIMING phase sums, and every 100th BA problem dumped (planner replay offline)
+cd "$GRAFT_REPO_ROOT"
+mkdir -p "$OUT/dumps"
+SFM_TIMING=1 SFM_SEQ_DUMP="$OUT/dumps" timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 --no-match --no-snavely --no-pmc --no-filter --no-dense --no-radial3 --no-cpu-baseline > "$OUT/loop.json" 2> "$OUT/loop_timing.err"
+grep "^\[bench\] loop" "$OUT/loop_timing.err" || true
+gzip -f "$OUT"/dumps/*.bin
+ls -la "$OUT/dumps"
