@@ -12,7 +12,8 @@ for path in sys.argv[1:]:
     fam = {}
     for r in rows:
         n = r["Name"]
-        key = n.split("(")[0].split("<")[0].split("::")[-1]
+        base = n.replace("(anonymous namespace)::", "").replace("void ", "", 1)
+        key = base.split("(")[0].split("<")[0].split("::")[-1]
         fam[key] = fam.get(key, 0.0) + float(r["TotalDurationNs"]) / 1e3
     bcr = sum(v for k, v in fam.items() if k.startswith("bcr_"))
     tot = sum(fam.values())
