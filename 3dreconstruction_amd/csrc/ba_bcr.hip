@@ -326,7 +326,7 @@ __device__ __forceinline__ void fmac_bc(double& acc, double src, double mul, int
 // a_ij -= (a_ik / d_k) a_jk.  Row k of X (x_k = (e_k - sum_p L_kp x_p) / L_kk)
 // is computed as soon as row k of L is final.  Single-wave issue bound:
 // about 30 fp64 instructions per pivot.
-// L overwrites the lower tile (upper zeroed); X gets L^-1 (upper zeroed).
+// X gets L^-1 (upper zeroed); the tile of A is left as it was loaded.
 // step K of diag16, expanded at compile time (an inline-asm body defeats the
 // loop unroller, and every broadcast lane must be an immediate)
 template <int K, int... J>
@@ -391,9 +391,10 @@ __device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, d
 #pragma unroll
     for (int j = 0; j < 16; ++j) lii = j == i ? a[j] : lii;
     if (__ballot(act && !(lii > 0.0)) != 0 && lane == 0) bad[0] = 1.0;
+    // only X = L^-1 goes back: nothing reads a factored diagonal tile of L
+    // (panels are A X', the inverse's off-diagonal tiles sums of L_nm X_mj
+    // with m < n), so its 16 stores are off the pivot wave's critical path
     if (act) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) Al[i * LD + j] = j <= i ? a[j] : 0.0;
 #pragma unroll
         for (int m = 0; m < 16; ++m) Xl[m * LD + i] = x[m];
     }
@@ -973,9 +974,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 1: full(2, 1, 1); break;
         case 2: full(3, 1, 1); break;
         case 3: full(2, 2, 1); break;
-        case 5: { GTile g; fetch_wl(g); fsub_l(0); fsub_r(0); bgC(2, g); break; }
-        case 6: { GTile z1, z2; fetch_z(z1, z2); fsub_z(0); bgR(3, z1, z2); break; }
-        case 7: { GTile gl, gr; fetch_wl(gl); fetch_wr(gr); tinv(1, 0); bgC(3, gl); bgCr(2, gr); break; }
+        case 5: { GTile g; fetch_wl(g); fsub_l(0); bgC(2, g); break; }
+        case 6: fsub_z(0); fsub_r(0); break;
+        case 7: { GTile g; fetch_wr(g); tinv(1, 0); bgCr(2, g); break; }
         default: break;
     }
     wend(1);
@@ -988,10 +989,10 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 0: dfac(2, tile_mm<false, true, true>(tile_ld(A, LD, 32, 32), L3(A), LD, 32, L3(A), LD, 32, 16, 32)); break;
         case 1: full(3, 2, 2); break;
         case 2: full(3, 3, 2); break;
-        case 3: { GTile g; fetch_wr(g); tinv(2, 0); tinv(2, 1); bgCr(3, g); break; }
+        case 3: tinv(2, 0); tinv(2, 1); break;
         case 5: fsub_l(1); break;
-        case 6: fsub_z(1); break;
-        case 7: fsub_r(1); break;
+        case 6: fsub_r(1); break;
+        case 7: { GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); fsub_z(1); break; }
         default: break;
     }
     wend(2);
@@ -1006,9 +1007,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 2: tinv(3, 1); break;
         case 3: tinv(3, 2); break;
         case 4: if (w < 3) store_x(64, threadIdx.x & 63); break;   // no MFMA on the pivot wave's SIMD
-        case 5: fsub_l(2); break;
-        case 6: fsub_z(2); break;
-        case 7: fsub_r(2); break;
+        case 5: { GTile g; fetch_wl(g); bgC(3, g); fsub_l(2); break; }
+        case 6: { GTile g; fetch_wr(g); bgCr(3, g); fsub_r(2); break; }
+        case 7: fsub_z(2); break;
         default: break;
     }
     wend(3);

@@ -14,7 +14,7 @@ for r in rows:
     name = r["Kernel_Name"]
     if "bcr_" not in name:
         continue
-    short = name.split("::")[-1].split("(")[0].split("<")[0]
+    short = name.replace("(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0].split("<")[0].split("::")[-1]
     if short == "bcr_pack_kernel":
         cur = []
         seqs.append(cur)
