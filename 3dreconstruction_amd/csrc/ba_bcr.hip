@@ -902,29 +902,20 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
 #pragma unroll
         for (int q = 0; q < 4; ++q) Wrg[(16 * k + li) * M + 16 * w + kk + 4 * q] = o[q];
     };
-    // one output's row tiles k0 (gs) and k0 + 1 (fs), wave-ordered through LDS
-    auto fsub_l = [&](int k0) {
-        gs_l(Cc, k0, Wlg, M);
-        if (k0 < 3) {
-            wave_sync();
-            fs_l(Cc, k0 + 1);
-        }
+    // gs of row tile k on waves 5-7 in the P(k) phase, right after the
+    // window that produced X_kk (those waves are idle there); fs of row tile
+    // k + 1 in window k + 1, after P(k) gave L_{k+1,k}
+    auto gs_k = [&](int k) {
+        if (wave == 5) gs_l(Cc, k, Wlg, M);
+        else if (wave == 6 && hr) gs_r(k);
+        else if (wave == 7 && hz) gs_l(Rc, k, Zg, b.nrhs);
     };
-    auto fsub_z = [&](int k0) {
-        if (!hz) return;
-        gs_l(Rc, k0, Zg, b.nrhs);
-        if (k0 < 3) {
-            wave_sync();
-            fs_l(Rc, k0 + 1);
-        }
+    auto fs_lk = [&](int k) { fs_l(Cc, k); };
+    auto fs_zk = [&](int k) {
+        if (hz) fs_l(Rc, k);
     };
-    auto fsub_r = [&](int k0) {
-        if (!hr) return;
-        gs_r(k0);
-        if (k0 < 3) {
-            wave_sync();
-            fs_r(k0 + 1);
-        }
+    auto fs_rk = [&](int k) {
+        if (hr) fs_r(k);
     };
     // this workgroup's row tile w of X for the back substitution (final after P(w))
     auto store_x = [&](int nth, int t0) {
@@ -962,6 +953,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         wave_sync();
         tile_st(A, LD, 16 * ii, 0, tile_mm<false, true, false>(zero4(), L3(A), LD, 16 * ii, L3(X), LD, 0, 0, 16));
     }
+    gs_k(0);
     __syncthreads();
     // ---- W1 -----------------------------------------------------------------
     if (st) tw = stamp();
@@ -974,14 +966,15 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 1: full(2, 1, 1); break;
         case 2: full(3, 1, 1); break;
         case 3: full(2, 2, 1); break;
-        case 5: { GTile g; fetch_wl(g); fsub_l(0); bgC(2, g); break; }
-        case 6: fsub_z(0); fsub_r(0); break;
+        case 5: { GTile g; fetch_wl(g); fs_lk(1); bgC(2, g); break; }
+        case 6: fs_rk(1); fs_zk(1); break;
         case 7: { GTile g; fetch_wr(g); tinv(1, 0); bgCr(2, g); break; }
         default: break;
     }
     wend(1);
     __syncthreads();
     pphase(1);
+    gs_k(1);
     __syncthreads();
     // ---- W2 -----------------------------------------------------------------
     if (st) tw = stamp();
@@ -990,14 +983,15 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 1: full(3, 2, 2); break;
         case 2: full(3, 3, 2); break;
         case 3: tinv(2, 0); tinv(2, 1); break;
-        case 5: fsub_l(1); break;
-        case 6: fsub_r(1); break;
-        case 7: { GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); fsub_z(1); break; }
+        case 5: fs_lk(2); break;
+        case 6: fs_rk(2); break;
+        case 7: { GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); fs_zk(2); break; }
         default: break;
     }
     wend(2);
     __syncthreads();
     pphase(2);
+    gs_k(2);
     __syncthreads();
     // ---- W3 -----------------------------------------------------------------
     if (st) tw = stamp();
@@ -1007,18 +1001,16 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         case 2: tinv(3, 1); break;
         case 3: tinv(3, 2); break;
         case 4: if (w < 3) store_x(64, threadIdx.x & 63); break;   // no MFMA on the pivot wave's SIMD
-        case 5: { GTile g; fetch_wl(g); bgC(3, g); fsub_l(2); break; }
-        case 6: { GTile g; fetch_wr(g); bgCr(3, g); fsub_r(2); break; }
-        case 7: fsub_z(2); break;
+        case 5: { GTile g; fetch_wl(g); bgC(3, g); fs_lk(3); break; }
+        case 6: { GTile g; fetch_wr(g); bgCr(3, g); fs_rk(3); break; }
+        case 7: fs_zk(3); break;
         default: break;
     }
     wend(3);
     __syncthreads();
     // ---- P3: X's last row tile; the last row tile of every output -----------
     pphase(3);
-    if (wave == 5) fsub_l(3);
-    else if (wave == 6) fsub_z(3);
-    else if (wave == 7) fsub_r(3);
+    gs_k(3);
     if (st && threadIdx.x == 0) {
         atomicAdd(st + 0, td);
         atomicAdd(st + 1, stamp() - tf0);
