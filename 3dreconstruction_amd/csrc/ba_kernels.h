@@ -114,6 +114,8 @@ struct DevProblem {
     double* part_f;     // [n_fblk][3] candidate-kernel partials
     int32_t n_fblk;
     double* scal;       // [kScCount]
+    double* fin_part;   // [16][12] finalize_kernel's workgroup partials
+    unsigned* fin_count;   // its ticket (zeroed once; the last workgroup resets it)
     double* scal_host;  // device view of host-mapped [kScCount + 1] (+ sequence word), or null
 };
 

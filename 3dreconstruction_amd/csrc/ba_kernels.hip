@@ -2435,23 +2435,25 @@ __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
     }
 }
 
-// fixed-order reduction of the per-block partials
-// 1024 threads: each strides over ~4 partials per list instead of ~16 (the
-// pass is a chain of dependent global loads); fixed order, so deterministic
-constexpr int kFinThreads = 1024;
+// fixed-order reduction of the per-block partials, in kFinBlocks
+// workgroups: workgroup g sums elements g * kFinThreads + t, stepping by
+// kFinBlocks * kFinThreads (every thread's loads in flight together), stores
+// its 12 partials write-through and takes a ticket; the last to arrive adds
+// the partials in workgroup order and publishes (Guideline 16, counter form).
+// One 1024-thread workgroup walking every list took 12-13 us at C4 (a chain
+// of dependent loads per thread); the sums are now in a different (still
+// fixed) order.
+constexpr int kFinThreads = 256, kFinBlocks = 16;
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks,
                                                                unsigned long long seq) {
     double s[7] = {0, 0, 0, 0, 0, 0, 0};
     double m[5] = {0, 0, 0, 0, 0};
     // the four lists in one loop, so every list's loads are in flight together
-    // (four separate loops were four serial memory latencies); each list is
-    // still summed by this thread in index order, as before
     const int nf = P.n_fblk, nu = P.n_img * P.gram_seg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
     const int nmax = max(max(nf, nu), max(ns, nt));
-    // (unrolled by four: C4's 3976 chunks are four rounds of the 1024 threads,
-    // so every load is in flight before the first add)
-#pragma unroll 4
-    for (int i = threadIdx.x; i < nmax; i += kFinThreads) {
+    constexpr int kStride = kFinBlocks * kFinThreads;
+#pragma unroll 2
+    for (int i = blockIdx.x * kFinThreads + threadIdx.x; i < nmax; i += kStride) {
         // loads from clamped indices (unconditional, so the compiler issues
         // them all before the first use), accumulated only where in range
         const bool bf = i < nf, bu = i < nu, bs = i < ns, bt = i < nt;
@@ -2476,6 +2478,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
     for (int k = 0; k < 5; ++k) m[k] = wave_max(m[k]);
     constexpr int kW = kFinThreads / 64;
     __shared__ double red[kW][12];
+    __shared__ int last;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) {
         for (int k = 0; k < 7; ++k) red[wave][k] = s[k];
@@ -2486,11 +2489,29 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
         const int k = threadIdx.x;
         double t = red[0][k];
         for (int w = 1; w < kW; ++w) t = k < 7 ? t + red[w][k] : fmax(t, red[w][k]);
+        st_wt64(P.fin_part + 12 * blockIdx.x + k, t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add((gu32_t*)P.fin_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(kFinBlocks - 1);
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x < 12) {   // the workgroups' partials in workgroup order
+        const int k = threadIdx.x;
+        double t = ld_wt64(P.fin_part + k);
+        for (int g = 1; g < kFinBlocks; ++g) {
+            const double v = ld_wt64(P.fin_part + 12 * g + k);
+            t = k < 7 ? t + v : fmax(t, v);
+        }
         constexpr int kSlot[12] = {kScCost, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E, kScXnorm2F,
                                    kScStepnorm2F, kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScGmaxF};
         P.scal[kSlot[k]] = t;
         if (P.scal_host) P.scal_host[kSlot[k]] = t;
     }
+    if (threadIdx.x == 0)   // ready for the next launch (stream order)
+        __hip_atomic_store((gu32_t*)P.fin_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (P.scal_host) {
         // publish to host-mapped memory: every scalar, a system-scope fence,
         // then the sequence word the host polls (no blit, no stream sync)
@@ -2735,7 +2756,7 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
 }
 
 void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq) {
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinThreads), 0, s, P, ba_step_blocks(P), seq);
+    hipLaunchKernelGGL(finalize_kernel, dim3(kFinBlocks), dim3(kFinThreads), 0, s, P, ba_step_blocks(P), seq);
     SFM_HIP(hipGetLastError());
 }
 

@@ -51,7 +51,8 @@ struct sfm_ba_plan {
     DBuf<double> X0, Xa, Xb, extr0, intr0, ea, eb, ia, ib;
     DBuf<CamPre> cpa, cpb;
     DBuf<double> scaleE, scaleF, gram, rcs, Lcol, Larrow, zF, yF, Wg, part_u, part_s,
-        part_t, part_f, scal, bcr_buf;
+        part_t, part_f, scal, bcr_buf, fin_part;
+    DBuf<unsigned> fin_count;
     DBuf<int32_t> long_targets;
     DBuf<int32_t> gblk_off, gblk_col, gblk_z;   // general points
     DBuf<int64_t> gz_off;
@@ -364,6 +365,11 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     pl->part_f.alloc(3 * (size_t)P.n_fblk);
     P.part_f = pl->part_f.p;
     P.scal = pl->scal.p;
+    pl->fin_part.alloc(16 * 12);
+    pl->fin_count.alloc(1);
+    pl->fin_count.zero(s);
+    P.fin_part = pl->fin_part.p;
+    P.fin_count = pl->fin_count.p;
     // (SFM_CTX_BA_SEQ_BAND: the sequential band solver, 4-wide intrinsics arrows only)
     pl->use_bcr = !h.dense && bcr_supported(P) && (!(ctx->flags & SFM_CTX_BA_SEQ_BAND) || P.iw != 4);
     SFM_REQUIRE(h.dense || pl->use_bcr || P.iw == 4, SFM_ERR_UNSUPPORTED, "band solver: 4-wide intrinsics only");
@@ -497,6 +503,31 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     auto relinearize = [&] {
         ba_image_gram(P, S.cp, S.in, S.X, s);
     };
+    // After an accepted step the image Gram pass (U, b, cost at the new
+    // point) and the next Schur pass are independent until the reduce.  When
+    // the Schur launch leaves wave slots free (a shard at N > 1: C4's rank 0
+    // of 8 has 1600 one-wave chunks for 2048 slots), the Gram pass runs on
+    // the context's side stream beside it and the reduce waits for both; a
+    // Schur pass that fills the chip (C4 at N = 1) keeps the serial order.
+    const bool gram_side = P.n_group > 0 && (int64_t)P.n_group < 8 * (int64_t)ctx->cu_count;
+    bool gram_forked = false;
+    auto relinearize_step = [&] {
+        if (!gram_side) {
+            relinearize();
+            return;
+        }
+        hipStream_t s2 = ctx_side(ctx);
+        SFM_HIP(hipEventRecord(ctx->side_ev[0], s));
+        SFM_HIP(hipStreamWaitEvent(s2, ctx->side_ev[0], 0));
+        ba_image_gram(P, S.cp, S.in, S.X, s2);
+        SFM_HIP(hipEventRecord(ctx->side_ev[1], s2));
+        gram_forked = true;
+    };
+    auto join_gram = [&] {
+        if (!gram_forked) return;
+        SFM_HIP(hipStreamWaitEvent(s, ctx->side_ev[1], 0));
+        gram_forked = false;
+    };
 
     // ---- iteration zero: Jacobi scaling from the corrected Jacobian at x0 ----
     ba_campre(S.e, h.n_img, S.cp, s);
@@ -557,6 +588,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(ev[0], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
         if (timed) SFM_HIP(hipEventRecord(ev[1], s));
+        join_gram();
         // across ranks each shard writes only the blocks its own points touch,
         // so the summed system of the last iteration is cleared first
         if (ctx->world > 1 && h.dense)
@@ -657,7 +689,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * q - 1.0, 3));
             radius = std::min(O.max_trust_region_radius, radius);
             decrease_factor = 2.0;
-            relinearize();
+            relinearize_step();
             relin_pending = true;
             pending = cur;
             continue;   // Finalize after the gradient at the new x is known
