@@ -192,7 +192,6 @@ __device__ __forceinline__ v4d mm_rt(v4d acc, const GTile& g, PB B, int ldb, int
     return acc;
 }
 __device__ __forceinline__ lds_cd* L3(const double* p) { return (lds_cd*)p; }
-__device__ __forceinline__ glb_cd* G1(const double* p) { return (glb_cd*)p; }
 
 __device__ __forceinline__ v4d tile_ld(const double* C, int ldc, int r0, int c0) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
@@ -700,10 +699,12 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     double* Rc = Cr + 16 * LD;      // [64][17] column tile w of R_i
     double* bad = Rc + M * L16;
     double* col = bad + 2;          // [16] diag16 column scratch; stamp maxima (diagnostic)
+    unsigned* pdone = reinterpret_cast<unsigned*>(col + 16);   // [4] P(k) items done (window hand-off)
     unsigned long long* st = (b.stamps && w == 0) ? b.stamps : nullptr;
     unsigned long long t0 = 0, t1 = 0;
     if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
+    if (threadIdx.x < 4) pdone[threadIdx.x] = 0u;
     {   // every tile's loads in flight together, then the LDS stores
         TileFetch<64, M, NTL> fa, fwa, fwb;
         TileFetch<16, M, NTL> fcc, frc;
@@ -744,11 +745,13 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     //   W0  wave 0: A_00, diag16(0) | helpers: A updates of tiles (1,0),
     //       (2,0), (3,0), (1,1) as 8 half products (one per neighbour),
     //       C_0
-    //   P0  L_i0 = (A_i0 - halves) X_00'
-    //   W1  wave 0: A_11 (- halves - L_10 L_10'), diag16(1) | helpers:
-    //       tiles (2,1), (3,1), (2,2) (A update + step 0), T_10, C_1..3
-    //   P1, W2: tiles (3,2), (3,3) (A update + steps 0, 1), T_20, T_21, Cr
-    //   P2, W3: T_30, T_31, T_32, R_0..2;  P3 with R_3 on wave 4
+    //   W1  wave 0: its own panel L_10 = (A_10 - halves) X_00', A_11
+    //       (- halves - L_10 L_10'), diag16(1) | helpers: first the other
+    //       panels L_20, L_30 (P(0), counted in LDS), then tiles (2,1),
+    //       (3,1), (2,2) (A update + step 0), T_10, C_1..3
+    //   W2 (P(1) first): tiles (3,2), (3,3) (A update + steps 0, 1), T_20,
+    //       T_21, Cr
+    //   W3 (P(2) first): T_30, T_31, T_32, R_0..2;  P3 with R_3 on wave 4
     // upd: the neighbours eliminated at stride sp update A / R / C (every
     // level but the first, whose blocks come straight from bcr_pack)
     const bool upd = sp > 0;
@@ -946,65 +949,122 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     }
     wend(0);
     __syncthreads();
-    // ---- P0 -----------------------------------------------------------------
-    if (wave < 3) {
-        const int ii = 1 + wave;
-        tile_st(A, LD, 16 * ii, 0, sub_halves(tile_ld(A, LD, 16 * ii, 0), wave));
-        wave_sync();
-        tile_st(A, LD, 16 * ii, 0, tile_mm<false, true, false>(zero4(), L3(A), LD, 16 * ii, L3(X), LD, 0, 0, 16));
-    }
-    gs_k(0);
-    __syncthreads();
+    // ---- window hand-offs without a P phase (round 5) ------------------------
+    // P(k)'s products (the panels L_ik = A_ik X_kk', the inverse's row tile k,
+    // the forward substitution's G steps) run at the start of window k + 1
+    // instead of in a phase of their own between two barriers: the pivot
+    // wave forms its own panel L_{k+1,k} = (X_kk A_{k+1,k}')' as an MFMA
+    // result whose registers are at once the operands of A_{k+1,k+1} -=
+    // L L' (no LDS round trip, no barrier before its next diagonal factor),
+    // and the helpers wait on an LDS counter for P(k)'s six items before the
+    // window's own work.
+    constexpr unsigned kPItems = 6;   // wave 0's panel, two items on waves 1-2, the G steps on waves 5-7
+    auto p_signal = [&](int k) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(pdone + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto p_wait = [&](int k) {
+        while (__hip_atomic_load(pdone + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kPItems)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
+    // P(k)'s item of wave 1 or 2: a panel L_ik (k = 0: its A update's halves
+    // first) or an inverse tile X_kj = -X_kk T_kj
+    auto p_item = [&](int k) {
+        if (wave < 3 - k) {
+            const int ii = k + 1 + wave;
+            if (k == 0) {
+                tile_st(A, LD, 16 * ii, 0, sub_halves(tile_ld(A, LD, 16 * ii, 0), wave));
+                wave_sync();
+            }
+            tile_st(A, LD, 16 * ii, 16 * k,
+                    tile_mm<false, true, false>(zero4(), L3(A), LD, 16 * ii, L3(X), LD, 16 * k, 16 * k, 16 * k + 16));
+        } else {
+            const int j = wave - (3 - k);
+            tile_st(X, LD, 16 * k, 16 * j,
+                    tile_mm<false, false, true>(zero4(), L3(X), LD, 16 * k, L3(X), LD, 16 * j, 16 * k, 16 * k + 16));
+        }
+    };
+    // the pivot wave between diagonal factors k and k + 1
+    auto self_panel = [&](int k, v4d c) {
+        const int n = k + 1;
+        if (k == 0) {   // L_10's A update (the halves of tile (1, 0))
+            tile_st(A, LD, 16, 0, sub_halves(tile_ld(A, LD, 16, 0), 0));
+            wave_sync();
+        }
+        // Y = L_{n,k}' = X_kk A_{n,k}': element (kk + 4r, i) in register r
+        const v4d y = tile_mm<false, true, false>(zero4(), L3(X), LD, 16 * k, L3(A), LD, 16 * n, 16 * k, 16 * k + 16);
+        {   // L_{n,k} (= Y') for the helpers: transposed store, then the count
+            const int lane = threadIdx.x & 63, li = lane & 15, kk = lane >> 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(16 * n + li) * LD + 16 * k + kk + 4 * r] = y[r];
+        }
+        p_signal(k);
+        // A_nn -= L L' = Y' Y: the MFMA A operand of Y' and the B operand of Y
+        // are Y's own accumulator registers
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-y[r], y[r], c, 0, 0, 0);
+        dfac(n, c);
+    };
+    // every helper's start of window k + 1: its P(k) item or G step, the count, the wait
+    auto p_helpers = [&](int k) {
+        if (wave == 1 || wave == 2) p_item(k);
+        else if (wave >= 5) gs_k(k);
+        if (wave == 1 || wave == 2 || wave >= 5) p_signal(k);
+        if (wave != 4 || k == 2) p_wait(k);   // wave 4 (the pivot wave's SIMD mate) has work in W3 only
+    };
     // ---- W1 -----------------------------------------------------------------
     if (st) tw = stamp();
-    switch (wave) {
-        case 0: {
-            v4d acc = sub_halves(tile_ld(A, LD, 16, 16), 3);
-            dfac(1, tile_mm<false, true, true>(acc, L3(A), LD, 16, L3(A), LD, 16, 0, 16));
-            break;
+    if (wave == 0) {
+        self_panel(0, sub_halves(tile_ld(A, LD, 16, 16), 3));
+    } else {
+        p_helpers(0);
+        switch (wave) {
+            case 1: full(2, 1, 1); break;
+            case 2: full(3, 1, 1); break;
+            case 3: full(2, 2, 1); break;
+            case 5: { GTile g; fetch_wl(g); fs_lk(1); bgC(2, g); break; }
+            case 6: fs_rk(1); fs_zk(1); break;
+            case 7: { GTile g; fetch_wr(g); tinv(1, 0); bgCr(2, g); break; }
+            default: break;
         }
-        case 1: full(2, 1, 1); break;
-        case 2: full(3, 1, 1); break;
-        case 3: full(2, 2, 1); break;
-        case 5: { GTile g; fetch_wl(g); fs_lk(1); bgC(2, g); break; }
-        case 6: fs_rk(1); fs_zk(1); break;
-        case 7: { GTile g; fetch_wr(g); tinv(1, 0); bgCr(2, g); break; }
-        default: break;
     }
     wend(1);
     __syncthreads();
-    pphase(1);
-    gs_k(1);
-    __syncthreads();
     // ---- W2 -----------------------------------------------------------------
     if (st) tw = stamp();
-    switch (wave) {
-        case 0: dfac(2, tile_mm<false, true, true>(tile_ld(A, LD, 32, 32), L3(A), LD, 32, L3(A), LD, 32, 16, 32)); break;
-        case 1: full(3, 2, 2); break;
-        case 2: full(3, 3, 2); break;
-        case 3: tinv(2, 0); tinv(2, 1); break;
-        case 5: fs_lk(2); break;
-        case 6: fs_rk(2); break;
-        case 7: { GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); fs_zk(2); break; }
-        default: break;
+    if (wave == 0) {
+        self_panel(1, tile_ld(A, LD, 32, 32));
+    } else {
+        p_helpers(1);
+        switch (wave) {
+            case 1: full(3, 2, 2); break;
+            case 2: full(3, 3, 2); break;
+            case 3: tinv(2, 0); tinv(2, 1); break;
+            case 5: fs_lk(2); break;
+            case 6: fs_rk(2); break;
+            case 7: { GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); fs_zk(2); break; }
+            default: break;
+        }
     }
     wend(2);
     __syncthreads();
-    pphase(2);
-    gs_k(2);
-    __syncthreads();
     // ---- W3 -----------------------------------------------------------------
     if (st) tw = stamp();
-    switch (wave) {
-        case 0: dfac(3, tile_mm<false, true, true>(tile_ld(A, LD, 48, 48), L3(A), LD, 48, L3(A), LD, 48, 32, 48)); break;
-        case 1: tinv(3, 0); break;
-        case 2: tinv(3, 1); break;
-        case 3: tinv(3, 2); break;
-        case 4: if (w < 3) store_x(64, threadIdx.x & 63); break;   // no MFMA on the pivot wave's SIMD
-        case 5: { GTile g; fetch_wl(g); bgC(3, g); fs_lk(3); break; }
-        case 6: { GTile g; fetch_wr(g); bgCr(3, g); fs_rk(3); break; }
-        case 7: fs_zk(3); break;
-        default: break;
+    if (wave == 0) {
+        self_panel(2, tile_ld(A, LD, 48, 48));
+    } else {
+        p_helpers(2);
+        switch (wave) {
+            case 1: tinv(3, 0); break;
+            case 2: tinv(3, 1); break;
+            case 3: tinv(3, 2); break;
+            case 4: if (w < 3) store_x(64, threadIdx.x & 63); break;   // no MFMA on the pivot wave's SIMD
+            case 5: { GTile g; fetch_wl(g); bgC(3, g); fs_lk(3); break; }
+            case 6: { GTile g; fetch_wr(g); bgCr(3, g); fs_rk(3); break; }
+            case 7: fs_zk(3); break;
+            default: break;
+        }
     }
     wend(3);
     __syncthreads();
@@ -1482,7 +1542,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     hipLaunchKernelGGL(bcr_pack_kernel, dim3(16 * b.N), dim3(NT), 0, s, b, P, radius);
     SFM_HIP(hipGetLastError());
     const size_t ldr = b.nrhs + 1;
-    const size_t lds_odd = (2 * M * LD + 2 * M * M + 2 * M * 17 + 16 * LD + 18) * sizeof(double);
+    const size_t lds_odd = (2 * M * LD + 2 * M * M + 2 * M * 17 + 16 * LD + 20) * sizeof(double);
     const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);
     const size_t lds_l = std::max(lds_odd, lds_even);
     const size_t lds_t = (3 * M * LD + 3 * M * ldr + 34) * sizeof(double);
