@@ -955,21 +955,22 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     // instead of in a phase of their own between two barriers: the pivot
     // wave forms its own panel L_{k+1,k} = (X_kk A_{k+1,k}')' as an MFMA
     // result whose registers are at once the operands of A_{k+1,k+1} -=
-    // L L' (no LDS round trip, no barrier before its next diagonal factor),
-    // and the helpers wait on an LDS counter for P(k)'s six items before the
-    // window's own work.
-    constexpr unsigned kPItems = 6;   // wave 0's panel, two items on waves 1-2, the G steps on waves 5-7
-    auto p_signal = [&](int k) {
+    // L L' (no LDS round trip, no barrier before its next diagonal factor).
+    // Each wave publishes its P(k) item as bit `wave` of pdone[k], and each
+    // window product waits for the bits of exactly the items it reads
+    // (products with no P(k) input run before the wait).
+    auto p_sig = [&](int k) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(pdone + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(pdone + k, 1u << wave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    auto p_wait = [&](int k) {
-        while (__hip_atomic_load(pdone + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < kPItems)
+    auto p_wait = [&](int k, unsigned bits) {
+        while ((__hip_atomic_load(pdone + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bits) != bits)
             __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     };
+    constexpr unsigned kL = 1u, kW1 = 2u, kW2 = 4u, kW7 = 128u;   // L_{k+1,k} (wave 0), waves 1, 2, 7's items
     // P(k)'s item of wave 1 or 2: a panel L_ik (k = 0: its A update's halves
-    // first) or an inverse tile X_kj = -X_kk T_kj
+    // first) or an inverse tile X_kj = -X_kk T_kj; then its bit
     auto p_item = [&](int k) {
         if (wave < 3 - k) {
             const int ii = k + 1 + wave;
@@ -984,6 +985,12 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
             tile_st(X, LD, 16 * k, 16 * j,
                     tile_mm<false, false, true>(zero4(), L3(X), LD, 16 * k, L3(X), LD, 16 * j, 16 * k, 16 * k + 16));
         }
+        p_sig(k);
+    };
+    // waves 5-7: P(k)'s G steps, then their bits
+    auto p_g = [&](int k) {
+        gs_k(k);
+        p_sig(k);
     };
     // the pivot wave between diagonal factors k and k + 1
     auto self_panel = [&](int k, v4d c) {
@@ -994,77 +1001,63 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
         }
         // Y = L_{n,k}' = X_kk A_{n,k}': element (kk + 4r, i) in register r
         const v4d y = tile_mm<false, true, false>(zero4(), L3(X), LD, 16 * k, L3(A), LD, 16 * n, 16 * k, 16 * k + 16);
-        {   // L_{n,k} (= Y') for the helpers: transposed store, then the count
+        {   // L_{n,k} (= Y') for the helpers: transposed store, then the bit
             const int lane = threadIdx.x & 63, li = lane & 15, kk = lane >> 4;
 #pragma unroll
             for (int r = 0; r < 4; ++r) A[(16 * n + li) * LD + 16 * k + kk + 4 * r] = y[r];
         }
-        p_signal(k);
+        p_sig(k);
         // A_nn -= L L' = Y' Y: the MFMA A operand of Y' and the B operand of Y
         // are Y's own accumulator registers
 #pragma unroll
         for (int r = 0; r < 4; ++r) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-y[r], y[r], c, 0, 0, 0);
         dfac(n, c);
     };
-    // every helper's start of window k + 1: its P(k) item or G step, the count, the wait
-    auto p_helpers = [&](int k) {
-        if (wave == 1 || wave == 2) p_item(k);
-        else if (wave >= 5) gs_k(k);
-        if (wave == 1 || wave == 2 || wave >= 5) p_signal(k);
-        if (wave != 4 || k == 2) p_wait(k);   // wave 4 (the pivot wave's SIMD mate) has work in W3 only
-    };
     // ---- W1 -----------------------------------------------------------------
     if (st) tw = stamp();
-    if (wave == 0) {
-        self_panel(0, sub_halves(tile_ld(A, LD, 16, 16), 3));
-    } else {
-        p_helpers(0);
-        switch (wave) {
-            case 1: full(2, 1, 1); break;
-            case 2: full(3, 1, 1); break;
-            case 3: full(2, 2, 1); break;
-            case 5: { GTile g; fetch_wl(g); fs_lk(1); bgC(2, g); break; }
-            case 6: fs_rk(1); fs_zk(1); break;
-            case 7: { GTile g; fetch_wr(g); tinv(1, 0); bgCr(2, g); break; }
-            default: break;
-        }
+    switch (wave) {
+        case 0: self_panel(0, sub_halves(tile_ld(A, LD, 16, 16), 3)); break;
+        case 1: p_item(0); p_wait(0, kL); full(2, 1, 1); break;                    // L_20
+        case 2: p_item(0); p_wait(0, kL); full(3, 1, 1); break;                    // L_30
+        case 3: p_wait(0, kW1); full(2, 2, 1); break;
+        case 5: { p_g(0); GTile g; fetch_wl(g); bgC(2, g); p_wait(0, kL); fs_lk(1); break; }
+        case 6: p_g(0); p_wait(0, kL); fs_rk(1); p_wait(0, kW7); fs_zk(1); break;
+        case 7: { p_g(0); GTile g; fetch_wr(g); bgCr(2, g); p_wait(0, kL); tinv(1, 0); break; }
+        default: break;
     }
     wend(1);
     __syncthreads();
     // ---- W2 -----------------------------------------------------------------
     if (st) tw = stamp();
-    if (wave == 0) {
-        self_panel(1, tile_ld(A, LD, 32, 32));
-    } else {
-        p_helpers(1);
-        switch (wave) {
-            case 1: full(3, 2, 2); break;
-            case 2: full(3, 3, 2); break;
-            case 3: tinv(2, 0); tinv(2, 1); break;
-            case 5: fs_lk(2); break;
-            case 6: fs_rk(2); break;
-            case 7: { GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); fs_zk(2); break; }
-            default: break;
-        }
+    switch (wave) {
+        case 0: self_panel(1, tile_ld(A, LD, 32, 32)); break;
+        case 1: p_item(1); p_wait(1, kL); full(3, 2, 2); break;                    // L_31
+        case 2: p_item(1); p_wait(1, kW1); full(3, 3, 2); break;                   // X_10
+        case 3: p_wait(1, kL | kW2); tinv(2, 0); tinv(2, 1); break;
+        case 5: p_g(1); p_wait(1, kL); fs_lk(2); break;
+        case 6: p_g(1); p_wait(1, kL); fs_rk(2); break;
+        case 7: { p_g(1); GTile z1, z2; fetch_z(z1, z2); bgR(3, z1, z2); p_wait(1, kL); fs_zk(2); break; }
+        default: break;
     }
     wend(2);
     __syncthreads();
     // ---- W3 -----------------------------------------------------------------
     if (st) tw = stamp();
-    if (wave == 0) {
-        self_panel(2, tile_ld(A, LD, 48, 48));
-    } else {
-        p_helpers(2);
-        switch (wave) {
-            case 1: tinv(3, 0); break;
-            case 2: tinv(3, 1); break;
-            case 3: tinv(3, 2); break;
-            case 4: if (w < 3) store_x(64, threadIdx.x & 63); break;   // no MFMA on the pivot wave's SIMD
-            case 5: { GTile g; fetch_wl(g); bgC(3, g); fs_lk(3); break; }
-            case 6: { GTile g; fetch_wr(g); bgCr(3, g); fs_rk(3); break; }
-            case 7: fs_zk(3); break;
-            default: break;
-        }
+    switch (wave) {
+        case 0: self_panel(2, tile_ld(A, LD, 48, 48)); break;
+        case 1: p_item(2); p_wait(2, kL); tinv(3, 0); break;                       // X_20
+        case 2: p_item(2); p_wait(2, kL); tinv(3, 1); break;                       // X_21
+        case 3: p_wait(2, kL); tinv(3, 2); break;
+        case 4:   // no MFMA on the pivot wave's SIMD; row tile 2 of X is final with X_20, X_21
+            if (w < 3) {
+                if (w == 2) p_wait(2, kW1 | kW2);
+                store_x(64, threadIdx.x & 63);
+            }
+            break;
+        case 5: { p_g(2); GTile g; fetch_wl(g); bgC(3, g); p_wait(2, kL); fs_lk(3); break; }
+        case 6: { p_g(2); GTile g; fetch_wr(g); bgCr(3, g); p_wait(2, kL); fs_rk(3); break; }
+        case 7: p_g(2); p_wait(2, kL); fs_zk(3); break;
+        default: break;
     }
     wend(3);
     __syncthreads();
