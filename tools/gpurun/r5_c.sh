@@ -25,6 +25,7 @@ for W in 1 8; do
   f=$(find "$OUT/p$W" -name "*kernel_stats.csv" | head -1); cp "$f" "$OUT/kernel_stats_n$W.csv"
   f=$(find "$OUT/p$W" -name "*kernel_trace.csv" | head -1)
   python3 "$GRAFT_REPO_ROOT/tools/bcr_levels.py" "$f" | tee "$OUT/bcr_levels_n$W.txt"
+  python3 "$GRAFT_REPO_ROOT/tools/iter_gaps.py" "$f" | tee "$OUT/iter_gaps_n$W.txt"
   rm -rf "$OUT/p$W"
 done
 python3 "$GRAFT_REPO_ROOT/tools/kstat_brief.py" "$OUT/kernel_stats_n1.csv" "$OUT/kernel_stats_n8.csv" | tee "$OUT/kstat_brief.txt"
