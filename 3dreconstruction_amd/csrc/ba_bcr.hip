@@ -57,6 +57,13 @@ __device__ __forceinline__ double solve_verdict(const double* fail) {
     return t != 0.0 ? kSolveWaitTimeout : __hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// after the verdict: the failure words start the next solve cleared (they
+// are zeroed once at allocation; no pack launch clears them)
+__device__ __forceinline__ void reset_verdict(const BcrArgs& b) {
+    __hip_atomic_store(b.fail, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(b.fail + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
 
 // Global-address-space agent-scope accesses for words handed between
@@ -536,87 +543,107 @@ __device__ __forceinline__ void chol_inv64(double* A, double* X, double* bad, do
 }
 
 // ---- pack: band (6x6 blocks) -> 64x64 super-blocks, D^2 added, identity pad --
+// Element (r, c) of super-block I's A, C (block (I, I-1)) and R, gathered from
+// the reduced band: every load is issued unconditionally from a clamped
+// address and the value selected after, so a caller's unrolled loop keeps all
+// its loads in flight.  The first level kernel gathers its blocks this way
+// (bcr_pack_kernel remains for a band of one super-block).
+struct PackIdx {
+    int c0, nreal;
+    __device__ PackIdx(const BcrArgs& b, const DevProblem& P, int I)
+        : c0(I * b.K), nreal(min(b.K, P.ncam - I * b.K) * 6) {}
+};
+__device__ __forceinline__ double pack_a(const BcrArgs& b, const DevProblem& P, double radius, int I, int r, int c) {
+    const PackIdx x(b, P, I);
+    const int Dp = P.D + 1;
+    const bool real = r < x.nreal && c < x.nreal;
+    const int ci = x.c0 + r / 6, cj = x.c0 + c / 6;
+    const int hi = max(ci, cj), lo = min(ci, cj), d = hi - lo;
+    const bool inband = real && d <= P.D;
+    // A: block (ci, cj) with cj in this super-block, cj <= ci (lower), mirror upper
+    const int rr = ci >= cj ? r % 6 : c % 6, cc = ci >= cj ? c % 6 : r % 6;
+    const double v = P.Sband[inband ? ((size_t)hi * Dp + d) * 36 + rr * 6 + cc : 0];
+    const double cn = P.cnF[real ? 6LL * ci + r % 6 : 0];
+    double a = inband ? v : 0.0;
+    if (real && r == c) {
+        const double lm = sqrt(clampd(cn, P.min_diag, P.max_diag) / radius);
+        a += lm * lm;
+    }
+    return r >= x.nreal && r == c ? 1.0 : a;   // padding: identity
+}
+__device__ __forceinline__ double pack_c(const BcrArgs& b, const DevProblem& P, int I, int r, int c) {
+    // block (ci, cj) with cj in the previous super-block (always full)
+    const PackIdx x(b, P, I);
+    const int Dp = P.D + 1;
+    const int ci = x.c0 + r / 6, cj = x.c0 - b.K + c / 6, d = ci - cj;
+    const bool ok = I > 0 && r < x.nreal && c / 6 < b.K && d >= 1 && d <= P.D;
+    const double v = P.Sband[ok ? ((size_t)ci * Dp + d) * 36 + (r % 6) * 6 + c % 6 : 0];
+    return ok ? v : 0.0;
+}
+// R: column 0 = rhs, columns 1 + iw k + a = arrow (intr k, row a) transposed
+__device__ __forceinline__ double pack_r(const BcrArgs& b, const DevProblem& P, int I, int r, int c) {
+    const PackIdx x(b, P, I);
+    const int ci = x.c0 + r / 6;
+    const bool real = r < x.nreal;
+    const bool rhs = real && c == 0, arrow = real && c > 0 && c - 1 < P.iw * P.nintr;
+    const int k = (c - 1) / P.iw, a = (c - 1) % P.iw;
+    const double vr = P.rhs[rhs ? 6LL * ci + r % 6 : 0];
+    const double va = P.Sarrow[arrow ? ((size_t)k * P.ncam + ci) * 6 * P.iw + a * 6 + r % 6 : 0];
+    return rhs ? vr : arrow ? va : 0.0;
+}
+// rows [r0, r0 + 16) of super-block I's A and R, gathered to global memory
+// (the first level kernel, for the even blocks beside its odd ones)
+template <int TH>
+__device__ __forceinline__ void pack_rows(const BcrArgs& b, const DevProblem& P, double radius, int I, int r0, int t) {
+    double* A = b.A + (size_t)I * M * M + (size_t)r0 * M;
+    double* R = b.R + (size_t)I * M * b.nrhs + (size_t)r0 * b.nrhs;
+    constexpr int NA = 16 * M / TH;
+    double va[NA];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+        const int e = t + q * TH;
+        va[q] = pack_a(b, P, radius, I, r0 + e / M, e % M);
+    }
+#pragma unroll
+    for (int q = 0; q < NA; ++q) A[t + q * TH] = va[q];
+    for (int e = t; e < 16 * b.nrhs; e += TH) R[e] = pack_r(b, P, I, r0 + e / b.nrhs, e % b.nrhs);
+}
+
 // One workgroup per 4 rows of a super-block (N * 16 workgroups).
 __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
     const int I = blockIdx.x >> 4, rg = blockIdx.x & 15;
     double* A = b.A + (size_t)I * M * M;
     double* Cm = b.C + (size_t)I * M * M;
     double* R = b.R + (size_t)I * M * b.nrhs;
-    const int c0 = I * b.K, nreal = min(b.K, P.ncam - c0) * 6;
-    const int Dp = P.D + 1;
     {
         const int e = 4 * rg * M + threadIdx.x;   // NT = 4 rows x 64 columns
         const int r = e / M, c = e % M;
-        double a = 0.0, cc = 0.0;
-        if (r < nreal) {
-            const int ci = c0 + r / 6;
-            // A: block (ci, cj) with cj in this super-block, cj <= ci (lower), mirror upper
-            if (c < nreal) {
-                const int cj = c0 + c / 6;
-                const int hi = max(ci, cj), lo = min(ci, cj);
-                const int d = hi - lo;
-                if (d <= P.D) {
-                    const int rr = ci >= cj ? r % 6 : c % 6, cc2 = ci >= cj ? c % 6 : r % 6;
-                    a = P.Sband[((size_t)hi * Dp + d) * 36 + rr * 6 + cc2];
-                }
-                if (r == c) {
-                    const double lm = sqrt(clampd(P.cnF[6LL * ci + r % 6], P.min_diag, P.max_diag) / radius);
-                    a += lm * lm;
-                }
-            }
-            // C: block (ci, cj) with cj in the previous super-block
-            if (I > 0 && c / 6 < b.K) {   // the previous super-block is always full
-                const int cj = c0 - b.K + c / 6;
-                const int d = ci - cj;
-                if (d >= 1 && d <= P.D) cc = P.Sband[((size_t)ci * Dp + d) * 36 + (r % 6) * 6 + c % 6];
-            }
-        } else if (r == c) {
-            a = 1.0;  // padding: identity
-        }
-        A[e] = a;
-        Cm[e] = cc;
+        A[e] = pack_a(b, P, radius, I, r, c);
+        Cm[e] = pack_c(b, P, I, r, c);
     }
-    // R: column 0 = rhs, columns 1 + iw k + a = arrow (intr k, row a) transposed
-    for (int e = 4 * rg * b.nrhs + threadIdx.x; e < 4 * (rg + 1) * b.nrhs; e += NT) {
-        const int r = e / b.nrhs, c = e % b.nrhs;
-        double v = 0.0;
-        if (r < nreal) {
-            const int ci = c0 + r / 6;
-            if (c == 0) v = P.rhs[6LL * ci + r % 6];
-            else if (c - 1 < P.iw * P.nintr) {
-                const int k = (c - 1) / P.iw, a = (c - 1) % P.iw;
-                v = P.Sarrow[((size_t)k * P.ncam + ci) * 6 * P.iw + a * 6 + r % 6];
-            }
-        }
-        R[e] = v;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        b.fail[0] = 0.0;   // numerical failure
-        b.fail[1] = 0.0;   // dataflow wait timeout
-        reinterpret_cast<unsigned*>(b.fail + 4)[0] = 0u;   // bcr_corner_kernel's finished workgroups
-        reinterpret_cast<unsigned*>(b.fail + 5)[0] = 0u;   // bcr_back_kernel<true>'s
-    }
+    for (int e = 4 * rg * b.nrhs + threadIdx.x; e < 4 * (rg + 1) * b.nrhs; e += NT)
+        R[e] = pack_r(b, P, I, e / b.nrhs, e % b.nrhs);
 }
 
 // ---- update of one 16-row tile w of an even block j after eliminating its odd
 // neighbours at stride s (they hold Wl = L^-1 C, Wr = L^-1 C_r', z = L^-1 R):
-// A_j -= Wr_{j-s}' Wr_{j-s} + Wl_{j+s}' Wl_{j+s};  R_j -= Wr' z + Wl' z;
-// new coupling C_j (block (j, j-2s)) = -Wr_{j-s}' Wl_{j-s}.  Wave v: tile (w, v).
+// A_j -= Wr_{j-s}' Wr_{j-s} + Wl_{j+s}' Wl_{j+s};  R_j -= Wr' z + Wl' z.
+// (The new coupling C_j is not formed: every odd block after the first level
+// forms its C_i and C_r from the neighbours' W blocks itself.)  Wave v: tile (w, v).
 template <int TH>
 __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* sm) {
     const int ldr = b.nrhs + 1;
     double* Wa = sm;               // Wr_{j-s}
     double* Wb = Wa + M * LD;      // Wl_{j+s}
-    double* Wc = Wb + M * LD;      // Wl_{j-s}
-    double* Za = Wc + M * LD;      // z_{j-s}
+    double* Za = Wb + M * LD;      // z_{j-s}
     double* Zb = Za + M * ldr;     // z_{j+s}
     // waves 0..3: A tile (w, v); waves 4..7: R and C tiles (w, v - 4)
     const int il = j - s, ir = j + s, wv = threadIdx.x >> 6, v = wv & 3;
-    const bool hl = il >= 0, hr = ir < b.N, hc = hl && j - 2 * s >= 0;
+    const bool hl = il >= 0, hr = ir < b.N;
     // every tile's loads in flight together (nrhs is 16 or 32: bcr_supported)
     auto loads = [&](auto ncz) {
         constexpr int NCZ = decltype(ncz)::value;
-        TileFetch<64, M, TH> fwa, fwb, fwc;
+        TileFetch<64, M, TH> fwa, fwb;
         TileFetch<NCZ, M, TH> fza, fzb;
         if (hl) {
             fwa.fetch(b.Wr + (size_t)il * M * M, M);
@@ -626,7 +653,6 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
             fwb.fetch(b.Wl + (size_t)ir * M * M, M);
             fzb.fetch(b.Z + (size_t)ir * M * b.nrhs, b.nrhs);
         }
-        if (hc) fwc.fetch(b.Wl + (size_t)il * M * M, M);
         if (hl) {
             fwa.put(Wa, LD);
             fza.put(Za, ldr);
@@ -635,7 +661,6 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
             fwb.put(Wb, LD);
             fzb.put(Zb, ldr);
         }
-        if (hc) fwc.put(Wc, LD);
     };
     if (b.nrhs == 16) loads(std::integral_constant<int, 16>{});
     else loads(std::integral_constant<int, 32>{});
@@ -655,9 +680,6 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
         if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Zb), ldr, 16 * v, 0, M);
         tile_st(Rj, b.nrhs, 16 * w, 16 * v, acc);
     }
-    if (hc)
-        tile_st(b.C + (size_t)j * M * M, M, 16 * w, 16 * v,
-                mm_ll<true, false, true>(zero4(), L3(Wa), LD, 16 * w, L3(Wc), LD, 16 * v, 0, M));
 }
 
 // ---- one cyclic-reduction level at stride s, one launch --------------------------
@@ -669,10 +691,12 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
 //     w = 0 for the back substitution), and store column tile w of
 //     Wl = X C_i, Wr = X C_r', z = X R_i.
 //   even block j (items >= n_odd, s > 1): update(s/2) of its row tile w, stored.
-// At s = 1 the inputs come straight from bcr_pack.
+// At s = 1 the odd blocks gather their inputs straight from the reduced band
+// (pack_a / pack_c / pack_r) and pack the even blocks' A and R rows for the
+// later levels.
 constexpr int NTL = 512, NWL = NTL / 64;   // level kernel: 8 waves
 
-__global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_odd) {
+__global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P, double radius, int s, int n_odd) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     // XCD-aware: workgroup b runs on XCD b % 8, so the four workgroups (w) of
     // one item are b = x + 8 (4 j + w): the same XCD, whose L2 then serves the
@@ -705,22 +729,53 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, int s, int n_
     if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
     if (threadIdx.x < 4) pdone[threadIdx.x] = 0u;
-    {   // every tile's loads in flight together, then the LDS stores
+    if (sp == 0) {
+        // first level: gather the block straight from the reduced band (no
+        // pack launch), A, column tile w of C_i, row tile w of C_r and column
+        // tile w of R_i, every load in flight first; and rows 16w.. of the
+        // even blocks beside it (i - 1, and the last block when that is even)
+        // to global memory for the later levels and the top
+        constexpr int QA = M * M / NTL, QC = M * 16 / NTL;
+        double va[QA], vc[QC], vr[QC], vz[QC];
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int e = threadIdx.x + q * NTL;
+            va[q] = pack_a(b, P, radius, i, e / M, e % M);
+        }
+#pragma unroll
+        for (int q = 0; q < QC; ++q) {
+            const int e = threadIdx.x + q * NTL;
+            vc[q] = pack_c(b, P, i, e / 16, 16 * w + e % 16);
+            vr[q] = hr ? pack_c(b, P, r, 16 * w + e / M, e % M) : 0.0;
+            vz[q] = hz ? pack_r(b, P, i, e / 16, 16 * w + e % 16) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int e = threadIdx.x + q * NTL;
+            A[(e / M) * LD + e % M] = va[q];
+        }
+#pragma unroll
+        for (int q = 0; q < QC; ++q) {
+            const int e = threadIdx.x + q * NTL;
+            Cc[(e / 16) * L16 + e % 16] = vc[q];
+            Cr[(e / M) * LD + e % M] = vr[q];
+            Rc[(e / 16) * L16 + e % 16] = vz[q];
+        }
+        pack_rows<NTL>(b, P, radius, i - 1, 16 * w, threadIdx.x);
+        if (i + 1 == b.N - 1) pack_rows<NTL>(b, P, radius, i + 1, 16 * w, threadIdx.x);
+    } else {   // every tile's loads in flight together, then the LDS stores
+        // (C_i and C_r come from the neighbours' W blocks at every level after
+        // the first: bgC / bgCr overwrite all of Cc and Cr, so they are not loaded)
         TileFetch<64, M, NTL> fa, fwa, fwb;
-        TileFetch<16, M, NTL> fcc, frc;
-        TileFetch<64, 16, NTL> fcr;
-        const bool hwa = sp > 0, hwb = sp > 0 && i + sp < b.N;   // the neighbours' W blocks (the A update's operands)
+        TileFetch<16, M, NTL> frc;
+        const bool hwb = i + sp < b.N;   // the neighbours' W blocks (the A update's operands)
         fa.fetch(b.A + (size_t)i * M * M, M);
-        fcc.fetch(b.C + (size_t)i * M * M + 16 * w, M);
-        if (hr) fcr.fetch(b.C + (size_t)r * M * M + 16 * w * M, M);
         if (hz) frc.fetch(b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs);
-        if (hwa) fwa.fetch(b.Wr + (size_t)(i - sp) * M * M, M);
+        fwa.fetch(b.Wr + (size_t)(i - sp) * M * M, M);
         if (hwb) fwb.fetch(b.Wl + (size_t)(i + sp) * M * M, M);
         fa.put(A, LD);
-        fcc.put(Cc, L16);
-        if (hr) fcr.put(Cr, LD);
         if (hz) frc.put(Rc, L16);
-        if (hwa) fwa.put(Wa_l, M);
+        fwa.put(Wa_l, M);
         if (hwb) fwb.put(Wb_l, M);
     }
     __syncthreads();
@@ -1197,7 +1252,7 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
 // instead of the 1 + na columns (padded to 16) a bordered back substitution
 // carries.  One workgroup per block: wave 0 forms Q_i = z_i' z_i on the MFMA
 // and stores its rows 1..na, columns 0..na; the last workgroup to finish (an
-// agent-scope counter, reset by bcr_pack) adds the partials in block order
+// agent-scope counter, which it resets) adds the partials in block order
 // and solves the corner.
 // (z_fresh: this workgroup wrote z_I itself just before -- the top, in the
 // fused launch -- so wave 0 reads it write-through, past this CU's L1)
@@ -1262,6 +1317,7 @@ __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProbl
         last = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (!last) return;
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // partials of blocks [g N/8, (g+1) N/8) per lane, the 8 lanes of an
     // element then combined by a fixed xor butterfly (deterministic)
     auto sum_parts = [&](int off, int g) {
@@ -1493,13 +1549,19 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, i
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0 &&
-            __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1)
+            __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
             P.scal[kScSolveFail] = solve_verdict(b.fail);
+            reset_verdict(b);
+            __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
 // the verdict after per-level back substitution launches
-__global__ void bcr_verdict_kernel(BcrArgs b, DevProblem P) { P.scal[kScSolveFail] = solve_verdict(b.fail); }
+__global__ void bcr_verdict_kernel(BcrArgs b, DevProblem P) {
+    P.scal[kScSolveFail] = solve_verdict(b.fail);
+    reset_verdict(b);
+}
 
 }  // namespace
 
@@ -1532,11 +1594,13 @@ void bcr_bind(BcrArgs& b, double* base) {
 }
 
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
-    hipLaunchKernelGGL(bcr_pack_kernel, dim3(16 * b.N), dim3(NT), 0, s, b, P, radius);
-    SFM_HIP(hipGetLastError());
+    if (b.N == 1) {   // no level: the top reads the packed block
+        hipLaunchKernelGGL(bcr_pack_kernel, dim3(16 * b.N), dim3(NT), 0, s, b, P, radius);
+        SFM_HIP(hipGetLastError());
+    }
     const size_t ldr = b.nrhs + 1;
     const size_t lds_odd = (2 * M * LD + 2 * M * M + 2 * M * 17 + 16 * LD + 20) * sizeof(double);
-    const size_t lds_even = (3 * M * LD + 2 * M * ldr) * sizeof(double);
+    const size_t lds_even = (2 * M * LD + 2 * M * ldr) * sizeof(double);
     const size_t lds_l = std::max(lds_odd, lds_even);
     const size_t lds_t = (3 * M * LD + 3 * M * ldr + 34) * sizeof(double);
     {   // sized for the largest nrhs (32)
@@ -1548,8 +1612,8 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     for (int stride = 1; stride < b.N; stride *= 2) {
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
         const int n_even = stride > 1 ? (b.N + 2 * stride - 1) / (2 * stride) : 0;
-        hipLaunchKernelGGL(bcr_level_kernel, dim3(32 * ((n_odd + n_even + 7) / 8)), dim3(NTL), lds_l, s, b, stride,
-                           n_odd);
+        hipLaunchKernelGGL(bcr_level_kernel, dim3(32 * ((n_odd + n_even + 7) / 8)), dim3(NTL), lds_l, s, b, P, radius,
+                           stride, n_odd);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
