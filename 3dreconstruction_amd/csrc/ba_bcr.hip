@@ -94,13 +94,20 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // 1/sqrt(d): hardware estimate + two Newton steps (full fp64 accuracy)
+#ifndef SFM_AB_D16
+#define SFM_AB_D16 0
+#endif
 __device__ __forceinline__ double rsqrt_nr(double d) {
     double y = __builtin_amdgcn_rsq(d);
+#if SFM_AB_D16 & 1
+    y = fma(y, fma(-(0.5 * d * y), y, 0.5), y);
+#else
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
         const double hy = 0.5 * d * y;
         y = fma(y, fma(-hy, y, 0.5), y);
     }
+#endif
     return y;
 }
 
@@ -307,14 +314,20 @@ __device__ __forceinline__ double row_bcast(double v, int l) {
 // the first FMA of each group; tests/test_bcr_asm.py checks the schedule.
 #define SFM_FMAC_BC(n)                                                                                 \
     case n:                                                                                            \
-        if (NOP)                                                                                       \
+        if (NOP && NEG)                                                                                \
+            asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf" \
+                         : "+v"(acc) : "v"(src), "v"(mul));                                            \
+        else if (NOP)                                                                                  \
             asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf" \
+                         : "+v"(acc) : "v"(src), "v"(mul));                                            \
+        else if (NEG)                                                                                  \
+            asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf"  \
                          : "+v"(acc) : "v"(src), "v"(mul));                                            \
         else                                                                                           \
             asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf"   \
                          : "+v"(acc) : "v"(src), "v"(mul));                                            \
         break;
-template <bool NOP>
+template <bool NOP, bool NEG = false>
 __device__ __forceinline__ void fmac_bc(double& acc, double src, double mul, int l) {
     switch (l) {
         SFM_FMAC_BC(0) SFM_FMAC_BC(1) SFM_FMAC_BC(2) SFM_FMAC_BC(3) SFM_FMAC_BC(4) SFM_FMAC_BC(5)
@@ -339,10 +352,10 @@ template <int K, int... J>
 __device__ __forceinline__ void diag16_update(double (&a)[16], double nt, std::integer_sequence<int, J...>) {
     (fmac_bc<J == 0>(a[K + 1 + J], a[K], nt, K + 1 + J), ...);
 }
-template <int K, int... P>
+template <int K, bool NEG, int... P>
 __device__ __forceinline__ void diag16_xrow(const double (&a)[16], const double (&x)[16], double& u0, double& u1,
                                             std::integer_sequence<int, P...>) {
-    ((P & 1 ? fmac_bc<false>(u1, a[P], x[P], K) : fmac_bc<P == 0>(u0, a[P], x[P], K)), ...);
+    ((P & 1 ? fmac_bc<false, NEG>(u1, a[P], x[P], K) : fmac_bc<P == 0, NEG>(u0, a[P], x[P], K)), ...);
 }
 // The wave is VALU-issue bound here (one wave, fp64: ~8 cycles per
 // instruction), so each pivot is kept to few instructions: no select for the
@@ -359,9 +372,16 @@ __device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], in
     diag16_update<K>(a, nt, std::make_integer_sequence<int, 15 - K>{});
     a[K] = lk;
     // row K of L is final: lane c gets x_K = (delta_Kc - sum_p L_Kp x_p) / L_KK
+#if SFM_AB_D16 & 2
+    (void)i;
+    double u0 = x[K], u1 = 0.0;   // x holds the identity's column until row K is formed
+    diag16_xrow<K, true>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
+    x[K] = (u0 + u1) * rinv;
+#else
     double u0 = 0.0, u1 = 0.0;
-    diag16_xrow<K>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
+    diag16_xrow<K, false>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
     x[K] = ((K == i ? 1.0 : 0.0) - (u0 + u1)) * rinv;
+#endif
     if constexpr (K + 1 < NP) diag16_step<K + 1, NP>(a, x, i);
 }
 
@@ -390,6 +410,10 @@ __device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, d
     for (int j = 0; j < 16; ++j) a[j] = Al[(i & 15) * LD + j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? a[j] : 0.0;
+#if SFM_AB_D16 & 2
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
+#endif
     diag16_step<0, NP>(a, x, i);
 #pragma unroll
     for (int m = NP; m < 16; ++m) x[m] = m == i ? 1.0 : 0.0;   // identity padding (a keeps it)

@@ -511,7 +511,11 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     // of 8 has 1600 one-wave chunks for 2048 slots), the Gram pass runs on
     // the context's side stream beside it and the reduce waits for both; a
     // Schur pass that fills the chip (C4 at N = 1) keeps the serial order.
+#ifdef SFM_AB_SERIAL_GRAM   // A/B (tools/build_variant.sh), removed after the measurement
+    const bool gram_side = false;
+#else
     const bool gram_side = P.n_group > 0 && (int64_t)P.n_group < 8 * (int64_t)ctx->cu_count;
+#endif
     bool gram_forked = false;
     auto relinearize_step = [&] {
         if (!gram_side) {
