@@ -129,6 +129,23 @@ void ba_fscale(const DevProblem& P, hipStream_t s);
 // U / Ub / Ucn of a unit-scale ba_image_gram pass -> the same pass at scaleF
 void ba_gram_rescale(const DevProblem& P, hipStream_t s);
 void ba_fill(double* p, int64_t n, double v, hipStream_t s);
+// several copies / fills in one launch (a solve's start: the working point
+// from the plan's initial values, unit scales)
+struct Seg {
+    double* dst;
+    const double* src;   // null: fill with v
+    int64_t n;
+    double v;
+};
+struct SegList {
+    static constexpr int kSegs = 6;
+    Seg seg[kSegs];
+    int n = 0;
+    void add(double* d, const double* src, int64_t cnt, double v = 0.0) {
+        if (cnt > 0) seg[n++] = Seg{d, src, cnt, v};
+    }
+};
+void ba_segs(const SegList& L, hipStream_t s);
 // stamps (diagnostic builds only, else nullptr): per chunk 6 phase cycle sums
 // scale_e: also form the Jacobi point scales (scaleE) in this pass (the
 // solve's first pass, replacing ba_point_scale)

@@ -575,6 +575,16 @@ __global__ void fill_kernel(double* p, int64_t n, double v) {
     if (i < n) p[i] = v;
 }
 
+// up to kSegs copies (src) or fills (src null: value v) in one launch, grid-stride
+__global__ void segs_kernel(SegList L) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = 0; k < L.n; ++k) {
+        const Seg& g = L.seg[k];
+        for (int64_t j = i; j < g.n; j += stride) g.dst[j] = g.src ? g.src[j] : g.v;
+    }
+}
+
 __global__ void fscale_kernel(DevProblem P) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c < P.nF) P.scaleF[c] = 1.0 / (1.0 + sqrt(P.cnF[c]));
@@ -2606,6 +2616,15 @@ void ba_gram_rescale(const DevProblem& P, hipStream_t s) {
 void ba_fill(double* p, int64_t n, double v, hipStream_t s) {
     if (n <= 0) return;
     hipLaunchKernelGGL(fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, n, v);
+    SFM_HIP(hipGetLastError());
+}
+
+void ba_segs(const SegList& L, hipStream_t s) {
+    int64_t nmax = 0;
+    for (int k = 0; k < L.n; ++k) nmax = std::max(nmax, L.seg[k].n);
+    if (nmax <= 0) return;
+    const unsigned g = (unsigned)std::min<int64_t>((nmax + 255) / 256, 2048);
+    hipLaunchKernelGGL(segs_kernel, dim3(g), dim3(256), 0, s, L);
     SFM_HIP(hipGetLastError());
 }
 

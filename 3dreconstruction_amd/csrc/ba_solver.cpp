@@ -495,9 +495,19 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     // working buffers: a = current point, b = candidate
     IterState S{pl->Xa.p, pl->Xb.p, pl->ea.p, pl->eb.p, pl->ia.p, pl->ib.p, pl->cpa.p, pl->cpb.p};
     const size_t ne = 6 * (size_t)h.n_img, ni = (size_t)h.iw * h.n_intr, nx = 3 * (size_t)h.n_spt;
-    if (nx) SFM_HIP(hipMemcpyAsync(S.X, pl->X0.p, nx * 8, hipMemcpyDeviceToDevice, s));
-    SFM_HIP(hipMemcpyAsync(S.e, pl->extr0.p, ne * 8, hipMemcpyDeviceToDevice, s));
-    SFM_HIP(hipMemcpyAsync(S.in, pl->intr0.p, ni * 8, hipMemcpyDeviceToDevice, s));
+    // the working point from the plan's initial values, and the unit column
+    // scales of the unscaled iteration-0 pass, in one launch (three blits and
+    // two fills were five launches and, at a shard's size, host-bound gaps
+    // between them)
+    {
+        SegList L;
+        L.add(S.X, pl->X0.p, (int64_t)nx);
+        L.add(S.e, pl->extr0.p, (int64_t)ne);
+        L.add(S.in, pl->intr0.p, (int64_t)ni);
+        L.add(pl->scaleF.p, nullptr, std::max<int64_t>(h.nF, 1), 1.0);
+        L.add(pl->scaleE.p, nullptr, (int64_t)nx, 1.0);
+        ba_segs(L, s);
+    }
 
     auto allreduce_rcs = [&] {
         ctx_allreduce(ctx, pl->rcs.p, pl->rcs_n, 0, s);
@@ -537,10 +547,6 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
 
     // ---- iteration zero: Jacobi scaling from the corrected Jacobian at x0 ----
     ba_campre(S.e, h.n_img, S.cp, s);
-    // unit column scales for the unscaled iteration-0 pass, filled on the device
-    // (a host vector + 12 MB upload + sync here cost 0.5 ms per solve at C4)
-    ba_fill(pl->scaleF.p, std::max<int64_t>(h.nF, 1), 1.0, s);
-    ba_fill(pl->scaleE.p, (int64_t)nx, 1.0, s);
     if (O.jacobi_scaling) {
         relinearize();                 // unscaled column norms of the F blocks
         if (ctx->world > 1 && h.dense)

@@ -1,7 +1,9 @@
 """Per-level duration of the BCR launches from a rocprofv3 kernel trace
 (--kernel-trace --output-format csv: *_kernel_trace.csv): every RCS solve
-launches bcr_pack, one bcr_level per level, bcr_top_corner, bcr_back; the
-mean duration of each position in that sequence is printed (us).
+launches (bcr_pack for a one-block band,) one bcr_level per level,
+bcr_top_corner, bcr_back; the mean duration of each position in that
+sequence is printed (us).  A sequence starts at the first BCR launch after
+any other kernel.
     python tools/bcr_levels.py kernel_trace.csv"""
 import csv
 import sys
@@ -13,12 +15,13 @@ seqs, cur = [], None
 for r in rows:
     name = r["Kernel_Name"]
     if "bcr_" not in name:
+        cur = None
         continue
     short = name.replace("(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0].split("<")[0].split("::")[-1]
-    if short == "bcr_pack_kernel":
+    if cur is None:
         cur = []
         seqs.append(cur)
-    if cur is not None:
+    if True:
         cur.append((short, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
                     int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
 acc = defaultdict(list)
