@@ -64,6 +64,11 @@ __device__ __forceinline__ void reset_verdict(const BcrArgs& b) {
     __hip_atomic_store(b.fail + 1, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// rows of a super-block that can be nonzero in its W / z blocks (K cameras:
+// 6K real rows, rounded up to the MFMA's k step of 4): the products over
+// block rows stop here (C4, K = 9: 56 of 64, 2 of every 16 MFMAs skipped)
+__device__ __forceinline__ int bcr_kM(const BcrArgs& b) { return min(M, (6 * b.K + 3) & ~3); }
+
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
 
 // Global-address-space agent-scope accesses for words handed between
@@ -93,26 +98,20 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// 1/sqrt(d): hardware estimate + two Newton steps (full fp64 accuracy)
-#ifndef SFM_AB_D16
-#define SFM_AB_D16 0
-#endif
+// 1/sqrt(d): the hardware estimate (v_rsq_f64, relative error below 2^-22)
+// and one Newton step (relative error ~1e-13, well inside the solve's
+// tolerance; a second step cost 4 of the pivot's ~33 instructions:
+// tools/probe/diag16_variants.hip, profiles/r05/g_ab)
 __device__ __forceinline__ double rsqrt_nr(double d) {
-    double y = __builtin_amdgcn_rsq(d);
-#if SFM_AB_D16 & 1
-    y = fma(y, fma(-(0.5 * d * y), y, 0.5), y);
-#else
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-        const double hy = 0.5 * d * y;
-        y = fma(y, fma(-hy, y, 0.5), y);
-    }
-#endif
-    return y;
+    const double y = __builtin_amdgcn_rsq(d);
+    return fma(y, fma(-(0.5 * d * y), y, 0.5), y);
 }
 
 // One wave, one 16x16 output tile: acc += op(A)[ar.., k] op(B)[k, bc..] for
-// k in [k0, k1) (k1 - k0 a multiple of 16).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
+// k in [k0, k1) (k1 - k0 a multiple of 4; operands are read in 16-deep
+// chunks, so a partial last chunk reads past k1 but multiplies nothing there:
+// a super-block's K real cameras fill 6K of its 64 rows, and its W / z rows
+// beyond them are zero, so the products over block rows stop at kM(K)).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
 // op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.  The LDS
 // operands of the next 16-wide k chunk are read while the current chunk's four
 // MFMAs run, so a runtime-length product is not LDS-latency bound.
@@ -134,7 +133,8 @@ __device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int
         const bool more = k + 16 < k1;
         if (more) load(k + 16, an, bn);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+            if (4 * j < k1 - k) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
         if (more) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) { a[j] = an[j]; b[j] = bn[j]; }
@@ -177,9 +177,9 @@ struct GTile {
             for (int j = 0; j < 4; ++j) v[4 * c + j] = p[(16 * c + 4 * j + kk) * ld + i];
     }
 };
-// acc +/-= A[k][ar + m]' G[k][n], k = 0..63 (A in LDS, transposed)
+// acc +/-= A[k][ar + m]' G[k][n], k = 0..kM-1 (A in LDS, transposed)
 template <bool NEG, class PA>
-__device__ __forceinline__ v4d mm_tr(v4d acc, PA A, int lda, int ar, const GTile& g) {
+__device__ __forceinline__ v4d mm_tr(v4d acc, PA A, int lda, int ar, const GTile& g, int kM) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -187,13 +187,14 @@ __device__ __forceinline__ v4d mm_tr(v4d acc, PA A, int lda, int ar, const GTile
 #pragma unroll
         for (int j = 0; j < 4; ++j) a[j] = A[(16 * c + 4 * j + kk) * lda + ar + i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], g.v[4 * c + j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+            if (16 * c + 4 * j < kM) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], g.v[4 * c + j], acc, 0, 0, 0);
     }
     return acc;
 }
-// acc +/-= G[k][m]' B[k][bc + n], k = 0..63 (B in LDS)
+// acc +/-= G[k][m]' B[k][bc + n], k = 0..kM-1 (B in LDS)
 template <bool NEG, class PB>
-__device__ __forceinline__ v4d mm_rt(v4d acc, const GTile& g, PB B, int ldb, int bc) {
+__device__ __forceinline__ v4d mm_rt(v4d acc, const GTile& g, PB B, int ldb, int bc, int kM) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -201,7 +202,9 @@ __device__ __forceinline__ v4d mm_rt(v4d acc, const GTile& g, PB B, int ldb, int
 #pragma unroll
         for (int j = 0; j < 4; ++j) bv[j] = B[(16 * c + 4 * j + kk) * ldb + bc + i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -g.v[4 * c + j] : g.v[4 * c + j], bv[j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+            if (16 * c + 4 * j < kM)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -g.v[4 * c + j] : g.v[4 * c + j], bv[j], acc, 0, 0, 0);
     }
     return acc;
 }
@@ -371,17 +374,13 @@ __device__ __forceinline__ void diag16_step(double (&a)[16], double (&x)[16], in
     const double nt = -(lk * rinv);      // -a_iK / d_K
     diag16_update<K>(a, nt, std::make_integer_sequence<int, 15 - K>{});
     a[K] = lk;
-    // row K of L is final: lane c gets x_K = (delta_Kc - sum_p L_Kp x_p) / L_KK
-#if SFM_AB_D16 & 2
+    // row K of L is final: lane c gets x_K = (delta_Kc - sum_p L_Kp x_p) / L_KK;
+    // x holds the identity's column until row K is formed, so the sum starts
+    // from delta_Kc and subtracts (a negated DPP source: no select per pivot)
     (void)i;
-    double u0 = x[K], u1 = 0.0;   // x holds the identity's column until row K is formed
+    double u0 = x[K], u1 = 0.0;
     diag16_xrow<K, true>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
     x[K] = (u0 + u1) * rinv;
-#else
-    double u0 = 0.0, u1 = 0.0;
-    diag16_xrow<K, false>(a, x, u0, u1, std::make_integer_sequence<int, K>{});
-    x[K] = ((K == i ? 1.0 : 0.0) - (u0 + u1)) * rinv;
-#endif
     if constexpr (K + 1 < NP) diag16_step<K + 1, NP>(a, x, i);
 }
 
@@ -410,13 +409,10 @@ __device__ __forceinline__ void diag16_body(double* A, double* X, double* bad, d
     for (int j = 0; j < 16; ++j) a[j] = Al[(i & 15) * LD + j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) a[j] = (act && j <= i) ? a[j] : 0.0;
-#if SFM_AB_D16 & 2
 #pragma unroll
     for (int j = 0; j < 16; ++j) x[j] = j == i ? 1.0 : 0.0;
-#endif
     diag16_step<0, NP>(a, x, i);
-#pragma unroll
-    for (int m = NP; m < 16; ++m) x[m] = m == i ? 1.0 : 0.0;   // identity padding (a keeps it)
+    // (rows NP..15, the identity padding: x keeps the identity it started from, a keeps it too)
     double lii = 1.0;   // this lane's L_ii (a[i], extracted without dynamic indexing)
 #pragma unroll
     for (int j = 0; j < 16; ++j) lii = j == i ? a[j] : lii;
@@ -656,6 +652,7 @@ __global__ void bcr_pack_kernel(BcrArgs b, DevProblem P, double radius) {
 // forms its C_i and C_r from the neighbours' W blocks itself.)  Wave v: tile (w, v).
 template <int TH>
 __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* sm) {
+    const int kM = bcr_kM(b);
     const int ldr = b.nrhs + 1;
     double* Wa = sm;               // Wr_{j-s}
     double* Wb = Wa + M * LD;      // Wl_{j+s}
@@ -692,16 +689,16 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
     double* Aj = b.A + (size_t)j * M * M;
     if (wv < 4) {
         v4d acc = tile_ld(Aj, M, 16 * w, 16 * v);
-        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Wa), LD, 16 * v, 0, M);
-        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Wb), LD, 16 * v, 0, M);
+        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Wa), LD, 16 * v, 0, kM);
+        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Wb), LD, 16 * v, 0, kM);
         tile_st(Aj, M, 16 * w, 16 * v, acc);
         return;
     }
     if (16 * v < b.nrhs) {
         double* Rj = b.R + (size_t)j * M * b.nrhs;
         v4d acc = tile_ld(Rj, b.nrhs, 16 * w, 16 * v);
-        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Za), ldr, 16 * v, 0, M);
-        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Zb), ldr, 16 * v, 0, M);
+        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Za), ldr, 16 * v, 0, kM);
+        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Zb), ldr, 16 * v, 0, kM);
         tile_st(Rj, b.nrhs, 16 * w, 16 * v, acc);
     }
 }
@@ -737,6 +734,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     const int r = i + s, wave = threadIdx.x >> 6;
     const bool hr = r < b.N, hz = 16 * w < b.nrhs;
     const int np3 = 6 * b.K - 48;   // real pivots of the last diagonal tile
+    const int kM = bcr_kM(b);
     constexpr int L16 = 17;
     double* A = sm;                 // [64][LD]
     double* X = A + M * LD;         // [64][LD]
@@ -855,7 +853,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         const int ti = kHt[h >> 1][0], tj = kHt[h >> 1][1];
         double* W = (h & 1) ? Wbl : Wal;
         if ((h & 1) && !hir) return;
-        tile_st(hp(h), LD, 0, 0, mm_ll<true, false, false>(zero4(), L3(W), M, 16 * ti, L3(W), M, 16 * tj, 0, M));
+        tile_st(hp(h), LD, 0, 0, mm_ll<true, false, false>(zero4(), L3(W), M, 16 * ti, L3(W), M, 16 * tj, 0, kM));
     };
     auto sub_halves = [&](v4d acc, int t) {   // acc - half a - half b of tile t (fixed order)
         if (!upd) return acc;
@@ -866,14 +864,19 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // tile (ti, tj): its A update, then the trailing updates of steps 0..nk-1
     auto full = [&](int ti, int tj, int nk) {
         v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-        if (upd) acc = mm_ll<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, 0, M);
-        if (hir) acc = mm_ll<true, false, true>(acc, L3(Wbl), M, 16 * ti, L3(Wbl), M, 16 * tj, 0, M);
+        if (upd) acc = mm_ll<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, 0, kM);
+        if (hir) acc = mm_ll<true, false, true>(acc, L3(Wbl), M, 16 * ti, L3(Wbl), M, 16 * tj, 0, kM);
         for (int k = 0; k < nk; ++k)
             acc = mm_ll<false, true, true>(acc, L3(A), LD, 16 * ti, L3(A), LD, 16 * tj, 16 * k, 16 * k + 16);
         tile_st(A, LD, 16 * ti, 16 * tj, acc);
     };
-    // T_nj = sum_{m=j..n-1} L_nm X_mj into X tile (n, j)
+    // T_nj = sum_{m=j..n-1} L_nm X_mj into X tile (n, j).  Of X = L^-1 this
+    // workgroup needs only row tile w (stored for the back substitution) and
+    // the rows above it that row w is formed from: the forward substitution
+    // and the panels read X's diagonal tiles only.  Rows n > w are skipped
+    // (C4: workgroup 0, which also carries the R column, forms none).
     auto tinv = [&](int n, int j) {
+        if (n > w) return;
         tile_st(X, LD, 16 * n, 16 * j, mm_ll<false, false, false>(zero4(), L3(A), LD, 16 * n, L3(X), LD, 16 * j, 16 * j, 16 * n));
     };
     // neighbour products; g*: the global operands, fetched into registers by
@@ -882,15 +885,15 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     auto bgR = [&](int v, const GTile& g1, const GTile& g2) {   // R_i[:, w] row tile v
         if (!hzu) return;
         v4d acc = tile_ld(Rc, L16, 16 * v, 0);
-        acc = mm_tr<true>(acc, L3(Wal), M, 16 * v, g1);
-        if (hir) acc = mm_tr<true>(acc, L3(Wbl), M, 16 * v, g2);
+        acc = mm_tr<true>(acc, L3(Wal), M, 16 * v, g1, kM);
+        if (hir) acc = mm_tr<true>(acc, L3(Wbl), M, 16 * v, g2, kM);
         tile_st(Rc, L16, 16 * v, 0, acc);
     };
     auto bgC = [&](int v, const GTile& gl) {   // block (i, i-2sp) = (i, i-s)
-        if (upd) tile_st(Cc, L16, 16 * v, 0, mm_tr<true>(zero4(), L3(Wal), M, 16 * v, gl));
+        if (upd) tile_st(Cc, L16, 16 * v, 0, mm_tr<true>(zero4(), L3(Wal), M, 16 * v, gl, kM));
     };
     auto bgCr = [&](int v, const GTile& gr) {   // block (r, r-s) = (r, i)
-        if (hr && hir) tile_st(Cr, LD, 0, 16 * v, mm_rt<true>(zero4(), gr, L3(Wbl), M, 16 * v));
+        if (hr && hir) tile_st(Cr, LD, 0, 16 * v, mm_rt<true>(zero4(), gr, L3(Wbl), M, 16 * v, kM));
     };
     auto fetch_z = [&](GTile& g1, GTile& g2) {
         if (!hzu) return;
@@ -906,6 +909,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // P(k), k >= 1: panels L_ik = A_ik X_kk' (i > k) and X_kj = -X_kk T_kj (j < k), waves 0..2
     auto pphase = [&](int k) {
         if (wave >= 3) return;
+        if (wave >= 3 - k && k > w) return;   // X row tile k: not needed here (tinv)
         if (wave < 3 - k) {
             const int ii = k + 1 + wave;
             tile_st(A, LD, 16 * ii, 16 * k,
@@ -945,8 +949,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     {
         const int v = wave & 3;
         v4d part = zero4();
-        if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, 16 * v + 16);
-        else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, 16 * v + 16);
+        const int k1 = min(16 * v + 16, kM);
+        if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, k1);
+        else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, k1);
         if (upd) tile_st(tile_at(1, kS0[wave][0], kS0[wave][1]), LD, 0, 0, part);
     }
     __syncthreads();
@@ -1059,7 +1064,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
             }
             tile_st(A, LD, 16 * ii, 16 * k,
                     tile_mm<false, true, false>(zero4(), L3(A), LD, 16 * ii, L3(X), LD, 16 * k, 16 * k, 16 * k + 16));
-        } else {
+        } else if (k <= w) {   // X row tile k: not needed here otherwise (tinv)
             const int j = wave - (3 - k);
             tile_st(X, LD, 16 * k, 16 * j,
                     tile_mm<false, false, true>(zero4(), L3(X), LD, 16 * k, L3(X), LD, 16 * j, 16 * k, 16 * k + 16));
@@ -1173,6 +1178,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
 // sp > 0: first block 0's update from its right neighbour sp, eliminated by
 // the last level (A_0 -= Wl_sp' Wl_sp, R_0 -= Wl_sp' z_sp; lower tiles only).
 __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* sm) {
+    const int kM = bcr_kM(b);
     const int ldr = b.nrhs + 1;
     double* A = sm;
     double* X = A + M * LD;
@@ -1214,7 +1220,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, M);
+            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, kM);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         };
         const int nrt = b.nrhs / 16;
@@ -1222,7 +1228,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
             double* scr = X + 16 * LD;
             if (wave < 4)
                 tile_st(scr + 256 * wave, 16, 0, 0,
-                        tile_mm<true, false, false>(zero4(), Wb, LD, 0, Wb, LD, 0, 16 * wave, 16 * wave + 16));
+                        tile_mm<true, false, false>(zero4(), Wb, LD, 0, Wb, LD, 0, 16 * wave, min(16 * wave + 16, kM)));
         }
         __syncthreads();
         auto pre0 = [&] {
@@ -1239,7 +1245,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
                 } else {
                     const int v = (t - 9) / nrt, tj = (t - 9) % nrt;
                     v4d acc = tile_ld(R, ldr, 16 * v, 16 * tj);
-                    acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, M);
+                    acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, kM);
                     tile_st(R, ldr, 16 * v, 16 * tj, acc);
                 }
             }

@@ -515,36 +515,6 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     auto relinearize = [&] {
         ba_image_gram(P, S.cp, S.in, S.X, s);
     };
-    // After an accepted step the image Gram pass (U, b, cost at the new
-    // point) and the next Schur pass are independent until the reduce.  When
-    // the Schur launch leaves wave slots free (a shard at N > 1: C4's rank 0
-    // of 8 has 1600 one-wave chunks for 2048 slots), the Gram pass runs on
-    // the context's side stream beside it and the reduce waits for both; a
-    // Schur pass that fills the chip (C4 at N = 1) keeps the serial order.
-#ifdef SFM_AB_SERIAL_GRAM   // A/B (tools/build_variant.sh), removed after the measurement
-    const bool gram_side = false;
-#else
-    const bool gram_side = P.n_group > 0 && (int64_t)P.n_group < 8 * (int64_t)ctx->cu_count;
-#endif
-    bool gram_forked = false;
-    auto relinearize_step = [&] {
-        if (!gram_side) {
-            relinearize();
-            return;
-        }
-        hipStream_t s2 = ctx_side(ctx);
-        SFM_HIP(hipEventRecord(ctx->side_ev[0], s));
-        SFM_HIP(hipStreamWaitEvent(s2, ctx->side_ev[0], 0));
-        ba_image_gram(P, S.cp, S.in, S.X, s2);
-        SFM_HIP(hipEventRecord(ctx->side_ev[1], s2));
-        gram_forked = true;
-    };
-    auto join_gram = [&] {
-        if (!gram_forked) return;
-        SFM_HIP(hipStreamWaitEvent(s, ctx->side_ev[1], 0));
-        gram_forked = false;
-    };
-
     // ---- iteration zero: Jacobi scaling from the corrected Jacobian at x0 ----
     ba_campre(S.e, h.n_img, S.cp, s);
     if (O.jacobi_scaling) {
@@ -600,7 +570,6 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         if (timed) SFM_HIP(hipEventRecord(ev[0], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);
         if (timed) SFM_HIP(hipEventRecord(ev[1], s));
-        join_gram();
         // across ranks each shard writes only the blocks its own points touch,
         // so the summed system of the last iteration is cleared first
         if (ctx->world > 1 && h.dense)
@@ -701,7 +670,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * q - 1.0, 3));
             radius = std::min(O.max_trust_region_radius, radius);
             decrease_factor = 2.0;
-            relinearize_step();
+            relinearize();
             relin_pending = true;
             pending = cur;
             continue;   // Finalize after the gradient at the new x is known

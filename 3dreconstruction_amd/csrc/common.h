@@ -230,24 +230,12 @@ struct sfm_ctx {
         return v ? 1 << (v - 1) : 0;
     }
     hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
-    hipStream_t side = nullptr;                  // second stream (BA: the image Gram pass beside the Schur pass)
-    hipEvent_t side_ev[2] = {nullptr, nullptr};  // fork / join events of the side stream
     double last_kernel_ms = -1.0;                // sfm_fmatrix_ac's kernel (sfm_ctx_last_kernel_ms)
 };
 
 namespace sfm {
 // releases the context's cached BA plan (ba_solver.cpp; sfm_ctx_destroy)
 void ba_cache_release(sfm_ctx* ctx);
-// the context's side stream and its fork / join events (created on first
-// use, destroyed with the context)
-inline hipStream_t ctx_side(sfm_ctx* ctx) {
-    if (!ctx->side) {
-        SFM_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-        SFM_HIP(hipEventCreateWithFlags(&ctx->side_ev[0], hipEventDisableTiming));
-        SFM_HIP(hipEventCreateWithFlags(&ctx->side_ev[1], hipEventDisableTiming));
-    }
-    return ctx->side;
-}
 // the context's two timing events (created once, destroyed with the context)
 inline hipEvent_t* ctx_events(sfm_ctx* ctx) {
     if (!ctx->ev[0]) {

@@ -395,10 +395,6 @@ extern "C" int sfm_ctx_destroy(sfm_ctx* ctx) {
         if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
         for (hipEvent_t e : ctx->ev)
             if (e) (void)hipEventDestroy(e);
-        if (ctx->side) (void)hipStreamSynchronize(ctx->side);
-        for (hipEvent_t e : ctx->side_ev)
-            if (e) (void)hipEventDestroy(e);
-        if (ctx->side) (void)hipStreamDestroy(ctx->side);
         if (ctx->stream) {
             dev_cache_release(ctx->stream);
             (void)hipStreamDestroy(ctx->stream);
