@@ -65,9 +65,10 @@ __device__ __forceinline__ void reset_verdict(const BcrArgs& b) {
 }
 
 // rows of a super-block that can be nonzero in its W / z blocks (K cameras:
-// 6K real rows, rounded up to the MFMA's k step of 4): the products over
-// block rows stop here (C4, K = 9: 56 of 64, 2 of every 16 MFMAs skipped)
-__device__ __forceinline__ int bcr_kM(const BcrArgs& b) { return min(M, (6 * b.K + 3) & ~3); }
+// 6K real rows, rounded up to the MFMA's k step of 4; K is 9 or 10): the
+// products over block rows stop here (C4, K = 9: 56 of 64).  Written so the
+// compiler sees 56 <= kM <= 64.
+__device__ __forceinline__ int bcr_kM(const BcrArgs& b) { return b.K <= 9 ? 56 : b.K == 10 ? 60 : 64; }
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return fmin(fmax(v, lo), hi); }
 
@@ -108,10 +109,7 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 }
 
 // One wave, one 16x16 output tile: acc += op(A)[ar.., k] op(B)[k, bc..] for
-// k in [k0, k1) (k1 - k0 a multiple of 4; operands are read in 16-deep
-// chunks, so a partial last chunk reads past k1 but multiplies nothing there:
-// a super-block's K real cameras fill 6K of its 64 rows, and its W / z rows
-// beyond them are zero, so the products over block rows stop at kM(K)).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
+// k in [k0, k1) (k1 - k0 a multiple of 16).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
 // op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.  The LDS
 // operands of the next 16-wide k chunk are read while the current chunk's four
 // MFMAs run, so a runtime-length product is not LDS-latency bound.
@@ -133,8 +131,7 @@ __device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int
         const bool more = k + 16 < k1;
         if (more) load(k + 16, an, bn);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (4 * j < k1 - k) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
         if (more) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) { a[j] = an[j]; b[j] = bn[j]; }
@@ -149,18 +146,57 @@ __device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int
 // typed by address space (LDS: ds_read; global: global_load), since a
 // generic pointer through a call would become flat accesses.
 typedef __attribute__((address_space(3))) const double lds_cd;
-typedef __attribute__((address_space(1))) const double glb_cd;
 template <bool TA, bool TB, bool NEG>
 __device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
-    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
+    // k1 - k0 is 16, 32, 48 or 64: every chunk's reads first, then the MFMA
+    // chain (the scheduler otherwise waits a full LDS latency per chunk)
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    const int nc = (k1 - k0) >> 4;
+    double a[16], b[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (c < nc) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kj = k0 + 16 * c + 4 * j + kk;
+                a[4 * c + j] = TA ? A[kj * lda + ar + i] : A[(ar + i) * lda + kj];
+                b[4 * c + j] = TB ? B[(bc + i) * ldb + kj] : B[kj * ldb + bc + i];
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (c < nc) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[4 * c + j] : a[4 * c + j], b[4 * c + j], acc, 0, 0, 0);
+        }
+    }
+    return acc;
 }
+// the same over block rows k in [0, kM), kM in {56, 60, 64}: a super-block's
+// K real cameras fill 6K of its 64 rows and its W / z rows beyond them are
+// zero, so the last 16-deep chunk multiplies only its first kM - 48 rows
+// (C4, K = 9: 14 of 16 MFMAs); the branches are uniform and in the tail only
 template <bool TA, bool TB, bool NEG>
-__device__ __noinline__ v4d mm_lg(v4d acc, lds_cd* A, int lda, int ar, glb_cd* B, int ldb, int bc, int k0, int k1) {
-    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
-}
-template <bool TA, bool TB, bool NEG>
-__device__ __noinline__ v4d mm_gl(v4d acc, glb_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
-    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
+__device__ __noinline__ v4d mm_ll_rows(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int kM) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    // every operand read first (16 k steps, 64 VGPRs), then the MFMA chain
+    double a[16], b[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int kj = 4 * q + kk;
+        a[q] = TA ? A[kj * lda + ar + i] : A[(ar + i) * lda + kj];
+        b[q] = TB ? B[(bc + i) * ldb + kj] : B[kj * ldb + bc + i];
+    }
+    // (without this the scheduler sinks each read next to its MFMA, which
+    // then waits a full LDS latency every step)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        if (q < 14 || 4 * q < kM) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[q] : a[q], b[q], acc, 0, 0, 0);
+    return acc;
 }
 // A 64 x 16 column block of a global matrix held in registers, in the
 // operand order of tile_mm's k loop (v[4 c + j]: row 16 c + 4 j + kk, column
@@ -181,31 +217,28 @@ struct GTile {
 template <bool NEG, class PA>
 __device__ __forceinline__ v4d mm_tr(v4d acc, PA A, int lda, int ar, const GTile& g, int kM) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    double a[16];   // every LDS operand read first (mm_ll)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        double a[4];
+    for (int q = 0; q < 16; ++q) a[q] = A[(4 * q + kk) * lda + ar + i];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = A[(16 * c + 4 * j + kk) * lda + ar + i];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (16 * c + 4 * j < kM) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], g.v[4 * c + j], acc, 0, 0, 0);
-    }
+    for (int q = 0; q < 16; ++q)
+        if (q < 14 || 4 * q < kM)   // rows >= kM are zero (mm_ll_rows)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[q] : a[q], g.v[q], acc, 0, 0, 0);
     return acc;
 }
 // acc +/-= G[k][m]' B[k][bc + n], k = 0..kM-1 (B in LDS)
 template <bool NEG, class PB>
 __device__ __forceinline__ v4d mm_rt(v4d acc, const GTile& g, PB B, int ldb, int bc, int kM) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    double bv[16];   // every LDS operand read first (mm_ll)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        double bv[4];
+    for (int q = 0; q < 16; ++q) bv[q] = B[(4 * q + kk) * ldb + bc + i];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bv[j] = B[(16 * c + 4 * j + kk) * ldb + bc + i];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (16 * c + 4 * j < kM)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -g.v[4 * c + j] : g.v[4 * c + j], bv[j], acc, 0, 0, 0);
-    }
+    for (int q = 0; q < 16; ++q)
+        if (q < 14 || 4 * q < kM)   // rows >= kM are zero (mm_ll_rows)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -g.v[q] : g.v[q], bv[q], acc, 0, 0, 0);
     return acc;
 }
 __device__ __forceinline__ lds_cd* L3(const double* p) { return (lds_cd*)p; }
@@ -689,16 +722,16 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
     double* Aj = b.A + (size_t)j * M * M;
     if (wv < 4) {
         v4d acc = tile_ld(Aj, M, 16 * w, 16 * v);
-        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Wa), LD, 16 * v, 0, kM);
-        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Wb), LD, 16 * v, 0, kM);
+        if (hl) acc = mm_ll_rows<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Wa), LD, 16 * v, kM);
+        if (hr) acc = mm_ll_rows<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Wb), LD, 16 * v, kM);
         tile_st(Aj, M, 16 * w, 16 * v, acc);
         return;
     }
     if (16 * v < b.nrhs) {
         double* Rj = b.R + (size_t)j * M * b.nrhs;
         v4d acc = tile_ld(Rj, b.nrhs, 16 * w, 16 * v);
-        if (hl) acc = mm_ll<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Za), ldr, 16 * v, 0, kM);
-        if (hr) acc = mm_ll<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Zb), ldr, 16 * v, 0, kM);
+        if (hl) acc = mm_ll_rows<true, false, true>(acc, L3(Wa), LD, 16 * w, L3(Za), ldr, 16 * v, kM);
+        if (hr) acc = mm_ll_rows<true, false, true>(acc, L3(Wb), LD, 16 * w, L3(Zb), ldr, 16 * v, kM);
         tile_st(Rj, b.nrhs, 16 * w, 16 * v, acc);
     }
 }
@@ -853,7 +886,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         const int ti = kHt[h >> 1][0], tj = kHt[h >> 1][1];
         double* W = (h & 1) ? Wbl : Wal;
         if ((h & 1) && !hir) return;
-        tile_st(hp(h), LD, 0, 0, mm_ll<true, false, false>(zero4(), L3(W), M, 16 * ti, L3(W), M, 16 * tj, 0, kM));
+        tile_st(hp(h), LD, 0, 0, mm_ll_rows<true, false, false>(zero4(), L3(W), M, 16 * ti, L3(W), M, 16 * tj, kM));
     };
     auto sub_halves = [&](v4d acc, int t) {   // acc - half a - half b of tile t (fixed order)
         if (!upd) return acc;
@@ -864,10 +897,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // tile (ti, tj): its A update, then the trailing updates of steps 0..nk-1
     auto full = [&](int ti, int tj, int nk) {
         v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-        if (upd) acc = mm_ll<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, 0, kM);
-        if (hir) acc = mm_ll<true, false, true>(acc, L3(Wbl), M, 16 * ti, L3(Wbl), M, 16 * tj, 0, kM);
-        for (int k = 0; k < nk; ++k)
-            acc = mm_ll<false, true, true>(acc, L3(A), LD, 16 * ti, L3(A), LD, 16 * tj, 16 * k, 16 * k + 16);
+        if (upd) acc = mm_ll_rows<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, kM);
+        if (hir) acc = mm_ll_rows<true, false, true>(acc, L3(Wbl), M, 16 * ti, L3(Wbl), M, 16 * tj, kM);
+        if (nk) acc = mm_ll<false, true, true>(acc, L3(A), LD, 16 * ti, L3(A), LD, 16 * tj, 0, 16 * nk);
         tile_st(A, LD, 16 * ti, 16 * tj, acc);
     };
     // T_nj = sum_{m=j..n-1} L_nm X_mj into X tile (n, j).  Of X = L^-1 this
@@ -949,9 +981,8 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     {
         const int v = wave & 3;
         v4d part = zero4();
-        const int k1 = min(16 * v + 16, kM);
-        if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, k1);
-        else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, k1);
+        if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, 16 * v + 16);
+        else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, 16 * v + 16);
         if (upd) tile_st(tile_at(1, kS0[wave][0], kS0[wave][1]), LD, 0, 0, part);
     }
     __syncthreads();
@@ -1178,7 +1209,6 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
 // sp > 0: first block 0's update from its right neighbour sp, eliminated by
 // the last level (A_0 -= Wl_sp' Wl_sp, R_0 -= Wl_sp' z_sp; lower tiles only).
 __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* sm) {
-    const int kM = bcr_kM(b);
     const int ldr = b.nrhs + 1;
     double* A = sm;
     double* X = A + M * LD;
@@ -1220,7 +1250,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, kM);
+            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, M);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         };
         const int nrt = b.nrhs / 16;
@@ -1228,7 +1258,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
             double* scr = X + 16 * LD;
             if (wave < 4)
                 tile_st(scr + 256 * wave, 16, 0, 0,
-                        tile_mm<true, false, false>(zero4(), Wb, LD, 0, Wb, LD, 0, 16 * wave, min(16 * wave + 16, kM)));
+                        tile_mm<true, false, false>(zero4(), Wb, LD, 0, Wb, LD, 0, 16 * wave, 16 * wave + 16));
         }
         __syncthreads();
         auto pre0 = [&] {
@@ -1245,7 +1275,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
                 } else {
                     const int v = (t - 9) / nrt, tj = (t - 9) % nrt;
                     v4d acc = tile_ld(R, ldr, 16 * v, 16 * tj);
-                    acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, kM);
+                    acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, M);
                     tile_st(R, ldr, 16 * v, 16 * tj, acc);
                 }
             }
