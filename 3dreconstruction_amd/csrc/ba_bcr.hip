@@ -1465,156 +1465,174 @@ __global__ __launch_bounds__(NTL) void bcr_top_corner_kernel(BcrArgs b, DevProbl
 // real rows go to yF.  256 threads: thread (row, p) takes 32 of the row's 128
 // [Wl | Wr] coefficients, then 16 of the rows of X' (X staged in LDS);
 // four-lane sums in a fixed order.
-// FLOW: every block of every level in one launch, top-down (workgroup k waits
-// only for workgroups < k, so any residency makes progress).  y_i (64
-// doubles) is handed over as 128 tagged granules {epoch, 32 bits} stored
-// write-through (Guideline 16 R2: the data is the flag, no fence either
-// side): a consumer's wave 0 re-reads its neighbours' granules until every
-// tag holds this solve's epoch, after staging everything the forward pass
-// left.  The last workgroup to finish publishes the solve verdict.
-constexpr int kYG = 128;   // granules per block
-__device__ __forceinline__ void put_y(unsigned long long* g, int row, double v, unsigned epoch) {
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(v), tag = (unsigned long long)epoch << 32;
-    __hip_atomic_store((gu64*)(g + 2 * row), tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu64*)(g + 2 * row + 1), tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// wave 0: granules of y_a (and y_b) into LDS dst_a / dst_b as doubles
-__device__ __forceinline__ void get_y(const unsigned long long* ga, const unsigned long long* gb, double* dst_a,
-                                      double* dst_b, unsigned epoch, double* fail) {
-    const int lane = threadIdx.x & 63;
-    unsigned va[2], vb[2];
-    for (unsigned spins = 0;;) {
-        bool ok = true;
+//
+// Round 5: dependency cones instead of a level-by-level dataflow.  Block i
+// needs y_{i-s} and y_{i+s}, both eliminated at coarser strides, and the
+// blocks a leaf (an odd block, eliminated first) depends on, transitively,
+// are about one per level: 8 blocks at C4's 100 super-blocks.  So one
+// workgroup per leaf computes its whole cone, root first, from the data the
+// forward pass left, with no hand-off between workgroups at all (the level-by-
+// level dataflow paid one inter-CU hand-off per level, ~2.7 us each), the
+// next block's coefficients prefetched into registers while the current one
+// is solved; each block's y goes to yF from one owner workgroup.  The
+// arithmetic per block is the same function in both launch shapes
+// (SFM_CTX_BA_SPLIT_BCR: one launch per level, y through global memory), so
+// they agree bit for bit.
+constexpr int kCone = 40;   // cone entries: log2(N) + 1 <= 40
+struct BackIn {             // one block's coefficients, in registers
+    double w[32];           // [Wl | Wr] row `row`, 32 columns from p
+    double x[16];           // this thread's 16 elements of X_i (staged to LDS)
+    double z[17];           // z_i row (p == 0): column 0, then the arrow columns
+};
+__device__ __forceinline__ void back_load(const BcrArgs& b, const DevProblem& P, int i, int s, BackIn& in) {
+    const int t = threadIdx.x, row = t >> 2, p = t & 3;
+    const bool hl = s > 0, hr = s > 0 && i + s < b.N;
+    const bool use = p < 2 ? hl : hr;
+    if (use) {
+        const double2* src = reinterpret_cast<const double2*>((p < 2 ? b.Wl : b.Wr) + (size_t)i * M * M + row * M +
+                                                              32 * (p & 1));
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const unsigned long long x = __hip_atomic_load((gu64*)(ga + lane + 64 * h), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-            va[h] = (unsigned)x;
-            ok &= (unsigned)(x >> 32) == epoch;
-            if (gb) {
-                const unsigned long long y = __hip_atomic_load((gu64*)(gb + lane + 64 * h), __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                vb[h] = (unsigned)y;
-                ok &= (unsigned)(y >> 32) == epoch;
-            }
-        }
-        if (__all(ok)) break;
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 22)) {   // ~ seconds: a lost producer, never a normal wait
-            if (lane == 0) st_sc1(fail + 1, 1.0);   // a wait timeout, not a numerical failure
-            break;
+        for (int q = 0; q < 16; ++q) {
+            const double2 v = src[q];
+            in.w[2 * q] = v.x;
+            in.w[2 * q + 1] = v.y;
         }
     }
+    const double* X = b.L + (size_t)i * M * M;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        reinterpret_cast<unsigned*>(dst_a)[lane + 64 * h] = va[h];   // little endian: granule 2j = low word of y_j
-        if (gb) reinterpret_cast<unsigned*>(dst_b)[lane + 64 * h] = vb[h];
+    for (int q = 0; q < 16; ++q) in.x[q] = X[t + q * NT];
+    if (p == 0) {
+        const double* z = b.Z + ((size_t)i * M + row) * b.nrhs;
+        const int na = P.iw * P.nintr;
+#pragma unroll
+        for (int a = 0; a < 17; ++a) in.z[a] = a <= na ? z[a] : 0.0;
+    }
+}
+// y_i from the staged coefficients and y_{i-s} / y_{i+s} (LDS); y_i into yo (LDS)
+__device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P, int i, int s, const BackIn& in,
+                                           const double* yl, const double* yr, double* yo, double* Xs, double* u,
+                                           bool own) {
+    const int t = threadIdx.x, row = t >> 2, p = t & 3;
+    const bool hl = s > 0, hr = s > 0 && i + s < b.N;
+    const bool use = p < 2 ? hl : hr;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int e = t + q * NT;
+        Xs[(e / M) * LD + e % M] = in.x[q];
+    }
+    double zr = 0.0;
+    if (p == 0) {
+        const double* xc = P.yF + P.nb;
+        zr = in.z[0];
+        for (int a = 0; a < P.iw * P.nintr; ++a) zr -= in.z[1 + a] * xc[a];
+    }
+    double acc = 0.0;
+    if (use) {
+        const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
+#pragma unroll
+        for (int q = 0; q < 32; ++q) acc = fma(in.w[q], y[q], acc);
+    }
+    acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
+    acc += __shfl_xor(acc, 2);
+    if (p == 0) u[row] = zr - acc;
+    __syncthreads();
+    // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
+    // exact zeros above the diagonal; the tiles above are not read)
+    double a2 = 0.0;
+    if (p >= (row >> 4)) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) a2 = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], a2);
+    }
+    a2 += __shfl_xor(a2, 1);
+    a2 += __shfl_xor(a2, 2);
+    if (p == 0) {
+        yo[row] = a2;
+        const int nreal = min(b.K, P.ncam - i * b.K) * 6;
+        if (own && row < nreal) P.yF[(size_t)i * b.K * 6 + row] = a2;
+    }
+}
+__device__ __forceinline__ int back_stride(int blk) { return blk & -blk; }   // 0 for the root
+
+// fused: one workgroup per leaf (odd block; the root alone for one block)
+__global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem P) {
+    __shared__ double Xs[M * LD];
+    __shared__ double u[M];
+    __shared__ double ys[kCone][M];
+    __shared__ int cb[kCone], cl[kCone], cr[kCone], cown[kCone];
+    __shared__ int ncone;
+    const int leaf = b.N >= 2 ? 2 * (int)blockIdx.x + 1 : 0;
+    if (threadIdx.x == 0) {
+        // the cone: leaf, then every block a cone block needs, transitively
+        int n = 0;
+        cb[n++] = leaf;
+        for (int k = 0; k < n; ++k) {
+            const int blk = cb[k], sb = back_stride(blk);
+            if (sb == 0) continue;
+            const int dep[2] = {blk - sb, blk + sb};
+            for (int d = 0; d < 2; ++d) {
+                if (dep[d] >= b.N) continue;
+                bool have = false;
+                for (int m = 0; m < n; ++m) have |= cb[m] == dep[d];
+                if (!have && n < kCone) cb[n++] = dep[d];
+            }
+        }
+        // dependency order: the root, then by decreasing stride
+        auto key = [](int blk) { return blk == 0 ? 1 << 30 : back_stride(blk); };
+        for (int k = 1; k < n; ++k)
+            for (int m = k; m > 0 && key(cb[m]) > key(cb[m - 1]); --m) {
+                const int tmp = cb[m];
+                cb[m] = cb[m - 1];
+                cb[m - 1] = tmp;
+            }
+        for (int k = 0; k < n; ++k) {
+            const int blk = cb[k], sb = back_stride(blk);
+            cl[k] = cr[k] = -1;
+            for (int m = 0; m < k; ++m) {
+                if (sb && cb[m] == blk - sb) cl[k] = m;
+                if (sb && cb[m] == blk + sb) cr[k] = m;
+            }
+            // owner of y_blk's yF rows: the leaf itself, the even block left
+            // of it, and the last block when it is even with no odd block right
+            cown[k] = blk == leaf || blk == leaf - 1 || (blk == leaf + 1 && blk == b.N - 1);
+        }
+        ncone = n;
+        if (blockIdx.x == 0) {   // every kernel that can set a failure word has finished
+            P.scal[kScSolveFail] = solve_verdict(b.fail);
+            reset_verdict(b);
+        }
+    }
+    __syncthreads();
+    const int n = ncone;
+    BackIn cur, nxt;
+    back_load(b, P, cb[0], back_stride(cb[0]), cur);
+    for (int k = 0; k < n; ++k) {
+        const int blk = cb[k], sb = back_stride(blk);
+        if (k + 1 < n) back_load(b, P, cb[k + 1], back_stride(cb[k + 1]), nxt);
+        back_block(b, P, blk, sb, cur, cl[k] >= 0 ? ys[cl[k]] : nullptr, cr[k] >= 0 ? ys[cr[k]] : nullptr, ys[k], Xs, u,
+                   cown[k] != 0);
+        __syncthreads();
+        cur = nxt;
     }
 }
 
-template <bool FLOW>
-__global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, int s_arg, unsigned epoch) {
+// SFM_CTX_BA_SPLIT_BCR: one launch per level (s = 0: the root), y through b.Y
+__global__ __launch_bounds__(NT) void bcr_back_level_kernel(BcrArgs b, DevProblem P, int s) {
     __shared__ double Xs[M * LD];
     __shared__ double u[M];
-    __shared__ double yl[M], yr[M];
-    int i = -1, s = 0;
-    if (FLOW) {   // workgroup k: the root, then the odd blocks of s_top / 2, ..., 1
-        int k = blockIdx.x;
-        if (k == 0) {
-            i = 0;
-        } else {
-            --k;
-            for (s = s_arg / 2; s >= 1; s >>= 1) {
-                const int n_odd = (b.N - s + 2 * s - 1) / (2 * s);
-                if (k < n_odd) {
-                    i = s + 2 * s * k;
-                    break;
-                }
-                k -= n_odd;
-            }
-        }
-    } else {      // one level: s_arg = 0 the root, else its odd blocks
-        s = s_arg;
-        i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
+    __shared__ double yl[M], yr[M], yo[M];
+    const int i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
+    if (i < 0 || i >= b.N) return;
+    BackIn in;
+    back_load(b, P, i, s, in);
+    const int t = threadIdx.x;
+    if (s > 0 && t < M) {
+        yl[t] = b.Y[(size_t)(i - s) * M + t];
+        if (i + s < b.N) yr[t] = b.Y[(size_t)(i + s) * M + t];
     }
-    unsigned long long* Yg = reinterpret_cast<unsigned long long*>(b.Y);   // [N][kYG] granules
-    const int t = threadIdx.x, row = t >> 2, p = t & 3;
-    const bool valid = i >= 0 && i < b.N;
-    if (valid) {
-        const int l = i - s, r = i + s;
-        const bool hl = s > 0, hr = s > 0 && r < b.N;
-        const bool use = p < 2 ? hl : hr;
-        // everything of the forward pass first: this row's [Wl | Wr]
-        // coefficients, X into LDS, and z'_row
-        double w[32];
-        if (use) {
-            const double2* src = reinterpret_cast<const double2*>(
-                (p < 2 ? b.Wl : b.Wr) + (size_t)i * M * M + row * M + 32 * (p & 1));
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const double2 v = src[q];
-                w[2 * q] = v.x;
-                w[2 * q + 1] = v.y;
-            }
-        }
-        load_tile<64, M, NT>(Xs, LD, b.L + (size_t)i * M * M, M);
-        double zr = 0.0;
-        if (p == 0) {
-            const double* z = b.Z + ((size_t)i * M + row) * b.nrhs;
-            const double* xc = P.yF + P.nb;
-            zr = z[0];
-            for (int a = 0; a < P.iw * P.nintr; ++a) zr -= z[1 + a] * xc[a];
-        }
-        if (hl) {
-            if (t < 64) {
-                if (FLOW) get_y(Yg + (size_t)l * kYG, hr ? Yg + (size_t)r * kYG : nullptr, yl, yr, epoch, b.fail);
-                else {   // an earlier launch wrote them
-                    for (int e = t; e < 2 * kYG; e += 64) {
-                        const bool right = e >= kYG;
-                        if (right && !hr) break;
-                        reinterpret_cast<unsigned*>(right ? yr : yl)[e & (kYG - 1)] =
-                            (unsigned)Yg[(size_t)(right ? r : l) * kYG + (e & (kYG - 1))];
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        double acc = 0.0;
-        if (use) {
-            const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
-#pragma unroll
-            for (int q = 0; q < 32; ++q) acc = fma(w[q], y[q], acc);
-        }
-        acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
-        acc += __shfl_xor(acc, 2);
-        if (p == 0) u[row] = zr - acc;
-        __syncthreads();
-        // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
-        // exact zeros above the diagonal; the tiles above are never written)
-        double a2 = 0.0;
-        if (p >= (row >> 4)) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) a2 = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], a2);
-        }
-        a2 += __shfl_xor(a2, 1);
-        a2 += __shfl_xor(a2, 2);
-        if (p == 0) {
-            put_y(Yg + (size_t)i * kYG, row, a2, epoch);
-            const int nreal = min(b.K, P.ncam - i * b.K) * 6;
-            if (row < nreal) P.yF[(size_t)i * b.K * 6 + row] = a2;
-        }
-    }
-    if (FLOW) {   // the last workgroup publishes the verdict (every timeout word drained before its ticket)
-        unsigned* counter = reinterpret_cast<unsigned*>(b.fail + 5);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0 &&
-            __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-            P.scal[kScSolveFail] = solve_verdict(b.fail);
-            reset_verdict(b);
-            __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    __syncthreads();
+    back_block(b, P, i, s, in, yl, yr, yo, Xs, u, true);
+    __syncthreads();
+    if (t < M) b.Y[(size_t)i * M + t] = yo[t];
 }
 
 // the verdict after per-level back substitution launches
@@ -1641,8 +1659,8 @@ void bcr_setup(BcrArgs& b, const DevProblem& P) {
 
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
-    // A C L(=X) Wl Wr | R Z Y | part | fail (+ counters) | y flags (one word per block)
-    return 5 * mm + 3 * mr + 512 * (size_t)b.N + 8 + ((size_t)b.N + 1) / 2 + 2;
+    // A C L(=X) Wl Wr | R Z Y (Y: [N][64] y of the split back substitution) | part | fail (+ counters)
+    return 5 * mm + 3 * mr + 512 * (size_t)b.N + 8;
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
@@ -1650,7 +1668,6 @@ void bcr_bind(BcrArgs& b, double* base) {
     b.A = base; b.C = b.A + mm; b.L = b.C + mm; b.Wl = b.L + mm; b.Wr = b.Wl + mm;
     b.R = b.Wr + mm; b.Z = b.R + mr; b.Y = b.Z + mr;
     b.part = b.Y + mr; b.fail = b.part + 512 * (size_t)b.N;
-    b.yflag = reinterpret_cast<unsigned*>(b.fail + 8);   // zeroed by the caller once
 }
 
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
@@ -1690,17 +1707,16 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
         SFM_HIP(hipGetLastError());
     }
-    int n_back = 1;
-    for (int stride = s_top / 2; stride >= 1; stride /= 2) n_back += (b.N - stride + 2 * stride - 1) / (2 * stride);
+    (void)epoch;
     if (!b.split) {
-        hipLaunchKernelGGL(bcr_back_kernel<true>, dim3(n_back), dim3(NT), 0, s, b, P, s_top, epoch);
+        hipLaunchKernelGGL(bcr_back_cone_kernel, dim3(b.N >= 2 ? b.N / 2 : 1), dim3(NT), 0, s, b, P);
         SFM_HIP(hipGetLastError());
     } else {   // SFM_CTX_BA_SPLIT_BCR: one launch per level
-        hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(1), dim3(NT), 0, s, b, P, 0, epoch);
+        hipLaunchKernelGGL(bcr_back_level_kernel, dim3(1), dim3(NT), 0, s, b, P, 0);
         SFM_HIP(hipGetLastError());
         for (int stride = s_top / 2; stride >= 1; stride /= 2) {
             const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-            hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(n_odd), dim3(NT), 0, s, b, P, stride, epoch);
+            hipLaunchKernelGGL(bcr_back_level_kernel, dim3(n_odd), dim3(NT), 0, s, b, P, stride);
             SFM_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(bcr_verdict_kernel, dim3(1), dim3(1), 0, s, b, P);
