@@ -644,18 +644,53 @@ __device__ __forceinline__ double pack_r(const BcrArgs& b, const DevProblem& P, 
     const double va = P.Sarrow[arrow ? ((size_t)k * P.ncam + ci) * 6 * P.iw + a * 6 + r % 6 : 0];
     return rhs ? vr : arrow ? va : 0.0;
 }
+// The first level kernel's gathers: a thread's column c of super-block I is
+// fixed, so its column terms -- and the one LM damping term its column can
+// need (the diagonal element (c, c)) -- are formed once; rows vary per
+// element.  Same values as pack_a (the damping is added to the band value in
+// one rounding, as there).
+struct BandCol {
+    int c0, nreal, Dp, cj, cm;
+    bool creal;
+    double dmp;   // lm^2 of column c (0 for a padding column)
+    __device__ BandCol(const BcrArgs& b, const DevProblem& P, double radius, int I, int c) {
+        c0 = I * b.K;
+        nreal = min(b.K, P.ncam - c0) * 6;
+        Dp = P.D + 1;
+        cj = c0 + c / 6;
+        cm = c % 6;
+        creal = c < nreal;
+        const double cn = P.cnF[creal ? 6 * cj + cm : 0];
+        const double lm = sqrt(clampd(cn, P.min_diag, P.max_diag) / radius);
+        dmp = creal ? lm * lm : 0.0;
+    }
+    // element (r, c) of A
+    __device__ __forceinline__ double a(const DevProblem& P, int r, int c) const {
+        const int ci = c0 + r / 6, rm = r % 6;
+        const bool real = r < nreal && creal;
+        const int d = ci >= cj ? ci - cj : cj - ci;
+        const bool inband = real && d <= P.D;
+        const int idx = ci >= cj ? ((ci * Dp + d) * 36 + rm * 6 + cm) : ((cj * Dp + d) * 36 + cm * 6 + rm);
+        const double v = P.Sband[inband ? idx : 0];
+        double x = inband ? v : 0.0;
+        x = (real && r == c) ? x + dmp : x;
+        return r >= nreal && r == c ? 1.0 : x;   // padding: identity
+    }
+};
 // rows [r0, r0 + 16) of super-block I's A and R, gathered to global memory
 // (the first level kernel, for the even blocks beside its odd ones)
 template <int TH>
 __device__ __forceinline__ void pack_rows(const BcrArgs& b, const DevProblem& P, double radius, int I, int r0, int t) {
     double* A = b.A + (size_t)I * M * M + (size_t)r0 * M;
     double* R = b.R + (size_t)I * M * b.nrhs + (size_t)r0 * b.nrhs;
+    static_assert(TH % M == 0, "a thread's column is fixed");
     constexpr int NA = 16 * M / TH;
+    const BandCol col(b, P, radius, I, t % M);
     double va[NA];
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
         const int e = t + q * TH;
-        va[q] = pack_a(b, P, radius, I, r0 + e / M, e % M);
+        va[q] = col.a(P, r0 + e / M, e % M);
     }
 #pragma unroll
     for (int q = 0; q < NA; ++q) A[t + q * TH] = va[q];
@@ -792,10 +827,11 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         // to global memory for the later levels and the top
         constexpr int QA = M * M / NTL, QC = M * 16 / NTL;
         double va[QA], vc[QC], vr[QC], vz[QC];
+        const BandCol col(b, P, radius, i, threadIdx.x % M);
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
             const int e = threadIdx.x + q * NTL;
-            va[q] = pack_a(b, P, radius, i, e / M, e % M);
+            va[q] = col.a(P, e / M, e % M);
         }
 #pragma unroll
         for (int q = 0; q < QC; ++q) {
