@@ -109,47 +109,13 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 }
 
 // One wave, one 16x16 output tile: acc += op(A)[ar.., k] op(B)[k, bc..] for
-// k in [k0, k1) (k1 - k0 a multiple of 16).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
-// op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.  The LDS
-// operands of the next 16-wide k chunk are read while the current chunk's four
-// MFMAs run, so a runtime-length product is not LDS-latency bound.
+// k in [k0, k1) (k1 - k0 a multiple of 16, at most 64).  op(A)[m][k] = TA ?
+// A[k][m] : A[m][k], op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the
+// product.  Every operand is read before the first MFMA, behind a scheduling
+// barrier: left alone, the scheduler sank each read next to its MFMA, which
+// then waited a full LDS latency per k step (round 5).
 template <bool TA, bool TB, bool NEG, class PA = const double*, class PB = const double*>
 __device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int ldb, int bc, int k0, int k1) {
-    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
-    double a[4], b[4];
-    auto load = [&](int k, double (&av)[4], double (&bv)[4]) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int kj = k + 4 * j + kk;
-            av[j] = TA ? A[kj * lda + ar + i] : A[(ar + i) * lda + kj];
-            bv[j] = TB ? B[(bc + i) * ldb + kj] : B[kj * ldb + bc + i];
-        }
-    };
-    load(k0, a, b);
-    for (int k = k0; k < k1; k += 16) {
-        double an[4], bn[4];
-        const bool more = k + 16 < k1;
-        if (more) load(k + 16, an, bn);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
-        if (more) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) { a[j] = an[j]; b[j] = bn[j]; }
-        }
-    }
-    return acc;
-}
-// Out-of-line tile products for the level kernel.  Its eight waves run
-// different code at the same time, and with every product inlined the kernel
-// was 61 KB of code: past the 64 KB instruction cache two CUs share, so the
-// pivot wave's diagonal factor waited on instruction fetches.  Operands are
-// typed by address space (LDS: ds_read; global: global_load), since a
-// generic pointer through a call would become flat accesses.
-typedef __attribute__((address_space(3))) const double lds_cd;
-template <bool TA, bool TB, bool NEG>
-__device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
-    // k1 - k0 is 16, 32, 48 or 64: every chunk's reads first, then the MFMA
-    // chain (the scheduler otherwise waits a full LDS latency per chunk)
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
     const int nc = (k1 - k0) >> 4;
     double a[16], b[16];
@@ -174,6 +140,17 @@ __device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B
         }
     }
     return acc;
+}
+// Out-of-line tile products for the level kernel.  Its eight waves run
+// different code at the same time, and with every product inlined the kernel
+// was 61 KB of code: past the 64 KB instruction cache two CUs share, so the
+// pivot wave's diagonal factor waited on instruction fetches.  Operands are
+// typed by address space (LDS: ds_read; global: global_load), since a
+// generic pointer through a call would become flat accesses.
+typedef __attribute__((address_space(3))) const double lds_cd;
+template <bool TA, bool TB, bool NEG>
+__device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
+    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
 }
 // the same over block rows k in [0, kM), kM in {56, 60, 64}: a super-block's
 // K real cameras fill 6K of its 64 rows and its W / z rows beyond them are
@@ -1050,7 +1027,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         tile_st(Cr, LD, 0, 16 * k, acc);
     };
     auto gs_r = [&](int k) {   // Cr(0, k) = Cr(0, k) X_kk' = O_k'; Wr rows 16k.. (transposed store)
-        const v4d o = mm_ll<false, true, false>(zero4(), L3(Cr), LD, 0, L3(X), LD, 16 * k, 16 * k, 16 * k + 16);
+        const v4d o = tile_mm<false, true, false>(zero4(), L3(Cr), LD, 0, L3(X), LD, 16 * k, 16 * k, 16 * k + 16);
         tile_st(Cr, LD, 0, 16 * k, o);
         const int lane = threadIdx.x & 63, li = lane & 15, kk = lane >> 4;
 #pragma unroll
@@ -1559,8 +1536,11 @@ __device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P
     double zr = 0.0;
     if (p == 0) {
         const double* xc = P.yF + P.nb;
+        const int na = P.iw * P.nintr;
         zr = in.z[0];
-        for (int a = 0; a < P.iw * P.nintr; ++a) zr -= in.z[1 + a] * xc[a];
+#pragma unroll
+        for (int a = 0; a < 16; ++a)   // (static register indices; the same sum order as before)
+            if (a < na) zr -= in.z[1 + a] * xc[a];
     }
     double acc = 0.0;
     if (use) {
@@ -1900,11 +1880,33 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, i
         load_tile<64>(Li, LD, d.A + (int64_t)i * kDM * np + (int64_t)kk * kDM, (int)np);
         if (i != j) load_tile<64>(Lj, LD, d.A + (int64_t)j * kDM * np + (int64_t)kk * kDM, (int)np);
         __syncthreads();
+        // the wave's four tiles share row tile `wave` of L_i: every operand of
+        // the column read first (80 doubles), then the four accumulator chains
+        // interleaved (the same k order per tile as tile_mm: bit-identical)
+        {   // 16-deep chunks, the next chunk's reads issued before this chunk's MFMAs
+            const int lane = threadIdx.x & 63, li = lane & 15, kq = lane >> 4;
+            double a[2][4], bq[2][4][4];
+            auto load = [&](int c, int slot) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
-            if (i == j && tj > ti) continue;   // the diagonal tile's lower half (and its diagonal sub-tiles)
-            acc[q] = tile_mm<false, true, true>(acc[q], Li, LD, 16 * ti, Lb, LD, 16 * tj, 0, M);
+                for (int st = 0; st < 4; ++st) {
+                    const int kj = 16 * c + 4 * st + kq;
+                    a[slot][st] = Li[(16 * wave + li) * LD + kj];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bq[slot][q][st] = Lb[(16 * q + li) * LD + kj];
+                }
+            };
+            load(0, 0);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (c + 1 < 4) load(c + 1, (c + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int st = 0; st < 4; ++st)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (!(i == j && q > wave))   // the diagonal tile's lower half (and its diagonal sub-tiles)
+                            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[c & 1][st], bq[c & 1][q][st], acc[q], 0, 0, 0);
+            }
         }
     }
 #pragma unroll
