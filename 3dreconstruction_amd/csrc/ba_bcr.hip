@@ -601,20 +601,21 @@ __device__ __forceinline__ double pack_a(const BcrArgs& b, const DevProblem& P, 
     }
     return r >= x.nreal && r == c ? 1.0 : a;   // padding: identity
 }
-__device__ __forceinline__ double pack_c(const BcrArgs& b, const DevProblem& P, int I, int r, int c) {
-    // block (ci, cj) with cj in the previous super-block (always full)
+__device__ __forceinline__ double pack_c(const BcrArgs& b, const DevProblem& P, int I, int r, int c, bool on = true) {
+    // block (ci, cj) with cj in the previous super-block (always full);
+    // on = false: 0 (the load still issued, from a clamped address: no branch)
     const PackIdx x(b, P, I);
     const int Dp = P.D + 1;
     const int ci = x.c0 + r / 6, cj = x.c0 - b.K + c / 6, d = ci - cj;
-    const bool ok = I > 0 && r < x.nreal && c / 6 < b.K && d >= 1 && d <= P.D;
+    const bool ok = on && I > 0 && r < x.nreal && c / 6 < b.K && d >= 1 && d <= P.D;
     const double v = P.Sband[ok ? ((size_t)ci * Dp + d) * 36 + (r % 6) * 6 + c % 6 : 0];
     return ok ? v : 0.0;
 }
 // R: column 0 = rhs, columns 1 + iw k + a = arrow (intr k, row a) transposed
-__device__ __forceinline__ double pack_r(const BcrArgs& b, const DevProblem& P, int I, int r, int c) {
+__device__ __forceinline__ double pack_r(const BcrArgs& b, const DevProblem& P, int I, int r, int c, bool on = true) {
     const PackIdx x(b, P, I);
     const int ci = x.c0 + r / 6;
-    const bool real = r < x.nreal;
+    const bool real = on && r < x.nreal;
     const bool rhs = real && c == 0, arrow = real && c > 0 && c - 1 < P.iw * P.nintr;
     const int k = (c - 1) / P.iw, a = (c - 1) % P.iw;
     const double vr = P.rhs[rhs ? 6LL * ci + r % 6 : 0];
@@ -669,9 +670,12 @@ __device__ __forceinline__ void pack_rows(const BcrArgs& b, const DevProblem& P,
         const int e = t + q * TH;
         va[q] = col.a(P, r0 + e / M, e % M);
     }
+    static_assert(16 * 32 <= TH, "one R element per thread at most (nrhs <= 32)");
+    const bool hasr = t < 16 * b.nrhs;
+    const double vr = pack_r(b, P, I, r0 + t / b.nrhs, t % b.nrhs, hasr);
 #pragma unroll
     for (int q = 0; q < NA; ++q) A[t + q * TH] = va[q];
-    for (int e = t; e < 16 * b.nrhs; e += TH) R[e] = pack_r(b, P, I, r0 + e / b.nrhs, e % b.nrhs);
+    if (hasr) R[t] = vr;
 }
 
 // One workgroup per 4 rows of a super-block (N * 16 workgroups).
@@ -814,8 +818,8 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         for (int q = 0; q < QC; ++q) {
             const int e = threadIdx.x + q * NTL;
             vc[q] = pack_c(b, P, i, e / 16, 16 * w + e % 16);
-            vr[q] = hr ? pack_c(b, P, r, 16 * w + e / M, e % M) : 0.0;
-            vz[q] = hz ? pack_r(b, P, i, e / 16, 16 * w + e % 16) : 0.0;
+            vr[q] = pack_c(b, P, r, 16 * w + e / M, e % M, hr);
+            vz[q] = pack_r(b, P, i, e / 16, 16 * w + e % 16, hz);
         }
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
@@ -1492,6 +1496,14 @@ __global__ __launch_bounds__(NTL) void bcr_top_corner_kernel(BcrArgs b, DevProbl
 // (SFM_CTX_BA_SPLIT_BCR: one launch per level, y through global memory), so
 // they agree bit for bit.
 constexpr int kCone = 40;   // cone entries: log2(N) + 1 <= 40
+// a workgroup barrier that orders LDS only: __syncthreads' release fence
+// waits for every outstanding vector memory access (vmcnt(0) on gfx9, loads
+// included), which would drain the next block's prefetch at every barrier
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 struct BackIn {             // one block's coefficients, in registers
     double w[32];           // [Wl | Wr] row `row`, 32 columns from p
     double x[16];           // this thread's 16 elements of X_i (staged to LDS)
@@ -1524,7 +1536,7 @@ __device__ __forceinline__ void back_load(const BcrArgs& b, const DevProblem& P,
 // y_i from the staged coefficients and y_{i-s} / y_{i+s} (LDS); y_i into yo (LDS)
 __device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P, int i, int s, const BackIn& in,
                                            const double* yl, const double* yr, double* yo, double* Xs, double* u,
-                                           bool own) {
+                                           const double* xc, bool own) {
     const int t = threadIdx.x, row = t >> 2, p = t & 3;
     const bool hl = s > 0, hr = s > 0 && i + s < b.N;
     const bool use = p < 2 ? hl : hr;
@@ -1534,8 +1546,7 @@ __device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P
         Xs[(e / M) * LD + e % M] = in.x[q];
     }
     double zr = 0.0;
-    if (p == 0) {
-        const double* xc = P.yF + P.nb;
+    if (p == 0) {   // xc: the corner solution x_c, staged in LDS
         const int na = P.iw * P.nintr;
         zr = in.z[0];
 #pragma unroll
@@ -1551,7 +1562,7 @@ __device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P
     acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
     acc += __shfl_xor(acc, 2);
     if (p == 0) u[row] = zr - acc;
-    __syncthreads();
+    lds_barrier();
     // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
     // exact zeros above the diagonal; the tiles above are not read)
     double a2 = 0.0;
@@ -1576,7 +1587,9 @@ __global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem
     __shared__ double ys[kCone][M];
     __shared__ int cb[kCone], cl[kCone], cr[kCone], cown[kCone];
     __shared__ int ncone;
+    __shared__ double xc[16];
     const int leaf = b.N >= 2 ? 2 * (int)blockIdx.x + 1 : 0;
+    if (threadIdx.x < 16) xc[threadIdx.x] = (int)threadIdx.x < P.iw * P.nintr ? P.yF[P.nb + threadIdx.x] : 0.0;
     if (threadIdx.x == 0) {
         // the cone: leaf, then every block a cone block needs, transitively
         int n = 0;
@@ -1625,8 +1638,8 @@ __global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem
         const int blk = cb[k], sb = back_stride(blk);
         if (k + 1 < n) back_load(b, P, cb[k + 1], back_stride(cb[k + 1]), nxt);
         back_block(b, P, blk, sb, cur, cl[k] >= 0 ? ys[cl[k]] : nullptr, cr[k] >= 0 ? ys[cr[k]] : nullptr, ys[k], Xs, u,
-                   cown[k] != 0);
-        __syncthreads();
+                   xc, cown[k] != 0);
+        lds_barrier();   // (not __syncthreads: it would wait for nxt's loads here)
         cur = nxt;
     }
 }
@@ -1635,18 +1648,19 @@ __global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem
 __global__ __launch_bounds__(NT) void bcr_back_level_kernel(BcrArgs b, DevProblem P, int s) {
     __shared__ double Xs[M * LD];
     __shared__ double u[M];
-    __shared__ double yl[M], yr[M], yo[M];
+    __shared__ double yl[M], yr[M], yo[M], xc[16];
     const int i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
     if (i < 0 || i >= b.N) return;
     BackIn in;
     back_load(b, P, i, s, in);
     const int t = threadIdx.x;
+    if (t < 16) xc[t] = t < P.iw * P.nintr ? P.yF[P.nb + t] : 0.0;
     if (s > 0 && t < M) {
         yl[t] = b.Y[(size_t)(i - s) * M + t];
         if (i + s < b.N) yr[t] = b.Y[(size_t)(i + s) * M + t];
     }
     __syncthreads();
-    back_block(b, P, i, s, in, yl, yr, yo, Xs, u, true);
+    back_block(b, P, i, s, in, yl, yr, yo, Xs, u, xc, true);
     __syncthreads();
     if (t < M) b.Y[(size_t)i * M + t] = yo[t];
 }
