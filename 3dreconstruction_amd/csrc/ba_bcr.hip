@@ -1504,60 +1504,78 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
-struct BackIn {             // one block's coefficients, in registers
-    double w[32];           // [Wl | Wr] row `row`, 32 columns from p
-    double x[16];           // this thread's 16 elements of X_i (staged to LDS)
-    double z[17];           // z_i row (p == 0): column 0, then the arrow columns
+// One block's coefficients in registers, read coalesced (consecutive
+// threads, consecutive addresses): [Wl | Wr] (64 x 128), X (64 x 64) and the
+// first 17 columns of z.  (Read per thread along a row, as the level-by-level
+// kernel did, each load instruction touched 64 cache lines: with one
+// workgroup walking a whole cone that cost ~5 us per block.)
+constexpr int kLDW = 129, kZW = 17;
+struct BackIn {
+    double w[32], x[16], z[5];
 };
-__device__ __forceinline__ void back_load(const BcrArgs& b, const DevProblem& P, int i, int s, BackIn& in) {
-    const int t = threadIdx.x, row = t >> 2, p = t & 3;
+__device__ __forceinline__ void back_load(const BcrArgs& b, int i, int s, BackIn& in) {
+    const int t = threadIdx.x;
     const bool hl = s > 0, hr = s > 0 && i + s < b.N;
-    const bool use = p < 2 ? hl : hr;
-    if (use) {
-        const double2* src = reinterpret_cast<const double2*>((p < 2 ? b.Wl : b.Wr) + (size_t)i * M * M + row * M +
-                                                              32 * (p & 1));
+    const double* Wl = b.Wl + (size_t)i * M * M;
+    const double* Wr = b.Wr + (size_t)i * M * M;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const double2 v = src[q];
-            in.w[2 * q] = v.x;
-            in.w[2 * q + 1] = v.y;
-        }
+    for (int q = 0; q < 32; ++q) {
+        const int e = t + q * NT, row = e >> 7, col = e & 127;
+        const bool use = col < M ? hl : hr;
+        in.w[q] = use ? (col < M ? Wl : Wr)[row * M + (col & (M - 1))] : 0.0;
     }
     const double* X = b.L + (size_t)i * M * M;
 #pragma unroll
     for (int q = 0; q < 16; ++q) in.x[q] = X[t + q * NT];
-    if (p == 0) {
-        const double* z = b.Z + ((size_t)i * M + row) * b.nrhs;
-        const int na = P.iw * P.nintr;
+    const double* Z = b.Z + (size_t)i * M * b.nrhs;
 #pragma unroll
-        for (int a = 0; a < 17; ++a) in.z[a] = a <= na ? z[a] : 0.0;
+    for (int q = 0; q < 5; ++q) {
+        const int e = t + q * NT;
+        in.z[q] = e < M * kZW && e % kZW < b.nrhs ? Z[(e / kZW) * b.nrhs + e % kZW] : 0.0;
     }
 }
-// y_i from the staged coefficients and y_{i-s} / y_{i+s} (LDS); y_i into yo (LDS)
-__device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P, int i, int s, const BackIn& in,
-                                           const double* yl, const double* yr, double* yo, double* Xs, double* u,
-                                           const double* xc, bool own) {
-    const int t = threadIdx.x, row = t >> 2, p = t & 3;
-    const bool hl = s > 0, hr = s > 0 && i + s < b.N;
-    const bool use = p < 2 ? hl : hr;
+// the staged block into LDS (after the barrier that ends the previous block)
+__device__ __forceinline__ void back_stage(const BackIn& in, double* Ws, double* Xs, double* Zs) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+        const int e = t + q * NT;
+        Ws[(e >> 7) * kLDW + (e & 127)] = in.w[q];
+    }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         const int e = t + q * NT;
         Xs[(e / M) * LD + e % M] = in.x[q];
     }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const int e = t + q * NT;
+        if (e < M * kZW) Zs[e] = in.z[q];
+    }
+}
+// y_i from the staged block (LDS) and y_{i-s} / y_{i+s} (LDS); y_i into yo
+// (LDS) and, if `own`, its real rows into yF.  Starts after a barrier that
+// made the staged block visible.
+__device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P, int i, int s, const double* Ws,
+                                           const double* Xs, const double* Zs, const double* yl, const double* yr,
+                                           double* yo, double* u, const double* xc, bool own) {
+    const int t = threadIdx.x, row = t >> 2, p = t & 3;
+    const bool hl = s > 0, hr = s > 0 && i + s < b.N;
+    const bool use = p < 2 ? hl : hr;
     double zr = 0.0;
     if (p == 0) {   // xc: the corner solution x_c, staged in LDS
         const int na = P.iw * P.nintr;
-        zr = in.z[0];
+        zr = Zs[row * kZW];
 #pragma unroll
-        for (int a = 0; a < 16; ++a)   // (static register indices; the same sum order as before)
-            if (a < na) zr -= in.z[1 + a] * xc[a];
+        for (int a = 0; a < 16; ++a)
+            if (a < na) zr -= Zs[row * kZW + 1 + a] * xc[a];
     }
     double acc = 0.0;
     if (use) {
         const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
+        const double* w = Ws + row * kLDW + 32 * p;   // [Wl | Wr]: p 0, 1 Wl halves, p 2, 3 Wr halves
 #pragma unroll
-        for (int q = 0; q < 32; ++q) acc = fma(in.w[q], y[q], acc);
+        for (int q = 0; q < 32; ++q) acc = fma(w[q], y[q], acc);
     }
     acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
     acc += __shfl_xor(acc, 2);
@@ -1579,15 +1597,20 @@ __device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P
     }
 }
 __device__ __forceinline__ int back_stride(int blk) { return blk & -blk; }   // 0 for the root
+// dynamic LDS of both back kernels (doubles)
+constexpr size_t kBackLds = (size_t)M * kLDW + (size_t)M * LD + (size_t)M * kZW + (size_t)kCone * M + 3 * M + 16;
 
 // fused: one workgroup per leaf (odd block; the root alone for one block)
 __global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem P) {
-    __shared__ double Xs[M * LD];
-    __shared__ double u[M];
-    __shared__ double ys[kCone][M];
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Ws = sm;
+    double* Xs = Ws + M * kLDW;
+    double* Zs = Xs + M * LD;
+    double* ys = Zs + M * kZW;       // [kCone][M]
+    double* u = ys + kCone * M;
+    double* xc = u + M;
     __shared__ int cb[kCone], cl[kCone], cr[kCone], cown[kCone];
     __shared__ int ncone;
-    __shared__ double xc[16];
     const int leaf = b.N >= 2 ? 2 * (int)blockIdx.x + 1 : 0;
     if (threadIdx.x < 16) xc[threadIdx.x] = (int)threadIdx.x < P.iw * P.nintr ? P.yF[P.nb + threadIdx.x] : 0.0;
     if (threadIdx.x == 0) {
@@ -1632,27 +1655,35 @@ __global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem
     }
     __syncthreads();
     const int n = ncone;
-    BackIn cur, nxt;
-    back_load(b, P, cb[0], back_stride(cb[0]), cur);
+    BackIn cur;
+    back_load(b, cb[0], back_stride(cb[0]), cur);
     for (int k = 0; k < n; ++k) {
         const int blk = cb[k], sb = back_stride(blk);
-        if (k + 1 < n) back_load(b, P, cb[k + 1], back_stride(cb[k + 1]), nxt);
-        back_block(b, P, blk, sb, cur, cl[k] >= 0 ? ys[cl[k]] : nullptr, cr[k] >= 0 ? ys[cr[k]] : nullptr, ys[k], Xs, u,
-                   xc, cown[k] != 0);
-        lds_barrier();   // (not __syncthreads: it would wait for nxt's loads here)
-        cur = nxt;
+        back_stage(cur, Ws, Xs, Zs);
+        if (k + 1 < n) back_load(b, cb[k + 1], back_stride(cb[k + 1]), cur);   // the next block, in flight meanwhile
+        lds_barrier();   // (not __syncthreads: it would wait for those loads here)
+        back_block(b, P, blk, sb, Ws, Xs, Zs, cl[k] >= 0 ? ys + cl[k] * M : nullptr, cr[k] >= 0 ? ys + cr[k] * M : nullptr,
+                   ys + k * M, u, xc, cown[k] != 0);
+        lds_barrier();
     }
 }
 
 // SFM_CTX_BA_SPLIT_BCR: one launch per level (s = 0: the root), y through b.Y
 __global__ __launch_bounds__(NT) void bcr_back_level_kernel(BcrArgs b, DevProblem P, int s) {
-    __shared__ double Xs[M * LD];
-    __shared__ double u[M];
-    __shared__ double yl[M], yr[M], yo[M], xc[16];
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* Ws = sm;
+    double* Xs = Ws + M * kLDW;
+    double* Zs = Xs + M * LD;
+    double* yl = Zs + M * kZW;
+    double* yr = yl + M;
+    double* yo = yr + M;
+    double* u = yo + M;
+    double* xc = u + M;
     const int i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
     if (i < 0 || i >= b.N) return;
     BackIn in;
-    back_load(b, P, i, s, in);
+    back_load(b, i, s, in);
+    back_stage(in, Ws, Xs, Zs);
     const int t = threadIdx.x;
     if (t < 16) xc[t] = t < P.iw * P.nintr ? P.yF[P.nb + t] : 0.0;
     if (s > 0 && t < M) {
@@ -1660,7 +1691,7 @@ __global__ __launch_bounds__(NT) void bcr_back_level_kernel(BcrArgs b, DevProble
         if (i + s < b.N) yr[t] = b.Y[(size_t)(i + s) * M + t];
     }
     __syncthreads();
-    back_block(b, P, i, s, in, yl, yr, yo, Xs, u, xc, true);
+    back_block(b, P, i, s, Ws, Xs, Zs, yl, yr, yo, u, xc, true);
     __syncthreads();
     if (t < M) b.Y[(size_t)i * M + t] = yo[t];
 }
@@ -1738,15 +1769,18 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         SFM_HIP(hipGetLastError());
     }
     (void)epoch;
+    const size_t lds_b = kBackLds * sizeof(double);
     if (!b.split) {
-        hipLaunchKernelGGL(bcr_back_cone_kernel, dim3(b.N >= 2 ? b.N / 2 : 1), dim3(NT), 0, s, b, P);
+        set_dyn_lds((const void*)bcr_back_cone_kernel, lds_b);
+        hipLaunchKernelGGL(bcr_back_cone_kernel, dim3(b.N >= 2 ? b.N / 2 : 1), dim3(NT), lds_b, s, b, P);
         SFM_HIP(hipGetLastError());
     } else {   // SFM_CTX_BA_SPLIT_BCR: one launch per level
-        hipLaunchKernelGGL(bcr_back_level_kernel, dim3(1), dim3(NT), 0, s, b, P, 0);
+        set_dyn_lds((const void*)bcr_back_level_kernel, lds_b);
+        hipLaunchKernelGGL(bcr_back_level_kernel, dim3(1), dim3(NT), lds_b, s, b, P, 0);
         SFM_HIP(hipGetLastError());
         for (int stride = s_top / 2; stride >= 1; stride /= 2) {
             const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-            hipLaunchKernelGGL(bcr_back_level_kernel, dim3(n_odd), dim3(NT), 0, s, b, P, stride);
+            hipLaunchKernelGGL(bcr_back_level_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, P, stride);
             SFM_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(bcr_verdict_kernel, dim3(1), dim3(1), 0, s, b, P);
