@@ -559,11 +559,12 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     const bool time_all = std::getenv("SFM_SCHUR_TIME_ALL") != nullptr;
     while (term < 0) {
         // ---- one step on the device ------------------------------------------
-        // the Schur launch is timed with events on the second and third steps of each
-        // solve only: an event pair costs ~12 us of stream serialisation
-        // (the first pass, which also forms the point scales, is not timed)
+        // the Schur launch is timed with events only on request
+        // (SFM_SCHUR_TIME_ALL, measurement: every launch but the first, which
+        // also forms the point scales): an event pair costs ~12 us of stream
+        // serialisation, which an untimed solve should not pay
         const bool first = step_no == 0;
-        const bool timed = time_all ? step_no >= 1 : (step_no == 1 || step_no == 2);
+        const bool timed = time_all && step_no >= 1;
         ++step_no;
         if (timed) SFM_HIP(hipEventRecord(ev[0], s));
         ba_schur(P, S.cp, S.in, S.X, radius, s, pl->stamps.p, O.jacobi_scaling && first);

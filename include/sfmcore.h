@@ -279,8 +279,12 @@ typedef struct sfm_ba_plan_info {
     double  last_kernel_ms[8];              /* per-phase device time of the
                                                last iteration (HIP events)   */
     int64_t schur_flops_per_iter;           /* algorithmic flops, Schur kernel*/
-    int64_t schur_launches;                 /* Schur launches in last run     */
-    double  schur_ms_total;                 /* summed Schur kernel time        */
+    int64_t schur_launches;                 /* timed Schur launches, last run  */
+    double  schur_ms_total;                 /* their summed kernel time (HIP
+                                               events; only with the
+                                               SFM_SCHUR_TIME_ALL diagnostic:
+                                               an event pair serialises the
+                                               stream, 0 launches otherwise) */
     int32_t rcs_solver;                     /* SFM_RCS_* the plan solves with  */
     int32_t tile_rows;                      /* Schur chunk tile height (64/80) */
 } sfm_ba_plan_info;
