@@ -18,6 +18,7 @@ struct BcrArgs {
     // Y: the back substitution's y, as 128 tagged granules per block; part: corner partials;
     // fail: [0] numerical, [1] wait timeout, [4] / [5] workgroup counters
     double *R = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
+    unsigned* yflag = nullptr;   // [N] back substitution: y_i published for epoch (bcr_back_kernel<true>)
     unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums
     bool split = false;   // SFM_CTX_BA_SPLIT_BCR: top, corner and each back-substitution level as own launches
 };
@@ -43,8 +44,10 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
 bool bcr_supported(const DevProblem& P);
 void bcr_setup(BcrArgs& b, const DevProblem& P);
 size_t bcr_doubles(const BcrArgs& b);
+// 8-byte words of the back substitution's tagged y granules at b.Y (zeroed once at bind)
+inline size_t bcr_y_granules(const BcrArgs& b) { return (size_t)b.N * 128; }
 void bcr_bind(BcrArgs& b, double* base);
-// (epoch: unused since the back substitution needs no flags; kept for the dense path's signature)
+// epoch: a value the y granules do not hold yet (the plan counts its solves from 1)
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch);
 
 }  // namespace sfm

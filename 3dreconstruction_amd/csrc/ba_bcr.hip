@@ -109,13 +109,47 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 }
 
 // One wave, one 16x16 output tile: acc += op(A)[ar.., k] op(B)[k, bc..] for
-// k in [k0, k1) (k1 - k0 a multiple of 16, at most 64).  op(A)[m][k] = TA ?
-// A[k][m] : A[m][k], op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the
-// product.  Every operand is read before the first MFMA, behind a scheduling
-// barrier: left alone, the scheduler sank each read next to its MFMA, which
-// then waited a full LDS latency per k step (round 5).
+// k in [k0, k1) (k1 - k0 a multiple of 16).  op(A)[m][k] = TA ? A[k][m] : A[m][k],
+// op(B)[k][n] = TB ? B[n][k] : B[k][n].  NEG negates the product.  The LDS
+// operands of the next 16-wide k chunk are read while the current chunk's four
+// MFMAs run, so a runtime-length product is not LDS-latency bound.
 template <bool TA, bool TB, bool NEG, class PA = const double*, class PB = const double*>
 __device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int ldb, int bc, int k0, int k1) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
+    double a[4], b[4];
+    auto load = [&](int k, double (&av)[4], double (&bv)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int kj = k + 4 * j + kk;
+            av[j] = TA ? A[kj * lda + ar + i] : A[(ar + i) * lda + kj];
+            bv[j] = TB ? B[(bc + i) * ldb + kj] : B[kj * ldb + bc + i];
+        }
+    };
+    load(k0, a, b);
+    for (int k = k0; k < k1; k += 16) {
+        double an[4], bn[4];
+        const bool more = k + 16 < k1;
+        if (more) load(k + 16, an, bn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(NEG ? -a[j] : a[j], b[j], acc, 0, 0, 0);
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[j] = an[j]; b[j] = bn[j]; }
+        }
+    }
+    return acc;
+}
+// Out-of-line tile products for the level kernel.  Its eight waves run
+// different code at the same time, and with every product inlined the kernel
+// was 61 KB of code: past the 64 KB instruction cache two CUs share, so the
+// pivot wave's diagonal factor waited on instruction fetches.  Operands are
+// typed by address space (LDS: ds_read; global: global_load), since a
+// generic pointer through a call would become flat accesses.
+typedef __attribute__((address_space(3))) const double lds_cd;
+template <bool TA, bool TB, bool NEG>
+__device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
+    // k1 - k0 is 16, 32, 48 or 64: every chunk's reads first, then the MFMA
+    // chain (the scheduler otherwise waits a full LDS latency per chunk)
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
     const int nc = (k1 - k0) >> 4;
     double a[16], b[16];
@@ -140,17 +174,6 @@ __device__ __forceinline__ v4d tile_mm(v4d acc, PA A, int lda, int ar, PB B, int
         }
     }
     return acc;
-}
-// Out-of-line tile products for the level kernel.  Its eight waves run
-// different code at the same time, and with every product inlined the kernel
-// was 61 KB of code: past the 64 KB instruction cache two CUs share, so the
-// pivot wave's diagonal factor waited on instruction fetches.  Operands are
-// typed by address space (LDS: ds_read; global: global_load), since a
-// generic pointer through a call would become flat accesses.
-typedef __attribute__((address_space(3))) const double lds_cd;
-template <bool TA, bool TB, bool NEG>
-__device__ __noinline__ v4d mm_ll(v4d acc, lds_cd* A, int lda, int ar, lds_cd* B, int ldb, int bc, int k0, int k1) {
-    return tile_mm<TA, TB, NEG>(acc, A, lda, ar, B, ldb, bc, k0, k1);
 }
 // the same over block rows k in [0, kM), kM in {56, 60, 64}: a super-block's
 // K real cameras fill 6K of its 64 rows and its W / z rows beyond them are
@@ -1482,218 +1505,156 @@ __global__ __launch_bounds__(NTL) void bcr_top_corner_kernel(BcrArgs b, DevProbl
 // real rows go to yF.  256 threads: thread (row, p) takes 32 of the row's 128
 // [Wl | Wr] coefficients, then 16 of the rows of X' (X staged in LDS);
 // four-lane sums in a fixed order.
-//
-// Round 5: dependency cones instead of a level-by-level dataflow.  Block i
-// needs y_{i-s} and y_{i+s}, both eliminated at coarser strides, and the
-// blocks a leaf (an odd block, eliminated first) depends on, transitively,
-// are about one per level: 8 blocks at C4's 100 super-blocks.  So one
-// workgroup per leaf computes its whole cone, root first, from the data the
-// forward pass left, with no hand-off between workgroups at all (the level-by-
-// level dataflow paid one inter-CU hand-off per level, ~2.7 us each), the
-// next block's coefficients prefetched into registers while the current one
-// is solved; each block's y goes to yF from one owner workgroup.  The
-// arithmetic per block is the same function in both launch shapes
-// (SFM_CTX_BA_SPLIT_BCR: one launch per level, y through global memory), so
-// they agree bit for bit.
-constexpr int kCone = 40;   // cone entries: log2(N) + 1 <= 40
-// a workgroup barrier that orders LDS only: __syncthreads' release fence
-// waits for every outstanding vector memory access (vmcnt(0) on gfx9, loads
-// included), which would drain the next block's prefetch at every barrier
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+// FLOW: every block of every level in one launch, top-down (workgroup k waits
+// only for workgroups < k, so any residency makes progress).  y_i (64
+// doubles) is handed over as 128 tagged granules {epoch, 32 bits} stored
+// write-through (Guideline 16 R2: the data is the flag, no fence either
+// side): a consumer's wave 0 re-reads its neighbours' granules until every
+// tag holds this solve's epoch, after staging everything the forward pass
+// left.  The last workgroup to finish publishes the solve verdict.
+constexpr int kYG = 128;   // granules per block
+__device__ __forceinline__ void put_y(unsigned long long* g, int row, double v, unsigned epoch) {
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(v), tag = (unsigned long long)epoch << 32;
+    __hip_atomic_store((gu64*)(g + 2 * row), tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)(g + 2 * row + 1), tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// One block's coefficients in registers, read coalesced (consecutive
-// threads, consecutive addresses): [Wl | Wr] (64 x 128), X (64 x 64) and the
-// first 17 columns of z.  (Read per thread along a row, as the level-by-level
-// kernel did, each load instruction touched 64 cache lines: with one
-// workgroup walking a whole cone that cost ~5 us per block.)
-constexpr int kLDW = 129, kZW = 17;
-struct BackIn {
-    double w[32], x[16], z[5];
-};
-__device__ __forceinline__ void back_load(const BcrArgs& b, int i, int s, BackIn& in) {
-    const int t = threadIdx.x;
-    const bool hl = s > 0, hr = s > 0 && i + s < b.N;
-    const double* Wl = b.Wl + (size_t)i * M * M;
-    const double* Wr = b.Wr + (size_t)i * M * M;
+// wave 0: granules of y_a (and y_b) into LDS dst_a / dst_b as doubles
+__device__ __forceinline__ void get_y(const unsigned long long* ga, const unsigned long long* gb, double* dst_a,
+                                      double* dst_b, unsigned epoch, double* fail) {
+    const int lane = threadIdx.x & 63;
+    unsigned va[2], vb[2];
+    for (unsigned spins = 0;;) {
+        bool ok = true;
 #pragma unroll
-    for (int q = 0; q < 32; ++q) {
-        const int e = t + q * NT, row = e >> 7, col = e & 127;
-        const bool use = col < M ? hl : hr;
-        in.w[q] = use ? (col < M ? Wl : Wr)[row * M + (col & (M - 1))] : 0.0;
+        for (int h = 0; h < 2; ++h) {
+            const unsigned long long x = __hip_atomic_load((gu64*)(ga + lane + 64 * h), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            va[h] = (unsigned)x;
+            ok &= (unsigned)(x >> 32) == epoch;
+            if (gb) {
+                const unsigned long long y = __hip_atomic_load((gu64*)(gb + lane + 64 * h), __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                vb[h] = (unsigned)y;
+                ok &= (unsigned)(y >> 32) == epoch;
+            }
+        }
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) {   // ~ seconds: a lost producer, never a normal wait
+            if (lane == 0) st_sc1(fail + 1, 1.0);   // a wait timeout, not a numerical failure
+            break;
+        }
     }
-    const double* X = b.L + (size_t)i * M * M;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) in.x[q] = X[t + q * NT];
-    const double* Z = b.Z + (size_t)i * M * b.nrhs;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        const int e = t + q * NT;
-        in.z[q] = e < M * kZW && e % kZW < b.nrhs ? Z[(e / kZW) * b.nrhs + e % kZW] : 0.0;
+    for (int h = 0; h < 2; ++h) {
+        reinterpret_cast<unsigned*>(dst_a)[lane + 64 * h] = va[h];   // little endian: granule 2j = low word of y_j
+        if (gb) reinterpret_cast<unsigned*>(dst_b)[lane + 64 * h] = vb[h];
     }
 }
-// the staged block into LDS (after the barrier that ends the previous block)
-__device__ __forceinline__ void back_stage(const BackIn& in, double* Ws, double* Xs, double* Zs) {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-        const int e = t + q * NT;
-        Ws[(e >> 7) * kLDW + (e & 127)] = in.w[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int e = t + q * NT;
-        Xs[(e / M) * LD + e % M] = in.x[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        const int e = t + q * NT;
-        if (e < M * kZW) Zs[e] = in.z[q];
-    }
-}
-// y_i from the staged block (LDS) and y_{i-s} / y_{i+s} (LDS); y_i into yo
-// (LDS) and, if `own`, its real rows into yF.  Starts after a barrier that
-// made the staged block visible.
-__device__ __forceinline__ void back_block(const BcrArgs& b, const DevProblem& P, int i, int s, const double* Ws,
-                                           const double* Xs, const double* Zs, const double* yl, const double* yr,
-                                           double* yo, double* u, const double* xc, bool own) {
-    const int t = threadIdx.x, row = t >> 2, p = t & 3;
-    const bool hl = s > 0, hr = s > 0 && i + s < b.N;
-    const bool use = p < 2 ? hl : hr;
-    double zr = 0.0;
-    if (p == 0) {   // xc: the corner solution x_c, staged in LDS
-        const int na = P.iw * P.nintr;
-        zr = Zs[row * kZW];
-#pragma unroll
-        for (int a = 0; a < 16; ++a)
-            if (a < na) zr -= Zs[row * kZW + 1 + a] * xc[a];
-    }
-    double acc = 0.0;
-    if (use) {
-        const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
-        const double* w = Ws + row * kLDW + 32 * p;   // [Wl | Wr]: p 0, 1 Wl halves, p 2, 3 Wr halves
-#pragma unroll
-        for (int q = 0; q < 32; ++q) acc = fma(w[q], y[q], acc);
-    }
-    acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
-    acc += __shfl_xor(acc, 2);
-    if (p == 0) u[row] = zr - acc;
-    lds_barrier();
-    // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
-    // exact zeros above the diagonal; the tiles above are not read)
-    double a2 = 0.0;
-    if (p >= (row >> 4)) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) a2 = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], a2);
-    }
-    a2 += __shfl_xor(a2, 1);
-    a2 += __shfl_xor(a2, 2);
-    if (p == 0) {
-        yo[row] = a2;
-        const int nreal = min(b.K, P.ncam - i * b.K) * 6;
-        if (own && row < nreal) P.yF[(size_t)i * b.K * 6 + row] = a2;
-    }
-}
-__device__ __forceinline__ int back_stride(int blk) { return blk & -blk; }   // 0 for the root
-// dynamic LDS of both back kernels (doubles)
-constexpr size_t kBackLds = (size_t)M * kLDW + (size_t)M * LD + (size_t)M * kZW + (size_t)kCone * M + 3 * M + 16;
 
-// fused: one workgroup per leaf (odd block; the root alone for one block)
-__global__ __launch_bounds__(NT) void bcr_back_cone_kernel(BcrArgs b, DevProblem P) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* Ws = sm;
-    double* Xs = Ws + M * kLDW;
-    double* Zs = Xs + M * LD;
-    double* ys = Zs + M * kZW;       // [kCone][M]
-    double* u = ys + kCone * M;
-    double* xc = u + M;
-    __shared__ int cb[kCone], cl[kCone], cr[kCone], cown[kCone];
-    __shared__ int ncone;
-    const int leaf = b.N >= 2 ? 2 * (int)blockIdx.x + 1 : 0;
-    if (threadIdx.x < 16) xc[threadIdx.x] = (int)threadIdx.x < P.iw * P.nintr ? P.yF[P.nb + threadIdx.x] : 0.0;
-    if (threadIdx.x == 0) {
-        // the cone: leaf, then every block a cone block needs, transitively
-        int n = 0;
-        cb[n++] = leaf;
-        for (int k = 0; k < n; ++k) {
-            const int blk = cb[k], sb = back_stride(blk);
-            if (sb == 0) continue;
-            const int dep[2] = {blk - sb, blk + sb};
-            for (int d = 0; d < 2; ++d) {
-                if (dep[d] >= b.N) continue;
-                bool have = false;
-                for (int m = 0; m < n; ++m) have |= cb[m] == dep[d];
-                if (!have && n < kCone) cb[n++] = dep[d];
+template <bool FLOW>
+__global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, int s_arg, unsigned epoch) {
+    __shared__ double Xs[M * LD];
+    __shared__ double u[M];
+    __shared__ double yl[M], yr[M];
+    int i = -1, s = 0;
+    if (FLOW) {   // workgroup k: the root, then the odd blocks of s_top / 2, ..., 1
+        int k = blockIdx.x;
+        if (k == 0) {
+            i = 0;
+        } else {
+            --k;
+            for (s = s_arg / 2; s >= 1; s >>= 1) {
+                const int n_odd = (b.N - s + 2 * s - 1) / (2 * s);
+                if (k < n_odd) {
+                    i = s + 2 * s * k;
+                    break;
+                }
+                k -= n_odd;
             }
         }
-        // dependency order: the root, then by decreasing stride
-        auto key = [](int blk) { return blk == 0 ? 1 << 30 : back_stride(blk); };
-        for (int k = 1; k < n; ++k)
-            for (int m = k; m > 0 && key(cb[m]) > key(cb[m - 1]); --m) {
-                const int tmp = cb[m];
-                cb[m] = cb[m - 1];
-                cb[m - 1] = tmp;
+    } else {      // one level: s_arg = 0 the root, else its odd blocks
+        s = s_arg;
+        i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
+    }
+    unsigned long long* Yg = reinterpret_cast<unsigned long long*>(b.Y);   // [N][kYG] granules
+    const int t = threadIdx.x, row = t >> 2, p = t & 3;
+    const bool valid = i >= 0 && i < b.N;
+    if (valid) {
+        const int l = i - s, r = i + s;
+        const bool hl = s > 0, hr = s > 0 && r < b.N;
+        const bool use = p < 2 ? hl : hr;
+        // everything of the forward pass first: this row's [Wl | Wr]
+        // coefficients, X into LDS, and z'_row
+        double w[32];
+        if (use) {
+            const double2* src = reinterpret_cast<const double2*>(
+                (p < 2 ? b.Wl : b.Wr) + (size_t)i * M * M + row * M + 32 * (p & 1));
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const double2 v = src[q];
+                w[2 * q] = v.x;
+                w[2 * q + 1] = v.y;
             }
-        for (int k = 0; k < n; ++k) {
-            const int blk = cb[k], sb = back_stride(blk);
-            cl[k] = cr[k] = -1;
-            for (int m = 0; m < k; ++m) {
-                if (sb && cb[m] == blk - sb) cl[k] = m;
-                if (sb && cb[m] == blk + sb) cr[k] = m;
-            }
-            // owner of y_blk's yF rows: the leaf itself, the even block left
-            // of it, and the last block when it is even with no odd block right
-            cown[k] = blk == leaf || blk == leaf - 1 || (blk == leaf + 1 && blk == b.N - 1);
         }
-        ncone = n;
-        if (blockIdx.x == 0) {   // every kernel that can set a failure word has finished
+        load_tile<64, M, NT>(Xs, LD, b.L + (size_t)i * M * M, M);
+        double zr = 0.0;
+        if (p == 0) {
+            const double* z = b.Z + ((size_t)i * M + row) * b.nrhs;
+            const double* xc = P.yF + P.nb;
+            zr = z[0];
+            for (int a = 0; a < P.iw * P.nintr; ++a) zr -= z[1 + a] * xc[a];
+        }
+        if (hl) {
+            if (t < 64) {
+                if (FLOW) get_y(Yg + (size_t)l * kYG, hr ? Yg + (size_t)r * kYG : nullptr, yl, yr, epoch, b.fail);
+                else {   // an earlier launch wrote them
+                    for (int e = t; e < 2 * kYG; e += 64) {
+                        const bool right = e >= kYG;
+                        if (right && !hr) break;
+                        reinterpret_cast<unsigned*>(right ? yr : yl)[e & (kYG - 1)] =
+                            (unsigned)Yg[(size_t)(right ? r : l) * kYG + (e & (kYG - 1))];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        double acc = 0.0;
+        if (use) {
+            const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
+#pragma unroll
+            for (int q = 0; q < 32; ++q) acc = fma(w[q], y[q], acc);
+        }
+        acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
+        acc += __shfl_xor(acc, 2);
+        if (p == 0) u[row] = zr - acc;
+        __syncthreads();
+        // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
+        // exact zeros above the diagonal; the tiles above are never written)
+        double a2 = 0.0;
+        if (p >= (row >> 4)) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) a2 = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], a2);
+        }
+        a2 += __shfl_xor(a2, 1);
+        a2 += __shfl_xor(a2, 2);
+        if (p == 0) {
+            put_y(Yg + (size_t)i * kYG, row, a2, epoch);
+            const int nreal = min(b.K, P.ncam - i * b.K) * 6;
+            if (row < nreal) P.yF[(size_t)i * b.K * 6 + row] = a2;
+        }
+    }
+    if (FLOW) {   // the last workgroup publishes the verdict (every timeout word drained before its ticket)
+        unsigned* counter = reinterpret_cast<unsigned*>(b.fail + 5);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0 &&
+            __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
             P.scal[kScSolveFail] = solve_verdict(b.fail);
             reset_verdict(b);
+            __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    __syncthreads();
-    const int n = ncone;
-    BackIn cur;
-    back_load(b, cb[0], back_stride(cb[0]), cur);
-    for (int k = 0; k < n; ++k) {
-        const int blk = cb[k], sb = back_stride(blk);
-        back_stage(cur, Ws, Xs, Zs);
-        if (k + 1 < n) back_load(b, cb[k + 1], back_stride(cb[k + 1]), cur);   // the next block, in flight meanwhile
-        lds_barrier();   // (not __syncthreads: it would wait for those loads here)
-        back_block(b, P, blk, sb, Ws, Xs, Zs, cl[k] >= 0 ? ys + cl[k] * M : nullptr, cr[k] >= 0 ? ys + cr[k] * M : nullptr,
-                   ys + k * M, u, xc, cown[k] != 0);
-        lds_barrier();
-    }
-}
-
-// SFM_CTX_BA_SPLIT_BCR: one launch per level (s = 0: the root), y through b.Y
-__global__ __launch_bounds__(NT) void bcr_back_level_kernel(BcrArgs b, DevProblem P, int s) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* Ws = sm;
-    double* Xs = Ws + M * kLDW;
-    double* Zs = Xs + M * LD;
-    double* yl = Zs + M * kZW;
-    double* yr = yl + M;
-    double* yo = yr + M;
-    double* u = yo + M;
-    double* xc = u + M;
-    const int i = s == 0 ? (blockIdx.x == 0 ? 0 : -1) : s + 2 * s * (int)blockIdx.x;
-    if (i < 0 || i >= b.N) return;
-    BackIn in;
-    back_load(b, i, s, in);
-    back_stage(in, Ws, Xs, Zs);
-    const int t = threadIdx.x;
-    if (t < 16) xc[t] = t < P.iw * P.nintr ? P.yF[P.nb + t] : 0.0;
-    if (s > 0 && t < M) {
-        yl[t] = b.Y[(size_t)(i - s) * M + t];
-        if (i + s < b.N) yr[t] = b.Y[(size_t)(i + s) * M + t];
-    }
-    __syncthreads();
-    back_block(b, P, i, s, Ws, Xs, Zs, yl, yr, yo, u, xc, true);
-    __syncthreads();
-    if (t < M) b.Y[(size_t)i * M + t] = yo[t];
 }
 
 // the verdict after per-level back substitution launches
@@ -1720,8 +1681,8 @@ void bcr_setup(BcrArgs& b, const DevProblem& P) {
 
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
-    // A C L(=X) Wl Wr | R Z Y (Y: [N][64] y of the split back substitution) | part | fail (+ counters)
-    return 5 * mm + 3 * mr + 512 * (size_t)b.N + 8;
+    // A C L(=X) Wl Wr | R Z Y | part | fail (+ counters) | y flags (one word per block)
+    return 5 * mm + 3 * mr + 512 * (size_t)b.N + 8 + ((size_t)b.N + 1) / 2 + 2;
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
@@ -1729,6 +1690,7 @@ void bcr_bind(BcrArgs& b, double* base) {
     b.A = base; b.C = b.A + mm; b.L = b.C + mm; b.Wl = b.L + mm; b.Wr = b.Wl + mm;
     b.R = b.Wr + mm; b.Z = b.R + mr; b.Y = b.Z + mr;
     b.part = b.Y + mr; b.fail = b.part + 512 * (size_t)b.N;
+    b.yflag = reinterpret_cast<unsigned*>(b.fail + 8);   // zeroed by the caller once
 }
 
 void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
@@ -1768,19 +1730,17 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
         SFM_HIP(hipGetLastError());
     }
-    (void)epoch;
-    const size_t lds_b = kBackLds * sizeof(double);
+    int n_back = 1;
+    for (int stride = s_top / 2; stride >= 1; stride /= 2) n_back += (b.N - stride + 2 * stride - 1) / (2 * stride);
     if (!b.split) {
-        set_dyn_lds((const void*)bcr_back_cone_kernel, lds_b);
-        hipLaunchKernelGGL(bcr_back_cone_kernel, dim3(b.N >= 2 ? b.N / 2 : 1), dim3(NT), lds_b, s, b, P);
+        hipLaunchKernelGGL(bcr_back_kernel<true>, dim3(n_back), dim3(NT), 0, s, b, P, s_top, epoch);
         SFM_HIP(hipGetLastError());
     } else {   // SFM_CTX_BA_SPLIT_BCR: one launch per level
-        set_dyn_lds((const void*)bcr_back_level_kernel, lds_b);
-        hipLaunchKernelGGL(bcr_back_level_kernel, dim3(1), dim3(NT), lds_b, s, b, P, 0);
+        hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(1), dim3(NT), 0, s, b, P, 0, epoch);
         SFM_HIP(hipGetLastError());
         for (int stride = s_top / 2; stride >= 1; stride /= 2) {
             const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-            hipLaunchKernelGGL(bcr_back_level_kernel, dim3(n_odd), dim3(NT), lds_b, s, b, P, stride);
+            hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(n_odd), dim3(NT), 0, s, b, P, stride, epoch);
             SFM_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(bcr_verdict_kernel, dim3(1), dim3(1), 0, s, b, P);
@@ -1928,33 +1888,11 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, i
         load_tile<64>(Li, LD, d.A + (int64_t)i * kDM * np + (int64_t)kk * kDM, (int)np);
         if (i != j) load_tile<64>(Lj, LD, d.A + (int64_t)j * kDM * np + (int64_t)kk * kDM, (int)np);
         __syncthreads();
-        // the wave's four tiles share row tile `wave` of L_i: every operand of
-        // the column read first (80 doubles), then the four accumulator chains
-        // interleaved (the same k order per tile as tile_mm: bit-identical)
-        {   // 16-deep chunks, the next chunk's reads issued before this chunk's MFMAs
-            const int lane = threadIdx.x & 63, li = lane & 15, kq = lane >> 4;
-            double a[2][4], bq[2][4][4];
-            auto load = [&](int c, int slot) {
 #pragma unroll
-                for (int st = 0; st < 4; ++st) {
-                    const int kj = 16 * c + 4 * st + kq;
-                    a[slot][st] = Li[(16 * wave + li) * LD + kj];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) bq[slot][q][st] = Lb[(16 * q + li) * LD + kj];
-                }
-            };
-            load(0, 0);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                if (c + 1 < 4) load(c + 1, (c + 1) & 1);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int st = 0; st < 4; ++st)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (!(i == j && q > wave))   // the diagonal tile's lower half (and its diagonal sub-tiles)
-                            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[c & 1][st], bq[c & 1][q][st], acc[q], 0, 0, 0);
-            }
+        for (int q = 0; q < 4; ++q) {
+            const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
+            if (i == j && tj > ti) continue;   // the diagonal tile's lower half (and its diagonal sub-tiles)
+            acc[q] = tile_mm<false, true, true>(acc[q], Li, LD, 16 * ti, Lb, LD, 16 * tj, 0, M);
         }
     }
 #pragma unroll

@@ -390,9 +390,11 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         pl->bcr.split = (ctx->flags & SFM_CTX_BA_SPLIT_BCR) != 0;
         pl->bcr_buf.alloc(bcr_doubles(pl->bcr));
         bcr_bind(pl->bcr, pl->bcr_buf.p);
-        // failure words and counters: zeroed once (each solve's last kernels
-        // reset what they used)
-        SFM_HIP(hipMemsetAsync(pl->bcr.fail, 0, 8 * sizeof(double), s));
+        // failure words, counters and y flags: zeroed once (each solve's last
+        // kernels reset what they used)
+        SFM_HIP(hipMemsetAsync(pl->bcr.fail, 0, 8 * sizeof(double) + sizeof(unsigned) * (size_t)pl->bcr.N, s));
+        // the back substitution's tagged y granules (tags = solve epochs from 1)
+        SFM_HIP(hipMemsetAsync(pl->bcr.Y, 0, sizeof(double) * bcr_y_granules(pl->bcr), s));
         if (std::getenv("SFM_BCR_STAMPS")) {
             pl->bcr_stamps.alloc(16);
             pl->bcr_stamps.zero(s);
