@@ -16,7 +16,7 @@ struct BcrArgs {
     double *A = nullptr, *C = nullptr, *L = nullptr, *Wl = nullptr, *Wr = nullptr;
     // R: rhs + arrow columns as updated; Z: each block's forward solve X R;
     // Y: the back substitution's y, as 128 tagged granules per block; part: corner partials;
-    // fail: [0] numerical, [1] wait timeout, [4] / [5] workgroup counters
+    // fail: [0] numerical, [1] wait timeout, [4] / [6] corner tickets, [5] back-substitution ticket
     double *R = nullptr, *Z = nullptr, *Y = nullptr, *part = nullptr, *fail = nullptr;
     unsigned* yflag = nullptr;   // [N] back substitution: y_i published for epoch (bcr_back_kernel<true>)
     unsigned long long* stamps = nullptr;   // SFM_BCR_STAMPS diagnostic: phase cycle sums

@@ -1410,32 +1410,61 @@ __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProbl
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // the partials are stored write-through (sc1) and drained above: a
-    // relaxed ticket publishes them, and the last arriver reads them with sc1
-    // loads (no release or acquire fence: Guideline 16, counter form)
+    // relaxed ticket publishes them, and a last arriver reads them with sc1
+    // loads (no release or acquire fence: Guideline 16, counter form).
+    // Two tickets (round 5): the last of blocks 1..N-1 sums their partials
+    // into slot N -- in the fused launch while workgroup 0 still factors the
+    // top -- and takes the second ticket, as does block 0 with its own
+    // partial; the last of those two adds slot 0 + slot N and solves.  (One
+    // ticket over all N left the N-partial sum to workgroup 0, after the top.)
+    unsigned* counter2 = reinterpret_cast<unsigned*>(b.fail + 6);
+    const int el = threadIdx.x >> 3, g = threadIdx.x & 7;   // 32 elements x 8 lanes per pass
+    const int nel = na * kQ;                                // partial doubles: rows 1..na, columns 0..na
     __syncthreads();
+    bool rest_sum = false;
+    if (I > 0) {
+        if (threadIdx.x == 0)
+            last = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (unsigned)b.N - 2;
+        __syncthreads();
+        if (!last) return;
+        if (threadIdx.x == 0) __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rest_sum = true;
+    }
+    if (rest_sum) {
+        // blocks [1 + g (N-1)/8, 1 + (g+1) (N-1)/8) per lane, the 8 lanes of an
+        // element then combined by a fixed xor butterfly (deterministic)
+        const int nr = b.N - 1;
+        for (int base = 0; base < nel && (int)threadIdx.x < NT; base += NT / 8) {
+            const int k = base + el;
+            const int J0 = 1 + nr * g / 8, J1 = 1 + nr * (g + 1) / 8;
+            double t = 0.0;
+            if (k < nel) {
+#pragma unroll 4
+                for (int J = J0; J < J1; ++J) t += ld_sc1(b.part + (size_t)J * 512 + k);
+            }
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o);
+            if (g == 0 && k < nel) st_sc1(b.part + (size_t)b.N * 512 + k, t);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        last = __hip_atomic_fetch_add((gu32*)counter2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (b.N > 1 ? 1u : 0u);
     __syncthreads();
     if (!last) return;
-    if (threadIdx.x == 0) __hip_atomic_store((gu32*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // partials of blocks [g N/8, (g+1) N/8) per lane, the 8 lanes of an
-    // element then combined by a fixed xor butterfly (deterministic)
-    auto sum_parts = [&](int off, int g) {
-        const int I0 = b.N * g / 8, I1 = b.N * (g + 1) / 8;
-        double t = 0.0;
-#pragma unroll 4
-        for (int J = I0; J < I1; ++J) t += ld_sc1(b.part + (size_t)J * 512 + off);
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o);
-        return t;
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)counter2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto sum_parts = [&](int off) {   // block 0's partial + the rest's sum (slot N)
+        const double t0 = ld_sc1(b.part + off);
+        return b.N > 1 ? t0 + ld_sc1(b.part + (size_t)b.N * 512 + off) : t0;
     };
-    const int el = threadIdx.x >> 3, g = threadIdx.x & 7;   // 32 elements x 8 lanes per pass
-    for (int base = 0; base < na * na + na && (int)threadIdx.x < NT; base += NT / 8) {
-        const int k = base + el;
+    for (int k = threadIdx.x; k < na * na + na; k += blockDim.x) {
         if (k < na * na) {
             const int a = k / na, c = k % na;   // lower triangle (a >= c), mirrored
-            const double red = sum_parts(a * kQ + (a >= c ? c : a) + 1, g);
-            if (g == 0 && a >= c) {
+            if (a >= c) {
+                const double red = sum_parts(a * kQ + c + 1);
                 double m = P.Scorner[(((size_t)(a / iw) * P.nintr + c / iw) * iw * iw) + (a % iw) * iw + c % iw];
                 if (a == c) {
                     const double lm = sqrt(clampd(P.cnF[P.nb + a], P.min_diag, P.max_diag) / radius);
@@ -1443,10 +1472,9 @@ __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProbl
                 }
                 Mc[a * 16 + c] = m - red;
             }
-        } else if (k < na * na + na) {
+        } else {
             const int a = k - na * na;
-            const double red = sum_parts(a * kQ, g);
-            if (g == 0) Mc[256 + a] = P.rhs[P.nb + a] - red;
+            Mc[256 + a] = P.rhs[P.nb + a] - sum_parts(a * kQ);
         }
     }
     __syncthreads();
@@ -1682,14 +1710,14 @@ void bcr_setup(BcrArgs& b, const DevProblem& P) {
 size_t bcr_doubles(const BcrArgs& b) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
     // A C L(=X) Wl Wr | R Z Y | part | fail (+ counters) | y flags (one word per block)
-    return 5 * mm + 3 * mr + 512 * (size_t)b.N + 8 + ((size_t)b.N + 1) / 2 + 2;
+    return 5 * mm + 3 * mr + 512 * ((size_t)b.N + 1) + 8 + ((size_t)b.N + 1) / 2 + 2;
 }
 
 void bcr_bind(BcrArgs& b, double* base) {
     const size_t mm = (size_t)b.N * M * M, mr = (size_t)b.N * M * b.nrhs;
     b.A = base; b.C = b.A + mm; b.L = b.C + mm; b.Wl = b.L + mm; b.Wr = b.Wl + mm;
     b.R = b.Wr + mm; b.Z = b.R + mr; b.Y = b.Z + mr;
-    b.part = b.Y + mr; b.fail = b.part + 512 * (size_t)b.N;
+    b.part = b.Y + mr; b.fail = b.part + 512 * ((size_t)b.N + 1);
     b.yflag = reinterpret_cast<unsigned*>(b.fail + 8);   // zeroed by the caller once
 }
 
