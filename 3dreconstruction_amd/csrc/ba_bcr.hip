@@ -1264,7 +1264,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
 // sp > 0: first block 0's update from its right neighbour sp, eliminated by
 // the last level (A_0 -= Wl_sp' Wl_sp, R_0 -= Wl_sp' z_sp; lower tiles only).
 __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* sm) {
-    const int ldr = b.nrhs + 1;
+    const int ldr = b.nrhs + 1, kM = bcr_kM(b);
     double* A = sm;
     double* X = A + M * LD;
     double* R = X + M * LD;
@@ -1305,7 +1305,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
             const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
             const int tj = q - ti * (ti + 1) / 2;
             v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-            acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * ti, Wb, LD, 16 * tj, 0, M);
+            acc = mm_ll_rows<true, false, true>(acc, L3(Wb), LD, 16 * ti, L3(Wb), LD, 16 * tj, kM);
             tile_st(A, LD, 16 * ti, 16 * tj, acc);
         };
         const int nrt = b.nrhs / 16;
@@ -1330,7 +1330,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
                 } else {
                     const int v = (t - 9) / nrt, tj = (t - 9) % nrt;
                     v4d acc = tile_ld(R, ldr, 16 * v, 16 * tj);
-                    acc = tile_mm<true, false, true>(acc, Wb, LD, 16 * v, Zb, ldr, 16 * tj, 0, M);
+                    acc = mm_ll_rows<true, false, true>(acc, L3(Wb), LD, 16 * v, L3(Zb), ldr, 16 * tj, kM);
                     tile_st(R, ldr, 16 * v, 16 * tj, acc);
                 }
             }
@@ -1345,7 +1345,7 @@ __device__ __forceinline__ void bcr_top_body(const BcrArgs& b, int sp, double* s
     if (wave < 4) {
         for (int tj = 0; tj < b.nrhs / 16; ++tj)
             tile_st(b.Z, b.nrhs, 16 * wave, 16 * tj,
-                    tile_mm<false, false, false>(zero4(), X, LD, 16 * wave, R, ldr, 16 * tj, 0, 16 * (wave + 1)));
+                    mm_ll<false, false, false>(zero4(), L3(X), LD, 16 * wave, L3(R), ldr, 16 * tj, 0, 16 * (wave + 1)));
     } else {
         for (int e = threadIdx.x - 256; e < M * M; e += NTL - 256) b.L[e] = X[(e / M) * LD + e % M];
     }
