@@ -184,6 +184,32 @@ def test_bcr_matches_sequential_band_solver(ctx):
         assert a.step_is_successful == b.step_is_successful
 
 
+@pytest.mark.parametrize("n_cam,k", [(105, 11), (64, 9)])
+def test_bcr_band_shapes_vs_oracle_and_band_solver(ctx, n_cam, k):
+    """BCR shapes the C4 scene does not reach: a band of 10 camera blocks
+    (k = 11: D = 10, K = 10 cameras per super-block, 60 real rows, the last
+    diagonal tile's 12-pivot factor, products over 60 rows) with an odd
+    super-block count (11: the first level also packs the last, even block);
+    and K = 9 with a short last super-block (64 cameras = 7 blocks + 1
+    camera).  Oracle trajectory and the sequential band solver's decisions."""
+    sc = H.Scene(n_cam, 6000, k, seed=5150 + k)
+    gs, os_ = _compare(ctx, sc)
+    assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
+    res = []
+    for band in (False, True):
+        with H.engine_ctx(abi.SFM_CTX_BA_SEQ_BAND if band else 0) as c:
+            plan = api.BAPlan(c, sc.problem(), *sc.params())
+            assert plan.info().rcs_solver == (abi.SFM_RCS_SEQ_BAND if band else abi.SFM_RCS_BCR)
+            _, s = plan.run()
+            res.append((s, plan.trace()))
+            plan.close()
+    (s0, t0), (s1, t1) = res
+    assert s0.iterations == s1.iterations
+    assert abs(s0.final_cost / s1.final_cost - 1) < 1e-9
+    for a, b in zip(t0, t1):
+        assert a.step_is_successful == b.step_is_successful
+
+
 def test_cpp_facade_drop_in():
     """The C++ façade (include/sfm/sfm.hpp) driven like SequentialActuator /
     sparseBuilder, checked against the oracle inside the binary."""
