@@ -93,14 +93,6 @@ __device__ __forceinline__ unsigned long long stamp() {
     return t;
 }
 
-// a workgroup barrier that orders LDS only: __syncthreads' release fence
-// waits for every outstanding vector memory access (vmcnt(0) on gfx9, loads
-// included), which would drain loads deliberately left in flight across it
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -831,9 +823,6 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
     if (threadIdx.x < 4) pdone[threadIdx.x] = 0u;
-    // levels after the first: A_i and R_i stay in flight in registers while
-    // S0 forms A_00's update from the neighbours' W blocks, and reach LDS
-    // after it (S0 reads only W; A is first read in window 0)
     TileFetch<64, M, NTL> fa;
     TileFetch<16, M, NTL> frc;
     if (sp == 0) {
@@ -882,9 +871,10 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         if (hz) frc.fetch(b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs);
         fwa.put(Wa_l, M);
         if (hwb) fwb.put(Wb_l, M);
+        fa.put(A, LD);
+        if (hz) frc.put(Rc, L16);
     }
-    if (sp == 0) __syncthreads();
-    else lds_barrier();   // (A_i, R_i still in flight: not __syncthreads)
+    __syncthreads();
     if (st) {
         t1 = stamp();
         if (threadIdx.x == 0) atomicAdd(st + 5, t1 - t0);   // loads
@@ -1035,10 +1025,6 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, 16 * v + 16);
         else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, 16 * v + 16);
         if (upd) tile_st(tile_at(1, kS0[wave][0], kS0[wave][1]), LD, 0, 0, part);
-        if (upd) {   // A_i and R_i, in flight since the loads (above)
-            fa.put(A, LD);
-            if (hz) frc.put(Rc, L16);
-        }
     }
     __syncthreads();
     // ---- forward substitution of this workgroup's column tile w -------------
