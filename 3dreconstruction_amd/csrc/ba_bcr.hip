@@ -678,45 +678,6 @@ struct BandCol {
         return r >= nreal && r == c ? 1.0 : x;   // padding: identity
     }
 };
-// C (block (I, I-1)) and R gathers with the column terms formed once (as BandCol)
-struct BandC {
-    int c0, nreal, Dp, cj, cm;
-    bool colok;
-    __device__ BandC(const BcrArgs& b, const DevProblem& P, int I, int c, bool on) {
-        c0 = I * b.K;
-        nreal = min(b.K, P.ncam - c0) * 6;
-        Dp = P.D + 1;
-        cj = c0 - b.K + c / 6;
-        cm = c % 6;
-        colok = on && I > 0 && c / 6 < b.K;
-    }
-    __device__ __forceinline__ double at(const DevProblem& P, int r) const {
-        const int ci = c0 + r / 6, d = ci - cj;
-        const bool ok = colok && r < nreal && d >= 1 && d <= P.D;
-        const double v = P.Sband[ok ? (ci * Dp + d) * 36 + (r % 6) * 6 + cm : 0];
-        return ok ? v : 0.0;
-    }
-};
-struct BandR {
-    int c0, nreal, off;   // off: rhs (0) or arrow column base (intr k, row a), -1: none
-    bool rhs;
-    __device__ BandR(const BcrArgs& b, const DevProblem& P, int I, int c, bool on) {
-        c0 = I * b.K;
-        nreal = min(b.K, P.ncam - c0) * 6;
-        rhs = on && c == 0;
-        const bool arrow = on && c > 0 && c - 1 < P.iw * P.nintr;
-        const int k = (c - 1) / P.iw, a = (c - 1) % P.iw;
-        off = arrow ? k * P.ncam * 6 * P.iw + a * 6 : -1;
-    }
-    __device__ __forceinline__ double at(const DevProblem& P, int r) const {
-        const int ci = c0 + r / 6, rm = r % 6;
-        const bool real = r < nreal;
-        const bool ar = real && off >= 0, rh = real && rhs;
-        const double vr = P.rhs[rh ? 6 * ci + rm : 0];
-        const double va = P.Sarrow[ar ? off + ci * 6 * P.iw + rm : 0];
-        return rh ? vr : ar ? va : 0.0;
-    }
-};
 // rows [r0, r0 + 16) of super-block I's A and R, gathered to global memory
 // (the first level kernel, for the even blocks beside its odd ones)
 template <int TH>
@@ -878,15 +839,12 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
             const int e = threadIdx.x + q * NTL;
             va[q] = col.a(P, e / M, e % M);
         }
-        const BandC ccol(b, P, i, 16 * w + threadIdx.x % 16, true);    // Cc: column 16w + t % 16
-        const BandC rcol(b, P, r, threadIdx.x % M, hr);                 // Cr: column t % 64
-        const BandR zcol(b, P, i, 16 * w + threadIdx.x % 16, hz);      // Rc: column 16w + t % 16
 #pragma unroll
         for (int q = 0; q < QC; ++q) {
             const int e = threadIdx.x + q * NTL;
-            vc[q] = ccol.at(P, e / 16);
-            vr[q] = rcol.at(P, 16 * w + e / M);
-            vz[q] = zcol.at(P, e / 16);
+            vc[q] = pack_c(b, P, i, e / 16, 16 * w + e % 16);
+            vr[q] = pack_c(b, P, r, 16 * w + e / M, e % M, hr);
+            vz[q] = pack_r(b, P, i, e / 16, 16 * w + e % 16, hz);
         }
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
