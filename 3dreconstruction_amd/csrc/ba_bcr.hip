@@ -789,22 +789,46 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
 // later levels.
 constexpr int NTL = 512, NWL = NTL / 64;   // level kernel: 8 waves
 
+__device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProblem& P, double radius, int I,
+                                                bool z_fresh);
+
+// TOP (round 5): the root, super-block 0, as a level item with only its right
+// neighbour sp = s / 2 (eliminated by the last level): workgroups 0..3 (w)
+// factor A_0 - Wl_sp' Wl_sp with the level schedule and store row tile w of
+// X_0 and column tile w of z_0 = X_0 (R_0 - Wl_sp' z_sp) -- no C_i / C_r
+// outputs.  Fused launch (grid > 4): workgroups 4.. add the corner partials
+// of blocks 1..N-1 meanwhile, and workgroup 0 adds block 0's after its z_0
+// (bcr_corner_body; nrhs = 16 only, so that z_0 is one workgroup's).  The
+// top used to be one workgroup with the barrier-phased chol_inv64.
+template <bool TOP>
 __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P, double radius, int s, int n_odd) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    // XCD-aware: workgroup b runs on XCD b % 8, so the four workgroups (w) of
-    // one item are b = x + 8 (4 j + w): the same XCD, whose L2 then serves the
-    // block's A and neighbour W tiles once for all four
-    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
-    const int item = xcd + 8 * (q >> 2), w = q & 3, sp = s >> 1;
-    if (item >= n_odd) {
+    int item, w;
+    if constexpr (TOP) {
+        if ((int)blockIdx.x >= 4) {
+            bcr_corner_body(b, P, radius, (int)blockIdx.x - 3, false);
+            return;
+        }
+        item = 0;
+        w = blockIdx.x;
+    } else {
+        // XCD-aware: workgroup b runs on XCD b % 8, so the four workgroups (w) of
+        // one item are b = x + 8 (4 j + w): the same XCD, whose L2 then serves the
+        // block's A and neighbour W tiles once for all four
+        const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3;
+        item = xcd + 8 * (q >> 2);
+        w = q & 3;
+    }
+    const int sp = s >> 1;
+    if (!TOP && item >= n_odd) {
         const int j = 2 * s * (item - n_odd);
         if (sp > 0 && j < b.N) update_tile_rows<NTL>(b, sp, j, w, sm);
         return;
     }
-    const int i = s + 2 * s * item;
+    const int i = TOP ? 0 : s + 2 * s * item;
     if (i >= b.N) return;
     const int r = i + s, wave = threadIdx.x >> 6;
-    const bool hr = r < b.N, hz = 16 * w < b.nrhs;
+    const bool hr = !TOP && r < b.N, hz = 16 * w < b.nrhs;
     const int np3 = 6 * b.K - 48;   // real pivots of the last diagonal tile
     const int kM = bcr_kM(b);
     constexpr int L16 = 17;
@@ -818,14 +842,14 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     double* bad = Rc + M * L16;
     double* col = bad + 2;          // [16] diag16 column scratch; stamp maxima (diagnostic)
     unsigned* pdone = reinterpret_cast<unsigned*>(col + 16);   // [4] P(k) items done (window hand-off)
-    unsigned long long* st = (b.stamps && w == 0) ? b.stamps : nullptr;
+    unsigned long long* st = (b.stamps && w == 0 && !TOP) ? b.stamps : nullptr;
     unsigned long long t0 = 0, t1 = 0;
     if (st) t0 = stamp();
     if (threadIdx.x == 0) bad[0] = 0.0;
     if (threadIdx.x < 4) pdone[threadIdx.x] = 0u;
     TileFetch<64, M, NTL> fa;
     TileFetch<16, M, NTL> frc;
-    if (sp == 0) {
+    if (!TOP && sp == 0) {
         // first level: gather the block straight from the reduced band (no
         // pack launch), A, column tile w of C_i, row tile w of C_r and column
         // tile w of R_i, every load in flight first; and rows 16w.. of the
@@ -865,11 +889,11 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         // the first: bgC / bgCr overwrite all of Cc and Cr, so they are not loaded)
         TileFetch<64, M, NTL> fwa, fwb;
         const bool hwb = i + sp < b.N;   // the neighbours' W blocks (the A update's operands)
-        fwa.fetch(b.Wr + (size_t)(i - sp) * M * M, M);
+        if (!TOP) fwa.fetch(b.Wr + (size_t)(i - sp) * M * M, M);
         if (hwb) fwb.fetch(b.Wl + (size_t)(i + sp) * M * M, M);
         fa.fetch(b.A + (size_t)i * M * M, M);
         if (hz) frc.fetch(b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs);
-        fwa.put(Wa_l, M);
+        if (!TOP) fwa.put(Wa_l, M);
         if (hwb) fwb.put(Wb_l, M);
         fa.put(A, LD);
         if (hz) frc.put(Rc, L16);
@@ -906,7 +930,8 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // upd: the neighbours eliminated at stride sp update A / R / C (every
     // level but the first, whose blocks come straight from bcr_pack)
     const bool upd = sp > 0;
-    const int il = i - sp, ir = i + sp;
+    // (TOP: no left neighbour -- its operands are never read, il is a placeholder)
+    const int il = TOP ? i : i - sp, ir = i + sp;
     const bool hir = upd && ir < b.N;
     const double* Z1 = b.Z + (size_t)il * M * b.nrhs + 16 * w;
     const double* Z2 = b.Z + (size_t)ir * M * b.nrhs + 16 * w;
@@ -927,18 +952,19 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         const int ti = kHt[h >> 1][0], tj = kHt[h >> 1][1];
         double* W = (h & 1) ? Wbl : Wal;
         if ((h & 1) && !hir) return;
+        if (!(h & 1) && TOP) return;
         tile_st(hp(h), LD, 0, 0, mm_ll_rows<true, false, false>(zero4(), L3(W), M, 16 * ti, L3(W), M, 16 * tj, kM));
     };
     auto sub_halves = [&](v4d acc, int t) {   // acc - half a - half b of tile t (fixed order)
         if (!upd) return acc;
-        acc -= tile_ld(hp(2 * t), LD, 0, 0);
+        if (!TOP) acc -= tile_ld(hp(2 * t), LD, 0, 0);
         if (hir) acc -= tile_ld(hp(2 * t + 1), LD, 0, 0);
         return acc;
     };
     // tile (ti, tj): its A update, then the trailing updates of steps 0..nk-1
     auto full = [&](int ti, int tj, int nk) {
         v4d acc = tile_ld(A, LD, 16 * ti, 16 * tj);
-        if (upd) acc = mm_ll_rows<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, kM);
+        if (upd && !TOP) acc = mm_ll_rows<true, false, true>(acc, L3(Wal), M, 16 * ti, L3(Wal), M, 16 * tj, kM);
         if (hir) acc = mm_ll_rows<true, false, true>(acc, L3(Wbl), M, 16 * ti, L3(Wbl), M, 16 * tj, kM);
         if (nk) acc = mm_ll<false, true, true>(acc, L3(A), LD, 16 * ti, L3(A), LD, 16 * tj, 0, 16 * nk);
         tile_st(A, LD, 16 * ti, 16 * tj, acc);
@@ -958,23 +984,23 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     auto bgR = [&](int v, const GTile& g1, const GTile& g2) {   // R_i[:, w] row tile v
         if (!hzu) return;
         v4d acc = tile_ld(Rc, L16, 16 * v, 0);
-        acc = mm_tr<true>(acc, L3(Wal), M, 16 * v, g1, kM);
+        if (!TOP) acc = mm_tr<true>(acc, L3(Wal), M, 16 * v, g1, kM);
         if (hir) acc = mm_tr<true>(acc, L3(Wbl), M, 16 * v, g2, kM);
         tile_st(Rc, L16, 16 * v, 0, acc);
     };
     auto bgC = [&](int v, const GTile& gl) {   // block (i, i-2sp) = (i, i-s)
-        if (upd) tile_st(Cc, L16, 16 * v, 0, mm_tr<true>(zero4(), L3(Wal), M, 16 * v, gl, kM));
+        if (upd && !TOP) tile_st(Cc, L16, 16 * v, 0, mm_tr<true>(zero4(), L3(Wal), M, 16 * v, gl, kM));
     };
     auto bgCr = [&](int v, const GTile& gr) {   // block (r, r-s) = (r, i)
         if (hr && hir) tile_st(Cr, LD, 0, 16 * v, mm_rt<true>(zero4(), gr, L3(Wbl), M, 16 * v, kM));
     };
     auto fetch_z = [&](GTile& g1, GTile& g2) {
         if (!hzu) return;
-        g1.fetch(Z1, b.nrhs);
+        if (!TOP) g1.fetch(Z1, b.nrhs);
         if (hir) g2.fetch(Z2, b.nrhs);
     };
     auto fetch_wl = [&](GTile& g) {
-        if (upd) g.fetch(WL, M);
+        if (upd && !TOP) g.fetch(WL, M);
     };
     auto fetch_wr = [&](GTile& g) {
         if (hr && hir) g.fetch(WR, M);
@@ -1022,8 +1048,9 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     {
         const int v = wave & 3;
         v4d part = zero4();
-        if (upd && wave < 4) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, 16 * v + 16);
-        else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, 16 * v + 16);
+        if (wave < 4) {
+            if (upd && !TOP) part = tile_mm<true, false, false>(part, L3(Wal), M, 0, L3(Wal), M, 0, 16 * v, 16 * v + 16);
+        } else if (hir) part = tile_mm<true, false, false>(part, L3(Wbl), M, 0, L3(Wbl), M, 0, 16 * v, 16 * v + 16);
         if (upd) tile_st(tile_at(1, kS0[wave][0], kS0[wave][1]), LD, 0, 0, part);
     }
     __syncthreads();
@@ -1065,11 +1092,17 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // window that produced X_kk (those waves are idle there); fs of row tile
     // k + 1 in window k + 1, after P(k) gave L_{k+1,k}
     auto gs_k = [&](int k) {
-        if (wave == 5) gs_l(Cc, k, Wlg, M);
-        else if (wave == 6 && hr) gs_r(k);
-        else if (wave == 7 && hz) gs_l(Rc, k, Zg, b.nrhs);
+        if (wave == 5) {
+            if (!TOP) gs_l(Cc, k, Wlg, M);
+        } else if (wave == 6 && hr) {
+            gs_r(k);
+        } else if (wave == 7 && hz) {
+            gs_l(Rc, k, Zg, b.nrhs);
+        }
     };
-    auto fs_lk = [&](int k) { fs_l(Cc, k); };
+    auto fs_lk = [&](int k) {
+        if (!TOP) fs_l(Cc, k);
+    };
     auto fs_zk = [&](int k) {
         if (hz) fs_l(Rc, k);
     };
@@ -1232,6 +1265,16 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     }
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
+    if constexpr (TOP) {
+        // fused launch: block 0's corner partial from the z_0 just stored
+        // (column tile 0: workgroup 0, nrhs = 16), drained first
+        if (w == 0 && gridDim.x > 4) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            bcr_corner_body(b, P, radius, 0, true);
+        }
+        return;
+    }
     if (st) {
         __syncthreads();
         if (threadIdx.x == 0) atomicAdd(st + 6, stamp() - t0);   // through the X copy
@@ -1734,22 +1777,34 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     const size_t lds_t = (3 * M * LD + 3 * M * ldr + 34) * sizeof(double);
     {   // sized for the largest nrhs (32)
         const size_t cap = 160 * 1024;
-        set_dyn_lds((const void*)bcr_level_kernel, cap);
+        set_dyn_lds((const void*)bcr_level_kernel<false>, cap);
         set_dyn_lds((const void*)bcr_top_kernel, cap);
+        set_dyn_lds((const void*)bcr_level_kernel<true>, lds_l);   // (+ the corner's static LDS)
     }
     int s_top = 1;
     for (int stride = 1; stride < b.N; stride *= 2) {
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
         const int n_even = stride > 1 ? (b.N + 2 * stride - 1) / (2 * stride) : 0;
-        hipLaunchKernelGGL(bcr_level_kernel, dim3(32 * ((n_odd + n_even + 7) / 8)), dim3(NTL), lds_l, s, b, P, radius,
-                           stride, n_odd);
+        hipLaunchKernelGGL(bcr_level_kernel<false>, dim3(32 * ((n_odd + n_even + 7) / 8)), dim3(NTL), lds_l, s, b, P,
+                           radius, stride, n_odd);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
     // the top, then the corner (one column left for the back substitution) --
     // one launch unless SFM_CTX_BA_SPLIT_BCR (A/B, tests) -- then every
-    // back-substitution level in one top-down dataflow launch
-    if (!b.split) {
+    // back-substitution level in one top-down dataflow launch.  The top runs
+    // as a level item (bcr_level_kernel<true>) when it has a neighbour and z_0
+    // is one column tile; else as one workgroup (bcr_top_body).
+    const bool top_level = b.N >= 2 && b.nrhs == 16;
+    if (top_level) {
+        hipLaunchKernelGGL(bcr_level_kernel<true>, dim3(b.split ? 4 : 3 + b.N), dim3(NTL), lds_l, s, b, P, radius,
+                           s_top, 1);
+        SFM_HIP(hipGetLastError());
+        if (b.split) {
+            hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);
+            SFM_HIP(hipGetLastError());
+        }
+    } else if (!b.split) {
         set_dyn_lds((const void*)bcr_top_corner_kernel, 156 * 1024);   // (160 KB less the corner's static LDS)
         hipLaunchKernelGGL(bcr_top_corner_kernel, dim3(b.N), dim3(NTL), lds_t, s, b, P, radius, s_top / 2);
         SFM_HIP(hipGetLastError());

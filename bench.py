@@ -752,6 +752,27 @@ def main():
     achieved = flops / (schur_avg_ms * 1e-3) / 1e12 if schur_n else 0.0
     log(f"BA: {iters} LM iterations in {dt:.3f}s -> {value:.1f} it/s, rmse "
         f"{summ.rmse_initial:.4f}->{summ.rmse_final:.4f}, schur avg {schur_avg_ms:.3f} ms")
+    fake_est = None
+    if args.fake_world > 1:
+        # --fake-world skips every exchange on the device, so its rate leaves
+        # out the per-iteration RCS all-reduce and scalar all-gather.  Estimate
+        # them as SURVEY §8(e) does: a ring all-reduce of the RCS over one
+        # 153 GB/s xGMI link, 2 (W-1)/W bytes, plus an assumed 10 us latency
+        # per collective (two per iteration).  An estimate, not a measurement.
+        W = args.fake_world
+        iw = ctx.lib.sfm_ba_intr_width(0)
+        ncam, nintr, D = info.n_cam_active, info.n_intr_active, info.band_blocks
+        nF = 6 * ncam + iw * nintr
+        rcs_doubles = ncam * (D + 1) * 36 + nintr * ncam * 6 * iw + (nintr * iw) ** 2 + 3 * nF + 1
+        ex_us = 2 * (W - 1) / W * rcs_doubles * 8 / 153e9 * 1e6 + 2 * 10.0
+        it_us = dt / iters * 1e6
+        fake_est = {"rank0_us_per_iter": it_us, "exchange_us_per_iter_est": ex_us,
+                    "rcs_bytes": rcs_doubles * 8,
+                    "lm_iters_per_s_with_exchange_est": 1e6 / (it_us + ex_us),
+                    "model": "ring all-reduce over one 153 GB/s xGMI link + 2 x 10 us collective latency"}
+        log(f"fake-world {W}: rank 0 {it_us:.1f} us/iter without exchanges; estimated exchange "
+            f"{ex_us:.1f} us/iter (RCS {rcs_doubles * 8 / 1e6:.2f} MB) -> "
+            f"~{fake_est['lm_iters_per_s_with_exchange_est']:.0f} LM-iters/s with exchanges (estimate)")
 
     # PCIe-inclusive: one sfm_ba_solve from host buffers (upload, symbolic
     # plan, solve, download) -- reported beside the bench value, never as it
@@ -1021,6 +1042,7 @@ def main():
                        "transport": transport},
             "obs_per_sec": obs_per_sec,
             "lm_iterations_per_solve": summ.iterations,
+            "fake_world_exchange_estimate": fake_est,
             "rmse_initial": summ.rmse_initial, "rmse_final": summ.rmse_final,
             "roofline": roof,
             "cpu_baseline": cpu,
