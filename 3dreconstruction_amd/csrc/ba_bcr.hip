@@ -790,7 +790,27 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
 constexpr int NTL = 512, NWL = NTL / 64;   // level kernel: 8 waves
 
 __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProblem& P, double radius, int I,
-                                                bool z_fresh);
+                                                bool z_fresh, bool part_done = false);
+// block I's corner partial (rows 1..na, columns 0..na of z_I' z_I) from this
+// wave's MFMA results q00 (and, nrhs = 32, q10 / q11), stored write-through
+__device__ __forceinline__ void corner_put(const BcrArgs& b, const DevProblem& P, int I, const v4d& q00,
+                                           const v4d& q10, const v4d& q11, int ntc) {
+    constexpr int kQ = 17;   // part row stride: columns 0..16
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4, na = P.iw * P.nintr;
+    double* out = b.part + (size_t)I * 512;
+    auto put = [&](const v4d& q, int r0, int c0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ga = r0 + kk + 4 * r, gc = c0 + i;
+            if (ga >= 1 && ga <= na && gc <= na) st_sc1(out + (ga - 1) * kQ + gc, q[r]);
+        }
+    };
+    put(q00, 0, 0);
+    if (ntc > 1) {
+        put(q10, 16, 0);
+        put(q11, 16, 16);
+    }
+}
 
 // TOP (round 5): the root, super-block 0, as a level item with only its right
 // neighbour sp = s / 2 (eliminated by the last level): workgroups 0..3 (w)
@@ -1075,7 +1095,14 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         const v4d o = mm_ll<false, false, false>(zero4(), L3(X), LD, 16 * k, L3(B), L16, 0, 16 * k, 16 * k + 16);
         tile_st(B, L16, 16 * k, 0, o);
         tile_st(G, ldg, 16 * k, 16 * w, o);
+        return o;
     };
+    // TOP, fused: wave 7 accumulates block 0's corner partial z_0' z_0 (column
+    // tile 0) from each row tile of z_0 as it forms it -- register r of the
+    // MFMA result holds rows 16k + kk + 4r, i.e. k-step 4k + r of the corner
+    // body's own product, in the same order (bit-identical)
+    v4d qz = zero4();
+    const bool q_here = TOP && w == 0 && gridDim.x > 4;
     auto fs_r = [&](int k) {   // Cr(0, k) -= sum_m Cr(0, m) L_km'
         v4d acc = tile_ld(Cr, LD, 0, 16 * k);
         acc = mm_ll<false, true, true>(acc, L3(Cr), LD, 0, L3(A), LD, 16 * k, 0, 16 * k);
@@ -1097,7 +1124,11 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         } else if (wave == 6 && hr) {
             gs_r(k);
         } else if (wave == 7 && hz) {
-            gs_l(Rc, k, Zg, b.nrhs);
+            const v4d o = gs_l(Rc, k, Zg, b.nrhs);
+            if (q_here) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) qz = __builtin_amdgcn_mfma_f64_16x16x4f64(o[r], o[r], qz, 0, 0, 0);
+            }
         }
     };
     auto fs_lk = [&](int k) {
@@ -1253,6 +1284,10 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // ---- P3: X's last row tile; the last row tile of every output -----------
     pphase(3);
     gs_k(3);
+    if (q_here && wave == 7) {   // block 0's corner partial, stored and drained
+        corner_put(b, P, 0, qz, zero4(), zero4(), 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (st && threadIdx.x == 0) {
         atomicAdd(st + 0, td);
         atomicAdd(st + 1, stamp() - tf0);
@@ -1266,12 +1301,11 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     if constexpr (TOP) {
-        // fused launch: block 0's corner partial from the z_0 just stored
-        // (column tile 0: workgroup 0, nrhs = 16), drained first
+        // fused launch: block 0's corner partial is stored (wave 7, above);
+        // its ticket, and the corner solve if this is the last arrival
         if (w == 0 && gridDim.x > 4) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            bcr_corner_body(b, P, radius, 0, true);
+            bcr_corner_body(b, P, radius, 0, true, true);
         }
         return;
     }
@@ -1401,14 +1435,14 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
 // (z_fresh: this workgroup wrote z_I itself just before -- the top, in the
 // fused launch -- so wave 0 reads it write-through, past this CU's L1)
 __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProblem& P, double radius, int I,
-                                                bool z_fresh) {
+                                                bool z_fresh, bool part_done) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int na = P.iw * P.nintr, iw = P.iw;   // bordered columns (<= 16)
     constexpr int kQ = 17;                      // part row stride: columns 0..16
     __shared__ double Mc[16 * 16 + 16];
     __shared__ int last;
     unsigned* counter = reinterpret_cast<unsigned*>(b.fail + 4);
-    if (wave == 0) {
+    if (wave == 0 && !part_done) {
         const int i = lane & 15, kk = lane >> 4, ntc = b.nrhs / 16;
         const double* Z = b.Z + (size_t)I * M * b.nrhs;
         double z0[16], z1[16];   // z[4 ks + kk][i], z[4 ks + kk][16 + i]: every load issued first
@@ -1438,19 +1472,7 @@ __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProbl
             }
         }
         // element (row kk + 4r, column i) of each tile; keep rows 1..na, columns 0..na
-        double* out = b.part + (size_t)I * 512;
-        auto put = [&](const v4d& q, int r0, int c0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int ga = r0 + kk + 4 * r, gc = c0 + i;
-                if (ga >= 1 && ga <= na && gc <= na) st_sc1(out + (ga - 1) * kQ + gc, q[r]);
-            }
-        };
-        put(q00, 0, 0);
-        if (ntc > 1) {
-            put(q10, 16, 0);
-            put(q11, 16, 16);
-        }
+        corner_put(b, P, I, q00, q10, q11, ntc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // the partials are stored write-through (sc1) and drained above: a
