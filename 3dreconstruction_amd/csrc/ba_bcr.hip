@@ -1714,10 +1714,12 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, i
         }
         __syncthreads();
         double acc = 0.0;
-        if (use) {
+        if (use) {   // four independent chains (a 32-long dependent fma chain was on the path)
             const double* y = (p < 2 ? yl : yr) + 32 * (p & 1);
+            double c4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int q = 0; q < 32; ++q) acc = fma(w[q], y[q], acc);
+            for (int q = 0; q < 32; ++q) c4[q & 3] = fma(w[q], y[q], c4[q & 3]);
+            acc = (c4[0] + c4[1]) + (c4[2] + c4[3]);
         }
         acc += __shfl_xor(acc, 1);   // (p0 + p1) + (p2 + p3): the same on the four lanes
         acc += __shfl_xor(acc, 2);
@@ -1726,9 +1728,11 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, i
         // y_j = sum_r X_rj u_r over X's lower tiles (its diagonal tiles carry
         // exact zeros above the diagonal; the tiles above are never written)
         double a2 = 0.0;
-        if (p >= (row >> 4)) {
+        if (p >= (row >> 4)) {   // (two independent chains)
+            double c2[2] = {0.0, 0.0};
 #pragma unroll
-            for (int q = 0; q < 16; ++q) a2 = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], a2);
+            for (int q = 0; q < 16; ++q) c2[q & 1] = fma(Xs[(16 * p + q) * LD + row], u[16 * p + q], c2[q & 1]);
+            a2 = c2[0] + c2[1];
         }
         a2 += __shfl_xor(a2, 1);
         a2 += __shfl_xor(a2, 2);
