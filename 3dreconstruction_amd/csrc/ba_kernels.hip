@@ -1156,6 +1156,42 @@ __device__ __forceinline__ double term_value(const DevProblem& P, const FlatTerm
     return (double)q.sign * P.src[idx];
 }
 
+// s += term k, k + step, ... (k < end), in that order.  Batches of 16: the
+// descriptors first, then the data they address; the next batch's
+// descriptors are issued behind this batch's data loads, and the tail batch
+// is masked (clamped loads, masked adds) -- so a lane's chain is about one
+// global round trip per 16 terms instead of two, and a few terms past a
+// multiple of 16 no longer run one dependent round trip pair each.  The
+// additions are those of the term-at-a-time loop, in its order (same bits).
+#ifndef SFM_REDUCE_BATCH
+#define SFM_REDUCE_BATCH 16
+#endif
+constexpr int kRB = SFM_REDUCE_BATCH;   // terms per batch (A/B builds only)
+__device__ __forceinline__ double sum_terms(const DevProblem& P, int k, int step, int end, int r, int cc) {
+    double s = 0.0;
+    if (k >= end) return s;
+    const int k_safe = k;
+    FlatTerm d[kRB];
+    auto ld_desc = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < kRB; ++j) {
+            const int kj = k0 + j * step;
+            d[j] = P.terms[kj < end ? kj : k_safe];
+        }
+    };
+    ld_desc(k);
+    for (; k < end; k += kRB * step) {
+        double v[kRB];
+#pragma unroll
+        for (int j = 0; j < kRB; ++j) v[j] = term_value(P, d[j], r, cc);
+        if (k + kRB * step < end) ld_desc(k + kRB * step);
+#pragma unroll
+        for (int j = 0; j < kRB; ++j)
+            if (k + j * step < end) s += v[j];
+    }
+    return s;
+}
+
 __device__ __forceinline__ double* target_base(const DevProblem& P, int kind) {
     switch (kind) {
         case 0: return P.Sband;
@@ -1228,29 +1264,10 @@ __global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_o
     // g, g + G, ... (a 6-vector target keeps 60 lanes busy instead of 6)
     const int E = live ? T.rows * T.cols : 64, G = 64 / E, g = e / E, el = e - g * E;
     const int r = live ? el / T.cols : 0, cc = live ? el % T.cols : 0;
-    // batches of 16 (then 4) independent loads; a target is a chain of
-    // dependent global round trips (term descriptor, then data), so the batch
-    // width sets its latency
+    // a target is a chain of dependent global round trips (term descriptor,
+    // then data): sum_terms keeps 16 terms and the next 16 descriptors in flight
     double s = 0.0;
-    if (live && g < G) {
-        const int GW = G * W;
-        int k = T.c_begin + ws * G + g;
-        for (; k + 15 * GW < T.c_end; k += 16 * GW) {
-            double v[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = term_value(P, P.terms[k + j * GW], r, cc);
-#pragma unroll
-            for (int j = 0; j < 16; ++j) s += v[j];
-        }
-        for (; k + 3 * GW < T.c_end; k += 4 * GW) {
-            double v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = term_value(P, P.terms[k + j * GW], r, cc);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s += v[j];
-        }
-        for (; k < T.c_end; k += GW) s += term_value(P, P.terms[k], r, cc);
-    }
+    if (live && g < G) s = sum_terms(P, T.c_begin + ws * G + g, G * W, T.c_end, r, cc);
     if (W > 1) {   // (uniform over the launch: every wave reaches the barrier)
         part[wave][e] = s;
         __syncthreads();
@@ -1290,18 +1307,7 @@ __device__ __forceinline__ void reduce_segment(const DevProblem& P, int vectors_
     constexpr int kQ = kReduceSeg / 4;
     const int q0 = k0 + wave * kQ, q1 = min(min(k0 + kReduceSeg, (int)T.c_end), q0 + kQ);
     double s = 0.0;
-    if (g < G) {
-        const int r = el / T.cols, cc = el % T.cols;
-        int k = q0 + g;
-        for (; k + 3 * G < q1; k += 4 * G) {
-            double v[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) v[t] = term_value(P, P.terms[k + t * G], r, cc);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) s += v[t];
-        }
-        for (; k < q1; k += G) s += term_value(P, P.terms[k], r, cc);
-    }
+    if (g < G) s = sum_terms(P, q0 + g, G, q1, el / T.cols, el % T.cols);
     __shared__ double part[4][64];
     __shared__ int last;
     part[wave][lane] = s;
