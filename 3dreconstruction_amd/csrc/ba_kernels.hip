@@ -1156,15 +1156,18 @@ __device__ __forceinline__ double term_value(const DevProblem& P, const FlatTerm
     return (double)q.sign * P.src[idx];
 }
 
-// s += term k, k + step, ... (k < end), in that order.  Batches of 16: the
+// s += term k, k + step, ... (k < end), in that order.  Batches of kRB: the
 // descriptors first, then the data they address; the next batch's
 // descriptors are issued behind this batch's data loads, and the tail batch
 // is masked (clamped loads, masked adds) -- so a lane's chain is about one
-// global round trip per 16 terms instead of two, and a few terms past a
-// multiple of 16 no longer run one dependent round trip pair each.  The
-// additions are those of the term-at-a-time loop, in its order (same bits).
+// global round trip per batch instead of two, and a few terms past a whole
+// batch no longer run one dependent round trip pair each.  The additions are
+// those of the term-at-a-time loop, in its order (same bits).  kRB = 8
+// (profiles/r05/r_red, same box): reduce 34.2 -> 34.9 us at C4, 20.5 ->
+// 19.0 at rank 0 of N = 8 (2836-2846 -> 2854-2856 LM-iters/s); 16 took the
+// kernel to 208 VGPRs, 2 waves per SIMD, and C4's reduce to 49.5 us.
 #ifndef SFM_REDUCE_BATCH
-#define SFM_REDUCE_BATCH 16
+#define SFM_REDUCE_BATCH 8
 #endif
 constexpr int kRB = SFM_REDUCE_BATCH;   // terms per batch (A/B builds only)
 __device__ __forceinline__ double sum_terms(const DevProblem& P, int k, int step, int end, int r, int cc) {
