@@ -14,6 +14,7 @@ enum : int {
     kScCost = 0, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E,  // summed over ranks
     kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScSolveFail,             // max over ranks
     kScXnorm2F, kScStepnorm2F, kScGmaxF,                                 // replicated
+    kScAccept,   // the device's copy of the host's accept decision (lm_spec_accept), 1 / 0
     kScCount
 };
 // kScSolveFail: 0 solved, 1 numerical failure (an invalid LM step),
@@ -46,6 +47,8 @@ struct DevProblem {
     const int32_t* gram_img;     // [n_gram_img] their indices (the Gram pass's workgroups)
     int64_t nb, nF;
     double huber_a, min_diag, max_diag;
+    // LM options the device's accept decision needs (lm_spec_accept)
+    double lm_min_rel, lm_ftol, lm_ptol;
     // shard data
     const int32_t* pt_off;
     const int32_t* obs_img;
@@ -121,8 +124,10 @@ struct DevProblem {
 
 void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s);
 // U blocks, cost and non-finite flag at (cp, intr, X); scaled with scaleF.
+// gate (device, optional): the pass runs only if *gate != 0 (the speculative
+// pass at the candidate, gated by finalize's kScAccept)
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
-                   hipStream_t s);
+                   hipStream_t s, const double* gate = nullptr);
 // Jacobi scaling at iteration 0: scaleF from the reduced cnF (after ba_reduce
 // of an unscaled pass); scaleE comes from ba_schur(..., scale_e = true).
 void ba_fscale(const DevProblem& P, hipStream_t s);
@@ -165,8 +170,8 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
 // seq: written to scal_host[kScCount] after the scalars when scal_host is set
 void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq = 0);
 // world > 1 (RCCL): combine the all-gathered scalars in rank order and publish them
-void ba_publish_gathered(const double* gathered, int world, double* scal, double* scal_host, hipStream_t s,
-                         unsigned long long seq);
+void ba_publish_gathered(const DevProblem& P, const double* gathered, int world, double* scal, double* scal_host,
+                         hipStream_t s, unsigned long long seq);
 size_t solve_lds_bytes(const DevProblem& P, bool* use_lds);
 size_t solve_window_doubles(const DevProblem& P);
 int ba_step_blocks(const DevProblem& P);

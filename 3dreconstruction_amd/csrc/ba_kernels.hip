@@ -434,7 +434,9 @@ __device__ __forceinline__ void reduce_scatter64(double (&v)[64], int lane) {
 template <int CM, int PASS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void image_gram_kernel(DevProblem P, const CamPre* __restrict__ cps,
                                                          const double* __restrict__ intr,
-                                                         const double* __restrict__ X) {
+                                                         const double* __restrict__ X,
+                                                         const double* __restrict__ gate) {
+    if (gate && *gate == 0.0) return;   // speculative pass, step not accepted (uniform)
     using kT = gram::SlotTable<CM>;
     constexpr int IW = kIW<CM>, FW = gram::FW<CM>, S0 = 64 * PASS;
     constexpr bool kHasCost = kT::kCost >= S0 && kT::kCost < S0 + 64;
@@ -2462,6 +2464,27 @@ __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
 // One 1024-thread workgroup walking every list took 12-13 us at C4 (a chain
 // of dependent loads per thread); the sums are now in a different (still
 // fixed) order.
+// The host's accept decision for this iteration's step (ba_solver.cpp
+// run_plan, "this iteration": an invalid step, the parameter and function
+// tolerance tests, then the relative decrease), restated on the scalars just
+// combined, same operations in the same order -- so the speculative Gram pass
+// at the candidate (ba_image_gram with gate) runs exactly when the host will
+// accept.  The host still checks the flag against its own decision (and runs
+// or redoes the pass on a mismatch), so no result depends on this copy.
+__device__ __forceinline__ bool lm_spec_accept(const double* sc, const DevProblem& P) {
+    const double model_change = -sc[kScModelAcc];
+    const bool finite = sc[kScSolveFail] == 0.0 && sc[kScStepBad] == 0.0 && isfinite(model_change);
+    if (!(finite && model_change > 0.0)) return false;
+    const double x_cost = sc[kScCost];
+    const double cand_cost = sc[kScCandBad] != 0.0 ? DBL_MAX : sc[kScCandCost];
+    const double x_norm = sqrt(sc[kScXnorm2E] + sc[kScXnorm2F]);
+    const double step_norm = sqrt(sc[kScStepnorm2E] + sc[kScStepnorm2F]);
+    if (step_norm <= P.lm_ptol * (x_norm + P.lm_ptol)) return false;
+    if (fabs(x_cost - cand_cost) <= P.lm_ftol * x_cost) return false;
+    const double rel = cand_cost >= DBL_MAX ? -DBL_MAX : (x_cost - cand_cost) / model_change;
+    return rel > P.lm_min_rel;
+}
+
 constexpr int kFinThreads = 256, kFinBlocks = 16;
 __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks,
                                                                unsigned long long seq) {
@@ -2535,11 +2558,19 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
         // publish to host-mapped memory: every scalar, a system-scope fence,
         // then the sequence word the host polls (no blit, no stream sync)
         if (threadIdx.x == 12) P.scal_host[kScSolveFail] = P.scal[kScSolveFail];
+        __syncthreads();   // every slot of P.scal is written
+        if (threadIdx.x == 0) {
+            const double acc = lm_spec_accept(P.scal, P) ? 1.0 : 0.0;
+            P.scal[kScAccept] = acc;
+            P.scal_host[kScAccept] = acc;
+        }
         if (threadIdx.x < 13) __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0)
             __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.scal_host + kScCount), seq,
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (threadIdx.x == 0) {
+        P.scal[kScAccept] = 0.0;   // a rank's partial scalars: decided after the combine
     }
 }
 
@@ -2547,10 +2578,11 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
 // combined in rank order (sums, maxima; the replicated slots are this rank's)
 // and published to host-mapped memory like finalize_kernel does at one rank,
 // so the host polls a sequence word instead of copying and synchronising
-__global__ void publish_gathered_kernel(const double* __restrict__ g, int world, double* __restrict__ scal,
-                                        double* __restrict__ host, unsigned long long seq) {
+__global__ void publish_gathered_kernel(DevProblem P, const double* __restrict__ g, int world,
+                                        double* __restrict__ scal, double* __restrict__ host,
+                                        unsigned long long seq) {
     const int k = threadIdx.x;
-    if (k < kScCount) {
+    if (k < kScCount && k != kScAccept) {
         double v = k < kScMaxEnd ? g[k] : scal[k];
         if (k < kScMaxEnd)
             for (int r = 1; r < world; ++r) {
@@ -2559,8 +2591,14 @@ __global__ void publish_gathered_kernel(const double* __restrict__ g, int world,
             }
         scal[k] = v;
         host[k] = v;
-        __threadfence_system();
     }
+    __syncthreads();   // the combined scalars: the accept decision (as finalize_kernel at one rank)
+    if (k == 0) {
+        const double acc = lm_spec_accept(scal, P) ? 1.0 : 0.0;
+        scal[kScAccept] = acc;
+        host[kScAccept] = acc;
+    }
+    if (k < kScCount) __threadfence_system();
     __syncthreads();
     if (k == 0)
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(host + kScCount), seq, __ATOMIC_RELEASE,
@@ -2605,12 +2643,14 @@ void ba_campre(const double* extr, int n_img, CamPre* out, hipStream_t s) {
     } while (0)
 
 void ba_image_gram(const DevProblem& P, const CamPre* cp, const double* intr, const double* X,
-                   hipStream_t s) {
+                   hipStream_t s, const double* gate) {
     if (P.n_gram_img <= 0) return;
     SFM_BY_MODEL_ALL(P, {
-        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_gram_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
+        hipLaunchKernelGGL((image_gram_kernel<CM, 0>), dim3(P.n_gram_img * P.gram_seg), dim3(256), 0, s, P, cp, intr,
+                           X, gate);
         if constexpr (gram::SlotTable<CM>::kPasses > 1)
-            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_gram_img * P.gram_seg), dim3(256), 0, s, P, cp, intr, X);
+            hipLaunchKernelGGL((image_gram_kernel<CM, 1>), dim3(P.n_gram_img * P.gram_seg), dim3(256), 0, s, P, cp,
+                               intr, X, gate);
     });
     SFM_HIP(hipGetLastError());
 }
@@ -2788,9 +2828,9 @@ void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq) {
     SFM_HIP(hipGetLastError());
 }
 
-void ba_publish_gathered(const double* gathered, int world, double* scal, double* scal_host, hipStream_t s,
-                         unsigned long long seq) {
-    hipLaunchKernelGGL(publish_gathered_kernel, dim3(1), dim3(64), 0, s, gathered, world, scal, scal_host, seq);
+void ba_publish_gathered(const DevProblem& P, const double* gathered, int world, double* scal, double* scal_host,
+                         hipStream_t s, unsigned long long seq) {
+    hipLaunchKernelGGL(publish_gathered_kernel, dim3(1), dim3(64), 0, s, P, gathered, world, scal, scal_host, seq);
     SFM_HIP(hipGetLastError());
 }
 

@@ -485,6 +485,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     DevProblem& P = pl->P;
     P.min_diag = O.min_lm_diagonal;
     P.max_diag = O.max_lm_diagonal;
+    P.lm_min_rel = O.min_relative_decrease;
+    P.lm_ftol = O.function_tolerance;
+    P.lm_ptol = O.parameter_tolerance;
     const auto t0 = std::chrono::steady_clock::now();
     std::memset(sum, 0, sizeof *sum);
     sum->num_residuals = 2 * h.n_obs;
@@ -535,6 +538,21 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     // (with an RCCL communicator, even a 1-rank one, the scalars go through
     // the all-gather and publish_gathered_kernel instead)
     P.scal_host = (!ctx->comm && (ctx->world == 1 || ctx->no_exchange)) ? pl->scal_dev : nullptr;
+    // Speculative Gram pass (round 5): where the device combines the scalars
+    // (finalize_kernel at one rank, publish_gathered_kernel over RCCL) it
+    // also takes the host's accept decision (lm_spec_accept), and the Gram
+    // pass at the candidate is launched right behind it, gated on that flag --
+    // so after an accepted step the pass runs while the host polls and
+    // decides, instead of after (the host-to-launch gap was 8 us at rank 0 of
+    // N = 8 and 16 us at C4 per accepted step, profiles/r05/*/iter_gaps_*).
+    // The host compares the flag with its own decision: it runs the pass if
+    // the device skipped it, and redoes it at the current point if the device
+    // ran it for a step the host rejects, so no result depends on the flag.
+#ifndef SFM_NO_SPEC_GRAM
+    const bool spec_gram = P.scal_host != nullptr || (ctx->comm && !ctx->host_allreduce);
+#else
+    const bool spec_gram = false;   // (A/B builds)
+#endif
     double radius = O.initial_trust_region_radius, decrease_factor = 2.0;
     int consecutive_invalid = 0;
     double x_cost = 0.0, x_norm = 0.0;
@@ -586,6 +604,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         const unsigned long long seq = ++pl->fin_seq;
         ba_finalize(P, s, seq);
         if (P.scal_host) {
+            if (spec_gram) ba_image_gram(P, S.cpc, S.inc, S.Xc, s, P.scal + kScAccept);
             wait_scalars(pl->scal_h, seq, s);
         } else if (ctx->comm && !ctx->host_allreduce) {
             // one RCCL collective: gather every rank's partial scalars; a
@@ -593,7 +612,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             // host-mapped memory, polled as at one rank (no copy, no sync)
             SFM_REQUIRE(rccl_allgather_f64(ctx->comm, P.scal, pl->scal_g.p, kScMaxEnd, s) == 0, SFM_ERR_COMM,
                         "RCCL all-gather failed");
-            ba_publish_gathered(pl->scal_g.p, ctx->world, P.scal, pl->scal_dev, s, seq);
+            ba_publish_gathered(P, pl->scal_g.p, ctx->world, P.scal, pl->scal_dev, s, seq);
+            if (spec_gram) ba_image_gram(P, S.cpc, S.inc, S.Xc, s, P.scal + kScAccept);
             wait_scalars(pl->scal_h, seq, s);
         } else {
             if (ctx->world > 1) {
@@ -612,6 +632,8 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             pl->last_ms[0] = ms;
         }
         const double* sc = pl->scal_h;
+        // the speculative pass at the candidate ran (spec_gram and the device accepted)
+        const bool spec_ran = spec_gram && sc[kScAccept] != 0.0;
 
         // ---- Finalize of the previous accepted iteration (needs g, x at x) ----
         if (relin_pending) {
@@ -647,6 +669,7 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         cur.step_is_valid = finite && model_change > 0.0;
         if (!cur.step_is_valid) {
             if (++consecutive_invalid >= O.max_num_consecutive_invalid_steps) { term = SFM_TERM_FAILURE; break; }
+            if (spec_ran) relinearize();   // (the device's copy of the decision differed: U back at x)
             radius = radius / decrease_factor;
             decrease_factor *= 2.0;
             cur.cost = x_cost;
@@ -671,12 +694,13 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
             radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * q - 1.0, 3));
             radius = std::min(O.max_trust_region_radius, radius);
             decrease_factor = 2.0;
-            relinearize();
+            if (!spec_ran) relinearize();   // (else already run at the candidate, now the current point)
             relin_pending = true;
             pending = cur;
             continue;   // Finalize after the gradient at the new x is known
         }
         cur.step_is_successful = 0;
+        if (spec_ran) relinearize();   // (the device's copy of the decision differed: U back at x)
         cur.cost = cand_cost;
         cur.gradient_max_norm = prev_gmax;
         radius = radius / decrease_factor;
