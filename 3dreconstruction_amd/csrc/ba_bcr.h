@@ -47,7 +47,18 @@ size_t bcr_doubles(const BcrArgs& b);
 // 8-byte words of the back substitution's tagged y granules at b.Y (zeroed once at bind)
 inline size_t bcr_y_granules(const BcrArgs& b) { return (size_t)b.N * 128; }
 void bcr_bind(BcrArgs& b, double* base);
+// The LM candidate, formed by the back substitution as each block's y is
+// known (cand_kernel's arithmetic, ba_cand.h): the current point's extrinsics
+// and intrinsics, and the candidate's extrinsics, intrinsics and CamPre
+struct BcrCand {
+    const double* extr;
+    const double* intr;
+    double* cand_extr;
+    double* cand_intr;
+    CamPre* cand_cp;
+};
 // epoch: a value the y granules do not hold yet (the plan counts its solves from 1)
-void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch);
+void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch,
+               const BcrCand& cand);
 
 }  // namespace sfm

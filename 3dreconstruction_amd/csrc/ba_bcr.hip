@@ -26,6 +26,7 @@
 #include <utility>
 
 #include "ba_bcr.h"
+#include "ba_cand.h"
 #include "common.h"
 
 // Inter-workgroup hand-offs in this file use the counter form of
@@ -1646,11 +1647,22 @@ __device__ __forceinline__ void get_y(const unsigned long long* ga, const unsign
     }
 }
 
+// The LM candidate of the block's cameras (BcrCand; round 5): as soon as y_i
+// is known, threads 0..K-1 each form one camera's candidate extrinsics and
+// CamPre with cand_kernel's arithmetic (ba_cand.h; their current values and
+// column scales loaded at the start, during the wait), and the block's norm
+// partial goes to part_f[i] (cameras in block order); the root also forms the
+// intrinsics' candidates (part_f[N]) and copies the images without camera
+// columns.  cand_kernel's launch and its dependent global round trips leave
+// the iteration (its ~8 us at C4 and at rank 0 of N = 8).
 template <bool FLOW>
-__global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, int s_arg, unsigned epoch) {
+__global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, int s_arg, unsigned epoch,
+                                                      BcrCand cand) {
     __shared__ double Xs[M * LD];
     __shared__ double u[M];
     __shared__ double yl[M], yr[M];
+    __shared__ double yc[M];
+    __shared__ double redc[16][3];
     int i = -1, s = 0;
     if (FLOW) {   // workgroup k: the root, then the odd blocks of s_top / 2, ..., 1
         int k = blockIdx.x;
@@ -1678,6 +1690,21 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, i
         const int l = i - s, r = i + s;
         const bool hl = s > 0, hr = s > 0 && r < b.N;
         const bool use = p < 2 ? hl : hr;
+        // this thread's camera (t < K) for the candidate: current values and
+        // column terms first, so their round trips overlap the wait for y
+        const int cb = i * b.K + t;
+        const bool cam = t < b.K && cb < P.ncam;
+        int cimg = 0;
+        double cx[6], csf[6], cbf[6];
+        if (cam) {
+            cimg = P.blk_img[cb];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                csf[a] = P.scaleF[6 * (size_t)cb + a];
+                cbf[a] = P.bF[6 * (size_t)cb + a];
+                cx[a] = cand.extr[6 * (size_t)cimg + a];
+            }
+        }
         // everything of the forward pass first: this row's [Wl | Wr]
         // coefficients, X into LDS, and z'_row
         double w[32];
@@ -1740,6 +1767,65 @@ __global__ __launch_bounds__(NT) void bcr_back_kernel(BcrArgs b, DevProblem P, i
             put_y(Yg + (size_t)i * kYG, row, a2, epoch);
             const int nreal = min(b.K, P.ncam - i * b.K) * 6;
             if (row < nreal) P.yF[(size_t)i * b.K * 6 + row] = a2;
+            yc[row] = a2;
+        }
+        __syncthreads();
+        // the candidate of camera t of this block (y published above)
+        CandAcc ca;
+        if (cam) {
+            double e[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                e[a] = cand_col(cx[a], yc[6 * t + a], csf[a], cbf[a], ca);
+                cand.cand_extr[6 * (size_t)cimg + a] = e[a];
+            }
+            cand.cand_cp[cimg] = make_campre(e);
+        }
+        if (t < 16) {
+            redc[t][0] = ca.x2;
+            redc[t][1] = ca.d2;
+            redc[t][2] = ca.gm;
+        }
+        if (i == 0) {
+            // the root: images without camera columns (copied, CamPre rebuilt
+            // as cand_kernel does) and the intrinsics (part_f[N])
+            for (int f = t; f < P.n_free; f += NT) {
+                const int img = P.free_img[f];
+                double e[6];
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    e[a] = cand.extr[6 * (size_t)img + a];
+                    cand.cand_extr[6 * (size_t)img + a] = e[a];
+                }
+                cand.cand_cp[img] = make_campre(e);
+            }
+            if (t == 0) {
+                CandAcc ci;
+                // SNAVELY: the 4th double is not a parameter (not moved, not in the norms)
+                const int iw = P.iw, na = P.cam_model == SFM_CAM_SNAVELY ? 3 : iw;
+                for (int q = 0; q < P.n_intr; ++q) {
+                    const int c0 = P.intr_col[q];
+                    for (int a = 0; a < iw; ++a) {
+                        const double x = cand.intr[iw * (size_t)q + a];
+                        const int64_t c = (int64_t)c0 + a;
+                        cand.cand_intr[iw * (size_t)q + a] =
+                            (c0 >= 0 && a < na) ? cand_col(x, P.yF[c], P.scaleF[c], P.bF[c], ci) : x;
+                    }
+                }
+                P.part_f[3 * (size_t)b.N] = ci.x2;
+                P.part_f[3 * (size_t)b.N + 1] = ci.d2;
+                P.part_f[3 * (size_t)b.N + 2] = ci.gm;
+            }
+        }
+        __syncthreads();
+        if (t == 0) {   // the block's cameras in order
+            double r3[3] = {0.0, 0.0, 0.0};
+            for (int c = 0; c < b.K; ++c) {
+                r3[0] += redc[c][0];
+                r3[1] += redc[c][1];
+                r3[2] = fmax(r3[2], redc[c][2]);
+            }
+            for (int k = 0; k < 3; ++k) P.part_f[3 * (size_t)i + k] = r3[k];
         }
     }
     if (FLOW) {   // the last workgroup publishes the verdict (every timeout word drained before its ticket)
@@ -1791,7 +1877,8 @@ void bcr_bind(BcrArgs& b, double* base) {
     b.yflag = reinterpret_cast<unsigned*>(b.fail + 8);   // zeroed by the caller once
 }
 
-void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
+void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t s, unsigned epoch,
+               const BcrCand& cand) {
     if (b.N == 1) {   // no level: the top reads the packed block
         hipLaunchKernelGGL(bcr_pack_kernel, dim3(16 * b.N), dim3(NT), 0, s, b, P, radius);
         SFM_HIP(hipGetLastError());
@@ -1843,14 +1930,14 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     int n_back = 1;
     for (int stride = s_top / 2; stride >= 1; stride /= 2) n_back += (b.N - stride + 2 * stride - 1) / (2 * stride);
     if (!b.split) {
-        hipLaunchKernelGGL(bcr_back_kernel<true>, dim3(n_back), dim3(NT), 0, s, b, P, s_top, epoch);
+        hipLaunchKernelGGL(bcr_back_kernel<true>, dim3(n_back), dim3(NT), 0, s, b, P, s_top, epoch, cand);
         SFM_HIP(hipGetLastError());
     } else {   // SFM_CTX_BA_SPLIT_BCR: one launch per level
-        hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(1), dim3(NT), 0, s, b, P, 0, epoch);
+        hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(1), dim3(NT), 0, s, b, P, 0, epoch, cand);
         SFM_HIP(hipGetLastError());
         for (int stride = s_top / 2; stride >= 1; stride /= 2) {
             const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
-            hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(n_odd), dim3(NT), 0, s, b, P, stride, epoch);
+            hipLaunchKernelGGL(bcr_back_kernel<false>, dim3(n_odd), dim3(NT), 0, s, b, P, stride, epoch, cand);
             SFM_HIP(hipGetLastError());
         }
         hipLaunchKernelGGL(bcr_verdict_kernel, dim3(1), dim3(1), 0, s, b, P);

@@ -63,6 +63,9 @@ struct DevProblem {
     const int32_t* img_coli;
     const int32_t* img_intr;
     const int32_t* intr_col;        // [n_intr] first F column of the intrinsic block or -1
+    const int32_t* blk_img;         // [ncam] image of each camera block (BCR back substitution's candidates)
+    const int32_t* free_img;        // [n_free] images without camera columns (their candidate is a copy)
+    int32_t n_free;
     const ReduceTarget* targets;
     const FlatTerm* terms;
     const double* src;              // contiguous [tiles | U | Ub | Ucn] the terms index
@@ -114,7 +117,8 @@ struct DevProblem {
     double* part_u;     // [n_img][2]
     double* part_s;     // [n_chunk + n_gpt][2]
     double* part_t;     // [n_step_blocks][kPartT]
-    double* part_f;     // [n_fblk][3] candidate-kernel partials
+    double* part_f;     // [n_fblk][3] candidate partials (cand_kernel's workgroups, or BCR: block i, then
+                        // [N] for the intrinsics)
     int32_t n_fblk;
     double* scal;       // [kScCount]
     double* fin_part;   // [16][12] finalize_kernel's workgroup partials

@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "ba_cand.h"
 #include "ba_kernels.h"
 #include "common.h"
 
@@ -49,7 +50,6 @@
 namespace sfm {
 namespace {
 
-constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::epsilon()
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
@@ -93,41 +93,8 @@ __device__ __forceinline__ double point_d2(const DevProblem& P, double diag, dou
 }
 
 // ---------------------------------------------------------------------------
-// per-camera precompute
+// per-camera precompute (make_campre: ba_cand.h)
 // ---------------------------------------------------------------------------
-__device__ inline CamPre make_campre(const double* e) {
-    CamPre cp;
-    const double w[3] = {e[0], e[1], e[2]};
-    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    cp.t[0] = e[3]; cp.t[1] = e[4]; cp.t[2] = e[5];
-    if (th2 > kEps) {
-        const double th = sqrt(th2), c = cos(th), s = sin(th), it = 1.0 / th, oc = 1.0 - c;
-        const double u[3] = {w[0] * it, w[1] * it, w[2] * it};
-        cp.c = c; cp.s = s; cp.omc = oc; cp.small = 0.0;
-        for (int a = 0; a < 3; ++a) cp.u[a] = u[a];
-        double* R = cp.R;
-        R[0] = c + oc * u[0] * u[0];        R[1] = oc * u[0] * u[1] - s * u[2]; R[2] = oc * u[0] * u[2] + s * u[1];
-        R[3] = oc * u[1] * u[0] + s * u[2]; R[4] = c + oc * u[1] * u[1];        R[5] = oc * u[1] * u[2] - s * u[0];
-        R[6] = oc * u[2] * u[0] - s * u[1]; R[7] = oc * u[2] * u[1] + s * u[0]; R[8] = c + oc * u[2] * u[2];
-        const double Wx[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-        for (int a = 0; a < 3; ++a)
-            for (int b = 0; b < 3; ++b) {
-                double acc = w[a] * w[b];
-                for (int k = 0; k < 3; ++k) acc += (R[k * 3 + a] - (a == k ? 1.0 : 0.0)) * Wx[k * 3 + b];
-                cp.Ar[a * 3 + b] = acc / th2;
-            }
-    } else {
-        cp.c = 1.0; cp.s = 0.0; cp.omc = 0.0; cp.small = 1.0;
-        for (int a = 0; a < 3; ++a) cp.u[a] = w[a];
-        const double Rs[9] = {1, -w[2], w[1], w[2], 1, -w[0], -w[1], w[0], 1};
-        for (int a = 0; a < 9; ++a) {
-            cp.R[a] = Rs[a];
-            cp.Ar[a] = (a % 4 == 0) ? 1.0 : 0.0;
-        }
-    }
-    return cp;
-}
-
 __global__ void campre_kernel(const double* __restrict__ extr, int n, CamPre* __restrict__ out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1608,17 +1575,8 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
                                                             double* __restrict__ cand_intr,
                                                             CamPre* __restrict__ cand_cp) {
     const int t = blockIdx.x * kCandThreads + threadIdx.x;
-    double v[2] = {0.0, 0.0};
-    double gm = 0.0;
-    auto col = [&](double x, int64_t c) {
-        const double cand = x + (-P.yF[c]) * P.scaleF[c];
-        const double d = x - cand;
-        v[0] += x * x;
-        v[1] += d * d;
-        const double g = P.bF[c] / P.scaleF[c];
-        gm = fmax(gm, fabs(x - (x - g)));
-        return cand;
-    };
+    CandAcc ca;
+    auto col = [&](double x, int64_t c) { return cand_col(x, P.yF[c], P.scaleF[c], P.bF[c], ca); };
     if (t < P.n_img) {
         const int c0 = P.img_colc[t];
         double e[6];
@@ -1639,8 +1597,9 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
             cand_intr[iw * (size_t)q + a] = (c0 >= 0 && a < na) ? col(x, (int64_t)c0 + a) : x;
         }
     }
+    double v[2] = {ca.x2, ca.d2};
     wave_sum(v);
-    gm = wave_max(gm);
+    const double gm = wave_max(ca.gm);
     constexpr int kW = kCandThreads / 64;
     __shared__ double red[kW][3];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;

@@ -42,7 +42,7 @@ struct sfm_ba_plan {
     DevProblem P{};
     DBuf<int32_t> gram_img;
     DBuf<int32_t> pt_off, obs_img, obs_slot, img_obs_ptr, img_colc,
-        img_coli, img_intr, intr_col, blk_img, blk_intr;
+        img_coli, img_intr, intr_col, blk_img, blk_intr, free_img;
     DBuf<double> obs_uv;
     DBuf<ChunkDesc> chunks;
     DBuf<int32_t> group_off;   // tile groups of chunks
@@ -164,6 +164,13 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(st, pl->img_intr, h.img_intr, s);
     up(st, pl->blk_img, h.blk_img, s);
     up(st, pl->blk_intr, h.blk_intr, s);
+    {   // images without camera columns (the gauge image, unobserved images)
+        std::vector<int32_t> fr;
+        for (int t = 0; t < prob.n_img; ++t)
+            if (h.img_colc[t] < 0) fr.push_back(t);
+        pl->P.n_free = (int32_t)fr.size();
+        up(st, pl->free_img, fr, s);
+    }
     if (h.zero_targets.empty()) {
         up(st, pl->targets, h.targets, s);
     } else {   // the zero list after the real targets, one buffer
@@ -271,6 +278,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.img_pt = pl->img_pt.p; P.img_uv = pl->img_uv.p;
     P.img_colc = pl->img_colc.p; P.img_coli = pl->img_coli.p; P.img_intr = pl->img_intr.p;
     P.intr_col = pl->intr_col.p;
+    P.blk_img = pl->blk_img.p;
+    P.free_img = pl->free_img.p;
     P.targets = pl->targets.p; P.terms = pl->terms.p; P.n_targets = (int32_t)h.targets.size();
     P.n_zero = (int32_t)h.zero_targets.size();
     {
@@ -361,9 +370,6 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     P.part_u = pl->part_u.p; P.part_s = pl->part_s.p;
     pl->part_t.alloc((size_t)kPartT * std::max(ba_step_blocks(P), 1));
     P.part_t = pl->part_t.p;
-    P.n_fblk = ba_cand_blocks(P);
-    pl->part_f.alloc(3 * (size_t)P.n_fblk);
-    P.part_f = pl->part_f.p;
     P.scal = pl->scal.p;
     pl->fin_part.alloc(16 * 12);
     pl->fin_count.alloc(1);
@@ -385,6 +391,17 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
             pl->dense.stamps = pl->bcr_stamps.p;
         }
     }
+    // candidate partials: the BCR back substitution forms them per super-block
+    // (+ one slot for the intrinsics), the other solvers through cand_kernel
+    if (pl->use_bcr) {
+        BcrArgs tmp;
+        bcr_setup(tmp, P);
+        P.n_fblk = tmp.N + 1;
+    } else {
+        P.n_fblk = ba_cand_blocks(P);
+    }
+    pl->part_f.alloc(3 * (size_t)P.n_fblk);
+    P.part_f = pl->part_f.p;
     if (pl->use_bcr) {
         bcr_setup(pl->bcr, P);
         pl->bcr.split = (ctx->flags & SFM_CTX_BA_SPLIT_BCR) != 0;
@@ -596,10 +613,11 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         ba_reduce(P, false, s);
         allreduce_rcs();
         if (P.dense) dense_solve(pl->dense, P, radius, s, ++pl->bcr_epoch);
-        else if (pl->use_bcr) bcr_solve(pl->bcr, P, radius, s, ++pl->bcr_epoch);
+        else if (pl->use_bcr)   // (the candidates: formed by its back substitution)
+            bcr_solve(pl->bcr, P, radius, s, ++pl->bcr_epoch, BcrCand{S.e, S.in, S.ec, S.inc, S.cpc});
         else ba_solve(P, radius, s);
         if (ctx->fail_solve_wait) ba_fill(P.scal + kScSolveFail, 1, kSolveWaitTimeout, s);   // diagnostic
-        ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
+        if (!pl->use_bcr) ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
         ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         const unsigned long long seq = ++pl->fin_seq;
         ba_finalize(P, s, seq);
