@@ -168,12 +168,9 @@ constexpr int kCandThreads = 256;
 int ba_cand_blocks(const DevProblem& P);
 void ba_cand(const DevProblem& P, const double* extr, const double* intr, double* cand_extr,
              double* cand_intr, CamPre* cand_cp, hipStream_t s);
-// (no general points: the step launch's last workgroup also does ba_finalize's
-// work -- ba_step_fuses_finalize -- and publishes with seq)
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
              const double* intr_cand, const double* X, double* X_cand, double radius,
-             hipStream_t s, unsigned long long seq);
-bool ba_step_fuses_finalize(const DevProblem& P);
+             hipStream_t s);
 // seq: written to scal_host[kScCount] after the scalars when scal_host is set
 void ba_finalize(const DevProblem& P, hipStream_t s, unsigned long long seq = 0);
 // world > 1 (RCCL): combine the all-gathered scalars in rank order and publish them

@@ -1612,139 +1612,6 @@ __global__ __launch_bounds__(kCandThreads) void cand_kernel(DevProblem P,
     }
 }
 
-// The host's accept decision for this iteration's step (ba_solver.cpp
-// run_plan, "this iteration": an invalid step, the parameter and function
-// tolerance tests, then the relative decrease), restated on the scalars just
-// combined, same operations in the same order -- so the speculative Gram pass
-// at the candidate (ba_image_gram with gate) runs exactly when the host will
-// accept.  The host still checks the flag against its own decision (and runs
-// or redoes the pass on a mismatch), so no result depends on this copy.
-__device__ __forceinline__ bool lm_spec_accept(const double* sc, const DevProblem& P) {
-    const double model_change = -sc[kScModelAcc];
-    const bool finite = sc[kScSolveFail] == 0.0 && sc[kScStepBad] == 0.0 && isfinite(model_change);
-    if (!(finite && model_change > 0.0)) return false;
-    const double x_cost = sc[kScCost];
-    const double cand_cost = sc[kScCandBad] != 0.0 ? DBL_MAX : sc[kScCandCost];
-    const double x_norm = sqrt(sc[kScXnorm2E] + sc[kScXnorm2F]);
-    const double step_norm = sqrt(sc[kScStepnorm2E] + sc[kScStepnorm2F]);
-    if (step_norm <= P.lm_ptol * (x_norm + P.lm_ptol)) return false;
-    if (fabs(x_cost - cand_cost) <= P.lm_ftol * x_cost) return false;
-    const double rel = cand_cost >= DBL_MAX ? -DBL_MAX : (x_cost - cand_cost) / model_change;
-    return rel > P.lm_min_rel;
-}
-
-constexpr int kFinThreads = 256, kFinBlocks = 16;
-// ONE: one workgroup (of 64..256 threads) sums every list itself and
-// publishes -- the fused tail of step_kernel (its last workgroup to finish);
-// else finalize_kernel's kFinBlocks workgroups of kFinThreads and a ticket.
-template <bool ONE>
-__device__ __forceinline__ void finalize_body(const DevProblem& P, int n_step_blocks, unsigned long long seq) {
-    double s[7] = {0, 0, 0, 0, 0, 0, 0};
-    double m[5] = {0, 0, 0, 0, 0};
-    // the four lists in one loop, so every list's loads are in flight together
-    const int nf = P.n_fblk, nu = P.n_img * P.gram_seg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
-    const int nmax = max(max(nf, nu), max(ns, nt));
-    const int kStride = ONE ? (int)blockDim.x : kFinBlocks * kFinThreads;
-#pragma unroll 2
-    for (int i = (ONE ? 0 : blockIdx.x * kFinThreads) + threadIdx.x; i < nmax; i += kStride) {
-        // loads from clamped indices (unconditional, so the compiler issues
-        // them all before the first use), accumulated only where in range
-        const bool bf = i < nf, bu = i < nu, bs = i < ns, bt = i < nt;
-        const int jf = bf ? i : 0, ju = bu ? i : 0, js = bs ? i : 0, jt = bt ? i : 0;
-        // (an empty list may have no buffer: its loads are skipped, uniformly)
-        double f0 = 0.0, f1 = 0.0, f2 = 0.0, u0 = 0.0, u1 = 0.0, s0 = 0.0, s1 = 0.0;
-        double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0, t4 = 0.0;
-        if (nf > 0) { f0 = P.part_f[3 * jf]; f1 = P.part_f[3 * jf + 1]; f2 = P.part_f[3 * jf + 2]; }
-        if (nu > 0) { u0 = P.part_u[2 * ju]; u1 = P.part_u[2 * ju + 1]; }
-        if (ns > 0) { s0 = P.part_s[2 * js]; s1 = P.part_s[2 * js + 1]; }
-        if (nt > 0) {
-            if (ONE) {   // (written by the other step workgroups of this launch: past L1)
-                const double* pt = P.part_t + kPartT * jt;
-                t0 = ld_wt64(pt); t1 = ld_wt64(pt + 1); t2 = ld_wt64(pt + 2); t3 = ld_wt64(pt + 3); t4 = ld_wt64(pt + 4);
-            } else {
-                t0 = P.part_t[kPartT * jt]; t1 = P.part_t[kPartT * jt + 1]; t2 = P.part_t[kPartT * jt + 2];
-                t3 = P.part_t[kPartT * jt + 3]; t4 = P.part_t[kPartT * jt + 4];
-            }
-        }
-        if (bf) { s[5] += f0; s[6] += f1; m[4] = fmax(m[4], f2); }
-        if (bu) { s[0] += u0; m[0] = fmax(m[0], u1); }
-        if (bs) { s[1] += s0; m[1] = fmax(m[1], s1); }
-        if (bt) { s[2] += t0; s[3] += t1; s[4] += t2; m[2] = fmax(m[2], t4); m[3] = fmax(m[3], t3); }
-    }
-    wave_sum(s);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) m[k] = wave_max(m[k]);
-    constexpr int kW = kFinThreads / 64;
-    __shared__ double red[kW][12];
-    __shared__ int last;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = ONE ? (int)(blockDim.x >> 6) : kW;
-    if (lane == 0) {
-        for (int k = 0; k < 7; ++k) red[wave][k] = s[k];
-        for (int k = 0; k < 5; ++k) red[wave][7 + k] = m[k];
-    }
-    __syncthreads();
-    constexpr int kSlot[12] = {kScCost, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E, kScXnorm2F,
-                               kScStepnorm2F, kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScGmaxF};
-    if (ONE) {
-        if (threadIdx.x < 12) {   // one thread per scalar, waves in order: the final values
-            const int k = threadIdx.x;
-            double t = red[0][k];
-            for (int w = 1; w < nw; ++w) t = k < 7 ? t + red[w][k] : fmax(t, red[w][k]);
-            P.scal[kSlot[k]] = t;
-            if (P.scal_host) P.scal_host[kSlot[k]] = t;
-        }
-    } else {
-        if (threadIdx.x < 12) {   // one thread per scalar, waves in order
-            const int k = threadIdx.x;
-            double t = red[0][k];
-            for (int w = 1; w < kW; ++w) t = k < 7 ? t + red[w][k] : fmax(t, red[w][k]);
-            st_wt64(P.fin_part + 12 * blockIdx.x + k, t);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0)
-            last = __hip_atomic_fetch_add((gu32_t*)P.fin_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   (unsigned)(kFinBlocks - 1);
-        __syncthreads();
-        if (!last) return;
-        if (threadIdx.x < 12) {   // the workgroups' partials in workgroup order
-            const int k = threadIdx.x;
-            double t = ld_wt64(P.fin_part + k);
-            for (int g = 1; g < kFinBlocks; ++g) {
-                const double v = ld_wt64(P.fin_part + 12 * g + k);
-                t = k < 7 ? t + v : fmax(t, v);
-            }
-            P.scal[kSlot[k]] = t;
-            if (P.scal_host) P.scal_host[kSlot[k]] = t;
-        }
-        if (threadIdx.x == 0)   // ready for the next launch (stream order)
-            __hip_atomic_store((gu32_t*)P.fin_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (P.scal_host) {
-        // publish to host-mapped memory: every scalar, a system-scope fence,
-        // then the sequence word the host polls (no blit, no stream sync)
-        if (threadIdx.x == 12) P.scal_host[kScSolveFail] = P.scal[kScSolveFail];
-        __syncthreads();   // every slot of P.scal is written
-        if (threadIdx.x == 0) {
-            const double acc = lm_spec_accept(P.scal, P) ? 1.0 : 0.0;
-            P.scal[kScAccept] = acc;
-            P.scal_host[kScAccept] = acc;
-        }
-        if (threadIdx.x < 13) __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.scal_host + kScCount), seq,
-                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else if (threadIdx.x == 0) {
-        P.scal[kScAccept] = 0.0;   // a rank's partial scalars: decided after the combine
-    }
-}
-
-__global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks,
-                                                               unsigned long long seq) {
-    finalize_body<false>(P, n_step_blocks, seq);
-}
-
 // ---------------------------------------------------------------------------
 // per-point back substitution, model cost change, candidate cost
 // One workgroup per Schur chunk, SPLIT threads per point (adjacent lanes, each
@@ -1764,8 +1631,7 @@ __global__ __launch_bounds__(kStepThreads) void step_kernel(DevProblem P, const 
                                                          const CamPre* __restrict__ cps_c,
                                                          const double* __restrict__ intr_c,
                                                          const double* __restrict__ X,
-                                                         double* __restrict__ Xc, double radius,
-                                                         unsigned long long seq, int fuse_fin) {
+                                                         double* __restrict__ Xc, double radius) {
     constexpr int IW = kIW<CM>;
     __shared__ CamPre scp[kCamSlots], scc[kCamSlots];
     __shared__ double csy[kCamSlots][6];        // camera scaleF * yF (0 for a constant image)
@@ -1918,24 +1784,8 @@ __global__ __launch_bounds__(kStepThreads) void step_kernel(DevProblem P, const 
     if (tid < kPartT) {
         double v = red[0][tid];
         for (int w = 1; w < nw; ++w) v = tid < 3 ? v + red[w][tid] : fmax(v, red[w][tid]);
-        if (fuse_fin) st_wt64(P.part_t + kPartT * (size_t)c + tid, v);
-        else P.part_t[kPartT * (size_t)c + tid] = v;
+        P.part_t[kPartT * (size_t)c + tid] = v;
     }
-    if (!fuse_fin) return;
-    // fused finalize (round 5; no general points, so this launch is the last
-    // producer of the iteration's partials): the partial is stored write-through
-    // and drained, a relaxed ticket (the counter form, as finalize_kernel), and
-    // the last workgroup sums every list and publishes (finalize_body<true>)
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0)
-        last = __hip_atomic_fetch_add((gu32_t*)P.fin_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    if (tid == 0) __hip_atomic_store((gu32_t*)P.fin_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    finalize_body<true>(P, (int)gridDim.x, seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -2573,6 +2423,116 @@ __global__ __launch_bounds__(kGStepThreads) void step_general_kernel(
 // One 1024-thread workgroup walking every list took 12-13 us at C4 (a chain
 // of dependent loads per thread); the sums are now in a different (still
 // fixed) order.
+// The host's accept decision for this iteration's step (ba_solver.cpp
+// run_plan, "this iteration": an invalid step, the parameter and function
+// tolerance tests, then the relative decrease), restated on the scalars just
+// combined, same operations in the same order -- so the speculative Gram pass
+// at the candidate (ba_image_gram with gate) runs exactly when the host will
+// accept.  The host still checks the flag against its own decision (and runs
+// or redoes the pass on a mismatch), so no result depends on this copy.
+__device__ __forceinline__ bool lm_spec_accept(const double* sc, const DevProblem& P) {
+    const double model_change = -sc[kScModelAcc];
+    const bool finite = sc[kScSolveFail] == 0.0 && sc[kScStepBad] == 0.0 && isfinite(model_change);
+    if (!(finite && model_change > 0.0)) return false;
+    const double x_cost = sc[kScCost];
+    const double cand_cost = sc[kScCandBad] != 0.0 ? DBL_MAX : sc[kScCandCost];
+    const double x_norm = sqrt(sc[kScXnorm2E] + sc[kScXnorm2F]);
+    const double step_norm = sqrt(sc[kScStepnorm2E] + sc[kScStepnorm2F]);
+    if (step_norm <= P.lm_ptol * (x_norm + P.lm_ptol)) return false;
+    if (fabs(x_cost - cand_cost) <= P.lm_ftol * x_cost) return false;
+    const double rel = cand_cost >= DBL_MAX ? -DBL_MAX : (x_cost - cand_cost) / model_change;
+    return rel > P.lm_min_rel;
+}
+
+constexpr int kFinThreads = 256, kFinBlocks = 16;
+__global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int n_step_blocks,
+                                                               unsigned long long seq) {
+    double s[7] = {0, 0, 0, 0, 0, 0, 0};
+    double m[5] = {0, 0, 0, 0, 0};
+    // the four lists in one loop, so every list's loads are in flight together
+    const int nf = P.n_fblk, nu = P.n_img * P.gram_seg, ns = P.n_chunk + P.n_gpt, nt = n_step_blocks;
+    const int nmax = max(max(nf, nu), max(ns, nt));
+    constexpr int kStride = kFinBlocks * kFinThreads;
+#pragma unroll 2
+    for (int i = blockIdx.x * kFinThreads + threadIdx.x; i < nmax; i += kStride) {
+        // loads from clamped indices (unconditional, so the compiler issues
+        // them all before the first use), accumulated only where in range
+        const bool bf = i < nf, bu = i < nu, bs = i < ns, bt = i < nt;
+        const int jf = bf ? i : 0, ju = bu ? i : 0, js = bs ? i : 0, jt = bt ? i : 0;
+        // (an empty list may have no buffer: its loads are skipped, uniformly)
+        double f0 = 0.0, f1 = 0.0, f2 = 0.0, u0 = 0.0, u1 = 0.0, s0 = 0.0, s1 = 0.0;
+        double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0, t4 = 0.0;
+        if (nf > 0) { f0 = P.part_f[3 * jf]; f1 = P.part_f[3 * jf + 1]; f2 = P.part_f[3 * jf + 2]; }
+        if (nu > 0) { u0 = P.part_u[2 * ju]; u1 = P.part_u[2 * ju + 1]; }
+        if (ns > 0) { s0 = P.part_s[2 * js]; s1 = P.part_s[2 * js + 1]; }
+        if (nt > 0) {
+            t0 = P.part_t[kPartT * jt]; t1 = P.part_t[kPartT * jt + 1]; t2 = P.part_t[kPartT * jt + 2];
+            t3 = P.part_t[kPartT * jt + 3]; t4 = P.part_t[kPartT * jt + 4];
+        }
+        if (bf) { s[5] += f0; s[6] += f1; m[4] = fmax(m[4], f2); }
+        if (bu) { s[0] += u0; m[0] = fmax(m[0], u1); }
+        if (bs) { s[1] += s0; m[1] = fmax(m[1], s1); }
+        if (bt) { s[2] += t0; s[3] += t1; s[4] += t2; m[2] = fmax(m[2], t4); m[3] = fmax(m[3], t3); }
+    }
+    wave_sum(s);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) m[k] = wave_max(m[k]);
+    constexpr int kW = kFinThreads / 64;
+    __shared__ double red[kW][12];
+    __shared__ int last;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+        for (int k = 0; k < 7; ++k) red[wave][k] = s[k];
+        for (int k = 0; k < 5; ++k) red[wave][7 + k] = m[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {   // one thread per scalar, waves in order
+        const int k = threadIdx.x;
+        double t = red[0][k];
+        for (int w = 1; w < kW; ++w) t = k < 7 ? t + red[w][k] : fmax(t, red[w][k]);
+        st_wt64(P.fin_part + 12 * blockIdx.x + k, t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add((gu32_t*)P.fin_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(kFinBlocks - 1);
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x < 12) {   // the workgroups' partials in workgroup order
+        const int k = threadIdx.x;
+        double t = ld_wt64(P.fin_part + k);
+        for (int g = 1; g < kFinBlocks; ++g) {
+            const double v = ld_wt64(P.fin_part + 12 * g + k);
+            t = k < 7 ? t + v : fmax(t, v);
+        }
+        constexpr int kSlot[12] = {kScCost, kScXnorm2E, kScModelAcc, kScCandCost, kScStepnorm2E, kScXnorm2F,
+                                   kScStepnorm2F, kScBadX, kScGmaxE, kScCandBad, kScStepBad, kScGmaxF};
+        P.scal[kSlot[k]] = t;
+        if (P.scal_host) P.scal_host[kSlot[k]] = t;
+    }
+    if (threadIdx.x == 0)   // ready for the next launch (stream order)
+        __hip_atomic_store((gu32_t*)P.fin_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (P.scal_host) {
+        // publish to host-mapped memory: every scalar, a system-scope fence,
+        // then the sequence word the host polls (no blit, no stream sync)
+        if (threadIdx.x == 12) P.scal_host[kScSolveFail] = P.scal[kScSolveFail];
+        __syncthreads();   // every slot of P.scal is written
+        if (threadIdx.x == 0) {
+            const double acc = lm_spec_accept(P.scal, P) ? 1.0 : 0.0;
+            P.scal[kScAccept] = acc;
+            P.scal_host[kScAccept] = acc;
+        }
+        if (threadIdx.x < 13) __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.scal_host + kScCount), seq,
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (threadIdx.x == 0) {
+        P.scal[kScAccept] = 0.0;   // a rank's partial scalars: decided after the combine
+    }
+}
+
 // world > 1 over RCCL: the all-gathered per-rank scalars [world][kScMaxEnd]
 // combined in rank order (sums, maxima; the replicated slots are this rank's)
 // and published to host-mapped memory like finalize_kernel does at one rank,
@@ -2797,12 +2757,8 @@ void ba_cand(const DevProblem& P, const double* extr, const double* intr, double
 
 int ba_step_blocks(const DevProblem& P) { return P.n_chunk + (P.n_gpt + kGStepThreads - 1) / kGStepThreads; }
 
-bool ba_step_fuses_finalize(const DevProblem& P) { return P.n_chunk > 0 && P.n_gpt == 0; }
-
 void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const CamPre* cp_cand,
-             const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s,
-             unsigned long long seq) {
-    const int fuse = ba_step_fuses_finalize(P) ? 1 : 0;
+             const double* intr_cand, const double* X, double* X_cand, double radius, hipStream_t s) {
     if (P.n_chunk > 0) {
         const int split = P.step_split;
         const int threads = std::min(kStepThreads, (P.chunk_pts_max * split + 63) / 64 * 64);
@@ -2810,7 +2766,7 @@ void ba_step(const DevProblem& P, const CamPre* cp, const double* intr, const Ca
         auto go = [&](auto tag) {
             constexpr int SP = decltype(tag)::value;
             SFM_BY_MODEL_ALL(P, hipLaunchKernelGGL((step_kernel<CM, SP>), dim3(P.n_chunk), dim3(threads), 0, s, P,
-                                                   cp, intr, cp_cand, intr_cand, X, X_cand, radius, seq, fuse));
+                                                   cp, intr, cp_cand, intr_cand, X, X_cand, radius));
         };
         if (split == 8) go(std::integral_constant<int, 8>{});
         else if (split == 4) go(std::integral_constant<int, 4>{});

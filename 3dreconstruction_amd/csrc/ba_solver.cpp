@@ -618,9 +618,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
         else ba_solve(P, radius, s);
         if (ctx->fail_solve_wait) ba_fill(P.scal + kScSolveFail, 1, kSolveWaitTimeout, s);   // diagnostic
         if (!pl->use_bcr) ba_cand(P, S.e, S.in, S.ec, S.inc, S.cpc, s);
+        ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s);
         const unsigned long long seq = ++pl->fin_seq;
-        ba_step(P, S.cp, S.in, S.cpc, S.inc, S.X, S.Xc, radius, s, seq);
-        if (!ba_step_fuses_finalize(P)) ba_finalize(P, s, seq);
+        ba_finalize(P, s, seq);
         if (P.scal_host) {
             if (spec_gram) ba_image_gram(P, S.cpc, S.inc, S.Xc, s, P.scal + kScAccept);
             wait_scalars(pl->scal_h, seq, s);
