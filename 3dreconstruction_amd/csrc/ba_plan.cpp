@@ -467,7 +467,10 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     // (profiles/r04/o_n8knobs/pts.txt, rank 0 of a C4 shard: N = 8 2147-2180
     // LM-iters/s at 31 points (2107 chunks), 2272-2282 at 40; N = 4 1838-1870
     // at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128).
-    constexpr int64_t kTargetChunks = 1600;
+#ifndef SFM_TARGET_CHUNKS
+#define SFM_TARGET_CHUNKS 1600   // (A/B builds only)
+#endif
+    constexpr int64_t kTargetChunks = SFM_TARGET_CHUNKS;
     int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
     // Chunks of one tile group share one slot layout and one tile: the Schur
     // kernel runs a group as one workgroup, a wave per chunk, and adds the
