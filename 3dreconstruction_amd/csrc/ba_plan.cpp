@@ -463,12 +463,16 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     // points: the Schur pass takes about one chunk's latency once the chunks
     // fit in one round of the chip's 2048 wave slots (256 CUs x 2 waves per
     // SIMD x 4), and a chunk count just past a round costs a second one.  So
-    // the target is 1600 chunks, a margin for the camera-window cuts
+    // the target is 1850 chunks, a margin for the camera-window cuts
     // (profiles/r04/o_n8knobs/pts.txt, rank 0 of a C4 shard: N = 8 2147-2180
     // LM-iters/s at 31 points (2107 chunks), 2272-2282 at 40; N = 4 1838-1870
-    // at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128).
+    // at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128.
+    // Round 5, profiles/r05/w_tc*: target 1600 / 1750 / 1850 gives N = 4
+    // 2407 / 2431 / 2463 and N = 8 2958-2967 / 2920 / 2979 LM-iters/s (1619 /
+    // 1806 / 1870 chunks at N = 8, 1987 at N = 4 with 1850); fewer, longer
+    // chunks (872 / 998) leave SIMDs with one wave: N = 8 2651-2726).
 #ifndef SFM_TARGET_CHUNKS
-#define SFM_TARGET_CHUNKS 1600   // (A/B builds only)
+#define SFM_TARGET_CHUNKS 1850   // (A/B builds only)
 #endif
     constexpr int64_t kTargetChunks = SFM_TARGET_CHUNKS;
     int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
