@@ -37,6 +37,8 @@ SFM_CTX_BA_SEQ_BAND = 1 << 5
 SFM_CTX_BA_TILE80 = 1 << 6
 SFM_CTX_BA_SPLIT_REDUCE = 1 << 7
 SFM_CTX_BA_SPLIT_BCR = 1 << 8
+SFM_CTX_BA_NO_SPEC_GRAM = 1 << 10
+SFM_CTX_DIAG_SPEC_ALWAYS = 1 << 11
 SFM_CTX_BA_DENSE_CHAIN = 1 << 9
 
 

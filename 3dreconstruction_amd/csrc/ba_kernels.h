@@ -49,6 +49,7 @@ struct DevProblem {
     double huber_a, min_diag, max_diag;
     // LM options the device's accept decision needs (lm_spec_accept)
     double lm_min_rel, lm_ftol, lm_ptol;
+    int32_t spec_force;   // SFM_CTX_DIAG_SPEC_ALWAYS (tests): the device's decision forced to accept
     // shard data
     const int32_t* pt_off;
     const int32_t* obs_img;

@@ -2519,7 +2519,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_kernel(DevProblem P, int
         if (threadIdx.x == 12) P.scal_host[kScSolveFail] = P.scal[kScSolveFail];
         __syncthreads();   // every slot of P.scal is written
         if (threadIdx.x == 0) {
-            const double acc = lm_spec_accept(P.scal, P) ? 1.0 : 0.0;
+            const double acc = (P.spec_force || lm_spec_accept(P.scal, P)) ? 1.0 : 0.0;
             P.scal[kScAccept] = acc;
             P.scal_host[kScAccept] = acc;
         }
@@ -2553,7 +2553,7 @@ __global__ void publish_gathered_kernel(DevProblem P, const double* __restrict__
     }
     __syncthreads();   // the combined scalars: the accept decision (as finalize_kernel at one rank)
     if (k == 0) {
-        const double acc = lm_spec_accept(scal, P) ? 1.0 : 0.0;
+        const double acc = (P.spec_force || lm_spec_accept(scal, P)) ? 1.0 : 0.0;
         scal[kScAccept] = acc;
         host[kScAccept] = acc;
     }

@@ -565,11 +565,9 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
     // The host compares the flag with its own decision: it runs the pass if
     // the device skipped it, and redoes it at the current point if the device
     // ran it for a step the host rejects, so no result depends on the flag.
-#ifndef SFM_NO_SPEC_GRAM
-    const bool spec_gram = P.scal_host != nullptr || (ctx->comm && !ctx->host_allreduce);
-#else
-    const bool spec_gram = false;   // (A/B builds)
-#endif
+    const bool spec_gram = !(ctx->flags & SFM_CTX_BA_NO_SPEC_GRAM) &&
+                           (P.scal_host != nullptr || (ctx->comm && !ctx->host_allreduce));
+    P.spec_force = (ctx->flags & SFM_CTX_DIAG_SPEC_ALWAYS) ? 1 : 0;
     double radius = O.initial_trust_region_radius, decrease_factor = 2.0;
     int consecutive_invalid = 0;
     double x_cost = 0.0, x_norm = 0.0;

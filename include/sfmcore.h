@@ -100,6 +100,11 @@ typedef struct sfm_ctx_opts {
  * alone.  Off by default: the extra stream synchronisation and event pair are
  * not part of the filter's production path. */
 #define SFM_CTX_TIME_KERNELS 8
+/* Diagnostic only (tests): the device's copy of the LM accept decision is
+ * forced to "accept", so the speculative Gram pass at the candidate runs after
+ * every step and the host has to redo it at the current point for each step
+ * it rejects (the path a device / host disagreement would take). */
+#define SFM_CTX_DIAG_SPEC_ALWAYS (1 << 11)
 /* BA engine shape (A/B measurement and tests; 0 = the measured defaults).
  * Every alternative is exact: the launch-shape bits and the per-point /
  * per-target lane counts change only how the same sums are launched
@@ -117,6 +122,8 @@ typedef struct sfm_ctx_opts {
  *                            back-substitution level as separate launches
  *   SFM_CTX_BA_DENSE_CHAIN   the dense factorisation and back substitution
  *                            as launch chains instead of dataflow kernels
+ *   SFM_CTX_BA_NO_SPEC_GRAM  the Gram pass after an accepted step launched by
+ *                            the host after its decision, not speculatively
  *   SFM_CTX_BA_STEP_LANES(n) n = 1, 2, 4, 8 lanes per point in the step pass
  *   SFM_CTX_BA_REDUCE_WAVES(n) n = 1, 2, 4 waves per reduce target */
 #define SFM_CTX_BA_DENSE_RCS      (1 << 4)
@@ -125,6 +132,7 @@ typedef struct sfm_ctx_opts {
 #define SFM_CTX_BA_SPLIT_REDUCE   (1 << 7)
 #define SFM_CTX_BA_SPLIT_BCR      (1 << 8)
 #define SFM_CTX_BA_DENSE_CHAIN    (1 << 9)
+#define SFM_CTX_BA_NO_SPEC_GRAM   (1 << 10)
 #define SFM_CTX_BA_STEP_LANES(n)  (((n) == 8 ? 4 : (n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 0) << 12)
 #define SFM_CTX_BA_REDUCE_WAVES(n) (((n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 0) << 15)
 

@@ -638,6 +638,35 @@ def test_step_split_and_reduce_waves_agree(vis_mode):
             assert abs(gs.final_cost / base.final_cost - 1) < 1e-10, (split, waves)
 
 
+def test_speculative_gram_bit_identical():
+    # After each step the Gram pass at the candidate is launched behind the
+    # finalize, gated by the device's copy of the host's accept decision
+    # (ba_solver.cpp run_plan).  A scene whose LM run rejects steps (large
+    # perturbations, 10 % outliers, a wide first trust region: 36 accepted /
+    # 15 rejected steps in the oracle) solves bit for bit alike (1) with the
+    # speculation, (2) without it (SFM_CTX_BA_NO_SPEC_GRAM), and (3) with the
+    # device's decision forced to accept (SFM_CTX_DIAG_SPEC_ALWAYS), so the host
+    # redoes the pass at the current point after every rejected step.
+    sc = H.Scene(40, 4000, 6, seed=4243, perturb=(0.5, 2.0, 2.0, 200.0), outliers=0.1)
+    lib = api.abi.load()
+    opts = abi.default_options()
+    opts.initial_trust_region_radius = 1e8
+    out = []
+    for flags in (0, abi.SFM_CTX_BA_NO_SPEC_GRAM, abi.SFM_CTX_DIAG_SPEC_ALWAYS):
+        e, i, x = sc.params()
+        with H.engine_ctx(flags) as c:
+            rc, gs = api.ba_solve(c, sc.problem(), e, i, x, opts)
+        assert rc == 0, lib.sfm_last_error()
+        out.append((gs.iterations, gs.successful_steps, gs.unsuccessful_steps, gs.initial_cost, gs.final_cost,
+                    e, i, x))
+    assert out[0][2] > 0, "the scene must reject steps"
+    a = out[0]
+    for b in out[1:]:
+        assert a[:5] == b[:5]
+        for u, v in zip(a[5:], b[5:]):
+            np.testing.assert_array_equal(u, v)
+
+
 def test_fused_launches_bit_identical():
     # Launch fusions with unchanged arithmetic: (1) the long reduce targets
     # (the intrinsics corner and arrow collect one tile term per chunk) are
