@@ -1224,19 +1224,7 @@ __global__ __launch_bounds__(256) void reduce_kernel(DevProblem P, int vectors_o
         return;
     }
     const int W = P.red_waves, wave = threadIdx.x >> 6, e = threadIdx.x & 63;
-#ifndef SFM_REDUCE_FLAT
-    // XCD-aware (round 5): workgroup b runs on XCD b % 8; give each XCD a
-    // contiguous run of the targets (neighbouring camera blocks, which read the
-    // same chunk tiles) so those tiles' lines are fetched into one L2, not eight
-    const int bx = [&] {
-        const int n = n_short_blocks, x = (int)blockIdx.x & 7, k = (int)blockIdx.x >> 3;
-        const int per = n >> 3, rem = n & 7;
-        return x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
-    }();
-#else
-    const int bx = blockIdx.x;   // (A/B builds)
-#endif
-    const int t = bx * (4 / W) + wave / W, ws = wave - (wave / W) * W;
+    const int t = blockIdx.x * (4 / W) + wave / W, ws = wave - (wave / W) * W;
     __shared__ double part[4][64];
     bool live = t < P.n_targets;
     ReduceTarget T{};
