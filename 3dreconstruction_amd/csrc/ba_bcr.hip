@@ -304,53 +304,6 @@ struct TileFetch {
             }
         }
     }
-    // (round 5) the lower 16x16 block tiles only, (r, c) with c <= r: the
-    // level kernel's A, whose upper tiles are scratch (their loads were 3/8 of A's)
-    __device__ __forceinline__ static bool lower(int e) {
-        const int r = e / (NC / 2), c = 2 * (e % (NC / 2));
-        return c < 16 * (r / 16 + 1);
-    }
-    __device__ __forceinline__ void fetch_lower(const double* __restrict__ src, int ld_src) {
-#pragma unroll
-        for (int q = 0; q < per; ++q) {
-            const int e = threadIdx.x + q * TH;
-            if (e < n2 && lower(e))
-                v[q] = *reinterpret_cast<const double2*>(src + (e / (NC / 2)) * ld_src + 2 * (e % (NC / 2)));
-        }
-    }
-    __device__ __forceinline__ void put_lower(double* dst, int ld_dst) const {
-#pragma unroll
-        for (int q = 0; q < per; ++q) {
-            const int e = threadIdx.x + q * TH;
-            if (e < n2 && lower(e)) {
-                double* d = dst + (e / (NC / 2)) * ld_dst + 2 * (e % (NC / 2));
-                d[0] = v[q].x;
-                d[1] = v[q].y;
-            }
-        }
-    }
-    // rows [0, nr) loaded, rows past them zero in LDS: a neighbour's W, whose
-    // rows past the 6K real ones are zero (and every product but S0's stops at kM)
-    __device__ __forceinline__ void fetch_rows(const double* __restrict__ src, int ld_src, int nr) {
-#pragma unroll
-        for (int q = 0; q < per; ++q) {
-            const int e = threadIdx.x + q * TH;
-            if (e < n2 && e / (NC / 2) < nr)
-                v[q] = *reinterpret_cast<const double2*>(src + (e / (NC / 2)) * ld_src + 2 * (e % (NC / 2)));
-        }
-    }
-    __device__ __forceinline__ void put_rows(double* dst, int ld_dst, int nr) const {
-#pragma unroll
-        for (int q = 0; q < per; ++q) {
-            const int e = threadIdx.x + q * TH;
-            if (e < n2) {
-                const bool in = e / (NC / 2) < nr;
-                double* d = dst + (e / (NC / 2)) * ld_dst + 2 * (e % (NC / 2));
-                d[0] = in ? v[q].x : 0.0;
-                d[1] = in ? v[q].y : 0.0;
-            }
-        }
-    }
 };
 // two 64x64 global tiles -> LDS [64][LD], every load of both in flight before
 // the first LDS store (one memory latency instead of two)
@@ -957,15 +910,6 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         // the first: bgC / bgCr overwrite all of Cc and Cr, so they are not loaded)
         TileFetch<64, M, NTL> fwa, fwb;
         const bool hwb = i + sp < b.N;   // the neighbours' W blocks (the A update's operands)
-#ifndef SFM_BCR_FULL_LOADS
-        if (!TOP) fwa.fetch_rows(b.Wr + (size_t)(i - sp) * M * M, M, kM);
-        if (hwb) fwb.fetch_rows(b.Wl + (size_t)(i + sp) * M * M, M, kM);
-        fa.fetch_lower(b.A + (size_t)i * M * M, M);
-        if (hz) frc.fetch(b.R + (size_t)i * M * b.nrhs + 16 * w, b.nrhs);
-        if (!TOP) fwa.put_rows(Wa_l, M, kM);
-        if (hwb) fwb.put_rows(Wb_l, M, kM);
-        fa.put_lower(A, LD);
-#else   // (A/B builds)
         if (!TOP) fwa.fetch(b.Wr + (size_t)(i - sp) * M * M, M);
         if (hwb) fwb.fetch(b.Wl + (size_t)(i + sp) * M * M, M);
         fa.fetch(b.A + (size_t)i * M * M, M);
@@ -973,7 +917,6 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
         if (!TOP) fwa.put(Wa_l, M);
         if (hwb) fwb.put(Wb_l, M);
         fa.put(A, LD);
-#endif
         if (hz) frc.put(Rc, L16);
     }
     __syncthreads();
