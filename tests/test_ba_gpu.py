@@ -406,6 +406,18 @@ def test_single_observation_tracks_and_unobserved_blocks(ctx):
     _compare(ctx, _subset(sc, keep), check_trace=False)
 
 
+def test_bcr_single_super_block_vs_oracle(ctx):
+    """Eight cameras (seven with pose blocks): one BCR super-block, so no
+    level runs -- the one-workgroup top (bcr_top_body) and the back
+    substitution's root alone, which also forms every LM candidate (the
+    cameras of block 0, the gauge image's copy, the intrinsics)."""
+    sc = H.Scene(8, 800, 4, seed=77)
+    plan = api.BAPlan(ctx, sc.problem(), *sc.params())
+    assert plan.info().rcs_solver == abi.SFM_RCS_BCR
+    plan.close()
+    _compare(ctx, sc)
+
+
 def test_no_observations(ctx):
     sc = _subset(H.Scene(6, 50, 3, seed=5), lambda p, ids: [])
     orc_rc, os_, _, _ = H.oracle_solve(sc)
