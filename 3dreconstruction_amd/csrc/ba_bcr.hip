@@ -791,7 +791,20 @@ __device__ void update_tile_rows(const BcrArgs& b, int s, int j, int w, double* 
 constexpr int NTL = 512, NWL = NTL / 64;   // level kernel: 8 waves
 
 __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProblem& P, double radius, int I,
-                                                bool z_fresh, bool part_done = false);
+                                                bool z_fresh, bool part_done = false, unsigned tag = 0,
+                                                const double* own = nullptr);
+__device__ __forceinline__ void put_y(unsigned long long* g, int row, double v, unsigned epoch);
+// block 0's corner partial (nrhs = 16: q00 only) into LDS, the part layout
+// (the fused top: workgroup 0 keeps it and solves the corner itself)
+__device__ __forceinline__ void corner_put_lds(const DevProblem& P, const v4d& q00, double* dst) {
+    constexpr int kQ = 17;
+    const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4, na = P.iw * P.nintr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int ga = kk + 4 * r, gc = i;
+        if (ga >= 1 && ga <= na && gc <= na) dst[(ga - 1) * kQ + gc] = q00[r];
+    }
+}
 // block I's corner partial (rows 1..na, columns 0..na of z_I' z_I) from this
 // wave's MFMA results q00 (and, nrhs = 32, q10 / q11), stored write-through
 __device__ __forceinline__ void corner_put(const BcrArgs& b, const DevProblem& P, int I, const v4d& q00,
@@ -822,12 +835,13 @@ __device__ __forceinline__ void corner_put(const BcrArgs& b, const DevProblem& P
 // (bcr_corner_body; nrhs = 16 only, so that z_0 is one workgroup's).  The
 // top used to be one workgroup with the barrier-phased chol_inv64.
 template <bool TOP>
-__global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P, double radius, int s, int n_odd) {
+__global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P, double radius, int s, int n_odd,
+                                                        unsigned epoch) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     int item, w;
     if constexpr (TOP) {
         if ((int)blockIdx.x >= 4) {
-            bcr_corner_body(b, P, radius, (int)blockIdx.x - 3, false);
+            bcr_corner_body(b, P, radius, (int)blockIdx.x - 3, false, false, epoch);
             return;
         }
         item = 0;
@@ -1285,10 +1299,7 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     // ---- P3: X's last row tile; the last row tile of every output -----------
     pphase(3);
     gs_k(3);
-    if (q_here && wave == 7) {   // block 0's corner partial, stored and drained
-        corner_put(b, P, 0, qz, zero4(), zero4(), 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (q_here && wave == 7) corner_put_lds(P, qz, Cc);   // block 0's corner partial (Cc: unused by the top)
     if (st && threadIdx.x == 0) {
         atomicAdd(st + 0, td);
         atomicAdd(st + 1, stamp() - tf0);
@@ -1302,11 +1313,11 @@ __global__ __launch_bounds__(NTL) void bcr_level_kernel(BcrArgs b, DevProblem P,
     }
     if (threadIdx.x == 0 && bad[0] != 0.0) b.fail[0] = 1.0;
     if constexpr (TOP) {
-        // fused launch: block 0's corner partial is stored (wave 7, above);
-        // its ticket, and the corner solve if this is the last arrival
+        // fused launch: block 0's corner partial is in LDS (wave 7, above);
+        // the rest's tagged sum, then the corner solve (bcr_corner_body)
         if (w == 0 && gridDim.x > 4) {
             __syncthreads();
-            bcr_corner_body(b, P, radius, 0, true, true);
+            bcr_corner_body(b, P, radius, 0, true, true, epoch, Cc);
         }
         return;
     }
@@ -1436,7 +1447,7 @@ __global__ __launch_bounds__(NTL) void bcr_top_kernel(BcrArgs b, int sp) {
 // (z_fresh: this workgroup wrote z_I itself just before -- the top, in the
 // fused launch -- so wave 0 reads it write-through, past this CU's L1)
 __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProblem& P, double radius, int I,
-                                                bool z_fresh, bool part_done) {
+                                                bool z_fresh, bool part_done, unsigned tag, const double* own) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int na = P.iw * P.nintr, iw = P.iw;   // bordered columns (<= 16)
     constexpr int kQ = 17;                      // part row stride: columns 0..16
@@ -1512,18 +1523,48 @@ __device__ __forceinline__ void bcr_corner_body(const BcrArgs& b, const DevProbl
             }
 #pragma unroll
             for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o);
-            if (g == 0 && k < nel) st_sc1(b.part + (size_t)b.N * 512 + k, t);
+            if (g == 0 && k < nel) {
+                if (tag) put_y(reinterpret_cast<unsigned long long*>(b.part + (size_t)b.N * 512), k, t, tag);
+                else st_sc1(b.part + (size_t)b.N * 512 + k, t);
+            }
         }
+        if (tag) return;   // (the fused top's workgroup 0 polls the tagged sums and solves)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add((gu32*)counter2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-               (b.N > 1 ? 1u : 0u);
-    __syncthreads();
-    if (!last) return;
-    if (threadIdx.x == 0) __hip_atomic_store((gu32*)counter2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!tag) {
+        if (threadIdx.x == 0)
+            last = __hip_atomic_fetch_add((gu32*)counter2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (b.N > 1 ? 1u : 0u);
+        __syncthreads();
+        if (!last) return;
+        if (threadIdx.x == 0) __hip_atomic_store((gu32*)counter2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // Tagged (the fused top, round 5): workgroup 0 always solves.  Its own
+    // partial never left the workgroup (own: LDS, as wave 7 formed it), and the
+    // rest's sum arrives as {tag, 32 bits} granules (the data is the flag, as
+    // the back substitution's y) -- no drain, no ticket, one poll.
+    const unsigned long long* rest_g = reinterpret_cast<const unsigned long long*>(b.part + (size_t)b.N * 512);
+    auto rest_tagged = [&](int off) {
+        unsigned lo = 0, hi = 0;
+        for (unsigned spins = 0;; ++spins) {
+            const unsigned long long x0 = __hip_atomic_load((gu64*)(rest_g + 2 * off), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long x1 = __hip_atomic_load((gu64*)(rest_g + 2 * off + 1), __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+            lo = (unsigned)x0;
+            hi = (unsigned)x1;
+            if ((unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (spins > (1u << 22)) {   // ~ seconds: a lost producer, never a normal wait
+                st_sc1(b.fail + 1, 1.0);
+                break;
+            }
+        }
+        return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    };
     auto sum_parts = [&](int off) {   // block 0's partial + the rest's sum (slot N)
+        if (tag) return own[off] + rest_tagged(off);
         const double t0 = ld_sc1(b.part + off);
         return b.N > 1 ? t0 + ld_sc1(b.part + (size_t)b.N * 512 + off) : t0;
     };
@@ -1899,7 +1940,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
         const int n_odd = (b.N - stride + 2 * stride - 1) / (2 * stride);
         const int n_even = stride > 1 ? (b.N + 2 * stride - 1) / (2 * stride) : 0;
         hipLaunchKernelGGL(bcr_level_kernel<false>, dim3(32 * ((n_odd + n_even + 7) / 8)), dim3(NTL), lds_l, s, b, P,
-                           radius, stride, n_odd);
+                           radius, stride, n_odd, 0u);
         SFM_HIP(hipGetLastError());
         s_top = stride * 2;
     }
@@ -1911,7 +1952,7 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
     const bool top_level = b.N >= 2 && b.nrhs == 16;
     if (top_level) {
         hipLaunchKernelGGL(bcr_level_kernel<true>, dim3(b.split ? 4 : 3 + b.N), dim3(NTL), lds_l, s, b, P, radius,
-                           s_top, 1);
+                           s_top, 1, epoch);
         SFM_HIP(hipGetLastError());
         if (b.split) {
             hipLaunchKernelGGL(bcr_corner_kernel, dim3(b.N), dim3(NT), 0, s, b, P, radius);

@@ -412,6 +412,8 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         SFM_HIP(hipMemsetAsync(pl->bcr.fail, 0, 8 * sizeof(double) + sizeof(unsigned) * (size_t)pl->bcr.N, s));
         // the back substitution's tagged y granules (tags = solve epochs from 1)
         SFM_HIP(hipMemsetAsync(pl->bcr.Y, 0, sizeof(double) * bcr_y_granules(pl->bcr), s));
+        // the fused top's tagged corner sums (slot N of the partials; tags = solve epochs from 1)
+        SFM_HIP(hipMemsetAsync(pl->bcr.part + (size_t)pl->bcr.N * 512, 0, 512 * sizeof(double), s));
         if (std::getenv("SFM_BCR_STAMPS")) {
             pl->bcr_stamps.alloc(16);
             pl->bcr_stamps.zero(s);
