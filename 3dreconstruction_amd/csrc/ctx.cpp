@@ -10,10 +10,10 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <vector>
 #include <tuple>
 #include <unordered_map>
 #include <unordered_set>
-#include <vector>
 
 #include "common.h"
 
@@ -95,13 +95,31 @@ int rccl_allgather_f64(void* comm, const double* in, double* out, size_t n, hipS
 void set_dyn_lds(const void* kernel, size_t bytes) {
     int dev = 0;
     SFM_HIP(hipGetDevice(&dev));
+    // hot path: a thread that has already seen the attribute raised
+    // far enough for this (device, kernel) returns without the process-wide
+    // lock -- the BCR / dense solves call this several times per LM iteration
+    struct Seen {
+        int dev;
+        const void* kernel;
+        size_t bytes;
+    };
+    thread_local std::vector<Seen> seen;
+    for (const Seen& x : seen)
+        if (x.dev == dev && x.kernel == kernel && x.bytes >= bytes) return;
     static std::mutex mu;
     static auto* done = new std::map<std::pair<int, const void*>, size_t>;   // never destroyed
     std::lock_guard<std::mutex> lk(mu);
     size_t& have = (*done)[{dev, kernel}];
-    if (have >= bytes) return;
-    SFM_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-    have = bytes;
+    if (have < bytes) {
+        SFM_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        have = bytes;
+    }
+    for (Seen& x : seen)
+        if (x.dev == dev && x.kernel == kernel) {
+            x.bytes = have;
+            return;
+        }
+    seen.push_back({dev, kernel, have});
 }
 
 int device_cu_count() {

@@ -125,7 +125,9 @@ typedef struct sfm_ctx_opts {
  *   SFM_CTX_BA_NO_SPEC_GRAM  the Gram pass after an accepted step launched by
  *                            the host after its decision, not speculatively
  *   SFM_CTX_BA_STEP_LANES(n) n = 1, 2, 4, 8 lanes per point in the step pass
- *   SFM_CTX_BA_REDUCE_WAVES(n) n = 1, 2, 4 waves per reduce target */
+ *   SFM_CTX_BA_REDUCE_WAVES(n) n = 1, 2, 4 waves per reduce target
+ * (a field of 0 means the planner's default; any other n gives the field
+ * value 7, which sfm_ctx_create rejects with SFM_ERR_INVALID_ARG) */
 #define SFM_CTX_BA_DENSE_RCS      (1 << 4)
 #define SFM_CTX_BA_SEQ_BAND       (1 << 5)
 #define SFM_CTX_BA_TILE80         (1 << 6)
@@ -133,8 +135,8 @@ typedef struct sfm_ctx_opts {
 #define SFM_CTX_BA_SPLIT_BCR      (1 << 8)
 #define SFM_CTX_BA_DENSE_CHAIN    (1 << 9)
 #define SFM_CTX_BA_NO_SPEC_GRAM   (1 << 10)
-#define SFM_CTX_BA_STEP_LANES(n)  (((n) == 8 ? 4 : (n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 0) << 12)
-#define SFM_CTX_BA_REDUCE_WAVES(n) (((n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 0) << 15)
+#define SFM_CTX_BA_STEP_LANES(n)  (((n) == 8 ? 4 : (n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 7) << 12)
+#define SFM_CTX_BA_REDUCE_WAVES(n) (((n) == 4 ? 3 : (n) == 2 ? 2 : (n) == 1 ? 1 : 7) << 15)
 
 /* [cpu] fill out[128] with a fresh RCCL unique id (rank 0 only). */
 int sfm_comm_unique_id(uint8_t* out128);

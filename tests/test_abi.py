@@ -86,3 +86,24 @@ def test_partition_balances_observations(world):
 def test_cpp_facade_builds():
     exe = os.path.join(ROOT, "tests", "cpp", "facade_test")
     assert os.path.exists(exe), "run make (builds the C++ façade test)"
+
+
+def test_engine_shape_macros_reject_unsupported_counts(tmp_path):
+    """SFM_CTX_BA_STEP_LANES(n) / SFM_CTX_BA_REDUCE_WAVES(n) of an
+    unsupported n give the field value 7, which sfm_ctx_create rejects (its
+    argument checks run before any device call, so this holds on the CPU)."""
+    import subprocess
+    src = tmp_path / "m.c"
+    src.write_text('#include <stdio.h>\n#include "sfmcore.h"\nint main(void) {\n'
+                   '  printf("%d %d %d %d %d %d\\n", SFM_CTX_BA_STEP_LANES(8) >> 12, SFM_CTX_BA_STEP_LANES(3) >> 12,\n'
+                   '         SFM_CTX_BA_STEP_LANES(16) >> 12, SFM_CTX_BA_REDUCE_WAVES(4) >> 15,\n'
+                   '         SFM_CTX_BA_REDUCE_WAVES(3) >> 15, SFM_CTX_BA_STEP_LANES(0) >> 12);\n  return 0;\n}\n')
+    exe = tmp_path / "m"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), "-I/opt/rocm/include", str(src),
+                    "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert vals == [4, 7, 7, 3, 7, 7]
+    for flags in (7 << 12, 7 << 15):
+        with pytest.raises(api.SfmError) as ei:
+            api.Context(0, flags=flags)
+        assert ei.value.code == abi.SFM_ERR_INVALID_ARG

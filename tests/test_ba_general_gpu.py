@@ -170,67 +170,103 @@ def test_very_long_track(ctx):
     _compare(ctx, sc)
 
 
-@pytest.mark.parametrize("chain", [True, False])
-def test_dense_solve_under_contention(chain):
-    """VERDICT r4 item 2: the dense RCS solved while another context keeps the
-    CUs busy.  A second context on its own stream runs back-to-back matcher
-    launches (~14k workgroups of 256 threads each), so the solve's kernels are
-    dispatched into a chip that is already full and their workgroups start
-    late and out of step -- the condition under which dense_panel_kernel's
-    former store of L_kk over A_kk (round 4) corrupted the
-    panels of late workgroups, and under which the dataflow kernels
-    (dense_flow_kernel, dense_back_all_kernel) wait for workgroups that are
-    not resident yet.  chain: the launch chain (panel + trailing-update
-    launches); else the dataflow kernels.  Both must take the oracle's
-    decisions, with the matcher provably running during the solves."""
-    import threading
-    sc = H.Scene(100, 12000, 8, vis_mode=1, seed=2718)   # random visibility: dense RCS, 10 block columns
-    _, os_, otr, _ = H.oracle_solve(sc, threads=8)
-    desc = api.synth_descriptors(60, 4096)
-    off = np.arange(61, dtype=np.int64) * 4096
-    pairs = api.exhaustive_pairs(60)
-    stop, started = threading.Event(), threading.Event()
-    runs = {"n": 0, "during": 0, "err": None}
-    solving = threading.Event()
+class _MatcherLoad:
+    """Another context keeping the CUs busy: back-to-back matcher launches
+    (~14k workgroups of 256 threads each) on its own stream, so a solve's
+    kernels are dispatched into a chip that is already full and their
+    workgroups start late and out of step.  `solving` marks the window in
+    which the matcher's launches are counted (`during`)."""
 
-    def matcher():
+    def __init__(self):
+        import threading
+        self.stop, self.started, self.solving = threading.Event(), threading.Event(), threading.Event()
+        self.runs = {"n": 0, "during": 0, "err": None}
+        self.th = threading.Thread(target=self._run)
+
+    def _run(self):
         try:
+            desc = api.synth_descriptors(60, 4096)
+            off = np.arange(61, dtype=np.int64) * 4096
+            pairs = api.exhaustive_pairs(60)
             c2 = api.Context(0)
             mp = api.MatchPlan(c2, desc, off)
-            while not stop.is_set():
+            while not self.stop.is_set():
                 mp.run(pairs, count=True)   # returns after the launch completes
-                runs["n"] += 1
-                if solving.is_set():
-                    runs["during"] += 1
-                started.set()
+                self.runs["n"] += 1
+                if self.solving.is_set():
+                    self.runs["during"] += 1
+                self.started.set()
             mp.close()
             c2.close()
         except Exception as ex:  # reported by the main thread
-            runs["err"] = ex
-            started.set()
+            self.runs["err"] = ex
+            self.started.set()
 
-    th = threading.Thread(target=matcher)
-    th.start()
-    try:
-        assert started.wait(120) and runs["err"] is None, runs["err"]
-        flags = abi.SFM_CTX_BA_DENSE_RCS | (abi.SFM_CTX_BA_DENSE_CHAIN if chain else 0)
-        with H.engine_ctx(flags) as c:
-            for rep in range(3):
-                plan = api.BAPlan(c, sc.problem(), *sc.params())
-                assert plan.info().rcs_solver == abi.SFM_RCS_DENSE
-                solving.set()
-                rc, gs = plan.run()
-                solving.clear()
-                tr = plan.trace()
-                plan.close()
-                assert rc == 0, abi.load().sfm_last_error()
-                assert (gs.iterations, gs.successful_steps) == (os_.iterations, os_.successful_steps), rep
-                assert [t.step_is_successful for t in tr] == [t.step_is_successful for t in otr]
-                for g, o in zip(tr, otr):
-                    assert abs(g.cost / o.cost - 1) < 1e-9
-                assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
-    finally:
-        stop.set()
-        th.join(300)
-    assert runs["err"] is None, runs["err"]
-    assert runs["during"] >= 1, runs   # the matcher ran while the solves did
+    def __enter__(self):
+        self.th.start()
+        assert self.started.wait(120) and self.runs["err"] is None, self.runs["err"]
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join(300)
+        if exc[0] is None:
+            assert self.runs["err"] is None, self.runs["err"]
+            assert self.runs["during"] >= 1, self.runs   # the matcher ran while the solves did
+        return False
+
+
+def _solves_under_load(load, sc, flags, solver, reps=3):
+    """reps plan + run cycles of sc on a context with `flags` while `load`
+    runs; each takes the oracle's decisions (no SFM_ERR_DEVICE from a false
+    dataflow wait-timeout, no wrong panel from a late workgroup)."""
+    _, os_, otr, _ = H.oracle_solve(sc, threads=8)
+    with H.engine_ctx(flags) as c:
+        for rep in range(reps):
+            plan = api.BAPlan(c, sc.problem(), *sc.params())
+            assert plan.info().rcs_solver == solver
+            load.solving.set()
+            rc, gs = plan.run()
+            load.solving.clear()
+            tr = plan.trace()
+            plan.close()
+            assert rc == 0, abi.load().sfm_last_error()
+            assert (gs.iterations, gs.successful_steps) == (os_.iterations, os_.successful_steps), rep
+            assert [t.step_is_successful for t in tr] == [t.step_is_successful for t in otr]
+            for g, o in zip(tr, otr):
+                assert abs(g.cost / o.cost - 1) < 1e-9
+            assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
+
+
+@pytest.mark.parametrize("chain", [True, False])
+def test_dense_solve_under_contention(chain):
+    """VERDICT r4 item 2: the dense RCS solved while another context keeps the
+    CUs busy -- the condition under which dense_panel_kernel's former store of
+    L_kk over A_kk (round 4) corrupted the panels of late
+    workgroups, and under which the dataflow kernels (dense_flow_kernel,
+    dense_back_all_kernel) wait for workgroups that are not resident yet.
+    chain: the launch chain (panel + trailing-update launches); else the
+    dataflow kernels.  Both must take the oracle's decisions, with the matcher
+    provably running during the solves."""
+    sc = H.Scene(100, 12000, 8, vis_mode=1, seed=2718)   # random visibility: dense RCS, 10 block columns
+    flags = abi.SFM_CTX_BA_DENSE_RCS | (abi.SFM_CTX_BA_DENSE_CHAIN if chain else 0)
+    with _MatcherLoad() as load:
+        _solves_under_load(load, sc, flags, abi.SFM_RCS_DENSE)
+
+
+# VERDICT r5 item 2 / ADVICE r5: the default band path's inter-workgroup
+# hand-offs under the same load (DESIGN.md §5, "Residency of the BCR
+# hand-offs"): the fused top + corner (workgroup 0 polls the tagged corner sum
+# the last of blocks 1..N-1 publishes), the back substitution's tagged y
+# granules (a block waits for its two neighbours, in-order dispatch), and the
+# forward levels.  Shapes: a C4-shaped band (K = 9, one intrinsics block:
+# the top as a level item, nrhs 16) over several levels, the same with the
+# launches split (SFM_CTX_BA_SPLIT_BCR), and four intrinsics blocks (nrhs 32:
+# the top + corner as one bcr_top_corner_kernel launch).
+@pytest.mark.parametrize("shape", ["c4", "c4_split", "arrow4"])
+def test_band_solve_under_contention(shape):
+    n_intr = 4 if shape == "arrow4" else 1
+    sc = H.Scene(240, 24000, 10, n_intr=n_intr, seed=3141)   # banded orbit: K = 9, 27 super-blocks, 5 levels
+    flags = abi.SFM_CTX_BA_SPLIT_BCR if shape == "c4_split" else 0
+    with _MatcherLoad() as load:
+        _solves_under_load(load, sc, flags, abi.SFM_RCS_BCR)
