@@ -234,6 +234,7 @@ SIGNATURES = [
     ("sfm_ba_solve", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,
                                C.POINTER(BAOptions), C.POINTER(BASummary)]),
     ("sfm_ba_cache_clear", C.c_int, [C.c_void_p]),
+    ("sfm_ba_cache_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     ("sfm_ba_plan_create", C.c_int, [C.c_void_p, C.POINTER(BAProblem), f64p, f64p, f64p,
                                      C.POINTER(C.c_void_p)]),
     ("sfm_ba_plan_run", C.c_int, [C.c_void_p, C.POINTER(BAOptions), C.POINTER(BASummary)]),
@@ -244,6 +245,8 @@ SIGNATURES = [
     ("sfm_ba_intr_width", C.c_int, [C.c_int32]),
     ("sfm_ba_partition", C.c_int, [C.POINTER(BAProblem), C.c_int32, i64p, i64p]),
     ("sfm_ba_describe", C.c_int, [C.POINTER(BAProblem), C.c_int32, C.c_int32, C.POINTER(BAPlanShape)]),
+    ("sfm_ba_grown_digest", C.c_int, [C.POINTER(BAProblem), C.POINTER(BAProblem), C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]),
     ("sfm_synth_ba", C.c_int, [C.POINTER(SynthBAConfig), i64p, i32p, f64p, i32p, f64p,
                                f64p, f64p, f64p, f64p, f64p, i64p]),
     ("sfm_match_dense", C.c_int, [C.c_void_p, u8p, C.c_int32, u8p, C.c_int32,

@@ -247,6 +247,16 @@ def ba_describe(problem, rank=0, world=1):
     return out
 
 
+def ba_grown_digest(prev, problem):
+    """[cpu] (fresh digest, grown digest, reused sorted points) of `problem`
+    planned from scratch and grown from `prev`'s plan (sfm_ba_grown_digest)."""
+    lib = abi.load()
+    df, dg, r = C.c_uint64(), C.c_uint64(), C.c_int64()
+    _check(lib.sfm_ba_grown_digest(C.byref(prev), C.byref(problem), C.byref(df), C.byref(dg), C.byref(r)),
+           "sfm_ba_grown_digest")
+    return df.value, dg.value, r.value
+
+
 class BAPlan:
     """Resident BA problem (sfm_ba_plan): upload once, run many times."""
 
@@ -307,6 +317,17 @@ def ba_solve(ctx, problem, extr, intr, X, opts=None):
                               abi.ptr(intr, abi.f64p), abi.ptr(X, abi.f64p), C.byref(o),
                               C.byref(s))
     return rc, s
+
+
+def ba_cache_stats(ctx):
+    """(reused, grown, fresh) plan counts of sfm_ba_solve on this context."""
+    r, g, f = C.c_int64(), C.c_int64(), C.c_int64()
+    _check(ctx.lib.sfm_ba_cache_stats(ctx.h, C.byref(r), C.byref(g), C.byref(f)), "sfm_ba_cache_stats")
+    return r.value, g.value, f.value
+
+
+def ba_cache_clear(ctx):
+    _check(ctx.lib.sfm_ba_cache_clear(ctx.h), "sfm_ba_cache_clear")
 
 
 def ba_partition(problem, world_size):

@@ -16,6 +16,7 @@
 #include <exception>
 #include <mutex>
 #include <cstdlib>
+#include <cstring>
 #include <numeric>
 #include <thread>
 
@@ -186,8 +187,9 @@ std::vector<int32_t> rcm_order(const sfm_ba_problem& P, const std::vector<int32_
 }  // namespace
 
 std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, int32_t* D_out, PointSpans* spans,
-                                   std::vector<char>* used_out) {
+                                   std::vector<char>* used_out, int32_t* lb_out, bool* rcm_out) {
     PhaseTimer tm("camera_blocks");
+    if (rcm_out) *rcm_out = false;
     std::vector<int32_t> cam_blk(P.n_img, -1);
     std::vector<char> used;
     mark_used(P.obs_img, P.n_obs, P.n_img, used);
@@ -214,9 +216,11 @@ std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, i
             cam_blk.swap(alt);
             D = D2;
             if (spans) *spans = std::move(alt_spans);
+            if (rcm_out) *rcm_out = true;
         }
         tm.mark("bandwidth2");
     }
+    if (lb_out) *lb_out = lb;
     if (ncam_out) *ncam_out = ncam;
     if (D_out) *D_out = D;
     if (used_out) used_out->swap(used);
@@ -225,13 +229,15 @@ std::vector<int32_t> camera_blocks(const sfm_ba_problem& P, int32_t* ncam_out, i
 
 namespace {
 
-void active_sets(const sfm_ba_problem& P, BAHostPlan& pl, PointSpans* spans) {
-    std::vector<char> im;   // observed images
-    pl.cam_blk = camera_blocks(P, &pl.ncam, &pl.D, spans, &im);
+// Everything of the active parameter blocks that follows from cam_blk (ncam,
+// D set) and the observed-image flags
+void active_from_blocks(const sfm_ba_problem& P, BAHostPlan& pl, const std::vector<char>& im) {
     pl.blk_img.assign(pl.ncam, -1);
     for (int i = 0; i < P.n_img; ++i)
         if (pl.cam_blk[i] >= 0) pl.blk_img[pl.cam_blk[i]] = i;
     pl.intr_blk.assign(P.n_intr, -1);
+    pl.blk_intr.clear();
+    pl.nintr = 0;
     // intrinsics blocks of observed images
     std::vector<char> iu(P.n_intr, 0);
     for (int i = 0; i < P.n_img; ++i)
@@ -361,7 +367,9 @@ bool chunkable(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t p) {
 
 }  // namespace
 
-void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, const PlanOpts& opts) {
+namespace {
+
+void validate_problem(const sfm_ba_problem& P) {
     SFM_REQUIRE(P.n_img >= 1 && P.n_intr >= 1 && P.n_pt >= 0 && P.n_obs >= 0 &&
                     P.pt_offsets && (P.n_obs == 0 || (P.obs_img && P.obs_uv)) && P.img_intr,
                 SFM_ERR_INVALID_ARG, "incomplete BA problem");
@@ -391,43 +399,297 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     SFM_REQUIRE(P.const_img >= -1 && P.const_img < P.n_img, SFM_ERR_INVALID_ARG, "bad const_img");
     SFM_REQUIRE(sfm_ba_intr_width(P.camera_model) > 0, SFM_ERR_INVALID_ARG, "unknown camera_model %d",
                 P.camera_model);
+}
 
-    PhaseTimer tm("build_plan");
-    tm.mark("validate");
-    pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
-    pl.rank = rank; pl.world = world;
-    PointSpans spans;   // every point's active camera span: the partition's sort keys
-    active_sets(P, pl, &spans);
-    tm.mark("active");
-    // RCS storage and solver, identical on every rank: the block-banded form
-    // (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
-    // and a few intrinsics blocks, else dense (blocked Cholesky, ba_dense.hip)
-    // (the band solver's arrow holds 4-wide intrinsics blocks: RADIAL3 is dense)
-    // (the BCR arrow carries iw * nintr <= 16 bordered columns: one MFMA column
-    // tile besides the rhs, and a corner system of at most 16 x 16)
+// RCS storage and solver, identical on every rank: the block-banded form
+// (block cyclic reduction, ba_bcr.hip) for a camera band of <= 10 blocks
+// and a few intrinsics blocks, else dense (blocked Cholesky, ba_dense.hip)
+// (the band solver's arrow holds 4-wide intrinsics blocks: RADIAL3 is dense)
+// (the BCR arrow carries iw * nintr <= 16 bordered columns: one MFMA column
+// tile besides the rhs, and a corner system of at most 16 x 16)
+void decide_rcs(BAHostPlan& pl, const PlanOpts& opts) {
     pl.dense = !(pl.D <= kBandMaxD && pl.iw * pl.nintr <= 16) || opts.force_dense;
+    pl.n_sdense = 0;
     if (pl.dense) {
         SFM_REQUIRE(pl.nF <= 40000, SFM_ERR_UNSUPPORTED, "dense reduced camera system of %lld columns",
                     (long long)pl.nF);
         pl.n_sdense = pl.nF * pl.nF;
     }
+}
 
-    partition_points(P, pl.cam_blk, world, pl.order, pl.bounds, &spans);
-    tm.mark("partition");
+// ---- Schur chunks ---------------------------------------------------------------
+// Greedy over shard chunk points: a chunk's F blocks (camera 6 rows, intrinsics 4
+// rows) must fit `cap` rows of its tile: 64 (4x4 MFMA tiles, -Zw on the
+// VALU) or 76 (5x5 tiles, -Zw in row 79).  The 64-row form does 2/3 of the
+// MFMA work per point; it is used unless it would need many more chunks.
+// 128 points per chunk: ~2x the co-resident waves of the chip at C4 size,
+// so the last round of chunks is short (256 measured 17% slower).
+// A shard too small to give every wave slot of the chip a 128-point chunk
+// (a landmark shard at N = 2, 4, 8) gets shorter chunks instead, down to 16
+// points: the Schur pass takes about one chunk's latency once the chunks
+// fit in one round of the chip's 2048 wave slots (256 CUs x 2 waves per
+// SIMD x 4), and a chunk count just past a round costs a second one.  So
+// the target is 1850 chunks, a margin for the camera-window cuts
+// (profiles/r04/o_n8knobs/pts.txt, rank 0 of a C4 shard: N = 8 2147-2180
+// LM-iters/s at 31 points (2107 chunks), 2272-2282 at 40; N = 4 1838-1870
+// at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128.
+// Round 5, profiles/r05/w_tc*: target 1600 / 1750 / 1850 gives N = 4
+// 2407 / 2431 / 2463 and N = 8 2958-2967 / 2920 / 2979 LM-iters/s (1619 /
+// 1806 / 1870 chunks at N = 8, 1987 at N = 4 with 1850); fewer, longer
+// chunks (872 / 998) leave SIMDs with one wave: N = 8 2651-2726).
+#ifndef SFM_TARGET_CHUNKS
+#define SFM_TARGET_CHUNKS 1850   // (A/B builds only)
+#endif
+constexpr int64_t kTargetChunks = SFM_TARGET_CHUNKS;
+int chunk_pts_for(int64_t n_cpt) {
+    return (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (n_cpt + kTargetChunks - 1) / kTargetChunks));
+}
+// Chunk points are chunked in fixed-length ranges on host threads (a chunk
+// never spans two ranges: at most 15 extra chunks out of thousands): 4096
+// points, doubled until there are at most 16 ranges.  The ranges depend on
+// the number of chunk points only, so a grown problem's chunking keeps every
+// whole range before its first moved point (round 6; until round 5 the
+// shard was cut into up to 16 equal parts).
+int64_t chunk_range_len(int64_t ncp) {
+    int64_t r = 4096;
+    while (ncp > 16 * r) r *= 2;
+    return r;
+}
+// algorithmic flops: the symmetric Z Z' over the point's own F
+// rows (r(r+1)/2 entries x 3 x 2 = 3 r (r+1)), the linearisation (600 per
+// observation) and the point block (V, its factor, M = Jx L^-T, Z = J' M: 180
+// per observation + 30)
+int64_t point_flops(int64_t rows, int64_t nobs) { return 3 * rows * (rows + 1) + 780 * nobs + 30; }
 
-    // ---- shard arrays: chunkable points first, then general points ---------
-    const int64_t b0 = pl.bounds[rank], b1 = pl.bounds[rank + 1];
-    {
-        std::vector<char> ck(b1 - b0);
-        parallel_ranges(b1 - b0, [&](int64_t k0, int64_t k1, int) {
-            for (int64_t k = k0; k < k1; ++k) ck[k] = chunkable(P, pl, pl.order[b0 + k]);
+// A chunking is abandoned as soon as its chunk count (over all ranges)
+// passes abort_at: from there on its outcome no longer matters (see the
+// choice of the tile height below), e.g. under random visibility, where
+// chunks are dropped whatever the count.  The ranges add their chunks to
+// one shared counter as they close them.
+struct ChunkShared {
+    std::atomic<int64_t> n_closed{0};
+    std::atomic<bool> abandoned{false};
+    int64_t abort_at = INT64_MAX;
+};
+
+// greedy chunking of shard chunk points [k_begin, k_end) at `cap` tile rows;
+// slot_out is indexed by shard observation (each range writes its own)
+int64_t chunk_range(const sfm_ba_problem& P, const BAHostPlan& pl, int cap, int chunk_pts, int group_pts,
+                    int32_t k_begin, int32_t k_end, std::vector<ChunkDesc>& chunks_out, int32_t* slot_out,
+                    ChunkShared& sh) {
+    int64_t flops = 0;
+    ChunkDesc cd{};
+    std::vector<int> cams, intrs, dcams;  // F-slot images / intrinsics, staged images
+    // O(1) membership for the open chunk: image -> F slot / staged index,
+    // intrinsics -> staged index (-1 = absent); reset through the lists
+    std::vector<int> cam_slot(P.n_img, -1), dcam_idx(P.n_img, -1), intr_idx(P.n_intr, -1);
+    int rows = 0;
+    auto reset = [&](int32_t p) {
+        cd = ChunkDesc{};
+        cd.pt_begin = p;
+        cd.obs_begin = pl.pt_off[p];
+        for (int s = 0; s < kMaxSlots; ++s) { cd.slot_img[s] = -1; cd.slot_intr[s] = -1; cd.slot_row[s] = -1; cd.slot_col[s] = -1; }
+        for (int s = 0; s < kCamSlots; ++s) { cd.cam_img[s] = -1; cd.cam_row[s] = -1; cd.cam_col[s] = -1; }
+        for (int s = 0; s < kIntrSlots; ++s) { cd.intr_id[s] = -1; cd.intr_row[s] = -1; cd.intr_col[s] = -1; }
+        for (int img : cams) cam_slot[img] = -1;
+        for (int img : dcams) dcam_idx[img] = -1;
+        for (int q : intrs) intr_idx[q] = -1;
+        cams.clear(); intrs.clear(); dcams.clear(); rows = 0;
+    };
+    // a tile group: its points split evenly into <= kGroupChunks chunks of
+    // <= chunk_pts points, every chunk carrying the group's slot layout
+    auto close = [&](int32_t p_end) {
+        cd.pt_end = p_end;
+        cd.obs_end = pl.pt_off[p_end];
+        cd.n_slots = (int32_t)(cams.size() + intrs.size());
+        cd.n_cams = (int32_t)dcams.size();
+        cd.n_intr = (int32_t)intrs.size();
+        const int32_t p0 = cd.pt_begin, npg = p_end - p0;
+        const int n_sub = std::max(1, (npg + chunk_pts - 1) / chunk_pts);
+        for (int j = 0; j < n_sub; ++j) {
+            ChunkDesc sub = cd;
+            sub.pt_begin = p0 + (int32_t)((int64_t)npg * j / n_sub);
+            sub.pt_end = p0 + (int32_t)((int64_t)npg * (j + 1) / n_sub);
+            sub.obs_begin = pl.pt_off[sub.pt_begin];
+            sub.obs_end = pl.pt_off[sub.pt_end];
+            sub.sub = j;
+            chunks_out.push_back(sub);
+        }
+        if (sh.n_closed.fetch_add(n_sub, std::memory_order_relaxed) + n_sub > sh.abort_at)
+            sh.abandoned.store(true, std::memory_order_relaxed);
+    };
+    // per-point image lists in fixed storage (<= kSubObs each): this loop
+    // runs once per point, and heap vectors here dominated planning time
+    struct Small {
+        int v[kSubObs];
+        int n = 0;
+        void push_back(int x) { v[n++] = x; }
+        const int* begin() const { return v; }
+        const int* end() const { return v + n; }
+        size_t size() const { return (size_t)n; }
+        bool has(int x) const { return std::find(v, v + n, x) != v + n; }
+    };
+    if (k_end > k_begin) reset(k_begin);
+    for (int32_t k = k_begin; k < k_end; ++k) {
+        if (((k - k_begin) & 255) == 0 && sh.abandoned.load(std::memory_order_relaxed)) return flops;
+        const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
+        Small pc, pi, pd;
+        for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+            const int img = pl.obs_img[s];
+            if (pl.cam_blk[img] >= 0) pc.push_back(img);
+            pd.push_back(img);
+            const int q = P.img_intr[img];
+            if (!pi.has(q)) pi.push_back(q);
+        }
+        const int own = 6 * (int)pc.size() + pl.iw * (int)pi.size();
+        SFM_REQUIRE(own <= cap, SFM_ERR_INVALID_ARG, "internal: chunk point over %d rows", cap);
+        int add = 0, add_slots = 0, add_d = 0, add_i = 0;
+        for (int img : pc) if (cam_slot[img] < 0) { add += 6; ++add_slots; }
+        for (int q : pi) if (intr_idx[q] < 0) { add += pl.iw; ++add_slots; ++add_i; }
+        for (int img : pd) if (dcam_idx[img] < 0) ++add_d;
+        const bool full = k > cd.pt_begin &&
+                          (rows + add > cap || k - cd.pt_begin >= group_pts ||
+                           (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots ||
+                           (int)dcams.size() + add_d > kCamSlots ||
+                           (int)intrs.size() + add_i > kIntrSlots);
+        if (full) { close(k); reset(k); }
+        for (int img : pc)
+            if (cam_slot[img] < 0) {
+                const int s = (int)(cams.size() + intrs.size());
+                cams.push_back(img);
+                cam_slot[img] = s;
+                cd.slot_img[s] = img; cd.slot_row[s] = rows; cd.slot_col[s] = pl.img_colc[img];
+                rows += 6;
+            }
+        for (int q : pi)
+            if (intr_idx[q] < 0) {
+                const int s = (int)(cams.size() + intrs.size());
+                const int t = (int)intrs.size();
+                intrs.push_back(q);
+                intr_idx[q] = t;
+                cd.slot_intr[s] = q; cd.slot_row[s] = rows;
+                cd.slot_col[s] = (int32_t)(pl.nb + (int64_t)pl.iw * pl.intr_blk[q]);
+                cd.intr_id[t] = q; cd.intr_row[t] = rows; cd.intr_col[t] = cd.slot_col[s];
+                rows += pl.iw;
+            }
+        for (int img : pd)
+            if (dcam_idx[img] < 0) {
+                const int t = (int)dcams.size();
+                dcams.push_back(img);
+                dcam_idx[img] = t;
+                cd.cam_img[t] = img;
+                const int s = cam_slot[img];   // constant images have no F slot
+                if (s >= 0) { cd.cam_row[t] = cd.slot_row[s]; cd.cam_col[t] = cd.slot_col[s]; }
+            }
+        // observation -> staged camera | staged intrinsics << 8
+        for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+            const int img = pl.obs_img[s];
+            slot_out[s] = dcam_idx[img] | (intr_idx[P.img_intr[img]] << 8);
+        }
+        flops += point_flops(own, nobs);
+    }
+    if (k_end > k_begin) close(k_end);
+    return flops;
+}
+
+// One chunking at `cap` rows over the ranges [g_begin, nseg) of the chunk
+// points [0, ncp) (the ranges before g_begin are a seed plan's, with
+// `prefix_chunks` chunks).  Returns false if the chunking was abandoned (more
+// than `limit` chunks in all).
+struct Chunking {
+    std::vector<std::vector<ChunkDesc>> seg;   // per range ([g_begin, nseg) filled)
+    std::vector<int64_t> flops;
+};
+bool make_chunks(const sfm_ba_problem& P, const BAHostPlan& pl, int cap, int chunk_pts, int64_t rlen, int64_t ncp,
+                 int g_begin, int64_t prefix_chunks, int64_t limit, Chunking& out, int32_t* slot_out) {
+    const int nseg = (int)((ncp + rlen - 1) / rlen);
+    out.seg.assign(nseg, {});
+    out.flops.assign(nseg, 0);
+    ChunkShared sh;
+    sh.n_closed = prefix_chunks;
+    sh.abort_at = limit;
+    if (prefix_chunks > limit) return false;
+    const int group_pts = schur_group(cap == 64 ? 4 : 5) * chunk_pts;
+    std::vector<int> rc(nseg, SFM_OK);
+    if (nseg > g_begin)
+        parallel_segments(nseg - g_begin, [&](int q) {
+            const int g = g_begin + q;
+            rc[g] = guarded([&] {
+                const int32_t k0 = (int32_t)(g * rlen), k1 = (int32_t)std::min<int64_t>(ncp, (g + 1) * rlen);
+                out.flops[g] = chunk_range(P, pl, cap, chunk_pts, group_pts, k0, k1, out.seg[g], slot_out, sh);
+                return SFM_OK;
+            });
         });
-        std::vector<int64_t> cpts, gpts;
-        for (int64_t k = b0; k < b1; ++k) (ck[k - b0] ? cpts : gpts).push_back(pl.order[k]);
-        pl.n_cpt = (int64_t)cpts.size();
-        pl.spt_global = std::move(cpts);
+    for (int g = 0; g < nseg; ++g)
+        if (rc[g] != SFM_OK) throw SfmError{rc[g]};
+    return !sh.abandoned.load();
+}
+
+// Per chunking range: the largest tile rows (6 per active camera, iw per
+// intrinsics block) and observation count of one of its points
+void range_shapes(const sfm_ba_problem& P, const BAHostPlan& pl, int64_t ncp, int64_t rlen, int g_begin,
+                  std::vector<int32_t>& own, std::vector<int32_t>& obs) {
+    const int nseg = (int)((ncp + rlen - 1) / rlen);
+    own.resize(nseg);
+    obs.resize(nseg);
+    if (nseg > g_begin)
+        parallel_segments(nseg - g_begin, [&](int q) {
+            const int g = g_begin + q;
+            int lo_own = 0, lo_obs = 0;
+            const int64_t k1 = std::min<int64_t>(ncp, (g + 1) * rlen);
+            for (int64_t k = g * rlen; k < k1; ++k) {
+                lo_obs = std::max(lo_obs, pl.pt_off[k + 1] - pl.pt_off[k]);
+                int nc = 0;
+                int32_t pi[kIntrSlots];
+                int ni = 0;
+                for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
+                    if (pl.cam_blk[pl.obs_img[s]] >= 0) ++nc;
+                    const int q2 = P.img_intr[pl.obs_img[s]];
+                    if (std::find(pi, pi + ni, q2) == pi + ni) pi[ni++] = q2;
+                }
+                lo_own = std::max(lo_own, 6 * nc + pl.iw * ni);
+            }
+            own[g] = lo_own;
+            obs[g] = lo_obs;
+        });
+}
+
+// What a grown plan takes from its seed (build_plan_grown)
+struct Seed {
+    BAHostPlan* q;
+    int64_t pos0;   // the first sorted position the growth changes
+};
+
+// Shard arrays, Schur chunks and general points of a planned order (pl.order,
+// pl.bounds).  With a seed, the sorted positions before seed->pos0 are the
+// seed plan's (same points, same observations) and only what follows them is
+// planned; every array ends up as the fresh plan makes it.
+void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, Seed* sd, PhaseTimer& tm) {
+    const int rank = pl.rank;
+    const int64_t b0 = pl.bounds[rank], b1 = pl.bounds[rank + 1];
+    BAHostPlan* q = sd ? sd->q : nullptr;
+    const int64_t pos0 = sd ? sd->pos0 : 0;   // (world 1: shard positions = sorted positions)
+    // ---- classification: chunkable points first, then general points --------
+    std::vector<char> ck(b1 - b0);
+    if (q) std::copy(q->grow.ck.begin(), q->grow.ck.begin() + pos0, ck.begin());
+    parallel_ranges(b1 - b0 - pos0, [&](int64_t k0, int64_t k1, int) {
+        for (int64_t k = pos0 + k0; k < pos0 + k1; ++k) ck[k] = chunkable(P, pl, pl.order[b0 + k]);
+    });
+    int64_t kc0 = 0;   // chunk points before pos0
+    for (int64_t k = 0; k < pos0; ++k) kc0 += ck[k];
+    const int64_t kg0 = pos0 - kc0;   // general points before pos0
+    {
+        std::vector<int64_t> gpts;
+        pl.spt_global.clear();
+        pl.spt_global.reserve(b1 - b0);
+        for (int64_t k = b0; k < b1; ++k) {
+            if (ck[k - b0]) pl.spt_global.push_back(pl.order[k]);
+            else gpts.push_back(pl.order[k]);
+        }
+        pl.n_cpt = (int64_t)pl.spt_global.size();
         pl.spt_global.insert(pl.spt_global.end(), gpts.begin(), gpts.end());
     }
+    const int64_t n_ck = pl.n_cpt;   // classified chunkable (the chunking may drop them)
     tm.mark("classify");
     pl.n_spt = b1 - b0;
     pl.pt_off.assign(pl.n_spt + 1, 0);
@@ -437,243 +699,74 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     }
     pl.n_sobs = pl.pt_off[pl.n_spt];
     tm.mark("pt_off");
-    pl.obs_img.resize(pl.n_sobs);
-    pl.obs_uv.resize(2 * pl.n_sobs);
-    parallel_ranges(pl.n_spt, [&](int64_t k0, int64_t k1, int) {
-        for (int64_t k = k0; k < k1; ++k) {
-            const int64_t p = pl.spt_global[k];
-            for (int64_t o = P.pt_offsets[p], s = pl.pt_off[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
-                pl.obs_img[s] = P.obs_img[o];
-                pl.obs_uv[2 * s] = P.obs_uv[2 * o];
-                pl.obs_uv[2 * s + 1] = P.obs_uv[2 * o + 1];
+    // the seed's general points before pos0 (observations in image order, their
+    // slots and permutation): kept aside, their place moves with the chunk part
+    std::vector<int32_t> gp_img, gp_slot, gp_perm;
+    bool q_kept = false;
+    if (q) {
+        // the seed's general part = its non-chunkable points (it kept its chunks)
+        q_kept = q->n_cpt == q->grow.n_ck;
+        const int32_t qg0 = q->pt_off[q->n_cpt], qg1 = q->pt_off[q->n_cpt + kg0];
+        if (q_kept && qg1 > qg0) {
+            gp_img.assign(q->obs_img.begin() + qg0, q->obs_img.begin() + qg1);
+            gp_slot.assign(q->obs_slot.begin() + qg0, q->obs_slot.begin() + qg1);
+            if (!q->gobs_perm.empty()) {
+                gp_perm.assign(q->gobs_perm.begin(), q->gobs_perm.begin() + (qg1 - qg0));
+            } else {   // the seed's general points were all in image order
+                gp_perm.resize(qg1 - qg0);
+                for (int64_t g = 0; g < kg0; ++g) {
+                    const int32_t s0 = q->pt_off[q->n_cpt + g] - qg0, s1 = q->pt_off[q->n_cpt + g + 1] - qg0;
+                    for (int32_t s = s0; s < s1; ++s) gp_perm[s] = s - s0;
+                }
             }
         }
-    });
-
+        pl.obs_img = std::move(q->obs_img);
+        pl.obs_slot = std::move(q->obs_slot);
+    }
+    // the chunk part before kc0 is the seed's, as it stands
+    const int64_t s_keep = q ? pl.pt_off[kc0] : 0;
+    pl.obs_img.resize(pl.n_sobs);
+    if (!pl.uv_on_device) pl.obs_uv.resize(2 * pl.n_sobs);
+    auto copy_obs = [&](int64_t k_lo, int64_t k_hi) {   // shard points [k_lo, k_hi) from the problem
+        parallel_ranges(k_hi - k_lo, [&](int64_t a0, int64_t a1, int) {
+            for (int64_t k = k_lo + a0; k < k_lo + a1; ++k) {
+                const int64_t p = pl.spt_global[k];
+                for (int64_t o = P.pt_offsets[p], s = pl.pt_off[k]; o < P.pt_offsets[p + 1]; ++o, ++s) {
+                    pl.obs_img[s] = P.obs_img[o];
+                    if (!pl.uv_on_device) {
+                        pl.obs_uv[2 * s] = P.obs_uv[2 * o];
+                        pl.obs_uv[2 * s + 1] = P.obs_uv[2 * o + 1];
+                    }
+                }
+            }
+        });
+    };
+    // fresh: every shard point; grown: the chunkable points from kc0 on (the
+    // general part once the chunking has decided where it starts)
+    if (q) copy_obs(kc0, n_ck);
+    else copy_obs(0, pl.n_spt);
+    (void)s_keep;
     tm.mark("shard");
+
     // ---- Schur chunks over [0, n_cpt) ------------------------------------------
-    // Greedy over shard points: a chunk's F blocks (camera 6 rows, intrinsics 4
-    // rows) must fit `cap` rows of its tile: 64 (4x4 MFMA tiles, -Zw on the
-    // VALU) or 76 (5x5 tiles, -Zw in row 79).  The 64-row form does 2/3 of the
-    // MFMA work per point; it is used unless it would need many more chunks.
-    // 128 points per chunk: ~2x the co-resident waves of the chip at C4 size,
-    // so the last round of chunks is short (256 measured 17% slower).
-    // A shard too small to give every wave slot of the chip a 128-point chunk
-    // (a landmark shard at N = 2, 4, 8) gets shorter chunks instead, down to 16
-    // points: the Schur pass takes about one chunk's latency once the chunks
-    // fit in one round of the chip's 2048 wave slots (256 CUs x 2 waves per
-    // SIMD x 4), and a chunk count just past a round costs a second one.  So
-    // the target is 1850 chunks, a margin for the camera-window cuts
-    // (profiles/r04/o_n8knobs/pts.txt, rank 0 of a C4 shard: N = 8 2147-2180
-    // LM-iters/s at 31 points (2107 chunks), 2272-2282 at 40; N = 4 1838-1870
-    // at 61, 1971-1981 at 75; N = 2 1427-1429 at 122, 1583-1592 at 128.
-    // Round 5, profiles/r05/w_tc*: target 1600 / 1750 / 1850 gives N = 4
-    // 2407 / 2431 / 2463 and N = 8 2958-2967 / 2920 / 2979 LM-iters/s (1619 /
-    // 1806 / 1870 chunks at N = 8, 1987 at N = 4 with 1850); fewer, longer
-    // chunks (872 / 998) leave SIMDs with one wave: N = 8 2651-2726).
-#ifndef SFM_TARGET_CHUNKS
-#define SFM_TARGET_CHUNKS 1850   // (A/B builds only)
-#endif
-    constexpr int64_t kTargetChunks = SFM_TARGET_CHUNKS;
-    int chunk_pts = (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (pl.n_cpt + kTargetChunks - 1) / kTargetChunks));
     // Chunks of one tile group share one slot layout and one tile: the Schur
     // kernel runs a group as one workgroup, a wave per chunk, and adds the
     // waves' tiles in LDS (wave order) before the one write -- a quarter of the
     // tile traffic and of the reduce plan's tile terms of single-chunk tiles
-    int group_pts = kGroupChunks * chunk_pts;   // set per tile height (schur_group) before each chunking
-    const int32_t ncp = (int32_t)pl.n_cpt;
-    auto point_flops = [](int64_t rows, int64_t nobs) {
-        // algorithmic flops: the symmetric Z Z' over the
-        // point's own F rows (r(r+1)/2 entries x 3 x 2 = 3 r (r+1)), the
-        // linearisation (600 per observation) and the point block (V, its
-        // factor, M = Jx L^-T, Z = J' M: 180 per observation + 30)
-        return 3 * rows * (rows + 1) + 780 * nobs + 30;
-    };
-    // A chunking is abandoned as soon as its chunk count (over all ranges)
-    // passes abort_at: from there on its outcome no longer matters (see the
-    // choice of the tile height below), e.g. under random visibility, where
-    // chunks are dropped whatever the count.  The ranges add their chunks to
-    // one shared counter as they close them.
-    std::atomic<int64_t> n_closed{0};
-    std::atomic<bool> abandoned{false};
-    int64_t abort_at = INT64_MAX;
-    // greedy chunking of shard points [k_begin, k_end); slot_out is indexed by
-    // shard observation (each range writes its own)
-    auto make_chunks_range = [&](int cap, int32_t k_begin, int32_t k_end, std::vector<ChunkDesc>& chunks_out,
-                                 HostVec<int32_t>& slot_out) -> int64_t {
-        int64_t flops = 0;
-        ChunkDesc cd{};
-        std::vector<int> cams, intrs, dcams;  // F-slot images / intrinsics, staged images
-        // O(1) membership for the open chunk: image -> F slot / staged index,
-        // intrinsics -> staged index (-1 = absent); reset through the lists
-        std::vector<int> cam_slot(P.n_img, -1), dcam_idx(P.n_img, -1), intr_idx(P.n_intr, -1);
-        int rows = 0;
-        auto reset = [&](int32_t p) {
-            cd = ChunkDesc{};
-            cd.pt_begin = p;
-            cd.obs_begin = pl.pt_off[p];
-            for (int s = 0; s < kMaxSlots; ++s) { cd.slot_img[s] = -1; cd.slot_intr[s] = -1; cd.slot_row[s] = -1; cd.slot_col[s] = -1; }
-            for (int s = 0; s < kCamSlots; ++s) { cd.cam_img[s] = -1; cd.cam_row[s] = -1; cd.cam_col[s] = -1; }
-            for (int s = 0; s < kIntrSlots; ++s) { cd.intr_id[s] = -1; cd.intr_row[s] = -1; cd.intr_col[s] = -1; }
-            for (int img : cams) cam_slot[img] = -1;
-            for (int img : dcams) dcam_idx[img] = -1;
-            for (int q : intrs) intr_idx[q] = -1;
-            cams.clear(); intrs.clear(); dcams.clear(); rows = 0;
-        };
-        // a tile group: its points split evenly into <= kGroupChunks chunks of
-        // <= chunk_pts points, every chunk carrying the group's slot layout
-        auto close = [&](int32_t p_end) {
-            cd.pt_end = p_end;
-            cd.obs_end = pl.pt_off[p_end];
-            cd.n_slots = (int32_t)(cams.size() + intrs.size());
-            cd.n_cams = (int32_t)dcams.size();
-            cd.n_intr = (int32_t)intrs.size();
-            const int32_t p0 = cd.pt_begin, npg = p_end - p0;
-            const int n_sub = std::max(1, (npg + chunk_pts - 1) / chunk_pts);
-            for (int j = 0; j < n_sub; ++j) {
-                ChunkDesc sub = cd;
-                sub.pt_begin = p0 + (int32_t)((int64_t)npg * j / n_sub);
-                sub.pt_end = p0 + (int32_t)((int64_t)npg * (j + 1) / n_sub);
-                sub.obs_begin = pl.pt_off[sub.pt_begin];
-                sub.obs_end = pl.pt_off[sub.pt_end];
-                sub.sub = j;
-                chunks_out.push_back(sub);
-            }
-            if (n_closed.fetch_add(n_sub, std::memory_order_relaxed) + n_sub > abort_at)
-                abandoned.store(true, std::memory_order_relaxed);
-        };
-        // per-point image lists in fixed storage (<= kSubObs each): this loop
-        // runs once per point, and heap vectors here dominated planning time
-        struct Small {
-            int v[kSubObs];
-            int n = 0;
-            void push_back(int x) { v[n++] = x; }
-            const int* begin() const { return v; }
-            const int* end() const { return v + n; }
-            size_t size() const { return (size_t)n; }
-            bool has(int x) const { return std::find(v, v + n, x) != v + n; }
-        };
-        if (k_end > k_begin) reset(k_begin);
-        for (int32_t k = k_begin; k < k_end; ++k) {
-            if (((k - k_begin) & 255) == 0 && abandoned.load(std::memory_order_relaxed)) return flops;
-            const int32_t nobs = pl.pt_off[k + 1] - pl.pt_off[k];
-            Small pc, pi, pd;
-            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
-                const int img = pl.obs_img[s];
-                if (pl.cam_blk[img] >= 0) pc.push_back(img);
-                pd.push_back(img);
-                const int q = P.img_intr[img];
-                if (!pi.has(q)) pi.push_back(q);
-            }
-            const int own = 6 * (int)pc.size() + pl.iw * (int)pi.size();
-            SFM_REQUIRE(own <= cap, SFM_ERR_INVALID_ARG, "internal: chunk point over %d rows", cap);
-            int add = 0, add_slots = 0, add_d = 0, add_i = 0;
-            for (int img : pc) if (cam_slot[img] < 0) { add += 6; ++add_slots; }
-            for (int q : pi) if (intr_idx[q] < 0) { add += pl.iw; ++add_slots; ++add_i; }
-            for (int img : pd) if (dcam_idx[img] < 0) ++add_d;
-            const bool full = k > cd.pt_begin &&
-                              (rows + add > cap || k - cd.pt_begin >= group_pts ||
-                               (int)(cams.size() + intrs.size()) + add_slots > kMaxSlots ||
-                               (int)dcams.size() + add_d > kCamSlots ||
-                               (int)intrs.size() + add_i > kIntrSlots);
-            if (full) { close(k); reset(k); }
-            for (int img : pc)
-                if (cam_slot[img] < 0) {
-                    const int s = (int)(cams.size() + intrs.size());
-                    cams.push_back(img);
-                    cam_slot[img] = s;
-                    cd.slot_img[s] = img; cd.slot_row[s] = rows; cd.slot_col[s] = pl.img_colc[img];
-                    rows += 6;
-                }
-            for (int q : pi)
-                if (intr_idx[q] < 0) {
-                    const int s = (int)(cams.size() + intrs.size());
-                    const int t = (int)intrs.size();
-                    intrs.push_back(q);
-                    intr_idx[q] = t;
-                    cd.slot_intr[s] = q; cd.slot_row[s] = rows;
-                    cd.slot_col[s] = (int32_t)(pl.nb + (int64_t)pl.iw * pl.intr_blk[q]);
-                    cd.intr_id[t] = q; cd.intr_row[t] = rows; cd.intr_col[t] = cd.slot_col[s];
-                    rows += pl.iw;
-                }
-            for (int img : pd)
-                if (dcam_idx[img] < 0) {
-                    const int t = (int)dcams.size();
-                    dcams.push_back(img);
-                    dcam_idx[img] = t;
-                    cd.cam_img[t] = img;
-                    const int s = cam_slot[img];   // constant images have no F slot
-                    if (s >= 0) { cd.cam_row[t] = cd.slot_row[s]; cd.cam_col[t] = cd.slot_col[s]; }
-                }
-            // observation -> staged camera | staged intrinsics << 8
-            for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
-                const int img = pl.obs_img[s];
-                slot_out[s] = dcam_idx[img] | (intr_idx[P.img_intr[img]] << 8);
-            }
-            flops += point_flops(own, nobs);
-        }
-        if (k_end > k_begin) close(k_end);
-        return flops;
-    };
-    // Shards are chunked in up to 16 fixed point ranges of >= 4096 points on
-    // host threads (a chunk never spans two ranges: at most 15 extra chunks
-    // out of thousands; the split depends on the shard only, never on the host)
-    // returns false if the chunking was abandoned (more than `limit` chunks)
-    auto make_chunks = [&](int cap, std::vector<ChunkDesc>& chunks_out, HostVec<int32_t>& slot_out, int64_t limit,
-                           int64_t& flops) -> bool {
-        n_closed = 0;
-        abandoned = false;
-        abort_at = limit;
-        const int gw = schur_group(cap == 64 ? 4 : 5);
-        group_pts = gw * chunk_pts;
-        slot_out.reserve(pl.n_sobs);        // (grown to every observation once kept, in place)
-        slot_out.resize(pl.pt_off[ncp]);   // every entry written by its range
-        const int nseg = (int)std::max<int64_t>(1, std::min<int64_t>(16, ncp / 4096));
-        std::vector<std::vector<ChunkDesc>> seg_chunks(nseg);
-        std::vector<int64_t> seg_flops(nseg, 0);
-        std::vector<int> seg_rc(nseg, SFM_OK);
-        auto run = [&](int g) {
-            seg_rc[g] = guarded([&] {
-                const int32_t k0 = (int32_t)((int64_t)ncp * g / nseg), k1 = (int32_t)((int64_t)ncp * (g + 1) / nseg);
-                seg_flops[g] = make_chunks_range(cap, k0, k1, seg_chunks[g], slot_out);
-                return SFM_OK;
-            });
-        };
-        parallel_segments(nseg, run);
-        flops = 0;
-        chunks_out.clear();
-        for (int g = 0; g < nseg; ++g)
-            if (seg_rc[g] != SFM_OK) throw SfmError{seg_rc[g]};
-        if (abandoned.load()) return false;
-        for (int g = 0; g < nseg; ++g) {
-            chunks_out.insert(chunks_out.end(), seg_chunks[g].begin(), seg_chunks[g].end());
-            flops += seg_flops[g];
-        }
-        return true;
-    };
-    tm.mark("shard_copy");
-    int max_own = 0, max_obs = 0;
-    {
-        int mo[16] = {0}, mb[16] = {0};
-        parallel_ranges(ncp, [&](int64_t k0, int64_t k1, int t) {
-            int lo_own = 0, lo_obs = 0;   // thread-local (the arrays share a cache line)
-            for (int64_t k = k0; k < k1; ++k) {
-                lo_obs = std::max(lo_obs, pl.pt_off[k + 1] - pl.pt_off[k]);
-                int nc = 0;
-                int32_t pi[kIntrSlots];
-                int ni = 0;
-                for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
-                    if (pl.cam_blk[pl.obs_img[s]] >= 0) ++nc;
-                    const int q = P.img_intr[pl.obs_img[s]];
-                    if (std::find(pi, pi + ni, q) == pi + ni) pi[ni++] = q;
-                }
-                lo_own = std::max(lo_own, 6 * nc + pl.iw * ni);
-            }
-            mo[t] = lo_own;
-            mb[t] = lo_obs;
-        });
-        for (int t = 0; t < 16; ++t) { max_own = std::max(max_own, mo[t]); max_obs = std::max(max_obs, mb[t]); }
+    const int chunk_pts = chunk_pts_for(pl.n_cpt);
+    const int64_t ncp = pl.n_cpt, rlen = chunk_range_len(ncp);
+    const int nseg = (int)((ncp + rlen - 1) / rlen);
+    // the seed's ranges before the one holding the first re-planned chunk point
+    const bool same_ranges = q && q->grow.rlen == rlen;
+    const int g_shape = same_ranges ? (int)(kc0 / rlen) : 0;
+    std::vector<int32_t> seg_own, seg_obs;
+    if (g_shape > 0) {
+        seg_own.assign(q->grow.seg_own.begin(), q->grow.seg_own.begin() + g_shape);
+        seg_obs.assign(q->grow.seg_obs.begin(), q->grow.seg_obs.begin() + g_shape);
     }
+    range_shapes(P, pl, ncp, rlen, g_shape, seg_own, seg_obs);
+    int max_own = 0, max_obs = 0;
+    for (int g = 0; g < nseg; ++g) { max_own = std::max(max_own, seg_own[g]); max_obs = std::max(max_obs, seg_obs[g]); }
     tm.mark("chunk_shape");
     int64_t flops = 0;
     HostVec<int32_t> cslot;
@@ -684,32 +777,77 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     // chunking of more than n_cpt / 4 chunks is dropped
     const int64_t keep_max = pl.n_cpt / 4;
     bool kept = true;
+    int kept_cap = 0;
+    const bool both = max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !opts.tile80;
+    std::vector<int32_t> seg_nch;
+    std::vector<int64_t> seg_fl;
+    auto take = [&](Chunking& c, int g_from) {   // ranges [g_from, nseg) of c after pl.chunks
+        for (int g = g_from; g < nseg; ++g) {
+            pl.chunks.insert(pl.chunks.end(), c.seg[g].begin(), c.seg[g].end());
+            seg_nch.push_back((int32_t)c.seg[g].size());
+            seg_fl.push_back(c.flops[g]);
+        }
+    };
+    pl.chunks.clear();
     // the 64-row kernel walks batches of at most schur4_obs observations
-    if (max_own <= 64 && max_obs <= schur4_obs(P.camera_model) && !opts.tile80) {
+    if (both) {
         // both tile heights are planned (each over the host threads); the
         // 64-row one is taken unless it needs 5/4 as many chunks.  80 rows
         // over keep_max: dropped if taken, so 64 rows matter only within
         // keep_max; else 64 rows matter only within 5/4 of the 80-row count
-        std::vector<ChunkDesc> c4, c5;
+        Chunking c4, c5;
         HostVec<int32_t> s4, s5;
-        int64_t f4 = 0, f5 = 0;
-        const bool ok5 = make_chunks(kTileRowsUsed, c5, s5, keep_max, f5);
-        const bool ok4 = make_chunks(64, c4, s4, ok5 ? (int64_t)c5.size() * 5 / 4 : keep_max, f4);
+        s4.resize(pl.pt_off[ncp]);
+        s5.resize(pl.pt_off[ncp]);
+        const bool ok5 = make_chunks(P, pl, kTileRowsUsed, chunk_pts, rlen, ncp, 0, 0, keep_max, c5, s5.data());
+        int64_t n5 = 0;
+        for (auto& v : c5.seg) n5 += (int64_t)v.size();
+        const bool ok4 = make_chunks(P, pl, 64, chunk_pts, rlen, ncp, 0, 0, ok5 ? n5 * 5 / 4 : keep_max, c4, s4.data());
         if (ok4) {
-            pl.tile_nt = 4; pl.chunks.swap(c4); cslot.swap(s4); flops = f4;
+            pl.tile_nt = 4; take(c4, 0); cslot.swap(s4); kept_cap = 64;
         } else if (ok5) {
-            pl.chunks.swap(c5); cslot.swap(s5); flops = f5;
+            take(c5, 0); cslot.swap(s5); kept_cap = kTileRowsUsed;
         } else {
             kept = false;
         }
     } else {
-        kept = make_chunks(kTileRowsUsed, pl.chunks, cslot, keep_max, flops);
+        // one height: the seed's whole ranges before the first re-planned
+        // chunk point are taken as they are (same chunk points, chunk length
+        // and range length), the rest chunked
+        const bool reuse = same_ranges && q_kept && q->grow.cap == kTileRowsUsed && q->grow.chunk_pts == chunk_pts;
+        const int g0 = reuse ? (int)(kc0 / rlen) : 0;
+        int64_t prefix = 0;
+        if (reuse) {
+            for (int g = 0; g < g0; ++g) prefix += q->grow.seg_nch[g];
+            pl.chunks.assign(q->chunks.begin(), q->chunks.begin() + prefix);
+            // the intrinsics' F columns follow the camera columns, whose count grew
+            for (ChunkDesc& c : pl.chunks) {
+                for (int a = 0; a < c.n_slots; ++a)
+                    if (c.slot_intr[a] >= 0) c.slot_col[a] = (int32_t)(pl.nb + (int64_t)pl.iw * pl.intr_blk[c.slot_intr[a]]);
+                for (int t = 0; t < c.n_intr; ++t)
+                    c.intr_col[t] = (int32_t)(pl.nb + (int64_t)pl.iw * pl.intr_blk[c.intr_id[t]]);
+            }
+            seg_nch.assign(q->grow.seg_nch.begin(), q->grow.seg_nch.begin() + g0);
+            seg_fl.assign(q->grow.seg_flops.begin(), q->grow.seg_flops.begin() + g0);
+            cslot = std::move(pl.obs_slot);   // the seed's slots of those ranges, in place
+        }
+        cslot.resize(pl.pt_off[ncp]);
+        Chunking c5;
+        kept = make_chunks(P, pl, kTileRowsUsed, chunk_pts, rlen, ncp, g0, prefix, keep_max, c5, cslot.data());
+        if (kept) {
+            take(c5, g0);
+            kept_cap = kTileRowsUsed;
+        }
     }
+    for (int64_t f : seg_fl) flops += f;
     if (!kept || (pl.n_cpt > 0 && (int64_t)pl.chunks.size() * 4 > pl.n_cpt)) {
         pl.chunks.clear();
         cslot.clear();
         pl.n_cpt = 0;
         flops = 0;
+        kept_cap = 0;
+        seg_nch.clear();
+        seg_fl.clear();
     }
     pl.group_off.clear();
     for (int32_t c = 0; c < (int32_t)pl.chunks.size(); ++c)
@@ -720,41 +858,66 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     cslot.resize(pl.n_sobs);
     pl.obs_slot.swap(cslot);
     pl.n_gpt = pl.n_spt - pl.n_cpt;
+
+    // ---- general points ---------------------------------------------------------
+    // (the seed's general points before pos0 are taken when both plans kept
+    // their chunks: the same general points lead the same general part)
+    const bool gen_reuse = q && q_kept && kept_cap != 0 && pl.n_cpt == n_ck;
+    const int64_t gk0 = gen_reuse ? kg0 : 0;   // general points taken from the seed
+    const int32_t gobs0 = pl.pt_off[pl.n_cpt];
+    const int32_t gkeep = pl.pt_off[pl.n_cpt + gk0] - gobs0;   // their observations
+    if (gen_reuse) {
+        std::copy(gp_img.begin(), gp_img.begin() + gkeep, pl.obs_img.begin() + gobs0);
+        std::copy(gp_slot.begin(), gp_slot.begin() + gkeep, pl.obs_slot.begin() + gobs0);
+    }
+    if (q) copy_obs(std::max<int64_t>(n_ck, pl.n_cpt + gk0), pl.n_spt);
     // a general point's observations in image order, so that repeated views
     // of one image are adjacent (the Z kernel sums runs of one camera block);
     // the permutation is kept for the plan cache's value refresh
-    const int32_t gobs0 = pl.pt_off[pl.n_cpt];
     pl.gobs_perm.assign(pl.n_sobs - gobs0, 0);
     int permuted[16] = {0};
-    parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int t) {
+    if (gen_reuse && gkeep > 0) {
+        std::copy(gp_perm.begin(), gp_perm.begin() + gkeep, pl.gobs_perm.begin());
+        for (int64_t g = 0; g < gk0 && !permuted[0]; ++g) {
+            const int32_t s0 = pl.pt_off[pl.n_cpt + g] - gobs0, s1 = pl.pt_off[pl.n_cpt + g + 1] - gobs0;
+            for (int32_t s = s0; s < s1; ++s) permuted[0] |= pl.gobs_perm[s] != s - s0;
+        }
+    }
+    parallel_ranges(pl.n_gpt - gk0, [&](int64_t a0, int64_t a1, int t) {
         std::vector<int32_t> idx;
         std::vector<int32_t> img;
         std::vector<double> uv;
-        for (int64_t g = g0; g < g1; ++g) {
+        for (int64_t g = gk0 + a0; g < gk0 + a1; ++g) {
             const int64_t k = pl.n_cpt + g;
             const int32_t s0 = pl.pt_off[k], n = pl.pt_off[k + 1] - s0;
             idx.resize(n);
             std::iota(idx.begin(), idx.end(), 0);
             auto before = [&](int32_t a, int32_t b) { return pl.obs_img[s0 + a] < pl.obs_img[s0 + b]; };
             if (n <= 64) {   // insertion sort: stable, no buffer (stable_sort allocated one per point)
-                for (int32_t q = 1; q < n; ++q) {
-                    const int32_t x = idx[q];
-                    int32_t r = q;
+                for (int32_t r0 = 1; r0 < n; ++r0) {
+                    const int32_t x = idx[r0];
+                    int32_t r = r0;
                     for (; r > 0 && before(x, idx[r - 1]); --r) idx[r] = idx[r - 1];
                     idx[r] = x;
                 }
             } else {
                 std::stable_sort(idx.begin(), idx.end(), before);
             }
-            img.assign(pl.obs_img.begin() + s0, pl.obs_img.begin() + s0 + n);
-            uv.assign(pl.obs_uv.begin() + 2 * s0, pl.obs_uv.begin() + 2 * (s0 + n));
-            for (int32_t q = 0; q < n; ++q) {
-                pl.obs_img[s0 + q] = img[idx[q]];
-                pl.obs_uv[2 * (s0 + q)] = uv[2 * idx[q]];
-                pl.obs_uv[2 * (s0 + q) + 1] = uv[2 * idx[q] + 1];
-                pl.gobs_perm[s0 + q - gobs0] = idx[q];
-                permuted[t] |= idx[q] != q;
+            bool moved = false;
+            for (int32_t r = 0; r < n; ++r) moved |= idx[r] != r;
+            if (moved) {
+                img.assign(pl.obs_img.begin() + s0, pl.obs_img.begin() + s0 + n);
+                for (int32_t r = 0; r < n; ++r) pl.obs_img[s0 + r] = img[idx[r]];
+                if (!pl.uv_on_device) {
+                    uv.assign(pl.obs_uv.begin() + 2 * s0, pl.obs_uv.begin() + 2 * (s0 + n));
+                    for (int32_t r = 0; r < n; ++r) {
+                        pl.obs_uv[2 * (s0 + r)] = uv[2 * idx[r]];
+                        pl.obs_uv[2 * (s0 + r) + 1] = uv[2 * idx[r] + 1];
+                    }
+                }
+                permuted[t] = 1;
             }
+            for (int32_t r = 0; r < n; ++r) pl.gobs_perm[s0 + r - gobs0] = idx[r];
         }
     });
     if (std::none_of(permuted, permuted + 16, [](int v) { return v != 0; })) pl.gobs_perm.clear();
@@ -762,10 +925,24 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     // ---- general points: their F blocks and Z buffer layout --------------------
     // blocks in F-column order; obs_slot = local camera block (0xffff: constant
     // image) | local intrinsics block << 16
-    pl.gblk_off.assign(pl.n_gpt + 1, 0);
-    pl.gz_off.assign(pl.n_gpt + 1, 0);
-    pl.gblk_col.clear();
-    pl.gblk_z.clear();
+    std::vector<int64_t> gflops(pl.n_gpt, 0);
+    if (gen_reuse) {
+        pl.gblk_off = std::move(q->gblk_off);
+        pl.gz_off = std::move(q->gz_off);
+        pl.gblk_col = std::move(q->gblk_col);
+        pl.gblk_z = std::move(q->gblk_z);
+        std::copy(q->grow.gflops.begin(), q->grow.gflops.begin() + gk0, gflops.begin());
+    }
+    if (gen_reuse && pl.nb != q->nb) {   // the seed's intrinsics columns, moved behind the new cameras'
+        const int32_t shift = (int32_t)(pl.nb - q->nb);
+        for (int32_t a = 0; a < pl.gblk_off[gk0]; ++a)
+            if (pl.gblk_col[a] >= q->nb) pl.gblk_col[a] += shift;
+    }
+    pl.gblk_off.resize(pl.n_gpt + 1);
+    pl.gz_off.resize(pl.n_gpt + 1);
+    pl.gblk_off[0] = 0;
+    pl.gz_off[0] = 0;
+    pl.gz_max = 0;
     {
         // two passes on the host threads: block counts and Z sizes per point,
         // then (after the prefix sums) every point writes its own blocks
@@ -784,38 +961,39 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
             for (int32_t c : cols) z += 3 * (c < pl.nb ? 6 : pl.iw);
             return z;
         };
-        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int) {
+        // per-point counts in [g + 1] (the seed's prefix sums stay for g < gk0)
+        std::vector<int32_t> nblk(pl.n_gpt - gk0), nz(pl.n_gpt - gk0);
+        parallel_ranges(pl.n_gpt - gk0, [&](int64_t a0, int64_t a1, int) {
             std::vector<int32_t> cols;
-            for (int64_t g = g0; g < g1; ++g) {
-                const int64_t k = pl.n_cpt + g;
+            for (int64_t a = a0; a < a1; ++a) {
+                const int64_t g = gk0 + a, k = pl.n_cpt + g;
                 point_cols(k, cols);
                 SFM_REQUIRE(cols.size() < 0xffff, SFM_ERR_UNSUPPORTED, "point with %zu parameter blocks", cols.size());
                 const int32_t z = zrows(cols);
                 SFM_REQUIRE(z + 3 <= kZMaxDoubles, SFM_ERR_UNSUPPORTED,
                             "point %lld observed by %zu parameter blocks (more than the %d rows one wavefront eliminates)",
                             (long long)pl.spt_global[k], cols.size(), kZMaxDoubles / 3);
-                pl.gblk_off[g + 1] = (int32_t)cols.size();
-                pl.gz_off[g + 1] = z + 3;   // + w = L^-1 g_E
+                nblk[a] = (int32_t)cols.size();
+                nz[a] = z + 3;   // + w = L^-1 g_E
             }
         });
-        for (int64_t g = 0; g < pl.n_gpt; ++g) {
-            pl.gz_max = std::max<int64_t>(pl.gz_max, pl.gz_off[g + 1]);
-            pl.gblk_off[g + 1] += pl.gblk_off[g];
-            pl.gz_off[g + 1] += pl.gz_off[g];
+        for (int64_t g = 0; g < gk0; ++g) pl.gz_max = std::max<int64_t>(pl.gz_max, pl.gz_off[g + 1] - pl.gz_off[g]);
+        for (int64_t g = gk0; g < pl.n_gpt; ++g) {
+            pl.gz_max = std::max<int64_t>(pl.gz_max, nz[g - gk0]);
+            pl.gblk_off[g + 1] = pl.gblk_off[g] + nblk[g - gk0];
+            pl.gz_off[g + 1] = pl.gz_off[g] + nz[g - gk0];
         }
         pl.gblk_col.resize(pl.gblk_off[pl.n_gpt]);
         pl.gblk_z.resize(pl.gblk_off[pl.n_gpt]);
-        int64_t gfl[16] = {0};
-        parallel_ranges(pl.n_gpt, [&](int64_t g0, int64_t g1, int t) {
+        parallel_ranges(pl.n_gpt - gk0, [&](int64_t a0, int64_t a1, int) {
             std::vector<int32_t> cols;
-            int64_t fl = 0;
-            for (int64_t g = g0; g < g1; ++g) {
+            for (int64_t g = gk0 + a0; g < gk0 + a1; ++g) {
                 const int64_t k = pl.n_cpt + g;
                 point_cols(k, cols);
-                int32_t z = 0, q = pl.gblk_off[g];
+                int32_t z = 0, qb = pl.gblk_off[g];
                 for (int32_t c : cols) {
-                    pl.gblk_col[q] = c;
-                    pl.gblk_z[q++] = z;
+                    pl.gblk_col[qb] = c;
+                    pl.gblk_z[qb++] = z;
                     z += 3 * (c < pl.nb ? 6 : pl.iw);
                 }
                 for (int32_t s = pl.pt_off[k]; s < pl.pt_off[k + 1]; ++s) {
@@ -826,11 +1004,10 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
                     const int32_t ib = (int32_t)(std::lower_bound(cols.begin(), cols.end(), pl.img_coli[img]) - cols.begin());
                     pl.obs_slot[s] = cb | (ib << 16);
                 }
-                fl += point_flops(z / 3, pl.pt_off[k + 1] - pl.pt_off[k]);
+                gflops[g] = point_flops(z / 3, pl.pt_off[k + 1] - pl.pt_off[k]);
             }
-            gfl[t] = fl;
         });
-        for (int64_t f : gfl) flops += f;
+        for (int64_t f : gflops) flops += f;
         pl.n_z = pl.gz_off[pl.n_gpt];
         // Z kernel work: batches of consecutive short points, the rest alone
         pl.zbatch.clear();
@@ -856,6 +1033,19 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
         close((int32_t)pl.n_gpt);
     }
     tm.mark("general");
+    pl.reused_pts = pos0;
+    // what the next grown plan takes (world 1)
+    PlanGrowState& gs = pl.grow;
+    gs.ck = std::move(ck);
+    gs.rlen = rlen;
+    gs.chunk_pts = chunk_pts;
+    gs.n_ck = n_ck;
+    gs.cap = !both && kept_cap == kTileRowsUsed ? kept_cap : 0;   // (a two-height choice is re-planned)
+    gs.seg_nch = std::move(seg_nch);
+    gs.seg_flops = std::move(seg_fl);
+    gs.seg_own = std::move(seg_own);
+    gs.seg_obs = std::move(seg_obs);
+    gs.gflops = std::move(gflops);
     // the observation arrays are final from here on: the caller may start
     // their upload while the reduce plan is built
     if (pl.on_shard_ready) pl.on_shard_ready(pl);
@@ -884,8 +1074,7 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
         // image (profiles/r04/cc_gseg: C4 at N = 1, ~5000 each: 1086-1088 /
         // 1080-1083 / 1047-1052 LM-iters/s with 3 / 4 / 6; rank 0 of N = 8,
         // ~625 each: 2438-2444 / 2398-2401 / 2344-2347 with 2 / 3 / 4, and one
-        // measured slower than three, profiles/r04/k_shard); SFM_GRAM_SEG
-        // overrides (A/B only)
+        // measured slower than three, profiles/r04/k_shard)
         pl.gram_img.clear();
         for (int i = 0; i < P.n_img; ++i)
             if (pl.img_obs_ptr[i + 1] != pl.img_obs_ptr[i]) pl.gram_img.push_back(i);
@@ -894,6 +1083,179 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
         pl.gram_seg = std::min<int32_t>(kGramSeg, avg >= 1600 ? 3 : avg >= 128 ? 2 : 1);
     }
     tm.mark("image_csr");
+}
+
+void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm);
+
+}  // namespace
+
+void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, const PlanOpts& opts) {
+    validate_problem(P);
+    PhaseTimer tm("build_plan");
+    tm.mark("validate");
+    pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
+    pl.rank = rank; pl.world = world;
+    PointSpans spans;   // every point's active camera span: the partition's sort keys
+    std::vector<char> im;   // observed images
+    bool rcm = false;
+    int32_t lb = 0;
+    pl.cam_blk = camera_blocks(P, &pl.ncam, &pl.D, &spans, &im, &lb, &rcm);
+    active_from_blocks(P, pl, im);
+    tm.mark("active");
+    decide_rcs(pl, opts);
+    partition_points(P, pl.cam_blk, world, pl.order, pl.bounds, &spans);
+    tm.mark("partition");
+    plan_points(P, pl, opts, nullptr, tm);
+    build_reduce_plan(P, pl, tm);
+    // a grown problem's plan can start from this one (world 1, the images'
+    // own camera order: a reordering moves every camera)
+    PlanGrowState& gs = pl.grow;
+    gs.ok = world == 1 && !rcm;
+    if (gs.ok) {
+        gs.span_lo = std::move(spans.lo);
+        gs.span_hi = std::move(spans.hi);
+        gs.used = std::move(im);
+        gs.lb = lb;
+    }
+}
+
+bool build_plan_grown(const sfm_ba_problem& P, const GrowPrev& prev, BAHostPlan& q, BAHostPlan& pl,
+                      const PlanOpts& opts) {
+    // ---- does P grow prev, and can q seed it?  (nothing of q moves before
+    // every check has passed) ----------------------------------------------------
+    if (!q.grow.ok || q.world != 1 || q.n_pt != prev.n_pt || q.n_obs != prev.n_obs || q.n_img != prev.n_img) return false;
+    if (P.n_intr != prev.n_intr || P.const_img != prev.const_img || P.camera_model != prev.model ||
+        P.n_img < prev.n_img || P.n_pt < prev.n_pt || P.n_obs < prev.n_obs || !P.pt_offsets || !P.img_intr ||
+        (P.n_obs > 0 && !P.obs_img))
+        return false;
+    if (prev.n_img > 0 && std::memcmp(P.img_intr, prev.img_intr, sizeof(int32_t) * prev.n_img) != 0) return false;
+    validate_problem(P);
+    PhaseTimer tm("build_plan_grown");
+    const int64_t n_old = prev.n_pt;
+    // every old point keeps its observations, in order, and may gain new ones
+    std::vector<char> chg(n_old, 0);
+    {
+        int bad[16] = {0};
+        parallel_ranges(n_old, [&](int64_t p0, int64_t p1, int t) {
+            for (int64_t p = p0; p < p1 && !bad[t]; ++p) {
+                const int64_t n0 = prev.pt_offsets[p + 1] - prev.pt_offsets[p], n1 = P.pt_offsets[p + 1] - P.pt_offsets[p];
+                if (n1 < n0 || std::memcmp(P.obs_img + P.pt_offsets[p], prev.obs_img + prev.pt_offsets[p],
+                                           sizeof(int32_t) * n0) != 0)
+                    bad[t] = 1;
+                chg[p] = n1 != n0;
+            }
+        });
+        if (std::any_of(bad, bad + 16, [](int v) { return v != 0; })) return false;
+    }
+    tm.mark("check");
+    // observed images and camera blocks: the old images keep their blocks
+    std::vector<char> used(q.grow.used);
+    used.resize(P.n_img, 0);
+    auto each_new_obs = [&](auto&& fn) {   // observations appended to old points, then the new points'
+        for (int64_t p = 0; p < n_old; ++p)
+            if (chg[p])
+                for (int64_t o = P.pt_offsets[p] + (prev.pt_offsets[p + 1] - prev.pt_offsets[p]); o < P.pt_offsets[p + 1]; ++o)
+                    fn(o);
+        for (int64_t o = P.pt_offsets[n_old]; o < P.n_obs; ++o) fn(o);
+    };
+    each_new_obs([&](int64_t o) { used[P.obs_img[o]] = 1; });
+    std::vector<int32_t> cam_blk(P.n_img, -1);
+    int32_t ncam = 0;
+    for (int i = 0; i < P.n_img; ++i)
+        if (used[i] && i != P.const_img) cam_blk[i] = ncam++;
+    for (int i = 0; i < prev.n_img; ++i)
+        if (cam_blk[i] != q.cam_blk[i]) return false;
+    {   // the same active intrinsics blocks
+        std::vector<char> iu(P.n_intr, 0);
+        for (int i = 0; i < P.n_img; ++i)
+            if (used[i]) iu[P.img_intr[i]] = 1;
+        for (int k = 0; k < P.n_intr; ++k)
+            if ((iu[k] != 0) != (q.intr_blk[k] >= 0)) return false;
+    }
+    // spans, the half bandwidth and the long-track bound of the moved points
+    std::vector<int32_t> lo(q.grow.span_lo), hi(q.grow.span_hi);
+    lo.resize(P.n_pt);
+    hi.resize(P.n_pt);
+    int32_t D = q.D, lb = q.grow.lb;
+    std::vector<int64_t> moved;   // old points with new observations, then the new points
+    for (int64_t p = 0; p < n_old; ++p)
+        if (chg[p]) moved.push_back(p);
+    for (int64_t p = n_old; p < P.n_pt; ++p) moved.push_back(p);
+    {
+        std::vector<int32_t> cs;
+        for (int64_t p : moved) {
+            int l = INT_MAX, h = -1;
+            cs.clear();
+            for (int64_t o = P.pt_offsets[p]; o < P.pt_offsets[p + 1]; ++o) {
+                const int b = cam_blk[P.obs_img[o]];
+                if (b >= 0) { l = std::min(l, b); h = std::max(h, b); cs.push_back(b); }
+            }
+            if (h >= 0) D = std::max(D, h - l);
+            lo[p] = h >= 0 ? l : ncam;
+            hi[p] = h + 1;
+            std::sort(cs.begin(), cs.end());
+            lb = std::max(lb, (int32_t)(std::unique(cs.begin(), cs.end()) - cs.begin()) - 1);
+        }
+    }
+    // the unmoved points without an active camera sort last: their key (ncam, 0)
+    // moves with ncam
+    if (ncam != q.ncam)
+        for (int64_t p = 0; p < n_old; ++p)
+            if (!chg[p] && hi[p] == 0) return false;
+    // build_plan would try a reverse Cuthill-McKee order here (camera_blocks)
+    if (D > kBandMaxD && lb <= kBandMaxD && ncam > 2 && P.n_obs <= (int64_t)8 << 20) return false;
+    tm.mark("active");
+
+    // ---- from here on q is consumed -------------------------------------------------
+    pl.n_img = P.n_img; pl.n_intr = P.n_intr; pl.n_pt = P.n_pt; pl.n_obs = P.n_obs;
+    pl.rank = 0; pl.world = 1;
+    pl.uv_on_device = true;
+    pl.cam_blk = std::move(cam_blk);
+    pl.ncam = ncam;
+    pl.D = D;
+    active_from_blocks(P, pl, used);
+    decide_rcs(pl, opts);
+    // the sorted order: the unmoved points keep their relative order (their
+    // keys did not change), the moved ones are merged in by (first, last
+    // camera block, index) -- the order of build_plan's stable counting sorts
+    auto less = [&](int64_t a, int64_t b) {
+        return lo[a] != lo[b] ? lo[a] < lo[b] : hi[a] != hi[b] ? hi[a] < hi[b] : a < b;
+    };
+    std::sort(moved.begin(), moved.end(), less);
+    pl.order.resize(P.n_pt);
+    {
+        size_t m = 0;
+        int64_t k = 0;
+        for (int64_t p : q.order) {
+            if (chg[p]) continue;
+            while (m < moved.size() && less(moved[m], p)) pl.order[k++] = moved[m++];
+            pl.order[k++] = p;
+        }
+        while (m < moved.size()) pl.order[k++] = moved[m++];
+    }
+    // the first sorted position that differs, or holds a point with new
+    // observations (a moved point may land where it was)
+    int64_t pos0 = 0;
+    while (pos0 < n_old && pl.order[pos0] == q.order[pos0] && !chg[pl.order[pos0]]) ++pos0;
+    pl.bounds = {0, P.n_pt};
+    tm.mark("order");
+    Seed sd{&q, pos0};
+    plan_points(P, pl, opts, &sd, tm);
+    build_reduce_plan(P, pl, tm);
+    PlanGrowState& gs = pl.grow;
+    gs.ok = true;
+    gs.span_lo = std::move(lo);
+    gs.span_hi = std::move(hi);
+    gs.used = std::move(used);
+    gs.lb = lb;
+    q.grow.ok = false;   // (its arrays are partly moved)
+    return true;
+}
+
+namespace {
+
+void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) {
+    const int world = pl.world;
     // ---- reduce plan -----------------------------------------------------------
     // Every matrix block (a, b), a >= b in F-block order (cameras, then
     // intrinsics), is a target summing its terms in a fixed order: sum terms
@@ -1346,7 +1708,67 @@ void build_plan(const sfm_ba_problem& P, int rank, int world, BAHostPlan& pl, co
     tm.mark("targets");
 }
 
+}  // namespace
+
 }  // namespace sfm
+
+namespace sfm {
+
+uint64_t plan_digest(const BAHostPlan& h, bool with_uv) {
+    uint64_t x = 1469598103934665603ull;
+    auto bytes = [&](const void* p, size_t n) {
+        const auto* b = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 1099511628211ull;
+    };
+    static const bool parts = std::getenv("SFM_PLAN_DIGEST") != nullptr;   // (diagnostic: per array)
+    int part = 0;
+    auto vec = [&](const auto& v) {   // (element types without padding)
+        const uint64_t n = v.size();
+        const uint64_t x0 = x;
+        x = 1469598103934665603ull;
+        bytes(&n, sizeof n);
+        if (n) bytes(v.data(), n * sizeof(v[0]));
+        if (parts) std::fprintf(stderr, "[digest] part %d n %llu -> %016llx\n", part, (unsigned long long)n,
+                                (unsigned long long)x);
+        const uint64_t xp = x;
+        x = x0;
+        bytes(&xp, sizeof xp);
+        ++part;
+    };
+    vec(h.targets); vec(h.zero_targets); vec(h.terms); vec(h.pterms); vec(h.chunks); vec(h.group_off);
+    vec(h.pt_off); vec(h.obs_img); vec(h.obs_slot); vec(h.gobs_perm);
+    vec(h.gblk_off); vec(h.gblk_col); vec(h.gblk_z); vec(h.gz_off); vec(h.zbatch); vec(h.zlong);
+    vec(h.spt_global); vec(h.img_obs_ptr); vec(h.gram_img);
+    vec(h.cam_blk); vec(h.intr_blk); vec(h.blk_img); vec(h.blk_intr); vec(h.img_colc); vec(h.img_coli);
+    if (with_uv) vec(h.obs_uv);
+    const int64_t sc[] = {h.n_img, h.n_intr, h.n_pt, h.n_obs, h.ncam, h.nintr, h.D, h.nb, h.na, h.nF, h.iw,
+                          h.nFB, h.dense, h.n_sdense, h.n_spt, h.n_sobs, h.n_cpt, h.n_gpt, h.gram_seg, h.n_z,
+                          h.gz_max, h.tile_nt, h.n_sband, h.n_sarrow, h.n_scorner, h.schur_flops, h.schur_bytes};
+    bytes(sc, sizeof sc);
+    return x;
+}
+
+}  // namespace sfm
+
+extern "C" int sfm_ba_grown_digest(const sfm_ba_problem* prev, const sfm_ba_problem* prob, uint64_t* digest_fresh,
+                                   uint64_t* digest_grown, int64_t* reused) {
+    using namespace sfm;
+    return guarded([&] {
+        SFM_REQUIRE(prev && prob && digest_fresh && digest_grown && reused, SFM_ERR_INVALID_ARG, "bad arguments");
+        BAHostPlan seed, grown, fresh;
+        build_plan(*prev, 0, 1, seed);
+        GrowPrev gp;
+        gp.n_img = prev->n_img; gp.n_intr = prev->n_intr; gp.const_img = prev->const_img; gp.model = prev->camera_model;
+        gp.n_pt = prev->n_pt; gp.n_obs = prev->n_obs;
+        gp.pt_offsets = prev->pt_offsets; gp.obs_img = prev->obs_img; gp.img_intr = prev->img_intr;
+        const bool ok = build_plan_grown(*prob, gp, seed, grown);
+        build_plan(*prob, 0, 1, fresh);
+        *digest_fresh = plan_digest(fresh, false);
+        *digest_grown = ok ? plan_digest(grown, false) : 0;
+        *reused = ok ? grown.reused_pts : -1;
+        return SFM_OK;
+    });
+}
 
 extern "C" int sfm_ba_intr_width(int32_t camera_model) {
     switch (camera_model) {

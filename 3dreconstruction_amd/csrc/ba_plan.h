@@ -10,6 +10,26 @@
 
 namespace sfm {
 
+// What a plan keeps so that the next call's plan, on a problem grown from this
+// one (sfm_ba_solve's plan cache: SequentialActuator's next BA call, one image
+// and its points added), can take its unchanged prefix instead of planning it
+// again (build_plan_grown).  World 1 only.
+struct PlanGrowState {
+    bool ok = false;                         // this plan can seed a grown one
+    std::vector<int32_t> span_lo, span_hi;   // every problem point's active camera span
+    std::vector<char> used;                  // observed images
+    int32_t lb = 0;                          // longest track, in distinct active cameras, minus one
+    std::vector<char> ck;                    // chunkable flag per sorted position
+    int64_t n_ck = 0;                        // classified chunkable points (n_cpt unless the chunking was dropped)
+    int64_t rlen = 0;                        // chunking range length (points)
+    int chunk_pts = 0;
+    int cap = 0;                             // tile rows of the kept one-height chunking (0: none)
+    std::vector<int32_t> seg_nch;            // its chunks per range
+    std::vector<int64_t> seg_flops;          // its algorithmic flops per range
+    std::vector<int32_t> seg_own, seg_obs;   // per range: largest tile rows / observations of a point
+    std::vector<int64_t> gflops;             // algorithmic flops per general point
+};
+
 struct BAHostPlan {
     // ---- global (identical on every rank) ---------------------------------
     int32_t n_img = 0, n_intr = 0;
@@ -82,6 +102,22 @@ struct BAHostPlan {
     // (their upload then overlaps the rest of the planning)
     std::function<void(BAHostPlan&)> on_shard_ready;
     int64_t schur_bytes = 0;    // algorithmic HBM bytes of one Schur pass
+    // obs_uv is left empty (grown plans): the caller gathers the measurements
+    // into shard order on the device (ba_obs_source, ba_gather_uv)
+    bool uv_on_device = false;
+    // grown plans: the sorted positions taken over from the seed plan unchanged
+    // (diagnostics, tests)
+    int64_t reused_pts = 0;
+    PlanGrowState grow;
+};
+
+// The previous problem's structure (the plan cache's key of sfm_ba_solve).
+struct GrowPrev {
+    int32_t n_img = 0, n_intr = 0, const_img = 0, model = 0;
+    int64_t n_pt = 0, n_obs = 0;
+    const int64_t* pt_offsets = nullptr;
+    const int32_t* obs_img = nullptr;
+    const int32_t* img_intr = nullptr;
 };
 
 // Engine choices the planner takes from the context (SFM_CTX_BA_*): the
@@ -93,6 +129,24 @@ struct PlanOpts {
 
 // Validates the problem and fills every field.  Throws SfmError.
 void build_plan(const sfm_ba_problem& prob, int rank, int world, BAHostPlan& plan, const PlanOpts& opts = {});
+
+// The plan of `prob` when it grows `prev` (the problem `seed` was built for):
+// the same images, intrinsics map and gauge with images, points and
+// observations appended only (every point keeps its observations, in order,
+// and may gain new ones at the end).  The sorted points before the first one
+// the growth moves keep their classification, shard arrays, chunks (whole
+// chunking ranges) and general-point blocks, taken from `seed`; the rest and
+// the reduce plan are planned as build_plan plans them, so the result equals
+// build_plan(prob, 0, 1, ...) array for array (tests: sfm_ba_grown_digest).
+// World 1.  The measurements are not gathered on the host (uv_on_device).
+// Returns false, with `seed` untouched, when prob does not grow prev or seed
+// cannot seed it (then build_plan).  `seed` is consumed otherwise.  Throws
+// SfmError.
+bool build_plan_grown(const sfm_ba_problem& prob, const GrowPrev& prev, BAHostPlan& seed, BAHostPlan& plan,
+                      const PlanOpts& opts = {});
+
+// FNV-1a digest of every plan array the device uses (diagnostics, tests)
+uint64_t plan_digest(const BAHostPlan& h, bool with_uv);
 
 // Every point's active camera span [lo, hi) under a camera order ((ncam, 0):
 // no active camera): the partition's sort keys.
@@ -110,7 +164,8 @@ void partition_points(const sfm_ba_problem& prob, const std::vector<int32_t>& ca
 // spans / used_out (optional): every point's span under the returned order,
 // and the observed-image flags, from the same passes.
 std::vector<int32_t> camera_blocks(const sfm_ba_problem& prob, int32_t* ncam_out, int32_t* D_out,
-                                   PointSpans* spans = nullptr, std::vector<char>* used_out = nullptr);
+                                   PointSpans* spans = nullptr, std::vector<char>* used_out = nullptr,
+                                   int32_t* lb_out = nullptr, bool* rcm_out = nullptr);
 
 // Largest camera half-bandwidth the block-cyclic-reduction solver takes.
 constexpr int kBandMaxD = 10;

@@ -126,8 +126,20 @@ void up(Staging& st, DBuf<T>& d, const std::vector<T, A>& h, hipStream_t s) {
     if (!h.empty()) d.upload(st.put(h.data(), h.size()), h.size(), s);
 }
 
-void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr, const double* intr,
-                 const double* X) {
+// the plan cache of sfm_ba_solve grows plans (SFM_BA_NO_PLAN_CACHE: no
+// cache, nothing kept for it; SFM_BA_NO_GROWN_PLAN: exact reuse only)
+bool cache_enabled_for_growth() {
+    static const bool on = std::getenv("SFM_BA_NO_PLAN_CACHE") == nullptr && std::getenv("SFM_BA_NO_GROWN_PLAN") == nullptr;
+    return on;
+}
+
+// The plan of a problem: from scratch, or -- seed set (sfm_ba_solve's plan
+// cache, a problem grown from the previous call's, GrowPrev) -- grown from
+// the seed plan (build_plan_grown: the same arrays; the measurements are
+// gathered into shard order on the device).  Returns false, with nothing
+// done and the seed intact, when the seed cannot seed this problem.
+bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr, const double* intr,
+                 const double* X, sfm_ba_plan* seed = nullptr, const GrowPrev* prev = nullptr) {
     sfm_ctx* ctx = pl->ctx;
     hipStream_t s = ctx->stream;
     BAHostPlan& h = pl->hp;
@@ -136,14 +148,40 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         up(pl->pt_off, hp.pt_off, s);
         up(pl->obs_img, hp.obs_img, s);
         up(pl->obs_slot, hp.obs_slot, s);
-        up(pl->obs_uv, hp.obs_uv, s);
+        if (!hp.uv_on_device) up(pl->obs_uv, hp.obs_uv, s);
     };
     PlanOpts po;
     po.force_dense = (ctx->flags & SFM_CTX_BA_DENSE_RCS) != 0;
     po.tile80 = (ctx->flags & SFM_CTX_BA_TILE80) != 0;
-    build_plan(prob, ctx->rank, ctx->world, h, po);
+    if (seed) {
+        if (!build_plan_grown(prob, *prev, seed->hp, h, po)) {
+            h.on_shard_ready = nullptr;
+            return false;
+        }
+    } else {
+        build_plan(prob, ctx->rank, ctx->world, h, po);
+    }
     h.on_shard_ready = nullptr;
-    tm.mark("build_plan");
+    tm.mark(seed ? "build_plan_grown" : "build_plan");
+    if (h.uv_on_device && h.n_sobs > 0) {
+        // the measurements into shard order on the device, through the
+        // shard -> problem maps the plan cache's refresh uses too
+        std::vector<int32_t> ps(h.n_spt);
+        for (int64_t k = 0; k < h.n_spt; ++k) ps[k] = (int32_t)h.spt_global[k];
+        up(pl->pt_src, ps, s);
+        pl->src_off.alloc(prob.n_pt + 1);
+        pl->src_off.upload(prob.pt_offsets, prob.n_pt + 1, s);
+        pl->obs_src.alloc(h.n_sobs);
+        DBuf<int32_t> gperm;   // back to the context's cache, stream-ordered
+        if (!h.gobs_perm.empty()) up(gperm, h.gobs_perm, s);
+        ba_obs_source(pl->pt_src.p, pl->src_off.p, pl->pt_off.p, (int32_t)h.n_spt, (int32_t)h.n_cpt,
+                      h.gobs_perm.empty() ? nullptr : gperm.p, pl->obs_src.p, s);
+        pl->raw_uv.alloc(2 * (size_t)prob.n_obs);
+        SFM_HIP(hipMemcpyAsync(pl->raw_uv.p, prob.obs_uv, 2 * (size_t)prob.n_obs * 8, hipMemcpyHostToDevice, s));
+        pl->obs_uv.alloc(2 * (size_t)h.n_sobs);
+        ba_gather_uv(pl->obs_src.p, pl->raw_uv.p, (int32_t)h.n_sobs, pl->obs_uv.p, s);
+        tm.mark("gather_uv");
+    }
     Staging st;
     up(st, pl->chunks, h.chunks, s);
     up(st, pl->group_off, h.group_off, s);
@@ -423,13 +461,19 @@ void create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     if (std::getenv("SFM_SCHUR_STAMPS")) pl->stamps.alloc(6 * std::max<size_t>(h.chunks.size(), 1));
     tm.mark("alloc+upload");
     SFM_HIP(hipStreamSynchronize(s));
-    // the observation staging goes back to the cache (the uploads are done)
-    h.obs_img = HostVec<int32_t>();
-    h.obs_slot = HostVec<int32_t>();
+    // the observation staging goes back to the cache (the uploads are done);
+    // a plan that can seed a grown one keeps its shard arrays (obs_img,
+    // obs_slot: build_plan_grown takes their unchanged prefix)
+    if (!(h.grow.ok && cache_enabled_for_growth())) {
+        h.obs_img = HostVec<int32_t>();
+        h.obs_slot = HostVec<int32_t>();
+        h.grow = PlanGrowState();
+    }
     h.obs_uv = HostVec<double>();
     h.pterms = HostVec<PTerm>();
     h.terms = HostVec<FlatTerm>();
     tm.mark("sync");
+    return true;
 }
 
 // New values for a plan whose problem structure is unchanged (the plan
@@ -973,6 +1017,16 @@ void sfm::ba_cache_release(sfm_ctx* ctx) {
     if (sfm_ba_plan* pl = cache_take(ctx, &k)) sfm_ba_plan_destroy(pl);
 }
 
+extern "C" int sfm_ba_cache_stats(sfm_ctx* ctx, int64_t* reused, int64_t* grown, int64_t* fresh) {
+    return guarded([&] {
+        SFM_REQUIRE(ctx, SFM_ERR_INVALID_ARG, "null ctx");
+        if (reused) *reused = ctx->plans_reused;
+        if (grown) *grown = ctx->plans_grown;
+        if (fresh) *fresh = ctx->plans_fresh;
+        return SFM_OK;
+    });
+}
+
 extern "C" int sfm_ba_cache_clear(sfm_ctx* ctx) {
     return guarded([&] {
         SFM_REQUIRE(ctx, SFM_ERR_INVALID_ARG, "null ctx");
@@ -991,12 +1045,13 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* ex
     sfm_ba_plan* pl = nullptr;
     PlanKey key;
     bool hit = false;
+    sfm_ba_plan* seed_pl = nullptr;   // a cached plan of another structure (a grown problem's seed?)
     if (cache_enabled()) {
         pl = cache_take(ctx, &key);
         if (pl) {
             hit = key.matches(*prob);
             if (!hit) {
-                sfm_ba_plan_destroy(pl);
+                seed_pl = pl;
                 pl = nullptr;
             }
         }
@@ -1010,14 +1065,48 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* ex
             return SFM_OK;
         });
         tm.mark("refresh");
+        ++ctx->plans_reused;
         if (rc != SFM_OK) {
             sfm_ba_plan_destroy(pl);
             return rc;
         }
     } else {
-        rc = sfm_ba_plan_create(ctx, prob, extr, intr, X, &pl);
-        tm.mark("create");
+        // a problem grown from the cached plan's (the next BundleAdjuster call
+        // of SequentialActuator, SequentialActuator.h:226-229): the cached
+        // plan seeds the new one (build_plan_grown), else a fresh plan
+        sfm_ba_plan* grown = nullptr;
+        if (seed_pl && cache_enabled_for_growth()) {
+            GrowPrev gp;
+            gp.n_img = key.n_img; gp.n_intr = key.n_intr; gp.const_img = key.const_img; gp.model = key.model;
+            gp.n_pt = key.n_pt; gp.n_obs = key.n_obs;
+            gp.pt_offsets = key.pt_offsets.data(); gp.obs_img = key.obs_img.data(); gp.img_intr = key.img_intr.data();
+            rc = guarded([&] {
+                CtxScope scope_(ctx);
+                (void)hipStreamSynchronize(ctx->stream);   // the seed's last solve has finished with its buffers
+                auto* np = new sfm_ba_plan;
+                np->ctx = ctx;
+                try {
+                    if (create_plan(np, *prob, extr, intr, X, seed_pl, &gp)) grown = np;
+                    else delete np;
+                } catch (...) {
+                    delete np;
+                    throw;
+                }
+                return SFM_OK;
+            });
+            tm.mark(grown ? "grown" : "not_grown");
+        }
+        if (seed_pl) sfm_ba_plan_destroy(seed_pl);
         if (rc != SFM_OK) return rc;
+        if (grown) {
+            pl = grown;
+            ++ctx->plans_grown;
+        } else {
+            rc = sfm_ba_plan_create(ctx, prob, extr, intr, X, &pl);
+            tm.mark("create");
+            if (rc != SFM_OK) return rc;
+            ++ctx->plans_fresh;
+        }
         if (cache_enabled()) key.assign(*prob);
     }
     rc = sfm_ba_plan_run(pl, opts, sum);

@@ -231,6 +231,9 @@ struct sfm_ctx {
     }
     hipEvent_t ev[2] = {nullptr, nullptr};       // timing events, created on first use
     double last_kernel_ms = -1.0;                // sfm_fmatrix_ac's kernel (sfm_ctx_last_kernel_ms)
+    // sfm_ba_solve's plan cache: plans reused as they were / grown from the
+    // cached one / built from scratch (sfm_ba_cache_stats)
+    int64_t plans_reused = 0, plans_grown = 0, plans_fresh = 0;
 };
 
 namespace sfm {

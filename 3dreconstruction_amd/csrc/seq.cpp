@@ -32,7 +32,8 @@ struct CtxMatcher {
     }
 };
 
-// SFM_SEQ_DUMP=<dir> (diagnostic): every 100th solve's problem is written to
+// SFM_SEQ_DUMP=<dir> (diagnostic): every 100th solve's problem, and the one
+// after it (a consecutive pair: the grown-structure relation), is written to
 // <dir>/ba_<call>.bin (int64 n_img n_intr n_pt n_obs const_img, then
 // pt_offsets, obs_img, obs_uv, img_intr) for replaying the planner offline
 void dump_problem(const sfm_ba_problem& pr) {
@@ -40,7 +41,7 @@ void dump_problem(const sfm_ba_problem& pr) {
     static std::atomic<int> calls{0};   // sequences may solve on several threads
     if (!dir) return;
     const int call = calls.fetch_add(1);
-    if (call % 100 != 99) return;
+    if (call % 100 != 99 && !(call >= 100 && call % 100 == 0)) return;
     char path[512];
     std::snprintf(path, sizeof path, "%s/ba_%03d.bin", dir, call);
     FILE* f = std::fopen(path, "wb");

@@ -116,11 +116,17 @@ class BasicBundleAdjuster {
             img_cam_.push_back(-1);
             return k;
         };
-        for (auto& f : world->local_frames_) {
-            const int k = add_img(f->getImage2(), false);
-            img_cam_[k] = add_cam(f->getImage2()->getCamera(), false);
-        }
-        const_img_ = world->local_frames_.empty() ? -1 : 0;
+        // Images are numbered in creation order (Image::getIdx(), the photo
+        // order of the sequence), the poses of the local frames' second images
+        // copied and every other observed image's pose block zero (:85-98,
+        // :118-119).  Ceres orders parameter blocks itself, so the numbering
+        // is free; creation order makes each call's problem an extension of
+        // the previous call's (a new image, new points and new observations
+        // appended, nothing renumbered), which the plan cache of sfm_ba_solve
+        // reuses ("Grown problems"), and keeps the orbit's
+        // cameras in band order.  (Until round 5 the local frames came first
+        // and the sequence's first photo last.)
+        std::vector<std::pair<Image::Ptr, bool>> imgs;   // (image, pose copied)
         // points in index order (the reference iterates its unordered_map).
         // The walk over the world is a pointer chase (every point and its
         // observation list are separate heap blocks), so it runs on host
@@ -168,11 +174,22 @@ class BasicBundleAdjuster {
         for (std::size_t k = 0; k < np; ++k) off_[k + 1] += off_[k];
         // image_extrinsic_[image] / camera_intrinsics_[camera] are operator[]:
         // unseen blocks are inserted as zeros (:118-119)
+        for (auto& f : world->local_frames_) imgs.push_back({f->getImage2(), true});
         for (const auto& f : first)
-            for (const Image::Ptr* im : f) {
-                const int k = add_img(*im, true);
-                if (img_cam_[k] < 0) img_cam_[k] = add_cam((*im)->getCamera(), true);
-            }
+            for (const Image::Ptr* im : f) imgs.push_back({*im, false});
+        // a camera keeps its intrinsics when any local frame's image uses it
+        // (loaded first, :85-98); only cameras of other images are zero blocks
+        for (auto& f : world->local_frames_) add_cam(f->getImage2()->getCamera(), false);
+        std::stable_sort(imgs.begin(), imgs.end(),
+                         [](const auto& a, const auto& b) { return a.first->getIdx() < b.first->getIdx(); });
+        for (const auto& e : imgs) {
+            const Image::Ptr& im = e.first;
+            const std::size_t id = im->getIdx();
+            if (id < img_slot_.size() && img_slot_[id] >= 0) continue;   // (a local frame's image, also observed)
+            const int k = add_img(im, !e.second);
+            img_cam_[k] = add_cam(im->getCamera(), true);
+        }
+        const_img_ = world->local_frames_.empty() ? -1 : img_slot_[world->local_frames_.front()->getImage2()->getIdx()];
         const int64_t nobs = off_[np];
         obs_img_.resize(nobs);
         uv_.resize(2 * nobs);

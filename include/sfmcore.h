@@ -262,10 +262,19 @@ int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob,
  * has the same structure (n_*, pt_offsets, obs_img, img_intr, const_img,
  * camera_model -- compared exactly) reuses it and only uploads the new values
  * (a world that did not grow since the previous BundleAdjuster call,
- * SequentialActuator.h:226-229).  This releases that plan (its device
- * memory); sfm_ctx_destroy does too.  SFM_BA_NO_PLAN_CACHE=1 turns the cache
- * off. */
+ * SequentialActuator.h:226-229).  A call whose problem grows the cached one
+ * (the same images, intrinsics map, gauge and model, with images, points and
+ * observations only appended: every point keeps its observations in order
+ * and may gain new ones at the end -- the next call of the incremental loop,
+ * SequentialActuator.h:226-229 after addSingleImage, main.cpp:99-108) plans
+ * only what the growth moved and takes the rest from the cached plan, with
+ * the same result as a fresh plan bit for bit (world 1).  This releases that
+ * plan (its device memory); sfm_ctx_destroy does too.  SFM_BA_NO_PLAN_CACHE=1
+ * turns the cache off, SFM_BA_NO_GROWN_PLAN=1 the growth only. */
 int sfm_ba_cache_clear(sfm_ctx* ctx);
+/* [diagnostic] sfm_ba_solve calls on this context that reused the cached plan
+ * as it was, grew it, or planned from scratch. */
+int sfm_ba_cache_stats(sfm_ctx* ctx, int64_t* reused, int64_t* grown, int64_t* fresh);
 
 /* Resident variant (used by the benchmark): the plan uploads the problem and
  * the initial parameters once; every sfm_ba_plan_run restarts from those
@@ -316,6 +325,18 @@ typedef struct sfm_ba_plan_shape {
     int64_t n_chunk_pts, n_general_pts, rcs_dim, n_targets, n_terms, n_pterms;
 } sfm_ba_plan_shape;
 int sfm_ba_describe(const sfm_ba_problem* prob, int32_t rank, int32_t world_size, sfm_ba_plan_shape* out);
+
+/* [cpu] Diagnostic (tests): plans `prob` twice -- from scratch, and grown
+ * from the plan of `prev` (sfm_ba_solve's path when a problem extends the
+ * previous call's: SequentialActuator::bundleAdjustment after
+ * addSingleImage, src/actuator/SequentialActuator.h:226-229) -- and returns
+ * the FNV-1a digest of every plan array the device reads in each (the
+ * measurements excluded: a grown plan gathers them on the device).
+ * *reused = the sorted points the grown plan took over from prev's plan, -1
+ * when prob does not grow prev or prev's plan cannot seed it (digest_grown
+ * then 0). */
+int sfm_ba_grown_digest(const sfm_ba_problem* prev, const sfm_ba_problem* prob, uint64_t* digest_fresh,
+                        uint64_t* digest_grown, int64_t* reused);
 
 /* [cpu] Landmark-block partition: contiguous point ranges of the
  * (min-camera)-sorted point order with ~equal observation counts.
