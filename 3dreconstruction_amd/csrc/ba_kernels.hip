@@ -2200,8 +2200,8 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
     // batch's Z loads, so a batch waits for one memory latency, not two)
     // (two scalars, not a PTerm: the struct was promoted to LDS, and its
     // store there waited for the load it was meant to prefetch)
-    const longlong2* pt2 = reinterpret_cast<const longlong2*>(P.pterms);
-    longlong2 nxt = make_longlong2(0, 0);
+    const int2* pt2 = reinterpret_cast<const int2*>(P.pterms);
+    int2 nxt = make_int2(0, 0);
     if (lane < min(kPtB, qb - qa)) nxt = pt2[qa + lane];
     for (int q0 = qa; q0 < qb; q0 += kPtB) {
         const int nb = min(kPtB, qb - q0);
@@ -2217,7 +2217,7 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
             // unconditional load (clamped index; Z is not empty when there
             // are terms): a conditional one left a 0.0 default whose
             // register write waited for the previous batch's loads
-            const int64_t off = isa ? Lt[t].za : Lt[t].zb;
+            const int32_t off = isa ? Lt[t].za : Lt[t].zb;
             v[t] = Z[(lane < L && t < nb) ? off + oo : 0];
         }
 #pragma unroll

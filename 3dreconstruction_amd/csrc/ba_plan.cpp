@@ -445,12 +445,15 @@ int chunk_pts_for(int64_t n_cpt) {
     return (int)std::max<int64_t>(16, std::min<int64_t>(kChunkPts, (n_cpt + kTargetChunks - 1) / kTargetChunks));
 }
 // Chunk points are chunked in fixed-length ranges on host threads (a chunk
-// never spans two ranges: at most 15 extra chunks out of thousands): 4096
-// points, doubled until there are at most 16 ranges.  The ranges depend on
-// the number of chunk points only, so a grown problem's chunking keeps every
-// whole range before its first moved point (round 6; until round 5 the
-// shard was cut into up to 16 equal parts).
+// never spans two ranges): up to 65536 chunk points, ranges of 1024 (at most
+// 63 extra chunks, against the ~1850 such a shard gets); above, 4096 points
+// doubled until there are at most 16 ranges (at most 15 extra chunks out of
+// thousands).  The ranges depend on the number of chunk points only, so a
+// grown problem's chunking keeps every whole range before its first moved
+// point and re-chunks about one range more than the growth moved (round 6;
+// until round 5 the shard was cut into up to 16 equal parts).
 int64_t chunk_range_len(int64_t ncp) {
+    if (ncp <= 64 * 1024) return 1024;
     int64_t r = 4096;
     while (ncp > 16 * r) r *= 2;
     return r;
@@ -460,6 +463,14 @@ int64_t chunk_range_len(int64_t ncp) {
 // observation) and the point block (V, its factor, M = Jx L^-T, Z = J' M: 180
 // per observation + 30)
 int64_t point_flops(int64_t rows, int64_t nobs) { return 3 * rows * (rows + 1) + 780 * nobs + 30; }
+
+// resize an array a grown plan took over from its seed, with room for the
+// next calls' growth (a reallocation copies the whole array)
+template <class V>
+void grow_to(V& v, size_t n) {
+    if (v.capacity() < n) v.reserve(n + n / 4);
+    v.resize(n);
+}
 
 // A chunking is abandoned as soon as its chunk count (over all ranges)
 // passes abort_at: from there on its outcome no longer matters (see the
@@ -725,7 +736,7 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
     }
     // the chunk part before kc0 is the seed's, as it stands
     const int64_t s_keep = q ? pl.pt_off[kc0] : 0;
-    pl.obs_img.resize(pl.n_sobs);
+    grow_to(pl.obs_img, pl.n_sobs);
     if (!pl.uv_on_device) pl.obs_uv.resize(2 * pl.n_sobs);
     auto copy_obs = [&](int64_t k_lo, int64_t k_hi) {   // shard points [k_lo, k_hi) from the problem
         parallel_ranges(k_hi - k_lo, [&](int64_t a0, int64_t a1, int) {
@@ -789,6 +800,7 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
         }
     };
     pl.chunks.clear();
+    int64_t reused_chunks = 0;   // the seed's chunks at the head of pl.chunks
     // the 64-row kernel walks batches of at most schur4_obs observations
     if (both) {
         // both tile heights are planned (each over the host threads); the
@@ -830,8 +842,9 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
             seg_nch.assign(q->grow.seg_nch.begin(), q->grow.seg_nch.begin() + g0);
             seg_fl.assign(q->grow.seg_flops.begin(), q->grow.seg_flops.begin() + g0);
             cslot = std::move(pl.obs_slot);   // the seed's slots of those ranges, in place
+            reused_chunks = prefix;
         }
-        cslot.resize(pl.pt_off[ncp]);
+        grow_to(cslot, pl.pt_off[ncp]);
         Chunking c5;
         kept = make_chunks(P, pl, kTileRowsUsed, chunk_pts, rlen, ncp, g0, prefix, keep_max, c5, cslot.data());
         if (kept) {
@@ -840,6 +853,7 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
         }
     }
     for (int64_t f : seg_fl) flops += f;
+    pl.reused_chunks = kept ? reused_chunks : 0;
     if (!kept || (pl.n_cpt > 0 && (int64_t)pl.chunks.size() * 4 > pl.n_cpt)) {
         pl.chunks.clear();
         cslot.clear();
@@ -855,7 +869,7 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
     pl.group_off.push_back((int32_t)pl.chunks.size());
     tm.mark("chunks");
     // the chunk points' slots are final; the general points' are written below
-    cslot.resize(pl.n_sobs);
+    grow_to(cslot, pl.n_sobs);
     pl.obs_slot.swap(cslot);
     pl.n_gpt = pl.n_spt - pl.n_cpt;
 
@@ -938,8 +952,8 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
         for (int32_t a = 0; a < pl.gblk_off[gk0]; ++a)
             if (pl.gblk_col[a] >= q->nb) pl.gblk_col[a] += shift;
     }
-    pl.gblk_off.resize(pl.n_gpt + 1);
-    pl.gz_off.resize(pl.n_gpt + 1);
+    grow_to(pl.gblk_off, pl.n_gpt + 1);
+    grow_to(pl.gz_off, pl.n_gpt + 1);
     pl.gblk_off[0] = 0;
     pl.gz_off[0] = 0;
     pl.gz_max = 0;
@@ -983,8 +997,8 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
             pl.gblk_off[g + 1] = pl.gblk_off[g] + nblk[g - gk0];
             pl.gz_off[g + 1] = pl.gz_off[g] + nz[g - gk0];
         }
-        pl.gblk_col.resize(pl.gblk_off[pl.n_gpt]);
-        pl.gblk_z.resize(pl.gblk_off[pl.n_gpt]);
+        grow_to(pl.gblk_col, pl.gblk_off[pl.n_gpt]);
+        grow_to(pl.gblk_z, pl.gblk_off[pl.n_gpt]);
         parallel_ranges(pl.n_gpt - gk0, [&](int64_t a0, int64_t a1, int) {
             std::vector<int32_t> cols;
             for (int64_t g = gk0 + a0; g < gk0 + a1; ++g) {
@@ -1009,6 +1023,8 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
         });
         for (int64_t f : gflops) flops += f;
         pl.n_z = pl.gz_off[pl.n_gpt];
+        SFM_REQUIRE(pl.n_z < INT32_MAX, SFM_ERR_UNSUPPORTED, "general points' Z buffer of %lld doubles",
+                    (long long)pl.n_z);
         // Z kernel work: batches of consecutive short points, the rest alone
         pl.zbatch.clear();
         pl.zlong.clear();
@@ -1034,6 +1050,8 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
     }
     tm.mark("general");
     pl.reused_pts = pos0;
+    pl.reused_gpts = gk0;
+    if (pl.n_cpt == 0) pl.reused_chunks = 0;
     // what the next grown plan takes (world 1)
     PlanGrowState& gs = pl.grow;
     gs.ck = std::move(ck);
@@ -1085,7 +1103,7 @@ void plan_points(const sfm_ba_problem& P, BAHostPlan& pl, const PlanOpts& opts, 
     tm.mark("image_csr");
 }
 
-void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm);
+void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm, BAHostPlan* seed = nullptr);
 
 }  // namespace
 
@@ -1241,7 +1259,7 @@ bool build_plan_grown(const sfm_ba_problem& P, const GrowPrev& prev, BAHostPlan&
     tm.mark("order");
     Seed sd{&q, pos0};
     plan_points(P, pl, opts, &sd, tm);
-    build_reduce_plan(P, pl, tm);
+    build_reduce_plan(P, pl, tm, &q);
     PlanGrowState& gs = pl.grow;
     gs.ok = true;
     gs.span_lo = std::move(lo);
@@ -1254,7 +1272,7 @@ bool build_plan_grown(const sfm_ba_problem& P, const GrowPrev& prev, BAHostPlan&
 
 namespace {
 
-void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) {
+void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm, BAHostPlan* seed) {
     const int world = pl.world;
     // ---- reduce plan -----------------------------------------------------------
     // Every matrix block (a, b), a >= b in F-block order (cameras, then
@@ -1452,8 +1470,54 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
     const int64_t n_terms = n_mc + n_vc + 2 * n_vb, n_pterms = n_mp + n_vp;
     SFM_REQUIRE(n_terms < INT32_MAX && n_pterms < INT32_MAX, SFM_ERR_UNSUPPORTED,
                 "reduce plan of %lld sum / %lld product terms", (long long)n_terms, (long long)n_pterms);
-    pl.terms.resize(n_terms);
-    pl.pterms.resize(n_pterms);
+    // A grown plan (seed): the matrix rows before f0 -- the first F-block row
+    // a re-planned chunk or general point writes, or a new camera's -- are the
+    // seed's, targets and terms alike (the same sources in the same order), in
+    // place; only their image-slice offsets (behind the tiles in the source
+    // buffer, whose count changed) and dense destinations (the RCS grew) move.
+    int32_t f0 = 0;
+    int64_t t_keep = 0;   // the seed's targets kept
+    if (seed && seed->row_tgt.size() == (size_t)seed->nFB + 1 && seed->dense == pl.dense && seed->D == D &&
+        seed->gram_seg == pl.gram_seg && seed->iw == pl.iw && seed->nintr == nintr && world == 1) {
+        int32_t f = std::min(seed->ncam, ncam);
+        for (int32_t c = 0; c < ngrp; ++c)
+            if (pl.group_off[c] >= pl.reused_chunks) f = std::min(f, g_lo[c]);
+        for (int64_t g = pl.reused_gpts; g < pl.n_gpt; ++g) f = std::min(f, p_lo[g]);
+        if (f > 0 && f <= seed->nFB) {
+            t_keep = seed->row_tgt[f];
+            const bool tail = t_keep < (int64_t)seed->targets.size();
+            if (tail && seed->targets[t_keep].c_begin == BS(kMc, f) && seed->targets[t_keep].p_begin == BS(kMp, f) &&
+                (int64_t)seed->terms.size() >= BS(kMc, f) && (int64_t)seed->pterms.size() >= BS(kMp, f))
+                f0 = f;
+        }
+    }
+    if (f0 > 0) {
+        BAHostPlan& q = *seed;
+        pl.terms = std::move(q.terms);
+        pl.pterms = std::move(q.pterms);
+        pl.targets = std::move(q.targets);
+        pl.targets.resize(t_keep);
+        const int64_t q_u = std::max<int64_t>(q.n_group(), 1) * kTileR * kTileR,
+                      q_ub = q_u + fw * fw * q.n_img * kGramSeg, q_ucn = q_ub + fw * q.n_img * kGramSeg;
+        const int64_t du = o_u - q_u, dub = o_ub - q_ub, ducn = o_ucn - q_ucn;
+        FlatTerm* T = pl.terms.data();
+        parallel_ranges(BS(kMc, f0), [&](int64_t a0, int64_t a1, int) {
+            for (int64_t k = a0; k < a1; ++k) {
+                const int64_t o = T[k].off;
+                T[k].off = o + (o >= q_ucn ? ducn : o >= q_ub ? dub : o >= q_u ? du : 0);
+            }
+        });
+        if (!band)
+            for (ReduceTarget& t : pl.targets) {   // camera rows: (fa, fb) columns unchanged, the row stride grew
+                const int64_t ca = t.dst / q.nF, cb = t.dst % q.nF;
+                t.dst = ca * pl.nF + cb;
+                t.ld = (int32_t)pl.nF;
+            }
+    } else {
+        pl.targets.clear();
+    }
+    grow_to(pl.terms, n_terms);
+    grow_to(pl.pterms, n_pterms);
     tm.mark("terms_count");
 
     // ---- targets and terms, by row ranges ----------------------------------
@@ -1500,24 +1564,28 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
         return t;
     };
     // row ranges of about equal work (terms, plus the row's targets)
-    std::vector<int32_t> cut{0};
-    {
+    // (matrix rows f0.. here; every row's vector terms below)
+    auto row_cuts = [&](int32_t fa0, bool matrix) {
+        std::vector<int32_t> cut{fa0};
         int64_t tot = 0;
         std::vector<int64_t> w(nFB);
-        for (int32_t f = 0; f < nFB; ++f) {
-            w[f] = RC(kMc, f) + RC(kMp, f) + RC(kVc, f) + RC(kVp, f) + 2 * RC(kVb, f) + row_slots(f);
+        for (int32_t f = fa0; f < nFB; ++f) {
+            w[f] = matrix ? RC(kMc, f) + RC(kMp, f) + row_slots(f) : RC(kVc, f) + RC(kVp, f) + 2 * RC(kVb, f);
             tot += w[f];
         }
-        const int nt = tot < 65536 ? 1 : std::min<int>(PlanPool::width(), std::max(1, nFB));
+        const int nt = tot < 65536 ? 1 : std::min<int>(PlanPool::width(), std::max(1, nFB - fa0));
         int64_t acc = 0;
-        for (int32_t f = 0; f < nFB; ++f) {
+        for (int32_t f = fa0; f < nFB; ++f) {
             acc += w[f];
             if ((int)cut.size() < nt && acc * nt >= (int64_t)cut.size() * tot && f + 1 < nFB) cut.push_back(f + 1);
         }
         cut.push_back(nFB);
-    }
+        return cut;
+    };
+    const std::vector<int32_t> cut = row_cuts(f0, true);
     const int nseg = (int)cut.size() - 1;
     std::vector<std::vector<ReduceTarget>> seg_targets(nseg);
+    std::vector<std::vector<int32_t>> seg_rows(nseg);   // each row's first target within its segment
     std::vector<int> seg_rc(nseg, SFM_OK);
     parallel_segments(nseg, [&](int sg) {
         seg_rc[sg] = guarded([&] {
@@ -1569,9 +1637,10 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
             }
             // (2) targets in slot order; the counts become write cursors
             auto& tg = seg_targets[sg];
+            seg_rows[sg].resize(r1 - r0);
             int64_t c_at = BS(kMc, r0), p_at = BS(kMp, r0);
             for (int32_t f = r0; f < r1; ++f)
-                for (int64_t s = 0; s < row_slots(f); ++s) {
+                for (int64_t s = (seg_rows[sg][f - r0] = (int32_t)tg.size(), 0); s < row_slots(f); ++s) {
                     const int64_t q = sbase[f - r0] + s;
                     const int64_t nc = cs[q], np = ps[q];
                     cs[q] = c_at;
@@ -1601,31 +1670,13 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
                     PT[ps[q - 1]++] = r;
                 }
             };
-            // vector cursors of this range's rows: rhs sum / product, bF, cnF
-            std::vector<int64_t> vcur(4 * (size_t)(r1 - r0));
-            for (int32_t f = r0; f < r1; ++f) {
-                vcur[4 * (f - r0) + 0] = n_mc + BS(kVc, f);
-                vcur[4 * (f - r0) + 1] = n_mp + BS(kVp, f);
-                vcur[4 * (f - r0) + 2] = n_mc + n_vc + BS(kVb, f);
-                vcur[4 * (f - r0) + 3] = n_mc + n_vc + n_vb + BS(kVb, f);
-            }
-            auto put_v = [&](int32_t f, int16_t ro, int32_t idx) {
-                int64_t* v = &vcur[4 * (f - r0)];
-                T[v[0]++] = flat(ReduceTerm{kSrcUb, idx, ro, 0, 1.f}, true);
-                T[v[2]++] = flat(ReduceTerm{kSrcUb, idx, ro, 0, 1.f}, true);
-                T[v[3]++] = flat(ReduceTerm{kSrcUcn, idx, ro, 0, 1.f}, true);
-            };
             for (const ImgSrc& s : isrc)
                 for (int g = 0; g < gseg; ++g) {
                     const int32_t idx = s.img * gseg + g;
-                    if (s.cb >= 0 && in(s.cb)) {
-                        put(S(s.cb, s.cb), false, ReduceTerm{kSrcU, idx, 0, 0, 1.f});
-                        put_v(s.cb, 0, idx);
-                    }
+                    if (s.cb >= 0 && in(s.cb)) put(S(s.cb, s.cb), false, ReduceTerm{kSrcU, idx, 0, 0, 1.f});
                     if (s.fq >= 0 && in(s.fq)) {
                         if (s.cb >= 0) put(S(s.fq, s.cb), false, ReduceTerm{kSrcU, idx, 6, 0, 1.f});
                         put(S(s.fq, s.fq), false, ReduceTerm{kSrcU, idx, 6, 6, 1.f});
-                        put_v(s.fq, 6, idx);
                     }
                 }
             for (int32_t c = 0; c < ngrp; ++c) {
@@ -1634,8 +1685,6 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
                 for (int a = 0; a < cd.n_slots; ++a) {
                     const int32_t fa = gfb[(size_t)c * kMaxSlots + a];
                     if (!in(fa)) continue;
-                    // rhs contribution (-Z w) from tile row 79
-                    T[vcur[4 * (fa - r0)]++] = flat(ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}, true);
                     for (int b = 0; b < cd.n_slots; ++b) {
                         const int32_t fb = gfb[(size_t)c * kMaxSlots + b];
                         if (fa < fb || !held(fa, fb)) continue;
@@ -1647,15 +1696,14 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
             for (int64_t g = 0; g < pl.n_gpt; ++g) {
                 if (p_hi[g] < r0 || p_lo[g] >= r1) continue;
                 const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
-                const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
+                const int64_t zb = pl.gz_off[g];
                 for (int32_t a = k0; a < k1; ++a) {
                     const int32_t fa = pfb[a];
                     if (fa < r0) continue;
                     if (fa >= r1) break;
-                    PT[vcur[4 * (fa - r0) + 1]++] = PTerm{zb + pl.gblk_z[a], wz};
                     for (int32_t b = k0; b <= a; ++b) {
                         const int32_t fb = pfb[b];
-                        put_p(S(fa, fb), twice(fa, fb), PTerm{zb + pl.gblk_z[a], zb + pl.gblk_z[b]});
+                        put_p(S(fa, fb), twice(fa, fb), PTerm{(int32_t)(zb + pl.gblk_z[a]), (int32_t)(zb + pl.gblk_z[b])});
                     }
                 }
             }
@@ -1665,12 +1713,81 @@ void build_reduce_plan(const sfm_ba_problem& P, BAHostPlan& pl, PhaseTimer& tm) 
     for (int sg = 0; sg < nseg; ++sg)
         if (seg_rc[sg] != SFM_OK) throw SfmError{seg_rc[sg]};
     tm.mark("terms");
+    // ---- every row's vector terms (rhs sum / product, bF, cnF): the image
+    // slices, then tile row 79 (-Z w) in group order, then the general points'
+    // w, per row -- the order of its matrix terms' sources -----------------------
     {
-        size_t nt = 3 * (size_t)nFB;
+        const std::vector<int32_t> vcut = row_cuts(0, false);
+        const int nv = (int)vcut.size() - 1;
+        std::vector<int> v_rc(nv, SFM_OK);
+        parallel_segments(nv, [&](int sg) {
+            v_rc[sg] = guarded([&] {
+                const int32_t r0 = vcut[sg], r1 = vcut[sg + 1];
+                auto in = [&](int32_t f) { return f >= r0 && f < r1; };
+                FlatTerm* T = pl.terms.data();
+                PTerm* PT = pl.pterms.data();
+                std::vector<int64_t> vcur(4 * (size_t)(r1 - r0));
+                for (int32_t f = r0; f < r1; ++f) {
+                    vcur[4 * (f - r0) + 0] = n_mc + BS(kVc, f);
+                    vcur[4 * (f - r0) + 1] = n_mp + BS(kVp, f);
+                    vcur[4 * (f - r0) + 2] = n_mc + n_vc + BS(kVb, f);
+                    vcur[4 * (f - r0) + 3] = n_mc + n_vc + n_vb + BS(kVb, f);
+                }
+                auto put_v = [&](int32_t f, int16_t ro, int32_t idx) {
+                    int64_t* v = &vcur[4 * (f - r0)];
+                    T[v[0]++] = flat(ReduceTerm{kSrcUb, idx, ro, 0, 1.f}, true);
+                    T[v[2]++] = flat(ReduceTerm{kSrcUb, idx, ro, 0, 1.f}, true);
+                    T[v[3]++] = flat(ReduceTerm{kSrcUcn, idx, ro, 0, 1.f}, true);
+                };
+                for (const ImgSrc& s : isrc)
+                    for (int g = 0; g < gseg; ++g) {
+                        const int32_t idx = s.img * gseg + g;
+                        if (s.cb >= 0 && in(s.cb)) put_v(s.cb, 0, idx);
+                        if (s.fq >= 0 && in(s.fq)) put_v(s.fq, 6, idx);
+                    }
+                for (int32_t c = 0; c < ngrp; ++c) {
+                    if (g_hi[c] < r0 || g_lo[c] >= r1) continue;
+                    const ChunkDesc& cd = grp(c);
+                    for (int a = 0; a < cd.n_slots; ++a) {
+                        const int32_t fa = gfb[(size_t)c * kMaxSlots + a];
+                        if (in(fa))   // rhs contribution (-Z w) from tile row 79
+                            T[vcur[4 * (fa - r0)]++] =
+                                flat(ReduceTerm{kSrcTile, c, (int16_t)kTileWRow, (int16_t)cd.slot_row[a], 1.f}, true);
+                    }
+                }
+                for (int64_t g = 0; g < pl.n_gpt; ++g) {
+                    if (p_hi[g] < r0 || p_lo[g] >= r1) continue;
+                    const int32_t k0 = pl.gblk_off[g], k1 = pl.gblk_off[g + 1];
+                    const int64_t zb = pl.gz_off[g], wz = pl.gz_off[g + 1] - 3;
+                    for (int32_t a = k0; a < k1; ++a) {
+                        const int32_t fa = pfb[a];
+                        if (fa < r0) continue;
+                        if (fa >= r1) break;
+                        PT[vcur[4 * (fa - r0) + 1]++] = PTerm{(int32_t)(zb + pl.gblk_z[a]), (int32_t)wz};
+                    }
+                }
+                return SFM_OK;
+            });
+        });
+        for (int sg = 0; sg < nv; ++sg)
+            if (v_rc[sg] != SFM_OK) throw SfmError{v_rc[sg]};
+    }
+    tm.mark("vector_terms");
+    {
+        // the matrix targets: the seed's rows before f0 (pl.targets already),
+        // then this plan's; every row's first target for the next grown plan
+        size_t nt = pl.targets.size() + 3 * (size_t)nFB;
         for (const auto& v : seg_targets) nt += v.size();
-        pl.targets.clear();
         pl.targets.reserve(nt);
         for (const auto& v : seg_targets) pl.targets.insert(pl.targets.end(), v.begin(), v.end());
+        pl.row_tgt.assign(nFB + 1, 0);
+        if (f0 > 0) std::copy(seed->row_tgt.begin(), seed->row_tgt.begin() + f0, pl.row_tgt.begin());
+        int64_t at = t_keep;
+        for (int sg = 0; sg < nseg; ++sg) {
+            for (int32_t f = cut[sg]; f < cut[sg + 1]; ++f) pl.row_tgt[f] = (int32_t)(at + seg_rows[sg][f - cut[sg]]);
+            at += (int64_t)seg_targets[sg].size();
+        }
+        pl.row_tgt[nFB] = (int32_t)at;
     }
     // vectors: rhs = bF - Z w, bF, cnF, per F block in order
     for (int pass = 0; pass < 3; ++pass)
@@ -1720,7 +1837,7 @@ uint64_t plan_digest(const BAHostPlan& h, bool with_uv) {
         const auto* b = static_cast<const unsigned char*>(p);
         for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 1099511628211ull;
     };
-    static const bool parts = std::getenv("SFM_PLAN_DIGEST") != nullptr;   // (diagnostic: per array)
+    static const bool parts = std::getenv("SFM_PLAN_DIGEST_PARTS") != nullptr;   // (diagnostic: per array)
     int part = 0;
     auto vec = [&](const auto& v) {   // (element types without padding)
         const uint64_t n = v.size();

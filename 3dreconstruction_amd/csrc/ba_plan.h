@@ -94,6 +94,7 @@ struct BAHostPlan {
     // ---- reduce plan ------------------------------------------------------
     std::vector<ReduceTarget> targets;
     std::vector<ReduceTarget> zero_targets;   // world > 1: blocks other shards write (zeroed by the reduce)
+    std::vector<int32_t> row_tgt;    // [nFB + 1] first matrix target of every F-block row (grown plans)
     HostVec<FlatTerm> terms;         // resolved against the solver's source buffer (default-initialised)
     HostVec<PTerm> pterms;           // uploaded as it is: page-locked staging
     int64_t n_sband = 0, n_sarrow = 0, n_scorner = 0;
@@ -108,6 +109,7 @@ struct BAHostPlan {
     // grown plans: the sorted positions taken over from the seed plan unchanged
     // (diagnostics, tests)
     int64_t reused_pts = 0;
+    int64_t reused_chunks = 0, reused_gpts = 0;   // chunks / general points taken from the seed
     PlanGrowState grow;
 };
 

@@ -463,15 +463,16 @@ bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     SFM_HIP(hipStreamSynchronize(s));
     // the observation staging goes back to the cache (the uploads are done);
     // a plan that can seed a grown one keeps its shard arrays (obs_img,
-    // obs_slot: build_plan_grown takes their unchanged prefix)
+    // obs_slot and the reduce plan's terms: build_plan_grown takes their
+    // unchanged prefix)
     if (!(h.grow.ok && cache_enabled_for_growth())) {
         h.obs_img = HostVec<int32_t>();
         h.obs_slot = HostVec<int32_t>();
+        h.pterms = HostVec<PTerm>();
+        h.terms = HostVec<FlatTerm>();
         h.grow = PlanGrowState();
     }
     h.obs_uv = HostVec<double>();
-    h.pterms = HostVec<PTerm>();
-    h.terms = HostVec<FlatTerm>();
     tm.mark("sync");
     return true;
 }

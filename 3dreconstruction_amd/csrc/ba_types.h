@@ -101,9 +101,11 @@ struct ReduceTarget {
 // target block gets -Z_a Z_b' (rows x cols, inner dimension 3), Z_a and Z_b
 // the point's eliminated rows of blocks a and b, row-major [rows][3] at
 // element offsets za / zb of the Z buffer; for a vector target Z_b is the
-// point's w = L^-1 g_E (one row of 3).
+// point's w = L^-1 g_E (one row of 3).  32-bit offsets (the planner requires
+// a Z buffer under 2^31 doubles): half the bytes the planner writes and the
+// reduce reads per term (round 6).
 struct PTerm {
-    int64_t za, zb;
+    int32_t za, zb;
 };
 
 // Kinds of dst_kind.
