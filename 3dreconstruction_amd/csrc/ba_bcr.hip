@@ -2038,10 +2038,11 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
     const int i = k + blockIdx.x;
     const int64_t np = d.np;
     const double* src = d.A + (int64_t)k * kDM * np + (int64_t)k * kDM;
-    load_tile<64>(Akk, LD, src, (int)np);
+    // A_kk and A_ik in flight together (round 6: one memory latency, not two)
     for (int e = threadIdx.x; e < M * LD; e += NT) Xkk[e] = 0.0;
     if (threadIdx.x == 0) flag[0] = 0.0;
-    if (i > k) load_tile<64>(Aik, LD, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
+    if (i > k) load_tiles2(Akk, src, Aik, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
+    else load_tile<64>(Akk, LD, src, (int)np);
     __syncthreads();
     chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(Akk, Xkk, flag, flag + 1);
     const int wave = threadIdx.x >> 6;
@@ -2121,11 +2122,21 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, i
         const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
         acc[q] = (i == j && tj > ti) ? zero4() : tile_ld(C, (int)np, 16 * ti, 16 * tj);
     }
+    // the L_ik / L_jk tiles of column kk + 1 are fetched into registers while
+    // column kk's MFMAs run (round 6; before, each column loaded its two tiles
+    // one after the other, two memory latencies per column on the path)
+    TileFetch<64, M, NT> fi, fj;
+    auto fetch = [&](int kk) {
+        fi.fetch(d.A + (int64_t)i * kDM * np + (int64_t)kk * kDM, (int)np);
+        if (i != j) fj.fetch(d.A + (int64_t)j * kDM * np + (int64_t)kk * kDM, (int)np);
+    };
+    fetch(k0);
     for (int kk = k0; kk < k0 + kw; ++kk) {
         if (kk > k0) __syncthreads();   // the previous column's tiles are consumed
-        load_tile<64>(Li, LD, d.A + (int64_t)i * kDM * np + (int64_t)kk * kDM, (int)np);
-        if (i != j) load_tile<64>(Lj, LD, d.A + (int64_t)j * kDM * np + (int64_t)kk * kDM, (int)np);
+        fi.put(Li, LD);
+        if (i != j) fj.put(Lj, LD);
         __syncthreads();
+        if (kk + 1 < k0 + kw) fetch(kk + 1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;

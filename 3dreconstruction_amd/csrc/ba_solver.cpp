@@ -33,6 +33,7 @@
 #include "ba_order.h"
 #include "ba_plan.h"
 #include "common.h"
+#include "../include/sfm/pool.hpp"
 
 using namespace sfm;
 
@@ -820,12 +821,21 @@ void download(sfm_ba_plan* pl, double* extr, double* intr, double* X) {
     const double* x = pl->cur_is_a ? pl->Xa.p : pl->Xb.p;
     if (extr) SFM_HIP(hipMemcpyAsync(extr, e, 6 * (size_t)h.n_img * 8, hipMemcpyDeviceToHost, s));
     if (intr) SFM_HIP(hipMemcpyAsync(intr, in, (size_t)h.iw * h.n_intr * 8, hipMemcpyDeviceToHost, s));
-    std::vector<double> xs(3 * (size_t)h.n_spt);
+    // (page-locked, cached staging: a DMA, and no page faults on a fresh
+    // vector per call -- the incremental loop downloads after every solve)
+    HostVec<double> xs(3 * (size_t)h.n_spt);
     if (X && h.n_spt) SFM_HIP(hipMemcpyAsync(xs.data(), x, xs.size() * 8, hipMemcpyDeviceToHost, s));
     SFM_HIP(hipStreamSynchronize(s));
-    if (X)
-        for (int64_t k = 0; k < h.n_spt; ++k)
-            for (int a = 0; a < 3; ++a) X[3 * h.spt_global[k] + a] = xs[3 * k + a];
+    if (X) {
+        const int64_t n = h.n_spt;
+        const int nt = n < 16384 ? 1 : std::min<int>(8, (int)(n / 8192));
+        auto part = [&](int t) {
+            for (int64_t k = n * t / nt; k < n * (t + 1) / nt; ++k)
+                for (int a = 0; a < 3; ++a) X[3 * h.spt_global[k] + a] = xs[3 * k + a];
+        };
+        if (nt == 1) part(0);
+        else PlanPool::get().run(nt, part);
+    }
 }
 
 }  // namespace
