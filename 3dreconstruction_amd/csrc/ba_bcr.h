@@ -30,10 +30,11 @@ struct DenseArgs {
     double *A = nullptr, *X = nullptr, *b = nullptr, *y = nullptr, *x = nullptr, *fail = nullptr;
     unsigned* xflag = nullptr;   // [nt] back substitution: x_k published for epoch (dense_back_all_kernel)
     unsigned* fflag = nullptr;   // [2 nt^2 + nt] dataflow factorisation: L tiles, chain inputs, y (dense_flow_kernel)
-    unsigned long long* stamps = nullptr;   // SFM_DENSE_STAMPS diagnostic: chain phase cycle sums [8]
+    unsigned long long* xg = nullptr;   // [nt][kYG] dataflow back substitution: x_k as tagged granules
+    unsigned long long* stamps = nullptr;   // SFM_DENSE_STAMPS diagnostic: chain phase sums, real-time spans
     bool chain = false;   // SFM_CTX_BA_DENSE_CHAIN: launch chains instead of the dataflow kernels
 };
-// flag words of a DenseArgs (x flags + the factorisation's), zeroed once at bind
+// flag words of a DenseArgs (x flags + the factorisation's + the x granules), zeroed once at bind
 size_t dense_flag_words(const DenseArgs& d);
 void dense_setup(DenseArgs& d, const DevProblem& P);
 size_t dense_doubles(const DenseArgs& d);

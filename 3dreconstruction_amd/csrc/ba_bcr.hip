@@ -1623,8 +1623,19 @@ __global__ __launch_bounds__(NT) void bcr_corner_kernel(BcrArgs b, DevProblem P,
 
 // top + corner in one launch: workgroup 0 solves the top system (z_0, X_0)
 // and then adds its corner partial; the other workgroups add theirs at once
-// (their z_i are final since the levels); the last to arrive, normally the
-// top's, solves the corner.  No workgroup waits for another.
+// (their z_i are final since the levels).
+// Untagged (bcr_corner_kernel after a separate top launch): the last to
+// arrive solves the corner and no workgroup waits for another.
+// Tagged (the default fused top): workgroup 0 always solves, and it WAITS for
+// the rest's tagged corner sums (slot N), which the last of workgroups
+// 1..N-1 to take the ticket writes (bcr_corner_body).  This is the one wait
+// in the file that runs against the lower-index rule: it relies on
+// workgroups 1..N-1 making progress while workgroup 0 spins.  They never wait on anything (their inputs are
+// final before the launch), so they finish as soon as they are resident; a
+// held CU only delays them.  The spin is bounded (2^22 polls with s_sleep 1,
+// about seconds) and reports a lost producer as SFM_ERR_DEVICE (fail[1])
+// instead of hanging.  tests/test_ba_general_gpu.py::test_band_solve_under_contention
+// runs this path (and the split path) while another context holds the CUs.
 __global__ __launch_bounds__(NTL) void bcr_top_corner_kernel(BcrArgs b, DevProblem P, double radius, int sp) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (blockIdx.x == 0) {
@@ -2363,7 +2374,6 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
     unsigned* fL = d.fflag;                 // [nt][nt]: L_ij final (i > j), X_j final (i == j)
     unsigned* fR = d.fflag + nt * nt;       // [nt][nt]: A~_ii (D), A~_i,i-1 (S) ready for the chain
     unsigned* fy = d.fflag + 2 * nt * nt;   // [nt]
-    unsigned* fx = d.xflag;                 // [nt]
     auto tA = [&](int i, int j) { return d.A + (int64_t)i * kDM * np + (int64_t)j * kDM; };
     // ---------------- the diagonal chain ----------------
     if (blockIdx.x == 0) {
@@ -2383,6 +2393,7 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             if (threadIdx.x == 0 && bad[0] != 0.0) st_wt(d.fail, 1.0);
         };
         if (stm) tp = stamp();
+        const unsigned long long rt0 = stm ? __builtin_amdgcn_s_memrealtime() : 0;
         for (int k = 0; k < nt; ++k) {
             // T2 holds X_k-1; A~_k,k-1 goes to T1 and A~_kk to T3, loaded together
             if (k > 0) {
@@ -2426,11 +2437,19 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             mark(4);
         }
         x_out(nt - 1);
+        // (diagnostic) the chain's end in real time (100 MHz, one clock for
+        // every CU): B(0) adds its own end minus this to slot 25
+        if (stm && threadIdx.x == 0) {
+            const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_store(d.stamps + 26, rt1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicAdd(d.stamps + 24, rt1 - rt0);
+        }
         df_publish(fL + (nt - 1) * nt + nt - 1, epoch);
         mark(5);
         if (stm && threadIdx.x == 0) {
             for (int q = 0; q < 6; ++q) atomicAdd(d.stamps + q, ts[q]);
             atomicAdd(d.stamps + 6, (unsigned long long)nt);
+            atomicAdd(d.stamps + 27, 1ull);
         }
         return;
     }
@@ -2508,55 +2527,121 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             }
             double* part = T1;   // [4][64]
             double* v = T1 + 4 * M;
+            double* part2 = T1 + 5 * M;   // [4][64]
             part[g * M + r] = s;
             df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j (the workgroup meets)
+            load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
             if (threadIdx.x < M)
                 v[r] = d.b[(int64_t)j * kDM + r] - (((part[r] + part[M + r]) + part[2 * M + r]) + part[3 * M + r]);
             __syncthreads();
-            if (threadIdx.x < M) {   // y_j = X_j v (X lower: columns c <= r)
-                const double* X = d.X + (int64_t)j * kDM * kDM + (int64_t)r * M;
-                double yv = 0.0;
-                for (int c = 0; c <= r; ++c) yv = fma(X[c], v[c], yv);
-                st_wt(d.y + (int64_t)j * kDM + r, yv);
+            // y_j = X_j v (X lower: columns c <= r), columns 16 g .. 16 g + 15
+            // per thread from LDS, the four partials summed in a fixed order
+            double t = 0.0;
+    #pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int c = 16 * g + q;
+                if (c <= r) t = fma(T2[r * LD + c], v[c], t);
             }
+            part2[g * M + r] = t;
+            __syncthreads();
+            if (threadIdx.x < M)
+                st_wt(d.y + (int64_t)j * kDM + r, ((part2[r] + part2[M + r]) + part2[2 * M + r]) + part2[3 * M + r]);
             df_publish(fy + j, epoch);
             return;
         }
-        // B(k), k = nt - 1 - t: x_k = X_k' (y_k - sum_{i > k} L_ik' x_i)
+        // B(k), k = nt - 1 - t: x_k = X_k' (y_k - sum_{i > k} L_ik' x_i), with
+        // one column of lookahead (round 6):
+        //   x_k = r_k - M_k x_k+1,  r_k = X_k' (y_k - sum_{i > k+1} L_ik' x_i),
+        //   M_k = X_k' L_k+1,k'  (formed while the substitution is still far)
+        // so the arrival of x_k+1 -- the chain's one dependency -- costs a
+        // 64 x 64 matrix-vector product from registers.  x goes out as tagged
+        // granules (put_y / get_y: the data is the flag, no drain, no flag
+        // round trip); every L_ik slice is fetched before its x_i is awaited.
         const int k = nt - 1 - t;
         if (k < 0) return;
         const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-        double s = 0.0;
-        // inputs i = nt - 1 down to k + 1, i.e. m = nt - 1 - i = 0 .. nt - 2 - k
-        for (int m = 0; m < nt - 1 - k;) {
-            const int m1 = df_wait_run(fx + nt - 1, -1, fL + (int64_t)(nt - 1) * nt + k, -nt, m, nt - 1 - k, epoch,
-                                       d.fail, sh);
-            for (; m < m1; ++m) {
-                const int i = nt - 1 - m;
-                const double* L = tA(i, k) + c;
-                const double* x = d.x + (int64_t)i * kDM;
+        const bool la = k + 1 < nt;
+        // X_k and every L_ik (i > k): final when the factorisation passes k
+        df_wait_run(fL + k * nt + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
+        for (int m = 0; m < nt - 1 - k;)
+            m = df_wait_run(fL + (int64_t)(k + 1) * nt + k, nt, nullptr, 0, m, nt - 1 - k, epoch, d.fail, sh);
+        load_tile<64>(T2, LD, d.X + (int64_t)k * kDM * kDM, M);
+        if (la) load_tile<64>(T1, LD, tA(k + 1, k), (int)np);
+        __syncthreads();
+        double mreg[16];
+        if (la) {
+            // M_k = X_k' L_k+1,k' (X lower: X[kk][m] = 0 for kk < m)
     #pragma unroll
-                for (int q = 0; q < M / 4; ++q) s = fma(L[(int64_t)(4 * q + g) * np], x[4 * q + g], s);
-            }
+            for (int q = 0; q < 4; ++q)
+                tile_st(T3, LD, 16 * wave, 16 * q,
+                        tile_mm<true, true, false>(zero4(), T2, LD, 16 * wave, T1, LD, 16 * q, 16 * wave, M));
+            __syncthreads();
+    #pragma unroll
+            for (int q = 0; q < 16; ++q) mreg[q] = T3[c * LD + 16 * g + q];
         }
-        double* part = T1;
-        double* v = T1 + 4 * M;
+        double* xs = T1;               // [2][64] x_i, double buffered
+        double* part = T1 + 2 * M;     // [4][64]
+        double* v = T1 + 6 * M;        // [64]
+        double* part2 = T1 + 7 * M;    // [4][64]
+        double* part3 = T1 + 11 * M;   // [4][64]
+        __syncthreads();               // (T1's L tile is read)
+        double s = 0.0;
+        int buf = 0;
+        for (int i = nt - 1; i >= k + 2; --i) {   // x_i arrive in this order
+            const double* L = tA(i, k) + c;
+            double lr[16];
+    #pragma unroll
+            for (int q = 0; q < 16; ++q) lr[q] = L[(int64_t)(4 * q + g) * np];
+            double* xb = xs + M * buf;
+            if (wave == 0) get_y(d.xg + (int64_t)i * kYG, nullptr, xb, nullptr, epoch, d.fail);
+            __syncthreads();
+    #pragma unroll
+            for (int q = 0; q < 16; ++q) s = fma(lr[q], xb[4 * q + g], s);
+            buf ^= 1;
+        }
         part[g * M + c] = s;
-        df_wait_run(fy + k, 0, fL + k * nt + k, 0, 0, 1, epoch, d.fail, sh);   // y_k, X_k
+        df_wait_run(fy + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // y_k (the workgroup meets)
         if (threadIdx.x < M)
             v[c] = d.y[(int64_t)k * kDM + c] - (((part[c] + part[M + c]) + part[2 * M + c]) + part[3 * M + c]);
         __syncthreads();
-        if (threadIdx.x < M) {   // x_k = X_k' v: X lower, rows m >= c
-            const double* X = d.X + (int64_t)k * kDM * kDM;
-            double xv = 0.0;
-            for (int m = c; m < M; ++m) xv = fma(X[(int64_t)m * M + c], v[m], xv);
-            st_wt(d.x + (int64_t)k * kDM + c, xv);
+        // r_k = X_k' v (X lower: rows m >= c), rows 16 g .. 16 g + 15 per thread
+        double u = 0.0;
+    #pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int m = 16 * g + q;
+            if (m >= c) u = fma(T2[m * LD + c], v[m], u);
+        }
+        part2[g * M + c] = u;
+        __syncthreads();
+        double xv = ((part2[c] + part2[M + c]) + part2[2 * M + c]) + part2[3 * M + c];
+        if (la) {
+            double* xb = xs + M * buf;
+            if (wave == 0) get_y(d.xg + (int64_t)(k + 1) * kYG, nullptr, xb, nullptr, epoch, d.fail);
+            __syncthreads();
+            double w = 0.0;
+    #pragma unroll
+            for (int q = 0; q < 16; ++q) w = fma(mreg[q], xb[16 * g + q], w);
+            part3[g * M + c] = w;
+            __syncthreads();
+            xv -= ((part3[c] + part3[M + c]) + part3[2 * M + c]) + part3[3 * M + c];
+        }
+        if (threadIdx.x < M) {
+            put_y(d.xg + (int64_t)k * kYG, c, xv, epoch);
             const int64_t e = (int64_t)k * kDM + c;
             if (e < P.nF) P.yF[e] = xv;
         }
-        df_publish(fx + k, epoch);
-        if (k == 0 && threadIdx.x == 0)   // every other task feeds x_0: the verdict is final
-            P.scal[kScSolveFail] = solve_verdict(d.fail);
+        if (k == 0) {
+            // every task feeds x_0; the factor verdicts travel with the X flags
+            // (acquired here: the x granules carry no ordering)
+            for (int m = 0; m < nt;) m = df_wait_run(fL, nt + 1, nullptr, 0, m, nt, epoch, d.fail, sh);
+            if (threadIdx.x == 0) {
+                P.scal[kScSolveFail] = solve_verdict(d.fail);
+                if (d.stamps)
+                    atomicAdd(d.stamps + 25, __builtin_amdgcn_s_memrealtime() -
+                                                 __hip_atomic_load(d.stamps + 26, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT));
+            }
+        }
     };
     const int ntask = df_tasks(nt);
     for (int t = blockIdx.x - 1; t < ntask; t += gridDim.x - 1) {
@@ -2572,10 +2657,13 @@ void dense_setup(DenseArgs& d, const DevProblem& P) {
     d.np = (int64_t)d.nt * kDM;
 }
 
-size_t dense_flag_words(const DenseArgs& d) { return (size_t)d.nt + 2 * (size_t)d.nt * d.nt + d.nt; }
+// flags: x (nt), L tiles + chain inputs (2 nt^2), y (nt); then (8-byte
+// aligned) the dataflow back substitution's tagged x granules (kYG per column)
+static size_t dense_granule_word(const DenseArgs& d) { return ((size_t)d.nt + 2 * (size_t)d.nt * d.nt + d.nt + 1) & ~(size_t)1; }
+size_t dense_flag_words(const DenseArgs& d) { return dense_granule_word(d) + 2 * (size_t)kYG * d.nt; }
 
 size_t dense_doubles(const DenseArgs& d) {
-    // A | X | b y x | fail (8) | flags: x (nt), L tiles + chain inputs (2 nt^2), y (nt)
+    // A | X | b y x | fail (8) | flags and granules
     return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8 + (dense_flag_words(d) + 1) / 2 + 2;
 }
 
@@ -2588,6 +2676,7 @@ void dense_bind(DenseArgs& d, double* base) {
     d.fail = d.x + d.np;
     d.xflag = reinterpret_cast<unsigned*>(d.fail + 8);   // zeroed by the caller once
     d.fflag = d.xflag + d.nt;
+    d.xg = reinterpret_cast<unsigned long long*>(d.xflag + dense_granule_word(d));
 }
 
 void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {

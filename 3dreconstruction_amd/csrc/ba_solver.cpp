@@ -425,7 +425,7 @@ bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
         dense_bind(pl->dense, pl->dense_buf.p);
         SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * dense_flag_words(pl->dense), s));
         if (std::getenv("SFM_DENSE_STAMPS")) {
-            pl->bcr_stamps.alloc(16);
+            pl->bcr_stamps.alloc(32);   // chain phases [0, 8), chol_inv64's [8, 24), real time [24, 28)
             pl->bcr_stamps.zero(s);
             pl->dense.stamps = pl->bcr_stamps.p;
         }
@@ -783,12 +783,14 @@ int run_plan(sfm_ba_plan* pl, const sfm_ba_options& O, sfm_ba_summary* sum) {
                      st[12] / n, st[13] / n, st[14] / n, st[15] / n, st[8] / n, st[9] / n, st[10] / n, st[11] / n);
     }
     if (pl->dense.stamps) {  // diagnostic: dataflow chain, average cycles per block column
-        unsigned long long st[16];
+        unsigned long long st[32];
         SFM_HIP(hipMemcpy(st, pl->dense.stamps, sizeof st, hipMemcpyDeviceToHost));
-        const double n = st[6] ? (double)st[6] : 1.0;
-        std::fprintf(stderr, "[dense stamps] cycles/column: wait S %.0f  L %.0f  wait D %.0f  update %.0f  "
-                     "factor %.0f (diag16 + updates %.0f, pivots %.0f)  X out %.0f  over %llu columns\n",
-                     st[0] / n, st[1] / n, st[2] / n, st[3] / n, st[4] / n, st[8] / n, st[15] / n, st[5] / n, st[6]);
+        const double n = st[6] ? (double)st[6] : 1.0, ns = st[27] ? (double)st[27] : 1.0;
+        std::fprintf(stderr, "[dense stamps] cycles/column: wait S+D %.0f  L + X out %.0f  update %.0f  sync %.0f  "
+                     "factor %.0f (diag16 %.0f, pivots %.0f)  last X %.0f  over %llu columns; per solve: chain "
+                     "%.2f us, chain end to x_0 %.2f us over %llu solves\n",
+                     st[0] / n, st[1] / n, st[2] / n, st[3] / n, st[4] / n, st[8] / n, st[15] / n, st[5] / n, st[6],
+                     st[24] / ns / 100.0, st[25] / ns / 100.0, st[27]);
     }
     if (pl->stamps.p) {  // diagnostic: average phase cycles per chunk (last Schur launch)
         std::vector<unsigned long long> st(pl->stamps.n);
