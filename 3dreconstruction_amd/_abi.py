@@ -247,6 +247,7 @@ SIGNATURES = [
     ("sfm_ba_describe", C.c_int, [C.POINTER(BAProblem), C.c_int32, C.c_int32, C.POINTER(BAPlanShape)]),
     ("sfm_ba_grown_digest", C.c_int, [C.POINTER(BAProblem), C.POINTER(BAProblem), C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64), C.POINTER(C.c_int64)]),
+    ("sfm_ba_dense_schedule", C.c_int, [C.POINTER(BAProblem), i32p, C.c_int64, i64p, i32p]),
     ("sfm_synth_ba", C.c_int, [C.POINTER(SynthBAConfig), i64p, i32p, f64p, i32p, f64p,
                                f64p, f64p, f64p, f64p, f64p, i64p]),
     ("sfm_match_dense", C.c_int, [C.c_void_p, u8p, C.c_int32, u8p, C.c_int32,

@@ -257,6 +257,22 @@ def ba_grown_digest(prev, problem):
     return df.value, dg.value, r.value
 
 
+def ba_dense_schedule(problem):
+    """[cpu] The dense dataflow solve's schedule for `problem`
+    (sfm_ba_dense_schedule): (shape dict, int32 array); the array is empty
+    when the dataflow solve does not run."""
+    lib = abi.load()
+    n = C.c_int64()
+    shape = np.zeros(7, np.int32)
+    _check(lib.sfm_ba_dense_schedule(C.byref(problem), None, 0, C.byref(n), shape.ctypes.data_as(abi.i32p)),
+           "sfm_ba_dense_schedule")
+    meta = np.zeros(max(n.value, 1), np.int32)
+    _check(lib.sfm_ba_dense_schedule(C.byref(problem), meta.ctypes.data_as(abi.i32p), n.value, C.byref(n),
+                                     shape.ctypes.data_as(abi.i32p)), "sfm_ba_dense_schedule")
+    keys = ("nt", "chains", "tasks", "flow", "nF", "nb", "D")
+    return dict(zip(keys, (int(v) for v in shape))), meta[:n.value]
+
+
 class BAPlan:
     """Resident BA problem (sfm_ba_plan): upload once, run many times."""
 

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "ba_kernels.h"
 
 namespace sfm {
@@ -32,11 +34,20 @@ struct DenseArgs {
     unsigned* fflag = nullptr;   // [2 nt^2 + nt] dataflow factorisation: L tiles, chain inputs, y (dense_flow_kernel)
     unsigned long long* xg = nullptr;   // [nt][kYG] dataflow back substitution: x_k as tagged granules
     unsigned long long* stamps = nullptr;   // SFM_DENSE_STAMPS diagnostic: chain phase sums, real-time spans
+    // dataflow solve (dense_flow_kernel, nt <= kDenseFlowMaxNt): the host's
+    // schedule (dense_flow_plan): tile order, chains, tile pattern, task list
+    const int32_t* meta = nullptr;
+    int nch = 0, ntask = 0;    // chain workgroups (1 or 2), tasks
+    int64_t meta_words = 0;    // int32 words at meta
+    bool flow = false;         // the dataflow kernel solves (else the launch chain)
     bool chain = false;   // SFM_CTX_BA_DENSE_CHAIN: launch chains instead of the dataflow kernels
 };
 // flag words of a DenseArgs (x flags + the factorisation's + the x granules), zeroed once at bind
 size_t dense_flag_words(const DenseArgs& d);
 void dense_setup(DenseArgs& d, const DevProblem& P);
+// the dataflow solve's schedule (host, once per plan; empty for the launch
+// chain): sets d.flow / nch / ntask / meta_words; the caller copies it to d.meta
+std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P);
 size_t dense_doubles(const DenseArgs& d);
 void dense_bind(DenseArgs& d, double* base);
 // epoch: a value the x flags do not hold yet (the plan counts its solves from 1)

@@ -22,6 +22,8 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
+#include <functional>
 #include <type_traits>
 #include <utility>
 
@@ -2017,6 +2019,8 @@ namespace {
 
 constexpr int kDM = 64;   // tile
 constexpr int kDenseW = 4;   // block columns per trailing update
+constexpr int kDenseFlowMaxNt = 29;   // the dataflow solve up to this many block columns
+enum : int { kTaskD = 0, kTaskS = 1, kTaskT = 2, kTaskY = 3, kTaskB = 4 };   // dataflow tasks (dense_flow_plan)
 
 __global__ __launch_bounds__(256) void dense_pack_kernel(DenseArgs d, DevProblem P, double radius) {
     const int64_t np = d.np;
@@ -2354,29 +2358,65 @@ __device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const uns
     return *sh;
 }
 
-// number of tasks (helper workgroups) for nt block columns
-__host__ __device__ __forceinline__ int df_tasks(int nt) {
-    int n = 0;
-    for (int j = 0; j < nt; ++j) n += j + 1 < nt ? nt - j + 1 : 1;
-    return n + nt;
+// tile (pi, pj) of S in the natural tile order (pi, pj: physical tiles of
+// a permuted pair) straight from the reduce's lower-triangle S, with the LM
+// diagonal D^2 and identity padding -- the values dense_pack_kernel gives --
+// into LDS [64][LD].  A tile above the diagonal (pi < pj) is the transpose
+// of the stored lower one.  (The dataflow solve has no pack pass: round 6.)
+__device__ __forceinline__ void df_load_a(double* T, const DevProblem& P, double radius, int pi, int pj) {
+    const int64_t nF = P.nF, R0 = (int64_t)pi * kDM, C0 = (int64_t)pj * kDM;
+    for (int e = threadIdx.x; e < M * M; e += NT) {
+        double v = 0.0;
+        int r, c;
+        if (pi >= pj) {   // source rows, c fastest
+            r = e / M;
+            c = e % M;
+            const int64_t a = R0 + r, b = C0 + c;
+            if (a < nF && b < nF) {
+                if (pi > pj || c <= r) v = P.Sdense[a * nF + b];
+                if (pi == pj && r == c) {
+                    const double lm = sqrt(clampd(P.cnF[a], P.min_diag, P.max_diag) / radius);
+                    v += lm * lm;
+                }
+            } else if (pi == pj && r == c) {
+                v = 1.0;
+            }
+        } else {          // transposed: (r, c) = S[C0 + c][R0 + r], r fastest
+            c = e / M;
+            r = e % M;
+            const int64_t a = C0 + c, b = R0 + r;
+            if (a < nF && b < nF) v = P.Sdense[a * nF + b];
+        }
+        T[r * LD + c] = v;
+    }
 }
 
-__global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem P, unsigned epoch) {
+__global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem P, double radius, unsigned epoch) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* T1 = sm;
     double* T2 = sm + M * LD;
-    double* T3 = T2 + M * LD;      // the chain's diagonal tile
+    double* T3 = T2 + M * LD;      // the chain's diagonal tile; a task's first A tile
     double* bad = T3 + M * LD;     // [2]
     double* col = bad + 2;         // [16] (diag16)
     int* sh = reinterpret_cast<int*>(col + 16);
     const int nt = d.nt, wave = threadIdx.x >> 6;
     const int64_t np = d.np;
     unsigned* fL = d.fflag;                 // [nt][nt]: L_ij final (i > j), X_j final (i == j)
-    unsigned* fR = d.fflag + nt * nt;       // [nt][nt]: A~_ii (D), A~_i,i-1 (S) ready for the chain
+    unsigned* fR = d.fflag + nt * nt;       // [nt][nt]: A~_kk (D), A~_kp (S) ready for the chain
     unsigned* fy = d.fflag + 2 * nt * nt;   // [nt]
-    auto tA = [&](int i, int j) { return d.A + (int64_t)i * kDM * np + (int64_t)j * kDM; };
-    // ---------------- the diagonal chain ----------------
-    if (blockIdx.x == 0) {
+    // the host's schedule (dense_flow_plan): permuted column k is natural tile perm[k]
+    const int32_t* perm = d.meta;
+    const int32_t* prevc = d.meta + nt;      // the chain's previous column (-1: none)
+    const int32_t* info = d.meta + 2 * nt;   // 1 linked to prevc, 2 D(k) task, 4 S(k) task
+    const int32_t* lav = d.meta + 3 * nt;    // the back substitution's lookahead row
+    const int32_t* tasks = d.meta + 6 * nt + 2;
+    const unsigned char* nzb = reinterpret_cast<const unsigned char*>(tasks + d.ntask);
+    auto nz = [&](int i, int j) { return nzb[i * nt + j] != 0; };
+    auto tA = [&](int i, int j) { return d.A + (int64_t)perm[i] * kDM * np + (int64_t)perm[j] * kDM; };
+    // ---------------- the diagonal chains ----------------
+    if ((int)blockIdx.x < d.nch) {
+        const int32_t* clist = d.meta + (4 + blockIdx.x) * nt;
+        const int clen = d.meta[6 * nt + blockIdx.x];
         unsigned long long ts[7] = {0, 0, 0, 0, 0, 0, 0}, tp = 0;
         const bool stm = d.stamps != nullptr;
         auto mark = [&](int ph) {
@@ -2394,40 +2434,56 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         };
         if (stm) tp = stamp();
         const unsigned long long rt0 = stm ? __builtin_amdgcn_s_memrealtime() : 0;
-        for (int k = 0; k < nt; ++k) {
-            // T2 holds X_k-1; A~_k,k-1 goes to T1 and A~_kk to T3, loaded together
-            if (k > 0) {
-                df_wait_run(fR + k * nt + k - 1, 0, fR + k * nt + k, 0, 0, 1, epoch, d.fail, sh);   // S(k), D(k)
+        for (int q = 0; q < clen; ++q) {
+            const int k = clist[q], p = prevc[k], inf = info[k];
+            const bool hd = (inf & 2) != 0, hs = (inf & 4) != 0;
+            if (inf & 1) {
+                // linked: T2 holds X_p.  A~_kp to T1 and A~_kk to T3, loaded together
+                if (hs || hd)
+                    df_wait_run(hs ? fR + k * nt + p : fR + k * nt + k, 0, (hs && hd) ? fR + k * nt + k : nullptr, 0, 0,
+                                1, epoch, d.fail, sh);   // S(k), D(k)
                 mark(0);
-                load_tiles2(T1, tA(k, k - 1), T3, tA(k, k), (int)np);
+                if (hs && hd) {
+                    load_tiles2(T1, tA(k, p), T3, tA(k, k), (int)np);
+                } else {
+                    if (hs) load_tile<64>(T1, LD, tA(k, p), (int)np);
+                    else df_load_a(T1, P, radius, perm[k], perm[p]);
+                    if (hd) load_tile<64>(T3, LD, tA(k, k), (int)np);
+                    else df_load_a(T3, P, radius, perm[k], perm[k]);
+                }
                 __syncthreads();
-                // L_k,k-1 = A~_k,k-1 X_k-1'
+                // L_kp = A~_kp X_p'
                 v4d acc[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
+                for (int c = 0; c < 4; ++c)
+                    acc[c] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * c, 0, 16 * c + 16);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) tile_st_wt(tA(k, k - 1), (int)np, 16 * wave, 16 * q, acc[q]);
-                // X_k-1 goes out with L_k,k-1; their drain and flags come after
-                // the diagonal update below, so the stores complete meanwhile
-                x_out(k - 1);
+                for (int c = 0; c < 4; ++c) tile_st_wt(tA(k, p), (int)np, 16 * wave, 16 * c, acc[c]);
+                // X_p goes out with L_kp; their drain and flags come after the
+                // diagonal update below, so the stores complete meanwhile
+                x_out(p);
                 __syncthreads();   // T1 and T2 are read
 #pragma unroll
-                for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
+                for (int c = 0; c < 4; ++c) tile_st(T1, LD, 16 * wave, 16 * c, acc[c]);
                 for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
                 mark(1);
                 __syncthreads();
                 // A~_kk -= L L': the 10 lower 16x16 tiles round robin over the waves
-                for (int q = wave; q < 10; q += NT / 64) {
-                    const int ti = q < 1 ? 0 : q < 3 ? 1 : q < 6 ? 2 : 3;
-                    const int tj = q - ti * (ti + 1) / 2;
+                for (int c = wave; c < 10; c += NT / 64) {
+                    const int ti = c < 1 ? 0 : c < 3 ? 1 : c < 6 ? 2 : 3;
+                    const int tj = c - ti * (ti + 1) / 2;
                     const v4d a = tile_ld(T3, LD, 16 * ti, 16 * tj);
                     tile_st(T3, LD, 16 * ti, 16 * tj, tile_mm<false, true, true>(a, T1, LD, 16 * ti, T1, LD, 16 * tj, 0, M));
                 }
-                df_publish2(fL + k * nt + k - 1, fL + (k - 1) * nt + k - 1, epoch);   // L_k,k-1 and X_k-1
+                df_publish2(fL + k * nt + p, fL + p * nt + p, epoch);   // L_kp and X_p
                 mark(2);
             } else {
-                load_tile<64>(T3, LD, tA(0, 0), (int)np);
+                if (hd) {
+                    df_wait_run(fR + k * nt + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // D(k)
+                    load_tile<64>(T3, LD, tA(k, k), (int)np);
+                } else {
+                    df_load_a(T3, P, radius, perm[k], perm[k]);
+                }
                 for (int e = threadIdx.x; e < M * LD; e += NT) T2[e] = 0.0;
             }
             if (threadIdx.x == 0) bad[0] = 0.0;
@@ -2435,95 +2491,94 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             mark(3);
             chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(T3, T2, bad, col, stm ? d.stamps + 8 : nullptr);
             mark(4);
+            // X_k goes out now unless the chain's next column is linked to k
+            // (then with L_next,k)
+            const int nx = q + 1 < clen ? clist[q + 1] : -1;
+            if (nx < 0 || !(info[nx] & 1)) {
+                x_out(k);
+                df_publish(fL + k * nt + k, epoch);
+                mark(5);
+            }
         }
-        x_out(nt - 1);
-        // (diagnostic) the chain's end in real time (100 MHz, one clock for
-        // every CU): B(0) adds its own end minus this to slot 25
         if (stm && threadIdx.x == 0) {
+            // (diagnostic) the chains' end in real time (100 MHz, one clock for
+            // every CU): the last back-substitution task adds its own end minus
+            // the later chain's to slot 25
             const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
-            __hip_atomic_store(d.stamps + 26, rt1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicAdd(d.stamps + 24, rt1 - rt0);
-        }
-        df_publish(fL + (nt - 1) * nt + nt - 1, epoch);
-        mark(5);
-        if (stm && threadIdx.x == 0) {
-            for (int q = 0; q < 6; ++q) atomicAdd(d.stamps + q, ts[q]);
-            atomicAdd(d.stamps + 6, (unsigned long long)nt);
-            atomicAdd(d.stamps + 27, 1ull);
+            atomicMax(d.stamps + 26, rt1);
+            if (blockIdx.x == 0) {
+                atomicAdd(d.stamps + 24, rt1 - rt0);
+                atomicAdd(d.stamps + 27, 1ull);
+            }
+            for (int c = 0; c < 6; ++c) atomicAdd(d.stamps + c, ts[c]);
+            atomicAdd(d.stamps + 6, (unsigned long long)clen);
         }
         return;
     }
-    // ---------------- tasks: round robin over the helper workgroups ----------------
-    // (every task waits only on tasks of lower index and on the chain, so the
-    // lowest unfinished task can always run: its worker has finished the ones
-    // before it)
+    // ---------------- tasks: in the host's order, round robin over the workers ----------------
+    // (every task waits only on earlier tasks and on chain steps that wait
+    // only on earlier tasks, so the earliest unfinished one can always run:
+    // its worker has finished the ones before it)
     auto task = [&](int t) {
-        int j = 0;
-        for (; j < nt; ++j) {   // column j's tasks: [D(j+1), S(j+1)] (j + 1 < nt), T(j+2.., j), Y(j)
-            const int c = j + 1 < nt ? nt - j + 1 : 1;
-            if (t < c) break;
-            t -= c;
-        }
-        if (j < nt) {
-            const bool two = j + 1 < nt;
-            const int kind = !two ? 3 : t == 0 ? 0 : t == 1 ? 1 : t < nt - j ? 2 : 3;   // D S T Y
-            if (kind <= 2) {
-                const int i = kind == 2 ? j + t : j + 1, jj = kind == 0 ? j + 1 : j;   // target tile (i, jj)
-                const int mend = j;   // D(j+1), S(j+1): m < j; T(i, j): m < j
-                const bool diag = kind == 0;
-                v4d acc[4];
-    #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc[q] = (diag && q > wave) ? zero4() : tile_ld(tA(i, jj), (int)np, 16 * wave, 16 * q);
-                for (int m = 0; m < mend;) {
-                    const int m1 = df_wait_run(fL + i * nt, 1, diag ? nullptr : fL + jj * nt, 1, m, mend, epoch, d.fail, sh);
-                    for (; m < m1; ++m) {
-                        if (diag) load_tile<64>(T1, LD, tA(i, m), (int)np);
-                        else load_tiles2(T1, tA(i, m), T2, tA(jj, m), (int)np);
-                        __syncthreads();
-                        const double* Lb = diag ? T1 : T2;
-    #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            if (diag && q > wave) continue;
-                            acc[q] = tile_mm<false, true, true>(acc[q], T1, LD, 16 * wave, Lb, LD, 16 * q, 0, M);
-                        }
-                        __syncthreads();
-                    }
-                }
-                if (kind < 2) {
-                    if (mend > 0) {   // (nothing subtracted: the packed tile stands)
-    #pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            if (!(diag && q > wave)) tile_st_wt(tA(i, jj), (int)np, 16 * wave, 16 * q, acc[q]);
-                    }
-                    df_publish(fR + i * nt + jj, epoch);
-                    return;
-                }
-                // T: L_ij = A~_ij X_j'
-    #pragma unroll
-                for (int q = 0; q < 4; ++q) tile_st(T1, LD, 16 * wave, 16 * q, acc[q]);
-                df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j
-                load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
+        const int code = tasks[t], kind = code >> 24, i = (code >> 12) & 0xfff, j = code & 0xfff;
+        if (kind <= kTaskT) {
+            // D(i): A~_ii = A_ii - sum L_im L_im' (m < i, not the chain's own
+            // m = prevc[i]); S(i): A~_ij = A_ij - sum L_im L_jm' (m < j = prevc[i]);
+            // T(i, j): L_ij = (A_ij - sum_{m < j} L_im L_jm') X_j'.  Nonzero m only.
+            const bool diag = kind == kTaskD;
+            const int excl = (diag && (info[i] & 1)) ? prevc[i] : -1, mend = diag ? i : j;
+            df_load_a(T3, P, radius, perm[i], perm[j]);
+            __syncthreads();
+            v4d acc[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = (diag && c > wave) ? zero4() : tile_ld(T3, LD, 16 * wave, 16 * c);
+            for (int m = 0; m < mend; ++m) {
+                if (m == excl || !nz(i, m) || (!diag && !nz(j, m))) continue;
+                df_wait_run(fL + i * nt + m, 0, diag ? nullptr : fL + j * nt + m, 0, 0, 1, epoch, d.fail, sh);
+                if (diag) load_tile<64>(T1, LD, tA(i, m), (int)np);
+                else load_tiles2(T1, tA(i, m), T2, tA(j, m), (int)np);
                 __syncthreads();
-    #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    acc[q] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * q, 0, 16 * q + 16);
-    #pragma unroll
-                for (int q = 0; q < 4; ++q) tile_st_wt(tA(i, j), (int)np, 16 * wave, 16 * q, acc[q]);
-                df_publish(fL + i * nt + j, epoch);
+                const double* Lb = diag ? T1 : T2;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (diag && c > wave) continue;
+                    acc[c] = tile_mm<false, true, true>(acc[c], T1, LD, 16 * wave, Lb, LD, 16 * c, 0, M);
+                }
+                __syncthreads();
+            }
+            if (kind != kTaskT) {
+                // (the diagonal tile's upper 16x16 tiles go out as zeros: the
+                // chain loads the whole tile)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) tile_st_wt(tA(i, j), (int)np, 16 * wave, 16 * c, acc[c]);
+                df_publish(fR + i * nt + j, epoch);
                 return;
             }
-            // Y(j): thread (g, r) sums columns 16 g .. 16 g + 15 of row r of every L_jm
+#pragma unroll
+            for (int c = 0; c < 4; ++c) tile_st(T1, LD, 16 * wave, 16 * c, acc[c]);
+            df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j
+            load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                acc[c] = tile_mm<false, true, false>(zero4(), T1, LD, 16 * wave, T2, LD, 16 * c, 0, 16 * c + 16);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) tile_st_wt(tA(i, j), (int)np, 16 * wave, 16 * c, acc[c]);
+            df_publish(fL + i * nt + j, epoch);
+            return;
+        }
+        if (kind == kTaskY) {
+            // Y(j): y_j = X_j (b_j - sum L_jm y_m); thread (g, r) sums columns
+            // 16 g .. 16 g + 15 of row r of every nonzero L_jm
             const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
             double s = 0.0;
-            for (int m = 0; m < j;) {
-                const int m1 = df_wait_run(fL + j * nt, 1, fy, 1, m, j, epoch, d.fail, sh);
-                for (; m < m1; ++m) {
-                    const double* L = tA(j, m) + (int64_t)r * np + 16 * g;
-                    const double* y = d.y + (int64_t)m * kDM + 16 * g;
-    #pragma unroll
-                    for (int c = 0; c < 16; ++c) s = fma(L[c], y[c], s);
-                }
+            for (int m = 0; m < j; ++m) {
+                if (!nz(j, m)) continue;
+                df_wait_run(fL + j * nt + m, 0, fy + m, 0, 0, 1, epoch, d.fail, sh);
+                const double* L = tA(j, m) + (int64_t)r * np + 16 * g;
+                const double* y = d.y + (int64_t)m * kDM + 16 * g;
+#pragma unroll
+                for (int c = 0; c < 16; ++c) s = fma(L[c], y[c], s);
             }
             double* part = T1;   // [4][64]
             double* v = T1 + 4 * M;
@@ -2531,52 +2586,53 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             part[g * M + r] = s;
             df_wait_run(fL + j * nt + j, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);   // X_j (the workgroup meets)
             load_tile<64>(T2, LD, d.X + (int64_t)j * kDM * kDM, M);
-            if (threadIdx.x < M)
-                v[r] = d.b[(int64_t)j * kDM + r] - (((part[r] + part[M + r]) + part[2 * M + r]) + part[3 * M + r]);
+            if (threadIdx.x < M) {
+                const int64_t e = (int64_t)perm[j] * kDM + r;
+                v[r] = (e < P.nF ? P.rhs[e] : 0.0) - (((part[r] + part[M + r]) + part[2 * M + r]) + part[3 * M + r]);
+            }
             __syncthreads();
             // y_j = X_j v (X lower: columns c <= r), columns 16 g .. 16 g + 15
             // per thread from LDS, the four partials summed in a fixed order
-            double t = 0.0;
-    #pragma unroll
+            double u = 0.0;
+#pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int c = 16 * g + q;
-                if (c <= r) t = fma(T2[r * LD + c], v[c], t);
+                if (c <= r) u = fma(T2[r * LD + c], v[c], u);
             }
-            part2[g * M + r] = t;
+            part2[g * M + r] = u;
             __syncthreads();
             if (threadIdx.x < M)
                 st_wt(d.y + (int64_t)j * kDM + r, ((part2[r] + part2[M + r]) + part2[2 * M + r]) + part2[3 * M + r]);
             df_publish(fy + j, epoch);
             return;
         }
-        // B(k), k = nt - 1 - t: x_k = X_k' (y_k - sum_{i > k} L_ik' x_i), with
-        // one column of lookahead (round 6):
-        //   x_k = r_k - M_k x_k+1,  r_k = X_k' (y_k - sum_{i > k+1} L_ik' x_i),
-        //   M_k = X_k' L_k+1,k'  (formed while the substitution is still far)
-        // so the arrival of x_k+1 -- the chain's one dependency -- costs a
-        // 64 x 64 matrix-vector product from registers.  x goes out as tagged
-        // granules (put_y / get_y: the data is the flag, no drain, no flag
-        // round trip); every L_ik slice is fetched before its x_i is awaited.
-        const int k = nt - 1 - t;
-        if (k < 0) return;
+        // B(k): x_k = X_k' (y_k - sum_{i > k} L_ik' x_i) over the nonzero L_ik,
+        // with one row of lookahead (round 6), la = the first such i (its x
+        // arrives last):
+        //   x_k = r_k - M_k x_la,  r_k = X_k' (y_k - sum_{i > k, i != la} L_ik' x_i),
+        //   M_k = X_k' L_la,k'  (formed while the substitution is still far)
+        // so the arrival of x_la costs one 64 x 64 matrix-vector product from
+        // registers.  x goes out as tagged granules (put_y / get_y: the data is
+        // the flag, no drain, no flag round trip); every L_ik slice is fetched
+        // before its x_i is awaited.
+        const int k = i, la = lav[k];
         const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-        const bool la = k + 1 < nt;
-        // X_k and every L_ik (i > k): final when the factorisation passes k
+        // X_k and every nonzero L_ik (i > k): final when the factorisation passes k
         df_wait_run(fL + k * nt + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
-        for (int m = 0; m < nt - 1 - k;)
-            m = df_wait_run(fL + (int64_t)(k + 1) * nt + k, nt, nullptr, 0, m, nt - 1 - k, epoch, d.fail, sh);
+        for (int r = k + 1; r < nt; ++r)
+            if (nz(r, k)) df_wait_run(fL + r * nt + k, 0, nullptr, 0, 0, 1, epoch, d.fail, sh);
         load_tile<64>(T2, LD, d.X + (int64_t)k * kDM * kDM, M);
-        if (la) load_tile<64>(T1, LD, tA(k + 1, k), (int)np);
+        if (la >= 0) load_tile<64>(T1, LD, tA(la, k), (int)np);
         __syncthreads();
         double mreg[16];
-        if (la) {
-            // M_k = X_k' L_k+1,k' (X lower: X[kk][m] = 0 for kk < m)
-    #pragma unroll
+        if (la >= 0) {
+            // M_k = X_k' L_la,k' (X lower: X[kk][m] = 0 for kk < m)
+#pragma unroll
             for (int q = 0; q < 4; ++q)
                 tile_st(T3, LD, 16 * wave, 16 * q,
                         tile_mm<true, true, false>(zero4(), T2, LD, 16 * wave, T1, LD, 16 * q, 16 * wave, M));
             __syncthreads();
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < 16; ++q) mreg[q] = T3[c * LD + 16 * g + q];
         }
         double* xs = T1;               // [2][64] x_i, double buffered
@@ -2587,15 +2643,16 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         __syncthreads();               // (T1's L tile is read)
         double s = 0.0;
         int buf = 0;
-        for (int i = nt - 1; i >= k + 2; --i) {   // x_i arrive in this order
-            const double* L = tA(i, k) + c;
+        for (int r = nt - 1; r > k; --r) {   // x_r arrive in this order
+            if (r == la || !nz(r, k)) continue;
+            const double* L = tA(r, k) + c;
             double lr[16];
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < 16; ++q) lr[q] = L[(int64_t)(4 * q + g) * np];
             double* xb = xs + M * buf;
-            if (wave == 0) get_y(d.xg + (int64_t)i * kYG, nullptr, xb, nullptr, epoch, d.fail);
+            if (wave == 0) get_y(d.xg + (int64_t)r * kYG, nullptr, xb, nullptr, epoch, d.fail);
             __syncthreads();
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < 16; ++q) s = fma(lr[q], xb[4 * q + g], s);
             buf ^= 1;
         }
@@ -2606,7 +2663,7 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         __syncthreads();
         // r_k = X_k' v (X lower: rows m >= c), rows 16 g .. 16 g + 15 per thread
         double u = 0.0;
-    #pragma unroll
+#pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int m = 16 * g + q;
             if (m >= c) u = fma(T2[m * LD + c], v[m], u);
@@ -2614,12 +2671,12 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         part2[g * M + c] = u;
         __syncthreads();
         double xv = ((part2[c] + part2[M + c]) + part2[2 * M + c]) + part2[3 * M + c];
-        if (la) {
+        if (la >= 0) {
             double* xb = xs + M * buf;
-            if (wave == 0) get_y(d.xg + (int64_t)(k + 1) * kYG, nullptr, xb, nullptr, epoch, d.fail);
+            if (wave == 0) get_y(d.xg + (int64_t)la * kYG, nullptr, xb, nullptr, epoch, d.fail);
             __syncthreads();
             double w = 0.0;
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < 16; ++q) w = fma(mreg[q], xb[16 * g + q], w);
             part3[g * M + c] = w;
             __syncthreads();
@@ -2627,15 +2684,20 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
         }
         if (threadIdx.x < M) {
             put_y(d.xg + (int64_t)k * kYG, c, xv, epoch);
-            const int64_t e = (int64_t)k * kDM + c;
+            const int64_t e = (int64_t)perm[k] * kDM + c;
             if (e < P.nF) P.yF[e] = xv;
         }
-        if (k == 0) {
-            // every task feeds x_0; the factor verdicts travel with the X flags
-            // (acquired here: the x granules carry no ordering)
-            for (int m = 0; m < nt;) m = df_wait_run(fL, nt + 1, nullptr, 0, m, nt, epoch, d.fail, sh);
-            if (threadIdx.x == 0) {
+        // the last back-substitution task to finish gives the verdict: every
+        // task's and chain's failure word is ordered before it (the flags'
+        // acquires, then this ticket's release sequence) -- and clears the
+        // words for the next solve (no pack pass clears them)
+        if (threadIdx.x == 0) {
+            unsigned* ticket = reinterpret_cast<unsigned*>(d.fail + 4);
+            if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nt - 1) {
                 P.scal[kScSolveFail] = solve_verdict(d.fail);
+                st_wt(d.fail, 0.0);
+                st_wt(d.fail + 1, 0.0);
+                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (d.stamps)
                     atomicAdd(d.stamps + 25, __builtin_amdgcn_s_memrealtime() -
                                                  __hip_atomic_load(d.stamps + 26, __ATOMIC_RELAXED,
@@ -2643,8 +2705,7 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             }
         }
     };
-    const int ntask = df_tasks(nt);
-    for (int t = blockIdx.x - 1; t < ntask; t += gridDim.x - 1) {
+    for (int t = (int)blockIdx.x - d.nch; t < d.ntask; t += (int)gridDim.x - d.nch) {
         __syncthreads();   // the previous task is done with the LDS tiles
         task(t);
     }
@@ -2657,14 +2718,215 @@ void dense_setup(DenseArgs& d, const DevProblem& P) {
     d.np = (int64_t)d.nt * kDM;
 }
 
+// ---- the dataflow solve's schedule (round 6) ----------------------------------
+// Tile pattern.  Camera blocks b, c (6 rows each, in the plan's order) couple
+// only within the half-bandwidth D; the intrinsics rows [nb, nF) couple with
+// everything; padding rows (>= nF) with nothing.  So 64-row tiles couple
+// within a tile bandwidth w, except the arrow tiles (those holding intrinsics
+// rows), which couple with all.
+// Order (one level of nested dissection, "twisted"): when the camera tiles
+// [0, tc) split as P1 = [0, h), a separator S = [h, h + w) and P2 = [h + w, tc),
+// P1 and P2 do not couple.  They are factored at the same time by two chain
+// workgroups -- P1 forward, P2 backward (from its far end towards S, so that
+// its fill stays in its band and S's rows fill only in P2's last w columns)
+// -- and S and the arrow tiles after both, by chain 0.  Permuted order:
+// P1, P2 reversed, S, arrow.  The chains are about half as long (the C5
+// loop's orbit: nt 29 -> 16 columns on the longer chain).
+// Pattern of L: the permuted pattern of S plus its symbolic fill (tile level).
+// Chain k links to its previous column p (forms L_kp = A~_kp X_p' itself with
+// X_p still in LDS) when L_kp is nonzero and no column j between them needs
+// L_kp first (L_kj with L_jp nonzero: T(k, j) would wait for the chain).
+// Tasks: D(k) A~_kk, S(k) A~_kp (the chain's inputs, left-looking sums over
+// the nonzero L_km, L_pm), T(i, j) L_ij, Y(j) forward, B(k) back substitution.
+// Their order: by the earliest start a list schedule with unbounded workers
+// gives them (each node's start exceeds its inputs'), so every task waits only
+// on earlier tasks and on chain steps that wait only on earlier tasks -- the
+// lowest unfinished node can always run (each worker takes tasks in order).
+
+std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
+    d.flow = !d.chain && d.nt <= kDenseFlowMaxNt;
+    d.nch = d.ntask = 0;
+    d.meta_words = 0;
+    if (!d.flow) return {};
+    const int nt = d.nt;
+    // natural tile pattern
+    auto cam_range = [&](int t, int& b0, int& b1) {
+        const int64_t r0 = (int64_t)t * kDM, r1 = std::min<int64_t>(r0 + kDM, P.nb);
+        if (r0 >= r1) return false;
+        b0 = (int)(r0 / 6);
+        b1 = (int)((r1 - 1) / 6);
+        return true;
+    };
+    auto arrow = [&](int t) { return (int64_t)t * kDM < P.nF && (int64_t)t * kDM + kDM > P.nb; };
+    auto couple = [&](int a, int b) {   // natural tiles a > b
+        int a0, a1, b0, b1;
+        const bool ca = cam_range(a, a0, a1), cb = cam_range(b, b0, b1);
+        if (arrow(a) && (cb || arrow(b))) return true;
+        if (arrow(b) && ca) return true;
+        return ca && cb && a0 - b1 <= P.D;
+    };
+    int tc = nt, w = 0;
+    for (int t = 0; t < nt; ++t)
+        if (arrow(t)) { tc = t; break; }
+    for (int a = 0; a < tc; ++a)
+        for (int b = 0; b < a; ++b)
+            if (couple(a, b)) w = std::max(w, a - b);
+    std::vector<int> perm(nt), c0, c1;
+    for (int t = 0; t < nt; ++t) perm[t] = t;
+    const int len = tc - w, h = (len + 1) / 2, n2 = len - h;
+    const bool split = w >= 1 && n2 >= 2 && !std::getenv("SFM_DENSE_NO_SPLIT");
+    if (split) {
+        int q = 0;
+        for (int t = 0; t < h; ++t) perm[q++] = t;
+        for (int t = tc - 1; t >= h + w; --t) perm[q++] = t;
+        for (int t = h; t < h + w; ++t) perm[q++] = t;
+        for (int t = tc; t < nt; ++t) perm[q++] = t;
+        for (int k = 0; k < h; ++k) c0.push_back(k);
+        for (int k = h; k < h + n2; ++k) c1.push_back(k);
+        for (int k = h + n2; k < nt; ++k) c0.push_back(k);
+    } else {
+        for (int k = 0; k < nt; ++k) c0.push_back(k);
+    }
+    // pattern of L (permuted, lower, with fill)
+    std::vector<char> nz((size_t)nt * nt, 0);
+    auto NZ = [&](int i, int j) -> char& { return nz[(size_t)i * nt + j]; };
+    for (int i = 0; i < nt; ++i) {
+        NZ(i, i) = 1;
+        for (int j = 0; j < i; ++j) NZ(i, j) = couple(std::max(perm[i], perm[j]), std::min(perm[i], perm[j]));
+    }
+    for (int k = 0; k < nt; ++k)
+        for (int i = k + 1; i < nt; ++i)
+            if (NZ(i, k))
+                for (int j = k + 1; j < i; ++j)
+                    if (NZ(j, k)) NZ(i, j) = 1;
+    // chains: previous column, link, chain inputs
+    std::vector<int> prev(nt, -1), next(nt, -1), info(nt, 0), la(nt, -1);
+    for (const auto* c : {&c0, &c1})
+        for (size_t q = 1; q < c->size(); ++q) {
+            prev[(*c)[q]] = (*c)[q - 1];
+            next[(*c)[q - 1]] = (*c)[q];
+        }
+    auto linked = [&](int k) { return (info[k] & 1) != 0; };
+    for (int k = 0; k < nt; ++k) {
+        const int p = prev[k];
+        bool ln = p >= 0 && NZ(k, p);
+        for (int j = p + 1; ln && j < k; ++j)
+            if (NZ(j, p) && NZ(k, j)) ln = false;
+        if (ln) info[k] |= 1;
+        for (int m = 0; m < k; ++m)
+            if (NZ(k, m) && !(ln && m == p)) info[k] |= 2;   // D(k) has terms
+        for (int m = 0; ln && m < p; ++m)
+            if (NZ(k, m) && NZ(p, m)) info[k] |= 4;           // S(k) has terms
+        for (int i = k + 1; i < nt && la[k] < 0; ++i)
+            if (NZ(i, k)) la[k] = i;
+    }
+    // tasks and their inputs (node ids: chain step k = k, task t = nt + t)
+    std::vector<int32_t> code;
+    std::vector<std::vector<int>> dep;
+    std::vector<double> dur;
+    std::vector<int> t_of((size_t)nt * nt, -1), d_of(nt, -1), s_of(nt, -1), y_of(nt, -1), b_of(nt, -1);
+    auto L_node = [&](int i, int j) { return (linked(i) && prev[i] == j) ? i : nt + t_of[(size_t)i * nt + j]; };
+    auto X_node = [&](int j) { return (next[j] >= 0 && linked(next[j])) ? next[j] : j; };
+    auto add = [&](int kind, int i, int j) {
+        code.push_back((kind << 24) | (i << 12) | j);
+        dep.emplace_back();
+        dur.push_back(1.0);
+        return (int)code.size() - 1;
+    };
+    // create every task first (the inputs refer to them by id)
+    for (int k = 0; k < nt; ++k) {
+        if (info[k] & 2) d_of[k] = add(kTaskD, k, k);
+        if (info[k] & 4) s_of[k] = add(kTaskS, k, prev[k]);
+    }
+    for (int j = 0; j < nt; ++j)
+        for (int i = j + 1; i < nt; ++i)
+            if (NZ(i, j) && !(linked(i) && prev[i] == j)) t_of[(size_t)i * nt + j] = add(kTaskT, i, j);
+    for (int j = 0; j < nt; ++j) y_of[j] = add(kTaskY, j, j);
+    for (int k = 0; k < nt; ++k) b_of[k] = add(kTaskB, k, k);
+    for (size_t t = 0; t < code.size(); ++t) {
+        const int kind = code[t] >> 24, i = (code[t] >> 12) & 0xfff, j = code[t] & 0xfff;
+        auto& dp = dep[t];
+        double terms = 0;
+        if (kind == kTaskD || kind == kTaskS || kind == kTaskT) {
+            const int jj = kind == kTaskD ? i : j, mend = kind == kTaskD ? i : jj;
+            for (int m = 0; m < mend; ++m) {
+                if (kind == kTaskD && linked(i) && m == prev[i]) continue;
+                if (!NZ(i, m) || !NZ(jj, m)) continue;
+                dp.push_back(L_node(i, m));
+                if (jj != i) dp.push_back(L_node(jj, m));
+                terms += 1;
+            }
+            if (kind == kTaskT) dp.push_back(X_node(j));
+            dur[t] = 2.0 + terms;
+        } else if (kind == kTaskY) {
+            dp.push_back(X_node(j));
+            for (int m = 0; m < j; ++m)
+                if (NZ(j, m)) { dp.push_back(L_node(j, m)); dp.push_back(nt + y_of[m]); terms += 1; }
+            dur[t] = 1.0 + 0.3 * terms;
+        } else {
+            dp.push_back(X_node(i));
+            dp.push_back(nt + y_of[i]);
+            for (int r = i + 1; r < nt; ++r)
+                if (NZ(r, i)) { dp.push_back(L_node(r, i)); dp.push_back(nt + b_of[r]); terms += 1; }
+            dur[t] = 1.0 + 0.3 * terms;
+        }
+    }
+    // earliest starts (memoised over the DAG; chain steps take 20 units)
+    const int nn = nt + (int)code.size();
+    std::vector<double> est(nn, -1.0);
+    std::vector<char> busy(nn, 0);
+    std::function<double(int)> fin = [&](int v) -> double {
+        if (est[v] < 0) {
+            SFM_REQUIRE(!busy[v], SFM_ERR_UNSUPPORTED, "dense dataflow schedule: cyclic inputs");
+            busy[v] = 1;
+            double e = 0.0;
+            if (v < nt) {
+                if (prev[v] >= 0) e = std::max(e, fin(prev[v]));
+                if (d_of[v] >= 0) e = std::max(e, fin(nt + d_of[v]));
+                if (s_of[v] >= 0) e = std::max(e, fin(nt + s_of[v]));
+            } else {
+                for (int u : dep[v - nt]) e = std::max(e, fin(u));
+            }
+            est[v] = e;
+        }
+        return est[v] + (v < nt ? 20.0 : dur[v - nt]);
+    };
+    for (int v = 0; v < nn; ++v) fin(v);
+    std::vector<int> order(code.size());
+    for (size_t t = 0; t < order.size(); ++t) order[t] = (int)t;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        if (est[nt + a] != est[nt + b]) return est[nt + a] < est[nt + b];
+        return (code[a] >> 24) < (code[b] >> 24);
+    });
+    // meta: perm | prev | info | la | chain 0 | chain 1 | lengths (2) | tasks | pattern bytes
+    d.nch = c1.empty() ? 1 : 2;
+    d.ntask = (int)code.size();
+    std::vector<int32_t> meta(6 * (size_t)nt + 2 + code.size() + ((size_t)nt * nt + 3) / 4, 0);
+    for (int k = 0; k < nt; ++k) {
+        meta[k] = perm[k];
+        meta[nt + k] = prev[k];
+        meta[2 * nt + k] = info[k];
+        meta[3 * nt + k] = la[k];
+    }
+    for (size_t q = 0; q < c0.size(); ++q) meta[4 * nt + q] = c0[q];
+    for (size_t q = 0; q < c1.size(); ++q) meta[5 * nt + q] = c1[q];
+    meta[6 * nt] = (int32_t)c0.size();
+    meta[6 * nt + 1] = (int32_t)c1.size();
+    for (size_t q = 0; q < order.size(); ++q) meta[6 * nt + 2 + q] = code[order[q]];
+    std::memcpy(meta.data() + 6 * nt + 2 + code.size(), nz.data(), nz.size());
+    d.meta_words = (int64_t)meta.size();
+    return meta;
+}
+
 // flags: x (nt), L tiles + chain inputs (2 nt^2), y (nt); then (8-byte
 // aligned) the dataflow back substitution's tagged x granules (kYG per column)
 static size_t dense_granule_word(const DenseArgs& d) { return ((size_t)d.nt + 2 * (size_t)d.nt * d.nt + d.nt + 1) & ~(size_t)1; }
 size_t dense_flag_words(const DenseArgs& d) { return dense_granule_word(d) + 2 * (size_t)kYG * d.nt; }
 
 size_t dense_doubles(const DenseArgs& d) {
-    // A | X | b y x | fail (8) | flags and granules
-    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8 + (dense_flag_words(d) + 1) / 2 + 2;
+    // A | X | b y x | fail (8) | flags and granules | the dataflow schedule
+    return (size_t)d.np * d.np + (size_t)d.nt * kDM * kDM + 3 * (size_t)d.np + 8 + (dense_flag_words(d) + 1) / 2 + 2 +
+           ((size_t)d.meta_words + 1) / 2 + 1;
 }
 
 void dense_bind(DenseArgs& d, double* base) {
@@ -2677,35 +2939,35 @@ void dense_bind(DenseArgs& d, double* base) {
     d.xflag = reinterpret_cast<unsigned*>(d.fail + 8);   // zeroed by the caller once
     d.fflag = d.xflag + d.nt;
     d.xg = reinterpret_cast<unsigned long long*>(d.xflag + dense_granule_word(d));
+    d.meta = reinterpret_cast<const int32_t*>(d.xflag + ((dense_flag_words(d) + 1) & ~(size_t)1));
 }
 
 void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
     const int64_t n2 = d.np * d.np;
-    hipLaunchKernelGGL(dense_pack_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d, P, radius);
-    SFM_HIP(hipGetLastError());
     const size_t lds_p = (3 * M * LD + 2) * sizeof(double), lds_u = 2 * M * LD * sizeof(double);
     set_dyn_lds((const void*)dense_panel_kernel, lds_p);
     set_dyn_lds((const void*)dense_update_kernel, lds_u);
     const int n_cu = device_cu_count();
-    // up to 29 block columns (the C5 loop's systems) the dataflow kernel; at
-    // dense-S's 94 it only equals the launch chain, which
-    // stays the form for wider systems (and every system under
-    // SFM_CTX_BA_DENSE_CHAIN)
-    constexpr int kFlowMaxNt = 29;
-    if (!d.chain && d.nt <= kFlowMaxNt) {
+    // up to kDenseFlowMaxNt block columns (the C5 loop's systems) the
+    // dataflow kernel; at dense-S's 94 it only equals the launch chain
+    // (DESIGN.md §5), which stays the form for wider systems (and every system
+    // under SFM_CTX_BA_DENSE_CHAIN)
+    if (d.flow) {
         // factorisation and both substitutions in one dataflow launch: the
-        // chain workgroup and up to n_cu - 1 task workers, one workgroup per CU
-        // (the LDS request forces it): the chain's pivot wave must not share
-        // its SIMD with another workgroup's fp64 MFMAs, which stall its fp64
-        // VALU (15x in tools/probe/diag16_probe.hip), and every workgroup is
-        // resident, so every wait ends
+        // chain workgroups and up to n_cu - nch task workers, one workgroup
+        // per CU (the LDS request forces it): a chain's pivot wave must not
+        // share its SIMD with another workgroup's fp64 MFMAs, which stall its
+        // fp64 VALU (15x in tools/probe/diag16_probe.hip), and every workgroup
+        // is resident, so every wait ends
         const size_t lds_f = std::max<size_t>(kDfLds * sizeof(double), 81 * 1024);
         set_dyn_lds((const void*)dense_flow_kernel, lds_f);
-        const int workers = std::min(df_tasks(d.nt), n_cu - 1);
-        hipLaunchKernelGGL(dense_flow_kernel, dim3(1 + workers), dim3(NT), lds_f, s, d, P, epoch);
+        const int workers = std::min(d.ntask, n_cu - d.nch);
+        hipLaunchKernelGGL(dense_flow_kernel, dim3(d.nch + workers), dim3(NT), lds_f, s, d, P, radius, epoch);
         SFM_HIP(hipGetLastError());
         return;
     }
+    hipLaunchKernelGGL(dense_pack_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d, P, radius);
+    SFM_HIP(hipGetLastError());
     // block columns in groups of W = kDenseW: panel c, then the group's
     // later columns updated from column c alone (rhs of column c fused), ...;
     // after the group's last panel every later tile is updated from all W

@@ -60,6 +60,7 @@ struct sfm_ba_plan {
     DBuf<int32_t> zbatch, zlong;
     DBuf<PTerm> pterms;
     DBuf<double> Zbuf, dense_buf;
+    std::vector<int32_t> dense_meta;   // the dense dataflow solve's schedule (host copy, dense_flow_plan)
     DenseArgs dense;
     DBuf<double> lpart;           // long-target segment partials [n_lseg][36]
     DBuf<unsigned> lcount;        // per long target: segment tickets of the fused reduce
@@ -421,9 +422,15 @@ bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     if (h.dense) {
         dense_setup(pl->dense, P);
         pl->dense.chain = (ctx->flags & SFM_CTX_BA_DENSE_CHAIN) != 0;
+        pl->dense_meta = dense_flow_plan(pl->dense, P);   // the dataflow solve's schedule (host)
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
-        SFM_HIP(hipMemsetAsync(pl->dense.xflag, 0, sizeof(unsigned) * dense_flag_words(pl->dense), s));
+        // failure words, tickets, flags and granules: zeroed once (the dataflow
+        // solve clears its failure words itself after each verdict)
+        SFM_HIP(hipMemsetAsync(pl->dense.fail, 0, 8 * sizeof(double) + sizeof(unsigned) * dense_flag_words(pl->dense), s));
+        if (!pl->dense_meta.empty())
+            SFM_HIP(hipMemcpyAsync(const_cast<int32_t*>(pl->dense.meta), pl->dense_meta.data(),
+                                   pl->dense_meta.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
         if (std::getenv("SFM_DENSE_STAMPS")) {
             pl->bcr_stamps.alloc(32);   // chain phases [0, 8), chol_inv64's [8, 24), real time [24, 28)
             pl->bcr_stamps.zero(s);
@@ -1135,4 +1142,24 @@ extern "C" int sfm_ba_solve(sfm_ctx* ctx, const sfm_ba_problem* prob, double* ex
     else sfm_ba_plan_destroy(pl);
     tm.mark(keep ? "cached" : "destroy");
     return rc;
+}
+
+extern "C" int sfm_ba_dense_schedule(const sfm_ba_problem* prob, int32_t* out, int64_t cap, int64_t* n_words,
+                                     int32_t* shape) {
+    using namespace sfm;
+    return guarded([&] {
+        SFM_REQUIRE(prob && n_words && shape && cap >= 0 && (out || cap == 0), SFM_ERR_INVALID_ARG, "bad arguments");
+        BAHostPlan h;
+        build_plan(*prob, 0, 1, h);
+        DevProblem P{};
+        P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D; P.nb = h.nb; P.nF = h.nF; P.iw = h.iw;
+        DenseArgs d;
+        dense_setup(d, P);
+        const std::vector<int32_t> meta = h.dense ? dense_flow_plan(d, P) : std::vector<int32_t>();
+        shape[0] = d.nt; shape[1] = d.nch; shape[2] = d.ntask; shape[3] = (h.dense && d.flow) ? 1 : 0;
+        shape[4] = (int32_t)h.nF; shape[5] = (int32_t)h.nb; shape[6] = h.D;
+        *n_words = (int64_t)meta.size();
+        if ((int64_t)meta.size() <= cap && !meta.empty()) std::memcpy(out, meta.data(), meta.size() * sizeof(int32_t));
+        return SFM_OK;
+    });
 }

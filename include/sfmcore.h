@@ -338,6 +338,16 @@ int sfm_ba_describe(const sfm_ba_problem* prob, int32_t rank, int32_t world_size
 int sfm_ba_grown_digest(const sfm_ba_problem* prev, const sfm_ba_problem* prob, uint64_t* digest_fresh,
                         uint64_t* digest_grown, int64_t* reused);
 
+/* [cpu] Diagnostic (tests): the schedule of the dense RCS dataflow solve
+ * (dense_flow_kernel) for `prob`'s plan, as the device reads it: permuted
+ * tile order | previous column per chain | link / D / S bits | lookahead row
+ * | chain 0 list | chain 1 list | the two lengths | tasks (kind << 24 | i << 12
+ * | j, in execution order) | the tile pattern of L (nt * nt bytes).  Copies it
+ * to out when *n_words <= cap (cap 0: size query).  shape[7] = {nt, chains,
+ * tasks, 1 if the dataflow solve runs, nF, nb, camera half-bandwidth}; no schedule (n_words 0) for a
+ * band problem or a system over the dataflow solve's size. */
+int sfm_ba_dense_schedule(const sfm_ba_problem* prob, int32_t* out, int64_t cap, int64_t* n_words, int32_t* shape);
+
 /* [cpu] Landmark-block partition: contiguous point ranges of the
  * (min-camera)-sorted point order with ~equal observation counts.
  * order[n_pt] receives the sorted point order, bounds[world_size+1] the

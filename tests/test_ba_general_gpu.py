@@ -238,25 +238,32 @@ def _solves_under_load(load, sc, flags, solver, reps=3):
             assert abs(gs.rmse_final / os_.rmse_final - 1) < 1e-6
 
 
-@pytest.mark.parametrize("chain", [True, False])
-def test_dense_solve_under_contention(chain):
+@pytest.mark.parametrize("chain,split", [(True, False), (False, False), (False, True)])
+def test_dense_solve_under_contention(chain, split):
     """the dense RCS solved while another context keeps the
     CUs busy -- the condition under which dense_panel_kernel's former store of
     L_kk over A_kk (round 4) corrupted the panels of late
     workgroups, and under which the dataflow kernels (dense_flow_kernel,
     dense_back_all_kernel) wait for workgroups that are not resident yet.
     chain: the launch chain (panel + trailing-update launches); else the
-    dataflow kernels.  Both must take the oracle's decisions, with the matcher
-    provably running during the solves."""
-    sc = H.Scene(100, 12000, 8, vis_mode=1, seed=2718)   # random visibility: dense RCS, 10 block columns
+    dataflow kernels.  split (round 6): a camera band of 13 blocks (14-view
+    tracks, too wide for the BCR solver), which the dataflow schedule factors
+    with two chain workgroups (nested dissection, dense_flow_plan).  Each must
+    take the oracle's decisions, with the matcher provably running during the
+    solves."""
+    if split:   # banded orbit, 14 views per point: 19 block columns, two chains
+        sc = H.Scene(200, 20000, 14, seed=2719)
+        assert api.ba_dense_schedule(sc.problem())[0]["chains"] == 2
+    else:       # random visibility: dense RCS, 10 block columns
+        sc = H.Scene(100, 12000, 8, vis_mode=1, seed=2718)
     flags = abi.SFM_CTX_BA_DENSE_RCS | (abi.SFM_CTX_BA_DENSE_CHAIN if chain else 0)
     with _MatcherLoad() as load:
         _solves_under_load(load, sc, flags, abi.SFM_RCS_DENSE)
 
 
 # VERDICT r5 item 2 / ADVICE r5: the default band path's inter-workgroup
-# hand-offs under the same load (DESIGN.md §5, "Residency of the BCR
-# hand-offs"): the fused top + corner (workgroup 0 polls the tagged corner sum
+# hand-offs under the same load (DESIGN.md §5, "Residency assumptions of the
+# inter-workgroup hand-offs"): the fused top + corner (workgroup 0 polls the tagged corner sum
 # the last of blocks 1..N-1 publishes), the back substitution's tagged y
 # granules (a block waits for its two neighbours, in-order dispatch), and the
 # forward levels.  Shapes: a C4-shaped band (K = 9, one intrinsics block:
