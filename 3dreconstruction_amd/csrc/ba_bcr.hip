@@ -2306,7 +2306,7 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
 // per CU, at most n_cu: the caller) and the task workers take tasks round
 // robin in an order where every input comes from a lower task or the chain,
 // so every wait ends; spins are bounded (a timeout fails the solve).
-constexpr int kDfLds = 3 * M * LD + 32;   // doubles: three tiles + small state
+constexpr int kDfLds = 4 * M * LD + 32;   // doubles: four tiles + small state
 
 __device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2396,7 +2396,8 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
     double* T1 = sm;
     double* T2 = sm + M * LD;
     double* T3 = T2 + M * LD;      // the chain's diagonal tile; a task's first A tile
-    double* bad = T3 + M * LD;     // [2]
+    double* T4 = T3 + M * LD;      // a D / S task's X_m (an L_im formed in place)
+    double* bad = T4 + M * LD;     // [2]
     double* col = bad + 2;         // [16] (diag16)
     int* sh = reinterpret_cast<int*>(col + 16);
     const int nt = d.nt, wave = threadIdx.x >> 6;
@@ -2410,6 +2411,8 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
     const int32_t* info = d.meta + 2 * nt;   // 1 linked to prevc, 2 D(k) task, 4 S(k) task
     const int32_t* lav = d.meta + 3 * nt;    // the back substitution's lookahead row
     const int32_t* tasks = d.meta + 6 * nt + 2;
+    // tile pattern of L: bit 0 nonzero, bit 1 formed by a T task with no
+    // terms (L_ij = A_ij X_j', which a D / S task forms itself: dense_flow_plan)
     const unsigned char* nzb = reinterpret_cast<const unsigned char*>(tasks + d.ntask);
     auto nz = [&](int i, int j) { return nzb[i * nt + j] != 0; };
     auto tA = [&](int i, int j) { return d.A + (int64_t)perm[i] * kDM * np + (int64_t)perm[j] * kDM; };
@@ -2532,11 +2535,30 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             v4d acc[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc[c] = (diag && c > wave) ? zero4() : tile_ld(T3, LD, 16 * wave, 16 * c);
+            __syncthreads();   // (T3 is reused below)
             for (int m = 0; m < mend; ++m) {
-                if (m == excl || !nz(i, m) || (!diag && !nz(j, m))) continue;
-                df_wait_run(fL + i * nt + m, 0, diag ? nullptr : fL + j * nt + m, 0, 0, 1, epoch, d.fail, sh);
-                if (diag) load_tile<64>(T1, LD, tA(i, m), (int)np);
-                else load_tiles2(T1, tA(i, m), T2, tA(j, m), (int)np);
+                const int zi = nzb[i * nt + m];
+                if (m == excl || !zi || (!diag && !nz(j, m))) continue;
+                if ((zi & 2) && kind != kTaskT) {
+                    // L_im = A_im X_m' formed here, from the values T(i, m) uses
+                    // (same products, same bits): the chain's inputs wait on
+                    // X_m instead of on T(i, m)'s hand-off (round 6)
+                    df_load_a(T3, P, radius, perm[i], perm[m]);
+                    df_wait_run(fL + m * nt + m, 0, diag ? nullptr : fL + j * nt + m, 0, 0, 1, epoch, d.fail, sh);
+                    load_tile<64>(T4, LD, d.X + (int64_t)m * kDM * kDM, M);
+                    if (!diag) load_tile<64>(T2, LD, tA(j, m), (int)np);
+                    __syncthreads();
+                    v4d l[4];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        l[c] = tile_mm<false, true, false>(zero4(), T3, LD, 16 * wave, T4, LD, 16 * c, 0, 16 * c + 16);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) tile_st(T1, LD, 16 * wave, 16 * c, l[c]);
+                } else {
+                    df_wait_run(fL + i * nt + m, 0, diag ? nullptr : fL + j * nt + m, 0, 0, 1, epoch, d.fail, sh);
+                    if (diag) load_tile<64>(T1, LD, tA(i, m), (int)np);
+                    else load_tiles2(T1, tA(i, m), T2, tA(j, m), (int)np);
+                }
                 __syncthreads();
                 const double* Lb = diag ? T1 : T2;
 #pragma unroll
@@ -2843,6 +2865,17 @@ std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
             if (NZ(i, j) && !(linked(i) && prev[i] == j)) t_of[(size_t)i * nt + j] = add(kTaskT, i, j);
     for (int j = 0; j < nt; ++j) y_of[j] = add(kTaskY, j, j);
     for (int k = 0; k < nt; ++k) b_of[k] = add(kTaskB, k, k);
+    // T tasks with no terms (L_ij = A_ij X_j'): a D / S task forms such an
+    // L_im itself (pattern bit 1)
+    auto t_terms = [&](int i, int j) {
+        int n = 0;
+        for (int m = 0; m < j; ++m) n += NZ(i, m) && NZ(j, m);
+        return n;
+    };
+    std::vector<char> simple((size_t)nt * nt, 0);
+    for (int j = 0; j < nt; ++j)
+        for (int i = j + 1; i < nt; ++i)
+            if (t_of[(size_t)i * nt + j] >= 0 && t_terms(i, j) == 0) simple[(size_t)i * nt + j] = 1;
     for (size_t t = 0; t < code.size(); ++t) {
         const int kind = code[t] >> 24, i = (code[t] >> 12) & 0xfff, j = code[t] & 0xfff;
         auto& dp = dep[t];
@@ -2852,6 +2885,12 @@ std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
             for (int m = 0; m < mend; ++m) {
                 if (kind == kTaskD && linked(i) && m == prev[i]) continue;
                 if (!NZ(i, m) || !NZ(jj, m)) continue;
+                if (kind != kTaskT && simple[(size_t)i * nt + m]) {
+                    dp.push_back(X_node(m));
+                    if (jj != i) dp.push_back(L_node(jj, m));
+                    terms += 2;
+                    continue;
+                }
                 dp.push_back(L_node(i, m));
                 if (jj != i) dp.push_back(L_node(jj, m));
                 terms += 1;
@@ -2913,6 +2952,7 @@ std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
     meta[6 * nt] = (int32_t)c0.size();
     meta[6 * nt + 1] = (int32_t)c1.size();
     for (size_t q = 0; q < order.size(); ++q) meta[6 * nt + 2 + q] = code[order[q]];
+    for (size_t e = 0; e < nz.size(); ++e) nz[e] = (char)(nz[e] | (simple[e] ? 2 : 0));
     std::memcpy(meta.data() + 6 * nt + 2 + code.size(), nz.data(), nz.size());
     d.meta_words = (int64_t)meta.size();
     return meta;

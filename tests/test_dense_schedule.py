@@ -125,13 +125,18 @@ def replay(sh, meta, S, rhs, workers):
                 diag = kind == 0
                 excl = prev[i] if diag and info[i] & 1 else -1
                 ms = [m for m in range(i if diag else j) if m != excl and nz[i, m] and (diag or nz[j, m])]
-                if not all(("L", i, m) in avail and ("L", j, m) in avail for m in ms):
+                # a D / S task forms a terms-free L_im (pattern bit 1) itself from X_m
+                local = {m for m in ms if kind != 2 and nz[i, m] & 2}
+                if not all((("X", m) if m in local else ("L", i, m)) in avail and ("L", j, m) in avail
+                           for m in ms if j != i or m not in local) or \
+                        not all(("X", m) in avail for m in local):
                     continue
                 if kind == 2 and ("X", j) not in avail:
                     continue
                 acc = T(Ap, i, j).copy()
                 for m in ms:
-                    acc -= Lt[(i, m)] @ Lt[(j, m)].T
+                    Li = T(Ap, i, m) @ X[m].T if m in local else Lt[(i, m)]
+                    acc -= Li @ (Li if j == i else Lt[(j, m)]).T
                 if kind == 2:
                     Lt[(i, j)] = acc @ X[j].T
                     avail.add(("L", i, j))
