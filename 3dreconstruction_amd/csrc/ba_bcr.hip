@@ -2005,7 +2005,8 @@ void bcr_solve(const BcrArgs& b, const DevProblem& P, double radius, hipStream_t
 // 64x64 fp64 tiles.  Used when the cameras do not form a narrow band (random
 // visibility, long tracks, many intrinsics blocks) -- Ceres' SPARSE_SCHUR +
 // EIGEN_SPARSE (BundleAdjuster.h:171-173) factors the same matrix.
-//   pack      A = lower(S) + D^2 (Ceres' LM diagonal), identity padding; b = rhs
+//   A         lower(S) + D^2 (Ceres' LM diagonal), identity padding; b = rhs --
+//             formed by each tile's first reader (pack_elem), no pack pass
 //   step k    panel: every workgroup of column k factors A_kk (chol_inv64:
 //             L_kk and X_kk = L_kk^-1, MFMA) and forms L_ik = A_ik X_kk';
 //             the k-th one stores L_kk, X_kk and y_k = X_kk b_k
@@ -2022,29 +2023,35 @@ constexpr int kDenseW = 4;   // block columns per trailing update
 constexpr int kDenseFlowMaxNt = 29;   // the dataflow solve up to this many block columns
 enum : int { kTaskD = 0, kTaskS = 1, kTaskT = 2, kTaskY = 3, kTaskB = 4 };   // dataflow tasks (dense_flow_plan)
 
-__global__ __launch_bounds__(256) void dense_pack_kernel(DenseArgs d, DevProblem P, double radius) {
-    const int64_t np = d.np;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e < np * np) {
-        const int64_t i = e / np, j = e % np;
-        double v = 0.0;
-        if (i < P.nF && j < P.nF) {
-            if (j <= i) v = P.Sdense[i * P.nF + j];
-            if (i == j) {
-                const double lm = sqrt(clampd(P.cnF[i], P.min_diag, P.max_diag) / radius);
-                v += lm * lm;
-            }
-        } else if (i == j) {
-            v = 1.0;
+__device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A's first values: lower(S) + D^2 (Ceres' LM diagonal), identity padding,
+// 0 above the diagonal, at (a, b).  No pack pass (round 6): each tile's first
+// reader -- the first panel, the first group's updates, a dataflow task --
+// forms it from the reduce's lower-triangle S (one np^2 write and read less:
+// 96 us per dense-S solve)
+__device__ __forceinline__ double pack_elem(const DevProblem& P, double radius, int64_t a, int64_t b) {
+    if (a < P.nF && b < P.nF) {
+        double v = b <= a ? P.Sdense[a * P.nF + b] : 0.0;
+        if (a == b) {
+            const double lm = sqrt(clampd(P.cnF[a], P.min_diag, P.max_diag) / radius);
+            v += lm * lm;
         }
-        d.A[e] = v;
+        return v;
     }
-    if (e < np) d.b[e] = e < P.nF ? P.rhs[e] : 0.0;
-    if (e == 0) { d.fail[0] = 0.0; d.fail[1] = 0.0; }
+    return a == b ? 1.0 : 0.0;
+}
+__device__ __forceinline__ double pack_rhs(const DevProblem& P, int64_t e) { return e < P.nF ? P.rhs[e] : 0.0; }
+// tile (i, j)'s first values into LDS [64][LD] (i >= j)
+__device__ __forceinline__ void pack_tile(double* T, const DevProblem& P, double radius, int i, int j) {
+    for (int e = threadIdx.x; e < M * M; e += NT)
+        T[(e / M) * LD + e % M] = pack_elem(P, radius, (int64_t)i * kDM + e / M, (int64_t)j * kDM + e % M);
 }
 
 // column k: workgroup w handles row tile i = k + w
-__global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
+__global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, DevProblem P, double radius, int k) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* Akk = sm;                 // [64][LD]
     double* Xkk = Akk + M * LD;       // [64][LD]
@@ -2056,8 +2063,17 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
     // A_kk and A_ik in flight together (round 6: one memory latency, not two)
     for (int e = threadIdx.x; e < M * LD; e += NT) Xkk[e] = 0.0;
     if (threadIdx.x == 0) flag[0] = 0.0;
-    if (i > k) load_tiles2(Akk, src, Aik, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
-    else load_tile<64>(Akk, LD, src, (int)np);
+    if (k == 0) {   // the tiles' first reader
+        pack_tile(Akk, P, radius, 0, 0);
+        if (i > k) pack_tile(Aik, P, radius, i, 0);
+    } else if (i > k) {
+        load_tiles2(Akk, src, Aik, d.A + (int64_t)i * kDM * np + (int64_t)k * kDM, (int)np);
+    } else {
+        load_tile<64>(Akk, LD, src, (int)np);
+    }
+    double* bk = Aik;   // (the diagonal workgroup's b_k, LDS)
+    if (i == k && threadIdx.x < M)
+        bk[threadIdx.x] = k == 0 ? pack_rhs(P, threadIdx.x) : d.b[(int64_t)k * kDM + threadIdx.x];
     __syncthreads();
     chol_inv64<NT / 64, NoPre, NoPre, NoBg, true>(Akk, Xkk, flag, flag + 1);
     const int wave = threadIdx.x >> 6;
@@ -2070,10 +2086,10 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
         // That was the round-3 look-ahead's wrong solves.
         double* xd = d.X + (int64_t)k * kDM * kDM;
         for (int e = threadIdx.x; e < M * M; e += NT) xd[e] = Xkk[(e / M) * LD + e % M];
-        // y_k = X_kk b_k (b_k final: every earlier column's update is done)
+        // y_k = X_kk b_k (b_k final: every earlier column's update is done;
+        // staged in LDS above)
         if (threadIdx.x < M) {
             const int r = threadIdx.x;
-            const double* bk = d.b + (int64_t)k * kDM;
             double s = 0.0;
             for (int c = 0; c <= r; ++c) s += Xkk[r * LD + c] * bk[c];
             d.y[(int64_t)k * kDM + r] = s;
@@ -2096,22 +2112,32 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, int k) {
 // write of A_ij per launch instead of per column; the fp64 MFMA chain is the
 // same, so the result is bit-identical); then rhs tiles i > rc get
 // b_i -= L_i,rc y_rc (forward substitution, fused).
-__global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, int kw, int j0, int n_tiles,
-                                                          int nw, int rc) {
+__global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, DevProblem P, double radius, int k0, int kw,
+                                                          int j0, int n_tiles, int nw, int rc) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* Li = sm;
     double* Lj = sm + M * LD;
     const int64_t np = d.np;
     const int t = blockIdx.x;
     if (t >= n_tiles) {   // rhs tile i: b_i -= L_i,rc y_rc
+        // thread (g, r): columns 16 g .. 16 g + 15 of row r, every load issued
+        // first; the four partials summed in a fixed order
         const int i = rc + 1 + (t - n_tiles);
+        const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
+        const double* L = d.A + ((int64_t)i * kDM + r) * np + (int64_t)rc * kDM + 16 * g;
+        const double* yk = d.y + (int64_t)rc * kDM + 16 * g;
+        double lv[16], yv[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) { lv[c] = L[c]; yv[c] = yk[c]; }
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) s = fma(lv[c], yv[c], s);
+        sm[g * M + r] = s;
+        __syncthreads();
         if (threadIdx.x < M) {
-            const int r = threadIdx.x;
-            const double* L = d.A + ((int64_t)i * kDM + r) * np + (int64_t)rc * kDM;
-            const double* yk = d.y + (int64_t)rc * kDM;
-            double s = 0.0;
-            for (int c = 0; c < M; ++c) s += L[c] * yk[c];
-            d.b[(int64_t)i * kDM + r] -= s;
+            const int64_t e = (int64_t)i * kDM + r;
+            const double b = rc == 0 ? pack_rhs(P, e) : d.b[e];   // (rc = 0: b's first reader)
+            d.b[e] = b - (((sm[r] + sm[M + r]) + sm[2 * M + r]) + sm[3 * M + r]);
         }
         return;
     }
@@ -2132,10 +2158,21 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, i
     const int wave = threadIdx.x >> 6;
     const double* Lb = i != j ? Lj : Li;
     v4d acc[4];
+    const bool first = k0 == 0;   // the first group's updates are the tiles' first readers
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
-        acc[q] = (i == j && tj > ti) ? zero4() : tile_ld(C, (int)np, 16 * ti, 16 * tj);
+        if (i == j && tj > ti) {
+            acc[q] = zero4();
+        } else if (first) {
+            const int lane = threadIdx.x & 63, kk = lane >> 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                acc[q][r] = pack_elem(P, radius, (int64_t)i * kDM + 16 * ti + kk + 4 * r,
+                                      (int64_t)j * kDM + 16 * tj + (lane & 15));
+        } else {
+            acc[q] = tile_ld(C, (int)np, 16 * ti, 16 * tj);
+        }
     }
     // the L_ik / L_jk tiles of column kk + 1 are fetched into registers while
     // column kk's MFMAs run (round 6; before, each column loaded its two tiles
@@ -2162,7 +2199,7 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, int k0, i
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
-        if (i == j && tj > ti) continue;
+        if (i == j && tj > ti && !first) continue;   // (first: the upper 16x16 tiles go out as zeros)
         tile_st(C, (int)np, 16 * ti, 16 * tj, acc[q]);
     }
 }
@@ -2195,7 +2232,11 @@ __global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem 
     __syncthreads();
     if (k == 0) {
         for (int64_t e = threadIdx.x; e < P.nF; e += NT) P.yF[e] = e < M ? xk[e] : d.x[e];
-        if (threadIdx.x == 0) P.scal[kScSolveFail] = solve_verdict(d.fail);
+        if (threadIdx.x == 0) {
+            P.scal[kScSolveFail] = solve_verdict(d.fail);
+            d.fail[0] = 0.0;   // cleared for the next solve (no pack pass clears them)
+            d.fail[1] = 0.0;
+        }
         return;
     }
     const int i = blockIdx.x;   // < k
@@ -2213,77 +2254,113 @@ __global__ __launch_bounds__(NT) void dense_back_kernel(DenseArgs d, DevProblem 
 
 // back substitution, every block column in one launch (dataflow): workgroup
 // w takes block k = nt - 1 - w, accumulates y_k - sum_{j>k} L_jk' x_j as the
-// x_j are published (j descending, the L_jk loads issued before each wait),
-// then x_k = X_kk' (...) and publishes x_k.  The hand-off follows the
-// write-through form of cdna_hip_programming.md Guideline 16 (MI355X_MICROARCH
-// § visibility, first table row): x is stored with agent-scope (sc1) stores,
-// every storing wave drains, the workgroup meets, one lane stores the flag;
-// the consumer polls the flag with an sc1 load and reads x only with sc1
-// loads after a workgroup barrier, one workgroup per CU (the dynamic LDS
-// below is sized for that).  Every workgroup must be resident (nt <= the CU
-// count, checked by the caller) and every spin is bounded (a timeout marks the
-// solve failed, which the LM loop treats as an invalid step).
-__device__ __forceinline__ void dense_wait_x(const unsigned* flag, unsigned epoch, double* fail) {
-    if (threadIdx.x == 0) {
-        unsigned spins = 0;
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22)) {
-                __hip_atomic_store(fail + 1, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // timeout
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
+// x_j arrive (j descending, each L_jk slice loaded before its wait), then
+// x_k = X_kk' (...) and publishes x_k.  Workgroup k waits only for workgroups
+// of lower index (in-order dispatch), one workgroup per CU (the dynamic LDS
+// below is sized for that), every workgroup resident (nt <= the CU count,
+// checked by the caller), and every spin bounded (a timeout marks the solve
+// failed: SFM_ERR_DEVICE).
+// Round 6: two columns of lookahead and tagged x granules.  The substitution's
+// chain is x_k+1 -> x_k (4.2 us per column at dense-S: the flag poll, a
+// 64-long dependent X' v loop, the drain, the flag).  Now
+//   x_k = r_k - M1 x_k+1 - M2 x_k+2,   M1 = X_k' L_k+1,k',  M2 = X_k' L_k+2,k',
+//   r_k = X_k' (y_k - sum_{j > k+2} L_jk' x_j)
+// with M1 / M2 formed at the start (MFMA) and held in registers, r_k ready
+// once x_k+3 is in, so the arrival of x_k+1 costs a 64 x 64 matrix-vector
+// product from registers; x_k goes out as 128 tagged granules (put_y / get_y:
+// the data is the flag -- no drain, no flag round trip).
 __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProblem P, unsigned epoch) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* Xs = sm;                 // [64][M + 1]
-    double* v = Xs + M * (M + 1);    // [64]
-    double (*part)[M] = reinterpret_cast<double (*)[M]>(v + M);   // [4][64]
-    const int k = d.nt - 1 - (int)blockIdx.x;
+    double* Xs = sm;                  // [64][LD] X_k
+    double* Lt = Xs + M * LD;         // [64][LD] L_k+1,k, then L_k+2,k
+    double* Mt = Lt + M * LD;         // [64][LD] M1, then M2
+    double* xs = Mt + M * LD;         // [2][64] x_j, double buffered
+    double* part = xs + 2 * M;        // [4][64]
+    double* v = part + 4 * M;         // [64]
+    double* part2 = v + M;            // [4][64]
+    double* part3 = part2 + 4 * M;    // [4][64]
+    const int nt = d.nt, k = nt - 1 - (int)blockIdx.x;
     const int64_t np = d.np;
-    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-    {   // X_kk (an earlier launch wrote it: plain loads)
-        const double* X = d.X + (int64_t)k * kDM * kDM;
-        double xv[M / 4];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6, wave = g;
+    auto tL = [&](int j) { return d.A + (int64_t)j * kDM * np + (int64_t)k * kDM; };   // L_jk
+    load_tile<64>(Xs, LD, d.X + (int64_t)k * kDM * kDM, M);
+    double m1[16], m2[16];
+    auto form = [&](int j, double (&mr)[16]) {   // mr = row c, columns 16 g .. of X_k' L_jk'
+        load_tile<64>(Lt, LD, tL(j), (int)np);
+        __syncthreads();
 #pragma unroll
-        for (int q = 0; q < M / 4; ++q) xv[q] = X[(4 * q + g) * M + c];
+        for (int q = 0; q < 4; ++q)
+            tile_st(Mt, LD, 16 * wave, 16 * q,
+                    tile_mm<true, true, false>(zero4(), Xs, LD, 16 * wave, Lt, LD, 16 * q, 16 * wave, M));
+        __syncthreads();
 #pragma unroll
-        for (int q = 0; q < M / 4; ++q) Xs[(4 * q + g) * (M + 1) + c] = xv[q];
+        for (int q = 0; q < 16; ++q) mr[q] = Mt[c * LD + 16 * g + q];
+        __syncthreads();   // (Lt / Mt reused)
+    };
+    if (k + 1 < nt) form(k + 1, m1);
+    if (k + 2 < nt) form(k + 2, m2);
+    __syncthreads();
+    // r_k: the x_j of j > k + 2 as they arrive (each L_jk slice fetched first)
+    double s = 0.0;
+    int buf = 0;
+    for (int j = nt - 1; j > k + 2; --j) {
+        const double* L = tL(j) + c;
+        double lr[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) lr[q] = L[(int64_t)(4 * q + g) * np];
+        double* xb = xs + M * buf;
+        if (wave == 0) get_y(d.xg + (int64_t)j * kYG, nullptr, xb, nullptr, epoch, d.fail);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s = fma(lr[q], xb[4 * q + g], s);
+        buf ^= 1;
     }
-    // thread (g, c): column c of L_jk', rows 4q + g
-    double acc = 0.0;
-    for (int j = d.nt - 1; j > k; --j) {
-        const double* L = d.A + (int64_t)j * kDM * np + (int64_t)k * kDM + c;
-        double lv[M / 4];
-#pragma unroll
-        for (int q = 0; q < M / 4; ++q) lv[q] = L[(int64_t)(4 * q + g) * np];
-        dense_wait_x(d.xflag + j, epoch, d.fail);
-        const double* xj = d.x + (int64_t)j * kDM;
-#pragma unroll
-        for (int q = 0; q < M / 4; ++q)
-            acc = fma(lv[q], __hip_atomic_load(xj + 4 * q + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), acc);
-    }
-    part[g][c] = acc;
+    part[g * M + c] = s;
     __syncthreads();
     if (threadIdx.x < M)
-        v[c] = d.y[(int64_t)k * kDM + c] - (((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+        v[c] = d.y[(int64_t)k * kDM + c] - (((part[c] + part[M + c]) + part[2 * M + c]) + part[3 * M + c]);
     __syncthreads();
-    if (threadIdx.x < M) {   // x_k = X_kk' v: X lower, so rows m >= c
-        double x = 0.0;
-        for (int m = c; m < M; ++m) x = fma(Xs[m * (M + 1) + c], v[m], x);
-        __hip_atomic_store(d.x + (int64_t)k * kDM + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int64_t e = (int64_t)k * kDM + c;
-        if (e < P.nF) P.yF[e] = x;
+    // r_k = X_k' v (X lower: rows m >= c), rows 16 g .. 16 g + 15 per thread
+    double u = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int m = 16 * g + q;
+        if (m >= c) u = fma(Xs[m * LD + c], v[m], u);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    part2[g * M + c] = u;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(d.xflag + k, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // block 0 finishes last (it waits for every other x): the solve's verdict
-        if (k == 0) P.scal[kScSolveFail] = solve_verdict(d.fail);
+    double xv = ((part2[c] + part2[M + c]) + part2[2 * M + c]) + part2[3 * M + c];
+    if (k + 1 < nt) {
+        double w = 0.0;
+        if (k + 2 < nt) {   // x_k+2 first (it arrives first), then x_k+1
+            double* xb = xs + M * buf;
+            if (wave == 0) get_y(d.xg + (int64_t)(k + 2) * kYG, nullptr, xb, nullptr, epoch, d.fail);
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 16; ++q) w = fma(m2[q], xb[16 * g + q], w);
+            buf ^= 1;
+        }
+        double* xb = xs + M * buf;
+        if (wave == 0) get_y(d.xg + (int64_t)(k + 1) * kYG, nullptr, xb, nullptr, epoch, d.fail);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w = fma(m1[q], xb[16 * g + q], w);
+        part3[g * M + c] = w;
+        __syncthreads();
+        xv -= ((part3[c] + part3[M + c]) + part3[2 * M + c]) + part3[3 * M + c];
+    }
+    if (threadIdx.x < M) {
+        put_y(d.xg + (int64_t)k * kYG, c, xv, epoch);
+        const int64_t e = (int64_t)k * kDM + c;
+        if (e < P.nF) P.yF[e] = xv;
+    }
+    // block 0 finishes last (it waits for every other x): the solve's verdict
+    // (the failure words come from the earlier launches), then the words
+    // cleared for the next solve (no pack pass clears them)
+    if (k == 0 && threadIdx.x == 0) {
+        P.scal[kScSolveFail] = solve_verdict(d.fail);
+        st_wt(d.fail, 0.0);
+        st_wt(d.fail + 1, 0.0);
     }
 }
 
@@ -2308,9 +2385,6 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
 // so every wait ends; spins are bounded (a timeout fails the solve).
 constexpr int kDfLds = 4 * M * LD + 32;   // doubles: four tiles + small state
 
-__device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void tile_st_wt(double* C, int ldc, int r0, int c0, v4d v) {
     const int lane = threadIdx.x & 63, i = lane & 15, kk = lane >> 4;
 #pragma unroll
@@ -2360,7 +2434,7 @@ __device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const uns
 
 // tile (pi, pj) of S in the natural tile order (pi, pj: physical tiles of
 // a permuted pair) straight from the reduce's lower-triangle S, with the LM
-// diagonal D^2 and identity padding -- the values dense_pack_kernel gives --
+// diagonal D^2 and identity padding -- pack_elem's values --
 // into LDS [64][LD].  A tile above the diagonal (pi < pj) is the transpose
 // of the stored lower one.  (The dataflow solve has no pack pass: round 6.)
 __device__ __forceinline__ void df_load_a(double* T, const DevProblem& P, double radius, int pi, int pj) {
@@ -2983,7 +3057,6 @@ void dense_bind(DenseArgs& d, double* base) {
 }
 
 void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
-    const int64_t n2 = d.np * d.np;
     const size_t lds_p = (3 * M * LD + 2) * sizeof(double), lds_u = 2 * M * LD * sizeof(double);
     set_dyn_lds((const void*)dense_panel_kernel, lds_p);
     set_dyn_lds((const void*)dense_update_kernel, lds_u);
@@ -3006,8 +3079,6 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         SFM_HIP(hipGetLastError());
         return;
     }
-    hipLaunchKernelGGL(dense_pack_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, s, d, P, radius);
-    SFM_HIP(hipGetLastError());
     // block columns in groups of W = kDenseW: panel c, then the group's
     // later columns updated from column c alone (rhs of column c fused), ...;
     // after the group's last panel every later tile is updated from all W
@@ -3016,28 +3087,29 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
     for (int k = 0; k < d.nt; k += W) {
         const int w = std::min(W, d.nt - k);
         for (int c = k; c < k + w; ++c) {
-            hipLaunchKernelGGL(dense_panel_kernel, dim3(d.nt - c), dim3(NT), lds_p, s, d, c);
+            hipLaunchKernelGGL(dense_panel_kernel, dim3(d.nt - c), dim3(NT), lds_p, s, d, P, radius, c);
             SFM_HIP(hipGetLastError());
             const int m = d.nt - c - 1;   // rows below column c
             if (c + 1 < k + w) {
                 const int nw = k + w - c - 1, n_tiles = nw * m;
-                hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m), dim3(NT), lds_u, s, d, c, 1, c + 1,
-                                   n_tiles, nw, c);
+                hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m), dim3(NT), lds_u, s, d, P, radius, c, 1,
+                                   c + 1, n_tiles, nw, c);
                 SFM_HIP(hipGetLastError());
             }
         }
         const int m2 = d.nt - k - w;   // trailing block columns
         if (m2 > 0) {
             const int n_tiles = m2 * (m2 + 1) / 2;
-            hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m2), dim3(NT), lds_u, s, d, k, w, k + w, n_tiles, 0,
-                               k + w - 1);
+            hipLaunchKernelGGL(dense_update_kernel, dim3(n_tiles + m2), dim3(NT), lds_u, s, d, P, radius, k, w, k + w,
+                               n_tiles, 0, k + w - 1);
             SFM_HIP(hipGetLastError());
         }
     }
     if (d.nt <= n_cu && !d.chain) {
         // one workgroup per block column, all resident: more than half a CU's
         // LDS each, so one per CU
-        constexpr size_t lds_all = 81 * 1024;
+        constexpr size_t lds_all = (3 * M * LD + 15 * M) * sizeof(double);
+        static_assert(lds_all > 80 * 1024 && lds_all <= 160 * 1024, "one back-substitution workgroup per CU");
         set_dyn_lds((const void*)dense_back_all_kernel, lds_all);
         hipLaunchKernelGGL(dense_back_all_kernel, dim3(d.nt), dim3(NT), lds_all, s, d, P, epoch);
         SFM_HIP(hipGetLastError());
