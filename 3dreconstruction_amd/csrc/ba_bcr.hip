@@ -2870,7 +2870,7 @@ std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
     std::vector<int> perm(nt), c0, c1;
     for (int t = 0; t < nt; ++t) perm[t] = t;
     const int len = tc - w, h = (len + 1) / 2, n2 = len - h;
-    const bool split = w >= 1 && n2 >= 2 && !std::getenv("SFM_DENSE_NO_SPLIT");
+    const bool split = w >= 1 && n2 >= 2;
     if (split) {
         int q = 0;
         for (int t = 0; t < h; ++t) perm[q++] = t;
