@@ -2112,11 +2112,28 @@ __global__ __launch_bounds__(NT) void dense_panel_kernel(DenseArgs d, DevProblem
 // write of A_ij per launch instead of per column; the fp64 MFMA chain is the
 // same, so the result is bit-identical); then rhs tiles i > rc get
 // b_i -= L_i,rc y_rc (forward substitution, fused).
-__global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, DevProblem P, double radius, int k0, int kw,
-                                                          int j0, int n_tiles, int nw, int rc) {
+// Retiled (round 6): the L tiles are staged 32 columns (k) at a time, 34 KB of
+// LDS per workgroup instead of 67 KB, so three update workgroups share a CU
+// instead of two (waves_per_eu 3: at most 168 VGPRs).  One workgroup
+// alternates its MFMAs with waits for the next stage's global loads (L tiles
+// from the MALL, a few us); two per CU left the fp64 MFMA pipes ~60 % idle
+// at dense-S.  The MFMA sequence of each output tile is unchanged (k ascending
+// in 16-deep chunks).  A/B (profiles/r06/d_dense_chain/tiling_ab.txt): dense-S
+// 107.9-108.1 (64-column stages, 2 per CU) / 110.0-110.1 (32, 4 per CU) /
+// 110.5-110.9 (32, 3 per CU) / 90.6 (16, 6) / 77.8 (16, 8) LM-iters/s.
+#ifndef SFM_UPD_KC
+#define SFM_UPD_KC 32   // (A/B builds only)
+#endif
+#ifndef SFM_UPD_WPE
+#define SFM_UPD_WPE 3
+#endif
+constexpr int kUpdKC = SFM_UPD_KC, kUpdLD = kUpdKC + 1;
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(SFM_UPD_WPE, SFM_UPD_WPE)))
+void dense_update_kernel(DenseArgs d, DevProblem P, double radius, int k0, int kw, int j0, int n_tiles, int nw,
+                         int rc) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* Li = sm;
-    double* Lj = sm + M * LD;
+    double* Lj = sm + M * kUpdLD;
     const int64_t np = d.np;
     const int t = blockIdx.x;
     if (t >= n_tiles) {   // rhs tile i: b_i -= L_i,rc y_rc
@@ -2174,26 +2191,29 @@ __global__ __launch_bounds__(NT) void dense_update_kernel(DenseArgs d, DevProble
             acc[q] = tile_ld(C, (int)np, 16 * ti, 16 * tj);
         }
     }
-    // the L_ik / L_jk tiles of column kk + 1 are fetched into registers while
-    // column kk's MFMAs run (round 6; before, each column loaded its two tiles
-    // one after the other, two memory latencies per column on the path)
-    TileFetch<64, M, NT> fi, fj;
-    auto fetch = [&](int kk) {
-        fi.fetch(d.A + (int64_t)i * kDM * np + (int64_t)kk * kDM, (int)np);
-        if (i != j) fj.fetch(d.A + (int64_t)j * kDM * np + (int64_t)kk * kDM, (int)np);
+    // stage st = (column kk, half h): the L_ik / L_jk columns 32 h .. 32 h + 31
+    // of column kk; the next stage's are fetched into registers while this
+    // stage's MFMAs run
+    TileFetch<kUpdKC, M, NT> fi, fj;
+    constexpr int kSt = M / kUpdKC;   // stages per column
+    auto fetch = [&](int st) {
+        const int64_t off = (int64_t)(k0 + st / kSt) * kDM + kUpdKC * (st % kSt);
+        fi.fetch(d.A + (int64_t)i * kDM * np + off, (int)np);
+        if (i != j) fj.fetch(d.A + (int64_t)j * kDM * np + off, (int)np);
     };
-    fetch(k0);
-    for (int kk = k0; kk < k0 + kw; ++kk) {
-        if (kk > k0) __syncthreads();   // the previous column's tiles are consumed
-        fi.put(Li, LD);
-        if (i != j) fj.put(Lj, LD);
+    const int n_st = kSt * kw;
+    fetch(0);
+    for (int st = 0; st < n_st; ++st) {
+        if (st > 0) __syncthreads();   // the previous stage's tiles are consumed
+        fi.put(Li, kUpdLD);
+        if (i != j) fj.put(Lj, kUpdLD);
         __syncthreads();
-        if (kk + 1 < k0 + kw) fetch(kk + 1);
+        if (st + 1 < n_st) fetch(st + 1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int tt = wave * 4 + q, ti = tt >> 2, tj = tt & 3;
             if (i == j && tj > ti) continue;   // the diagonal tile's lower half (and its diagonal sub-tiles)
-            acc[q] = tile_mm<false, true, true>(acc[q], Li, LD, 16 * ti, Lb, LD, 16 * tj, 0, M);
+            acc[q] = tile_mm<false, true, true>(acc[q], Li, kUpdLD, 16 * ti, Lb, kUpdLD, 16 * tj, 0, kUpdKC);
         }
     }
 #pragma unroll
@@ -3057,7 +3077,7 @@ void dense_bind(DenseArgs& d, double* base) {
 }
 
 void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStream_t s, unsigned epoch) {
-    const size_t lds_p = (3 * M * LD + 2) * sizeof(double), lds_u = 2 * M * LD * sizeof(double);
+    const size_t lds_p = (3 * M * LD + 2) * sizeof(double), lds_u = 2 * M * kUpdLD * sizeof(double);
     set_dyn_lds((const void*)dense_panel_kernel, lds_p);
     set_dyn_lds((const void*)dense_update_kernel, lds_u);
     const int n_cu = device_cu_count();
