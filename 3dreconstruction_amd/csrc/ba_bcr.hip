@@ -2020,7 +2020,10 @@ namespace {
 
 constexpr int kDM = 64;   // tile
 constexpr int kDenseW = 4;   // block columns per trailing update
-constexpr int kDenseFlowMaxNt = 29;   // the dataflow solve up to this many block columns
+#ifndef SFM_DENSE_FLOW_MAX_NT
+#define SFM_DENSE_FLOW_MAX_NT 100   // (A/B builds only; 29 until round 6)
+#endif
+constexpr int kDenseFlowMaxNt = SFM_DENSE_FLOW_MAX_NT;   // the dataflow solve up to this many block columns
 enum : int { kTaskD = 0, kTaskS = 1, kTaskT = 2, kTaskY = 3, kTaskB = 4 };   // dataflow tasks (dense_flow_plan)
 
 __device__ __forceinline__ void st_wt(double* p, double v) {   // write-through store
@@ -2385,9 +2388,9 @@ __global__ __launch_bounds__(NT) void dense_back_all_kernel(DenseArgs d, DevProb
 }
 
 // ---- the whole factorisation + both substitutions in one dataflow launch ----
-// For small dense systems (the C5 loop's: nt <= 29 block columns) the panel /
-// update launch chain is latency bound (a 64-pivot factor per column plus two
-// launches).  Here workgroup 0 runs the diagonal chain -- for k: L_k,k-1 =
+// For dense systems up to kDenseFlowMaxNt block columns (the C5 loop's, nt <=
+// 29; RADIAL3 per camera, 38; dense-S, 94) the panel / update launch chain is
+// latency bound (a 64-pivot factor per column plus two launches).  Here workgroup 0 runs the diagonal chain -- for k: L_k,k-1 =
 // A~_k,k-1 X_k-1', A_kk -= L_k,k-1 L_k,k-1', factor + invert A_kk -- and every
 // other workgroup owns one task, left-looking:
 //   D(i)     A~_ii    = A_ii    - sum_{m < i-1} L_im L_im'       (for the chain)
@@ -3081,10 +3084,11 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
     set_dyn_lds((const void*)dense_panel_kernel, lds_p);
     set_dyn_lds((const void*)dense_update_kernel, lds_u);
     const int n_cu = device_cu_count();
-    // up to kDenseFlowMaxNt block columns (the C5 loop's systems) the
-    // dataflow kernel; at dense-S's 94 it only equals the launch chain
-    // (DESIGN.md §5), which stays the form for wider systems (and every system
-    // under SFM_CTX_BA_DENSE_CHAIN)
+    // up to kDenseFlowMaxNt block columns the dataflow kernel (round 6, with
+    // the host schedule and the lookahead back substitution: RADIAL3 per
+    // camera 480 -> 540, dense-S 110 -> 112 LM-iters/s against the launch
+    // chain, profiles/r06/f_flow_max); the launch chain stays the form for
+    // wider systems (and every system under SFM_CTX_BA_DENSE_CHAIN)
     if (d.flow) {
         // factorisation and both substitutions in one dataflow launch: the
         // chain workgroups and up to n_cu - nch task workers, one workgroup
