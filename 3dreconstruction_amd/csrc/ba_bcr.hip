@@ -2824,8 +2824,24 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
             }
         }
     };
-    for (int t = (int)blockIdx.x - d.nch; t < d.ntask; t += (int)gridDim.x - d.nch) {
-        __syncthreads();   // the previous task is done with the LDS tiles
+    // Workers take the next task of the order from a shared counter as they
+    // finish one (round 6; a fixed round-robin assignment left a worker whose
+    // task waited blocking the later tasks assigned to it while others idled).
+    // Each worker holds one task at a time and the tasks are taken in order,
+    // so the earliest unfinished task is always held by a worker with nothing
+    // earlier unfinished: it can run.  The counter grows monotonically over
+    // the plan's solves, by ntask + workers per solve (every worker's last
+    // take fails once), so solve `epoch` (1, 2, ...) starts at a known base.
+    unsigned long long* take = reinterpret_cast<unsigned long long*>(d.fail + 6);
+    const unsigned long long base = (unsigned long long)(epoch - 1) * (unsigned long long)(d.ntask + gridDim.x - d.nch);
+    int* tsh = sh + 1;
+    for (;;) {
+        __syncthreads();   // the previous task is done with the LDS tiles (and with tsh)
+        if (threadIdx.x == 0)
+            *tsh = (int)(__hip_atomic_fetch_add(take, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base);
+        __syncthreads();
+        const int t = *tsh;
+        if (t >= d.ntask) break;
         task(t);
     }
 }
