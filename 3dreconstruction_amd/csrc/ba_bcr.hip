@@ -328,6 +328,34 @@ __device__ __forceinline__ void load_tiles2(double* d1, const double* __restrict
         d2[r * LD + c + 1] = v[per + q].y;
     }
 }
+// up to four 64x64 global tiles -> LDS [64][LD] (tiles t < n), every load in
+// flight before the first LDS store (one memory latency for all of them)
+__device__ __forceinline__ void load_tiles4(int n, double* d0, const double* s0, double* d1, const double* s1,
+                                            double* d2, const double* s2, double* d3, const double* s3, int ld_src) {
+    constexpr int n2 = M * M / 2, per = n2 / NT;
+    double* const dd[4] = {d0, d1, d2, d3};
+    const double* const ss[4] = {s0, s1, s2, s3};
+    double2 v[4][per];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        if (t < n) {
+#pragma unroll
+            for (int q = 0; q < per; ++q) {
+                const int e = threadIdx.x + q * NT, r = e / (M / 2), c = 2 * (e % (M / 2));
+                v[t][q] = *reinterpret_cast<const double2*>(ss[t] + r * ld_src + c);
+            }
+        }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        if (t < n) {
+#pragma unroll
+            for (int q = 0; q < per; ++q) {
+                const int e = threadIdx.x + q * NT, r = e / (M / 2), c = 2 * (e % (M / 2));
+                dd[t][r * LD + c] = v[t][q].x;
+                dd[t][r * LD + c + 1] = v[t][q].y;
+            }
+        }
+}
 template <int TH = NT>
 __device__ __forceinline__ void load_rows(double* dst, int ld_dst, const double* src, int ld_src, int nc) {
     if (nc == 64) load_tile<64, M, TH>(dst, ld_dst, src, ld_src);
@@ -2454,6 +2482,35 @@ __device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const uns
     __syncthreads();
     return *sh;
 }
+// wait until the flags of term m[0] hold epoch (fa + m * sa, and fb + m * sb
+// if given), then count how many of the terms m[0 .. n) are ready from the
+// first on (at least 1; one acquire for all); every thread gets the count
+__device__ __forceinline__ int df_wait_batch(const unsigned* fa, int sa, const unsigned* fb, int sb, const int (&mb)[4],
+                                             int n, unsigned epoch, double* fail, int* sh) {
+    if (threadIdx.x == 0) {
+        auto ready = [&](int q) {
+            const int m = q == 0 ? mb[0] : q == 1 ? mb[1] : q == 2 ? mb[2] : mb[3];
+            return __hip_atomic_load(fa + (int64_t)m * sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+                   (!fb ||
+                    __hip_atomic_load(fb + (int64_t)m * sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
+        };
+        unsigned spins = 0;
+        while (!ready(0)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) {
+                __hip_atomic_store(fail + 1, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // timeout
+                break;
+            }
+        }
+        int q = 1;
+        while (q < n && ready(q)) ++q;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *sh = q;
+    }
+    __syncthreads();
+    return *sh;
+}
 
 // tile (pi, pj) of S in the natural tile order (pi, pj: physical tiles of
 // a permuted pair) straight from the reduce's lower-triangle S, with the LM
@@ -2633,10 +2690,52 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc[c] = (diag && c > wave) ? zero4() : tile_ld(T3, LD, 16 * wave, 16 * c);
             __syncthreads();   // (T3 is reused below)
-            for (int m = 0; m < mend; ++m) {
+            // the terms in m order; runs of ready terms in batches (up to four
+            // L_im of a D task, two L_im / L_jm pairs otherwise) loaded with
+            // one memory latency (round 6: the dense-S solve is bound by its
+            // task workers' throughput); the same products in the same order
+            auto term_at = [&](int m) {   // the next term from m on (mend: none)
+                for (; m < mend; ++m)
+                    if (m != excl && nzb[i * nt + m] && (diag || nz(j, m))) break;
+                return m;
+            };
+            const int bmax = diag ? 4 : 2;
+            for (int m = term_at(0); m < mend;) {
                 const int zi = nzb[i * nt + m];
-                if (m == excl || !zi || (!diag && !nz(j, m))) continue;
-                if ((zi & 2) && kind != kTaskT) {
+                if (!((zi & 2) && kind != kTaskT)) {
+                    // (registers, no dynamic indexing: the batch's terms)
+                    int mb[4] = {m, m, m, m}, nb = 1, q = term_at(m + 1);
+#pragma unroll
+                    for (int t = 1; t < 4; ++t)
+                        if (nb == t && t < bmax && q < mend && !((nzb[i * nt + q] & 2) && kind != kTaskT)) {
+                            mb[t] = q;
+                            nb = t + 1;
+                            q = term_at(q + 1);
+                        }
+                    const int nr = df_wait_batch(fL + i * nt, 1, diag ? nullptr : fL + j * nt, 1, mb, nb, epoch, d.fail, sh);
+                    if (diag)
+                        load_tiles4(nr, T1, tA(i, mb[0]), T2, tA(i, mb[1]), T3, tA(i, mb[2]), T4, tA(i, mb[3]), (int)np);
+                    else
+                        load_tiles4(2 * nr, T1, tA(i, mb[0]), T2, tA(j, mb[0]), T3, tA(i, mb[1]), T4, tA(j, mb[1]),
+                                    (int)np);
+                    __syncthreads();
+                    double* const Tb[4] = {T1, T2, T3, T4};
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        if (b >= nr) break;
+                        const double* La = diag ? Tb[b] : Tb[2 * (b & 1)];
+                        const double* Lb = diag ? Tb[b] : Tb[2 * (b & 1) + 1];
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            if (diag && c > wave) continue;
+                            acc[c] = tile_mm<false, true, true>(acc[c], La, LD, 16 * wave, Lb, LD, 16 * c, 0, M);
+                        }
+                    }
+                    __syncthreads();
+                    m = nr == nb ? q : nr == 1 ? mb[1] : nr == 2 ? mb[2] : mb[3];
+                    continue;
+                }
+                {
                     // L_im = A_im X_m' formed here, from the values T(i, m) uses
                     // (same products, same bits): the chain's inputs wait on
                     // X_m instead of on T(i, m)'s hand-off (round 6)
@@ -2651,10 +2750,6 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                         l[c] = tile_mm<false, true, false>(zero4(), T3, LD, 16 * wave, T4, LD, 16 * c, 0, 16 * c + 16);
 #pragma unroll
                     for (int c = 0; c < 4; ++c) tile_st(T1, LD, 16 * wave, 16 * c, l[c]);
-                } else {
-                    df_wait_run(fL + i * nt + m, 0, diag ? nullptr : fL + j * nt + m, 0, 0, 1, epoch, d.fail, sh);
-                    if (diag) load_tile<64>(T1, LD, tA(i, m), (int)np);
-                    else load_tiles2(T1, tA(i, m), T2, tA(j, m), (int)np);
                 }
                 __syncthreads();
                 const double* Lb = diag ? T1 : T2;
@@ -2664,6 +2759,7 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
                     acc[c] = tile_mm<false, true, true>(acc[c], T1, LD, 16 * wave, Lb, LD, 16 * c, 0, M);
                 }
                 __syncthreads();
+                m = term_at(m + 1);
             }
             if (kind != kTaskT) {
                 // (the diagonal tile's upper 16x16 tiles go out as zeros: the
@@ -3114,7 +3210,10 @@ void dense_solve(const DenseArgs& d, const DevProblem& P, double radius, hipStre
         // is resident, so every wait ends
         const size_t lds_f = std::max<size_t>(kDfLds * sizeof(double), 81 * 1024);
         set_dyn_lds((const void*)dense_flow_kernel, lds_f);
-        const int workers = std::min(d.ntask, n_cu - d.nch);
+#ifndef SFM_DF_WORKER_DIV
+#define SFM_DF_WORKER_DIV 1   // (A/B only: fewer task workers)
+#endif
+        const int workers = std::min(d.ntask, (n_cu - d.nch) / SFM_DF_WORKER_DIV);
         hipLaunchKernelGGL(dense_flow_kernel, dim3(d.nch + workers), dim3(NT), lds_f, s, d, P, radius, epoch);
         SFM_HIP(hipGetLastError());
         return;
