@@ -2461,9 +2461,11 @@ __device__ __forceinline__ void df_publish2(unsigned* f1, unsigned* f2, unsigned
 __device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const unsigned* fb, int sb, int m0, int m1,
                                            unsigned epoch, double* fail, int* sh) {
     if (threadIdx.x == 0) {
-        auto ready = [&](int m) {
-            return __hip_atomic_load(fa + (int64_t)m * sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-                   (!fb || __hip_atomic_load(fb + (int64_t)m * sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
+        auto ready = [&](int m) {   // (both flags loaded together: one round trip)
+            const unsigned a = __hip_atomic_load(fa + (int64_t)m * sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned b =
+                fb ? __hip_atomic_load(fb + (int64_t)m * sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : epoch;
+            return (a == epoch) & (b == epoch);
         };
         unsigned spins = 0;
         while (!ready(m0)) {
@@ -2488,25 +2490,39 @@ __device__ __forceinline__ int df_wait_run(const unsigned* fa, int sa, const uns
 __device__ __forceinline__ int df_wait_batch(const unsigned* fa, int sa, const unsigned* fb, int sb, const int (&mb)[4],
                                              int n, unsigned epoch, double* fail, int* sh) {
     if (threadIdx.x == 0) {
-        auto ready = [&](int q) {
-            const int m = q == 0 ? mb[0] : q == 1 ? mb[1] : q == 2 ? mb[2] : mb[3];
-            return __hip_atomic_load(fa + (int64_t)m * sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
-                   (!fb ||
-                    __hip_atomic_load(fb + (int64_t)m * sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch);
+        // every flag of the batch loaded at once (one round trip, not one per
+        // term and flag), then term 0's re-polled until it is set
+        unsigned va[4], vb[4];
+        auto fetch = [&](int q1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < q1) {
+                    const int m = q == 0 ? mb[0] : q == 1 ? mb[1] : q == 2 ? mb[2] : mb[3];
+                    va[q] = __hip_atomic_load(fa + (int64_t)m * sa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    vb[q] = fb ? __hip_atomic_load(fb + (int64_t)m * sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : epoch;
+                }
         };
+        fetch(n);
         unsigned spins = 0;
-        while (!ready(0)) {
+        while (va[0] != epoch || vb[0] != epoch) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 22)) {
                 __hip_atomic_store(fail + 1, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // timeout
                 break;
             }
+            fetch(1);
         }
-        int q = 1;
-        while (q < n && ready(q)) ++q;
+        int cnt = 1;
+        bool run = true;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            run = run && q < n && va[q] == epoch && vb[q] == epoch;
+            cnt += run ? 1 : 0;
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        *sh = q;
+        *sh = cnt;
     }
     __syncthreads();
     return *sh;
@@ -2928,6 +2944,9 @@ __global__ __launch_bounds__(NT) void dense_flow_kernel(DenseArgs d, DevProblem 
     // earlier unfinished: it can run.  The counter grows monotonically over
     // the plan's solves, by ntask + workers per solve (every worker's last
     // take fails once), so solve `epoch` (1, 2, ...) starts at a known base.
+    // (Drawing the next ticket when a task starts, to hide the counter's
+    // round trip, measured slower: the drawn task then waits for its busy
+    // worker while idle ones pass it by -- profiles/r06/f_flow_max.)
     unsigned long long* take = reinterpret_cast<unsigned long long*>(d.fail + 6);
     const unsigned long long base = (unsigned long long)(epoch - 1) * (unsigned long long)(d.ntask + gridDim.x - d.nch);
     int* tsh = sh + 1;
