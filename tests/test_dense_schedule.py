@@ -49,6 +49,31 @@ def orbit_problem(n_img, max_len, n_intr=1, closed=False, seed=5, pts_per_img=40
     return pr
 
 
+def random_problem(n_img, n_pt, seed=7):
+    """Points seen by 2..5 random images: a dense camera system (the dense-S
+    benchmark's shape), long left-looking sums everywhere.  One point is seen
+    by every tenth image, so no camera order gives a band and the plan keeps
+    image order (true_matrix's assumption)."""
+    rng = np.random.default_rng(seed)
+    img = list(range(0, n_img, 10))
+    off = [0, len(img)]
+    for _ in range(n_pt):
+        ims = sorted(set(int(v) for v in rng.integers(0, n_img, int(rng.integers(2, 6)))))
+        if len(ims) < 2:
+            continue
+        img += ims
+        off.append(off[-1] + len(ims))
+    keep = {"off": np.array(off, np.int64), "img": np.array(img, np.int32),
+            "uv": rng.normal(0, 100, 2 * len(img)), "intr": np.zeros(n_img, np.int32)}
+    pr = abi.BAProblem()
+    pr.n_img, pr.n_intr, pr.n_pt, pr.n_obs = n_img, 1, len(off) - 1, len(img)
+    pr.pt_offsets, pr.obs_img = abi.ptr(keep["off"], abi.i64p), abi.ptr(keep["img"], abi.i32p)
+    pr.obs_uv, pr.img_intr = abi.ptr(keep["uv"], abi.f64p), abi.ptr(keep["intr"], abi.i32p)
+    pr.const_img, pr.camera_model, pr.huber_a = 0, 0, 4.0
+    pr._keep = keep
+    return pr
+
+
 def true_matrix(pr, sh, rng):
     """Random SPD S (nF x nF) with the problem's block pattern, in the plan's
     camera order (image order without the constant image: no reordering for
@@ -183,6 +208,21 @@ def test_dense_schedule_replays_to_the_solution(n_img, max_len, closed, chains):
     for workers in (254, 5, 1):
         got = replay(sh, meta, S, rhs, workers)
         np.testing.assert_allclose(got, ref, rtol=0, atol=1e-11 * np.abs(ref).max())
+
+
+def test_dense_schedule_random_visibility():
+    """A dense camera system (38 block columns, sums of up to 37 terms, one
+    chain): the replay solves it and never stalls with 254, 3 or 1 workers."""
+    pr = random_problem(400, 3000)
+    sh, meta = api.ba_dense_schedule(pr)
+    assert sh["flow"] == 1 and sh["chains"] == 1 and sh["nt"] == 38, sh
+    rng = np.random.default_rng(11)
+    S = true_matrix(pr, sh, rng)
+    rhs = rng.normal(size=S.shape[0])
+    ref = np.linalg.solve(S, rhs)
+    for workers in (254, 3, 1):
+        got = replay(sh, meta, S, rhs, workers)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-10 * np.abs(ref).max())
 
 
 def test_dense_schedule_absent_for_band_problems():
