@@ -2179,51 +2179,84 @@ constexpr int kLongPTerms = 64;
 // at a time: the wave loads each term's two blocks once, coalesced (the rows
 // are contiguous 3-vectors), instead of every lane gathering its own six
 // doubles per term (36 lanes x 6 scattered 8-byte loads per term made the
-// reduce address-bound).  Rows are padded to 4 doubles in LDS (two 16-byte
-// reads per 3-vector).  ra / rb: rows of the a / b block (b = w: 1 row).
+// reduce address-bound).  Round 6: in 16-byte pieces -- a term's two blocks
+// are ceil(3 ra / 2) + ceil(3 rb / 2) pieces (18 for 6 x 6), the batch's 288
+// pieces five wave loads instead of sixteen 8-byte ones -- each piece's two
+// doubles put in their padded LDS places.  Rows are padded to 4 doubles in
+// LDS (two 16-byte reads per 3-vector).  ra / rb: rows of the a / b block
+// (b = w: 1 row).
 constexpr int kPtB = 16;   // terms per staged batch of the product-term reduce
 constexpr int kPtLds = kPtB * 12 * 4 + 2 * kPtB;   // doubles of LDS per wave (<= 6 + 6 rows per term, the terms)
+constexpr int kPtRounds = (kPtB * 18 + 63) / 64;   // a lane's 16-byte pieces per batch
+typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));   // (Z blocks are 8-byte aligned)
 __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb, int G, int g, int r, int cc,
                                             int ra, int rb, double* lds) {
     const double* Z = P.Z;
     const int lane = threadIdx.x & 63;
-    const int la = 3 * ra, L = la + 3 * rb;   // doubles per term
+    const int la = 3 * ra, lb = 3 * rb;                          // doubles per a / b block
+    const int na2 = (la + 1) >> 1, n2 = na2 + ((lb + 1) >> 1);   // 16-byte pieces per term
     double* La = lds;                          // [kPtB][ra][4]
     double* Lb = lds + kPtB * ra * 4;          // [kPtB][rb][4]
     PTerm* Lt = reinterpret_cast<PTerm*>(lds + kPtB * 12 * 4);   // [kPtB] the batch's terms
-    const bool isa = lane < la;
-    const int oo = isa ? lane : lane - la, orow = oo / 3, ok = oo - 3 * orow;
-    double* dst = (isa ? La + orow * 4 : Lb + orow * 4) + ok;
-    const int dstep = 4 * (isa ? ra : rb);
+    // this lane's pieces (the same in every batch): piece f = lane + 64 q is
+    // term f / n2's piece o = f % n2, doubles 2o, 2o + 1 of its a block (o <
+    // na2) or of its b block; an odd block's last piece carries one double
+    // (its second is read and dropped: Z is allocated two doubles longer)
+    int pt[kPtRounds], pe[kPtRounds], d0[kPtRounds], d1[kPtRounds];
+#pragma unroll
+    for (int q = 0; q < kPtRounds; ++q) {
+        const int f = lane + 64 * q, t = f / n2, o = f - t * n2;
+        const bool sb = o >= na2;
+        const int e = sb ? 2 * (o - na2) : 2 * o, len = sb ? lb : la;
+        const int rows = sb ? rb : ra, base = (sb ? kPtB * ra * 4 : 0) + t * rows * 4;
+        pt[q] = t < kPtB ? t : kPtB;
+        pe[q] = e | (sb ? 256 : 0);
+        d0[q] = base + (e / 3) * 4 + e % 3;
+        d1[q] = e + 1 < len ? base + ((e + 1) / 3) * 4 + (e + 1) % 3 : -1;
+    }
     double s = 0.0;
-    // the next batch's term offsets are loaded one batch ahead (with this
-    // batch's Z loads, so a batch waits for one memory latency, not two)
+    // software pipeline: batch b + 1's pieces are loaded into registers while
+    // batch b is multiplied from LDS, and batch b + 2's term offsets with them
     // (two scalars, not a PTerm: the struct was promoted to LDS, and its
     // store there waited for the load it was meant to prefetch)
     const int2* pt2 = reinterpret_cast<const int2*>(P.pterms);
     int2 nxt = make_int2(0, 0);
-    if (lane < min(kPtB, qb - qa)) nxt = pt2[qa + lane];
-    for (int q0 = qa; q0 < qb; q0 += kPtB) {
-        const int nb = min(kPtB, qb - q0);
-        // stage: the batch's term offsets through LDS, then lane o < L loads
-        // element o of every term (its row and column fixed: no index
-        // division), all kPtB loads in flight before the first store
-        if (lane < nb) Lt[lane] = PTerm{nxt.x, nxt.y};
-        if (lane < min(kPtB, qb - q0 - kPtB)) nxt = pt2[q0 + kPtB + lane];
-        wsync();
-        double v[kPtB];
+    auto load_offs = [&](int q0) {   // batch q0's term offsets -> nxt
+        if (lane < min(kPtB, qb - q0)) nxt = pt2[q0 + lane];
+    };
+    d2u v[kPtRounds];
+    auto load_pieces = [&](int nb) {   // the staged batch's (Lt) pieces -> v
+        // every piece's load in flight at once (unconditional: pieces past
+        // the batch read term 0's first piece)
 #pragma unroll
-        for (int t = 0; t < kPtB; ++t) {
-            // unconditional load (clamped index; Z is not empty when there
-            // are terms): a conditional one left a 0.0 default whose
-            // register write waited for the previous batch's loads
-            const int32_t off = isa ? Lt[t].za : Lt[t].zb;
-            v[t] = Z[(lane < L && t < nb) ? off + oo : 0];
+        for (int q = 0; q < kPtRounds; ++q) {
+            const bool live = pt[q] < nb;
+            const PTerm tm = Lt[live ? pt[q] : 0];
+            const int32_t off = live ? ((pe[q] & 256) ? tm.zb : tm.za) + (pe[q] & 255) : tm.za;
+            v[q] = *reinterpret_cast<const d2u*>(Z + off);
         }
+    };
+    if (qa >= qb) return s;
+    load_offs(qa);
+    int nb = min(kPtB, qb - qa);
+    if (lane < nb) Lt[lane] = PTerm{nxt.x, nxt.y};
+    load_offs(qa + kPtB);
+    wsync();
+    load_pieces(nb);
+    for (int q0 = qa; q0 < qb; q0 += kPtB) {
+        wsync();   // (the previous batch's reads of La / Lb and Lt are done)
 #pragma unroll
-        for (int t = 0; t < kPtB; ++t)
-            if (lane < L && t < nb) dst[t * dstep] = v[t];
+        for (int q = 0; q < kPtRounds; ++q)
+            if (pt[q] < nb) {
+                lds[d0[q]] = v[q].x;
+                if (d1[q] >= 0) lds[d1[q]] = v[q].y;
+            }
+        // the next batch: its offsets to Lt, its pieces in flight
+        const int q1 = q0 + kPtB, nb1 = min(kPtB, qb - q1);
+        if (nb1 > 0 && lane < nb1) Lt[lane] = PTerm{nxt.x, nxt.y};
+        if (nb1 > 0) load_offs(q1 + kPtB);
         wsync();
+        if (nb1 > 0) load_pieces(nb1);
         if (g >= 0) {
             // this group's terms in the batch: j = g - (q0 - qa) mod G, + G, ...
             int j = (g - (q0 - qa) % G + G) % G;
@@ -2235,8 +2268,9 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
                 s += a01.x * b01.x + a01.y * b01.y + a2 * b2;
             }
         }
-        wsync();
+        nb = nb1;
     }
+    wsync();
     return s;
 }
 

@@ -225,7 +225,7 @@ bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     up(st, pl->zbatch, h.zbatch, s);
     up(st, pl->zlong, h.zlong, s);
     up(pl->pterms, h.pterms, s);
-    pl->Zbuf.alloc(std::max<int64_t>(h.n_z, 1));
+    pl->Zbuf.alloc(h.n_z + 2);   // (+2: preduce's 16-byte pieces read one double past an odd block)
     HostVec<double> xs(3 * std::max<int64_t>(h.n_spt, 1));
     for (int64_t k = 0; k < h.n_spt; ++k)
         for (int a = 0; a < 3; ++a) xs[3 * k + a] = X[3 * h.spt_global[k] + a];
