@@ -2189,8 +2189,12 @@ constexpr int kPtB = 16;   // terms per staged batch of the product-term reduce
 constexpr int kPtLds = kPtB * 12 * 4 + 2 * kPtB;   // doubles of LDS per wave (<= 6 + 6 rows per term, the terms)
 constexpr int kPtRounds = (kPtB * 18 + 63) / 64;   // a lane's 16-byte pieces per batch
 typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));   // (Z blocks are 8-byte aligned)
+// ch > 0 (a block target with an even number of columns, round 6): the lane
+// also sums element (r, cc + ch) into s1 -- one read of Z_a's row r for two
+// elements, and half the lanes per element, so three lane groups share a
+// 6 x 6 target's terms instead of one (36 of 64 lanes)
 __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb, int G, int g, int r, int cc,
-                                            int ra, int rb, double* lds) {
+                                            int ra, int rb, double* lds, int ch, double& s1) {
     const double* Z = P.Z;
     const int lane = threadIdx.x & 63;
     const int la = 3 * ra, lb = 3 * rb;                          // doubles per a / b block
@@ -2215,6 +2219,7 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
         d1[q] = e + 1 < len ? base + ((e + 1) / 3) * 4 + (e + 1) % 3 : -1;
     }
     double s = 0.0;
+    s1 = 0.0;
     // software pipeline: batch b + 1's pieces are loaded into registers while
     // batch b is multiplied from LDS, and batch b + 2's term offsets with them
     // (two scalars, not a PTerm: the struct was promoted to LDS, and its
@@ -2266,6 +2271,11 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
                 const double2 b01 = *reinterpret_cast<const double2*>(Lb + (j * rb + cc) * 4);
                 const double b2 = Lb[(j * rb + cc) * 4 + 2];
                 s += a01.x * b01.x + a01.y * b01.y + a2 * b2;
+                if (ch) {
+                    const double2 c01 = *reinterpret_cast<const double2*>(Lb + (j * rb + cc + ch) * 4);
+                    const double c2 = Lb[(j * rb + cc + ch) * 4 + 2];
+                    s1 += a01.x * c01.x + a01.y * c01.y + a2 * c2;
+                }
             }
         }
         nb = nb1;
@@ -2273,6 +2283,31 @@ __device__ __forceinline__ double pterm_sum(const DevProblem& P, int qa, int qb,
     wsync();
     return s;
 }
+
+// A product-term target's lane layout: E2 lane slots of one element (r, cc)
+// -- or two, (r, cc) and (r, cc + ch), when the target has an even number of
+// columns -- in G = 64 / E2 lane groups; slot e2 = r * (ch ? ch : cols) + cc.
+struct PLanes {
+    int E2, G, g, r, cc, ch;
+    __device__ __forceinline__ PLanes(const ReduceTarget& T, int lane) {
+        const bool vec = T.cols == 1;
+        ch = (!vec && (T.cols & 1) == 0) ? T.cols / 2 : 0;
+        const int w = ch ? ch : T.cols;
+        E2 = T.rows * w;
+        G = 64 / E2;
+        g = lane / E2;
+        const int e2 = lane - g * E2;
+        r = e2 / w;
+        cc = e2 % w;
+        if (g >= G) g = -1;
+    }
+    // element e (= r * cols + c) of the target: its slot and which sum
+    __device__ __forceinline__ int slot(const ReduceTarget& T, int e, bool& second) const {
+        const int rr = e / T.cols, c = e % T.cols;
+        second = ch && c >= ch;
+        return rr * (ch ? ch : T.cols) + (second ? c - ch : c);
+    }
+};
 
 // One wave per target: its E = rows x cols elements are computed by
 // G = 64 / E lane groups, group g summing terms g, g + G, ... (a 6-vector
@@ -2290,15 +2325,22 @@ __global__ __launch_bounds__(256) void preduce_kernel(DevProblem P) {
     }
     if (!act) return;   // whole waves only: the exchange below is wave-local
     __shared__ __attribute__((aligned(16))) double stage[4][kPtLds];
-    const int E = T.rows * T.cols, G = 64 / E, g = lane / E, e = lane - g * E;
+    __shared__ double part1[4][64];
+    const PLanes pl(T, lane);
+    const int E = T.rows * T.cols;
     const bool vec = T.cols == 1;
-    const double s = pterm_sum(P, T.p_begin, T.p_end, G, g < G ? g : -1, e / T.cols, vec ? 0 : e % T.cols,
-                               T.rows, vec ? 1 : T.cols, stage[wave]);
+    double s1;
+    const double s = pterm_sum(P, T.p_begin, T.p_end, pl.G, pl.g, pl.r, pl.cc, T.rows, vec ? 1 : T.cols, stage[wave],
+                               pl.ch, s1);
     part[wave][lane] = s;
+    part1[wave][lane] = s1;
     wsync();
     if (lane < E) {
+        bool second;
+        const int e2 = pl.slot(T, lane, second);
+        const double* src = second ? part1[wave] : part[wave];
         double tot = 0.0;
-        for (int k = 0; k < G; ++k) tot += part[wave][k * E + lane];
+        for (int k = 0; k < pl.G; ++k) tot += src[k * pl.E2 + e2];
         const int r = lane / T.cols, cc = lane % T.cols;
         target_base(P, T.dst_kind)[T.dst + (vec ? r : (int64_t)r * T.ld + cc)] -= tot;
     }
@@ -2311,23 +2353,28 @@ __global__ __launch_bounds__(256) void preduce_seg_kernel(DevProblem P) {
     const int sg = blockIdx.x;
     const int j = P.plseg[2 * sg], k0 = P.plseg[2 * sg + 1];
     const ReduceTarget T = P.targets[P.plong_targets[j]];
-    const int E = T.rows * T.cols, G = 64 / E;
+    const int E = T.rows * T.cols;
     const bool vec = T.cols == 1;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane / E, e = lane - g * E;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const PLanes pl(T, lane);
     constexpr int kQ = kReduceSeg / 4;
     const int q0 = k0 + wave * kQ, q1 = min(min(k0 + kReduceSeg, (int)T.p_end), q0 + kQ);
     __shared__ __attribute__((aligned(16))) double stage[4][kPtLds];
-    const double s = q0 < q1 ? pterm_sum(P, q0, q1, G, g < G ? g : -1, e / T.cols, vec ? 0 : e % T.cols, T.rows,
-                                         vec ? 1 : T.cols, stage[wave])
+    double s1 = 0.0;
+    const double s = q0 < q1 ? pterm_sum(P, q0, q1, pl.G, pl.g, pl.r, pl.cc, T.rows, vec ? 1 : T.cols, stage[wave],
+                                         pl.ch, s1)
                              : 0.0;
-    __shared__ double part[4][64];
+    __shared__ double part[4][64], part1[4][64];
     part[wave][lane] = s;
+    part1[wave][lane] = s1;
     __syncthreads();
     if ((int)threadIdx.x < E) {
         const int t = threadIdx.x;
+        bool second;
+        const int e2 = pl.slot(T, t, second);
         double tot = 0.0;
         for (int w = 0; w < 4; ++w)
-            for (int k = 0; k < G; ++k) tot += part[w][k * E + t];
+            for (int k = 0; k < pl.G; ++k) tot += (second ? part1[w] : part[w])[k * pl.E2 + e2];
         P.plpart[(size_t)sg * 36 + t] = tot;
     }
 }
