@@ -47,7 +47,12 @@ size_t dense_flag_words(const DenseArgs& d);
 void dense_setup(DenseArgs& d, const DevProblem& P);
 // the dataflow solve's schedule (host, once per plan; empty for the launch
 // chain): sets d.flow / nch / ntask / meta_words; the caller copies it to d.meta
-std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P);
+// exact: the natural tiles' coupling from the reduce targets (dense_tile_pattern),
+// used to order the tiles when the intrinsics arrow is itself banded
+std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P, const std::vector<char>* exact = nullptr);
+// tile (a, b), a >= b, of the natural order is nonzero: some dense reduce
+// target touches it, or a == b ([nt][nt] bytes, lower triangle)
+std::vector<char> dense_tile_pattern(const std::vector<ReduceTarget>& targets, int64_t nF, int nt);
 size_t dense_doubles(const DenseArgs& d);
 void dense_bind(DenseArgs& d, double* base);
 // epoch: a value the x flags do not hold yet (the plan counts its solves from 1)

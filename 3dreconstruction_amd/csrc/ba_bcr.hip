@@ -2993,7 +2993,20 @@ void dense_setup(DenseArgs& d, const DevProblem& P) {
 // on earlier tasks and on chain steps that wait only on earlier tasks -- the
 // lowest unfinished node can always run (each worker takes tasks in order).
 
-std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
+std::vector<char> dense_tile_pattern(const std::vector<ReduceTarget>& targets, int64_t nF, int nt) {
+    std::vector<char> e((size_t)nt * nt, 0);
+    for (int t = 0; t < nt; ++t) e[(size_t)t * nt + t] = 1;
+    for (const ReduceTarget& T : targets) {
+        if (T.dst_kind != kDstDense || T.cols < 1) continue;
+        const int64_t ld = T.ld > 0 ? T.ld : nF, r0 = T.dst / ld, c0 = T.dst % ld;
+        for (int64_t a = r0 / kDM; a <= (r0 + T.rows - 1) / kDM; ++a)
+            for (int64_t b = c0 / kDM; b <= (c0 + T.cols - 1) / kDM; ++b)
+                e[(size_t)std::max(a, b) * nt + std::min(a, b)] = 1;
+    }
+    return e;
+}
+
+std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P, const std::vector<char>* exact) {
     d.flow = !d.chain && d.nt <= kDenseFlowMaxNt;
     d.nch = d.ntask = 0;
     d.meta_words = 0;
@@ -3018,19 +3031,73 @@ std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
     int tc = nt, w = 0;
     for (int t = 0; t < nt; ++t)
         if (arrow(t)) { tc = t; break; }
-    for (int a = 0; a < tc; ++a)
-        for (int b = 0; b < a; ++b)
-            if (couple(a, b)) w = std::max(w, a - b);
+    // Banded arrow (round 6): when the arrow is several tiles and none of them
+    // couples with half of the tiles or more (one intrinsics block per
+    // camera: reconstruction()'s grouping), the exact tile pattern is banded
+    // in a better order than cameras-then-intrinsics -- Cuthill-McKee over the
+    // tile graph puts each intrinsics tile among its cameras' tiles -- and
+    // nested dissection then splits the whole system into two chains instead
+    // of leaving the arrow to chain 0 (RADIAL3 per camera: 30 + 8 columns).
+    // ord[k]: the natural tile at banded position k.
+    std::vector<int> ord(nt);
+    for (int t = 0; t < nt; ++t) ord[t] = t;
+    bool banded_arrow = false;
+    if (exact && nt - tc >= 3) {
+        auto E = [&](int a, int b) { return (*exact)[(size_t)std::max(a, b) * nt + std::min(a, b)] != 0; };
+        std::vector<int> deg(nt, 0);
+        for (int a = 0; a < nt; ++a)
+            for (int b = 0; b < nt; ++b)
+                if (a != b && E(a, b)) ++deg[a];
+        bool hub = false;
+        for (int t = tc; t < nt; ++t) hub = hub || 2 * deg[t] > nt;
+        if (!hub) {
+            // Cuthill-McKee from tile 0 (an end of the camera band), neighbours
+            // by ascending degree, then natural index
+            std::vector<int> cm;
+            std::vector<char> seen(nt, 0);
+            for (int s0 = 0; s0 < nt; ++s0) {
+                if (seen[s0]) continue;
+                seen[s0] = 1;
+                cm.push_back(s0);
+                for (size_t q = cm.size() - 1; q < cm.size(); ++q) {
+                    std::vector<int> nb;
+                    for (int b = 0; b < nt; ++b)
+                        if (!seen[b] && E(cm[q], b)) nb.push_back(b);
+                    std::stable_sort(nb.begin(), nb.end(), [&](int x, int y) { return deg[x] < deg[y]; });
+                    for (int b : nb) {
+                        seen[b] = 1;
+                        cm.push_back(b);
+                    }
+                }
+            }
+            std::vector<int> pos(nt);
+            for (int k = 0; k < nt; ++k) pos[cm[k]] = k;
+            int wb = 0;
+            for (int a = 0; a < nt; ++a)
+                for (int b = 0; b < a; ++b)
+                    if (E(a, b)) wb = std::max(wb, std::abs(pos[a] - pos[b]));
+            if (wb >= 1 && nt - wb - (nt - wb + 1) / 2 >= 2) {
+                banded_arrow = true;
+                ord = cm;
+                tc = nt;
+                w = wb;
+            }
+        }
+    }
+    if (!banded_arrow)
+        for (int a = 0; a < tc; ++a)
+            for (int b = 0; b < a; ++b)
+                if (couple(a, b)) w = std::max(w, a - b);
     std::vector<int> perm(nt), c0, c1;
-    for (int t = 0; t < nt; ++t) perm[t] = t;
+    for (int t = 0; t < nt; ++t) perm[t] = ord[t];
     const int len = tc - w, h = (len + 1) / 2, n2 = len - h;
     const bool split = w >= 1 && n2 >= 2;
     if (split) {
         int q = 0;
-        for (int t = 0; t < h; ++t) perm[q++] = t;
-        for (int t = tc - 1; t >= h + w; --t) perm[q++] = t;
-        for (int t = h; t < h + w; ++t) perm[q++] = t;
-        for (int t = tc; t < nt; ++t) perm[q++] = t;
+        for (int t = 0; t < h; ++t) perm[q++] = ord[t];
+        for (int t = tc - 1; t >= h + w; --t) perm[q++] = ord[t];
+        for (int t = h; t < h + w; ++t) perm[q++] = ord[t];
+        for (int t = tc; t < nt; ++t) perm[q++] = ord[t];
         for (int k = 0; k < h; ++k) c0.push_back(k);
         for (int k = h; k < h + n2; ++k) c1.push_back(k);
         for (int k = h + n2; k < nt; ++k) c0.push_back(k);
@@ -3042,7 +3109,10 @@ std::vector<int32_t> dense_flow_plan(DenseArgs& d, const DevProblem& P) {
     auto NZ = [&](int i, int j) -> char& { return nz[(size_t)i * nt + j]; };
     for (int i = 0; i < nt; ++i) {
         NZ(i, i) = 1;
-        for (int j = 0; j < i; ++j) NZ(i, j) = couple(std::max(perm[i], perm[j]), std::min(perm[i], perm[j]));
+        for (int j = 0; j < i; ++j) {
+            const int a = std::max(perm[i], perm[j]), b = std::min(perm[i], perm[j]);
+            NZ(i, j) = banded_arrow ? (*exact)[(size_t)a * nt + b] : couple(a, b);
+        }
     }
     for (int k = 0; k < nt; ++k)
         for (int i = k + 1; i < nt; ++i)

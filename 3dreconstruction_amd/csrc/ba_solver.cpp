@@ -422,7 +422,8 @@ bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     if (h.dense) {
         dense_setup(pl->dense, P);
         pl->dense.chain = (ctx->flags & SFM_CTX_BA_DENSE_CHAIN) != 0;
-        pl->dense_meta = dense_flow_plan(pl->dense, P);   // the dataflow solve's schedule (host)
+        const std::vector<char> exact = dense_tile_pattern(h.targets, P.nF, pl->dense.nt);
+        pl->dense_meta = dense_flow_plan(pl->dense, P, &exact);   // the dataflow solve's schedule (host)
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
         // failure words, tickets, flags and granules: zeroed once (the dataflow
@@ -1155,7 +1156,8 @@ extern "C" int sfm_ba_dense_schedule(const sfm_ba_problem* prob, int32_t* out, i
         P.ncam = h.ncam; P.nintr = h.nintr; P.D = h.D; P.nb = h.nb; P.nF = h.nF; P.iw = h.iw;
         DenseArgs d;
         dense_setup(d, P);
-        const std::vector<int32_t> meta = h.dense ? dense_flow_plan(d, P) : std::vector<int32_t>();
+        const std::vector<char> exact = h.dense ? dense_tile_pattern(h.targets, P.nF, d.nt) : std::vector<char>();
+        const std::vector<int32_t> meta = h.dense ? dense_flow_plan(d, P, &exact) : std::vector<int32_t>();
         shape[0] = d.nt; shape[1] = d.nch; shape[2] = d.ntask; shape[3] = (h.dense && d.flow) ? 1 : 0;
         shape[4] = (int32_t)h.nF; shape[5] = (int32_t)h.nb; shape[6] = h.D;
         *n_words = (int64_t)meta.size();

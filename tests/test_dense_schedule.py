@@ -225,6 +225,53 @@ def test_dense_schedule_random_visibility():
         np.testing.assert_allclose(got, ref, rtol=0, atol=1e-10 * np.abs(ref).max())
 
 
+def percam_problem(n_img, max_len, closed, seed=9, pts_per_img=30):
+    """RADIAL3 with one intrinsics block per image (reconstruction()'s
+    grouping): the intrinsics arrow is as wide as the camera band and itself
+    banded.  Observations as orbit_problem's."""
+    pr = orbit_problem(n_img, max_len, n_intr=n_img, closed=closed, seed=seed, pts_per_img=pts_per_img)
+    pr.camera_model = abi.SFM_CAM_RADIAL3
+    return pr
+
+
+def percam_matrix(pr, sh, rng, iw=6):
+    """Random SPD S with the per-camera problem's exact block pattern: every
+    pair of the point's camera blocks and intrinsics blocks couples."""
+    k = pr._keep
+    nF, nb = sh["nF"], sh["nb"]
+    S = np.zeros((nF, nF))
+    for p in range(pr.n_pt):
+        ims = [int(i) for i in k["img"][k["off"][p]:k["off"][p + 1]]]
+        rows = [6 * (i - 1) for i in ims if i != pr.const_img] + [nb + iw * int(k["intr"][i]) for i in ims]
+        for a in rows:
+            for b in rows:
+                S[a:a + 6, b:b + 6] = 1.0
+    V = np.tril(rng.normal(0, 0.1, (nF, nF)) * S)
+    V = V + V.T
+    return V + np.eye(nF) * (np.abs(V).sum(1).max() + 1.0)
+
+
+@pytest.mark.parametrize("n_img,max_len", [(200, 10), (150, 6)])
+def test_dense_schedule_banded_arrow(n_img, max_len):
+    """One intrinsics block per camera: the tiles are ordered by Cuthill-McKee
+    over the exact tile pattern (the reduce's targets) and split over two
+    chains; the replay solves the system with that pattern and never stalls."""
+    pr = percam_problem(n_img, max_len, False)   # (open: the plan keeps image order, percam_matrix's)
+    sh, meta = api.ba_dense_schedule(pr)
+    nt = sh["nt"]
+    assert sh["flow"] == 1 and sh["chains"] == 2, sh
+    # intrinsics tiles (natural index >= nb / 64) among the first columns: the
+    # arrow is ordered into the band, not left to the end of chain 0
+    assert any(int(p) >= sh["nb"] // 64 for p in meta[:nt // 2]), meta[:nt]
+    rng = np.random.default_rng(n_img)
+    S = percam_matrix(pr, sh, rng)
+    rhs = rng.normal(size=S.shape[0])
+    ref = np.linalg.solve(S, rhs)
+    for workers in (254, 3, 1):
+        got = replay(sh, meta, S, rhs, workers)
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-10 * np.abs(ref).max())
+
+
 def test_dense_schedule_absent_for_band_problems():
     sh, meta = api.ba_dense_schedule(orbit_problem(200, 8))   # band of 7 blocks: the BCR solver
     assert sh["flow"] == 0 and len(meta) == 0
