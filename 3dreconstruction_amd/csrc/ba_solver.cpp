@@ -422,8 +422,12 @@ bool create_plan(sfm_ba_plan* pl, const sfm_ba_problem& prob, const double* extr
     if (h.dense) {
         dense_setup(pl->dense, P);
         pl->dense.chain = (ctx->flags & SFM_CTX_BA_DENSE_CHAIN) != 0;
-        const std::vector<char> exact = dense_tile_pattern(h.targets, P.nF, pl->dense.nt);
-        pl->dense_meta = dense_flow_plan(pl->dense, P, &exact);   // the dataflow solve's schedule (host)
+        // (the exact tile pattern needs every block's target: one rank lists
+        // only the blocks its shard touches, so a multi-rank plan keeps the
+        // structural pattern -- every rank then plans the same schedule)
+        const std::vector<char> exact =
+            ctx->world == 1 ? dense_tile_pattern(h.targets, P.nF, pl->dense.nt) : std::vector<char>();
+        pl->dense_meta = dense_flow_plan(pl->dense, P, exact.empty() ? nullptr : &exact);   // the dataflow solve's schedule (host)
         pl->dense_buf.alloc(dense_doubles(pl->dense));
         dense_bind(pl->dense, pl->dense_buf.p);
         // failure words, tickets, flags and granules: zeroed once (the dataflow
