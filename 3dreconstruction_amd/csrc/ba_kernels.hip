@@ -1985,8 +1985,10 @@ __global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* 
                                                     double radius) {
     constexpr int IW = kIW<CM>;
     constexpr int NI = CM == SFM_CAM_SNAVELY ? 3 : IW;   // intrinsics parameters with a column
-    __shared__ double rc[64][kZRow];      // camera rows J_c' M (18); before that V | g_E (9), column norms (3)
-    __shared__ double ri[64][kZRow];      // intrinsics rows J_i' M (3 NI)
+    // camera rows J_c' M (18), then (round 6: one array, not two -- 2 -> 3
+    // workgroups per SIMD) the intrinsics rows J_i' M (3 NI); before them
+    // V | g_E (9), column norms (3)
+    __shared__ double rc[64][kZRow];
     __shared__ double pv[kZBatchPts][12]; // per point: V (6) | g_E (3) | sE (3)
     __shared__ int poff[kZBatchPts + 1], okey[64], oib[64];
     const int lane = threadIdx.x;
@@ -2096,14 +2098,14 @@ __global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* 
     const double i22 = rsqrt_nr(V[5] - l20 * l20 - l21 * l21);
     const double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
     const double i20 = -(l20 * i00 + l21 * i10) * i22;
-    if (act) {
-        double M[2][3];
+    double M[2][3];
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            M[r][0] = j[r][0] * i00;
-            M[r][1] = j[r][0] * i10 + j[r][1] * i11;
-            M[r][2] = j[r][0] * i20 + j[r][1] * i21 + j[r][2] * i22;
-        }
+    for (int r = 0; r < 2; ++r) {
+        M[r][0] = j[r][0] * i00;
+        M[r][1] = j[r][0] * i10 + j[r][1] * i11;
+        M[r][2] = j[r][0] * i20 + j[r][1] * i21 + j[r][2] * i22;
+    }
+    if (act) {
         if (cb != 0xffff) {
             const int colc = P.img_colc[img];
 #pragma unroll
@@ -2113,20 +2115,13 @@ __global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* 
                 for (int a = 0; a < 3; ++a) rc[lane][3 * r + a] = (L.Jc[0][r] * sc) * M[0][a] + (L.Jc[1][r] * sc) * M[1][a];
             }
         }
-        const int coli = P.img_coli[img];
-#pragma unroll
-        for (int r = 0; r < NI; ++r) {
-            const double sc = P.scaleF[coli + r];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) ri[lane][3 * r + a] = (L.Ji[0][r] * sc) * M[0][a] + (L.Ji[1][r] * sc) * M[1][a];
-        }
     }
     okey[lane] = act ? (pl << 17 | cb) : -1;
     oib[lane] = ib;
     wsync();
+    double* Zp = P.Z + P.gz_off[g];
+    const int b0 = P.gblk_off[g], pend = poff[pl + 1];
     if (act) {
-        double* Zp = P.Z + P.gz_off[g];
-        const int b0 = P.gblk_off[g], pend = poff[pl + 1];
         // camera block: the first lane of a run of one (point, camera block)
         // adds the run in order (the planner sorts a point's views by image)
         if (cb != 0xffff && (lane == poff[pl] || okey[lane - 1] != okey[lane])) {
@@ -2140,6 +2135,19 @@ __global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* 
 #pragma unroll
             for (int e = 0; e < 18; ++e) dst[e] = acc[e];
         }
+    }
+    wsync();   // (the camera rows are read; the intrinsics rows take their place)
+    if (act) {
+        const int coli = P.img_coli[img];
+#pragma unroll
+        for (int r = 0; r < NI; ++r) {
+            const double sc = P.scaleF[coli + r];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) rc[lane][3 * r + a] = (L.Ji[0][r] * sc) * M[0][a] + (L.Ji[1][r] * sc) * M[1][a];
+        }
+    }
+    wsync();
+    if (act) {
         // intrinsics block: the point's first lane with that block adds all of
         // the point's lanes with it, in order
         bool first = true;
@@ -2147,11 +2155,11 @@ __global__ __launch_bounds__(64) void zbatch_kernel(DevProblem P, const CamPre* 
         if (first) {
             double acc[3 * NI];
 #pragma unroll
-            for (int e = 0; e < 3 * NI; ++e) acc[e] = ri[lane][e];
+            for (int e = 0; e < 3 * NI; ++e) acc[e] = rc[lane][e];
             for (int q = lane + 1; q < pend; ++q)
                 if (oib[q] == ib)
 #pragma unroll
-                    for (int e = 0; e < 3 * NI; ++e) acc[e] += ri[q][e];
+                    for (int e = 0; e < 3 * NI; ++e) acc[e] += rc[q][e];
             double* dst = Zp + P.gblk_z[b0 + ib];
 #pragma unroll
             for (int e = 0; e < 3 * IW; ++e) dst[e] = e < 3 * NI ? acc[e < 3 * NI ? e : 0] : 0.0;   // SNAVELY: row 3 is 0
